@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Headline benchmark: SCST training captions/sec (whole job).
+
+Workload (BASELINE.json / BASELINE.md): MSR-VTT-shaped CaptionModel
+(``concat``, 4 modalities resnet 2048 / c3d 4096 / mfcc 1024 / category 300,
+LSTM 512, embedding 512, vocab 10,509, max length 30, dropout 0.5),
+B = 64 videos x 20 captions = 1,280 caption rows per GPU per step (weak
+scaling), SCST recipe of the reference README (``USE_RL=1 USE_CST=0
+USE_MIXER=1 MIXER_FROM=1 USE_EOS=1``): multinomial rollout from t=1, greedy
+baseline, CIDEr-D reward, REINFORCE loss, backward, gradient all-reduce,
+clip 0.25, Adam.  Synthetic data (6,513 videos x 20 captions, Zipf
+captions) and random-init weights: there is no network for datasets or
+checkpoints.
+
+Every step inside the timed region does ALL of the above (nothing cached,
+no layers skipped).  Timed region: barrier + synchronize, K steps, barrier +
+synchronize; the MAX over ranks is reported.
+
+Modes:
+  --impl hip   (default) fused HIP engine + on-GPU CIDEr-D, bf16 MFMA
+  --impl torch --reward cpu --precision fp32 --dedupe_greedy 0
+               reference semantics (PyTorch ops, CPU CIDEr-D in Python):
+               the baseline BASELINE.md asks to beat.
+
+Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1
+--master-port P bench.py --gpus N``.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE_FILE = os.path.join(REPO, 'profiles', 'reference_semantics_baseline.json')
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--impl', default='hip', choices=['hip', 'torch'])
+    p.add_argument('--reward', default='gpu', choices=['gpu', 'cpu'])
+    p.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
+    p.add_argument('--mode', default='scst', choices=['scst', 'cst', 'xe'])
+    p.add_argument('--dedupe_greedy', type=int, default=1)
+    p.add_argument('--batch_size', type=int, default=64)
+    p.add_argument('--videos', type=int, default=6513)
+    p.add_argument('--vocab', type=int, default=10509)
+    p.add_argument('--seed', type=int, default=123)
+    p.add_argument('--json_out', default='')
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    from cst_captioning_amd.config import default_opts
+    from cst_captioning_amd.data import CaptionLoader, make_synthetic
+    from cst_captioning_amd.parallel import init_distributed
+    from cst_captioning_amd.cli import build_model, seed_everything
+    from cst_captioning_amd.train.trainer import Trainer
+
+    ctx = init_distributed()
+    if a.impl == 'torch':
+        os.environ['CSTCAP_ALLOW_TORCH_FALLBACK'] = '1'
+    seed_everything(a.seed, ctx.rank)
+    t_gen = time.time()
+    ds = make_synthetic('msrvtt', num_videos=a.videos, vocab_size=a.vocab, seed=a.seed)
+    t_gen = time.time() - t_gen
+    S = 20
+    opt = default_opts(
+        batch_size=a.batch_size, train_seq_per_img=S, test_seq_per_img=S, rnn_size=512,
+        input_encoding_size=512, drop_prob_lm=0.5, learning_rate=1e-4, grad_clip=0.25,
+        model_type='concat', eval_metric='CIDEr', max_epochs=10 ** 9, print_log_interval=0,
+        use_rl=1 if a.mode != 'xe' else 0, use_rl_after=0, use_cst=1 if a.mode == 'cst' else 0,
+        use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=2, scb_captions=S,
+        impl=a.impl, precision=a.precision, reward_device=a.reward,
+        dedupe_greedy=a.dedupe_greedy, seed=a.seed, loglevel='WARNING', save_last=0)
+    opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
+    opt.vocab_size = ds.vocab_size
+    opt.seq_length = ds.seq_length
+    opt.feat_dims = ds.feat_dims
+    dev = ctx.device
+    loader = CaptionLoader(ds, a.batch_size, S, 'train', dev, ctx.rank, ctx.world_size, a.seed)
+    model, engine = build_model(opt, dev, a.impl)
+    trainer = Trainer(opt, model, loader, None, ctx, engine)
+    trainer.rl_training = a.mode != 'xe'
+    n_params = sum(p.numel() for p in model.parameters())
+
+    def step():
+        data = loader.get_batch()
+        return trainer.train_step(data, 0)
+
+    sync = torch.cuda.synchronize if dev.type == 'cuda' else (lambda: None)
+    for _ in range(a.warmup):
+        out = step()
+    sync()
+    ctx.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step()
+    sync()
+    ctx.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt = ctx.max_scalar(dt)
+    loss = float(out['loss'])
+    ms = dt / a.steps * 1e3
+    caps = a.batch_size * S * ctx.world_size * a.steps / dt
+    baseline = None
+    if os.path.exists(BASELINE_FILE):
+        with open(BASELINE_FILE) as f:
+            baseline = json.load(f).get('value')
+    rec = {
+        'metric': 'SCST training captions/sec (whole node), MSR-VTT LSTM-attn at 1/2/4/8 MI355X'
+        if a.mode == 'scst' else '%s training captions/sec (whole job)' % a.mode.upper(),
+        'value': round(caps, 2), 'unit': 'captions/s', 'n_gpus': ctx.world_size,
+        'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': round(ms, 3),
+        'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': round(caps / baseline, 3) if (baseline and a.mode == 'scst') else None,
+        'dtype': a.precision, 'data': 'synthetic (MSR-VTT-shaped, random-init weights)',
+        'config': {'model': 'CaptionModel concat LSTM-512 (resnet+c3d+mfcc+category, '
+                            'V=%d, L=30)' % a.vocab,
+                   'global_batch': a.batch_size * S * ctx.world_size,
+                   'videos_per_gpu': a.batch_size, 'seq_per_img': S, 'seq_len': 30,
+                   'parallelism': 'dp%d' % ctx.world_size, 'impl': a.impl,
+                   'reward': a.reward, 'mode': a.mode, 'params': n_params,
+                   'dedupe_greedy': a.dedupe_greedy},
+        'final_loss': loss, 'datagen_s': round(t_gen, 1),
+    }
+    if ctx.is_main:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, 'w') as f:
+                f.write(line + '\n')
+    ctx.destroy()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,134 @@
+"""Flag system.
+
+Accepts every flag name of the reference (``/root/reference/opts.py:5-345``) so
+Makefile recipes written for the reference keep working, plus the new
+MI355X-specific flags (data parallelism, precision, kernel selection,
+synthetic data).
+
+Reference quirks kept on purpose:
+  * ``--optim*`` flags are accepted; the reference ignores them and always
+    uses Adam with default betas (``train.py:492``).  We honour them only when
+    ``--honor_optim_flags 1`` is given, so defaults reproduce the reference.
+  * ``--train_cached_tokens`` is ``type=str`` with an (odd) int default 30.
+"""
+import argparse
+import sys
+
+
+def build_parser():
+    p = argparse.ArgumentParser(
+        description='MI355X-native consensus/self-critical video captioning trainer')
+    add = p.add_argument
+
+    # ---- data (opts.py:8-57) -------------------------------------------------
+    for split in ('train', 'val', 'test'):
+        add('--%s_label_h5' % split, type=str,
+            help='path to the label file (h5, or .npz written by this framework)')
+        add('--%s_feat_h5' % split, type=str, nargs='+',
+            help='path(s) to the per-modality feature file(s)')
+        add('--%s_cocofmt_file' % split, type=str,
+            help='gold captions in MSCOCO format for language metrics')
+    add('--train_bcmrscores_pkl', type=str,
+        help='precomputed consensus scores of the GT captions (pkl or npz)')
+
+    # ---- optimisation (opts.py:58-150) --------------------------------------
+    add('--max_patience', type=int, default=5)
+    add('--batch_size', type=int, default=128)
+    add('--test_batch_size', type=int, default=32)
+    add('--train_seq_per_img', type=int, default=20)
+    add('--test_seq_per_img', type=int, default=20)
+    add('--learning_rate', type=float, default=1e-4)
+    add('--lr_update', type=int, default=50)
+    add('--rnn_type', type=str, default='lstm', choices=['lstm', 'gru', 'rnn'])
+    add('--rnn_size', type=int, default=512)
+    add('--num_lm_layer', type=int, default=1, help='unused (as in the reference)')
+    add('--input_encoding_size', type=int, default=512)
+    add('--max_epochs', type=int, default=sys.maxsize)
+    add('--grad_clip', type=float, default=0.25)
+    add('--drop_prob_lm', type=float, default=0.5)
+    add('--optim', type=str, default='adam')
+    add('--optim_alpha', type=float, default=0.8)
+    add('--optim_beta', type=float, default=0.999)
+    add('--optim_epsilon', type=float, default=1e-8)
+
+    # ---- evaluation / checkpointing (opts.py:153-233) -----------------------
+    add('--save_checkpoint_from', type=int, default=20)
+    add('--save_checkpoint_every', type=int, default=1)
+    add('--use_rl', type=int, default=0)
+    add('--use_rl_after', type=int, default=30)
+    add('--train_cached_tokens', type=str, default=30,
+        help='path to the index document-frequency pickle for CIDEr-D')
+    add('--expand_feat', type=int, default=1)
+    add('--model_file', type=str)
+    add('--result_file', type=str)
+    add('--start_from', type=str, default='')
+    add('--language_eval', type=int, default=1)
+    add('--eval_metric', default='CIDEr',
+        choices=['Loss', 'Bleu_4', 'METEOR', 'ROUGE_L', 'CIDEr', 'MSRVTT'])
+    add('--test_language_eval', type=int, default=1, help='unused (as in the reference)')
+    add('--print_log_interval', type=int, default=20)
+    add('--loglevel', type=str, default='DEBUG',
+        choices=['DEBUG', 'INFO', 'WARNING', 'ERROR', 'CRITICAL'])
+
+    # ---- misc / model (opts.py:234-345) -------------------------------------
+    add('--seed', type=int, default=123)
+    add('--gpuid', type=int, default=7, help='unused; device comes from LOCAL_RANK')
+    add('--num_chunks', type=int, default=1,
+        help='1: no attention, > 1: temporal attention over num_chunks frames')
+    add('--num_layers', type=int, default=1)
+    add('--model_type', type=str, default='concat',
+        choices=['standard', 'concat', 'manet'])
+    add('--beam_size', type=int, default=5)
+    add('--use_ss', type=int, default=0)
+    add('--use_ss_after', type=int, default=0)
+    add('--ss_max_prob', type=float, default=0.25)
+    add('--ss_k', type=float, default=30.0)
+    add('--use_mixer', type=int, default=1)
+    add('--mixer_from', type=int, default=-1)
+    add('--mixer_descrease_every', type=int, default=2)
+    add('--use_cst', type=int, default=0)
+    add('--use_cst_after', type=int, default=0)
+    add('--cst_increase_every', type=int, default=5)
+    add('--scb_baseline', type=int, default=1)
+    add('--scb_captions', type=int, default=20)
+    add('--use_eos', type=int, default=0)
+    add('--output_logp', type=int, default=0)
+
+    # ---- new: MI355X framework flags ----------------------------------------
+    add('--impl', type=str, default='auto', choices=['auto', 'hip', 'torch'],
+        help='decoder implementation: fused HIP engine, or plain PyTorch ops')
+    add('--precision', type=str, default='bf16', choices=['bf16', 'fp32'],
+        help='compute precision of the decoder GEMMs (master weights stay fp32)')
+    add('--reward_device', type=str, default='gpu', choices=['gpu', 'cpu'],
+        help='CIDEr-D reward: on-GPU HIP kernel, or the CPU scorer (reference semantics)')
+    add('--mask_after_eos', type=int, default=0,
+        help='fix for SURVEY §2.8.1: mask MIXER tokens sampled after EOS (0 = reference parity)')
+    add('--dedupe_greedy', type=int, default=1,
+        help='SCST: decode the greedy baseline once per video instead of x seq_per_img '
+             '(bit-identical rows; see models/caption_model.py)')
+    add('--honor_optim_flags', type=int, default=0,
+        help='use --optim_alpha/--optim_beta/--optim_epsilon for Adam (reference ignores them)')
+    add('--synthetic', type=str, default='',
+        help="'msrvtt' or 'msvd': generate a synthetic dataset of that shape instead of files")
+    add('--synthetic_vocab', type=int, default=10509)
+    add('--synthetic_videos', type=int, default=0, help='0 = dataset default')
+    add('--feat_dims', type=int, nargs='+', default=None,
+        help='synthetic feature dims (default: resnet 2048, c3d 4096, mfcc 1024, category 300)')
+    add('--seq_length', type=int, default=30, help='synthetic label length')
+    add('--save_last', type=int, default=1,
+        help='write a _last.pth sidecar with optimizer/RNG/loader state for exact resume')
+    add('--nan_guard', type=int, default=1, help='skip a step whose loss is not finite')
+    add('--profile_phases', type=int, default=0, help='log per-phase HIP-event timings')
+    return p
+
+
+def parse_opts(argv=None):
+    return build_parser().parse_args(argv)
+
+
+def default_opts(**overrides):
+    """Namespace with every default, optionally overridden (used by tests/bench)."""
+    opt = build_parser().parse_args([])
+    for k, v in overrides.items():
+        setattr(opt, k, v)
+    return opt

@@ -1,0 +1,284 @@
+"""HBM-resident dataset and batch loader.
+
+Reference: ``/root/reference/dataloader.py:15-218`` reads h5 features video by
+video in a Python loop every batch.  Here the whole split (MSR-VTT train:
+~6.5k videos x ~7.5k floats = ~0.2 GB) is uploaded to device memory once;
+a batch is an index gather on the GPU.  Per-batch host work is only the
+caption-slot choice (numpy, B x S ints) and one small H2D index copy.
+
+Batch semantics kept from the reference:
+  * ``seq_per_img`` captions per video: all captions plus uniform random
+    repeats when ``ncap <= S``, otherwise the first ``S`` of a random
+    permutation (``dataloader.py:125-135``);
+  * masks cover the caption plus its EOS (``nonzeros + 1``, ``:158-163``);
+  * ``gts`` = every GT label row of the video (for the reward);
+  * the epoch counter advances when the iterator wraps, and the train order
+    is reshuffled every epoch (``:146-152``).
+
+Data parallelism: all ranks share the shuffle seed, so they see the same
+global order; rank ``r`` takes videos ``[r*B, (r+1)*B)`` of each global batch
+of ``world_size * B`` videos (weak scaling; ``world_size=1`` is the reference).
+"""
+import logging
+
+import numpy as np
+import torch
+
+from . import formats
+
+logger = logging.getLogger(__name__)
+
+
+class VideoCaptionDataset:
+    """One split: vocabulary, labels, per-modality features, optional
+    consensus scores, GT references and the CIDEr-D df table."""
+
+    def __init__(self, vocab, videos, feats, labels=None, label_start_ix=None,
+                 label_end_ix=None, bcmrscores=None, gt_refs=None, cocofmt_file=None,
+                 df=None):
+        self.vocab = list(vocab)
+        self.ix_to_word = {i: w for i, w in enumerate(self.vocab)}
+        self.videos = [str(v) for v in videos]
+        self.video_ids = np.array([int(v) for v in self.videos], dtype=np.int64)
+        self.feats = [np.asarray(f, dtype=np.float32) for f in feats]
+        for f in self.feats:
+            if f.ndim != 3 or f.shape[0] != len(self.videos):
+                raise ValueError('features must be (N, C, dim), got %s' % (f.shape,))
+        self.labels = None if labels is None else np.asarray(labels, dtype=np.int64)
+        self.label_start_ix = None if labels is None else np.asarray(label_start_ix, np.int64)
+        self.label_end_ix = None if labels is None else np.asarray(label_end_ix, np.int64)
+        if self.labels is not None:
+            ncap = self.label_end_ix - self.label_start_ix
+            if (ncap <= 0).any():
+                raise ValueError('No captions!!')
+        self.bcmrscores = None if bcmrscores is None else np.asarray(bcmrscores, np.float64)
+        self.gt_refs = gt_refs
+        self.cocofmt_file = cocofmt_file
+        self.df = df  # (keys uint64, values float32, ref_len)
+        self._device_cache = {}
+
+    # -- reference getters (dataloader.py:172-218) ---------------------------
+    @property
+    def has_label(self):
+        return self.labels is not None
+
+    @property
+    def num_videos(self):
+        return len(self.videos)
+
+    @property
+    def seq_length(self):
+        return self.labels.shape[1]
+
+    @property
+    def vocab_size(self):
+        return len(self.vocab)
+
+    @property
+    def feat_dims(self):
+        return [f.shape[2] for f in self.feats]
+
+    @property
+    def num_chunks(self):
+        return self.feats[0].shape[1]
+
+    def gts_of(self, vid_index):
+        return self.labels[self.label_start_ix[vid_index]:self.label_end_ix[vid_index]]
+
+    def refs(self):
+        """GT references {video_id: [captions]} for language evaluation."""
+        if self.gt_refs is None and self.cocofmt_file:
+            from ..eval import load_gt_refs
+            self.gt_refs = load_gt_refs(self.cocofmt_file)
+        return self.gt_refs
+
+    def device_tensors(self, device):
+        """Features/labels uploaded once and cached per device."""
+        key = str(device)
+        if key not in self._device_cache:
+            d = {'feats': [torch.from_numpy(f).to(device) for f in self.feats]}
+            if self.has_label:
+                d['labels'] = torch.from_numpy(self.labels).to(device)
+            if self.bcmrscores is not None:
+                d['bcmrscores'] = torch.from_numpy(self.bcmrscores).float().to(device)
+            self._device_cache[key] = d
+        return self._device_cache[key]
+
+    @classmethod
+    def from_files(cls, label_file, feat_files, num_chunks=1, bcmrscores_file=None,
+                   eval_metric='CIDEr', cocofmt_file=None, df_file=None):
+        store = formats.load_label_file(label_file)
+        feats = [formats.load_feature_file(p, store['videos'], num_chunks) for p in feat_files]
+        bcmr = None
+        if bcmrscores_file:
+            from ..prepro.evalscores import load_scores
+            bcmr = load_scores(bcmrscores_file, eval_metric)
+        df = None
+        if df_file and isinstance(df_file, str):
+            from ..prepro.ciderdf import load_packed_df
+            df = load_packed_df(df_file)
+        return cls(store['vocab'], store['videos'], feats, store.get('labels'),
+                   store.get('label_start_ix'), store.get('label_end_ix'), bcmr,
+                   cocofmt_file=cocofmt_file, df=df)
+
+
+class CaptionLoader:
+    """Batch iterator over a :class:`VideoCaptionDataset` (reference
+    ``DataLoader`` API: ``get_batch``, ``reset``, getters, epoch counter)."""
+
+    def __init__(self, dataset, batch_size, seq_per_img, mode='train', device='cpu',
+                 rank=0, world_size=1, seed=123):
+        self.ds = dataset
+        self.batch_size = batch_size
+        self.seq_per_img = seq_per_img
+        self.mode = mode
+        self.device = torch.device(device)
+        self.rank = rank
+        self.world_size = world_size
+        self.iterator = 0
+        self.epoch = 0
+        self.index = np.arange(dataset.num_videos)
+        self._order_rng = np.random.RandomState(seed)          # shared by all ranks
+        self._cap_rng = np.random.RandomState(seed * 1009 + 7 + rank)  # rank-local
+        if mode == 'train':
+            self.shuffle_videos()
+
+    # -- reference getters ----------------------------------------------------
+    def get_vocab(self):
+        return self.ds.ix_to_word
+
+    def get_vocab_size(self):
+        return self.ds.vocab_size
+
+    def get_feat_dims(self):
+        return self.ds.feat_dims
+
+    def get_seq_length(self):
+        return self.ds.seq_length
+
+    def get_seq_per_img(self):
+        return self.seq_per_img
+
+    def get_num_videos(self):
+        return self.ds.num_videos
+
+    def get_batch_size(self):
+        return self.batch_size
+
+    def get_current_epoch(self):
+        return self.epoch
+
+    def set_current_epoch(self, epoch):
+        self.epoch = epoch
+
+    def get_current_index(self):
+        return self.iterator
+
+    def set_current_index(self, index):
+        self.iterator = index
+
+    def reset(self):
+        self.iterator = 0
+
+    def shuffle_videos(self):
+        self._order_rng.shuffle(self.index)
+
+    @property
+    def has_label(self):
+        return self.ds.has_label
+
+    @property
+    def cocofmt_file(self):
+        return self.ds.cocofmt_file
+
+    def state_dict(self):
+        return {'iterator': self.iterator, 'epoch': self.epoch, 'index': self.index.copy(),
+                'order_rng': self._order_rng.get_state(), 'cap_rng': self._cap_rng.get_state()}
+
+    def load_state_dict(self, s):
+        self.iterator, self.epoch = s['iterator'], s['epoch']
+        self.index = np.asarray(s['index'])
+        self._order_rng.set_state(s['order_rng'])
+        self._cap_rng.set_state(s['cap_rng'])
+
+    # -- batching ---------------------------------------------------------------
+    def _next_videos(self):
+        """Dataset indices of this rank's videos for the next batch."""
+        n = self.ds.num_videos
+        take = []
+        for g in range(self.batch_size * self.world_size):
+            idx = self.index[self.iterator]
+            if self.rank * self.batch_size <= g < (self.rank + 1) * self.batch_size:
+                take.append(idx)
+            self.iterator += 1
+            if self.iterator >= n:
+                logger.info('===> Finished loading epoch %d', self.epoch)
+                self.iterator = 0
+                self.epoch += 1
+                if self.mode == 'train':
+                    self.shuffle_videos()
+        return np.array(take, dtype=np.int64)
+
+    def _caption_rows(self, vids):
+        S = self.seq_per_img
+        rows = np.empty((len(vids), S), dtype=np.int64)
+        for i, v in enumerate(vids):
+            s, e = self.ds.label_start_ix[v], self.ds.label_end_ix[v]
+            ncap = e - s
+            if ncap <= S:
+                pick = np.concatenate([np.arange(ncap),
+                                       self._cap_rng.randint(ncap, size=S - ncap)])
+            else:
+                pick = self._cap_rng.permutation(ncap)[:S]
+            rows[i] = s + pick
+        return rows.reshape(-1)
+
+    def get_batch(self):
+        return self._assemble(self._next_videos())
+
+    def get_batch_at(self, ii):
+        """Evaluation batch ``ii`` of the fixed order: videos
+        ``[ii*B, min((ii+1)*B, N))``.  This equals the reference's
+        wrap-around batch followed by the last-batch truncation
+        (``train.py:296-308``) and lets ranks take disjoint batches."""
+        lo = ii * self.batch_size
+        hi = min(lo + self.batch_size, self.ds.num_videos)
+        return self._assemble(self.index[lo:hi].astype(np.int64))
+
+    def _assemble(self, vids):
+        dev = self.ds.device_tensors(self.device)
+        vid_t = torch.from_numpy(vids).to(self.device, non_blocking=True)
+        data = {'video_index': vid_t, 'vids': vids,
+                'ids': self.ds.video_ids[vids].tolist(),
+                'feats': [f.index_select(0, vid_t) for f in dev['feats']]}
+        if self.has_label:
+            rows = self._caption_rows(vids)
+            rows_t = torch.from_numpy(rows).to(self.device, non_blocking=True)
+            labels = dev['labels'].index_select(0, rows_t)
+            n = (labels != 0).sum(1, keepdim=True) + 1
+            pos = torch.arange(labels.shape[1], device=labels.device)[None, :]
+            data['labels'] = labels
+            data['masks'] = (pos < n).float()
+            data['gts'] = _LazyGts(self.ds, vids)
+            if 'bcmrscores' in dev:
+                data['bcmrscores'] = dev['bcmrscores'].index_select(0, vid_t)
+            else:
+                data['bcmrscores'] = None
+        return data
+
+
+class _LazyGts:
+    """List-like per-video GT label arrays, materialised only if a CPU
+    scorer asks for them (the GPU reward never does)."""
+
+    def __init__(self, ds, vids):
+        self.ds, self.vids = ds, vids
+
+    def __len__(self):
+        return len(self.vids)
+
+    def __getitem__(self, i):
+        return self.ds.gts_of(self.vids[i])
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))

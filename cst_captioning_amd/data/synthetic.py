@@ -1,0 +1,115 @@
+"""Synthetic datasets with the shapes of MSR-VTT and MSVD.
+
+There is no network (no datasets, no features), so benchmarks and
+integration tests run on generated data that has the reference workload's
+*shape*:
+
+  * ``msrvtt``: 6,513 train videos, exactly 20 captions each, 4 modalities
+    (ResNet-152 2048, C3D 4096, MFCC 1024, category GloVe 300 -- dims are
+    the SURVEY.md §2.3 assumptions), vocabulary ~10.5k, max length 30;
+  * ``msvd``: 1,200 videos with a *variable* number of captions (≈20-60,
+    so ``ncap > S`` and ``ncap < S`` both occur), 2 modalities.
+
+Captions are not noise: every video has a latent topic, features are a
+topic embedding plus noise, and caption words are drawn from a Zipf law over
+a topic-specific word permutation.  A model can therefore learn the task
+(used by the "loss decreases / CIDEr improves" integration tests).
+
+The generator goes through the real preprocessing code path
+(tokens -> vocab -> label store -> df table), so synthetic artefacts are
+exactly what ``prepro`` would write for a real dataset of that shape.
+"""
+import numpy as np
+
+from ..prepro.vocab import SPECIALS
+from ..prepro.labels import build_label_store
+from ..prepro.ciderdf import df_from_token_refs
+from .dataset import VideoCaptionDataset
+
+MSRVTT_FEAT_DIMS = [2048, 4096, 1024, 300]
+MSVD_FEAT_DIMS = [2048, 4096]
+
+
+def _captions_for(rng, topic_perm, n_words, ncap, mean_len, max_words, zipf_a):
+    caps = []
+    for _ in range(ncap):
+        n = int(np.clip(np.round(rng.normal(mean_len, 3.0)), 3, max_words))
+        ranks = np.minimum(rng.zipf(zipf_a, size=n) - 1, n_words - 1)
+        caps.append(['w%d' % topic_perm[r] for r in ranks])
+    return caps
+
+
+def make_synthetic(kind='msrvtt', num_videos=None, vocab_size=10509, seq_length=30,
+                   feat_dims=None, num_chunks=1, n_topics=64, seed=0, mean_len=9.3,
+                   with_consensus=False, split='train', start_video_id=0, consensus_cols=20):
+    rng = np.random.RandomState(seed)
+    if kind == 'msrvtt':
+        num_videos = num_videos or 6513
+        feat_dims = feat_dims or MSRVTT_FEAT_DIMS
+        caps_per_video = lambda: 20
+    elif kind == 'msvd':
+        num_videos = num_videos or 1200
+        feat_dims = feat_dims or MSVD_FEAT_DIMS
+        caps_per_video = lambda: int(rng.randint(8, 61))
+    else:
+        raise ValueError('unknown synthetic dataset %r' % kind)
+    n_words = vocab_size - len(SPECIALS)
+    if n_words < 8:
+        raise ValueError('vocab_size too small')
+    # topic structure: a shared Zipf head + topic-specific tails
+    topic_perm = [np.concatenate([np.arange(min(32, n_words)),
+                                  rng.permutation(np.arange(min(32, n_words), n_words))])
+                  for _ in range(n_topics)]
+    topics = rng.randint(n_topics, size=num_videos)
+    # Every word appears in the vocab: word ids are w0..w{n_words-1}, and the
+    # vocabulary is built in id order (threshold 0), so ids are stable.
+    words = ['w%d' % i for i in range(n_words)]
+    vocab = SPECIALS + words
+    videos = []
+    for i in range(num_videos):
+        toks = _captions_for(rng, topic_perm[topics[i]], n_words, caps_per_video(), mean_len,
+                             seq_length + 6, 1.35)
+        videos.append({'video_id': start_video_id + i, 'captions': [' '.join(t) for t in toks],
+                       'processed_tokens': toks, 'category': int(topics[i])})
+    store = build_label_store(vocab, videos, seq_length)
+    # features: topic embedding + noise (+ per-chunk jitter)
+    feats = []
+    for d in feat_dims:
+        emb = rng.normal(0, 1, size=(n_topics, d)).astype(np.float32)
+        base = emb[topics] + 0.5 * rng.normal(0, 1, size=(num_videos, d)).astype(np.float32)
+        f = np.repeat(base[:, None, :], num_chunks, axis=1)
+        if num_chunks > 1:
+            f = f + 0.25 * rng.normal(0, 1, size=f.shape).astype(np.float32)
+        feats.append(np.maximum(f, 0) if d != 300 else f)  # ReLU-like CNN features
+    # CIDEr-D df over index refs (compute_ciderdf.py semantics: no BOS, + EOS)
+    wtoi = {w: i for i, w in enumerate(vocab)}
+    eos = wtoi['<end>']
+    refs_idx = [[[wtoi[w] for w in t] + [eos] for t in v['processed_tokens']] for v in videos]
+    df = df_from_token_refs(refs_idx)
+    keys = np.fromiter(df[0].keys(), dtype=np.uint64, count=len(df[0]))
+    vals = np.fromiter(df[0].values(), dtype=np.float32, count=len(df[0]))
+    gt_refs = {start_video_id + i: v['captions'] for i, v in enumerate(videos)}
+    bcmr = None
+    if with_consensus:
+        from ..prepro.evalscores import compute_consensus_scores
+        bcmr = compute_consensus_scores(gt_refs, consensus_cols, True, tokenize=False,
+                                        metrics=('CIDEr',))['CIDEr']
+    return VideoCaptionDataset(vocab, store['videos'], feats, store['labels'],
+                               store['label_start_ix'], store['label_end_ix'], bcmr,
+                               gt_refs=gt_refs, df=(keys, vals, df[1]))
+
+
+def make_splits(kind='msrvtt', vocab_size=10509, seq_length=30, feat_dims=None,
+                num_chunks=1, train_videos=None, eval_videos=None, seed=0,
+                with_consensus=False, seq_per_img=20):
+    """(train, val, test) synthetic splits sharing one vocabulary."""
+    tr = make_synthetic(kind, train_videos, vocab_size, seq_length, feat_dims, num_chunks,
+                        seed=seed, with_consensus=with_consensus, consensus_cols=seq_per_img)
+    n_eval = eval_videos or max(8, (train_videos or 600) // 10)
+    va = make_synthetic(kind, n_eval, vocab_size, seq_length, feat_dims, num_chunks,
+                        seed=seed + 1, start_video_id=10 ** 6)
+    te = make_synthetic(kind, n_eval, vocab_size, seq_length, feat_dims, num_chunks,
+                        seed=seed + 2, start_video_id=2 * 10 ** 6)
+    # train df is the one used for CIDEr-D rewards on every split
+    va.df = te.df = tr.df
+    return tr, va, te

@@ -1,0 +1,92 @@
+"""Fused global-norm clip + Adam over one flat parameter buffer.
+
+Replaces ``clip_grad_norm_(model.parameters(), grad_clip)`` +
+``optim.Adam(lr)`` (``/root/reference/train.py:217-218,492``; default betas
+(0.9, 0.999), eps 1e-8, no weight decay) with one pass over the flat
+buffers of :class:`..parallel.FlatGradBucket`:
+
+  * pass 1: sum of squares of the gradient (one block-reduction kernel);
+  * pass 2: ``coef = min(1, clip / (norm + 1e-6))`` is computed ON DEVICE
+    and applied inside the Adam update, which also refreshes the bf16
+    shadow copies of the decoder weights used by the MFMA kernels.
+
+No host synchronisation.  The math is PyTorch's Adam:
+``denom = sqrt(v) / sqrt(1 - b2^t) + eps``,
+``p -= lr / (1 - b1^t) * m / denom``.
+
+Without the HIP extension (CPU) the same math runs as torch ops.
+"""
+import math
+
+import torch
+
+from .. import _ext
+
+
+class FlatAdam:
+    def __init__(self, bucket, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, grad_clip=0.25):
+        self.bucket = bucket
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.grad_clip = grad_clip
+        self.step_count = 0
+        self.exp_avg = torch.zeros_like(bucket.data)
+        self.exp_avg_sq = torch.zeros_like(bucket.data)
+        self.param_groups = [{'lr': lr}]  # for adjust_learning_rate()
+        self.last_norm = None
+        self._use_hip = _ext.available() and bucket.data.is_cuda
+        if self._use_hip:
+            self._partials = torch.empty(1024, dtype=torch.float32, device=bucket.data.device)
+            self._scal = torch.empty(2, dtype=torch.float32, device=bucket.data.device)
+
+    def zero_grad(self):
+        self.bucket.zero_grad()
+
+    def step(self, skip=None):
+        """``skip``: optional 0-dim bool device tensor; when true the update
+        is a no-op (NaN guard without a host sync)."""
+        self.lr = self.param_groups[0]['lr']
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
+        g, p = self.bucket.grad, self.bucket.data
+        if self._use_hip:
+            self.last_norm = _ext.ops().flat_adam_step(
+                p, g, self.exp_avg, self.exp_avg_sq, self._partials, self._scal,
+                skip if skip is not None else torch.zeros((), dtype=torch.bool, device=p.device),
+                float(self.lr), float(b1), float(b2), float(self.eps),
+                float(self.grad_clip), float(bc1), float(bc2))
+            return self.last_norm
+        norm = torch.linalg.vector_norm(g)
+        self.last_norm = norm
+        coef = torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0)
+        if skip is not None:
+            keep = (~skip).float()
+        else:
+            keep = None
+        gc = g * coef
+        m_new = self.exp_avg * b1 + gc * (1 - b1)
+        v_new = self.exp_avg_sq * b2 + gc * gc * (1 - b2)
+        denom = v_new.sqrt() / math.sqrt(bc2) + self.eps
+        upd = m_new / denom * (self.lr / bc1)
+        if keep is None:
+            self.exp_avg.copy_(m_new)
+            self.exp_avg_sq.copy_(v_new)
+            p.sub_(upd)
+        else:
+            self.exp_avg.copy_(torch.lerp(self.exp_avg, m_new, keep))
+            self.exp_avg_sq.copy_(torch.lerp(self.exp_avg_sq, v_new, keep))
+            p.sub_(upd * keep)
+        return norm
+
+    def state_dict(self):
+        return {'step': self.step_count, 'exp_avg': self.exp_avg, 'exp_avg_sq': self.exp_avg_sq,
+                'lr': self.param_groups[0]['lr'], 'betas': self.betas, 'eps': self.eps}
+
+    def load_state_dict(self, s):
+        self.step_count = s['step']
+        self.exp_avg.copy_(s['exp_avg'])
+        self.exp_avg_sq.copy_(s['exp_avg_sq'])
+        self.param_groups[0]['lr'] = s['lr']

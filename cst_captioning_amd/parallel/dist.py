@@ -1,0 +1,175 @@
+"""Data-parallel communication over ``torch.distributed`` (RCCL on ROCm).
+
+The reference is single-GPU with no collectives.  This
+layer adds DP for one node of MI355X GPUs, one process per GPU:
+
+  C1  broadcast of parameters/buffers from rank 0 at start;
+  C2  ONE all-reduce per step of the whole gradient as a single flat
+      bucket.  The decoder is trained by BPTT, so every gradient is only
+      final after the full reverse time loop: bucketed overlap with backward
+      would buy nothing, while one large message is what a point-to-point
+      xGMI ring moves at full per-link bandwidth (~20 M params = 81 MB fp32,
+      ~0.5 ms at 8 GPUs).  288 GB HBM makes the contiguous buffer free;
+  C3  all-reduce of a small vector of log scalars;
+  C4  all-gather of per-rank evaluation results;
+  C5  broadcast of rank-0 decisions (best model / early stop);
+  C6  barrier around rank-0 checkpoint IO.
+
+CPU tests use the gloo backend with the same code.
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class DistContext:
+    def __init__(self, rank=0, world_size=1, local_rank=0, device=None, backend=None):
+        self.rank = rank
+        self.world_size = world_size
+        self.local_rank = local_rank
+        self.device = device if device is not None else torch.device('cpu')
+        self.backend = backend
+
+    @property
+    def enabled(self):
+        return self.world_size > 1
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+    # -- collectives ------------------------------------------------------------
+    def barrier(self):
+        if self.enabled:
+            if self.backend == 'nccl':
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def all_reduce_(self, t, average=False):
+        if self.enabled:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            if average:
+                t.div_(self.world_size)
+        return t
+
+    def broadcast_(self, t, src=0):
+        if self.enabled:
+            dist.broadcast(t, src)
+        return t
+
+    def broadcast_object(self, obj, src=0):
+        if not self.enabled:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src)
+        return box[0]
+
+    def all_gather_object(self, obj):
+        if not self.enabled:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj)
+        return out
+
+    def max_scalar(self, x):
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.comm_device)
+        if self.enabled:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    @property
+    def comm_device(self):
+        return self.device if self.backend == 'nccl' else torch.device('cpu')
+
+    def broadcast_module(self, module):
+        """C1: every parameter and buffer from rank 0 (one flat message)."""
+        if not self.enabled:
+            return
+        tensors = [t for t in list(module.parameters()) + list(module.buffers())
+                   if t.dtype.is_floating_point]
+        if not tensors:
+            return
+        flat = torch.cat([t.detach().reshape(-1).float() for t in tensors]).to(self.comm_device)
+        dist.broadcast(flat, 0)
+        off = 0
+        with torch.no_grad():
+            for t in tensors:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t).to(t.device, t.dtype))
+                off += n
+
+    def destroy(self):
+        if self.enabled and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def init_distributed(device_type=None, timeout_s=600):
+    """Initialise from the torchrun environment (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR/PORT).  Single process when WORLD_SIZE is unset."""
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if device_type is None:
+        device_type = 'cuda' if torch.cuda.is_available() else 'cpu'
+    if device_type == 'cuda':
+        torch.cuda.set_device(local)
+        device = torch.device('cuda', local)
+    else:
+        device = torch.device('cpu')
+    backend = None
+    if world > 1:
+        backend = 'nccl' if device_type == 'cuda' else 'gloo'
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        kw = {}
+        if backend == 'nccl':
+            kw['device_id'] = device
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return DistContext(rank, world, local, device, backend)
+
+
+class FlatGradBucket:
+    """All trainable parameters re-homed into one contiguous fp32 buffer,
+    with their ``.grad`` tensors viewing one contiguous gradient buffer.
+
+    Autograd accumulates into the views in place, so after ``backward()`` the
+    whole gradient is one tensor: one all-reduce (C2) and one fused
+    clip + Adam kernel cover every parameter.
+    """
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError('no trainable parameters')
+        dev = self.params[0].device
+        total = sum(p.numel() for p in self.params)
+        self.data = torch.empty(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.slices = []
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            self.data[off:off + n].copy_(p.detach().reshape(-1))
+            p.data = self.data[off:off + n].view_as(p)
+            p.grad = self.grad[off:off + n].view_as(p)
+            self.slices.append((off, n))
+            off += n
+        self.numel = total
+
+    def zero_grad(self):
+        self.grad.zero_()
+        # autograd may have replaced a view (e.g. after set_to_none); re-point
+        for p, (off, n) in zip(self.params, self.slices):
+            if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
+                p.grad = self.grad[off:off + n].view_as(p)
+
+    def all_reduce(self, ctx):
+        if ctx.enabled:
+            if ctx.backend == 'nccl':
+                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+            else:
+                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+            self.grad.div_(ctx.world_size)

@@ -1,0 +1,371 @@
+"""Training / validation driver.
+
+Behaviour of ``/root/reference/train.py:45-418``:
+
+  * loop ``while True``: batch -> scheduled-sampling / RL / MIXER / SCB
+    schedules -> forward -> loss -> backward -> clip(0.25) -> Adam;
+  * XE: teacher-forced cross entropy;
+  * RL (``--use_rl 1`` from epoch ``use_rl_after``; 0 = the resume epoch):
+      - SCST (``use_cst 0``): greedy decode baseline (``train.py:175-180``),
+      - CST (``use_cst 1``): consensus baseline from GT or sample scores,
+      - WXE (``use_cst 1, use_mixer 0``): precomputed GT scores as weights;
+  * LR step decay on epoch change; validation + best-model checkpoint from
+    ``save_checkpoint_from``; stop at ``max_epochs`` or after
+    ``max_patience`` epochs without improvement.
+
+MI355X-side changes (same semantics): the batch comes from HBM, the reward
+is computed on the GPU (no host round trip), the greedy SCST baseline is
+decoded once per video instead of once per (video, caption) row (FeatPool
+dropout is applied before the x seq_per_img expansion, ``model.py:220-221``,
+so the expanded rows are identical), gradients live in one flat bucket that
+is all-reduced once per step (DP), and clip + Adam is one fused kernel.
+Host synchronisation happens only at log / eval time.
+"""
+import json
+import logging
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..models import CrossEntropyCriterion, RewardCriterion
+from ..ops.adam import FlatAdam
+from ..ops.cider_d import CiderDScorer, GenericScorer
+from ..parallel import FlatGradBucket
+from ..reward.rewards import cst_from_scores, scst_from_scores
+from ..utils import schedules
+from ..utils.text import decode_sequence, compute_avglogp
+from ..utils.timers import PhaseTimer
+from . import checkpoint as ckpt
+
+logger = logging.getLogger(__name__)
+
+
+def build_scorer(opt, dataset, device):
+    metric = opt.eval_metric
+    if metric in ('CIDEr', 'MSRVTT', 'Loss'):
+        backend = 'auto'
+        if getattr(opt, 'reward_device', 'gpu') == 'cpu':
+            backend = 'cpu-ref'
+        return CiderDScorer(dataset, use_eos=opt.use_eos, device=device, backend=backend)
+    from ..eval.metrics import Bleu, Meteor, Rouge
+    sc = {'Bleu_4': Bleu(4), 'METEOR': Meteor(), 'ROUGE_L': Rouge()}[metric]
+    return GenericScorer(dataset, sc, opt.use_eos)
+
+
+class Trainer:
+    def __init__(self, opt, model, train_loader, val_loader=None, ctx=None, engine=None):
+        from ..parallel import DistContext
+        self.opt = opt
+        self.model = model
+        self.train_loader = train_loader
+        self.val_loader = val_loader
+        self.ctx = ctx or DistContext()
+        self.engine = engine
+        self.device = self.ctx.device
+        self.xe_criterion = CrossEntropyCriterion()
+        self.rl_criterion = RewardCriterion()
+        self.ctx.broadcast_module(model)
+        self.bucket = FlatGradBucket(model.parameters())
+        if getattr(opt, 'honor_optim_flags', 0):
+            betas, eps = (opt.optim_alpha, opt.optim_beta), opt.optim_epsilon
+        else:
+            betas, eps = (0.9, 0.999), 1e-8  # train.py:492 ignores --optim_*
+        self.optimizer = FlatAdam(self.bucket, opt.learning_rate, betas, eps, opt.grad_clip)
+        if engine is not None:
+            engine.attach_optimizer(self)
+        self.scorer = None
+        self.timer = PhaseTimer(enabled=bool(getattr(opt, 'profile_phases', 0)))
+        self.infos = {'iter': 0, 'epoch': 0, 'start_epoch': 0, 'best_score': float('-inf'),
+                      'best_iter': 0, 'best_epoch': opt.max_epochs}
+        self.history = {}
+        self.rl_training = False
+
+    # ------------------------------------------------------------------ RL ---
+    def _ensure_scorer(self):
+        if self.scorer is None:
+            self.scorer = build_scorer(self.opt, self.train_loader.ds, self.device)
+        return self.scorer
+
+    def _decode_rollout(self, data):
+        """Forward pass.  Returns (sample_seq, sample_logprobs, pred)."""
+        m = self.model
+        if self.engine is not None:
+            return self.engine.rollout(m, data['feats'], data['labels'])
+        pred, seq, lp = m(data['feats'], data['labels'])
+        return seq, lp, pred
+
+    def _greedy_scores(self, data, scorer, S):
+        """SCST baseline scores, one per rewarded row (R,)."""
+        opt, m = self.opt, self.model
+        vid = data['video_index']
+        if opt.expand_feat == 1 and getattr(opt, 'dedupe_greedy', 1):
+            with torch.no_grad():
+                g, _ = m.sample(data['feats'], {'sample_max': 1, 'expand_feat': 0})
+            gs = scorer.score(g, vid)
+            return gs.repeat_interleave(S)
+        with torch.no_grad():
+            g, _ = m.sample(data['feats'], {'sample_max': 1, 'expand_feat': opt.expand_feat})
+        gvid = vid.repeat_interleave(S) if opt.expand_feat == 1 else vid
+        return scorer.score(g, gvid)
+
+    def rl_loss(self, data, scb_captions):
+        opt = self.opt
+        S = self.train_loader.get_seq_per_img()
+        model_res, logprobs, _ = self._decode_rollout(data)
+        self.timer.mark('rollout')
+        scorer = self._ensure_scorer()
+        vid_rows = data['video_index'].repeat_interleave(S)
+        if opt.use_cst == 0:
+            sample_scores = scorer.score(model_res, vid_rows)
+            greedy_scores = self._greedy_scores(data, scorer, S)
+            reward, m_score, b_score = scst_from_scores(sample_scores.float(),
+                                                        greedy_scores.float())
+        else:
+            bcmr = data.get('bcmrscores')
+            if bcmr is None or opt.use_mixer == 1:
+                scores = scorer.score(model_res, vid_rows).float().view(-1, S)
+            else:
+                scores = bcmr.float()
+            reward, m_score, b_score = cst_from_scores(scores, bcmr, scb_captions,
+                                                       opt.scb_baseline)
+        self.timer.mark('reward')
+        loss = self.rl_criterion(model_res, logprobs, reward.detach().to(logprobs.dtype))
+        return loss, {'reward': reward, 'm': m_score, 'b': b_score}
+
+    def xe_loss(self, data):
+        if self.engine is not None:
+            lp = self.engine.teacher_forced(self.model, data['feats'], data['labels'])
+            self.timer.mark('rollout')
+            return self.xe_criterion(lp, data['labels'][:, 1:], data['masks'][:, 1:]), {}
+        pred = self.model(data['feats'], data['labels'])[0]
+        self.timer.mark('rollout')
+        return self.xe_criterion(pred, data['labels'][:, 1:], data['masks'][:, 1:]), {}
+
+    # --------------------------------------------------------------- step ---
+    def train_step(self, data, epoch):
+        opt, m, infos = self.opt, self.model, self.infos
+        self.timer.reset()
+        self.timer.mark('start')
+        m.train()
+        ssp = schedules.ss_prob(opt, epoch)
+        opt.ss_prob = ssp
+        if ssp > 0 or opt.use_ss == 1:
+            m.set_ss_prob(ssp)
+        if opt.use_rl == 1 and epoch >= opt.use_rl_after and not self.rl_training:
+            logger.info('Using RL objective...')
+            self.rl_training = True
+        mixer_from = opt.mixer_from
+        if opt.use_mixer == 1 and self.rl_training:
+            mixer_from = schedules.mixer_from(opt, epoch, opt.seq_length)
+            m.set_mixer_from(mixer_from)
+        scb = opt.scb_captions
+        if opt.use_cst == 1 and self.rl_training:
+            scb = schedules.scb_captions(opt, epoch, self.train_loader.get_seq_per_img())
+        self.optimizer.zero_grad()
+        m.set_seq_per_img(self.train_loader.get_seq_per_img())
+        if self.rl_training:
+            loss, extra = self.rl_loss(data, scb)
+        else:
+            loss, extra = self.xe_loss(data)
+        loss.backward()
+        self.timer.mark('backward')
+        self.bucket.all_reduce(self.ctx)
+        self.timer.mark('allreduce')
+        skip = None
+        if getattr(opt, 'nan_guard', 1):
+            bad = ~torch.isfinite(loss.detach())
+            if self.ctx.enabled:  # every rank must skip together
+                b = bad.float().reshape(1)
+                self.ctx.all_reduce_(b)
+                bad = b[0] > 0
+            skip = bad
+        self.optimizer.step(skip)
+        if self.engine is not None:
+            self.engine.after_step()
+        self.timer.mark('optimizer')
+        extra.update(loss=loss.detach(), mixer_from=mixer_from, scb_captions=scb)
+        return extra
+
+    # --------------------------------------------------------------- loop ---
+    def resume(self):
+        opt = self.opt
+        path = ckpt.resolve_start_from(opt.start_from, opt.model_file or '')
+        last = ckpt.last_path(opt.model_file) if opt.model_file else None
+        if last and getattr(opt, 'save_last', 1) and os.path.exists(last):
+            s = ckpt.load_checkpoint(last, map_location=self.device)
+            self.model.load_state_dict(s['model'])
+            self.optimizer.load_state_dict(s['optimizer'])
+            self.train_loader.load_state_dict(s['loader'])
+            ckpt.restore_rng(s['rng'])
+            self.infos = s['infos']
+            logger.info('Resumed exactly from %s (iter %d)', last, self.infos['iter'])
+            return True
+        if path and os.path.exists(path):
+            logger.info('Loading state from: %s', path)
+            s = ckpt.load_checkpoint(path, map_location=self.device)
+            self.model.load_state_dict(s['model'])
+            self.infos = s['infos']
+            self.infos['start_epoch'] = self.infos['epoch']
+            return True
+        logger.info('No checkpoint found! Training from the scratch')
+        return False
+
+    def train(self):
+        opt, infos = self.opt, None
+        checked = self.resume()
+        infos = self.infos
+        if opt.model_file and self.ctx.is_main and not os.path.exists(opt.model_file):
+            logger.info('>>> No model file found. Write a base checkpoint.')
+            ckpt.save_checkpoint(self.model, infos, opt, opt.model_file)
+        self.ctx.barrier()
+        if opt.use_rl == 1 and opt.use_rl_after == 0:
+            opt.use_rl_after = infos['epoch']
+            opt.use_cst_after = infos['epoch']
+            self.train_loader.set_current_epoch(infos['epoch'])
+        while True:
+            t0 = time.time()
+            data = self.train_loader.get_batch()
+            out = self.train_step(data, infos['epoch'])
+            infos['mixer_from'] = out['mixer_from']
+            infos['scb_captions'] = out['scb_captions']
+            if opt.print_log_interval and infos['iter'] % opt.print_log_interval == 0:
+                self._log(out, time.time() - t0)
+            infos['iter'] += 1
+            if infos['epoch'] < self.train_loader.get_current_epoch():
+                infos['epoch'] = self.train_loader.get_current_epoch()
+                checked = False
+                lr = schedules.adjust_learning_rate(opt, self.optimizer,
+                                                    infos['epoch'] - infos['start_epoch'])
+                logger.info('===> Learning rate: %f: ', lr)
+                if opt.model_file and getattr(opt, 'save_last', 1) and self.ctx.is_main:
+                    ckpt.save_last(ckpt.last_path(opt.model_file), self.model, self.optimizer,
+                                   infos, opt, self.train_loader)
+            if (self.val_loader is not None and infos['epoch'] >= opt.save_checkpoint_from
+                    and infos['epoch'] % opt.save_checkpoint_every == 0 and not checked):
+                results = self.validate(self.val_loader)
+                if self.ctx.is_main:
+                    logger.info('Validation output: %s',
+                                json.dumps(results['scores'], indent=4, sort_keys=True))
+                infos.update(results['scores'])
+                self.check_model()
+                checked = True
+            if infos['epoch'] >= opt.max_epochs or \
+                    infos['epoch'] - infos['best_epoch'] > opt.max_patience:
+                logger.info('>>> Terminating...')
+                break
+        return infos
+
+    def _log(self, out, elapsed):
+        opt, infos = self.opt, self.infos
+        loss = float(out['loss'])
+        infos['TrainLoss'] = loss
+        items = [('Epoch', infos['epoch']), ('Iter', infos['iter']), ('Loss', loss)]
+        if self.rl_training:
+            items += [('Reward', float(out['reward'].float().mean())),
+                      ('{} (m)'.format(opt.eval_metric), float(out['m'])),
+                      ('{} (b)'.format(opt.eval_metric), float(out['b']))]
+        if opt.use_ss == 1:
+            items.append(('ss_prob', opt.ss_prob))
+        if opt.use_mixer == 1:
+            items.append(('mixer_from', out['mixer_from']))
+        if opt.use_cst == 1:
+            items.append(('scb_captions', out['scb_captions']))
+        items.append(('Time', elapsed))
+        ph = self.timer.summary()
+        if ph:
+            items.append(('phases_ms', ','.join('%s=%.2f' % kv for kv in ph.items())))
+        if self.ctx.is_main:
+            logger.info('%s', '\t'.join('{}: {}'.format(k, v) for k, v in items))
+
+    # ----------------------------------------------------------- validate ---
+    @torch.no_grad()
+    def validate(self, loader):
+        opt, m, ctx = self.opt, self.model, self.ctx
+        m.eval()
+        n_videos = loader.get_num_videos()
+        bsz = loader.get_batch_size()
+        n_iters = int(math.ceil(n_videos / bsz))
+        S = loader.get_seq_per_img()
+        m.set_seq_per_img(S)
+        local = {'pred': [], 'loss': [], 'gt_avglogp': [], 'test_avglogp': []}
+        for ii in range(ctx.rank, n_iters, ctx.world_size):  # C4: batches sharded over ranks
+            data = loader.get_batch_at(ii)
+            if loader.has_label:
+                if self.engine is not None:
+                    lp = self.engine.teacher_forced(m, data['feats'], data['labels'])
+                    loss = self.xe_criterion(lp, data['labels'][:, 1:], data['masks'][:, 1:])
+                    gt_seq, gt_lp = data['labels'][:, 1:lp.size(1) + 1], lp
+                else:
+                    pred, gt_seq, gt_lp = m(data['feats'], data['labels'])
+                    loss = self.xe_criterion(pred, data['labels'][:, 1:], data['masks'][:, 1:])
+                local['loss'].append((ii, float(loss)))
+                if opt.output_logp == 1:
+                    local['gt_avglogp'].append(
+                        (ii, compute_avglogp(gt_seq.cpu().numpy(), gt_lp.cpu().numpy())))
+            seq, logseq = m.sample(data['feats'], {'beam_size': opt.beam_size})
+            seq, logseq = seq.cpu().numpy(), logseq.cpu().numpy()
+            sents = decode_sequence(loader.get_vocab(), seq)
+            avg = compute_avglogp(seq, logseq) if opt.output_logp == 1 else None
+            for jj, sent in enumerate(sents):
+                e = {'image_id': data['ids'][jj], 'caption': sent}
+                if avg is not None:
+                    e['avglogp'] = avg[jj]
+                local['pred'].append((ii, jj, e))
+                logger.debug('[%d] video %s: %s', jj, e['image_id'], sent)
+        gathered = ctx.all_gather_object(local)
+        preds = sorted((p for g in gathered for p in g['pred']), key=lambda x: (x[0], x[1]))
+        predictions = [p[2] for p in preds]
+        losses = [l for g in gathered for _, l in g['loss']]
+        results = {'predictions': predictions}
+        scores = {'Loss': -round(sum(losses) / n_iters, 3) if losses else 0.0}
+        if ctx.is_main and opt.language_eval == 1 and loader.has_label:
+            from ..eval import language_eval
+            refs = loader.ds.refs()
+            if refs:
+                scores.update(language_eval(refs, predictions))
+        if opt.output_logp == 1:
+            ta = [p['avglogp'] for p in predictions]
+            scores['avglogp'] = sum(ta) / len(ta)
+            gl = sorted((x for g in gathered for x in g['gt_avglogp']), key=lambda x: x[0])
+            gt = np.array([v for _, l in gl for v in l]).reshape(-1, S)
+            if ctx.is_main and opt.model_file:
+                np.save(opt.model_file.replace('.pth', '_gt_avglogps.npy', 1), gt)
+        results['scores'] = ctx.broadcast_object(scores)
+        m.train()
+        return results
+
+    def test(self, loader):
+        results = self.validate(loader)
+        if self.ctx.is_main:
+            logger.info('Test output: %s', json.dumps(results['scores'], indent=4))
+            if self.opt.result_file:
+                with open(self.opt.result_file, 'w') as f:
+                    json.dump(results, f)
+                logger.info('Wrote output caption to: %s ', self.opt.result_file)
+        return results
+
+    def check_model(self):
+        opt, infos = self.opt, self.infos
+        if opt.eval_metric == 'MSRVTT':
+            cur = infos['Bleu_4'] + infos['METEOR'] + infos['ROUGE_L'] + infos['CIDEr']
+        else:
+            cur = infos[opt.eval_metric]
+        if cur >= infos['best_score']:
+            infos['best_score'] = cur
+            infos['best_iter'] = infos['iter']
+            infos['best_epoch'] = infos['epoch']
+            logger.info('>>> Found new best [%s] score: %f, at iter: %d, epoch %d',
+                        opt.eval_metric, cur, infos['iter'], infos['epoch'])
+            if self.ctx.is_main and opt.model_file:
+                ckpt.save_checkpoint(self.model, infos, opt, opt.model_file)
+        else:
+            logger.info('>>> Current best [%s] score: %f, at iter %d, epoch %d',
+                        opt.eval_metric, infos['best_score'], infos['best_iter'],
+                        infos['best_epoch'])
+        self.history[infos['epoch']] = dict(infos)
+        if self.ctx.is_main:
+            ckpt.write_history(getattr(opt, 'history_file', None), self.history)
+        self.ctx.barrier()
