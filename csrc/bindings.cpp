@@ -1,0 +1,84 @@
+// Python bindings of the native extension cst_captioning_amd._C.
+#include <torch/extension.h>
+
+#include "host/cider_host.h"
+
+namespace cst {
+std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor wlog,
+                                        at::Tensor blog, at::Tensor vgate, int64_t vgate_div,
+                                        at::Tensor labels, at::Tensor bos, int64_t R, int64_t T,
+                                        std::vector<int64_t> modes, double ss_prob,
+                                        double drop_p, double temperature, int64_t seed,
+                                        bool save, bool want_xe, bool use_counts,
+                                        bool use_unfinished);
+std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor lse,
+                                         at::Tensor logits16, at::Tensor hdrop_all,
+                                         at::Tensor gates_all, at::Tensor c_all,
+                                         at::Tensor xh_all, at::Tensor seq, at::Tensor labels,
+                                         at::Tensor dg_sel, at::Tensor dg_xe, double drop_p,
+                                         int64_t seed);
+at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
+                       double log_ref_len, int64_t use_eos);
+at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
+                          at::Tensor partials, at::Tensor scal, at::Tensor skip, double lr,
+                          double b1, double b2, double eps, double clip, double bc1, double bc2);
+
+template <class T>
+static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
+  at::Tensor t = at::empty({(int64_t)v.size()}, at::TensorOptions().dtype(st));
+  if (!v.empty()) std::memcpy(t.data_ptr(), v.data(), v.size() * sizeof(T));
+  return t;
+}
+
+static std::map<std::string, at::Tensor> cider_build_tables(at::Tensor labels, at::Tensor start,
+                                                            at::Tensor end, at::Tensor df_keys,
+                                                            at::Tensor df_vals,
+                                                            double log_ref_len, int64_t use_eos) {
+  TORCH_CHECK(!labels.is_cuda(), "host builder takes CPU tensors");
+  labels = labels.contiguous().to(at::kLong);
+  start = start.contiguous().to(at::kLong);
+  end = end.contiguous().to(at::kLong);
+  df_keys = df_keys.contiguous().to(at::kLong);
+  df_vals = df_vals.contiguous().to(at::kFloat);
+  CiderTables t = build_cider_tables(labels.data_ptr<int64_t>(), (int)labels.size(0),
+                                     (int)labels.size(1), start.data_ptr<int64_t>(),
+                                     end.data_ptr<int64_t>(), (int)start.numel(),
+                                     df_keys.data_ptr<int64_t>(), df_vals.data_ptr<float>(),
+                                     (int)df_keys.numel(), log_ref_len, (int)use_eos);
+  return {{"ht_keys", to_tensor(t.ht_keys, at::kLong)},
+          {"ht_vals", to_tensor(t.ht_vals, at::kFloat)},
+          {"vid_ref_off", to_tensor(t.vid_ref_off, at::kInt)},
+          {"ref_ng_off", to_tensor(t.ref_ng_off, at::kInt)},
+          {"ref_norm", to_tensor(t.ref_norm, at::kFloat)},
+          {"ref_len", to_tensor(t.ref_len, at::kInt)},
+          {"ng_key", to_tensor(t.ng_key, at::kLong)},
+          {"ng_val", to_tensor(t.ng_val, at::kFloat)}};
+}
+
+static at::Tensor cider_score_cpu(at::Tensor hyps, at::Tensor hyp_video,
+                                  std::map<std::string, at::Tensor> t, double log_ref_len,
+                                  int64_t use_eos) {
+  hyps = hyps.contiguous().to(at::kLong);
+  hyp_video = hyp_video.contiguous().to(at::kLong);
+  CiderTablesView v{(uint32_t)t["ht_keys"].numel(), t["ht_keys"].data_ptr<int64_t>(),
+                    t["ht_vals"].data_ptr<float>(), t["vid_ref_off"].data_ptr<int32_t>(),
+                    t["ref_ng_off"].data_ptr<int32_t>(), t["ref_norm"].data_ptr<float>(),
+                    t["ref_len"].data_ptr<int32_t>(), t["ng_key"].data_ptr<int64_t>(),
+                    t["ng_val"].data_ptr<float>()};
+  at::Tensor out = at::empty({hyps.size(0)}, at::TensorOptions().dtype(at::kFloat));
+  cider_score_host(hyps.data_ptr<int64_t>(), (int)hyps.size(0), (int)hyps.size(1),
+                   hyp_video.data_ptr<int64_t>(), v, log_ref_len, (int)use_eos,
+                   out.data_ptr<float>());
+  return out;
+}
+}  // namespace cst
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "cst_captioning_amd native extension: gfx950 HIP kernels + C++ decoder executor";
+  m.def("decoder_forward", &cst::decoder_forward);
+  m.def("decoder_backward", &cst::decoder_backward);
+  m.def("cider_build_tables", &cst::cider_build_tables);
+  m.def("cider_score", &cst::cider_score);
+  m.def("cider_score_cpu", &cst::cider_score_cpu);
+  m.def("flat_adam_step", &cst::flat_adam_step);
+}

@@ -1,0 +1,101 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * wavefront = 64 lanes; block sizes are multiples of 64;
+//   * bf16 values travel as raw 16-bit patterns (uint16_t / short vectors) and
+//     are bit-cast to __bf16 vectors only at the MFMA call;
+//   * all launchers take an explicit hipStream_t (the caller passes PyTorch's
+//     current HIP stream) and never synchronise or allocate, so the whole
+//     decoder step can be captured in a HIP graph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cst {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float bf2f(uint16_t b) {
+  return __uint_as_float(((uint32_t)b) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (NaN stays NaN)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float h2f(uint16_t h) {
+  return (float)__builtin_bit_cast(_Float16, h);
+}
+__device__ __forceinline__ uint16_t f2h(float f) {
+  return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// ---- wave64 reductions --------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- Philox4x32-10 counter-based RNG ------------------------------------------
+// Deterministic per (seed, counter): the same draw is regenerated in backward
+// (dropout masks) and is independent of launch geometry.
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32(u32x4 ctr, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    u32x4 n;
+    n.x = hi1 ^ ctr.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ ctr.w ^ k1;
+    n.w = lo0;
+    ctr = n;
+    k0 += W0;
+    k1 += W1;
+  }
+  return ctr;
+}
+
+// uniform in (0, 1]: never 0, so log() is finite
+__device__ __forceinline__ float u01(uint32_t r) {
+  return ((float)(r >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// RNG streams (the `z` word of the counter)
+enum RngStream : uint32_t {
+  RNG_GUMBEL = 1,     // multinomial rollout sampling (Gumbel-max)
+  RNG_DROPOUT_H = 2,  // dropout on h before the vocab projection
+  RNG_SS = 3,         // scheduled-sampling coin per row
+};
+
+// Keep-mask of dropout on element (row, col) of step t: 4 columns per draw.
+__device__ __forceinline__ bool dropout_keep(uint32_t seed, int step, int row, int col,
+                                             float p) {
+  u32x4 c = {(uint32_t)(col >> 2), (uint32_t)row, RNG_DROPOUT_H, (uint32_t)step};
+  u32x4 r = philox4x32(c, seed, 0x5bd1e995u);
+  uint32_t w = (col & 3) == 0 ? r.x : (col & 3) == 1 ? r.y : (col & 3) == 2 ? r.z : r.w;
+  return u01(w) > p;
+}
+
+}  // namespace cst

@@ -1,0 +1,121 @@
+#include "hip/hip_runtime.h"
+// K12: fused global-norm gradient clipping + Adam over ONE flat fp32 buffer.
+//
+// Reference: clip_grad_norm_(params, 0.25) + optim.Adam(lr) (default betas
+// 0.9/0.999, eps 1e-8) at /root/reference/train.py:217-218,492 -- per-tensor
+// kernels plus a host-side norm.  Here the whole model (~20 M fp32 params) is
+// one contiguous buffer (the same buffer the DP all-reduce moves), so:
+//   pass 1  adam_sumsq_kernel: grid-stride float4 sum of squares ->
+//           one partial per block (deterministic tree, no atomics);
+//   pass 2  adam_update_kernel: every block re-reduces the <=1024 partials
+//           (4 KB, L2-resident) to the global norm, computes
+//           coef = min(1, clip / (norm + 1e-6)) on device and applies
+//           PyTorch's Adam update with the clipped gradient; an optional
+//           device-side skip flag (non-finite loss) turns the step into a
+//           no-op without a host round trip.
+// Memory-bound: 5 x 4 B read + 3 x 4 B write per parameter.
+#include "../common.h"
+
+namespace cst {
+
+constexpr int ADAM_THREADS = 256;
+constexpr int ADAM_MAX_PARTIALS = 1024;
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x < ADAM_THREADS / 64) r = sh[threadIdx.x];
+  if (w == 0) r = wave_sum(r);
+  return r;  // valid in wave 0
+}
+
+__global__ __launch_bounds__(ADAM_THREADS) void adam_sumsq_kernel(const float* __restrict__ g,
+                                                                   int64_t n,
+                                                                   float* __restrict__ partials) {
+  __shared__ float sh[ADAM_THREADS / 64];
+  float acc = 0.f;
+  const int64_t n4 = n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = blockIdx.x * (int64_t)ADAM_THREADS + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * ADAM_THREADS) {
+    const float4 x = g4[i];
+    acc += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += ADAM_THREADS) acc += g[i] * g[i];
+  }
+  const float s = block_sum(acc, sh);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, float coef,
+                                         float lr_bc1, float b1, float b2, float eps,
+                                         float inv_sqrt_bc2) {
+  g *= coef;
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) * inv_sqrt_bc2 + eps;
+  p -= lr_bc1 * m / denom;
+}
+
+__global__ __launch_bounds__(ADAM_THREADS) void adam_update_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ v, int64_t n, const float* __restrict__ partials, int nparts,
+    const bool* __restrict__ skip, float* __restrict__ scal, float lr_bc1, float b1, float b2,
+    float eps, float inv_sqrt_bc2, float clip) {
+  __shared__ float sh[ADAM_THREADS / 64];
+  __shared__ float s_coef;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += ADAM_THREADS) acc += partials[i];
+  const float tot = block_sum(acc, sh);
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(tot);
+    s_coef = fminf(1.f, clip / (norm + 1e-6f));
+    if (blockIdx.x == 0) {
+      scal[0] = norm;
+      scal[1] = s_coef;
+    }
+  }
+  __syncthreads();
+  if (*skip) return;
+  const float coef = s_coef;
+  const int64_t n4 = n >> 2;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = blockIdx.x * (int64_t)ADAM_THREADS + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * ADAM_THREADS) {
+    float4 pp = p4[i], mm = m4[i], vv = v4[i];
+    const float4 gg = g4[i];
+    adam_one(pp.x, mm.x, vv.x, gg.x, coef, lr_bc1, b1, b2, eps, inv_sqrt_bc2);
+    adam_one(pp.y, mm.y, vv.y, gg.y, coef, lr_bc1, b1, b2, eps, inv_sqrt_bc2);
+    adam_one(pp.z, mm.z, vv.z, gg.z, coef, lr_bc1, b1, b2, eps, inv_sqrt_bc2);
+    adam_one(pp.w, mm.w, vv.w, gg.w, coef, lr_bc1, b1, b2, eps, inv_sqrt_bc2);
+    p4[i] = pp;
+    m4[i] = mm;
+    v4[i] = vv;
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += ADAM_THREADS)
+      adam_one(p[i], m[i], v[i], g[i], coef, lr_bc1, b1, b2, eps, inv_sqrt_bc2);
+  }
+}
+
+void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float* partials,
+                      const bool* skip, float* scal, float lr, float b1, float b2, float eps,
+                      float clip, float bc1, float bc2, hipStream_t stream) {
+  int blocks = (int)std::min<int64_t>(ADAM_MAX_PARTIALS, std::max<int64_t>(1, (n / 4 + 255) / 256));
+  hipLaunchKernelGGL(adam_sumsq_kernel, dim3(blocks), dim3(ADAM_THREADS), 0, stream, g, n,
+                     partials);
+  int ublocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n / 4 + 255) / 256));
+  hipLaunchKernelGGL(adam_update_kernel, dim3(ublocks), dim3(ADAM_THREADS), 0, stream, p, g, m,
+                     v, n, partials, blocks, skip, scal, lr / bc1, b1, b2, eps,
+                     1.f / sqrtf(bc2), clip);
+}
+
+}  // namespace cst

@@ -1,0 +1,167 @@
+// K1/K9: fused LSTM decode step (embedding gather + gate GEMM + cell) and
+// the per-step cell backward.
+//
+// Reference per decode step (/root/reference/model.py:271-278, 93-116):
+// embed(it) -> cat([x, fc_feats]) -> cuDNN LSTM (bias=False, gate order
+// i,f,g,o) with input size E + F*H = 2560.
+//
+// MI355X design:
+//   * the video part W_ih[:, E:] . v is constant over time and identical for
+//     the seq_per_img rows of a video, so it is computed ONCE per video by the
+//     caller (vgate, B x 4H) and added in the epilogue: the per-step GEMM is
+//     K = E + H = 1024 instead of 2560, and the 20x row duplication of
+//     FeatExpander (model.py:84-86) disappears;
+//   * gate rows are packed so that one 64-column tile holds 16 hidden units x
+//     4 gates (packed row 4u+g <- original row g*H+u): the whole cell update
+//     happens in the GEMM epilogue, nothing but h/c leaves the kernel;
+//   * the A operand is gathered on the fly: K-tiles < E come from embedding
+//     rows picked by token id, the rest from h_{t-1};
+//   * training mode also emits, for the backward: the [x_t ; h_{t-1}] rows
+//     (the A operand itself, written by the tile-column-0 blocks while
+//     staging), post-activation gates, c_t, and h after dropout (the input of
+//     the vocabulary projection; mask from Philox, regenerated in backward).
+#include "gemm_tile.h"
+
+namespace cst {
+
+constexpr int LB_M = 128, LB_N = 64;
+using LTile = Tile<LB_M, LB_N>;
+
+__device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
+    const int64_t* __restrict__ tok, int64_t tok_stride, const uint16_t* __restrict__ emb, int E,
+    const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
+    const float* __restrict__ vgate, int vgate_div, int R, int H,
+    const uint16_t* __restrict__ wx, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
+    uint16_t* __restrict__ hdrop_out, float drop_p, uint32_t seed, int step,
+    float* __restrict__ gates_out, uint16_t* __restrict__ xh_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
+  const int b = xcd_remap_l(blockIdx.x, n_nt * n_rt);
+  const int nt = b / n_rt, rt = b % n_rt;
+  const int r0 = rt * LB_M, n0 = nt * LB_N;
+  const int K = E + H, nk = K / 64, nke = E / 64;
+
+  f32x16 acc[LTile::TM][LTile::TN];
+  auto arow = [&](int row, int kt) -> const uint16_t* {
+    const int r = min(r0 + row, R - 1);
+    if (kt < nke) return emb + tok[(int64_t)r * tok_stride] * E + kt * 64;
+    return h_prev + (int64_t)r * H + (kt - nke) * 64;
+  };
+  auto brow = [&](int row, int kt) { return wx + (int64_t)(n0 + row) * K + kt * 64; };
+  const bool write_xh = xh_out != nullptr && nt == 0;
+  auto hook = [&](int row, int kt, int c, const uint4& v) {
+    const int r = r0 + row;
+    if (write_xh && r < R)
+      *reinterpret_cast<uint4*>(xh_out + (int64_t)r * K + kt * 64 + c * 8) = v;
+  };
+  gemm_nt_mainloop<LTile>(nk, arow, brow, hook, lds, acc);
+
+  float* C = reinterpret_cast<float*>(lds);
+  store_acc_to_lds<LTile>(acc, C, [](int) { return 0.f; });
+  __syncthreads();
+
+  const int tid = threadIdx.x, u = tid & 15, rg = tid >> 4;
+  const int hu = nt * 16 + u;  // global hidden unit
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+#pragma unroll 2
+  for (int i = 0; i < LB_M / 16; ++i) {
+    const int row = rg + 16 * i, r = r0 + row;
+    if (r >= R) break;
+    const float4 pre = *reinterpret_cast<const float4*>(C + row * LTile::CSTRIDE + 4 * u);
+    const float4 vg = *reinterpret_cast<const float4*>(
+        vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
+    const float gi = sigmoidf_(pre.x + vg.x);
+    const float gf = sigmoidf_(pre.y + vg.y);
+    const float gg = tanhf(pre.z + vg.z);
+    const float go = sigmoidf_(pre.w + vg.w);
+    const int64_t o = (int64_t)r * H + hu;
+    const float c = gf * c_prev[o] + gi * gg;
+    const float hv = go * tanhf(c);
+    c_out[o] = c;
+    h_out[o] = f2bf(hv);
+    if (hdrop_out) {
+      const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
+      hdrop_out[o] = f2bf(keep ? hv * inv_keep : 0.f);
+    }
+    if (gates_out)
+      *reinterpret_cast<float4*>(gates_out + (int64_t)r * 4 * H + n0 + 4 * u) =
+          make_float4(gi, gf, gg, go);
+  }
+}
+
+// Cell backward of one step; one thread per (row, hidden unit).
+//   dh = dh_rec + mask * dh_logit / (1 - p)
+//   dc = dc_carry + dh * o * (1 - tanh(c)^2);  dc_carry <- dc * f
+//   dpre = [dc*g*i(1-i), dc*c_prev*f(1-f), dc*i*(1-g^2), dh*tanh(c)*o(1-o)]
+__global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
+    const float* __restrict__ dh_logit, const float* __restrict__ dh_rec,
+    float* __restrict__ dc_carry, const float* __restrict__ gates, const float* __restrict__ c_t,
+    const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
+    uint16_t* __restrict__ dG, float* __restrict__ dvg_acc) {
+  const int64_t idx = blockIdx.x * 256ll + threadIdx.x;
+  if (idx >= (int64_t)R * H) return;
+  const int r = (int)(idx / H), u = (int)(idx % H);
+  float dh = dh_rec ? dh_rec[idx] : 0.f;
+  if (dh_logit) {
+    const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, u, drop_p);
+    if (keep) dh += dh_logit[idx] * (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
+  }
+  const int64_t go_ = (int64_t)r * 4 * H + 4 * u;
+  const float4 g4 = *reinterpret_cast<const float4*>(gates + go_);
+  const float c = c_t[idx];
+  const float tc = tanhf(c);
+  const float dc = dc_carry[idx] + dh * g4.w * (1.f - tc * tc);
+  const float cp = c_prev ? c_prev[idx] : 0.f;
+  const float dpi = dc * g4.z * g4.x * (1.f - g4.x);
+  const float dpf = dc * cp * g4.y * (1.f - g4.y);
+  const float dpg = dc * g4.x * (1.f - g4.z * g4.z);
+  const float dpo = dh * tc * g4.w * (1.f - g4.w);
+  dc_carry[idx] = dc * g4.y;
+  uint2 pk;
+  pk.x = (uint32_t)f2bf(dpi) | ((uint32_t)f2bf(dpf) << 16);
+  pk.y = (uint32_t)f2bf(dpg) | ((uint32_t)f2bf(dpo) << 16);
+  *reinterpret_cast<uint2*>(dG + go_) = pk;
+  if (dvg_acc) {
+    float4 a = *reinterpret_cast<float4*>(dvg_acc + go_);
+    a.x += dpi;
+    a.y += dpf;
+    a.z += dpg;
+    a.w += dpo;
+    *reinterpret_cast<float4*>(dvg_acc + go_) = a;
+  }
+}
+
+void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
+                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
+                          int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
+                          float* c_out, uint16_t* hdrop_out, float drop_p, uint32_t seed,
+                          int step, float* gates_out, uint16_t* xh_out, hipStream_t stream) {
+  const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)lstm_step_fwd_kernel,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, LTile::LDS_BYTES);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(lstm_step_fwd_kernel, dim3(n_nt * n_rt), dim3(256), LTile::LDS_BYTES, stream,
+                     tok, tok_stride, emb, E, h_prev, c_prev, vgate, vgate_div, R, H, wx, h_out,
+                     c_out, hdrop_out, drop_p, seed, step, gates_out, xh_out);
+}
+
+void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
+                          const float* gates, const float* c_t, const float* c_prev, int R, int H,
+                          float drop_p, uint32_t seed, int step, uint16_t* dG, float* dvg_acc,
+                          hipStream_t stream) {
+  const int64_t n = (int64_t)R * H;
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     stream, dh_logit, dh_rec, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
+                     step, dG, dvg_acc);
+}
+
+}  // namespace cst

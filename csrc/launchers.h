@@ -1,0 +1,51 @@
+// Host-callable launchers of the gfx950 kernels (defined in csrc/kernels/*.hip).
+// None of them allocates or synchronises: they only enqueue on `stream`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cst {
+
+// cider_d.hip
+void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
+                    const int64_t* ht_keys, const float* ht_vals, uint32_t ht_cap,
+                    const int32_t* vid_ref_off, const int32_t* ref_ng_off,
+                    const float* ref_norm, const int32_t* ref_len, const int64_t* ng_key,
+                    const float* ng_val, float log_ref_len, int use_eos, float* out,
+                    hipStream_t stream);
+
+// adam.hip
+void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float* partials,
+                      const bool* skip, float* scal, float lr, float b1, float b2, float eps,
+                      float clip, float bc1, float bc2, hipStream_t stream);
+
+// vocab.hip
+enum SelModeHost : int { SEL_GT_H = 0, SEL_SAMPLE_H = 1, SEL_GREEDY_H = 2, SEL_SS_H = 3 };
+int vocab_num_tiles(int V);
+int vocab_partial_bytes();
+void launch_vocab_fwd(const uint16_t* hd, int R, int H, const uint16_t* W, const float* bias,
+                      int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
+                      int64_t tgt_stride, int do_sample, float inv_temp, uint32_t seed, int step,
+                      hipStream_t stream);
+void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
+                          int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
+                          int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
+                          float ss_prob, uint32_t seed, int step, int* counts, int count_step,
+                          uint8_t* unfinished, hipStream_t stream);
+void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
+                         const float* lse, const int64_t* y_sel, int64_t ysel_rs,
+                         const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
+                         int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, hipStream_t stream);
+
+// lstm.hip
+void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
+                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
+                          int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
+                          float* c_out, uint16_t* hdrop_out, float drop_p, uint32_t seed,
+                          int step, float* gates_out, uint16_t* xh_out, hipStream_t stream);
+void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
+                          const float* gates, const float* c_t, const float* c_prev, int R, int H,
+                          float drop_p, uint32_t seed, int step, uint16_t* dG, float* dvg_acc,
+                          hipStream_t stream);
+
+}  // namespace cst

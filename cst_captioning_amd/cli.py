@@ -62,7 +62,11 @@ def build_model(opt, device, impl=None):
     if impl == 'auto':
         impl = 'hip' if device.type == 'cuda' else 'torch'
     if impl == 'hip':
-        from .models.decoder_engine import DecoderEngine
+        from .models.decoder_engine import DecoderEngine, engine_supports
+        if not engine_supports(opt):
+            logger.warning('fused HIP decoder supports lstm/1-layer/concat/num_chunks=1; '
+                           'using the PyTorch decoder path for this configuration')
+            return model, None
         engine = DecoderEngine(model, opt)
         model.impl = 'hip'
         model._engine = engine

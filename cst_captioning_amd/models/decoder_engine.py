@@ -1,0 +1,232 @@
+"""Fused HIP decoder engine (MI355X path of :class:`CaptionModel`).
+
+Wraps the C++ executor of ``csrc/engine.cpp`` (time loops) and the gfx950
+kernels of ``csrc/kernels`` in one autograd Function, so a whole
+rollout / teacher-forced pass is ONE node of the autograd graph:
+
+  * forward : ``decoder_forward`` runs T decode steps, each = fused LSTM step
+    (embedding gather + gate MFMA GEMM + cell) -> fused vocab projection
+    (MFMA + LSE / Gumbel-max / argmax epilogue) -> row combine, and returns
+    the chosen tokens plus the *gathered* log-probs ``G[r, t]`` of the tokens
+    that the losses need (sampled tokens for REINFORCE, targets for XE).
+    No ``R x T x V`` log-prob tensor exists.
+  * backward: ``decoder_backward`` takes ``dL/dG`` and returns the weight
+    gradients (vocab head batched over all T*R rows; LSTM recurrence in
+    reverse).
+
+What stays in PyTorch autograd: FeatPool (video encoder, 64 rows) and the
+video gate term ``vgate = W_ih[:, E:] . v`` computed once per *video* (the
+reference feeds the same video vector at every step to 20 identical rows,
+``model.py:84-86,278``), whose gradient the engine returns summed over time
+and rows.
+
+Semantics match :class:`CaptionModel`'s PyTorch path (reference
+``model.py:218-367``) with two documented differences that are
+distribution-identical, not value-identical:
+  * RNG: multinomial sampling is Gumbel-max with Philox counters (exact
+    samples from the same softmax), dropout masks come from Philox;
+  * precision: bf16 MFMA operands, fp32 accumulation, cell state and
+    softmax statistics in fp32.
+Supported configuration: ``rnn_type lstm``, ``num_layers 1``, ``model_type
+concat``, ``num_chunks 1`` (the reference default); other configurations use
+the PyTorch path (``build_model`` decides).
+"""
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+from ..utils.text import BOS
+
+SEL_GT, SEL_SAMPLE, SEL_GREEDY, SEL_SS = 0, 1, 2, 3
+
+
+def engine_supports(opt):
+    return (getattr(opt, 'rnn_type', 'lstm') == 'lstm' and getattr(opt, 'num_layers', 1) == 1
+            and getattr(opt, 'model_type', 'concat') == 'concat'
+            and getattr(opt, 'num_chunks', 1) == 1
+            and opt.input_encoding_size % 64 == 0 and opt.rnn_size % 64 == 0)
+
+
+class _DecoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, vgate, w_ih, w_hh, emb_w, logit_w, logit_b, eng, labels, bos, R, T, modes,
+                ss_prob, drop_p, temperature, seed, vdiv, want_xe, use_counts, use_unfinished,
+                save):
+        outs = _ext.ops().decoder_forward(
+            eng.wx, eng.emb, eng.wlog, logit_b.detach().float().contiguous(),
+            vgate.detach().float().contiguous(), vdiv,
+            labels if labels is not None else torch.empty(0, dtype=torch.long),
+            bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
+            drop_p, temperature, seed, save, want_xe, use_counts, use_unfinished)
+        seq, g_sel, g_xe, lse = outs[:4]
+        ctx.save_dims = (R, T, vdiv, want_xe)
+        ctx.eng = eng
+        ctx.drop_p, ctx.seed = drop_p, seed
+        ctx.shapes = (w_ih.shape, emb_w.shape)
+        if save:
+            ctx.saved = (lse, *outs[4:], seq, labels, bos)
+        else:
+            ctx.saved = None
+        ctx.mark_non_differentiable(seq)
+        if g_xe is None:
+            g_xe = torch.zeros(0, device=g_sel.device)
+        return seq, g_sel, g_xe
+
+    @staticmethod
+    def backward(ctx, dseq, dg_sel, dg_xe):
+        if ctx.saved is None:
+            raise RuntimeError('decoder forward ran without saving activations')
+        R, T, vdiv, want_xe = ctx.save_dims
+        eng = ctx.eng
+        lse, logits16, hdrop, gates, c_all, xh, seq, labels, bos = ctx.saved
+        ctx.saved = None  # logits buffer is overwritten in place by dS
+        g_sel = dg_sel.contiguous() if dg_sel is not None else None
+        g_xe = dg_xe.contiguous() if (want_xe and dg_xe is not None and dg_xe.numel()) else None
+        empty = torch.empty(0, device=lse.device)
+        dWx, dWlog, dblog, dX, dvg = _ext.ops().decoder_backward(
+            eng.wx, eng.wlog, lse, logits16, hdrop, gates, c_all, xh, seq,
+            labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
+            g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
+            ctx.drop_p, ctx.seed)
+        E = eng.E
+        n_steps = logits16.shape[0]
+        d_orig = dWx.index_select(0, eng.inv_perm)
+        w_ih_shape, emb_shape = ctx.shapes
+        d_wih = torch.zeros(w_ih_shape, dtype=torch.float32, device=dWx.device)
+        d_wih[:, :E] = d_orig[:, :E]
+        d_whh = d_orig[:, E:].contiguous()
+        # input token of every step: it_0 = BOS / labels[:, 0], it_t = seq[:, t-1]
+        first = labels[:, :1] if labels is not None else bos.view(-1, 1)
+        toks = torch.cat([first, seq[:, :n_steps - 1]], 1).t().reshape(-1)
+        d_emb = torch.zeros(emb_shape, dtype=torch.float32, device=dWx.device)
+        d_emb.index_add_(0, toks, dX)
+        nv = R // vdiv
+        d_vgate = dvg.view(nv, vdiv, -1).sum(1)
+        return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 15
+
+
+class DecoderEngine:
+    def __init__(self, model, opt):
+        if not engine_supports(opt):
+            raise ValueError('fused engine supports lstm/1 layer/concat/num_chunks=1')
+        if not _ext.available():
+            raise RuntimeError('HIP extension not available')
+        self.H = model.rnn_size
+        self.E = model.input_encoding_size
+        self.V = model.vocab_size
+        dev = model.embed.weight.device
+        H = self.H
+        # packed gate row 4u+g  <-  original row g*H+u
+        self.perm = torch.arange(4 * H, device=dev).view(4, H).t().reshape(-1).contiguous()
+        self.inv_perm = torch.argsort(self.perm)
+        self.model = model
+        self.refresh_weights()
+
+    # -- bf16 shadow weights (refreshed after every optimizer step) -----------
+    @torch.no_grad()
+    def refresh_weights(self):
+        m = self.model
+        E = self.E
+        w_ih = m.core.rnn.weight_ih_l0
+        w_hh = m.core.rnn.weight_hh_l0
+        self.wx = torch.cat([w_ih[:, :E], w_hh], 1).index_select(0, self.perm) \
+            .to(torch.bfloat16).contiguous()
+        self.emb = m.embed.weight.detach().to(torch.bfloat16).contiguous()
+        self.wlog = m.logit.weight.detach().to(torch.bfloat16).contiguous()
+
+    def attach_optimizer(self, trainer):
+        self.refresh_weights()  # params were re-homed into the flat buffer
+
+    def after_step(self):
+        self.refresh_weights()
+
+    def _seed(self):
+        return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+    def _vgate(self, model, feats, expand):
+        fc = model.encode(feats)  # (B, F*H), FeatPool dropout in train mode
+        w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
+        vg = F.linear(fc, w_iv)
+        return vg.index_select(1, self.perm), fc.size(0)
+
+    def _run(self, model, feats, labels, modes, want_xe, use_counts, use_unfinished,
+             expand=True, ss_prob=0.0, drop=True, temperature=1.0, bos_rows=None):
+        vg, B = self._vgate(model, feats, expand)
+        S = model.feat_expander.n if expand else 1
+        R = labels.size(0) if labels is not None else B * S
+        if labels is not None:
+            T = labels.size(1) - 1
+            bos = None
+        else:
+            T = model.seq_length - 1
+            bos = torch.full((R,), BOS, dtype=torch.long, device=vg.device)
+        drop_p = model.drop_prob_lm if (model.training and drop) else 0.0
+        m = model
+        ws = (m.core.rnn.weight_ih_l0, m.core.rnn.weight_hh_l0, m.embed.weight, m.logit.weight,
+              m.logit.bias)
+        # (inside Function.forward grad mode is off, so decide here)
+        save = torch.is_grad_enabled() and (vg.requires_grad or any(w.requires_grad for w in ws))
+        return _DecoderFn.apply(vg, *ws, self,
+                                labels.contiguous() if labels is not None else None, bos, R, T,
+                                modes, float(ss_prob), float(drop_p), float(temperature),
+                                self._seed(), S, want_xe, use_counts, use_unfinished, save)
+
+    # -- public entry points ------------------------------------------------------
+    def rollout(self, model, feats, labels):
+        """Reference ``forward(feats, seq)`` for RL: returns
+        (sample_seq (R, T-1), sample_logprobs (R, T-1), None)."""
+        T = labels.size(1) - 1
+        modes = self._modes(model, T)
+        mask_eos = getattr(model, 'mask_after_eos', False)
+        seq, g_sel, _ = self._run(model, feats, labels, modes, want_xe=False, use_counts=True,
+                                  use_unfinished=mask_eos, ss_prob=model.ss_prob)
+        return seq, g_sel, None
+
+    def teacher_forced(self, model, feats, labels):
+        """Gathered log-probs of the GT targets ``labels[:, 1:]`` (R, T) --
+        what CrossEntropyCriterion needs.  Honours scheduled sampling."""
+        T = labels.size(1) - 1
+        modes = self._modes(model, T, rl=False)
+        _, _, g_xe = self._run(model, feats, labels, modes, want_xe=True, use_counts=True,
+                               use_unfinished=False, ss_prob=model.ss_prob)
+        return g_xe
+
+    def _modes(self, model, T, rl=True):
+        modes = []
+        for t in range(T - 1):
+            tok_idx = t + 1
+            if model.training and model.ss_prob > 0.0:
+                modes.append(SEL_SS)
+            elif rl and model.training and model.mixer_from > 0 and tok_idx >= model.mixer_from:
+                modes.append(SEL_SAMPLE)
+            else:
+                modes.append(SEL_GT)
+        return modes
+
+    def forward_full(self, model, feats, seq):
+        """``model(feats, seq)`` API: full (R, T, V) log-probs need the plain
+        path; delegate to it."""
+        model.impl = 'torch'
+        try:
+            return model(feats, seq)
+        finally:
+            model.impl = 'hip'
+
+    @torch.no_grad()
+    def sample(self, model, feats, opt):
+        sample_max = opt.get('sample_max', 1)
+        temperature = opt.get('temperature', 1.0)
+        expand = opt.get('expand_feat', 0) == 1
+        T = model.seq_length - 1
+        modes = [SEL_GREEDY if sample_max == 1 else SEL_SAMPLE] * (T - 1)
+        seq, lp, _ = self._run(model, feats, None, modes, want_xe=False, use_counts=False,
+                               use_unfinished=True, expand=expand, drop=False,
+                               temperature=temperature)
+        return seq, lp
+
+    def sample_beam(self, model, feats, opt):
+        model.impl = 'torch'
+        try:
+            return model.sample_beam(feats, opt)
+        finally:
+            model.impl = 'hip'

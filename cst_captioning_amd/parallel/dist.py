@@ -29,7 +29,10 @@ class DistContext:
         self.rank = rank
         self.world_size = world_size
         self.local_rank = local_rank
-        self.device = device if device is not None else torch.device('cpu')
+        if device is None:
+            device = (torch.device('cuda', torch.cuda.current_device())
+                      if torch.cuda.is_available() else torch.device('cpu'))
+        self.device = device
         self.backend = backend
 
     @property
