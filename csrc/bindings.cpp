@@ -11,12 +11,12 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         double drop_p, double temperature, int64_t seed,
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished);
-std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor lse,
-                                         at::Tensor logits16, at::Tensor hdrop_all,
-                                         at::Tensor gates_all, at::Tensor c_all,
-                                         at::Tensor xh_all, at::Tensor seq, at::Tensor labels,
-                                         at::Tensor dg_sel, at::Tensor dg_xe, double drop_p,
-                                         int64_t seed);
+std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
+                                         at::Tensor lse, at::Tensor logits16,
+                                         at::Tensor hdrop_all, at::Tensor gates_all,
+                                         at::Tensor c_all, at::Tensor h_all, at::Tensor seq,
+                                         at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
+                                         at::Tensor dg_xe, double drop_p, int64_t seed);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
                        double log_ref_len, int64_t use_eos);
 at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,

@@ -25,6 +25,10 @@ namespace cst {
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// h_drop rows carry HAUG extra columns [1, 0, ...] (written by the LSTM kernel)
+// so that one GEMM dS^T [h | 1] gives the logit weight AND bias gradients.
+constexpr int64_t HAUG = 16;
+
 template <class T>
 static T* ptr_or_null(const at::Tensor& t) {
   return t.defined() && t.numel() > 0 ? reinterpret_cast<T*>(t.data_ptr()) : nullptr;
@@ -87,17 +91,17 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       use_unfinished ? at::ones({R}, at::TensorOptions().dtype(at::kByte).device(dev))
                      : at::Tensor();
   const int64_t ldl = (V + 7) / 8 * 8;
-  at::Tensor logits16, hdrop_all, gates_all, c_all, xh_all;
+  at::Tensor logits16, hdrop_all, gates_all, c_all, h_all;
   if (save) {
     logits16 = at::empty({n_steps, R, ldl}, at::TensorOptions().dtype(at::kHalf).device(dev));
-    hdrop_all = at::empty({n_steps, R, H}, bf);
+    hdrop_all = at::empty({n_steps, R, H + HAUG}, bf);  // [h_drop | 1 | 0...]
     gates_all = at::empty({n_steps, R, H4}, f32);
     c_all = at::empty({n_steps, R, H}, f32);
-    xh_all = at::empty({n_steps, R, E + H}, bf);
+    h_all = at::empty({n_steps, R, H}, bf);
   }
   at::Tensor h_a = at::zeros({R, H}, bf), h_b = at::empty({R, H}, bf);
   at::Tensor c_a = at::zeros({R, H}, f32), c_b = at::empty({R, H}, f32);
-  at::Tensor hd_tmp = (!save && drop_p > 0) ? at::empty({R, H}, bf) : at::Tensor();
+  at::Tensor hd_tmp = (!save && drop_p > 0) ? at::empty({R, H + HAUG}, bf) : at::Tensor();
 
   const uint32_t seed_drop = (uint32_t)(seed * 2654435761u + 17u);
   const uint32_t seed_samp = (uint32_t)(seed * 40503u + 0x9E37u);
@@ -117,8 +121,15 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       tok = seq.data_ptr<int64_t>() + (t - 1);
       tok_stride = T - 1;
     }
-    uint16_t* h_prev = reinterpret_cast<uint16_t*>((t & 1 ? h_b : h_a).data_ptr());
-    uint16_t* h_out = reinterpret_cast<uint16_t*>((t & 1 ? h_a : h_b).data_ptr());
+    uint16_t* h_prev;
+    uint16_t* h_out;
+    if (save) {
+      h_prev = reinterpret_cast<uint16_t*>(t == 0 ? h_a.data_ptr() : h_all[t - 1].data_ptr());
+      h_out = reinterpret_cast<uint16_t*>(h_all[t].data_ptr());
+    } else {
+      h_prev = reinterpret_cast<uint16_t*>((t & 1 ? h_b : h_a).data_ptr());
+      h_out = reinterpret_cast<uint16_t*>((t & 1 ? h_a : h_b).data_ptr());
+    }
     const float* c_prev;
     float* c_out;
     if (save) {
@@ -132,15 +143,16 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     if (save) hd = reinterpret_cast<uint16_t*>(hdrop_all[t].data_ptr());
     else if (drop_p > 0) hd = reinterpret_cast<uint16_t*>(hd_tmp.data_ptr());
     launch_lstm_step_fwd(tok, tok_stride, EMB, (int)E, h_prev, c_prev, vgate.data_ptr<float>(),
-                         (int)vgate_div, (int)R, (int)H, WX, h_out, c_out, hd, (float)drop_p,
-                         seed_drop, (int)t, save ? gates_all[t].data_ptr<float>() : nullptr,
-                         save ? reinterpret_cast<uint16_t*>(xh_all[t].data_ptr()) : nullptr, st);
+                         (int)vgate_div, (int)R, (int)H, WX, h_out, c_out, hd, (int)(H + HAUG),
+                         (float)drop_p,
+                         seed_drop, (int)t, save ? gates_all[t].data_ptr<float>() : nullptr, st);
     const uint16_t* vin = hd ? hd : h_out;
+    const int ldh = hd ? (int)(H + HAUG) : (int)H;
     const bool choose = t < T - 1;
     const int mode = choose ? (int)modes[t] : SEL_GT_H;
     const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
     const int64_t* tgt = (have_labels && t + 1 < L) ? LAB + (t + 1) : nullptr;
-    launch_vocab_fwd(vin, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
+    launch_vocab_fwd(vin, ldh, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
                      save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
                      part.data_ptr(), tgt, L, do_sample, inv_temp, seed_samp, (int)t, st);
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
@@ -157,18 +169,19 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     out.push_back(hdrop_all);
     out.push_back(gates_all);
     out.push_back(c_all);
-    out.push_back(xh_all);
+    out.push_back(h_all);
   }
   return out;
 }
 
 // Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), dX (n_steps*R, E), dvg_rows (R, 4H)}.
-std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor lse,
-                                         at::Tensor logits16, at::Tensor hdrop_all,
-                                         at::Tensor gates_all, at::Tensor c_all,
-                                         at::Tensor xh_all, at::Tensor seq, at::Tensor labels,
-                                         at::Tensor dg_sel, at::Tensor dg_xe, double drop_p,
-                                         int64_t seed) {
+// toks: (n_steps*R) input token of every (step, row), step-major.
+std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
+                                         at::Tensor lse, at::Tensor logits16,
+                                         at::Tensor hdrop_all, at::Tensor gates_all,
+                                         at::Tensor c_all, at::Tensor h_all, at::Tensor seq,
+                                         at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
+                                         at::Tensor dg_xe, double drop_p, int64_t seed) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -179,6 +192,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const bool has_xe = dg_xe.defined() && dg_xe.numel() > 0;
   if (has_sel) TORCH_CHECK(dg_sel.is_contiguous() && dg_sel.size(1) == T_sel, "dg_sel shape");
   if (has_xe) TORCH_CHECK(dg_xe.is_contiguous() && labels.defined(), "dg_xe needs labels");
+  TORCH_CHECK(toks.numel() == n_steps * R, "toks must hold one token per (step, row)");
   const uint32_t seed_drop = (uint32_t)(seed * 2654435761u + 17u);
 
   // 1. dS = dG (onehot - softmax), in place (fp16 logits -> bf16 dS)
@@ -191,13 +205,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                       has_xe ? dg_xe.size(1) : 0, st);
   at::Tensor dS = logits16.view(at::kBFloat16).view({n_steps * R, ldl}).narrow(1, 0, V);
   // 2. batched vocab-head GEMMs over all n_steps*R rows (hipBLASLt)
-  at::Tensor dHd = at::mm(dS, wlog, at::kFloat);                       // (n*R, H)
-  at::Tensor hd2 = hdrop_all.view({n_steps * R, H});
-  at::Tensor dWlog = at::mm(dS.t(), hd2, at::kFloat);                  // (V, H)
-  at::Tensor dblog = dS.sum(0, false, at::kFloat);                     // (V)
+  at::Tensor dHd = at::mm(dS, wlog, at::kFloat);                        // (n*R, H)
+  at::Tensor hd2 = hdrop_all.view({n_steps * R, H + HAUG});
+  at::Tensor dW_aug = at::mm(dS.t(), hd2, at::kFloat);                  // (V, H+HAUG)
+  at::Tensor dWlog = dW_aug.narrow(1, 0, H).contiguous();
+  at::Tensor dblog = dW_aug.select(1, H).contiguous();                  // column sums of dS
   // 3. reverse recurrence
   at::Tensor dG_all = at::empty({n_steps, R, H4}, wx.options());
-  at::Tensor dvg = at::zeros({R, H4}, f32);
   at::Tensor dc = at::zeros({R, H}, f32);
   at::Tensor whh = wx.narrow(1, E, H);  // (4H, H) packed rows, strided view
   at::Tensor dh_rec;
@@ -208,14 +222,22 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          c_all[t].data_ptr<float>(),
                          t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R, (int)H,
                          (float)drop_p, seed_drop, (int)t,
-                         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()),
-                         dvg.data_ptr<float>(), st);
+                         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), st);
     if (t > 0) dh_rec = at::mm(dG_all[t], whh, at::kFloat);  // (R, H)
   }
-  // 4. batched weight gradients
+  // 4. batched weight gradients: dWx = dG^T [x ; h_prev] as two GEMMs
   at::Tensor dG2 = dG_all.view({n_steps * R, H4});
-  at::Tensor dWx = at::mm(dG2.t(), xh_all.view({n_steps * R, E + H}), at::kFloat);
-  at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);       // (n*R, E)
+  at::Tensor x_in = emb.index_select(0, toks);                            // (n*R, E) bf16
+  at::Tensor dWx = at::empty({H4, E + H}, f32);
+  dWx.narrow(1, 0, E).copy_(at::mm(dG2.t(), x_in, at::kFloat));
+  if (n_steps > 1) {
+    at::Tensor hprev = h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H});
+    dWx.narrow(1, E, H).copy_(at::mm(dG2.narrow(0, R, (n_steps - 1) * R).t(), hprev, at::kFloat));
+  } else {
+    dWx.narrow(1, E, H).zero_();
+  }
+  at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);        // (n*R, E)
+  at::Tensor dvg = dG_all.sum(0, false, at::kFloat);                   // (R, 4H), sum over time
   return {dWx, dWlog, dblog, dX, dvg};
 }
 

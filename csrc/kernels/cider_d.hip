@@ -6,7 +6,7 @@
 // (tf-idf values, per-order norms, bigram "lengths") are precomputed once per
 // dataset by csrc/host/cider_host.cpp; this kernel only processes hypotheses.
 //
-// One wavefront per hypothesis (4 per 256-thread block):
+// One 256-thread block per hypothesis:
 //   1. token compaction with ballots, reproducing array_to_str
 //      (utils.py:135-152): drop BOS (=1) anywhere, stop at the first EOS (=0)
 //      and keep that "0" when use_eos;
@@ -14,20 +14,21 @@
 //      O(W) scan, counted once at the first occurrence (later duplicates get
 //      value 0, which contributes exactly 0 to the clipped dot product);
 //   3. idf from the df hash table in HBM, per-order norms by wave reduction;
-//   4. for every reference of the video: lanes stride over the reference's
+//   4. the 4 waves split the video's references; for each one, lanes stride over its
 //      unique n-grams, look each up among the hypothesis n-grams in LDS
 //      (broadcast reads), accumulate min(vh, vr) * vr per order, normalise,
 //      apply exp(-(lh - lr)^2 / (2 * 6^2));
 //   5. score = 10 * sum_refs mean_n(val_n) / n_refs.
-// Deterministic: fixed-order wave reductions, no atomics.
+// Deterministic: fixed-order wave/block reductions, no atomics.
 #include "../common.h"
 #include "../cider_common.h"
 
 namespace cst {
 
-constexpr int CIDER_WAVES = 4;
 constexpr int CIDER_MAXT = 64;
 
+// One 256-thread block per hypothesis: wave 0 builds the hypothesis vector
+// (steps 1-3) in LDS, then the 4 waves split the video's references.
 __global__ __launch_bounds__(256) void cider_d_kernel(
     const int64_t* __restrict__ hyps, int T, const int64_t* __restrict__ hyp_video, int N,
     const int64_t* __restrict__ ht_keys, const float* __restrict__ ht_vals, uint32_t ht_cap,
@@ -35,54 +36,55 @@ __global__ __launch_bounds__(256) void cider_d_kernel(
     const float* __restrict__ ref_norm, const int32_t* __restrict__ ref_len,
     const int64_t* __restrict__ ng_key, const float* __restrict__ ng_val, float log_ref_len,
     int use_eos, float* __restrict__ out) {
-  __shared__ int s_tok[CIDER_WAVES][CIDER_MAXT];
-  __shared__ uint64_t s_key[CIDER_WAVES][4][CIDER_MAXT];
-  __shared__ float s_val[CIDER_WAVES][4][CIDER_MAXT];
+  __shared__ int s_tok[CIDER_MAXT];
+  __shared__ uint64_t s_key[4][CIDER_MAXT];
+  __shared__ float s_val[4][CIDER_MAXT];
+  __shared__ float s_norm[4];
+  __shared__ float s_part[4];
+  __shared__ int s_W;
 
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  const int hyp_raw = blockIdx.x * CIDER_WAVES + w;
-  const bool valid = hyp_raw < N;  // invalid waves still take part in the barriers
-  const int hyp = valid ? hyp_raw : N - 1;
+  const int hyp = blockIdx.x;
 
-  // -- 1. compaction ------------------------------------------------------------
-  int tok = lane < T ? (int)hyps[(int64_t)hyp * T + lane] : 0;
-  uint64_t zmask = __ballot(lane >= T || tok == 0);
-  int e = zmask ? __ffsll((long long)zmask) - 1 : 64;  // first EOS (or end)
-  bool keep = lane < e && tok != 1;
-  uint64_t kmask = __ballot(keep);
-  int pos = __popcll(kmask & ((1ull << lane) - 1ull));
-  int W = __popcll(kmask);
-  if (keep) s_tok[w][pos] = tok;
-  if (use_eos && e < T) {
-    if (lane == 0) s_tok[w][W] = 0;
-    W += 1;
+  // -- 1. compaction (wave 0) ----------------------------------------------------
+  if (w == 0) {
+    const int tok = lane < T ? (int)hyps[(int64_t)hyp * T + lane] : 0;
+    const uint64_t zmask = __ballot(lane >= T || tok == 0);
+    const int e = zmask ? __ffsll((long long)zmask) - 1 : 64;  // first EOS (or end)
+    const bool keep = lane < e && tok != 1;
+    const uint64_t kmask = __ballot(keep);
+    const int pos = __popcll(kmask & ((1ull << lane) - 1ull));
+    int W = __popcll(kmask);
+    if (keep) s_tok[pos] = tok;
+    if (use_eos && e < T) {
+      if (lane == 0) s_tok[W] = 0;
+      W += 1;
+    }
+    if (lane == 0) s_W = W;
   }
   __syncthreads();
-
-  // -- 2./3. hypothesis n-grams, tf, idf, norms ---------------------------------
-  float norm_h[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int cnt = W - n;  // number of n-grams of order n+1
+  const int W = s_W;
+  // -- 2. packed n-gram keys: wave n builds the order-(n+1) keys ------------------
+  {
+    const int n = w, cnt = W - n;
     uint64_t key = 0;
     if (lane < cnt) {
-#pragma unroll
-      for (int i = 0; i <= n; ++i) key |= (uint64_t)(s_tok[w][lane + i] + 1) << (16 * i);
+      for (int i = 0; i <= n; ++i) key |= (uint64_t)(s_tok[lane + i] + 1) << (16 * i);
     }
-    s_key[w][n][lane] = key;
+    s_key[n][lane] = key;
   }
   __syncthreads();
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int cnt = W - n;
+  // -- 3. tf (first occurrence), idf, per-order norm: wave n handles order n+1 ----
+  {
+    const int n = w, cnt = W - n;
     float v = 0.f;
     if (lane < cnt) {
-      const uint64_t key = s_key[w][n][lane];
+      const uint64_t key = s_key[n][lane];
       int tf = 0;
       bool first = true;
       for (int j = 0; j < cnt; ++j) {
-        const bool eq = s_key[w][n][j] == key;
+        const bool eq = s_key[n][j] == key;
         tf += eq;
         first = first && !(eq && j < lane);
       }
@@ -91,17 +93,19 @@ __global__ __launch_bounds__(256) void cider_d_kernel(
         v = (float)tf * (log_ref_len - __logf(fmaxf(1.f, df)));
       }
     }
-    s_val[w][n][lane] = v;
-    norm_h[n] = sqrtf(wave_sum(v * v));
+    s_val[n][lane] = v;
+    const float nrm = sqrtf(wave_sum(v * v));
+    if (lane == 0) s_norm[n] = nrm;
   }
   __syncthreads();
   const float len_h = (float)max(W - 1, 0);
+  float norm_h[4] = {s_norm[0], s_norm[1], s_norm[2], s_norm[3]};
 
-  // -- 4./5. references --------------------------------------------------------
+  // -- 4. references, split over the 4 waves --------------------------------------
   const int v = (int)hyp_video[hyp];
   const int r0 = vid_ref_off[v], r1 = vid_ref_off[v + 1];
   float total = 0.f;
-  for (int r = r0; r < r1; ++r) {
+  for (int r = r0 + w; r < r1; r += 4) {
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
     const int g0 = ref_ng_off[r], g1 = ref_ng_off[r + 1];
     for (int g = g0 + lane; g < g1; g += 64) {
@@ -111,14 +115,14 @@ __global__ __launch_bounds__(256) void cider_d_kernel(
       const int cnt = W - n;
       float c = 0.f;
       for (int j = 0; j < cnt; ++j) {
-        if (s_key[w][n][j] == key) c += fminf(s_val[w][n][j], vr) * vr;
+        if (s_key[n][j] == key) c += fminf(s_val[n][j], vr) * vr;
       }
       acc0 += n == 0 ? c : 0.f;
       acc1 += n == 1 ? c : 0.f;
       acc2 += n == 2 ? c : 0.f;
       acc3 += n == 3 ? c : 0.f;
     }
-    float acc[4] = {wave_sum(acc0), wave_sum(acc1), wave_sum(acc2), wave_sum(acc3)};
+    const float acc[4] = {wave_sum(acc0), wave_sum(acc1), wave_sum(acc2), wave_sum(acc3)};
     const float delta = len_h - (float)ref_len[r];
     const float pen = __expf(-(delta * delta) / 72.f);
     float s = 0.f;
@@ -131,9 +135,12 @@ __global__ __launch_bounds__(256) void cider_d_kernel(
     }
     total += s;
   }
-  if (lane == 0 && valid) {
+  if (lane == 0) s_part[w] = total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
     const int nref = r1 - r0;
-    out[hyp] = nref > 0 ? 10.f * total / (4.f * (float)nref) : 0.f;
+    const float t4 = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
+    out[hyp] = nref > 0 ? 10.f * t4 / (4.f * (float)nref) : 0.f;
   }
 }
 
@@ -144,7 +151,7 @@ void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
                     const float* ng_val, float log_ref_len, int use_eos, float* out,
                     hipStream_t stream) {
   if (N <= 0) return;
-  dim3 grid((N + CIDER_WAVES - 1) / CIDER_WAVES), block(64 * CIDER_WAVES);
+  dim3 grid(N), block(256);
   hipLaunchKernelGGL(cider_d_kernel, grid, block, 0, stream, hyps, T, hyp_video, N, ht_keys,
                      ht_vals, ht_cap, vid_ref_off, ref_ng_off, ref_norm, ref_len, ng_key,
                      ng_val, log_ref_len, use_eos, out);

@@ -9,9 +9,9 @@
 //
 // Geometry: 256 threads = 4 wavefronts in a 2x2 grid; block tile BM x BN,
 // K staged 64 at a time (one 128-byte row per tile row) through LDS, double
-// buffered: the next K-tile's global loads are issued before the current
-// tile's MFMAs and written to the other LDS buffer after them, so HBM/L2
-// latency hides under the matrix work and there is ONE barrier per K-tile.
+// buffered: the next K-tile's LDS-DMA loads are issued before the current
+// tile's MFMAs, so HBM/L2 latency hides under the matrix work, and there is
+// ONE barrier per K-tile.
 // LDS rows are 16-byte-chunk XOR-swizzled (chunk ^ ((row >> 1) & 7)) so the
 // 16-lane groups of ds_read_b128 hit 16 distinct bank slots.
 //
@@ -35,21 +35,36 @@ struct Tile {
   static constexpr int C_BYTES = BM * CSTRIDE * 4;
   static constexpr int LDS_BYTES = (2 * STAGE_BYTES > C_BYTES) ? 2 * STAGE_BYTES : C_BYTES;
   static_assert(TM >= 1 && TN >= 1, "tile too small");
-  static_assert(BM * 8 % THREADS == 0 && BN * 8 % THREADS == 0, "chunk split");
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "glds split: 8 rows per wave-instruction");
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) const void* gbl_ptr_t;
+
+// One wave-instruction of LDS-DMA: each lane moves 16 bytes from its own
+// global address to (wave-uniform base + 16 * lane).
+__device__ __forceinline__ void glds16(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_base, 16, 0, 0);
+}
+
 // ARow(row, kt) / BRow(row, kt): pointer to the 64 bf16 of K-tile kt of that
 // tile row (callers clamp out-of-range rows to a valid row).
-template <class TL, class ARow, class BRow, class AHook>
-__device__ __forceinline__ void gemm_nt_mainloop(int nk, ARow arow, BRow brow, AHook ahook,
-                                                 char* lds, f32x16 (&acc)[TL::TM][TL::TN]) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+//
+// Staging is global -> LDS direct (global_load_lds_dwordx4): no staging
+// registers at all.  One wave-instruction fills 1 KiB = 8 tile rows; lane l
+// writes LDS byte 16*l of it, i.e. row 8j + l/8 and *physical* chunk l%8, so
+// the XOR swizzle is applied to the SOURCE address (logical chunk =
+// physical ^ ((row >> 1) & 7)) and undone by the same XOR on the ds_read.
+template <class TL, class ARow, class BRow>
+__device__ __forceinline__ void gemm_nt_mainloop(int nk, ARow arow, BRow brow, char* lds,
+                                                 f32x16 (&acc)[TL::TM][TL::TN]) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
-  uint4 ra[TL::A_CHUNKS], rb[TL::B_CHUNKS];
 
 #pragma unroll
   for (int i = 0; i < TL::TM; ++i)
@@ -58,40 +73,28 @@ __device__ __forceinline__ void gemm_nt_mainloop(int nk, ARow arow, BRow brow, A
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  auto gload = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < TL::A_CHUNKS; ++i) {
-      const int idx = tid + i * TL::THREADS, row = idx >> 3, c = idx & 7;
-      ra[i] = *reinterpret_cast<const uint4*>(arow(row, kt) + c * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < TL::B_CHUNKS; ++i) {
-      const int idx = tid + i * TL::THREADS, row = idx >> 3, c = idx & 7;
-      rb[i] = *reinterpret_cast<const uint4*>(brow(row, kt) + c * 8);
-    }
-  };
-  auto lstore = [&](int buf, int kt) {
+  auto issue = [&](int buf, int kt) {
     char* A = lds + buf * TL::STAGE_BYTES;
     char* B = A + TL::A_BYTES;
 #pragma unroll
-    for (int i = 0; i < TL::A_CHUNKS; ++i) {
-      const int idx = tid + i * TL::THREADS, row = idx >> 3, c = idx & 7;
-      *reinterpret_cast<uint4*>(A + swz(row, c)) = ra[i];
-      ahook(row, kt, c, ra[i]);
+    for (int i = 0; i < TL::BM / 32; ++i) {
+      const int j = w + 4 * i, row = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      glds16(arow(row, kt) + c * 8, A + 1024 * j);
     }
 #pragma unroll
-    for (int i = 0; i < TL::B_CHUNKS; ++i) {
-      const int idx = tid + i * TL::THREADS, row = idx >> 3, c = idx & 7;
-      *reinterpret_cast<uint4*>(B + swz(row, c)) = rb[i];
+    for (int i = 0; i < TL::BN / 32; ++i) {
+      const int j = w + 4 * i, row = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      glds16(brow(row, kt) + c * 8, B + 1024 * j);
     }
   };
 
-  gload(0);
-  lstore(0, 0);
-  __syncthreads();
+  issue(0, 0);
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+    if (kt + 1 < nk) issue(cur ^ 1, kt + 1);  // in flight during this tile's MFMAs
     const char* A = lds + cur * TL::STAGE_BYTES;
     const char* B = A + TL::A_BYTES;
 #pragma unroll
@@ -110,8 +113,7 @@ __device__ __forceinline__ void gemm_nt_mainloop(int nk, ARow arow, BRow brow, A
         for (int j = 0; j < TL::TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1, kt + 1);
-    __syncthreads();
+    __syncthreads();  // vmcnt(0) + barrier: next tile landed, this one free
   }
 }
 

@@ -16,16 +16,16 @@
 //     happens in the GEMM epilogue, nothing but h/c leaves the kernel;
 //   * the A operand is gathered on the fly: K-tiles < E come from embedding
 //     rows picked by token id, the rest from h_{t-1};
-//   * training mode also emits, for the backward: the [x_t ; h_{t-1}] rows
-//     (the A operand itself, written by the tile-column-0 blocks while
-//     staging), post-activation gates, c_t, and h after dropout (the input of
-//     the vocabulary projection; mask from Philox, regenerated in backward).
+//   * training mode also emits, for the backward: post-activation gates, c_t,
+//     h_t, and h after dropout (the input of the vocabulary projection; mask
+//     from Philox, regenerated in backward).
 #include "gemm_tile.h"
 
 namespace cst {
 
 constexpr int LB_M = 128, LB_N = 64;
 using LTile = Tile<LB_M, LB_N>;
+constexpr int LSTM_LDS_BYTES = LTile::LDS_BYTES + LB_M * 4;  // + staged token ids
 
 __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -38,8 +38,8 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
     const float* __restrict__ vgate, int vgate_div, int R, int H,
     const uint16_t* __restrict__ wx, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
-    uint16_t* __restrict__ hdrop_out, float drop_p, uint32_t seed, int step,
-    float* __restrict__ gates_out, uint16_t* __restrict__ xh_out) {
+    uint16_t* __restrict__ hdrop_out, int ldh, float drop_p, uint32_t seed, int step,
+    float* __restrict__ gates_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
   const int b = xcd_remap_l(blockIdx.x, n_nt * n_rt);
@@ -47,20 +47,20 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
   const int r0 = rt * LB_M, n0 = nt * LB_N;
   const int K = E + H, nk = K / 64, nke = E / 64;
 
+  // token ids of this row tile, staged once (keeps the id -> row lookup off
+  // the critical path of every K-tile)
+  int* s_tok = reinterpret_cast<int*>(lds + LTile::LDS_BYTES);
+  if (threadIdx.x < LB_M)
+    s_tok[threadIdx.x] = (int)tok[(int64_t)min(r0 + (int)threadIdx.x, R - 1) * tok_stride];
+  __syncthreads();
+
   f32x16 acc[LTile::TM][LTile::TN];
   auto arow = [&](int row, int kt) -> const uint16_t* {
-    const int r = min(r0 + row, R - 1);
-    if (kt < nke) return emb + tok[(int64_t)r * tok_stride] * E + kt * 64;
-    return h_prev + (int64_t)r * H + (kt - nke) * 64;
+    if (kt < nke) return emb + (int64_t)s_tok[row] * E + kt * 64;
+    return h_prev + (int64_t)min(r0 + row, R - 1) * H + (kt - nke) * 64;
   };
   auto brow = [&](int row, int kt) { return wx + (int64_t)(n0 + row) * K + kt * 64; };
-  const bool write_xh = xh_out != nullptr && nt == 0;
-  auto hook = [&](int row, int kt, int c, const uint4& v) {
-    const int r = r0 + row;
-    if (write_xh && r < R)
-      *reinterpret_cast<uint4*>(xh_out + (int64_t)r * K + kt * 64 + c * 8) = v;
-  };
-  gemm_nt_mainloop<LTile>(nk, arow, brow, hook, lds, acc);
+  gemm_nt_mainloop<LTile>(nk, arow, brow, lds, acc);
 
   float* C = reinterpret_cast<float*>(lds);
   store_acc_to_lds<LTile>(acc, C, [](int) { return 0.f; });
@@ -87,7 +87,10 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     h_out[o] = f2bf(hv);
     if (hdrop_out) {
       const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
-      hdrop_out[o] = f2bf(keep ? hv * inv_keep : 0.f);
+      hdrop_out[(int64_t)r * ldh + hu] = f2bf(keep ? hv * inv_keep : 0.f);
+      // augmented columns [H, ldh): a 1 then zeros, so the backward's
+      // dS^T . [h | 1] GEMM also yields the bias gradient
+      if (nt == 0 && u < ldh - H) hdrop_out[(int64_t)r * ldh + H + u] = u == 0 ? 0x3f80 : 0;
     }
     if (gates_out)
       *reinterpret_cast<float4*>(gates_out + (int64_t)r * 4 * H + n0 + 4 * u) =
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
     const float* __restrict__ dh_logit, const float* __restrict__ dh_rec,
     float* __restrict__ dc_carry, const float* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
-    uint16_t* __restrict__ dG, float* __restrict__ dvg_acc) {
+    uint16_t* __restrict__ dG) {
   const int64_t idx = blockIdx.x * 256ll + threadIdx.x;
   if (idx >= (int64_t)R * H) return;
   const int r = (int)(idx / H), u = (int)(idx % H);
@@ -127,41 +130,33 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
   pk.x = (uint32_t)f2bf(dpi) | ((uint32_t)f2bf(dpf) << 16);
   pk.y = (uint32_t)f2bf(dpg) | ((uint32_t)f2bf(dpo) << 16);
   *reinterpret_cast<uint2*>(dG + go_) = pk;
-  if (dvg_acc) {
-    float4 a = *reinterpret_cast<float4*>(dvg_acc + go_);
-    a.x += dpi;
-    a.y += dpf;
-    a.z += dpg;
-    a.w += dpo;
-    *reinterpret_cast<float4*>(dvg_acc + go_) = a;
-  }
 }
 
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
                           const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
-                          float* c_out, uint16_t* hdrop_out, float drop_p, uint32_t seed,
-                          int step, float* gates_out, uint16_t* xh_out, hipStream_t stream) {
+                          float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
+                          uint32_t seed, int step, float* gates_out, hipStream_t stream) {
   const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)lstm_step_fwd_kernel,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, LTile::LDS_BYTES);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_LDS_BYTES);
     attr_set = true;
   }
-  hipLaunchKernelGGL(lstm_step_fwd_kernel, dim3(n_nt * n_rt), dim3(256), LTile::LDS_BYTES, stream,
+  hipLaunchKernelGGL(lstm_step_fwd_kernel, dim3(n_nt * n_rt), dim3(256), LSTM_LDS_BYTES, stream,
                      tok, tok_stride, emb, E, h_prev, c_prev, vgate, vgate_div, R, H, wx, h_out,
-                     c_out, hdrop_out, drop_p, seed, step, gates_out, xh_out);
+                     c_out, hdrop_out, ldh, drop_p, seed, step, gates_out);
 }
 
 void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
                           const float* gates, const float* c_t, const float* c_prev, int R, int H,
-                          float drop_p, uint32_t seed, int step, uint16_t* dG, float* dvg_acc,
+                          float drop_p, uint32_t seed, int step, uint16_t* dG,
                           hipStream_t stream) {
   const int64_t n = (int64_t)R * H;
   hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream, dh_logit, dh_rec, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
-                     step, dG, dvg_acc);
+                     step, dG);
 }
 
 }  // namespace cst

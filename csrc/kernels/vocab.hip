@@ -56,7 +56,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 __global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
-    const uint16_t* __restrict__ hd, int R, int H, const uint16_t* __restrict__ W,
+    const uint16_t* __restrict__ hd, int ldh, int R, int H, const uint16_t* __restrict__ W,
     const float* __restrict__ bias, int V, uint16_t* __restrict__ logits16, int64_t ldl,
     VocabPartial* __restrict__ part, const int64_t* __restrict__ tgt, int64_t tgt_stride,
     int do_sample, float inv_temp, uint32_t seed, int step) {
@@ -70,14 +70,13 @@ __global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
   f32x16 acc[VTile::TM][VTile::TN];
   auto arow = [&](int row, int kt) {
     const int r = min(r0 + row, R - 1);
-    return hd + (int64_t)r * H + kt * 64;
+    return hd + (int64_t)r * ldh + kt * 64;
   };
   auto brow = [&](int row, int kt) {
     const int v = min(v0 + row, V - 1);
     return W + (int64_t)v * H + kt * 64;
   };
-  auto nohook = [](int, int, int, const uint4&) {};
-  gemm_nt_mainloop<VTile>(nk, arow, brow, nohook, lds, acc);
+  gemm_nt_mainloop<VTile>(nk, arow, brow, lds, acc);
 
   float* C = reinterpret_cast<float*>(lds);
   store_acc_to_lds<VTile>(acc, C, [&](int col) {
@@ -189,6 +188,33 @@ __global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
 // token-selection modes of one decode step
 enum SelMode : int { SEL_GT = 0, SEL_SAMPLE = 1, SEL_GREEDY = 2, SEL_SS = 3 };
 
+// 8 lanes per row, 32 rows per 256-thread block: lanes with the same sub-index
+// read 32 consecutive partial records (1 KiB) per tile -> coalesced.
+constexpr int CMB_LANES = 8, CMB_ROWS = 256 / CMB_LANES;
+
+struct RowStat {
+  float m, s, zv, zl, xm, xt;
+  int zi, xi;
+};
+
+__device__ __forceinline__ void merge_stat(RowStat& a, float m2, float s2, float zv2, float zl2,
+                                           int zi2, float xm2, int xi2, float xt2) {
+  const float M = fmaxf(a.m, m2);
+  a.s = (a.m == -INFINITY ? 0.f : a.s * __expf(a.m - M)) +
+        (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - M));
+  a.m = M;
+  if (zv2 > a.zv || (zv2 == a.zv && zi2 < a.zi)) {
+    a.zv = zv2;
+    a.zi = zi2;
+    a.zl = zl2;
+  }
+  if (xm2 > a.xm || (xm2 == a.xm && xi2 < a.xi)) {
+    a.xm = xm2;
+    a.xi = xi2;
+  }
+  a.xt = fmaxf(a.xt, xt2);
+}
+
 __global__ __launch_bounds__(256) void vocab_combine_kernel(
     const VocabPartial* __restrict__ part, int n_vt, int R, float* __restrict__ lse_out,
     int64_t* __restrict__ tok_out, int64_t tok_stride, float* __restrict__ g_sel,
@@ -196,85 +222,67 @@ __global__ __launch_bounds__(256) void vocab_combine_kernel(
     const int64_t* __restrict__ gt, int64_t gt_stride, int mode, float ss_prob,
     uint32_t seed, int step, int* __restrict__ counts, int count_step,
     uint8_t* __restrict__ unfinished) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + w;
-  if (r >= R) return;  // no barriers below
-  float m = -INFINITY, s = 0.f, zv = -INFINITY, zl = 0.f, xt = -INFINITY;
-  int zi = 0x7fffffff, xi = 0x7fffffff;
-  float xm = -INFINITY;  // value at xi
-  for (int t = lane; t < n_vt; t += 64) {
-    const VocabPartial p = part[(int64_t)t * R + r];
-    const float M = fmaxf(m, p.m);
-    s = (m == -INFINITY ? 0.f : s * __expf(m - M)) + (p.m == -INFINITY ? 0.f : p.s * __expf(p.m - M));
-    m = M;
-    if (p.zval > zv || (p.zval == zv && p.zidx < zi)) {
-      zv = p.zval;
-      zi = p.zidx;
-      zl = p.zlogit;
+  __shared__ int s_nonzero;
+  const int sub = threadIdx.x & (CMB_LANES - 1);
+  const int r = blockIdx.x * CMB_ROWS + (threadIdx.x / CMB_LANES);
+  const bool valid = r < R;
+  if (threadIdx.x == 0) s_nonzero = 0;
+  RowStat a = {-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff};
+  if (valid) {
+    for (int t = sub; t < n_vt; t += CMB_LANES) {
+      const VocabPartial p = part[(int64_t)t * R + r];
+      merge_stat(a, p.m, p.s, p.zval, p.zlogit, p.zidx, p.m, p.xidx, p.xtgt);
     }
-    if (p.m > xm || (p.m == xm && p.xidx < xi)) {
-      xm = p.m;
-      xi = p.xidx;
-    }
-    xt = fmaxf(xt, p.xtgt);
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
-    const float M = fmaxf(m, m2);
-    s = (m == -INFINITY ? 0.f : s * __expf(m - M)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - M));
-    m = M;
-    const float zv2 = __shfl_xor(zv, o, 64), zl2 = __shfl_xor(zl, o, 64);
-    const int zi2 = __shfl_xor(zi, o, 64);
-    if (zv2 > zv || (zv2 == zv && zi2 < zi)) {
-      zv = zv2;
-      zi = zi2;
-      zl = zl2;
+  for (int o = 1; o < CMB_LANES; o <<= 1) {
+    merge_stat(a, __shfl_xor(a.m, o, 64), __shfl_xor(a.s, o, 64), __shfl_xor(a.zv, o, 64),
+               __shfl_xor(a.zl, o, 64), __shfl_xor(a.zi, o, 64), __shfl_xor(a.xm, o, 64),
+               __shfl_xor(a.xi, o, 64), __shfl_xor(a.xt, o, 64));
+  }
+  __syncthreads();  // s_nonzero initialised
+  if (valid && sub == 0) {
+    const float lse = a.m + __logf(a.s);
+    if (lse_out) lse_out[r] = lse;
+    if (g_xe) g_xe[(int64_t)r * gxe_stride] = a.xt - lse;
+    if (tok_out != nullptr) {
+      const int64_t gt_tok = gt ? gt[(int64_t)r * gt_stride] : 0;
+      int64_t tok;
+      float tl;
+      switch (mode) {
+        case SEL_SAMPLE: tok = a.zi; tl = a.zl; break;
+        case SEL_GREEDY: tok = a.xi; tl = a.xm; break;
+        case SEL_SS: {
+          const u32x4 u = philox4x32({(uint32_t)r, RNG_SS, (uint32_t)step, 0u}, seed, 0x68E31DA4u);
+          const bool use_sample = u01(u.x) < ss_prob;
+          tok = use_sample ? (int64_t)a.zi : gt_tok;
+          tl = use_sample ? a.zl : a.xt;
+          break;
+        }
+        default: tok = gt_tok; tl = a.xt; break;
+      }
+      // reference forward(): once every row emitted EOS at one step, decoding stops
+      if (counts != nullptr) {
+        bool dead = false;
+        for (int k = 1; k < count_step; ++k) dead |= (counts[k] == 0);
+        if (dead) tok = 0;
+      }
+      // per-row finished mask: reference sample(), or forward() with the
+      // --mask_after_eos fix
+      if (unfinished != nullptr) {
+        const uint8_t u = unfinished[r] && (tok > 0);
+        unfinished[r] = u;
+        if (!u) tok = 0;
+      }
+      tok_out[(int64_t)r * tok_stride] = tok;
+      if (g_sel) g_sel[(int64_t)r * gsel_stride] = tl - lse;
+      if (counts != nullptr && tok != 0) atomicAdd(&s_nonzero, 1);
     }
-    const float xm2 = __shfl_xor(xm, o, 64);
-    const int xi2 = __shfl_xor(xi, o, 64);
-    if (xm2 > xm || (xm2 == xm && xi2 < xi)) {
-      xm = xm2;
-      xi = xi2;
-    }
-    xt = fmaxf(xt, __shfl_xor(xt, o, 64));
   }
-  if (lane != 0) return;
-  const float lse = m + __logf(s);
-  if (lse_out) lse_out[r] = lse;
-  if (g_xe) g_xe[(int64_t)r * gxe_stride] = xt - lse;
-  if (tok_out == nullptr) return;
-  const int64_t gt_tok = gt ? gt[(int64_t)r * gt_stride] : 0;
-  int64_t tok;
-  float tl;
-  switch (mode) {
-    case SEL_SAMPLE: tok = zi; tl = zl; break;
-    case SEL_GREEDY: tok = xi; tl = xm; break;
-    case SEL_SS: {
-      const u32x4 u = philox4x32({(uint32_t)r, RNG_SS, (uint32_t)step, 0u}, seed, 0x68E31DA4u);
-      const bool use_sample = u01(u.x) < ss_prob;
-      tok = use_sample ? (int64_t)zi : gt_tok;
-      tl = use_sample ? zl : xt;
-      break;
-    }
-    default: tok = gt_tok; tl = xt; break;
+  if (counts != nullptr && tok_out != nullptr) {
+    __syncthreads();
+    if (threadIdx.x == 0 && s_nonzero > 0) atomicAdd(&counts[count_step], s_nonzero);
   }
-  // reference forward(): once every row emitted EOS at some step, decoding stops
-  if (counts != nullptr) {
-    bool dead = false;
-    for (int k = 1; k < count_step; ++k) dead |= (counts[k] == 0);
-    if (dead) tok = 0;
-  }
-  // per-row finished mask: reference sample(), or forward() with the
-  // --mask_after_eos fix
-  if (unfinished != nullptr) {
-    const uint8_t u = unfinished[r] && (tok > 0);
-    unfinished[r] = u;
-    if (!u) tok = 0;
-  }
-  tok_out[(int64_t)r * tok_stride] = tok;
-  if (g_sel) g_sel[(int64_t)r * gsel_stride] = tl - lse;
-  if (counts != nullptr && tok != 0) atomicAdd(&counts[count_step], 1);
 }
 
 __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
@@ -315,7 +323,8 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
 }
 
 // -------------------------------------------------------------------------------
-void launch_vocab_fwd(const uint16_t* hd, int R, int H, const uint16_t* W, const float* bias,
+void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                      const float* bias,
                       int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
                       int64_t tgt_stride, int do_sample, float inv_temp, uint32_t seed, int step,
                       hipStream_t stream) {
@@ -327,7 +336,7 @@ void launch_vocab_fwd(const uint16_t* hd, int R, int H, const uint16_t* W, const
     attr_set = true;
   }
   hipLaunchKernelGGL(vocab_fwd_kernel, dim3(n_vt * n_rt), dim3(256), VTile::LDS_BYTES, stream,
-                     hd, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt, tgt_stride,
+                     hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt, tgt_stride,
                      do_sample, inv_temp, seed, step);
 }
 
@@ -340,7 +349,8 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
                           float ss_prob, uint32_t seed, int step, int* counts, int count_step,
                           uint8_t* unfinished, hipStream_t stream) {
-  hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + 3) / 4), dim3(256), 0, stream,
+  hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + CMB_ROWS - 1) / CMB_ROWS), dim3(256), 0,
+                     stream,
                      (const VocabPartial*)part, n_vt, R, lse_out, tok_out, tok_stride, g_sel,
                      gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode, ss_prob, seed, step,
                      counts, count_step, unfinished);

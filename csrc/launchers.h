@@ -23,7 +23,8 @@ void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, f
 enum SelModeHost : int { SEL_GT_H = 0, SEL_SAMPLE_H = 1, SEL_GREEDY_H = 2, SEL_SS_H = 3 };
 int vocab_num_tiles(int V);
 int vocab_partial_bytes();
-void launch_vocab_fwd(const uint16_t* hd, int R, int H, const uint16_t* W, const float* bias,
+void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                      const float* bias,
                       int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
                       int64_t tgt_stride, int do_sample, float inv_temp, uint32_t seed, int step,
                       hipStream_t stream);
@@ -41,11 +42,11 @@ void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
                           const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
-                          float* c_out, uint16_t* hdrop_out, float drop_p, uint32_t seed,
-                          int step, float* gates_out, uint16_t* xh_out, hipStream_t stream);
+                          float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
+                          uint32_t seed, int step, float* gates_out, hipStream_t stream);
 void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
                           const float* gates, const float* c_t, const float* c_prev, int R, int H,
-                          float drop_p, uint32_t seed, int step, uint16_t* dG, float* dvg_acc,
+                          float drop_p, uint32_t seed, int step, uint16_t* dG,
                           hipStream_t stream);
 
 }  // namespace cst

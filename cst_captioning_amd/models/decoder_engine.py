@@ -78,26 +78,26 @@ class _DecoderFn(torch.autograd.Function):
             raise RuntimeError('decoder forward ran without saving activations')
         R, T, vdiv, want_xe = ctx.save_dims
         eng = ctx.eng
-        lse, logits16, hdrop, gates, c_all, xh, seq, labels, bos = ctx.saved
+        lse, logits16, hdrop, gates, c_all, h_all, seq, labels, bos = ctx.saved
         ctx.saved = None  # logits buffer is overwritten in place by dS
         g_sel = dg_sel.contiguous() if dg_sel is not None else None
         g_xe = dg_xe.contiguous() if (want_xe and dg_xe is not None and dg_xe.numel()) else None
         empty = torch.empty(0, device=lse.device)
+        n_steps = logits16.shape[0]
+        # input token of every step: it_0 = BOS / labels[:, 0], it_t = seq[:, t-1]
+        first = labels[:, :1] if labels is not None else bos.view(-1, 1)
+        toks = torch.cat([first, seq[:, :n_steps - 1]], 1).t().reshape(-1)
         dWx, dWlog, dblog, dX, dvg = _ext.ops().decoder_backward(
-            eng.wx, eng.wlog, lse, logits16, hdrop, gates, c_all, xh, seq,
+            eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
-            g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
+            toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
             ctx.drop_p, ctx.seed)
         E = eng.E
-        n_steps = logits16.shape[0]
         d_orig = dWx.index_select(0, eng.inv_perm)
         w_ih_shape, emb_shape = ctx.shapes
         d_wih = torch.zeros(w_ih_shape, dtype=torch.float32, device=dWx.device)
         d_wih[:, :E] = d_orig[:, :E]
         d_whh = d_orig[:, E:].contiguous()
-        # input token of every step: it_0 = BOS / labels[:, 0], it_t = seq[:, t-1]
-        first = labels[:, :1] if labels is not None else bos.view(-1, 1)
-        toks = torch.cat([first, seq[:, :n_steps - 1]], 1).t().reshape(-1)
         d_emb = torch.zeros(emb_shape, dtype=torch.float32, device=dWx.device)
         d_emb.index_add_(0, toks, dX)
         nv = R // vdiv

@@ -114,13 +114,29 @@ class Trainer:
     def rl_loss(self, data, scb_captions):
         opt = self.opt
         S = self.train_loader.get_seq_per_img()
-        model_res, logprobs, _ = self._decode_rollout(data)
-        self.timer.mark('rollout')
         scorer = self._ensure_scorer()
         vid_rows = data['video_index'].repeat_interleave(S)
+        side = None
+        if opt.use_cst == 0 and self.device.type == 'cuda':
+            # The greedy baseline only depends on the inputs and the current
+            # weights: decode + score it on a second HIP stream, concurrently
+            # with the rollout on the main stream.
+            if getattr(self, '_side_stream', None) is None:
+                self._side_stream = torch.cuda.Stream(device=self.device)
+            side = self._side_stream
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                greedy_scores = self._greedy_scores(data, scorer, S)
+        model_res, logprobs, _ = self._decode_rollout(data)
+        self.timer.mark('rollout')
         if opt.use_cst == 0:
             sample_scores = scorer.score(model_res, vid_rows)
-            greedy_scores = self._greedy_scores(data, scorer, S)
+            if side is not None:
+                main.wait_stream(side)
+                greedy_scores.record_stream(main)
+            else:
+                greedy_scores = self._greedy_scores(data, scorer, S)
             reward, m_score, b_score = scst_from_scores(sample_scores.float(),
                                                         greedy_scores.float())
         else:
