@@ -2,6 +2,7 @@
 #include <torch/extension.h>
 
 #include "host/cider_host.h"
+#include "launchers.h"
 
 namespace cst {
 std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor wlog,
@@ -81,4 +82,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cider_score", &cst::cider_score);
   m.def("cider_score_cpu", &cst::cider_score_cpu);
   m.def("flat_adam_step", &cst::flat_adam_step);
+  m.def("set_vocab_variant", &cst::set_vocab_variant);
 }

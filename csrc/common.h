@@ -24,12 +24,9 @@ __device__ __forceinline__ float bf2f(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }
 
-// round-to-nearest-even f32 -> bf16 (NaN stays NaN)
+// round-to-nearest-even f32 -> bf16 (hardware v_cvt_pk_bf16_f32; NaN stays NaN)
 __device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ float h2f(uint16_t h) {
@@ -39,7 +36,26 @@ __device__ __forceinline__ uint16_t f2h(float f) {
   return __builtin_bit_cast(uint16_t, (_Float16)f);
 }
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// fast gate nonlinearities: one exp + one reciprocal each (rel. err ~1e-6)
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+__device__ __forceinline__ float tanhf_(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  const float t = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
+  return copysignf(t, x);
+}
+
+// murmur3 32-bit finaliser: avalanche hash used as a counter-based RNG for
+// the per-element sampling draws (hash(row-key ^ v * odd constant)).
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
 
 // ---- wave64 reductions --------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
@@ -89,13 +105,13 @@ enum RngStream : uint32_t {
   RNG_SS = 3,         // scheduled-sampling coin per row
 };
 
-// Keep-mask of dropout on element (row, col) of step t: 4 columns per draw.
+// Keep-mask of dropout on element (row, col) of step t: a counter hash, so the
+// backward regenerates exactly the forward's mask.
 __device__ __forceinline__ bool dropout_keep(uint32_t seed, int step, int row, int col,
                                              float p) {
-  u32x4 c = {(uint32_t)(col >> 2), (uint32_t)row, RNG_DROPOUT_H, (uint32_t)step};
-  u32x4 r = philox4x32(c, seed, 0x5bd1e995u);
-  uint32_t w = (col & 3) == 0 ? r.x : (col & 3) == 1 ? r.y : (col & 3) == 2 ? r.z : r.w;
-  return u01(w) > p;
+  const uint32_t h = mix32(mix32(seed ^ ((uint32_t)step * 0x9E3779B1u) ^ (uint32_t)row * 0x7FEB352Du) ^
+                           (uint32_t)col * 0x846CA68Bu);
+  return u01(h) > p;
 }
 
 }  // namespace cst

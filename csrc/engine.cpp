@@ -142,7 +142,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     uint16_t* hd = nullptr;
     if (save) hd = reinterpret_cast<uint16_t*>(hdrop_all[t].data_ptr());
     else if (drop_p > 0) hd = reinterpret_cast<uint16_t*>(hd_tmp.data_ptr());
-    launch_lstm_step_fwd(tok, tok_stride, EMB, (int)E, h_prev, c_prev, vgate.data_ptr<float>(),
+    launch_lstm_step_fwd(tok, tok_stride, EMB, (int)E, (int)V, h_prev, c_prev, vgate.data_ptr<float>(),
                          (int)vgate_div, (int)R, (int)H, WX, h_out, c_out, hd, (int)(H + HAUG),
                          (float)drop_p,
                          seed_drop, (int)t, save ? gates_all[t].data_ptr<float>() : nullptr, st);

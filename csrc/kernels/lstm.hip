@@ -24,7 +24,7 @@
 namespace cst {
 
 constexpr int LB_M = 128, LB_N = 64;
-using LTile = Tile<LB_M, LB_N>;
+using LTile = Tile<LB_M, LB_N, 3>;  // 3-stage pipeline: 72 KB + tokens, 2 blocks/CU
 constexpr int LSTM_LDS_BYTES = LTile::LDS_BYTES + LB_M * 4;  // + staged token ids
 
 __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
@@ -35,7 +35,7 @@ __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
 
 __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     const int64_t* __restrict__ tok, int64_t tok_stride, const uint16_t* __restrict__ emb, int E,
-    const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
+    int n_emb_rows, const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
     const float* __restrict__ vgate, int vgate_div, int R, int H,
     const uint16_t* __restrict__ wx, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
     uint16_t* __restrict__ hdrop_out, int ldh, float drop_p, uint32_t seed, int step,
@@ -55,12 +55,29 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
   __syncthreads();
 
   f32x16 acc[LTile::TM][LTile::TN];
-  auto arow = [&](int row, int kt) -> const uint16_t* {
-    if (kt < nke) return emb + (int64_t)s_tok[row] * E + kt * 64;
-    return h_prev + (int64_t)min(r0 + row, R - 1) * H + (kt - nke) * 64;
-  };
-  auto brow = [&](int row, int kt) { return wx + (int64_t)(n0 + row) * K + kt * 64; };
-  gemm_nt_mainloop<LTile>(nk, arow, brow, lds, acc);
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    DmaSrc<LB_M / 32> a;
+    DmaSrc<LB_N / 32> bsrc;
+    a.r0 = make_rsrc(emb, (int64_t)n_emb_rows * E * 2);
+    a.r1 = make_rsrc(h_prev, (int64_t)R * H * 2);
+    a.ksplit = nke;
+#pragma unroll
+    for (int i = 0; i < LB_M / 32; ++i) {
+      const int row = dma_row(w, i, lane), c = dma_chunk(row, lane);
+      a.voff0[i] = s_tok[row] * E * 2 + c * 16;
+      a.voff1[i] = min(r0 + row, R - 1) * H * 2 + c * 16;
+    }
+    bsrc.r0 = bsrc.r1 = make_rsrc(wx, (int64_t)4 * H * K * 2);
+    bsrc.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < LB_N / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      bsrc.voff0[i] = (n0 + row) * K * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff1[i] = bsrc.voff0[i];
+    }
+    gemm_nt_mainloop<LTile>(nk, a, bsrc, lds, acc);
+  }
 
   float* C = reinterpret_cast<float*>(lds);
   store_acc_to_lds<LTile>(acc, C, [](int) { return 0.f; });
@@ -78,11 +95,11 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
         vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
     const float gi = sigmoidf_(pre.x + vg.x);
     const float gf = sigmoidf_(pre.y + vg.y);
-    const float gg = tanhf(pre.z + vg.z);
+    const float gg = tanhf_(pre.z + vg.z);
     const float go = sigmoidf_(pre.w + vg.w);
     const int64_t o = (int64_t)r * H + hu;
     const float c = gf * c_prev[o] + gi * gg;
-    const float hv = go * tanhf(c);
+    const float hv = go * tanhf_(c);
     c_out[o] = c;
     h_out[o] = f2bf(hv);
     if (hdrop_out) {
@@ -118,7 +135,7 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
   const int64_t go_ = (int64_t)r * 4 * H + 4 * u;
   const float4 g4 = *reinterpret_cast<const float4*>(gates + go_);
   const float c = c_t[idx];
-  const float tc = tanhf(c);
+  const float tc = tanhf_(c);
   const float dc = dc_carry[idx] + dh * g4.w * (1.f - tc * tc);
   const float cp = c_prev ? c_prev[idx] : 0.f;
   const float dpi = dc * g4.z * g4.x * (1.f - g4.x);
@@ -133,7 +150,7 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
 }
 
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
-                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
+                          int n_emb_rows, const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
                           uint32_t seed, int step, float* gates_out, hipStream_t stream) {
@@ -145,7 +162,7 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t
     attr_set = true;
   }
   hipLaunchKernelGGL(lstm_step_fwd_kernel, dim3(n_nt * n_rt), dim3(256), LSTM_LDS_BYTES, stream,
-                     tok, tok_stride, emb, E, h_prev, c_prev, vgate, vgate_div, R, H, wx, h_out,
+                     tok, tok_stride, emb, E, n_emb_rows, h_prev, c_prev, vgate, vgate_div, R, H, wx, h_out,
                      c_out, hdrop_out, ldh, drop_p, seed, step, gates_out);
 }
 

@@ -12,9 +12,12 @@
 //   * C = h_drop(R x H) . W(V x H)^T + b  with v_mfma_f32_32x32x16_bf16;
 //   * optional fp16 copy of the logits (the backward's softmax input, so
 //     the backward never recomputes the 0.4 TFLOP projection);
-//   * per (row, tile) partials: max, sum(exp(x - max)), Gumbel-max sample
-//     argmax(x / temp - log(-log u)) with u from Philox(seed, step, row, v)
-//     -- exact multinomial sampling from softmax(x / temp) in one pass --,
+//   * per (row, tile) partials: max, sum(exp(x - max)), a multinomial draw
+//     from softmax(x / temp) done in two exact levels -- inverse CDF inside
+//     the tile over the exp() weights kept in registers, and an exponential
+//     race across tiles (key log(tile mass) - log(E), E ~ Exp(1)) --, both
+//     driven by counter hashes of (seed, step, row, tile), so no per-element
+//     random numbers;
 //     greedy argmax, and the logit of the row's target token.
 // vocab_combine_kernel (one wavefront per row)
 //   * merges the tile partials: LSE, sampled / greedy / target token and
@@ -42,8 +45,7 @@ struct VocabPartial {  // 32 bytes per (tile, row)
   float pad;
 };
 
-constexpr int VB_M = 128, VB_N = 128;
-using VTile = Tile<VB_M, VB_N>;
+constexpr int VB_M = 128;
 
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch),
 // so consecutive ids of the remapped index land on the same XCD's L2.  Vocab
@@ -55,11 +57,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
-__global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
+template <int VB_N, int STAGES, int OCC>
+__global__ __launch_bounds__(256, OCC) void vocab_fwd_kernel(
     const uint16_t* __restrict__ hd, int ldh, int R, int H, const uint16_t* __restrict__ W,
     const float* __restrict__ bias, int V, uint16_t* __restrict__ logits16, int64_t ldl,
     VocabPartial* __restrict__ part, const int64_t* __restrict__ tgt, int64_t tgt_stride,
     int do_sample, float inv_temp, uint32_t seed, int step) {
+  using VTile = Tile<VB_M, VB_N, STAGES>;
+  constexpr int NG = VB_N / 8;  // 4-column groups per thread (2 threads per row)
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_vt = (V + VB_N - 1) / VB_N, n_rt = (R + VB_M - 1) / VB_M;
   const int b = xcd_remap(blockIdx.x, n_vt * n_rt);
@@ -68,15 +73,28 @@ __global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
   const int nk = H / 64;
 
   f32x16 acc[VTile::TM][VTile::TN];
-  auto arow = [&](int row, int kt) {
-    const int r = min(r0 + row, R - 1);
-    return hd + (int64_t)r * ldh + kt * 64;
-  };
-  auto brow = [&](int row, int kt) {
-    const int v = min(v0 + row, V - 1);
-    return W + (int64_t)v * H + kt * 64;
-  };
-  gemm_nt_mainloop<VTile>(nk, arow, brow, lds, acc);
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    DmaSrc<VB_M / 32> a;
+    DmaSrc<VB_N / 32> bsrc;
+    a.r0 = a.r1 = make_rsrc(hd, (int64_t)R * ldh * 2);
+    a.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < VB_M / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      a.voff0[i] = min(r0 + row, R - 1) * ldh * 2 + dma_chunk(row, lane) * 16;
+      a.voff1[i] = a.voff0[i];
+    }
+    bsrc.r0 = bsrc.r1 = make_rsrc(W, (int64_t)V * H * 2);
+    bsrc.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < VB_N / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      bsrc.voff0[i] = min(v0 + row, V - 1) * H * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff1[i] = bsrc.voff0[i];
+    }
+    gemm_nt_mainloop<VTile>(nk, a, bsrc, lds, acc);
+  }
 
   float* C = reinterpret_cast<float*>(lds);
   store_acc_to_lds<VTile>(acc, C, [&](int col) {
@@ -86,39 +104,43 @@ __global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
   __syncthreads();
   const int tid = threadIdx.x;
 
-  // (a) fp16 logits, row-major coalesced 16-byte stores
+  // (a) fp16 logits: lane l of a wave stores columns 4(l&31)..+3 of one row
+  //     (32 lanes = one 256-byte row segment, coalesced); each 16-lane group
+  //     reads 256 contiguous LDS bytes (bank-conflict free).
   if (logits16 != nullptr) {
-#pragma unroll
-    for (int i = 0; i < (VB_M * VB_N / 8) / 256; ++i) {
-      const int idx = tid + i * 256, row = idx >> 4, c8 = (idx & 15) * 8;
-      const int r = r0 + row, v = v0 + c8;
+    constexpr int LPR = VB_N / 4;  // lanes per row
+#pragma unroll 4
+    for (int i = 0; i < (VB_M * VB_N / 4) / 256; ++i) {
+      const int idx = tid + i * 256, row = idx / LPR, c4 = (idx % LPR) * 4;
+      const int r = r0 + row, v = v0 + c4;
       if (r < R && v < V) {
-        const float* src = C + row * VTile::CSTRIDE + c8;
+        const float4 x = *reinterpret_cast<const float4*>(C + row * VTile::CSTRIDE + c4);
         uint16_t* dst = logits16 + (int64_t)r * ldl + v;
-        if (v + 8 <= V) {
-          uint4 pk;
-          pk.x = (uint32_t)f2h(src[0]) | ((uint32_t)f2h(src[1]) << 16);
-          pk.y = (uint32_t)f2h(src[2]) | ((uint32_t)f2h(src[3]) << 16);
-          pk.z = (uint32_t)f2h(src[4]) | ((uint32_t)f2h(src[5]) << 16);
-          pk.w = (uint32_t)f2h(src[6]) | ((uint32_t)f2h(src[7]) << 16);
-          *reinterpret_cast<uint4*>(dst) = pk;
+        if (v + 4 <= V) {
+          uint2 pk;
+          pk.x = (uint32_t)f2h(x.x) | ((uint32_t)f2h(x.y) << 16);
+          pk.y = (uint32_t)f2h(x.z) | ((uint32_t)f2h(x.w) << 16);
+          *reinterpret_cast<uint2*>(dst) = pk;
         } else {
-          for (int e = 0; e < V - v; ++e) dst[e] = f2h(src[e]);
+          const float xs[4] = {x.x, x.y, x.z, x.w};
+          for (int e = 0; e < V - v; ++e) dst[e] = f2h(xs[e]);
         }
       }
     }
   }
 
-  // (b) per-row statistics: 2 threads per row, interleaved 4-column groups
+  // (b) per-row statistics: 2 threads per row (adjacent lanes), interleaved
+  //     4-column groups (thread h owns groups 2j+h).
   const int row = tid >> 1, h = tid & 1;
   const int r = r0 + row;
   const int rr = min(r, R - 1);
   const int target = tgt != nullptr ? (int)tgt[(int64_t)rr * tgt_stride] : -1;
   const float* Crow = C + row * VTile::CSTRIDE;
+  // pass 1: max and first argmax
   float m = -INFINITY;
   int xidx = 0x7fffffff;
-#pragma unroll 4
-  for (int j = 0; j < 16; ++j) {
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
     const int c0 = 4 * (2 * j + h);
     const float4 x = *reinterpret_cast<const float4*>(Crow + c0);
     const int v = v0 + c0;
@@ -130,54 +152,88 @@ __global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
         xidx = v + e;
       }
   }
-  float s = 0.f, zval = -INFINITY, zlogit = 0.f, xtgt = -INFINITY;
-  int zidx = 0x7fffffff;
-#pragma unroll 2
-  for (int j = 0; j < 16; ++j) {
+  {
+    const float m2 = __shfl_xor(m, 1, 64);
+    const int xi2 = __shfl_xor(xidx, 1, 64);
+    if (m2 > m || (m2 == m && xi2 < xidx)) xidx = xi2;
+    m = fmaxf(m, m2);  // row max of the tile, shared by both threads
+  }
+  // pass 2: exp weights kept in registers; softmax sum; target logit
+  const bool temp1 = inv_temp == 1.f;
+  float ev[NG][4];
+  float s = 0.f, sw = 0.f, xtgt = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
     const int c0 = 4 * (2 * j + h);
     const float4 x = *reinterpret_cast<const float4*>(Crow + c0);
     const int v = v0 + c0;
     const float xs[4] = {x.x, x.y, x.z, x.w};
-    u32x4 rnd = {0, 0, 0, 0};
-    if (do_sample) rnd = philox4x32({(uint32_t)(v >> 2), (uint32_t)rr, RNG_GUMBEL, (uint32_t)step},
-                                    seed, 0x2545F491u);
-    const uint32_t rs[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      if (v + e >= V) continue;
-      s += __expf(xs[e] - m);
+      const bool ok = v + e < V;
+      const float ex = ok ? __expf(xs[e] - m) : 0.f;
+      s += ex;
       if (v + e == target) xtgt = xs[e];
-      if (do_sample) {
-        const float g = -__logf(-__logf(u01(rs[e])));
-        const float z = xs[e] * inv_temp + g;
-        if (z > zval) {
-          zval = z;
-          zidx = v + e;
-          zlogit = xs[e];
+      const float wv = (temp1 || !ok) ? ex : __expf((xs[e] - m) * inv_temp);
+      ev[j][e] = wv;
+      sw += wv;
+    }
+  }
+  const float s_other = __shfl_xor(s, 1, 64);
+  const float sw_other = __shfl_xor(sw, 1, 64);
+  const float S = s + s_other;
+  // pass 3 (sampling): exact two-level multinomial draw.  Within the tile:
+  // inverse CDF over the register-resident weights (thread 0's columns first);
+  // across tiles (in the combine): exponential race with key
+  // z = m/temp + log(sum_w) - log(E),  E ~ Exp(1)  => tile chosen w.p. ~ mass.
+  float zval = -INFINITY, zlogit = 0.f;
+  int zidx = 0x7fffffff;
+  if (do_sample) {
+    const uint32_t key = mix32(seed ^ mix32((uint32_t)rr * 0x9E3779B1u + (uint32_t)step * 0x85EBCA77u) ^
+                               (uint32_t)vt * 0xC2B2AE3Du);
+    const float u = ((float)(key >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    const float sw0 = h == 0 ? sw : sw_other;  // thread 0's mass
+    const float tot = sw + sw_other;
+    float tgt_mass = u * tot - (h == 0 ? 0.f : sw0);
+    int cand = -1;
+    float cum = 0.f;
+    int last = -1;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int v = v0 + 4 * (2 * j + h) + e;
+        if (v < V) {
+          cum += ev[j][e];
+          last = v;
+          if (cand < 0 && cum > tgt_mass) cand = v;
         }
       }
     }
+    // thread 0 wins if the target falls in its mass; rounding: fall back to last
+    const bool mine = (h == 0) ? (u * tot < sw0) : !(u * tot < sw0);
+    const int pick = cand >= 0 ? cand : last;
+    const int pick2 = __shfl_xor(pick, 1, 64);
+    const int chosen = mine ? pick : pick2;
+    const uint32_t key2 = mix32(key ^ 0x68E31DA4u);
+    const float u2 = ((float)(key2 >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    zidx = chosen;
+    zval = (tot > 0.f && chosen >= 0) ? m * inv_temp + __logf(tot) - __logf(-__logf(u2))
+                                      : -INFINITY;
   }
-  // merge the two threads of the row (adjacent lanes)
+  // logit of the sampled token: read it back from the C tile (a row's two
+  // threads agree on zidx)
+  if (do_sample && zidx >= v0 && zidx < v0 + VB_N) zlogit = Crow[zidx - v0];
   {
-    const float m2 = __shfl_xor(m, 1, 64), s2 = __shfl_xor(s, 1, 64);
-    const int xi2 = __shfl_xor(xidx, 1, 64);
-    const float M = fmaxf(m, m2);
-    const float S = (m == -INFINITY ? 0.f : s * __expf(m - M)) +
-                    (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - M));
-    int xi = (m > m2 || (m == m2 && xidx < xi2)) ? xidx : xi2;
-    const float zv2 = __shfl_xor(zval, 1, 64), zl2 = __shfl_xor(zlogit, 1, 64);
-    const int zi2 = __shfl_xor(zidx, 1, 64);
-    const bool mine = zval > zv2 || (zval == zv2 && zidx < zi2);
     const float xt2 = __shfl_xor(xtgt, 1, 64);
     if (h == 0 && r < R) {
       VocabPartial p;
-      p.m = M;
+      p.m = m;
       p.s = S;
-      p.zval = mine ? zval : zv2;
-      p.zlogit = mine ? zlogit : zl2;
-      p.zidx = mine ? zidx : zi2;
-      p.xidx = xi;
+      p.zval = zval;
+      p.zlogit = zlogit;
+      p.zidx = zidx;
+      p.xidx = xidx;
       p.xtgt = fmaxf(xtgt, xt2);
       p.pad = 0.f;
       part[(int64_t)vt * R + r] = p;
@@ -188,9 +244,9 @@ __global__ __launch_bounds__(256, 2) void vocab_fwd_kernel(
 // token-selection modes of one decode step
 enum SelMode : int { SEL_GT = 0, SEL_SAMPLE = 1, SEL_GREEDY = 2, SEL_SS = 3 };
 
-// 8 lanes per row, 32 rows per 256-thread block: lanes with the same sub-index
-// read 32 consecutive partial records (1 KiB) per tile -> coalesced.
-constexpr int CMB_LANES = 8, CMB_ROWS = 256 / CMB_LANES;
+// 32 lanes per row (a half wavefront), 8 rows per 256-thread block: each lane
+// merges ~3 tiles, then a 5-step shuffle tree finishes the row.
+constexpr int CMB_LANES = 32, CMB_ROWS = 256 / CMB_LANES;
 
 struct RowStat {
   float m, s, zv, zl, xm, xt;
@@ -323,26 +379,56 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
 }
 
 // -------------------------------------------------------------------------------
-void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
-                      const float* bias,
-                      int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
-                      int64_t tgt_stride, int do_sample, float inv_temp, uint32_t seed, int step,
-                      hipStream_t stream) {
-  const int n_vt = (V + VB_N - 1) / VB_N, n_rt = (R + VB_M - 1) / VB_M;
+// Tile-shape variants (A/B-tested on MI355X, see profiles/); the partial
+// record layout depends on the vocab tile width, so the choice is global.
+static int g_vocab_variant = 0;
+void set_vocab_variant(int v) { g_vocab_variant = v; }
+static int vocab_bn() { return g_vocab_variant == 1 || g_vocab_variant == 3 ? 64 : 128; }
+
+template <int BN, int STAGES, int OCC>
+static void launch_vocab_fwd_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                               const float* bias, int V, uint16_t* logits16, int64_t ldl,
+                               void* part, const int64_t* tgt, int64_t tgt_stride,
+                               int do_sample, float inv_temp, uint32_t seed, int step,
+                               hipStream_t stream) {
+  using TL = Tile<VB_M, BN, STAGES>;
+  const int n_vt = (V + BN - 1) / BN, n_rt = (R + VB_M - 1) / VB_M;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        VTile::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)vocab_fwd_kernel<BN, STAGES, OCC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, TL::LDS_BYTES);
     attr_set = true;
   }
-  hipLaunchKernelGGL(vocab_fwd_kernel, dim3(n_vt * n_rt), dim3(256), VTile::LDS_BYTES, stream,
-                     hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt, tgt_stride,
-                     do_sample, inv_temp, seed, step);
+  hipLaunchKernelGGL((vocab_fwd_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256),
+                     TL::LDS_BYTES, stream, hd, ldh, R, H, W, bias, V, logits16, ldl,
+                     (VocabPartial*)part, tgt, tgt_stride, do_sample, inv_temp, seed, step);
 }
 
-int vocab_num_tiles(int V) { return (V + VB_N - 1) / VB_N; }
+void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                      const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
+                      const int64_t* tgt, int64_t tgt_stride, int do_sample, float inv_temp,
+                      uint32_t seed, int step, hipStream_t stream) {
+  switch (g_vocab_variant) {
+    case 1:  // 128x64 tile, 3 stages (72 KB LDS, 2 blocks/CU)
+      launch_vocab_fwd_t<64, 3, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                   tgt_stride, do_sample, inv_temp, seed, step, stream);
+      break;
+    case 2:  // 128x128 tile, 3 stages (96 KB LDS, 1 block/CU)
+      launch_vocab_fwd_t<128, 3, 1>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                    tgt_stride, do_sample, inv_temp, seed, step, stream);
+      break;
+    case 3:  // 128x64 tile, 2 stages
+      launch_vocab_fwd_t<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                   tgt_stride, do_sample, inv_temp, seed, step, stream);
+      break;
+    default:  // 128x128 tile, 2 stages (70 KB LDS incl. C tile, 2 blocks/CU)
+      launch_vocab_fwd_t<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                    tgt_stride, do_sample, inv_temp, seed, step, stream);
+  }
+}
+
+int vocab_num_tiles(int V) { return (V + vocab_bn() - 1) / vocab_bn(); }
 int vocab_partial_bytes() { return (int)sizeof(VocabPartial); }
-int vocab_fwd_lds_bytes() { return VTile::LDS_BYTES; }
 
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,

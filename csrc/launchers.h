@@ -22,6 +22,7 @@ void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, f
 // vocab.hip
 enum SelModeHost : int { SEL_GT_H = 0, SEL_SAMPLE_H = 1, SEL_GREEDY_H = 2, SEL_SS_H = 3 };
 int vocab_num_tiles(int V);
+void set_vocab_variant(int v);
 int vocab_partial_bytes();
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                       const float* bias,
@@ -40,7 +41,7 @@ void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_
 
 // lstm.hip
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
-                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
+                          int n_emb_rows, const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
                           uint32_t seed, int step, float* gates_out, hipStream_t stream);

@@ -20,7 +20,11 @@ labels = torch.randint(3, V, (R, L), device=dev)
 labels[:, 0] = 1
 bos = torch.ones(R, dtype=torch.long, device=dev)
 res = {}
-for name, modes, save, drop in [('greedy_nosave', [2] * (T - 1), False, 0.0),
+import os
+variants = [int(x) for x in os.environ.get('VARIANTS', '0').split(',')]
+for var in variants:
+  C.set_vocab_variant(var)
+  for name, modes, save, drop in [('greedy_nosave', [2] * (T - 1), False, 0.0),
                                 ('sample_nosave', [1] * (T - 1), False, 0.0),
                                 ('sample_save_drop', [1] * (T - 1), True, 0.5),
                                 ('gt_save_drop', [0] * (T - 1), True, 0.5)]:
@@ -33,5 +37,5 @@ for name, modes, save, drop in [('greedy_nosave', [2] * (T - 1), False, 0.0),
     for _ in range(10):
         args()
     torch.cuda.synchronize()
-    res[name] = (time.perf_counter() - t0) / 10 * 1e3
+    res['v%d_%s' % (var, name)] = round((time.perf_counter() - t0) / 10 * 1e3, 3)
 print(json.dumps(res))
