@@ -5,7 +5,8 @@
 #include "launchers.h"
 
 namespace cst {
-std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor wlog,
+std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor ptab,
+                                        at::Tensor whh, at::Tensor wlog,
                                         at::Tensor blog, at::Tensor vgate, int64_t vgate_div,
                                         at::Tensor labels, at::Tensor bos, int64_t R, int64_t T,
                                         std::vector<int64_t> modes, double ss_prob,

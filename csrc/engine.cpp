@@ -25,9 +25,11 @@ namespace cst {
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
-// h_drop rows carry HAUG extra columns [1, 0, ...] (written by the LSTM kernel)
-// so that one GEMM dS^T [h | 1] gives the logit weight AND bias gradients.
-constexpr int64_t HAUG = 16;
+// h_drop rows may carry HAUG extra columns [1, 0, ...] (written by the LSTM
+// kernel) so that one GEMM dS^T [h | 1] also yields the bias gradient.  The
+// MI355X measurement (hipBLASLt at N=528 vs 512) made the dS kernel's
+// column-sum partials the faster route, so HAUG = 0.
+constexpr int64_t HAUG = 0;
 
 template <class T>
 static T* ptr_or_null(const at::Tensor& t) {
@@ -40,7 +42,8 @@ static void check_cuda(const at::Tensor& t, const char* name) {
 }
 
 // modes[t] = token-selection mode for token t+1 (see SelModeHost)
-std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor wlog,
+std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor ptab,
+                                        at::Tensor whh, at::Tensor wlog,
                                         at::Tensor blog, at::Tensor vgate, int64_t vgate_div,
                                         at::Tensor labels, at::Tensor bos, int64_t R, int64_t T,
                                         std::vector<int64_t> modes, double ss_prob,
@@ -56,6 +59,12 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                   wlog.scalar_type() == at::kBFloat16,
               "decoder weights must be bf16");
   TORCH_CHECK(vgate.scalar_type() == at::kFloat, "vgate must be fp32");
+  check_cuda(ptab, "ptab");
+  check_cuda(whh, "whh");
+  TORCH_CHECK(ptab.scalar_type() == at::kFloat && ptab.size(0) == emb.size(0) &&
+                  ptab.size(1) == wx.size(0), "ptab must be fp32 (V, 4H)");
+  TORCH_CHECK(whh.scalar_type() == at::kBFloat16 && whh.size(0) == wx.size(0) &&
+                  whh.size(1) * 4 == wx.size(0), "whh must be bf16 (4H, H)");
   const int64_t H4 = wx.size(0), H = H4 / 4, E = emb.size(1), V = wlog.size(0);
   TORCH_CHECK(wx.size(1) == E + H, "wx must be (4H, E+H)");
   TORCH_CHECK(E % 64 == 0 && H % 64 == 0, "E and H must be multiples of 64");
@@ -95,7 +104,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   if (save) {
     logits16 = at::empty({n_steps, R, ldl}, at::TensorOptions().dtype(at::kHalf).device(dev));
     hdrop_all = at::empty({n_steps, R, H + HAUG}, bf);  // [h_drop | 1 | 0...]
-    gates_all = at::empty({n_steps, R, H4}, f32);
+    gates_all = at::empty({n_steps, R, H4}, bf);
     c_all = at::empty({n_steps, R, H}, f32);
     h_all = at::empty({n_steps, R, H}, bf);
   }
@@ -107,8 +116,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   const uint32_t seed_samp = (uint32_t)(seed * 40503u + 0x9E37u);
   const float inv_temp = (float)(1.0 / temperature);
   const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
-  const uint16_t* EMB = reinterpret_cast<const uint16_t*>(emb.data_ptr());
-  const uint16_t* WX = reinterpret_cast<const uint16_t*>(wx.data_ptr());
+  const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
   const int64_t* LAB = have_labels ? labels.data_ptr<int64_t>() : nullptr;
 
   for (int64_t t = 0; t < n_steps; ++t) {
@@ -142,10 +150,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     uint16_t* hd = nullptr;
     if (save) hd = reinterpret_cast<uint16_t*>(hdrop_all[t].data_ptr());
     else if (drop_p > 0) hd = reinterpret_cast<uint16_t*>(hd_tmp.data_ptr());
-    launch_lstm_step_fwd(tok, tok_stride, EMB, (int)E, (int)V, h_prev, c_prev, vgate.data_ptr<float>(),
-                         (int)vgate_div, (int)R, (int)H, WX, h_out, c_out, hd, (int)(H + HAUG),
-                         (float)drop_p,
-                         seed_drop, (int)t, save ? gates_all[t].data_ptr<float>() : nullptr, st);
+    launch_lstm_step_fwd(tok, tok_stride, ptab.data_ptr<float>(), h_prev, c_prev,
+                         vgate.data_ptr<float>(), (int)vgate_div, (int)R, (int)H, WHH, h_out,
+                         c_out, hd, (int)(H + HAUG), (float)drop_p, seed_drop, (int)t,
+                         save ? reinterpret_cast<uint16_t*>(gates_all[t].data_ptr()) : nullptr,
+                         st);
     const uint16_t* vin = hd ? hd : h_out;
     const int ldh = hd ? (int)(H + HAUG) : (int)H;
     const bool choose = t < T - 1;
@@ -195,21 +204,23 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   TORCH_CHECK(toks.numel() == n_steps * R, "toks must hold one token per (step, row)");
   const uint32_t seed_drop = (uint32_t)(seed * 2654435761u + 17u);
 
-  // 1. dS = dG (onehot - softmax), in place (fp16 logits -> bf16 dS)
+  // 1. dS = dG (onehot - softmax), in place (fp16 logits -> bf16 dS), plus
+  //    per-block column sums of dS (bias gradient)
+  TORCH_CHECK(V <= 8 * 2048, "vocab larger than the dS kernel's register tiling");
+  at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n_steps, (int)R), V}, f32);
   launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
                       (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
                       has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
                       has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
                       has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
                       has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                      has_xe ? dg_xe.size(1) : 0, st);
+                      has_xe ? dg_xe.size(1) : 0, colsum.data_ptr<float>(), st);
   at::Tensor dS = logits16.view(at::kBFloat16).view({n_steps * R, ldl}).narrow(1, 0, V);
   // 2. batched vocab-head GEMMs over all n_steps*R rows (hipBLASLt)
   at::Tensor dHd = at::mm(dS, wlog, at::kFloat);                        // (n*R, H)
-  at::Tensor hd2 = hdrop_all.view({n_steps * R, H + HAUG});
-  at::Tensor dW_aug = at::mm(dS.t(), hd2, at::kFloat);                  // (V, H+HAUG)
-  at::Tensor dWlog = dW_aug.narrow(1, 0, H).contiguous();
-  at::Tensor dblog = dW_aug.select(1, H).contiguous();                  // column sums of dS
+  at::Tensor hd2 = hdrop_all.view({n_steps * R, H + HAUG}).narrow(1, 0, H);
+  at::Tensor dWlog = at::mm(dS.t(), hd2, at::kFloat);                   // (V, H)
+  at::Tensor dblog = colsum.sum(0);                                     // (V)
   // 3. reverse recurrence
   at::Tensor dG_all = at::empty({n_steps, R, H4}, wx.options());
   at::Tensor dc = at::zeros({R, H}, f32);
@@ -218,7 +229,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     launch_lstm_cell_bwd(dHd.data_ptr<float>() + t * R * H,
                          dh_rec.defined() ? dh_rec.data_ptr<float>() : nullptr,
-                         dc.data_ptr<float>(), gates_all[t].data_ptr<float>(),
+                         dc.data_ptr<float>(),
+                         reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
                          c_all[t].data_ptr<float>(),
                          t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R, (int)H,
                          (float)drop_p, seed_drop, (int)t,

@@ -8,14 +8,15 @@
 // MI355X design:
 //   * the video part W_ih[:, E:] . v is constant over time and identical for
 //     the seq_per_img rows of a video, so it is computed ONCE per video by the
-//     caller (vgate, B x 4H) and added in the epilogue: the per-step GEMM is
-//     K = E + H = 1024 instead of 2560, and the 20x row duplication of
-//     FeatExpander (model.py:84-86) disappears;
+//     caller (vgate, B x 4H) and added in the epilogue, and the 20x row
+//     duplication of FeatExpander (model.py:84-86) disappears;
 //   * gate rows are packed so that one 64-column tile holds 16 hidden units x
 //     4 gates (packed row 4u+g <- original row g*H+u): the whole cell update
 //     happens in the GEMM epilogue, nothing but h/c leaves the kernel;
-//   * the A operand is gathered on the fly: K-tiles < E come from embedding
-//     rows picked by token id, the rest from h_{t-1};
+//   * the input-token term W_ie . emb[tok] is a row of the table
+//     P = emb . W_ie^T (V x 4H, refreshed once per optimizer step by one
+//     hipBLASLt GEMM), gathered in the epilogue, so the per-step GEMM is only
+//     h_{t-1} . W_hh^T (K = H);
 //   * training mode also emits, for the backward: post-activation gates, c_t,
 //     h_t, and h after dropout (the input of the vocabulary projection; mask
 //     from Philox, regenerated in backward).
@@ -34,84 +35,97 @@ __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
 }
 
 __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
-    const int64_t* __restrict__ tok, int64_t tok_stride, const uint16_t* __restrict__ emb, int E,
-    int n_emb_rows, const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
+    const int64_t* __restrict__ tok, int64_t tok_stride, const float* __restrict__ ptab,
+    const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
     const float* __restrict__ vgate, int vgate_div, int R, int H,
-    const uint16_t* __restrict__ wx, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
+    const uint16_t* __restrict__ whh, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
     uint16_t* __restrict__ hdrop_out, int ldh, float drop_p, uint32_t seed, int step,
-    float* __restrict__ gates_out) {
+    uint16_t* __restrict__ gates_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
   const int b = xcd_remap_l(blockIdx.x, n_nt * n_rt);
   const int nt = b / n_rt, rt = b % n_rt;
   const int r0 = rt * LB_M, n0 = nt * LB_N;
-  const int K = E + H, nk = K / 64, nke = E / 64;
+  const int nk = H / 64;
 
-  // token ids of this row tile, staged once (keeps the id -> row lookup off
-  // the critical path of every K-tile)
+  // token ids of this row tile (used by the epilogue's table gather)
   int* s_tok = reinterpret_cast<int*>(lds + LTile::LDS_BYTES);
   if (threadIdx.x < LB_M)
     s_tok[threadIdx.x] = (int)tok[(int64_t)min(r0 + (int)threadIdx.x, R - 1) * tok_stride];
   __syncthreads();
+
+  // Epilogue operands are gathered BEFORE the main loop, so their latency
+  // (random rows of an 86 MB table, video gates, c_{t-1}) hides under the GEMM.
+  const int tid = threadIdx.x, u = tid & 15, rg = tid >> 4;
+  const int hu = nt * 16 + u;  // global hidden unit
+  constexpr int RPT = LB_M / 16;  // rows per thread
+  float4 pre_px[RPT], pre_vg[RPT];
+  float pre_c[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int row = rg + 16 * i, r = min(r0 + row, R - 1);
+    pre_px[i] = *reinterpret_cast<const float4*>(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u);
+    pre_vg[i] = *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
+    pre_c[i] = c_prev[(int64_t)r * H + hu];
+  }
 
   f32x16 acc[LTile::TM][LTile::TN];
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     DmaSrc<LB_M / 32> a;
     DmaSrc<LB_N / 32> bsrc;
-    a.r0 = make_rsrc(emb, (int64_t)n_emb_rows * E * 2);
-    a.r1 = make_rsrc(h_prev, (int64_t)R * H * 2);
-    a.ksplit = nke;
+    a.r0 = a.r1 = make_rsrc(h_prev, (int64_t)R * H * 2);
+    a.ksplit = nk;
 #pragma unroll
     for (int i = 0; i < LB_M / 32; ++i) {
-      const int row = dma_row(w, i, lane), c = dma_chunk(row, lane);
-      a.voff0[i] = s_tok[row] * E * 2 + c * 16;
-      a.voff1[i] = min(r0 + row, R - 1) * H * 2 + c * 16;
+      const int row = dma_row(w, i, lane);
+      a.voff0[i] = min(r0 + row, R - 1) * H * 2 + dma_chunk(row, lane) * 16;
+      a.voff1[i] = a.voff0[i];
     }
-    bsrc.r0 = bsrc.r1 = make_rsrc(wx, (int64_t)4 * H * K * 2);
+    bsrc.r0 = bsrc.r1 = make_rsrc(whh, (int64_t)4 * H * H * 2);
     bsrc.ksplit = nk;
 #pragma unroll
     for (int i = 0; i < LB_N / 32; ++i) {
       const int row = dma_row(w, i, lane);
-      bsrc.voff0[i] = (n0 + row) * K * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff0[i] = (n0 + row) * H * 2 + dma_chunk(row, lane) * 16;
       bsrc.voff1[i] = bsrc.voff0[i];
     }
-    gemm_nt_mainloop<LTile>(nk, a, bsrc, lds, acc);
+    gemm_nt_mainloop<LTile>(nk, a, bsrc, lds, acc);  // ends with a barrier (s_tok visible)
   }
 
   float* C = reinterpret_cast<float*>(lds);
   store_acc_to_lds<LTile>(acc, C, [](int) { return 0.f; });
   __syncthreads();
 
-  const int tid = threadIdx.x, u = tid & 15, rg = tid >> 4;
-  const int hu = nt * 16 + u;  // global hidden unit
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-#pragma unroll 2
-  for (int i = 0; i < LB_M / 16; ++i) {
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
     const int row = rg + 16 * i, r = r0 + row;
-    if (r >= R) break;
-    const float4 pre = *reinterpret_cast<const float4*>(C + row * LTile::CSTRIDE + 4 * u);
-    const float4 vg = *reinterpret_cast<const float4*>(
-        vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
-    const float gi = sigmoidf_(pre.x + vg.x);
-    const float gf = sigmoidf_(pre.y + vg.y);
-    const float gg = tanhf_(pre.z + vg.z);
-    const float go = sigmoidf_(pre.w + vg.w);
-    const int64_t o = (int64_t)r * H + hu;
-    const float c = gf * c_prev[o] + gi * gg;
-    const float hv = go * tanhf_(c);
-    c_out[o] = c;
-    h_out[o] = f2bf(hv);
-    if (hdrop_out) {
-      const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
-      hdrop_out[(int64_t)r * ldh + hu] = f2bf(keep ? hv * inv_keep : 0.f);
-      // augmented columns [H, ldh): a 1 then zeros, so the backward's
-      // dS^T . [h | 1] GEMM also yields the bias gradient
-      if (nt == 0 && u < ldh - H) hdrop_out[(int64_t)r * ldh + H + u] = u == 0 ? 0x3f80 : 0;
+    if (r < R) {
+      const float4 pre = *reinterpret_cast<const float4*>(C + row * LTile::CSTRIDE + 4 * u);
+      const float4 vg = pre_vg[i], px = pre_px[i];
+      const float gi = sigmoidf_(pre.x + vg.x + px.x);
+      const float gf = sigmoidf_(pre.y + vg.y + px.y);
+      const float gg = tanhf_(pre.z + vg.z + px.z);
+      const float go = sigmoidf_(pre.w + vg.w + px.w);
+      const int64_t o = (int64_t)r * H + hu;
+      const float c = gf * pre_c[i] + gi * gg;
+      const float hv = go * tanhf_(c);
+      c_out[o] = c;
+      h_out[o] = f2bf(hv);
+      if (hdrop_out) {
+        const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
+        hdrop_out[(int64_t)r * ldh + hu] = f2bf(keep ? hv * inv_keep : 0.f);
+        // augmented columns [H, ldh): a 1 then zeros (bias-gradient GEMM trick)
+        if (nt == 0 && u < ldh - H) hdrop_out[(int64_t)r * ldh + H + u] = u == 0 ? 0x3f80 : 0;
+      }
+      if (gates_out) {
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(gi) | ((uint32_t)f2bf(gf) << 16);
+        pk.y = (uint32_t)f2bf(gg) | ((uint32_t)f2bf(go) << 16);
+        *reinterpret_cast<uint2*>(gates_out + (int64_t)r * 4 * H + n0 + 4 * u) = pk;
+      }
     }
-    if (gates_out)
-      *reinterpret_cast<float4*>(gates_out + (int64_t)r * 4 * H + n0 + 4 * u) =
-          make_float4(gi, gf, gg, go);
   }
 }
 
@@ -121,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
 //   dpre = [dc*g*i(1-i), dc*c_prev*f(1-f), dc*i*(1-g^2), dh*tanh(c)*o(1-o)]
 __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
     const float* __restrict__ dh_logit, const float* __restrict__ dh_rec,
-    float* __restrict__ dc_carry, const float* __restrict__ gates, const float* __restrict__ c_t,
+    float* __restrict__ dc_carry, const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
     uint16_t* __restrict__ dG) {
   const int64_t idx = blockIdx.x * 256ll + threadIdx.x;
@@ -133,7 +147,9 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
     if (keep) dh += dh_logit[idx] * (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
   }
   const int64_t go_ = (int64_t)r * 4 * H + 4 * u;
-  const float4 g4 = *reinterpret_cast<const float4*>(gates + go_);
+  const uint2 gp = *reinterpret_cast<const uint2*>(gates + go_);
+  const float4 g4 = make_float4(bf2f(gp.x & 0xffff), bf2f(gp.x >> 16), bf2f(gp.y & 0xffff),
+                                bf2f(gp.y >> 16));
   const float c = c_t[idx];
   const float tc = tanhf_(c);
   const float dc = dc_carry[idx] + dh * g4.w * (1.f - tc * tc);
@@ -149,11 +165,11 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
   *reinterpret_cast<uint2*>(dG + go_) = pk;
 }
 
-void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
-                          int n_emb_rows, const uint16_t* h_prev, const float* c_prev, const float* vgate,
-                          int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
+void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
+                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
+                          int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
-                          uint32_t seed, int step, float* gates_out, hipStream_t stream) {
+                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream) {
   const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
   static bool attr_set = false;
   if (!attr_set) {
@@ -162,13 +178,13 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t
     attr_set = true;
   }
   hipLaunchKernelGGL(lstm_step_fwd_kernel, dim3(n_nt * n_rt), dim3(256), LSTM_LDS_BYTES, stream,
-                     tok, tok_stride, emb, E, n_emb_rows, h_prev, c_prev, vgate, vgate_div, R, H, wx, h_out,
+                     tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh, h_out,
                      c_out, hdrop_out, ldh, drop_p, seed, step, gates_out);
 }
 
 void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
-                          const float* gates, const float* c_t, const float* c_prev, int R, int H,
-                          float drop_p, uint32_t seed, int step, uint16_t* dG,
+                          const uint16_t* gates, const float* c_t, const float* c_prev, int R,
+                          int H, float drop_p, uint32_t seed, int step, uint16_t* dG,
                           hipStream_t stream) {
   const int64_t n = (int64_t)R * H;
   hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,

@@ -72,6 +72,20 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_kernel(
   const int r0 = rt * VB_M, v0 = vt * VB_N;
   const int nk = H / 64;
 
+  // epilogue operands prefetched before the main loop (latency hides under it)
+  float pre_bias[VTile::TN];
+  {
+    const int lane = threadIdx.x & 63, wc = (threadIdx.x >> 6) & 1;
+#pragma unroll
+    for (int j = 0; j < VTile::TN; ++j) {
+      const int v = v0 + wc * VTile::WN + j * 32 + (lane & 31);
+      pre_bias[j] = v < V ? bias[v] : 0.f;
+    }
+  }
+  const int target = tgt != nullptr
+                         ? (int)tgt[(int64_t)min(r0 + (int)(threadIdx.x >> 1), R - 1) * tgt_stride]
+                         : -1;
+
   f32x16 acc[VTile::TM][VTile::TN];
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -98,8 +112,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_kernel(
 
   float* C = reinterpret_cast<float*>(lds);
   store_acc_to_lds<VTile>(acc, C, [&](int col) {
-    const int v = v0 + col;
-    return v < V ? bias[v] : 0.f;
+    return pre_bias[(col % VTile::WN) / 32];  // col = wc*WN + j*32 + lane%32
   });
   __syncthreads();
   const int tid = threadIdx.x;
@@ -134,7 +147,6 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_kernel(
   const int row = tid >> 1, h = tid & 1;
   const int r = r0 + row;
   const int rr = min(r, R - 1);
-  const int target = tgt != nullptr ? (int)tgt[(int64_t)rr * tgt_stride] : -1;
   const float* Crow = C + row * VTile::CSTRIDE;
   // pass 1: max and first argmax
   float m = -INFINITY;
@@ -341,40 +353,83 @@ __global__ __launch_bounds__(256) void vocab_combine_kernel(
   }
 }
 
+// DS_ROWS rows of the [T*R][ldl] buffer per block.  Each thread owns the same
+// 8-column chunks in every row, so the bias gradient (column sums of dS) is
+// accumulated in registers and written once per block as a partial row.
+constexpr int DS_ROWS = 64, DS_MAXCH = 8;  // V <= DS_MAXCH * 2048
+
 __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
     uint16_t* __restrict__ buf, int64_t ldl, int V, int R, int T, int T_sel,
     const float* __restrict__ lse, const int64_t* __restrict__ y_sel, int64_t ysel_rs,
     const float* __restrict__ dg_sel, int64_t dgsel_rs, const int64_t* __restrict__ y_xe,
-    int64_t yxe_rs, const float* __restrict__ dg_xe, int64_t dgxe_rs) {
-  // one block per (t, r) row of the [T][R][ldl] buffer
-  const int64_t rowid = blockIdx.x;
-  const int t = (int)(rowid / R), r = (int)(rowid % R);
-  const bool has_sel = dg_sel != nullptr && t < T_sel;
-  const float a = has_sel ? dg_sel[(int64_t)r * dgsel_rs + t] : 0.f;
-  const float bb = dg_xe ? dg_xe[(int64_t)r * dgxe_rs + t] : 0.f;
-  const int ys = has_sel ? (int)y_sel[(int64_t)r * ysel_rs + t] : -1;
-  const int yx = dg_xe ? (int)y_xe[(int64_t)r * yxe_rs + t] : -1;
-  const float L = lse[rowid];
-  const float ab = a + bb;
-  uint16_t* row = buf + rowid * ldl;
+    int64_t yxe_rs, const float* __restrict__ dg_xe, int64_t dgxe_rs,
+    float* __restrict__ colsum_part) {
+  const int64_t nrows = (int64_t)T * R;
+  const int64_t row0 = (int64_t)blockIdx.x * DS_ROWS;
   const int nvec = V >> 3;
-  for (int i = threadIdx.x; i < nvec; i += 256) {
-    uint4 x = *reinterpret_cast<const uint4*>(row + i * 8);
-    uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+  float cs[DS_MAXCH][8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int v = i * 8 + 2 * k;
-      float lo = -ab * __expf(h2f(ws[k] & 0xffff) - L);
-      float hi = -ab * __expf(h2f(ws[k] >> 16) - L);
-      lo += (v == ys ? a : 0.f) + (v == yx ? bb : 0.f);
-      hi += (v + 1 == ys ? a : 0.f) + (v + 1 == yx ? bb : 0.f);
-      ws[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  for (int c = 0; c < DS_MAXCH; ++c)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs[c][k] = 0.f;
+  for (int rr = 0; rr < DS_ROWS; ++rr) {
+    const int64_t rowid = row0 + rr;
+    if (rowid >= nrows) break;
+    const int t = (int)(rowid / R), r = (int)(rowid % R);
+    const bool has_sel = dg_sel != nullptr && t < T_sel;
+    const float a = has_sel ? dg_sel[(int64_t)r * dgsel_rs + t] : 0.f;
+    const float bb = dg_xe ? dg_xe[(int64_t)r * dgxe_rs + t] : 0.f;
+    const int ys = has_sel ? (int)y_sel[(int64_t)r * ysel_rs + t] : -1;
+    const int yx = dg_xe ? (int)y_xe[(int64_t)r * yxe_rs + t] : -1;
+    const float L = lse[rowid];
+    const float ab = a + bb;
+    uint16_t* row = buf + rowid * ldl;
+#pragma unroll
+    for (int c = 0; c < DS_MAXCH; ++c) {
+      const int i = threadIdx.x + c * 256;
+      if (i < nvec) {
+        uint4 x = *reinterpret_cast<const uint4*>(row + i * 8);
+        uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int v = i * 8 + 2 * k;
+          float lo = -ab * __expf(h2f(ws[k] & 0xffff) - L);
+          float hi = -ab * __expf(h2f(ws[k] >> 16) - L);
+          lo += (v == ys ? a : 0.f) + (v == yx ? bb : 0.f);
+          hi += (v + 1 == ys ? a : 0.f) + (v + 1 == yx ? bb : 0.f);
+          const uint16_t blo = f2bf(lo), bhi = f2bf(hi);
+          cs[c][2 * k] += bf2f(blo);  // sum what the GEMMs see (bf16 dS)
+          cs[c][2 * k + 1] += bf2f(bhi);
+          ws[k] = (uint32_t)blo | ((uint32_t)bhi << 16);
+        }
+        *reinterpret_cast<uint4*>(row + i * 8) = make_uint4(ws[0], ws[1], ws[2], ws[3]);
+      }
     }
-    *reinterpret_cast<uint4*>(row + i * 8) = make_uint4(ws[0], ws[1], ws[2], ws[3]);
+    if (threadIdx.x < (V & 7)) {  // ragged tail columns
+      const int v = (nvec << 3) + threadIdx.x;
+      const float d = -ab * __expf(h2f(row[v]) - L) + (v == ys ? a : 0.f) + (v == yx ? bb : 0.f);
+      row[v] = f2bf(d);  // column sum added after the row loop
+    }
   }
-  for (int v = (nvec << 3) + threadIdx.x; v < V; v += 256) {
-    float d = -ab * __expf(h2f(row[v]) - L) + (v == ys ? a : 0.f) + (v == yx ? bb : 0.f);
-    row[v] = f2bf(d);
+  float* out = colsum_part + (int64_t)blockIdx.x * V;
+#pragma unroll
+  for (int c = 0; c < DS_MAXCH; ++c) {
+    const int i = threadIdx.x + c * 256;
+    if (i < nvec) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) out[i * 8 + k] = cs[c][k];
+    }
+  }
+  // tail columns: re-sum from the (already converted) buffer
+  if (threadIdx.x < (V & 7)) {
+    const int v = (nvec << 3) + threadIdx.x;
+    float acc = 0.f;
+    for (int rr = 0; rr < DS_ROWS; ++rr) {
+      const int64_t rowid = row0 + rr;
+      if (rowid >= nrows) break;
+      acc += bf2f(buf[rowid * ldl + v]);
+    }
+    out[v] = acc;
   }
 }
 
@@ -442,13 +497,16 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                      counts, count_step, unfinished);
 }
 
+int vocab_bwd_ds_blocks(int T, int R) { return (int)(((int64_t)T * R + DS_ROWS - 1) / DS_ROWS); }
+
 void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
                          const float* lse, const int64_t* y_sel, int64_t ysel_rs,
                          const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
-                         int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, hipStream_t stream) {
-  hipLaunchKernelGGL(vocab_bwd_ds_kernel, dim3((unsigned)((int64_t)T * R)), dim3(256), 0, stream,
+                         int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
+                         hipStream_t stream) {
+  hipLaunchKernelGGL(vocab_bwd_ds_kernel, dim3(vocab_bwd_ds_blocks(T, R)), dim3(256), 0, stream,
                      buf, ldl, V, R, T, T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe,
-                     yxe_rs, dg_xe, dgxe_rs);
+                     yxe_rs, dg_xe, dgxe_rs, colsum_part);
 }
 
 }  // namespace cst

@@ -34,20 +34,22 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
                           float ss_prob, uint32_t seed, int step, int* counts, int count_step,
                           uint8_t* unfinished, hipStream_t stream);
+int vocab_bwd_ds_blocks(int T, int R);
 void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
                          const float* lse, const int64_t* y_sel, int64_t ysel_rs,
                          const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
-                         int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, hipStream_t stream);
+                         int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
+                         hipStream_t stream);
 
 // lstm.hip
-void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* emb, int E,
-                          int n_emb_rows, const uint16_t* h_prev, const float* c_prev, const float* vgate,
-                          int vgate_div, int R, int H, const uint16_t* wx, uint16_t* h_out,
+void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
+                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
+                          int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
-                          uint32_t seed, int step, float* gates_out, hipStream_t stream);
+                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream);
 void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
-                          const float* gates, const float* c_t, const float* c_prev, int R, int H,
-                          float drop_p, uint32_t seed, int step, uint16_t* dG,
+                          const uint16_t* gates, const float* c_t, const float* c_prev, int R,
+                          int H, float drop_p, uint32_t seed, int step, uint16_t* dG,
                           hipStream_t stream);
 
 }  // namespace cst

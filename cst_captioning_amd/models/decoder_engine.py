@@ -53,7 +53,7 @@ class _DecoderFn(torch.autograd.Function):
                 ss_prob, drop_p, temperature, seed, vdiv, want_xe, use_counts, use_unfinished,
                 save):
         outs = _ext.ops().decoder_forward(
-            eng.wx, eng.emb, eng.wlog, logit_b.detach().float().contiguous(),
+            eng.wx, eng.emb, eng.ptab, eng.whh, eng.wlog, logit_b.detach().float().contiguous(),
             vgate.detach().float().contiguous(), vdiv,
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
@@ -131,8 +131,12 @@ class DecoderEngine:
         w_hh = m.core.rnn.weight_hh_l0
         self.wx = torch.cat([w_ih[:, :E], w_hh], 1).index_select(0, self.perm) \
             .to(torch.bfloat16).contiguous()
+        self.whh = self.wx[:, E:].contiguous()
         self.emb = m.embed.weight.detach().to(torch.bfloat16).contiguous()
         self.wlog = m.logit.weight.detach().to(torch.bfloat16).contiguous()
+        # input-token gate table P = emb . W_ie^T (V x 4H, packed gate order):
+        # one GEMM per optimizer step instead of K=E of work in every decode step
+        self.ptab = torch.mm(self.emb, self.wx[:, :E].t(), out_dtype=torch.float32)
 
     def attach_optimizer(self, trainer):
         self.refresh_weights()  # params were re-homed into the flat buffer

@@ -19,6 +19,8 @@ vg = torch.randn(64, 4 * H, device=dev) * 0.1
 labels = torch.randint(3, V, (R, L), device=dev)
 labels[:, 0] = 1
 bos = torch.ones(R, dtype=torch.long, device=dev)
+whh = wx[:, E:].contiguous()
+ptab = torch.mm(emb, wx[:, :E].t(), out_dtype=torch.float32)
 res = {}
 import os
 variants = [int(x) for x in os.environ.get('VARIANTS', '0').split(',')]
@@ -28,7 +30,7 @@ for var in variants:
                                 ('sample_nosave', [1] * (T - 1), False, 0.0),
                                 ('sample_save_drop', [1] * (T - 1), True, 0.5),
                                 ('gt_save_drop', [0] * (T - 1), True, 0.5)]:
-    args = lambda: C.decoder_forward(wx, emb, wlog, blog, vg, 20, labels, bos, R, T, modes, 0.0,
+    args = lambda: C.decoder_forward(wx, emb, ptab, whh, wlog, blog, vg, 20, labels, bos, R, T, modes, 0.0,
                                      drop, 1.0, 7, save, False, True, False)
     for _ in range(3):
         args()
