@@ -160,10 +160,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     const bool choose = t < T - 1;
     const int mode = choose ? (int)modes[t] : SEL_GT_H;
     const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
+    const int vflags = do_sample | ((choose && mode == SEL_GREEDY_H) ? 2 : 0);
     const int64_t* tgt = (have_labels && t + 1 < L) ? LAB + (t + 1) : nullptr;
     launch_vocab_fwd(vin, ldh, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
                      save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
-                     part.data_ptr(), tgt, L, do_sample, inv_temp, seed_samp, (int)t, st);
+                     part.data_ptr(), tgt, L, vflags, inv_temp, seed_samp, (int)t, st);
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                          choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
                          choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,

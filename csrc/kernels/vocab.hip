@@ -253,6 +253,245 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_kernel(
   }
 }
 
+// -------------------------------------------------------------------------------
+// Transposed-epilogue variant: the MFMA computes C^T = W . h_drop^T (vocab rows
+// as the M operand, caption rows as N).  In the 32x32 MFMA output layout lane l
+// then holds, for caption row (l & 31) of each 32-row sub-tile, 16 vocabulary
+// entries per 32-vocab sub-tile: the lane's 32 (TM = 2) logits of one row sit
+// in its own registers.  Every per-row statistic (max, sum exp, argmax, target
+// logit, inverse-CDF draw) is a register loop with no LDS C tile and no
+// shuffles; only the 4 lane groups that share a row (2 half-waves x 2 vocab
+// waves) are merged, through 16 KB of LDS, once per block.
+//
+// Sampling stays exact: each group draws inside its own 32 weights by inverse
+// CDF and enters an exponential race with key m/temp + log(mass) - log(E)
+// (E ~ Exp(1)); the race continues across the 4 groups here and across vocab
+// tiles in vocab_combine_kernel, and the union of independent races is the
+// race over all of V.
+constexpr int VT_V = 128;  // vocab entries per block
+enum VocabFlags : int { VF_SAMPLE = 1, VF_ARGMAX = 2 };
+
+struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS
+  float m, s, zkey, zlogit;
+  int zidx, xidx;
+  float xt, pad;
+};
+
+template <int BN, int STAGES, int OCC>
+__global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(
+    const uint16_t* __restrict__ hd, int ldh, int R, int H, const uint16_t* __restrict__ W,
+    const float* __restrict__ bias, int V, uint16_t* __restrict__ logits16, int64_t ldl,
+    VocabPartial* __restrict__ part, const int64_t* __restrict__ tgt, int64_t tgt_stride,
+    int flags, float inv_temp, uint32_t seed, int step) {
+  using TL = Tile<VT_V, BN, STAGES>;  // M = vocab, N = caption rows
+  constexpr int TM = TL::TM, TN = TL::TN;
+  static_assert(TM == 2, "lane owns 32 vocab entries per row");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
+  const int b = xcd_remap(blockIdx.x, n_vt * n_rt);
+  const int vt = b / n_rt, rt = b % n_rt;
+  const int v0 = vt * VT_V, r0 = rt * BN;
+  const int nk = H / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  const int half = lane >> 5;
+  // the lane's vocab entries: vb + 32 i + 8 q + e   (i < TM, q < 4, e < 4)
+  const int vb = v0 + wr * TL::WM + 4 * half;
+
+  // epilogue operands prefetched before the main loop; columns past V get a
+  // -inf bias so they vanish from every statistic
+  float pb[TM][16];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int v = vb + 32 * i + 8 * q;
+      if (v + 4 <= V) {
+        const float4 x = *reinterpret_cast<const float4*>(bias + v);
+        pb[i][4 * q] = x.x, pb[i][4 * q + 1] = x.y, pb[i][4 * q + 2] = x.z, pb[i][4 * q + 3] = x.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pb[i][4 * q + e] = v + e < V ? bias[v + e] : -INFINITY;
+      }
+    }
+  int tg[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int r = min(r0 + wc * TL::WN + 32 * j + (lane & 31), R - 1);
+    tg[j] = tgt != nullptr ? (int)tgt[(int64_t)r * tgt_stride] : -1;
+  }
+
+  f32x16 acc[TM][TN];
+  {
+    DmaSrc<VT_V / 32> a;
+    DmaSrc<BN / 32> bsrc;
+    a.r0 = a.r1 = make_rsrc(W, (int64_t)V * H * 2);
+    a.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < VT_V / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      a.voff0[i] = min(v0 + row, V - 1) * H * 2 + dma_chunk(row, lane) * 16;
+      a.voff1[i] = a.voff0[i];
+    }
+    bsrc.r0 = bsrc.r1 = make_rsrc(hd, (int64_t)R * ldh * 2);
+    bsrc.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < BN / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      bsrc.voff0[i] = min(r0 + row, R - 1) * ldh * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff1[i] = bsrc.voff0[i];
+    }
+    gemm_nt_mainloop<TL>(nk, a, bsrc, lds, acc);
+  }
+
+  GroupStat* gs = reinterpret_cast<GroupStat*>(lds);  // [4 groups][BN rows]
+  const int g = wr * 2 + half;
+  const bool temp1 = inv_temp == 1.f;
+  constexpr float L2E = 1.4426950408889634f;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int row_l = wc * TL::WN + 32 * j + (lane & 31);
+    const int r = r0 + row_l;
+    float x[TM][16];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[i][k] = acc[i][j][k] + pb[i][k];
+
+    if (logits16 != nullptr && r < R) {
+      uint16_t* dst = logits16 + (int64_t)r * ldl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int v = vb + 32 * i + 8 * q;
+          if (v + 4 <= V) {
+            uint2 pk;
+            pk.x = (uint32_t)f2h(x[i][4 * q]) | ((uint32_t)f2h(x[i][4 * q + 1]) << 16);
+            pk.y = (uint32_t)f2h(x[i][4 * q + 2]) | ((uint32_t)f2h(x[i][4 * q + 3]) << 16);
+            *reinterpret_cast<uint2*>(dst + v) = pk;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (v + e < V) dst[v + e] = f2h(x[i][4 * q + e]);
+          }
+        }
+    }
+
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m = fmaxf(m, x[i][k]);
+    const float msafe = m == -INFINITY ? 0.f : m;
+    const float ml = msafe * L2E;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += __builtin_amdgcn_exp2f(fmaf(x[i][k], L2E, -ml));
+
+    GroupStat st;
+    st.m = m;
+    st.s = s;
+    st.pad = 0.f;
+    st.xidx = 0x7fffffff;
+    if (flags & VF_ARGMAX) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int v = vb + 32 * i + 8 * (k >> 2) + (k & 3);
+          st.xidx = min(st.xidx, x[i][k] == m ? v : 0x7fffffff);
+        }
+    }
+    st.xt = -INFINITY;
+    if (tgt != nullptr) {
+      const int d = tg[j] - vb;
+      const bool mine = d >= 0 && d < 32 * TM && (d & 4) == 0;
+      const int kk = mine ? (d >> 5) * 16 + ((d >> 3) & 3) * 4 + (d & 3) : -1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) st.xt = (i * 16 + k == kk) ? x[i][k] : st.xt;
+    }
+    st.zkey = -INFINITY;
+    st.zlogit = 0.f;
+    st.zidx = 0x7fffffff;
+    if (flags & VF_SAMPLE) {
+      const float wl = msafe * inv_temp * L2E, wsc = inv_temp * L2E;
+      float sw = s;
+      if (!temp1) {
+        sw = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) sw += __builtin_amdgcn_exp2f(fmaf(x[i][k], wsc, -wl));
+      }
+      const uint32_t rr = (uint32_t)min(r, R - 1);
+      const uint32_t key = mix32(seed ^ mix32(rr * 0x9E3779B1u + (uint32_t)step * 0x85EBCA77u) ^
+                                 (uint32_t)(vt * 4 + g) * 0xC2B2AE3Du);
+      const float u = ((float)(key >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      const float tm = u * sw;
+      // inverse CDF in the same summation order as sw, so the last positive
+      // weight always satisfies cum >= tm
+      float cum = 0.f, cl = 0.f;
+      int cand = -1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const float wv = temp1 ? __builtin_amdgcn_exp2f(fmaf(x[i][k], L2E, -ml))
+                                 : __builtin_amdgcn_exp2f(fmaf(x[i][k], wsc, -wl));
+          cum += wv;
+          const bool hit = cand < 0 && cum >= tm && wv > 0.f;
+          cand = hit ? vb + 32 * i + 8 * (k >> 2) + (k & 3) : cand;
+          cl = hit ? x[i][k] : cl;
+        }
+      if (sw > 0.f && cand >= 0) {
+        const uint32_t key2 = mix32(key ^ 0x68E31DA4u);
+        const float u2 = ((float)(key2 >> 8) + 0.5f) * (1.0f / 16777216.0f);
+        st.zkey = msafe * inv_temp + __logf(sw) - __logf(-__logf(u2));
+        st.zidx = cand;
+        st.zlogit = cl;
+      }
+    }
+    gs[g * BN + row_l] = st;
+  }
+  __syncthreads();
+  // merge the 4 lane groups of each row -> one VocabPartial per (tile, row)
+  if (threadIdx.x < BN) {
+    const int row_l = threadIdx.x, r = r0 + row_l;
+    if (r < R) {
+      GroupStat a = gs[row_l];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        const GroupStat c = gs[q * BN + row_l];
+        const float M = fmaxf(a.m, c.m);
+        a.s = (a.m == -INFINITY ? 0.f : a.s * __expf(a.m - M)) +
+              (c.m == -INFINITY ? 0.f : c.s * __expf(c.m - M));
+        if (c.m > a.m || (c.m == a.m && c.xidx < a.xidx)) a.xidx = c.xidx;
+        a.m = M;
+        if (c.zkey > a.zkey || (c.zkey == a.zkey && c.zidx < a.zidx)) {
+          a.zkey = c.zkey;
+          a.zidx = c.zidx;
+          a.zlogit = c.zlogit;
+        }
+        a.xt = fmaxf(a.xt, c.xt);
+      }
+      VocabPartial p;
+      p.m = a.m;
+      p.s = a.s;
+      p.zval = a.zkey;
+      p.zlogit = a.zlogit;
+      p.zidx = a.zidx;
+      p.xidx = a.xidx;
+      p.xtgt = a.xt;
+      p.pad = 0.f;
+      part[(int64_t)vt * R + r] = p;
+    }
+  }
+}
+
 // token-selection modes of one decode step
 enum SelMode : int { SEL_GT = 0, SEL_SAMPLE = 1, SEL_GREEDY = 2, SEL_SS = 3 };
 
@@ -436,9 +675,10 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
 // -------------------------------------------------------------------------------
 // Tile-shape variants (A/B-tested on MI355X, see profiles/); the partial
 // record layout depends on the vocab tile width, so the choice is global.
-static int g_vocab_variant = 0;
+static int g_vocab_variant = 4;  // transposed epilogue (fastest on MI355X, profiles/)
 void set_vocab_variant(int v) { g_vocab_variant = v; }
 static int vocab_bn() { return g_vocab_variant == 1 || g_vocab_variant == 3 ? 64 : 128; }
+static bool vocab_tr() { return g_vocab_variant >= 4; }
 
 template <int BN, int STAGES, int OCC>
 static void launch_vocab_fwd_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
@@ -459,11 +699,45 @@ static void launch_vocab_fwd_t(const uint16_t* hd, int ldh, int R, int H, const 
                      (VocabPartial*)part, tgt, tgt_stride, do_sample, inv_temp, seed, step);
 }
 
+template <int BN, int STAGES, int OCC>
+static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                                const float* bias, int V, uint16_t* logits16, int64_t ldl,
+                                void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
+                                float inv_temp, uint32_t seed, int step, hipStream_t stream) {
+  using TL = Tile<VT_V, BN, STAGES>;
+  constexpr int LDS = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
+                          ? TL::STAGES * TL::STAGE_BYTES
+                          : 4 * BN * (int)sizeof(GroupStat);
+  const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)vocab_fwd_tr_kernel<BN, STAGES, OCC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((vocab_fwd_tr_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256), LDS,
+                     stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt,
+                     tgt_stride, flags, inv_temp, seed, step);
+}
+
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                       const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
-                      const int64_t* tgt, int64_t tgt_stride, int do_sample, float inv_temp,
+                      const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                       uint32_t seed, int step, hipStream_t stream) {
+  const int do_sample = flags & VF_SAMPLE;
   switch (g_vocab_variant) {
+    case 4:  // transposed epilogue, 128 vocab x 128 rows, 2 stages (64 KB, 2 blocks/CU)
+      launch_vocab_fwd_tr<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                     tgt_stride, flags, inv_temp, seed, step, stream);
+      break;
+    case 5:  // transposed epilogue, 128 vocab x 64 rows, 3 stages (72 KB, 2 blocks/CU)
+      launch_vocab_fwd_tr<64, 3, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                    tgt_stride, flags, inv_temp, seed, step, stream);
+      break;
+    case 6:  // transposed epilogue, 128 vocab x 64 rows, 2 stages (48 KB)
+      launch_vocab_fwd_tr<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                    tgt_stride, flags, inv_temp, seed, step, stream);
+      break;
     case 1:  // 128x64 tile, 3 stages (72 KB LDS, 2 blocks/CU)
       launch_vocab_fwd_t<64, 3, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
                                    tgt_stride, do_sample, inv_temp, seed, step, stream);
@@ -482,7 +756,10 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
   }
 }
 
-int vocab_num_tiles(int V) { return (V + vocab_bn() - 1) / vocab_bn(); }
+int vocab_num_tiles(int V) {
+  const int bn = vocab_tr() ? VT_V : vocab_bn();
+  return (V + bn - 1) / bn;
+}
 int vocab_partial_bytes() { return (int)sizeof(VocabPartial); }
 
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,

@@ -27,8 +27,8 @@ int vocab_partial_bytes();
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                       const float* bias,
                       int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
-                      int64_t tgt_stride, int do_sample, float inv_temp, uint32_t seed, int step,
-                      hipStream_t stream);
+                      int64_t tgt_stride, int flags, float inv_temp, uint32_t seed, int step,
+                      hipStream_t stream);  // flags: 1 = sample, 2 = argmax
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,

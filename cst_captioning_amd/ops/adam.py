@@ -62,10 +62,7 @@ class FlatAdam:
         norm = torch.linalg.vector_norm(g)
         self.last_norm = norm
         coef = torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0)
-        if skip is not None:
-            keep = (~skip).float()
-        else:
-            keep = None
+        keep = None if skip is None else ~skip
         gc = g * coef
         m_new = self.exp_avg * b1 + gc * (1 - b1)
         v_new = self.exp_avg_sq * b2 + gc * gc * (1 - b2)
@@ -76,9 +73,10 @@ class FlatAdam:
             self.exp_avg_sq.copy_(v_new)
             p.sub_(upd)
         else:
-            self.exp_avg.copy_(torch.lerp(self.exp_avg, m_new, keep))
-            self.exp_avg_sq.copy_(torch.lerp(self.exp_avg_sq, v_new, keep))
-            p.sub_(upd * keep)
+            # torch.where, not a 0/1 multiply: NaN * 0 is NaN
+            self.exp_avg.copy_(torch.where(keep, m_new, self.exp_avg))
+            self.exp_avg_sq.copy_(torch.where(keep, v_new, self.exp_avg_sq))
+            p.copy_(torch.where(keep, p - upd, p))
         return norm
 
     def state_dict(self):

@@ -1,0 +1,62 @@
+"""Worker for tests/test_dist.py, launched by torchrun (gloo on CPU, or RCCL
+on GPUs): one XE gradient all-reduce, two optimizer steps, and a sharded
+validation.  Writes rank 0's results to ``argv[1]`` (torch.save)."""
+import sys
+
+import torch
+
+from cst_captioning_amd.cli import build_model, load_splits
+from cst_captioning_amd.config import parse_opts
+from cst_captioning_amd.data import CaptionLoader
+from cst_captioning_amd.parallel import init_distributed
+from cst_captioning_amd.train.trainer import Trainer
+
+ARGS = ['--synthetic', 'msvd', '--synthetic_videos', '24', '--synthetic_vocab', '40',
+        '--seq_length', '10', '--rnn_size', '32', '--input_encoding_size', '32',
+        '--feat_dims', '16', '8', '--batch_size', '4', '--train_seq_per_img', '3',
+        '--test_batch_size', '3', '--test_seq_per_img', '3', '--beam_size', '2',
+        '--impl', 'torch', '--loglevel', 'WARNING', '--drop_prob_lm', '0',
+        '--learning_rate', '1e-3', '--language_eval', '0']
+
+
+def build(rank, world, device):
+    opt = parse_opts(ARGS)
+    torch.manual_seed(1234 + rank)  # different init per rank: broadcast must fix it
+    tr, va, _ = load_splits(opt)
+    loader = CaptionLoader(tr, opt.batch_size, opt.train_seq_per_img, 'train', device,
+                           rank, world, opt.seed)
+    opt.vocab, opt.vocab_size = loader.get_vocab(), loader.get_vocab_size()
+    opt.seq_length, opt.feat_dims = loader.get_seq_length(), loader.get_feat_dims()
+    model, engine = build_model(opt, device)
+    val = CaptionLoader(va, opt.test_batch_size, opt.test_seq_per_img, 'test', device)
+    return opt, model, engine, loader, val
+
+
+def main(out):
+    ctx = init_distributed()
+    opt, model, engine, loader, val = build(ctx.rank, ctx.world_size, ctx.device)
+    tr = Trainer(opt, model, loader, val, ctx, engine)  # C1 broadcast happens here
+    init = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+    res = tr.validate(val)  # C4, on the broadcast initial weights
+    # one all-reduced XE gradient
+    data = loader.get_batch()
+    tr.optimizer.zero_grad()
+    loss, _ = tr.xe_loss(data)
+    loss.backward()
+    tr.bucket.all_reduce(ctx)
+    grad = tr.bucket.grad.detach().cpu().clone()
+    # two full steps: parameters must stay identical on every rank
+    for _ in range(2):
+        tr.train_step(loader.get_batch(), 0)
+    flat = tr.bucket.data.detach().cpu().clone()
+    allp = ctx.all_gather_object(flat)
+    same = all(torch.equal(allp[0], p) for p in allp)
+    if ctx.is_main:
+        torch.save({'init': init, 'grad': grad, 'same_after_steps': same,
+                    'predictions': res['predictions'], 'loss': res['scores']['Loss'],
+                    'world': ctx.world_size}, out)
+    ctx.destroy()
+
+
+if __name__ == '__main__':
+    main(sys.argv[1])

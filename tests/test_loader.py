@@ -1,0 +1,121 @@
+"""CaptionLoader semantics (``/root/reference/dataloader.py:83-170``):
+caption selection for ncap <, =, > seq_per_img, masks (+1 for EOS), epoch
+wrap and shuffle, DP sharding, evaluation batches, state round trip, and the
+on-disk label/feature formats."""
+import numpy as np
+import pytest
+import torch
+
+from cst_captioning_amd.data import CaptionLoader, VideoCaptionDataset
+from cst_captioning_amd.data.formats import (load_feature_file, load_label_file,
+                                             save_feature_file, save_label_file)
+from cst_captioning_amd.data.synthetic import make_synthetic
+from cst_captioning_amd.prepro.labels import build_label_store
+
+
+def _tiny_ds(ncaps=(2, 3, 5), L=6):
+    vocab = ['<end>', '<start>', '<unk>'] + ['w%d' % i for i in range(10)]
+    videos = []
+    for i, n in enumerate(ncaps):
+        toks = [['w%d' % ((i + j) % 10)] * (1 + j % 3) for j in range(n)]
+        videos.append({'video_id': 100 + i, 'captions': [' '.join(t) for t in toks],
+                       'processed_tokens': toks})
+    st = build_label_store(vocab, videos, L)
+    feats = [np.arange(len(ncaps) * 4, dtype=np.float32).reshape(len(ncaps), 1, 4)]
+    return VideoCaptionDataset(vocab, st['videos'], feats, st['labels'], st['label_start_ix'],
+                               st['label_end_ix'])
+
+
+def test_caption_selection_and_masks():
+    ds = _tiny_ds()
+    S = 3
+    ld = CaptionLoader(ds, batch_size=3, seq_per_img=S, mode='test')
+    d = ld.get_batch()
+    assert d['labels'].shape == (9, 6)
+    for b, v in enumerate(d['vids']):
+        s, e = ds.label_start_ix[v], ds.label_end_ix[v]
+        rows = d['labels'][b * S:(b + 1) * S].numpy()
+        allc = ds.labels[s:e]
+        ncap = e - s
+        if ncap <= S:
+            # all captions first, in order, then random repeats
+            np.testing.assert_array_equal(rows[:ncap], allc)
+            for r in rows[ncap:]:
+                assert any((r == c).all() for c in allc)
+        else:
+            # a random subset without repetition
+            idx = [int(np.where((allc == r).all(1))[0][0]) for r in rows]
+            assert len(set(idx)) == len(idx)
+    # mask: nonzero tokens + 1 (the EOS)
+    n = (d['labels'] != 0).sum(1) + 1
+    for i in range(9):
+        assert d['masks'][i, :n[i]].eq(1).all() and d['masks'][i, n[i]:].eq(0).all()
+    assert len(d['gts']) == 3 and d['gts'][0].shape[1] == 6
+
+
+def test_epoch_wrap_and_shuffle():
+    ds = make_synthetic('msvd', num_videos=10, vocab_size=40, seq_length=8, seed=0)
+    ld = CaptionLoader(ds, batch_size=4, seq_per_img=2, mode='train', seed=5)
+    seen = []
+    for _ in range(5):  # 20 videos = 2 epochs
+        seen.extend(ld.get_batch()['vids'].tolist())
+    assert ld.get_current_epoch() == 2
+    assert sorted(seen[:10]) == list(range(10)) and sorted(seen[10:]) == list(range(10))
+    assert seen[:10] != seen[10:]  # reshuffled
+
+
+def test_dp_shards_are_disjoint_and_cover_global_batch():
+    ds = make_synthetic('msvd', num_videos=24, vocab_size=40, seq_length=8, seed=0)
+    ref = CaptionLoader(ds, batch_size=8, seq_per_img=2, seed=9)
+    shards = [CaptionLoader(ds, batch_size=4, seq_per_img=2, rank=r, world_size=2, seed=9)
+              for r in range(2)]
+    for _ in range(4):
+        g = ref.get_batch()['vids'].tolist()
+        parts = [s.get_batch()['vids'].tolist() for s in shards]
+        assert parts[0] + parts[1] == g
+    assert all(s.get_current_epoch() == ref.get_current_epoch() for s in shards)
+
+
+def test_eval_batches_truncate_last():
+    ds = make_synthetic('msvd', num_videos=10, vocab_size=40, seq_length=8, seed=0)
+    ld = CaptionLoader(ds, batch_size=4, seq_per_img=1, mode='test')
+    got = [ld.get_batch_at(i)['vids'].tolist() for i in range(3)]
+    assert got == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+
+
+def test_state_dict_roundtrip():
+    ds = make_synthetic('msvd', num_videos=12, vocab_size=40, seq_length=8, seed=0)
+    a = CaptionLoader(ds, batch_size=5, seq_per_img=3, seed=2)
+    a.get_batch()
+    st = a.state_dict()
+    x = a.get_batch()
+    b = CaptionLoader(ds, batch_size=5, seq_per_img=3, seed=77)
+    b.load_state_dict(st)
+    y = b.get_batch()
+    assert x['vids'].tolist() == y['vids'].tolist()
+    assert torch.equal(x['labels'], y['labels'])
+
+
+def test_label_and_feature_files_roundtrip(tmp_path):
+    ds = _tiny_ds()
+    st = {'labels': ds.labels, 'label_start_ix': ds.label_start_ix,
+          'label_end_ix': ds.label_end_ix, 'videos': [str(v) for v in ds.video_ids],
+          'vocab': list(ds.vocab)}
+    p = save_label_file(str(tmp_path / 'lab.npz'), st)
+    back = load_label_file(p)
+    np.testing.assert_array_equal(back['labels'], ds.labels)
+    assert back['vocab'] == list(ds.vocab)
+    feats = np.random.RandomState(0).rand(3, 4).astype(np.float32)
+    fp = save_feature_file(str(tmp_path / 'f.npz'), ['102', '100', '101'], feats)
+    arr = load_feature_file(fp, ['100', '101', '102'], num_chunks=2)
+    assert arr.shape == (3, 2, 4)
+    np.testing.assert_array_equal(arr[0, 0], feats[1])
+    np.testing.assert_array_equal(arr[2, 1], feats[0])
+
+
+def test_h5_without_h5py_is_a_clear_error(tmp_path):
+    from cst_captioning_amd.data import formats
+    if formats.HAVE_H5PY:
+        pytest.skip('h5py installed')
+    with pytest.raises(RuntimeError, match='h5py'):
+        load_label_file(str(tmp_path / 'x.h5'))
