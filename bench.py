@@ -53,6 +53,8 @@ def parse():
     p.add_argument('--vocab', type=int, default=10509)
     p.add_argument('--seed', type=int, default=123)
     p.add_argument('--json_out', default='')
+    p.add_argument('--sync_debug', type=int, default=0,
+                   help='after warmup: report host-synchronising calls and host enqueue time of one step')
     return p.parse_args()
 
 
@@ -100,6 +102,21 @@ def main():
     for _ in range(a.warmup):
         out = step()
     sync()
+    if a.sync_debug and dev.type == 'cuda':
+        import warnings
+        warnings.simplefilter('always')
+        torch.cuda.set_sync_debug_mode('warn')
+        th = time.perf_counter()
+        step()
+        th = time.perf_counter() - th
+        torch.cuda.set_sync_debug_mode(0)
+        sync()
+        tg = time.perf_counter()
+        step()
+        sync()
+        tg = time.perf_counter() - tg
+        print('sync_debug: host enqueue %.3f ms, synced step %.3f ms' % (th * 1e3, tg * 1e3),
+              file=sys.stderr, flush=True)
     ctx.barrier()
     sync()
     t0 = time.perf_counter()

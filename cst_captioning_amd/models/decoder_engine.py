@@ -44,7 +44,8 @@ def engine_supports(opt):
     return (getattr(opt, 'rnn_type', 'lstm') == 'lstm' and getattr(opt, 'num_layers', 1) == 1
             and getattr(opt, 'model_type', 'concat') == 'concat'
             and getattr(opt, 'num_chunks', 1) == 1
-            and opt.input_encoding_size % 64 == 0 and opt.rnn_size % 64 == 0)
+            and opt.input_encoding_size % 64 == 0 and opt.input_encoding_size <= 1024
+            and opt.rnn_size % 64 == 0)
 
 
 class _DecoderFn(torch.autograd.Function):
@@ -87,7 +88,7 @@ class _DecoderFn(torch.autograd.Function):
         # input token of every step: it_0 = BOS / labels[:, 0], it_t = seq[:, t-1]
         first = labels[:, :1] if labels is not None else bos.view(-1, 1)
         toks = torch.cat([first, seq[:, :n_steps - 1]], 1).t().reshape(-1)
-        dWx, dWlog, dblog, dX, dvg = _ext.ops().decoder_backward(
+        dWx, dWlog, dblog, d_emb, dvg = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
@@ -98,8 +99,6 @@ class _DecoderFn(torch.autograd.Function):
         d_wih = torch.zeros(w_ih_shape, dtype=torch.float32, device=dWx.device)
         d_wih[:, :E] = d_orig[:, :E]
         d_whh = d_orig[:, E:].contiguous()
-        d_emb = torch.zeros(emb_shape, dtype=torch.float32, device=dWx.device)
-        d_emb.index_add_(0, toks, dX)
         nv = R // vdiv
         d_vgate = dvg.view(nv, vdiv, -1).sum(1)
         return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 15

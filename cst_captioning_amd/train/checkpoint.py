@@ -57,12 +57,20 @@ def last_path(model_file):
         else model_file + '_last.pth'
 
 
-def save_last(path, model, optimizer, infos, opt, loader, rng_extra=None):
+def rng_state(extra=None):
+    return {'torch': torch.get_rng_state(), 'numpy': np.random.get_state(),
+            'cuda': torch.cuda.get_rng_state_all() if torch.cuda.is_available() else None,
+            'extra': extra}
+
+
+def save_last(path, model, optimizer, infos, opt, loader, rng_extra=None, per_rank=None):
+    """``per_rank``: optional list (one entry per DP rank) of
+    ``{'loader': state, 'rng': state}``; rank r resumes from entry r."""
     state = {'model': model.state_dict(), 'infos': infos, 'opt': opt,
              'optimizer': optimizer.state_dict(), 'loader': loader.state_dict(),
-             'rng': {'torch': torch.get_rng_state(), 'numpy': np.random.get_state(),
-                     'cuda': torch.cuda.get_rng_state_all() if torch.cuda.is_available()
-                     else None, 'extra': rng_extra}}
+             'rng': rng_state(rng_extra)}
+    if per_rank is not None:
+        state['per_rank'] = per_rank
     _atomic_save(state, path)
 
 

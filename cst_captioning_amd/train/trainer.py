@@ -43,6 +43,24 @@ from . import checkpoint as ckpt
 logger = logging.getLogger(__name__)
 
 
+def maybe_inject_fault(rank, it):
+    """Fault injection for the recovery tests:
+    ``CSTCAP_FAULT_INJECT=rank:iter:marker`` makes that rank die abruptly
+    (``os._exit``, no cleanup, like a killed process) when it reaches
+    iteration ``iter``, once: the marker file records that the fault fired,
+    so the restarted job (torchrun ``--max-restarts``) runs through and resumes
+    from the ``_last.pth`` sidecar."""
+    spec = os.environ.get('CSTCAP_FAULT_INJECT')
+    if not spec:
+        return
+    r, i, marker = spec.split(':', 2)
+    if int(r) == rank and int(i) == it and not os.path.exists(marker):
+        with open(marker, 'w') as f:
+            f.write('rank %d killed at iter %d\n' % (rank, it))
+        logger.error('fault injection: rank %d exits at iter %d', rank, it)
+        os._exit(13)
+
+
 def build_scorer(opt, dataset, device):
     metric = opt.eval_metric
     if metric in ('CIDEr', 'MSRVTT', 'Loss'):
@@ -214,8 +232,13 @@ class Trainer:
             s = ckpt.load_checkpoint(last, map_location=self.device)
             self.model.load_state_dict(s['model'])
             self.optimizer.load_state_dict(s['optimizer'])
-            self.train_loader.load_state_dict(s['loader'])
-            ckpt.restore_rng(s['rng'])
+            pr = s.get('per_rank')
+            if pr is not None and len(pr) == self.ctx.world_size:
+                self.train_loader.load_state_dict(pr[self.ctx.rank]['loader'])
+                ckpt.restore_rng(pr[self.ctx.rank]['rng'])
+            else:  # written by a run with another world size: shared state only
+                self.train_loader.load_state_dict(s['loader'])
+                ckpt.restore_rng(s['rng'])
             self.infos = s['infos']
             logger.info('Resumed exactly from %s (iter %d)', last, self.infos['iter'])
             return True
@@ -250,15 +273,22 @@ class Trainer:
             if opt.print_log_interval and infos['iter'] % opt.print_log_interval == 0:
                 self._log(out, time.time() - t0)
             infos['iter'] += 1
+            maybe_inject_fault(self.ctx.rank, infos['iter'])
             if infos['epoch'] < self.train_loader.get_current_epoch():
                 infos['epoch'] = self.train_loader.get_current_epoch()
                 checked = False
                 lr = schedules.adjust_learning_rate(opt, self.optimizer,
                                                     infos['epoch'] - infos['start_epoch'])
                 logger.info('===> Learning rate: %f: ', lr)
-                if opt.model_file and getattr(opt, 'save_last', 1) and self.ctx.is_main:
-                    ckpt.save_last(ckpt.last_path(opt.model_file), self.model, self.optimizer,
-                                   infos, opt, self.train_loader)
+                if opt.model_file and getattr(opt, 'save_last', 1):
+                    # every rank's loader position and RNG streams, written by rank 0
+                    per_rank = self.ctx.all_gather_object(
+                        {'loader': self.train_loader.state_dict(), 'rng': ckpt.rng_state()})
+                    if self.ctx.is_main:
+                        ckpt.save_last(ckpt.last_path(opt.model_file), self.model,
+                                       self.optimizer, infos, opt, self.train_loader,
+                                       per_rank=per_rank)
+                    self.ctx.barrier()
             if (self.val_loader is not None and infos['epoch'] >= opt.save_checkpoint_from
                     and infos['epoch'] % opt.save_checkpoint_every == 0 and not checked):
                 results = self.validate(self.val_loader)

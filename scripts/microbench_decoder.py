@@ -23,9 +23,11 @@ whh = wx[:, E:].contiguous()
 ptab = torch.mm(emb, wx[:, :E].t(), out_dtype=torch.float32)
 res = {}
 import os
-variants = [int(x) for x in os.environ.get('VARIANTS', '0').split(',')]
-for var in variants:
+variants = [int(x) for x in os.environ.get('VARIANTS', '4').split(',')]
+lvariants = [int(x) for x in os.environ.get('LSTM_VARIANTS', '0').split(',')]
+for var, lvar in [(a, b) for a in variants for b in lvariants]:
   C.set_vocab_variant(var)
+  C.set_lstm_fwd_variant(lvar)
   for name, modes, save, drop in [('greedy_nosave', [2] * (T - 1), False, 0.0),
                                 ('sample_nosave', [1] * (T - 1), False, 0.0),
                                 ('sample_save_drop', [1] * (T - 1), True, 0.5),
@@ -39,5 +41,5 @@ for var in variants:
     for _ in range(10):
         args()
     torch.cuda.synchronize()
-    res['v%d_%s' % (var, name)] = round((time.perf_counter() - t0) / 10 * 1e3, 3)
+    res['v%d_l%d_%s' % (var, lvar, name)] = round((time.perf_counter() - t0) / 10 * 1e3, 3)
 print(json.dumps(res))

@@ -1,0 +1,39 @@
+"""Single-kernel microbenchmarks (HIP-event timed, back-to-back launches).
+
+vocab_fwd at the rollout shape (R = 1280 rows) and the greedy shape (R = 64),
+per tile variant, with the epilogue pieces switched on one at a time:
+  mainloop = GEMM only; stats = max/LSE (+target); sample; sample+save
+  (fp16 logits for the backward); argmax.
+"""
+import json
+import os
+
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from cst_captioning_amd import _ext
+
+C = _ext.ops()
+torch.manual_seed(0)
+dev = 'cuda'
+V, H = 10509, 512
+W = (torch.randn(V, H, device=dev) * 0.05).bfloat16()
+b = torch.randn(V, device=dev) * 0.1
+variants = [int(x) for x in os.environ.get('VARIANTS', '0,4,5,6,7').split(',')]
+res = {}
+for R in (1280, 64):
+    hd = torch.randn(R, H, device=dev).bfloat16()
+    tgt = torch.randint(0, V, (R,), device=dev)
+    for var in variants:
+        C.set_vocab_variant(var)
+        for name, flags, save, t in (('mainloop', 4, False, None), ('stats', 0, False, tgt),
+                                     ('sample', 1, False, None), ('sample_save', 1, True, None),
+                                     ('argmax', 2, False, None)):
+            if var < 4 and flags == 4:
+                continue
+            us = C.vocab_fwd_bench(hd, W, b, t if t is not None else torch.empty(0, dtype=torch.long, device=dev),
+                                   flags, save, 50)
+            res['R%d_v%d_%s' % (R, var, name)] = round(us, 2)
+C.set_vocab_variant(4)
+print(json.dumps(res))
