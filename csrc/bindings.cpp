@@ -19,6 +19,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor c_all, at::Tensor h_all, at::Tensor seq,
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
                                          at::Tensor dg_xe, double drop_p, int64_t seed);
+std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
+                                    at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
+                                    int64_t K, int64_t T, int64_t bos_index);
+double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
+                       int64_t flags, bool save, int64_t iters);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
                        double log_ref_len, int64_t use_eos);
 at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
@@ -84,4 +89,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cider_score_cpu", &cst::cider_score_cpu);
   m.def("flat_adam_step", &cst::flat_adam_step);
   m.def("set_vocab_variant", &cst::set_vocab_variant);
+  m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
+  m.def("beam_search", &cst::beam_search);
+  m.def("set_lstm_fwd_variant", &cst::set_lstm_fwd_variant);
 }

@@ -184,7 +184,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   return out;
 }
 
-// Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), dX (n_steps*R, E), dvg_rows (R, 4H)}.
+// Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), d_emb (V, E), dvg_rows (R, 4H)}.
 // toks: (n_steps*R) input token of every (step, row), step-major.
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
@@ -225,33 +225,50 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // 3. reverse recurrence
   at::Tensor dG_all = at::empty({n_steps, R, H4}, wx.options());
   at::Tensor dc = at::zeros({R, H}, f32);
-  at::Tensor whh = wx.narrow(1, E, H);  // (4H, H) packed rows, strided view
-  at::Tensor dh_rec;
+  // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel
+  at::Tensor whhT = wx.narrow(1, E, H).t().contiguous();
   for (int64_t t = n_steps - 1; t >= 0; --t) {
-    launch_lstm_cell_bwd(dHd.data_ptr<float>() + t * R * H,
-                         dh_rec.defined() ? dh_rec.data_ptr<float>() : nullptr,
-                         dc.data_ptr<float>(),
-                         reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
-                         c_all[t].data_ptr<float>(),
-                         t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R, (int)H,
-                         (float)drop_p, seed_drop, (int)t,
-                         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), st);
-    if (t > 0) dh_rec = at::mm(dG_all[t], whh, at::kFloat);  // (R, H)
+    launch_lstm_step_bwd(
+        t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
+        reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dHd.data_ptr<float>() + t * R * H,
+        dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
+        c_all[t].data_ptr<float>(), t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R,
+        (int)H, (float)drop_p, seed_drop, (int)t,
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), st);
   }
-  // 4. batched weight gradients: dWx = dG^T [x ; h_prev] as two GEMMs
+  // 4. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
+  //    reductions run as batched GEMMs over groups of steps (many more output
+  //    tiles in flight than one K = 35k GEMM), summed afterwards.
   at::Tensor dG2 = dG_all.view({n_steps * R, H4});
-  at::Tensor x_in = emb.index_select(0, toks);                            // (n*R, E) bf16
   at::Tensor dWx = at::empty({H4, E + H}, f32);
-  dWx.narrow(1, 0, E).copy_(at::mm(dG2.t(), x_in, at::kFloat));
+  auto grouped_wgrad = [&](at::Tensor a_rows, at::Tensor b_rows, int64_t nsteps) {
+    int64_t G = 1;  // steps per group: largest divisor <= 7
+    for (int64_t g = 7; g >= 1; --g)
+      if (nsteps % g == 0) { G = g; break; }
+    const int64_t nc = nsteps / G;
+    at::Tensor a = a_rows.view({nc, G * R, a_rows.size(1)}).transpose(1, 2);
+    at::Tensor b = b_rows.reshape({nc, G * R, b_rows.size(1)});
+    return at::bmm(a, b, at::kFloat).sum(0);
+  };
+  at::Tensor x_in = emb.index_select(0, toks);                            // (n*R, E) bf16
+  dWx.narrow(1, 0, E).copy_(grouped_wgrad(dG2, x_in, n_steps));
   if (n_steps > 1) {
-    at::Tensor hprev = h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H});
-    dWx.narrow(1, E, H).copy_(at::mm(dG2.narrow(0, R, (n_steps - 1) * R).t(), hprev, at::kFloat));
+    dWx.narrow(1, E, H).copy_(grouped_wgrad(dG2.narrow(0, R, (n_steps - 1) * R),
+                                            h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
+                                            n_steps - 1));
   } else {
     dWx.narrow(1, E, H).zero_();
   }
+  //    embedding: dX = dG W_ie, then a sorted segmented sum into d_emb
+  TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
   at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);        // (n*R, E)
+  auto sorted = at::sort(toks);
+  at::Tensor stok = std::get<0>(sorted), srow = std::get<1>(sorted);
+  at::Tensor d_emb = at::zeros({V, E}, f32);
+  launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int64_t>(),
+                        srow.data_ptr<int64_t>(), (int)(n_steps * R), d_emb.data_ptr<float>(), st);
   at::Tensor dvg = dG_all.sum(0, false, at::kFloat);                   // (R, 4H), sum over time
-  return {dWx, dWlog, dblog, dX, dvg};
+  return {dWx, dWlog, dblog, d_emb, dvg};
 }
 
 // On-GPU CIDEr-D scores of N hypotheses.
@@ -284,6 +301,112 @@ at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v
                    skip.data_ptr<bool>(), scal.data_ptr<float>(), (float)lr, (float)b1,
                    (float)b2, (float)eps, (float)clip, (float)bc1, (float)bc2, cur_stream());
   return scal.narrow(0, 0, 1).squeeze(0);
+}
+
+// Batched beam search (reference sample_beam, model.py:369-512) for B videos
+// x K beams, entirely on the GPU: per step one LSTM launch (h/c of each row's
+// parent beam via row_map), one vocab launch (fp32 logits + LSE partials),
+// the LSE combine, a top-K launch and one beam-step launch.  Returns
+// {best_seq (B, T) int64, best_logprobs (B, T) fp32}, T = seq_length,
+// padded with zeros like the reference.
+std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
+                                    at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
+                                    int64_t K, int64_t T, int64_t bos_index) {
+  check_cuda(wx, "wx");
+  check_cuda(vgate, "vgate");
+  TORCH_CHECK(get_vocab_variant() >= 4, "beam search needs a transposed-epilogue vocab variant");
+  TORCH_CHECK(K >= 1 && K <= 16, "beam_size must be in [1, 16]");
+  const int64_t H4 = wx.size(0), H = H4 / 4, V = wlog.size(0), B = vgate.size(0), R = B * K;
+  TORCH_CHECK(K <= V, "beam_size > vocab_size");
+  auto dev = wx.device();
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+  auto i64 = at::TensorOptions().dtype(at::kLong).device(dev);
+  auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
+  hipStream_t st = cur_stream();
+  const int64_t ldl = (V + 7) / 8 * 8;
+  at::Tensor logits = at::empty({R, ldl}, f32);
+  at::Tensor lse = at::empty({R}, f32);
+  const int n_vt = vocab_num_tiles((int)V);
+  at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4}, f32);
+  at::Tensor top_v = at::empty({R, K}, f32);
+  at::Tensor top_i = at::empty({R, K}, i32);
+  at::Tensor beam_sum = at::zeros({R}, f32);
+  at::Tensor seq_hist = at::zeros({2, R, T}, i64);
+  at::Tensor lp_hist = at::zeros({2, R, T}, f32);
+  at::Tensor best_ppl = at::full({B}, INFINITY, f32);
+  at::Tensor best_seq = at::zeros({B, T}, i64);
+  at::Tensor best_lp = at::zeros({B, T}, f32);
+  at::Tensor tok = at::full({R}, bos_index, i64);
+  at::Tensor parent = at::empty({R}, i32);
+  at::Tensor h[2] = {at::zeros({R, H}, wx.options()), at::empty({R, H}, wx.options())};
+  at::Tensor c[2] = {at::zeros({R, H}, f32), at::empty({R, H}, f32)};
+  const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
+  const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
+  for (int64_t t = 0; t < T - 1; ++t) {
+    if (t >= 1) {
+      launch_beam_topk(logits.data_ptr<float>(), ldl, (int)V, (int)R, (int)K,
+                       lse.data_ptr<float>(), top_v.data_ptr<float>(), top_i.data_ptr<int>(), st);
+      launch_beam_step(top_v.data_ptr<float>(), top_i.data_ptr<int>(), (int)B, (int)K, (int)T,
+                       (int)t, beam_sum.data_ptr<float>(), seq_hist.data_ptr<int64_t>(),
+                       lp_hist.data_ptr<float>(), best_ppl.data_ptr<float>(),
+                       best_seq.data_ptr<int64_t>(), best_lp.data_ptr<float>(),
+                       tok.data_ptr<int64_t>(), parent.data_ptr<int>(), st);
+      if (t == T - 2) break;  // the reference's last LSTM step feeds nothing
+    }
+    const at::Tensor& hp = h[t & 1];
+    const at::Tensor& cp = c[t & 1];
+    at::Tensor& ho = h[(t + 1) & 1];
+    at::Tensor& co = c[(t + 1) & 1];
+    launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, ptab.data_ptr<float>(),
+                         reinterpret_cast<const uint16_t*>(hp.data_ptr()), cp.data_ptr<float>(),
+                         vgate.data_ptr<float>(), (int)K, (int)R, (int)H, WHH,
+                         reinterpret_cast<uint16_t*>(ho.data_ptr()), co.data_ptr<float>(), nullptr,
+                         (int)H, 0.f, 0u, (int)t, nullptr, st,
+                         t >= 1 ? parent.data_ptr<int>() : nullptr);
+    launch_vocab_fwd(reinterpret_cast<const uint16_t*>(ho.data_ptr()), (int)H, (int)R, (int)H, W,
+                     blog.data_ptr<float>(), (int)V,
+                     reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl, part.data_ptr(),
+                     nullptr, 0, /*flags=*/8, 1.f, 0u, (int)t, st);
+    launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse.data_ptr<float>(), nullptr, 0,
+                         nullptr, 0, nullptr, 0, nullptr, 0, SEL_GT_H, 0.f, 0u, (int)t, nullptr,
+                         0, nullptr, st);
+  }
+  return {best_seq, best_lp};
+}
+
+// Microbenchmarks of single kernels (scripts/microbench_kernels.py): mean
+// microseconds per launch over `iters` back-to-back launches, HIP events.
+double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
+                       int64_t flags, bool save, int64_t iters) {
+  const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
+  TORCH_CHECK(H % 64 == 0 && wlog.size(1) == H && blog.numel() == V, "shapes");
+  auto dev = hd.device();
+  const int64_t ldl = (V + 7) / 8 * 8;
+  at::Tensor logits = save ? at::empty({R, ldl}, hd.options().dtype(at::kHalf)) : at::Tensor();
+  const int n_vt = vocab_num_tiles((int)V);
+  at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4},
+                              at::TensorOptions().dtype(at::kFloat).device(dev));
+  const int64_t* tg = tgt.defined() && tgt.numel() ? tgt.data_ptr<int64_t>() : nullptr;
+  hipStream_t st = cur_stream();
+  auto launch = [&](int i) {
+    launch_vocab_fwd(reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R, (int)H,
+                     reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
+                     (int)V, save ? reinterpret_cast<uint16_t*>(logits.data_ptr()) : nullptr,
+                     ldl, part.data_ptr(), tg, 1, (int)flags, 1.f, 1234u, i, st);
+  };
+  launch(0);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < iters; ++i) launch(i);
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 1000.0 * ms / (double)iters;
 }
 
 }  // namespace cst

@@ -1,0 +1,187 @@
+// K10: batched beam search step on the GPU.
+//
+// Reference (/root/reference/model.py:369-512): one video at a time; each
+// step moves the K x V log-probs to the host, sorts every beam's row
+// (torch.sort on the CPU), builds Python candidate dicts, re-forks the beams by
+// copying histories and LSTM state, and harvests finished beams into lists.
+//
+// Here all B videos advance together and nothing leaves the GPU:
+//   * the vocab projection runs through the fused vocab kernel (fp32 logits +
+//     per-row LSE), then beam_topk_kernel takes each beam row's K best
+//     log-probs (one wavefront per row, register top-K per lane + K rounds of
+//     wave arg-max);
+//   * beam_step_kernel (one wavefront per video) applies the reference's
+//     selection rules exactly: at t = 1 only beam 0 expands; candidates are
+//     ordered word-rank-major (for c: for q) and stably sorted by cumulative
+//     log-prob; the K best fork their parent's history; a beam that emitted
+//     EOS (0) -- or any beam at the last step -- is harvested, and the
+//     harvested beam with the lowest perplexity exp(-sum / (t - 1)) (10000 at
+//     t = 1) wins, earliest on ties.  Beams keep expanding after EOS, as in
+//     the reference;
+//   * the LSTM state is not copied: the next step's LSTM kernel reads h/c of
+//     row `parent[r]` (row_map).
+#include "../common.h"
+
+namespace cst {
+
+constexpr int BEAM_MAXK = 16;
+
+// top-K (value, index) of logit - lse for each of R rows; ties -> smaller index
+__global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict__ logits,
+                                                        int64_t ldl, int V, int R, int K,
+                                                        const float* __restrict__ lse,
+                                                        float* __restrict__ top_v,
+                                                        int* __restrict__ top_i) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* x = logits + (int64_t)r * ldl;
+  // lane-local sorted top-K by an unrolled insertion pass (static register
+  // indices only; strict > keeps the earlier, smaller index on ties)
+  float bv[BEAM_MAXK];
+  int bi[BEAM_MAXK];
+#pragma unroll
+  for (int k = 0; k < BEAM_MAXK; ++k) bv[k] = -INFINITY, bi[k] = 0x7fffffff;
+  for (int v = lane; v < V; v += 64) {
+    float cv = x[v];
+    int ci = v;
+    {
+#pragma unroll
+      for (int p = 0; p < BEAM_MAXK; ++p) {
+        if (p < K && cv > bv[p]) {
+          const float tv = bv[p];
+          const int ti = bi[p];
+          bv[p] = cv, bi[p] = ci;
+          cv = tv, ci = ti;
+        }
+      }
+    }
+  }
+  // K rounds of wave arg-max over the lanes' list heads; the winner shifts
+  const float L = lse[r];
+  for (int k = 0; k < K; ++k) {
+    float best = bv[0];
+    int besti = bi[0];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(besti, o, 64);
+      if (ov > best || (ov == best && oi < besti)) best = ov, besti = oi;
+    }
+    if (bi[0] == besti) {
+#pragma unroll
+      for (int p = 0; p + 1 < BEAM_MAXK; ++p) bv[p] = bv[p + 1], bi[p] = bi[p + 1];
+      bv[BEAM_MAXK - 1] = -INFINITY, bi[BEAM_MAXK - 1] = 0x7fffffff;
+    }
+    if (lane == 0) {
+      top_v[(int64_t)r * K + k] = best - L;
+      top_i[(int64_t)r * K + k] = besti;
+    }
+  }
+}
+
+// One wavefront per video.  State (per video b, beam q):
+//   beam_sum[b*K+q], seq/lp histories [2][B*K][T] (double-buffered by step
+//   parity), best_ppl[b], best_seq[b][T], best_lp[b][T].
+// Writes tok[b*K+v] (next input token) and parent[b*K+v] (row whose h/c the
+// new beam continues).
+__global__ __launch_bounds__(64) void beam_step_kernel(
+    const float* __restrict__ top_v, const int* __restrict__ top_i, int B, int K, int T, int t,
+    float* __restrict__ beam_sum, int64_t* __restrict__ seq_hist, float* __restrict__ lp_hist,
+    float* __restrict__ best_ppl, int64_t* __restrict__ best_seq, float* __restrict__ best_lp,
+    int64_t* __restrict__ tok_out, int* __restrict__ parent_out) {
+  __shared__ float s_p[BEAM_MAXK * BEAM_MAXK];
+  __shared__ int s_sel[BEAM_MAXK];
+  __shared__ float s_sum_old[BEAM_MAXK];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int rows = t == 1 ? 1 : K;
+  const int ncand = rows * K;
+  if (lane < K) s_sum_old[lane] = beam_sum[b * K + lane];
+  __syncthreads();
+  // candidate j = c * rows + q  (word rank c of beam q): the reference order
+  for (int j = lane; j < ncand; j += 64) {
+    const int c = j / rows, q = j % rows;
+    s_p[j] = s_sum_old[q] + top_v[(int64_t)(b * K + q) * K + c];
+  }
+  __syncthreads();
+  // stable selection of the K best: K rounds of (max p, then smallest j)
+  for (int v = 0; v < K; ++v) {
+    float best = -INFINITY;
+    int bj = 0x7fffffff;
+    for (int j = lane; j < ncand; j += 64) {
+      bool taken = false;
+      for (int u = 0; u < v; ++u) taken |= (s_sel[u] == j);
+      const float p = s_p[j];
+      if (!taken && (p > best || (p == best && j < bj))) best = p, bj = j;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oj = __shfl_xor(bj, o, 64);
+      if (ov > best || (ov == best && oj < bj)) best = ov, bj = oj;
+    }
+    if (lane == 0) s_sel[v] = bj;
+    __syncthreads();
+  }
+  // fork: new beam v continues parent q with word rank c
+  const int64_t* sh_old = seq_hist + (int64_t)((t + 1) & 1) * B * K * T;
+  const float* lh_old = lp_hist + (int64_t)((t + 1) & 1) * B * K * T;
+  int64_t* sh_new = seq_hist + (int64_t)(t & 1) * B * K * T;
+  float* lh_new = lp_hist + (int64_t)(t & 1) * B * K * T;
+  for (int e = lane; e < K * T; e += 64) {
+    const int v = e / T, pos = e % T;
+    const int j = s_sel[v], c = j / rows, q = j % rows;
+    const int64_t src = (int64_t)(b * K + q) * T + pos, dst = (int64_t)(b * K + v) * T + pos;
+    if (pos < t - 1) {
+      sh_new[dst] = sh_old[src];
+      lh_new[dst] = lh_old[src];
+    } else if (pos == t - 1) {
+      sh_new[dst] = top_i[(int64_t)(b * K + q) * K + c];
+      lh_new[dst] = top_v[(int64_t)(b * K + q) * K + c];
+    } else {
+      sh_new[dst] = 0;
+      lh_new[dst] = 0.f;
+    }
+  }
+  __syncthreads();
+  if (lane < K) {
+    const int v = lane, j = s_sel[v], c = j / rows, q = j % rows;
+    beam_sum[b * K + v] = s_p[j];
+    tok_out[b * K + v] = top_i[(int64_t)(b * K + q) * K + c];
+    parent_out[b * K + v] = b * K + q;
+  }
+  // harvest, in beam order (earliest wins ties)
+  if (lane == 0) {
+    for (int v = 0; v < K; ++v) {
+      const int j = s_sel[v], c = j / rows, q = j % rows;
+      const int w = top_i[(int64_t)(b * K + q) * K + c];
+      if (w == 0 || t == T - 2) {
+        const float ppl = t > 1 ? __expf(-s_p[j] / (float)(t - 1)) : 10000.f;
+        if (ppl < best_ppl[b]) {
+          best_ppl[b] = ppl;
+          for (int pos = 0; pos < T; ++pos) {
+            best_seq[(int64_t)b * T + pos] = sh_new[(int64_t)(b * K + v) * T + pos];
+            best_lp[(int64_t)b * T + pos] = lh_new[(int64_t)(b * K + v) * T + pos];
+          }
+        }
+      }
+    }
+  }
+}
+
+void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,
+                      float* top_v, int* top_i, hipStream_t stream) {
+  hipLaunchKernelGGL(beam_topk_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, logits, ldl, V,
+                     R, K, lse, top_v, top_i);
+}
+
+void launch_beam_step(const float* top_v, const int* top_i, int B, int K, int T, int t,
+                      float* beam_sum, int64_t* seq_hist, float* lp_hist, float* best_ppl,
+                      int64_t* best_seq, float* best_lp, int64_t* tok_out, int* parent_out,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(beam_step_kernel, dim3(B), dim3(64), 0, stream, top_v, top_i, B, K, T, t,
+                     beam_sum, seq_hist, lp_hist, best_ppl, best_seq, best_lp, tok_out,
+                     parent_out);
+}
+
+}  // namespace cst

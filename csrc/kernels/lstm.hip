@@ -25,8 +25,9 @@
 namespace cst {
 
 constexpr int LB_M = 128, LB_N = 64;
-using LTile = Tile<LB_M, LB_N, 3>;  // 3-stage pipeline: 72 KB + tokens, 2 blocks/CU
-constexpr int LSTM_LDS_BYTES = LTile::LDS_BYTES + LB_M * 4;  // + staged token ids
+// backward step: 1 block per CU (160 blocks at R = 1280), so the pipeline is
+// deep instead (5 K-tiles = 80 KB in flight) to cover L2 latency
+constexpr int LSTM_BWD_STAGES = 6;
 
 __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -34,23 +35,25 @@ __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
+template <int BM, int STAGES>
 __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     const int64_t* __restrict__ tok, int64_t tok_stride, const float* __restrict__ ptab,
     const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
     const float* __restrict__ vgate, int vgate_div, int R, int H,
     const uint16_t* __restrict__ whh, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
     uint16_t* __restrict__ hdrop_out, int ldh, float drop_p, uint32_t seed, int step,
-    uint16_t* __restrict__ gates_out) {
+    uint16_t* __restrict__ gates_out, const int* __restrict__ row_map) {
+  using LTile = Tile<BM, LB_N, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
+  const int n_nt = (4 * H) / LB_N, n_rt = (R + BM - 1) / BM;
   const int b = xcd_remap_l(blockIdx.x, n_nt * n_rt);
   const int nt = b / n_rt, rt = b % n_rt;
-  const int r0 = rt * LB_M, n0 = nt * LB_N;
+  const int r0 = rt * BM, n0 = nt * LB_N;
   const int nk = H / 64;
 
   // token ids of this row tile (used by the epilogue's table gather)
   int* s_tok = reinterpret_cast<int*>(lds + LTile::LDS_BYTES);
-  if (threadIdx.x < LB_M)
+  if (threadIdx.x < BM)
     s_tok[threadIdx.x] = (int)tok[(int64_t)min(r0 + (int)threadIdx.x, R - 1) * tok_stride];
   __syncthreads();
 
@@ -58,7 +61,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
   // (random rows of an 86 MB table, video gates, c_{t-1}) hides under the GEMM.
   const int tid = threadIdx.x, u = tid & 15, rg = tid >> 4;
   const int hu = nt * 16 + u;  // global hidden unit
-  constexpr int RPT = LB_M / 16;  // rows per thread
+  constexpr int RPT = BM / 16;  // rows per thread
   float4 pre_px[RPT], pre_vg[RPT];
   float pre_c[RPT];
 #pragma unroll
@@ -66,20 +69,21 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     const int row = rg + 16 * i, r = min(r0 + row, R - 1);
     pre_px[i] = *reinterpret_cast<const float4*>(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u);
     pre_vg[i] = *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
-    pre_c[i] = c_prev[(int64_t)r * H + hu];
+    pre_c[i] = c_prev[(int64_t)(row_map ? row_map[r] : r) * H + hu];
   }
 
   f32x16 acc[LTile::TM][LTile::TN];
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    DmaSrc<LB_M / 32> a;
+    DmaSrc<BM / 32> a;
     DmaSrc<LB_N / 32> bsrc;
     a.r0 = a.r1 = make_rsrc(h_prev, (int64_t)R * H * 2);
     a.ksplit = nk;
 #pragma unroll
-    for (int i = 0; i < LB_M / 32; ++i) {
+    for (int i = 0; i < BM / 32; ++i) {
       const int row = dma_row(w, i, lane);
-      a.voff0[i] = min(r0 + row, R - 1) * H * 2 + dma_chunk(row, lane) * 16;
+      const int src = min(r0 + row, R - 1);  // beam search: h of the parent beam
+      a.voff0[i] = (row_map ? row_map[src] : src) * H * 2 + dma_chunk(row, lane) * 16;
       a.voff1[i] = a.voff0[i];
     }
     bsrc.r0 = bsrc.r1 = make_rsrc(whh, (int64_t)4 * H * H * 2);
@@ -165,21 +169,166 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
   *reinterpret_cast<uint2*>(dG + go_) = pk;
 }
 
+// Fused backward step (replaces cell backward + a separate recurrent GEMM):
+//   dh_rec = dG_{t+1} . W_hh            (MFMA, K = 4H, B operand W_hh^T)
+//   dh     = dh_rec + mask * dh_logit / (1 - p)
+//   cell backward of step t in the epilogue -> dG_t (bf16, packed gates),
+//   dc_carry <- dc * f.
+// One block owns BM rows x 64 hidden units; every epilogue operand is
+// prefetched before the main loop.
+template <int BM>
+__global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
+    const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
+    const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
+    const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
+    const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
+    uint16_t* __restrict__ dG) {
+  using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int n_ut = H / 64, n_rt = (R + BM - 1) / BM;
+  const int b = xcd_remap_l(blockIdx.x, n_ut * n_rt);
+  const int ut = b / n_rt, rt = b % n_rt;
+  const int r0 = rt * BM, u0 = ut * 64;
+  const int H4 = 4 * H;
+  const int nk = dg_next != nullptr ? H4 / 64 : 0;
+  const int tid = threadIdx.x, u = tid & 63, rg = tid >> 6;
+  const int hu = u0 + u;
+  constexpr int RPT = BM / 4;
+
+  uint2 pg[RPT];
+  float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = min(r0 + rg + 4 * i, R - 1);
+    const int64_t o = (int64_t)r * H + hu;
+    pg[i] = *reinterpret_cast<const uint2*>(gates + (int64_t)r * H4 + 4 * hu);
+    pc[i] = c_t[o];
+    pcp[i] = c_prev ? c_prev[o] : 0.f;
+    pdc[i] = dc_carry[o];
+    pdl[i] = dh_logit[o];
+  }
+
+  f32x16 acc[TL::TM][TL::TN];
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    DmaSrc<BM / 32> a;
+    DmaSrc<64 / 32> bsrc;
+    a.r0 = a.r1 = make_rsrc(dg_next ? dg_next : whhT, (int64_t)R * H4 * 2);
+    a.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < BM / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      a.voff0[i] = min(r0 + row, R - 1) * H4 * 2 + dma_chunk(row, lane) * 16;
+      a.voff1[i] = a.voff0[i];
+    }
+    bsrc.r0 = bsrc.r1 = make_rsrc(whhT, (int64_t)H * H4 * 2);
+    bsrc.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = dma_row(w, i, lane);
+      bsrc.voff0[i] = (u0 + row) * H4 * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff1[i] = bsrc.voff0[i];
+    }
+    gemm_nt_mainloop<TL>(nk, a, bsrc, lds, acc);
+  }
+  float* C = reinterpret_cast<float*>(lds);
+  store_acc_to_lds<TL>(acc, C, [](int) { return 0.f; });
+  __syncthreads();
+
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int row = rg + 4 * i, r = r0 + row;
+    if (r < R) {
+      const int64_t o = (int64_t)r * H + hu;
+      float dh = C[row * TL::CSTRIDE + u];
+      const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
+      if (keep) dh += pdl[i] * inv_keep;
+      const uint2 gp = pg[i];
+      const float gi = bf2f(gp.x & 0xffff), gf = bf2f(gp.x >> 16);
+      const float gg = bf2f(gp.y & 0xffff), go = bf2f(gp.y >> 16);
+      const float tc = tanhf_(pc[i]);
+      const float dc = pdc[i] + dh * go * (1.f - tc * tc);
+      const float dpi = dc * gg * gi * (1.f - gi);
+      const float dpf = dc * pcp[i] * gf * (1.f - gf);
+      const float dpg = dc * gi * (1.f - gg * gg);
+      const float dpo = dh * tc * go * (1.f - go);
+      dc_carry[o] = dc * gf;
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(dpi) | ((uint32_t)f2bf(dpf) << 16);
+      pk.y = (uint32_t)f2bf(dpg) | ((uint32_t)f2bf(dpo) << 16);
+      *reinterpret_cast<uint2*>(dG + (int64_t)r * H4 + 4 * hu) = pk;
+    }
+  }
+}
+
+
+template <int BM>
+static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT,
+                                   const float* dh_logit, float* dc_carry,
+                                   const uint16_t* gates, const float* c_t, const float* c_prev,
+                                   int R, int H, float drop_p, uint32_t seed, int step,
+                                   uint16_t* dG, hipStream_t stream) {
+  using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, TL::LDS_BYTES);
+    attr_set = true;
+  }
+  const int n = (H / 64) * ((R + BM - 1) / BM);
+  hipLaunchKernelGGL(lstm_step_bwd_kernel<BM>, dim3(n), dim3(256), TL::LDS_BYTES, stream,
+                     dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
+                     step, dG);
+}
+
+void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
+                          float* dc_carry, const uint16_t* gates, const float* c_t,
+                          const float* c_prev, int R, int H, float drop_p, uint32_t seed,
+                          int step, uint16_t* dG, hipStream_t stream) {
+  launch_lstm_step_bwd_t<64>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
+                             drop_p, seed, step, dG, stream);
+}
+
+static int g_lstm_fwd_variant = 0;
+void set_lstm_fwd_variant(int v) { g_lstm_fwd_variant = v; }
+
+template <int BM, int STAGES>
+static void launch_lstm_step_fwd_t(const int64_t* tok, int64_t tok_stride, const float* ptab,
+                                   const uint16_t* h_prev, const float* c_prev,
+                                   const float* vgate, int vgate_div, int R, int H,
+                                   const uint16_t* whh, uint16_t* h_out, float* c_out,
+                                   uint16_t* hdrop_out, int ldh, float drop_p, uint32_t seed,
+                                   int step, uint16_t* gates_out, const int* row_map,
+                                   hipStream_t stream) {
+  constexpr int LDS = Tile<BM, LB_N, STAGES>::LDS_BYTES + BM * 4;  // + staged token ids
+  const int n_nt = (4 * H) / LB_N, n_rt = (R + BM - 1) / BM;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)lstm_step_fwd_kernel<BM, STAGES>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((lstm_step_fwd_kernel<BM, STAGES>), dim3(n_nt * n_rt), dim3(256), LDS,
+                     stream, tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh,
+                     h_out, c_out, hdrop_out, ldh, drop_p, seed, step, gates_out, row_map);
+}
+
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
                           const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
-                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream) {
-  const int n_nt = (4 * H) / LB_N, n_rt = (R + LB_M - 1) / LB_M;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)lstm_step_fwd_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_LDS_BYTES);
-    attr_set = true;
+                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream,
+                          const int* row_map) {
+#define LSTM_FWD_ARGS tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh, h_out, \
+    c_out, hdrop_out, ldh, drop_p, seed, step, gates_out, row_map, stream
+  switch (g_lstm_fwd_variant) {
+    case 1: launch_lstm_step_fwd_t<128, 4>(LSTM_FWD_ARGS); break;  // 96 KB, 1 block/CU
+    case 2: launch_lstm_step_fwd_t<64, 4>(LSTM_FWD_ARGS); break;   // 64 KB, 2 blocks/CU
+    case 3: launch_lstm_step_fwd_t<64, 3>(LSTM_FWD_ARGS); break;   // 48 KB, 3 blocks/CU
+    default: launch_lstm_step_fwd_t<128, 3>(LSTM_FWD_ARGS);        // 72 KB, 2 blocks/CU
   }
-  hipLaunchKernelGGL(lstm_step_fwd_kernel, dim3(n_nt * n_rt), dim3(256), LSTM_LDS_BYTES, stream,
-                     tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh, h_out,
-                     c_out, hdrop_out, ldh, drop_p, seed, step, gates_out);
+#undef LSTM_FWD_ARGS
 }
 
 void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,

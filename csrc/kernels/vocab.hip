@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_kernel(
 // tiles in vocab_combine_kernel, and the union of independent races is the
 // race over all of V.
 constexpr int VT_V = 128;  // vocab entries per block
-enum VocabFlags : int { VF_SAMPLE = 1, VF_ARGMAX = 2 };
+enum VocabFlags : int { VF_SAMPLE = 1, VF_ARGMAX = 2, VF_BENCH_MAINLOOP = 4, VF_SAVE_F32 = 8 };
 
 struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS
   float m, s, zkey, zlogit;
@@ -342,6 +342,10 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(
     }
     gemm_nt_mainloop<TL>(nk, a, bsrc, lds, acc);
   }
+  if (flags & VF_BENCH_MAINLOOP) {  // microbenchmark: main loop only
+    if (acc[0][0][0] == 1234.5f) part[0].pad = acc[TM - 1][TN - 1][15];
+    return;
+  }
 
   GroupStat* gs = reinterpret_cast<GroupStat*>(lds);  // [4 groups][BN rows]
   const int g = wr * 2 + half;
@@ -357,7 +361,23 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(
 #pragma unroll
       for (int k = 0; k < 16; ++k) x[i][k] = acc[i][j][k] + pb[i][k];
 
-    if (logits16 != nullptr && r < R) {
+    if ((flags & VF_SAVE_F32) && logits16 != nullptr && r < R) {  // fp32 logits (beam search)
+      float* dst = reinterpret_cast<float*>(logits16) + (int64_t)r * ldl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int v = vb + 32 * i + 8 * q;
+          if (v + 4 <= V) {
+            *reinterpret_cast<float4*>(dst + v) =
+                make_float4(x[i][4 * q], x[i][4 * q + 1], x[i][4 * q + 2], x[i][4 * q + 3]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (v + e < V) dst[v + e] = x[i][4 * q + e];
+          }
+        }
+    } else if (logits16 != nullptr && r < R) {
       uint16_t* dst = logits16 + (int64_t)r * ldl;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -677,6 +697,7 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
 // record layout depends on the vocab tile width, so the choice is global.
 static int g_vocab_variant = 4;  // transposed epilogue (fastest on MI355X, profiles/)
 void set_vocab_variant(int v) { g_vocab_variant = v; }
+int get_vocab_variant() { return g_vocab_variant; }
 static int vocab_bn() { return g_vocab_variant == 1 || g_vocab_variant == 3 ? 64 : 128; }
 static bool vocab_tr() { return g_vocab_variant >= 4; }
 
@@ -726,9 +747,14 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
                       uint32_t seed, int step, hipStream_t stream) {
   const int do_sample = flags & VF_SAMPLE;
   switch (g_vocab_variant) {
-    case 4:  // transposed epilogue, 128 vocab x 128 rows, 2 stages (64 KB, 2 blocks/CU)
-      launch_vocab_fwd_tr<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                     tgt_stride, flags, inv_temp, seed, step, stream);
+    case 4:  // transposed epilogue, 128 vocab x 128 rows, 2 stages (64 KB, 2 blocks/CU);
+             // 64-row tiles when there are only 64 rows (greedy baseline: one per video)
+      if (R <= 64)
+        launch_vocab_fwd_tr<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                      tgt_stride, flags, inv_temp, seed, step, stream);
+      else
+        launch_vocab_fwd_tr<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                       tgt_stride, flags, inv_temp, seed, step, stream);
       break;
     case 5:  // transposed epilogue, 128 vocab x 64 rows, 3 stages (72 KB, 2 blocks/CU)
       launch_vocab_fwd_tr<64, 3, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
@@ -737,6 +763,10 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
     case 6:  // transposed epilogue, 128 vocab x 64 rows, 2 stages (48 KB)
       launch_vocab_fwd_tr<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
                                     tgt_stride, flags, inv_temp, seed, step, stream);
+      break;
+    case 7:  // transposed epilogue, 128 x 128, 3 stages (96 KB, 1 block/CU)
+      launch_vocab_fwd_tr<128, 3, 1>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                     tgt_stride, flags, inv_temp, seed, step, stream);
       break;
     case 1:  // 128x64 tile, 3 stages (72 KB LDS, 2 blocks/CU)
       launch_vocab_fwd_t<64, 3, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,

@@ -46,10 +46,30 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* p
                           const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
-                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream);
+                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream,
+                          const int* row_map = nullptr);  // row_map: h/c source row (beam)
+void set_lstm_fwd_variant(int v);
 void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
                           const uint16_t* gates, const float* c_t, const float* c_prev, int R,
                           int H, float drop_p, uint32_t seed, int step, uint16_t* dG,
                           hipStream_t stream);
+
+void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
+                          float* dc_carry, const uint16_t* gates, const float* c_t,
+                          const float* c_prev, int R, int H, float drop_p, uint32_t seed,
+                          int step, uint16_t* dG, hipStream_t stream);
+
+// embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows sorted by token; C <= 1024)
+void launch_token_rows_sum(const float* x, int C, const int64_t* stok, const int64_t* srow, int N,
+                           float* out, hipStream_t stream);
+
+// beam.hip
+void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,
+                      float* top_v, int* top_i, hipStream_t stream);
+int get_vocab_variant();
+void launch_beam_step(const float* top_v, const int* top_i, int B, int K, int T, int t,
+                      float* beam_sum, int64_t* seq_hist, float* lp_hist, float* best_ppl,
+                      int64_t* best_seq, float* best_lp, int64_t* tok_out, int* parent_out,
+                      hipStream_t stream);
 
 }  // namespace cst

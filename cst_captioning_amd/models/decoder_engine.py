@@ -227,9 +227,21 @@ class DecoderEngine:
                                temperature=temperature)
         return seq, lp
 
+    @torch.no_grad()
     def sample_beam(self, model, feats, opt):
-        model.impl = 'torch'
-        try:
-            return model.sample_beam(feats, opt)
-        finally:
-            model.impl = 'hip'
+        """Batched on-GPU beam search (``csrc/kernels/beam.hip``) with the
+        reference's selection / harvesting / perplexity-ranking semantics
+        (``model.py:369-512``)."""
+        K = opt.get('beam_size', 5)
+        if K > 16:
+            model.impl = 'torch'
+            try:
+                return model.sample_beam(feats, opt)
+            finally:
+                model.impl = 'hip'
+        vg, _ = self._vgate(model, feats, False)
+        seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog,
+                                         model.logit.bias.detach().float().contiguous(),
+                                         vg.detach().float().contiguous(), K, model.seq_length,
+                                         BOS)
+        return seq, lp

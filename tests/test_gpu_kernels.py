@@ -161,6 +161,30 @@ def test_greedy_sample_matches_torch():
     assert ((lp[:, :1] - lp_ref[:, :1]).abs()[ok] < 0.05).all()
 
 
+@pytest.mark.parametrize('K', [2, 3, 5])
+def test_beam_search_kernel_matches_torch(K):
+    """GPU beam step (beam.hip) vs the batched PyTorch beam search, which
+    itself is pinned to a per-video spec of the reference in test_model.py.
+    The torch side runs on the same bf16-rounded weights."""
+    ds, opt, model, loader = _tiny(seed=2)
+    with torch.no_grad():
+        model.logit.weight.mul_(3.0)  # peaked distributions: few near-ties
+    eng = _engine(model, opt)
+    model.eval()
+    data = loader.get_batch()
+    ref = copy.deepcopy(model)
+    ref.impl = 'torch'
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(p.bfloat16().float())
+    seq_ref, lp_ref = ref.sample(data['feats'], {'beam_size': K})
+    seq, lp = eng.sample_beam(model, data['feats'], {'beam_size': K})
+    assert seq.shape == seq_ref.shape == (data['feats'][0].size(0), opt.seq_length)
+    same = (seq == seq_ref).all(1)
+    assert same.float().mean().item() >= 0.8, (seq, seq_ref)
+    assert ((lp - lp_ref).abs()[same] < 0.05).all()
+
+
 def test_rl_rollout_gradient_matches_torch():
     """REINFORCE gradient through the sampled-token path (y_sel)."""
     ds, opt, model, loader = _tiny(seed=2)
