@@ -17,7 +17,10 @@
 //                   reverse LSTM recurrence (cell kernel + one GEMM per step),
 //                   then the batched weight-gradient GEMMs.
 #include <torch/extension.h>
+#include <cstdlib>
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
 
 #include "launchers.h"
 
@@ -119,59 +122,97 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
   const int64_t* LAB = have_labels ? labels.data_ptr<int64_t>() : nullptr;
 
-  for (int64_t t = 0; t < n_steps; ++t) {
-    const int64_t* tok;
-    int64_t tok_stride;
-    if (t == 0) {
-      tok = have_labels ? LAB : bos.data_ptr<int64_t>();
-      tok_stride = have_labels ? L : 1;
-    } else {
-      tok = seq.data_ptr<int64_t>() + (t - 1);
-      tok_stride = T - 1;
+  // Step t's buffers: h_t / c_t (saved per step in training, else ping-pong),
+  // hd_t = dropout(h_t) (the vocab input).
+  auto h_buf = [&](int64_t t) -> uint16_t* {
+    return reinterpret_cast<uint16_t*>(save ? h_all[t].data_ptr() : (t & 1 ? h_b : h_a).data_ptr());
+  };
+  auto c_buf = [&](int64_t t) -> float* {
+    return save ? c_all[t].data_ptr<float>() : (t & 1 ? c_b : c_a).data_ptr<float>();
+  };
+  auto hd_buf = [&](int64_t t) -> uint16_t* {
+    if (save) return reinterpret_cast<uint16_t*>(hdrop_all[t].data_ptr());
+    return drop_p > 0 ? reinterpret_cast<uint16_t*>(hd_tmp.data_ptr()) : nullptr;
+  };
+  auto gates_buf = [&](int64_t t) -> uint16_t* {
+    return save ? reinterpret_cast<uint16_t*>(gates_all[t].data_ptr()) : nullptr;
+  };
+  at::Tensor zeros_h = at::zeros({R, H}, bf), zeros_c = at::zeros({R, H}, f32);
+  at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
+
+  static const bool merged = [] {
+    const char* e = std::getenv("CSTCAP_FWD_MERGED");  // A/B knob (default on)
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (!merged) {  // reference structure: LSTM step -> vocab -> combine, per step
+    for (int64_t t = 0; t < n_steps; ++t) {
+      const int64_t* tok = t == 0 ? (have_labels ? LAB : bos.data_ptr<int64_t>())
+                                  : seq.data_ptr<int64_t>() + (t - 1);
+      const int64_t tok_stride = t == 0 ? (have_labels ? L : 1) : T - 1;
+      launch_lstm_step_fwd(tok, tok_stride, ptab.data_ptr<float>(),
+                           t == 0 ? reinterpret_cast<uint16_t*>(zeros_h.data_ptr()) : h_buf(t - 1),
+                           t == 0 ? zeros_c.data_ptr<float>() : c_buf(t - 1),
+                           vgate.data_ptr<float>(), (int)vgate_div, (int)R, (int)H, WHH, h_buf(t),
+                           c_buf(t), hd_buf(t), (int)(H + HAUG), (float)drop_p, seed_drop, (int)t,
+                           gates_buf(t), st);
+      uint16_t* hd = hd_buf(t);
+      const bool choose = t < T - 1;
+      const int mode = choose ? (int)modes[t] : SEL_GT_H;
+      const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
+      const int vflags = do_sample | ((choose && mode == SEL_GREEDY_H) ? 2 : 0);
+      const int64_t* tgt = (have_labels && t + 1 < L) ? LAB + (t + 1) : nullptr;
+      launch_vocab_fwd(hd ? hd : h_buf(t), hd ? (int)(H + HAUG) : (int)H, (int)R, (int)H, W,
+                       blog.data_ptr<float>(), (int)V,
+                       save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
+                       part.data_ptr(), tgt, L, vflags, inv_temp, seed_samp, (int)t, st);
+      launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
+                           choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
+                           choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,
+                           want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
+                           (float)ss_prob, seed_samp, (int)t,
+                           use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
+                           use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st);
     }
-    uint16_t* h_prev;
-    uint16_t* h_out;
-    if (save) {
-      h_prev = reinterpret_cast<uint16_t*>(t == 0 ? h_a.data_ptr() : h_all[t - 1].data_ptr());
-      h_out = reinterpret_cast<uint16_t*>(h_all[t].data_ptr());
-    } else {
-      h_prev = reinterpret_cast<uint16_t*>((t & 1 ? h_b : h_a).data_ptr());
-      h_out = reinterpret_cast<uint16_t*>((t & 1 ? h_a : h_b).data_ptr());
-    }
-    const float* c_prev;
-    float* c_out;
-    if (save) {
-      c_prev = t == 0 ? c_a.data_ptr<float>() : c_all[t - 1].data_ptr<float>();
-      c_out = c_all[t].data_ptr<float>();
-    } else {
-      c_prev = (t & 1 ? c_b : c_a).data_ptr<float>();
-      c_out = (t & 1 ? c_a : c_b).data_ptr<float>();
-    }
-    uint16_t* hd = nullptr;
-    if (save) hd = reinterpret_cast<uint16_t*>(hdrop_all[t].data_ptr());
-    else if (drop_p > 0) hd = reinterpret_cast<uint16_t*>(hd_tmp.data_ptr());
-    launch_lstm_step_fwd(tok, tok_stride, ptab.data_ptr<float>(), h_prev, c_prev,
-                         vgate.data_ptr<float>(), (int)vgate_div, (int)R, (int)H, WHH, h_out,
-                         c_out, hd, (int)(H + HAUG), (float)drop_p, seed_drop, (int)t,
-                         save ? reinterpret_cast<uint16_t*>(gates_all[t].data_ptr()) : nullptr,
-                         st);
-    const uint16_t* vin = hd ? hd : h_out;
+  }
+  // step 0: fused LSTM step (h_{-1} = c_{-1} = 0)
+  if (merged) launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
+                       ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(zeros_h.data_ptr()),
+                       zeros_c.data_ptr<float>(), vgate.data_ptr<float>(), (int)vgate_div, (int)R,
+                       (int)H, WHH, h_buf(0), c_buf(0), hd_buf(0), (int)(H + HAUG), (float)drop_p,
+                       seed_drop, 0, gates_buf(0), st);
+  // Steps t >= 0: ONE launch runs the vocab projection of step t together with
+  // the recurrent GEMM of step t+1 (pre = h_t W_hh^T + vgate), then the combine
+  // picks token t+1 and applies step t+1's cell epilogue (pre + P[token]).
+  for (int64_t t = 0; merged && t < n_steps; ++t) {
+    const bool next = t + 1 < n_steps;
+    uint16_t* hd = hd_buf(t);
+    const uint16_t* vin = hd ? hd : h_buf(t);
     const int ldh = hd ? (int)(H + HAUG) : (int)H;
     const bool choose = t < T - 1;
     const int mode = choose ? (int)modes[t] : SEL_GT_H;
     const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
     const int vflags = do_sample | ((choose && mode == SEL_GREEDY_H) ? 2 : 0);
     const int64_t* tgt = (have_labels && t + 1 < L) ? LAB + (t + 1) : nullptr;
-    launch_vocab_fwd(vin, ldh, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
-                     save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
-                     part.data_ptr(), tgt, L, vflags, inv_temp, seed_samp, (int)t, st);
+    launch_vocab_lstm_fwd(vin, ldh, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
+                          save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
+                          part.data_ptr(), tgt, L, vflags, inv_temp, seed_samp, (int)t,
+                          h_buf(t), WHH, vgate.data_ptr<float>(), (int)vgate_div,
+                          next ? pre.data_ptr<float>() : nullptr, st);
+    CellLaunch cl{};
+    if (next) {
+      TORCH_CHECK(choose, "internal: a next step needs a chosen token");
+      cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_buf(t), c_buf(t + 1),
+                      h_buf(t + 1), hd_buf(t + 1), (int)(H + HAUG), gates_buf(t + 1), (int)H,
+                      (float)drop_p, seed_drop, (int)(t + 1)};
+    }
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                          choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
                          choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,
                          want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
                          (float)ss_prob, seed_samp, (int)t,
                          use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
-                         use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st);
+                         use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st,
+                         next ? &cl : nullptr);
   }
   std::vector<at::Tensor> out = {seq, g_sel, want_xe ? g_xe : at::Tensor(), lse};
   if (save) {
@@ -205,29 +246,61 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   TORCH_CHECK(toks.numel() == n_steps * R, "toks must hold one token per (step, row)");
   const uint32_t seed_drop = (uint32_t)(seed * 2654435761u + 17u);
 
-  // 1. dS = dG (onehot - softmax), in place (fp16 logits -> bf16 dS), plus
-  //    per-block column sums of dS (bias gradient)
+  // 1-3. Vocab head + reverse recurrence, pipelined over row chunks.
+  //    Side stream, last chunk first: dS = dG (onehot - softmax) in place
+  //    (fp16 logits -> bf16 dS, plus per-block column sums for the bias), then
+  //    dHd = dS W for the chunk; finally dWlog = dS^T Hd.
+  //    Main stream: the reverse LSTM loop, which needs dHd of step t only, so
+  //    it starts as soon as the last chunk is ready and overlaps the rest.
   TORCH_CHECK(V <= 8 * 2048, "vocab larger than the dS kernel's register tiling");
+  const int64_t NR = n_steps * R;
   at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n_steps, (int)R), V}, f32);
-  launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
-                      (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
-                      has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
-                      has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
-                      has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
-                      has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                      has_xe ? dg_xe.size(1) : 0, colsum.data_ptr<float>(), st);
-  at::Tensor dS = logits16.view(at::kBFloat16).view({n_steps * R, ldl}).narrow(1, 0, V);
-  // 2. batched vocab-head GEMMs over all n_steps*R rows (hipBLASLt)
-  at::Tensor dHd = at::mm(dS, wlog, at::kFloat);                        // (n*R, H)
-  at::Tensor hd2 = hdrop_all.view({n_steps * R, H + HAUG}).narrow(1, 0, H);
-  at::Tensor dWlog = at::mm(dS.t(), hd2, at::kFloat);                   // (V, H)
-  at::Tensor dblog = colsum.sum(0);                                     // (V)
-  // 3. reverse recurrence
+  at::Tensor dS = logits16.view(at::kBFloat16).view({NR, ldl}).narrow(1, 0, V);
+  at::Tensor hd2 = hdrop_all.view({NR, H + HAUG}).narrow(1, 0, H);
+  at::Tensor dHd = at::empty({NR, H}, f32);
+  at::Tensor dWlog = at::empty({V, H}, f32);
+  const int64_t DR = vocab_bwd_ds_rows();
+  static const int max_chunks = [] {
+    const char* e = std::getenv("CSTCAP_BWD_CHUNKS");  // A/B knob for the pipeline depth
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  const int n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(max_chunks, NR / (8 * DR)));
+  std::vector<int64_t> cb(n_chunks + 1);
+  for (int c = 0; c <= n_chunks; ++c) cb[c] = c == n_chunks ? NR : (NR * c / n_chunks) / DR * DR;
+  std::vector<hipEvent_t> ev(n_chunks + 2);
+  for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  hipEvent_t ev_ready = ev[n_chunks], ev_done = ev[n_chunks + 1];
+  (void)hipEventRecord(ev_ready, st);
+  {
+    auto side = c10::hip::getStreamFromPool(false, dev.index());
+    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
+    c10::hip::HIPStreamGuard guard(side);
+    for (int c = n_chunks - 1; c >= 0; --c) {
+      launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
+                          (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
+                          has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
+                          has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
+                          has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
+                          has_xe ? labels.size(1) : 0,
+                          has_xe ? dg_xe.data_ptr<float>() : nullptr,
+                          has_xe ? dg_xe.size(1) : 0, colsum.data_ptr<float>(), cb[c], cb[c + 1],
+                          side.stream());
+      at::Tensor out = dHd.narrow(0, cb[c], cb[c + 1] - cb[c]);
+      at::mm_out(out, dS.narrow(0, cb[c], cb[c + 1] - cb[c]), wlog, at::kFloat);
+      (void)hipEventRecord(ev[c], side.stream());
+    }
+    at::mm_out(dWlog, dS.t(), hd2, at::kFloat);
+    (void)hipEventRecord(ev_done, side.stream());
+  }
   at::Tensor dG_all = at::empty({n_steps, R, H4}, wx.options());
   at::Tensor dc = at::zeros({R, H}, f32);
   // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel
   at::Tensor whhT = wx.narrow(1, E, H).t().contiguous();
+  int waited = n_chunks;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
+    int need = 0;  // chunk holding the first row of step t (chunks finish high to low)
+    while (need + 1 < n_chunks && cb[need + 1] <= t * R) ++need;
+    while (waited > need) (void)hipStreamWaitEvent(st, ev[--waited], 0);
     launch_lstm_step_bwd(
         t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
         reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dHd.data_ptr<float>() + t * R * H,
@@ -236,6 +309,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         (int)H, (float)drop_p, seed_drop, (int)t,
         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), st);
   }
+  while (waited > 0) (void)hipStreamWaitEvent(st, ev[--waited], 0);
+  at::Tensor dblog = colsum.sum(0);                                     // (V)
   // 4. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
   //    reductions run as batched GEMMs over groups of steps (many more output
   //    tiles in flight than one K = 35k GEMM), summed afterwards.
@@ -268,6 +343,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int64_t>(),
                         srow.data_ptr<int64_t>(), (int)(n_steps * R), d_emb.data_ptr<float>(), st);
   at::Tensor dvg = dG_all.sum(0, false, at::kFloat);                   // (R, 4H), sum over time
+  (void)hipStreamWaitEvent(st, ev_done, 0);  // join the side stream (dWlog)
+  for (auto& e : ev) (void)hipEventDestroy(e);
   return {dWx, dWlog, dblog, d_emb, dvg};
 }
 

@@ -25,9 +25,9 @@
 namespace cst {
 
 constexpr int LB_M = 128, LB_N = 64;
-// backward step: 1 block per CU (160 blocks at R = 1280), so the pipeline is
-// deep instead (5 K-tiles = 80 KB in flight) to cover L2 latency
-constexpr int LSTM_BWD_STAGES = 6;
+// backward step pipeline depth (48 KB of LDS: co-resides with the dWlog GEMM
+// that runs concurrently on a side stream; 6 stages measured no faster)
+constexpr int LSTM_BWD_STAGES = 3;
 
 __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;

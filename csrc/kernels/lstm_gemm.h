@@ -1,0 +1,78 @@
+// Recurrent half of the LSTM step as a device function, so it can ride in
+// the same launch as the vocabulary projection of the previous step:
+//
+//   pre_{t+1}[r][n] = sum_k h_t[r][k] W_hh[n][k] + vgate[r / vdiv][n]
+//
+// (packed gate order, fp32 out).  It depends only on h_t, not on the token
+// sampled at step t, so it runs CONCURRENTLY with vocab_t; the input-token
+// term P[tok_{t+1}] and the cell nonlinearity are applied by the combine
+// kernel once the token is known (vocab_combine_kernel's cell epilogue).
+#pragma once
+#include "gemm_tile.h"
+
+namespace cst {
+
+__device__ __forceinline__ int xcd_remap_g(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+constexpr int LG_BM = 128, LG_BN = 64, LG_STAGES = 3;
+using LGTile = Tile<LG_BM, LG_BN, LG_STAGES>;
+
+__host__ __device__ constexpr int lstm_gemm_blocks(int R, int H) {
+  return ((4 * H) / LG_BN) * ((R + LG_BM - 1) / LG_BM);
+}
+
+__device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restrict__ h, int R,
+                                                int H, const uint16_t* __restrict__ whh,
+                                                const float* __restrict__ vgate, int vdiv,
+                                                float* __restrict__ pre, char* lds) {
+  const int n_nt = (4 * H) / LG_BN, n_rt = (R + LG_BM - 1) / LG_BM;
+  const int b = xcd_remap_g(bid, n_nt * n_rt);
+  const int nt = b / n_rt, rt = b % n_rt;
+  const int r0 = rt * LG_BM, n0 = nt * LG_BN;
+  const int nk = H / 64;
+  f32x16 acc[LGTile::TM][LGTile::TN];
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    DmaSrc<LG_BM / 32> a;
+    DmaSrc<LG_BN / 32> bsrc;
+    a.r0 = a.r1 = make_rsrc(h, (int64_t)R * H * 2);
+    a.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < LG_BM / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      a.voff0[i] = min(r0 + row, R - 1) * H * 2 + dma_chunk(row, lane) * 16;
+      a.voff1[i] = a.voff0[i];
+    }
+    bsrc.r0 = bsrc.r1 = make_rsrc(whh, (int64_t)4 * H * H * 2);
+    bsrc.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < LG_BN / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      bsrc.voff0[i] = (n0 + row) * H * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff1[i] = bsrc.voff0[i];
+    }
+    gemm_nt_mainloop<LGTile>(nk, a, bsrc, lds, acc);
+  }
+  float* C = reinterpret_cast<float*>(lds);
+  store_acc_to_lds<LGTile>(acc, C, [](int) { return 0.f; });
+  __syncthreads();
+  // 16 lanes per row x 4 columns: 256-byte coalesced fp32 rows
+  const int u = threadIdx.x & 15, rg = threadIdx.x >> 4;
+#pragma unroll 4
+  for (int i = 0; i < LG_BM / 16; ++i) {
+    const int row = rg + 16 * i, r = r0 + row;
+    if (r < R) {
+      const float4 x = *reinterpret_cast<const float4*>(C + row * LGTile::CSTRIDE + 4 * u);
+      const float4 vg =
+          *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * (4 * H) + n0 + 4 * u);
+      *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) =
+          make_float4(x.x + vg.x, x.y + vg.y, x.z + vg.z, x.w + vg.w);
+    }
+  }
+}
+
+}  // namespace cst

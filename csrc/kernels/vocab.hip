@@ -31,6 +31,8 @@
 //     p = exp(x - lse), written as bf16 in place of the fp16 logits; the two
 //     plain GEMMs dH = dS W and dW = dS^T H then run on hipBLASLt.
 #include "gemm_tile.h"
+#include "lstm_gemm.h"
+#include "../launchers.h"
 
 namespace cst {
 
@@ -277,18 +279,21 @@ struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS
   float xt, pad;
 };
 
-template <int BN, int STAGES, int OCC>
-__global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(
-    const uint16_t* __restrict__ hd, int ldh, int R, int H, const uint16_t* __restrict__ W,
-    const float* __restrict__ bias, int V, uint16_t* __restrict__ logits16, int64_t ldl,
-    VocabPartial* __restrict__ part, const int64_t* __restrict__ tgt, int64_t tgt_stride,
-    int flags, float inv_temp, uint32_t seed, int step) {
+#define VOCAB_TR_PARAMS                                                                     \
+  const uint16_t *__restrict__ hd, int ldh, int R, int H, const uint16_t *__restrict__ W,    \
+      const float *__restrict__ bias, int V, uint16_t *__restrict__ logits16, int64_t ldl,   \
+      VocabPartial *__restrict__ part, const int64_t *__restrict__ tgt, int64_t tgt_stride, \
+      int flags, float inv_temp, uint32_t seed, int step
+#define VOCAB_TR_ARGS \
+  hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, seed, step
+
+template <int BN, int STAGES>
+__device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARAMS) {
   using TL = Tile<VT_V, BN, STAGES>;  // M = vocab, N = caption rows
   constexpr int TM = TL::TM, TN = TL::TN;
   static_assert(TM == 2, "lane owns 32 vocab entries per row");
-  extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
-  const int b = xcd_remap(blockIdx.x, n_vt * n_rt);
+  const int b = xcd_remap(bid, n_vt * n_rt);
   const int vt = b / n_rt, rt = b % n_rt;
   const int v0 = vt * VT_V, r0 = rt * BN;
   const int nk = H / 64;
@@ -512,12 +517,56 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(
   }
 }
 
+template <int BN, int STAGES, int OCC>
+__global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(VOCAB_TR_PARAMS) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  vocab_tr_block<BN, STAGES>(blockIdx.x, lds, VOCAB_TR_ARGS);
+}
+
+// One launch = vocab projection of step t (rows hd_t) + the recurrent GEMM of
+// step t+1 (pre_{t+1} = h_t W_hh^T + vgate, lstm_gemm.h).  The two are
+// independent, so the LSTM's latency-bound GEMM fills the CUs the vocab
+// tiles leave idle instead of running before it.  The first n_lstm_pad
+// blocks (a multiple of 8, so both halves keep their XCD-aware mapping) are
+// LSTM tiles.
+template <int BN, int STAGES, int OCC>
+__global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
+    VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
+    const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if ((int)blockIdx.x < n_lstm_pad) {
+    if ((int)blockIdx.x < lstm_gemm_blocks(R, H))
+      lstm_gemm_block(blockIdx.x, h_t, R, H, whh, vgate, vdiv, pre, lds);
+    return;
+  }
+  vocab_tr_block<BN, STAGES>(blockIdx.x - n_lstm_pad, lds, VOCAB_TR_ARGS);
+}
+
 // token-selection modes of one decode step
 enum SelMode : int { SEL_GT = 0, SEL_SAMPLE = 1, SEL_GREEDY = 2, SEL_SS = 3 };
 
 // 32 lanes per row (a half wavefront), 8 rows per 256-thread block: each lane
 // merges ~3 tiles, then a 5-step shuffle tree finishes the row.
-constexpr int CMB_LANES = 32, CMB_ROWS = 256 / CMB_LANES;
+// 64-thread blocks (2 rows): 640 blocks at R = 1280 spread the combine and
+// the cell epilogue's 33 MB of traffic over every CU.
+constexpr int CMB_LANES = 32, CMB_THREADS = 64, CMB_ROWS = CMB_THREADS / CMB_LANES;
+
+// Cell epilogue of the NEXT decode step, applied as soon as its input token
+// is chosen (see lstm_gemm.h): gates = pre + P[tok] -> i, f, g, o -> c, h.
+struct CellArgs {
+  const float* pre;    // (R, 4H) h_t W_hh^T + vgate, packed gates; nullptr = no cell
+  const float* ptab;   // (V, 4H) projected embedding table
+  const float* c_prev;
+  float* c_out;
+  uint16_t* h_out;
+  uint16_t* hdrop_out;  // nullable; row stride ldh
+  int ldh;
+  uint16_t* gates_out;  // nullable (training: saved for the backward)
+  int H;
+  float drop_p;
+  uint32_t seed;
+  int step;  // decode step of the cell (dropout mask index)
+};
 
 struct RowStat {
   float m, s, zv, zl, xm, xt;
@@ -542,14 +591,15 @@ __device__ __forceinline__ void merge_stat(RowStat& a, float m2, float s2, float
   a.xt = fmaxf(a.xt, xt2);
 }
 
-__global__ __launch_bounds__(256) void vocab_combine_kernel(
+__global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     const VocabPartial* __restrict__ part, int n_vt, int R, float* __restrict__ lse_out,
     int64_t* __restrict__ tok_out, int64_t tok_stride, float* __restrict__ g_sel,
     int64_t gsel_stride, float* __restrict__ g_xe, int64_t gxe_stride,
     const int64_t* __restrict__ gt, int64_t gt_stride, int mode, float ss_prob,
     uint32_t seed, int step, int* __restrict__ counts, int count_step,
-    uint8_t* __restrict__ unfinished) {
+    uint8_t* __restrict__ unfinished, CellArgs cell) {
   __shared__ int s_nonzero;
+  int tok_final = 0;
   const int sub = threadIdx.x & (CMB_LANES - 1);
   const int r = blockIdx.x * CMB_ROWS + (threadIdx.x / CMB_LANES);
   const bool valid = r < R;
@@ -604,6 +654,58 @@ __global__ __launch_bounds__(256) void vocab_combine_kernel(
       tok_out[(int64_t)r * tok_stride] = tok;
       if (g_sel) g_sel[(int64_t)r * gsel_stride] = tl - lse;
       if (counts != nullptr && tok != 0) atomicAdd(&s_nonzero, 1);
+      tok_final = (int)tok;
+    }
+  }
+  if (cell.pre != nullptr && tok_out != nullptr) {
+    // the row's 32 lanes: lane k owns hidden units k, k + 32, ... (coalesced)
+    const int tk = __shfl(tok_final, (int)(threadIdx.x & 63) & ~(CMB_LANES - 1), 64);
+    if (valid) {
+      const int H = cell.H;
+      const float* prow = cell.pre + (int64_t)r * 4 * H;
+      const float* trow = cell.ptab + (int64_t)tk * 4 * H;
+      const float inv_keep = cell.drop_p > 0.f ? 1.f / (1.f - cell.drop_p) : 1.f;
+      // batches of CELL_U units: every load of a batch is issued before the
+      // first store (the stores could alias the inputs as far as the
+      // compiler knows, which would serialise each unit's loads)
+      constexpr int CELL_U = 8;
+      for (int u0 = sub; u0 < H; u0 += CMB_LANES * CELL_U) {
+        float4 p[CELL_U], x[CELL_U];
+        float cp[CELL_U];
+#pragma unroll
+        for (int k = 0; k < CELL_U; ++k) {
+          const int u = u0 + k * CMB_LANES;
+          if (u < H) {
+            p[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
+            x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
+            cp[k] = cell.c_prev[(int64_t)r * H + u];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < CELL_U; ++k) {
+          const int u = u0 + k * CMB_LANES;
+          if (u < H) {
+            const float gi = sigmoidf_(p[k].x + x[k].x), gf = sigmoidf_(p[k].y + x[k].y);
+            const float gg = tanhf_(p[k].z + x[k].z), go = sigmoidf_(p[k].w + x[k].w);
+            const int64_t o = (int64_t)r * H + u;
+            const float c = gf * cp[k] + gi * gg;
+            const float hv = go * tanhf_(c);
+            cell.c_out[o] = c;
+            cell.h_out[o] = f2bf(hv);
+            if (cell.hdrop_out) {
+              const bool keep =
+                  cell.drop_p <= 0.f || dropout_keep(cell.seed, cell.step, r, u, cell.drop_p);
+              cell.hdrop_out[(int64_t)r * cell.ldh + u] = f2bf(keep ? hv * inv_keep : 0.f);
+            }
+            if (cell.gates_out) {
+              uint2 pk;
+              pk.x = (uint32_t)f2bf(gi) | ((uint32_t)f2bf(gf) << 16);
+              pk.y = (uint32_t)f2bf(gg) | ((uint32_t)f2bf(go) << 16);
+              *reinterpret_cast<uint2*>(cell.gates_out + (int64_t)r * 4 * H + 4 * u) = pk;
+            }
+          }
+        }
+      }
     }
   }
   if (counts != nullptr && tok_out != nullptr) {
@@ -622,9 +724,10 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
     const float* __restrict__ lse, const int64_t* __restrict__ y_sel, int64_t ysel_rs,
     const float* __restrict__ dg_sel, int64_t dgsel_rs, const int64_t* __restrict__ y_xe,
     int64_t yxe_rs, const float* __restrict__ dg_xe, int64_t dgxe_rs,
-    float* __restrict__ colsum_part) {
-  const int64_t nrows = (int64_t)T * R;
-  const int64_t row0 = (int64_t)blockIdx.x * DS_ROWS;
+    float* __restrict__ colsum_part, int64_t row_begin, int64_t row_end) {
+  const int64_t nrows = row_end;
+  const int64_t row0 = row_begin + (int64_t)blockIdx.x * DS_ROWS;
+  const int64_t blk = row0 / DS_ROWS;  // global block index (row_begin % DS_ROWS == 0)
   const int nvec = V >> 3;
   float cs[DS_MAXCH][8];
 #pragma unroll
@@ -670,7 +773,7 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
       row[v] = f2bf(d);  // column sum added after the row loop
     }
   }
-  float* out = colsum_part + (int64_t)blockIdx.x * V;
+  float* out = colsum_part + blk * V;
 #pragma unroll
   for (int c = 0; c < DS_MAXCH; ++c) {
     const int i = threadIdx.x + c * 256;
@@ -796,24 +899,71 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
                           float ss_prob, uint32_t seed, int step, int* counts, int count_step,
-                          uint8_t* unfinished, hipStream_t stream) {
-  hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + CMB_ROWS - 1) / CMB_ROWS), dim3(256), 0,
+                          uint8_t* unfinished, hipStream_t stream, const CellLaunch* cl) {
+  CellArgs cell{};
+  if (cl != nullptr) {
+    cell = CellArgs{cl->pre, cl->ptab, cl->c_prev, cl->c_out, cl->h_out, cl->hdrop_out,
+                    cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->seed, cl->step};
+  }
+  hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + CMB_ROWS - 1) / CMB_ROWS), dim3(CMB_THREADS), 0,
                      stream,
                      (const VocabPartial*)part, n_vt, R, lse_out, tok_out, tok_stride, g_sel,
                      gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode, ss_prob, seed, step,
-                     counts, count_step, unfinished);
+                     counts, count_step, unfinished, cell);
+}
+
+template <int BN, int STAGES, int OCC>
+static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                                const float* bias, int V, uint16_t* logits16, int64_t ldl,
+                                void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
+                                float inv_temp, uint32_t seed, int step, const uint16_t* h_t,
+                                const uint16_t* whh, const float* vgate, int vdiv, float* pre,
+                                hipStream_t stream) {
+  using TL = Tile<VT_V, BN, STAGES>;
+  constexpr int LV = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
+                         ? TL::STAGES * TL::STAGE_BYTES
+                         : 4 * BN * (int)sizeof(GroupStat);
+  constexpr int LDS = LV > LGTile::LDS_BYTES ? LV : LGTile::LDS_BYTES;
+  const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
+  const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H) + 7) / 8 * 8 : 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC>), dim3(n_l + n_vt * n_rt), dim3(256),
+                     LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
+                     tgt, tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, n_l);
+}
+
+void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                           const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
+                           const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
+                           uint32_t seed, int step, const uint16_t* h_t, const uint16_t* whh,
+                           const float* vgate, int vdiv, float* pre, hipStream_t stream) {
+  if (R <= 64)
+    launch_vocab_lstm_t<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
+                                  flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, stream);
+  else
+    launch_vocab_lstm_t<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                   tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv,
+                                   pre, stream);
 }
 
 int vocab_bwd_ds_blocks(int T, int R) { return (int)(((int64_t)T * R + DS_ROWS - 1) / DS_ROWS); }
+int vocab_bwd_ds_rows() { return DS_ROWS; }
 
 void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
                          const float* lse, const int64_t* y_sel, int64_t ysel_rs,
                          const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
                          int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
-                         hipStream_t stream) {
-  hipLaunchKernelGGL(vocab_bwd_ds_kernel, dim3(vocab_bwd_ds_blocks(T, R)), dim3(256), 0, stream,
-                     buf, ldl, V, R, T, T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe,
-                     yxe_rs, dg_xe, dgxe_rs, colsum_part);
+                         int64_t row_begin, int64_t row_end, hipStream_t stream) {
+  if (row_end <= row_begin) return;
+  const int nb = (int)((row_end - row_begin + DS_ROWS - 1) / DS_ROWS);
+  hipLaunchKernelGGL(vocab_bwd_ds_kernel, dim3(nb), dim3(256), 0, stream, buf, ldl, V, R, T,
+                     T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe, yxe_rs, dg_xe, dgxe_rs,
+                     colsum_part, row_begin, row_end);
 }
 
 }  // namespace cst

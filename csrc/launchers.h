@@ -29,17 +29,41 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
                       int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
                       int64_t tgt_stride, int flags, float inv_temp, uint32_t seed, int step,
                       hipStream_t stream);  // flags: 1 = sample, 2 = argmax
+// Cell epilogue of the next step, fused into the combine (see lstm_gemm.h).
+struct CellLaunch {
+  const float* pre;
+  const float* ptab;
+  const float* c_prev;
+  float* c_out;
+  uint16_t* h_out;
+  uint16_t* hdrop_out;
+  int ldh;
+  uint16_t* gates_out;
+  int H;
+  float drop_p;
+  uint32_t seed;
+  int step;
+};
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
                           float ss_prob, uint32_t seed, int step, int* counts, int count_step,
-                          uint8_t* unfinished, hipStream_t stream);
+                          uint8_t* unfinished, hipStream_t stream, const CellLaunch* cell = nullptr);
+// vocab projection of step t + recurrent GEMM of step t+1 in one launch
+// (transposed-epilogue vocab kernel; pre == nullptr: vocab only)
+void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                           const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
+                           const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
+                           uint32_t seed, int step, const uint16_t* h_t, const uint16_t* whh,
+                           const float* vgate, int vdiv, float* pre, hipStream_t stream);
 int vocab_bwd_ds_blocks(int T, int R);
+// rows [row_begin, row_end) of the (T*R, ldl) buffer; row_begin % vocab_bwd_ds_rows() == 0
 void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
                          const float* lse, const int64_t* y_sel, int64_t ysel_rs,
                          const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
                          int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
-                         hipStream_t stream);
+                         int64_t row_begin, int64_t row_end, hipStream_t stream);
+int vocab_bwd_ds_rows();
 
 // lstm.hip
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
