@@ -22,6 +22,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index);
+double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
+                          int64_t iters);
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
                        int64_t flags, bool save, int64_t iters);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
@@ -90,6 +92,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flat_adam_step", &cst::flat_adam_step);
   m.def("set_vocab_variant", &cst::set_vocab_variant);
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
+  m.def("vocab_bwd_ds_bench", &cst::vocab_bwd_ds_bench);
   m.def("beam_search", &cst::beam_search);
   m.def("set_lstm_fwd_variant", &cst::set_lstm_fwd_variant);
 }

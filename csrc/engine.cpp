@@ -18,6 +18,7 @@
 //                   then the batched weight-gradient GEMMs.
 #include <torch/extension.h>
 #include <cstdlib>
+#include <map>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -272,7 +273,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   hipEvent_t ev_ready = ev[n_chunks], ev_done = ev[n_chunks + 1];
   (void)hipEventRecord(ev_ready, st);
   {
-    auto side = c10::hip::getStreamFromPool(false, dev.index());
+    // one persistent side stream per device: pool streams rotate, and every
+    // new stream pays hipBLASLt handle/workspace setup on first use
+    static std::map<int, c10::hip::HIPStream> side_streams;
+    auto it = side_streams.find(dev.index());
+    if (it == side_streams.end())
+      it = side_streams.emplace(dev.index(), c10::hip::getStreamFromPool(false, dev.index())).first;
+    auto side = it->second;
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
     for (int c = n_chunks - 1; c >= 0; --c) {
@@ -477,6 +484,35 @@ double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tens
   (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, st);
   for (int i = 0; i < iters; ++i) launch(i);
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 1000.0 * ms / (double)iters;
+}
+
+double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
+                          int64_t iters) {
+  const int64_t n = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
+  const int64_t V = ldl;  // benchmark over the padded width
+  const int64_t T_sel = seq.size(1);
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(logits16.device());
+  at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n, (int)R), V}, f32);
+  hipStream_t st = cur_stream();
+  auto launch = [&]() {
+    launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
+                        (int)n, (int)T_sel, lse.data_ptr<float>(), seq.data_ptr<int64_t>(), T_sel,
+                        dg_sel.data_ptr<float>(), T_sel, nullptr, 0, nullptr, 0,
+                        colsum.data_ptr<float>(), 0, n * R, st);
+  };
+  launch();
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < iters; ++i) launch();
   (void)hipEventRecord(e1, st);
   (void)hipEventSynchronize(e1);
   float ms = 0.f;

@@ -604,8 +604,26 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   const int r = blockIdx.x * CMB_ROWS + (threadIdx.x / CMB_LANES);
   const bool valid = r < R;
   if (threadIdx.x == 0) s_nonzero = 0;
+  // The cell epilogue's token-independent operands (pre-activations of the
+  // row, c_{t}) are loaded first, so their latency overlaps the merge below.
+  constexpr int CELL_PF = 16;  // units per lane held in registers (H <= 512)
+  const bool do_cell = cell.pre != nullptr && tok_out != nullptr;
+  const bool pf = do_cell && cell.H <= CMB_LANES * CELL_PF;
+  float4 pf_p[CELL_PF];
+  float pf_c[CELL_PF];
+  if (pf && valid) {
+#pragma unroll
+    for (int k = 0; k < CELL_PF; ++k) {
+      const int u = sub + k * CMB_LANES;
+      if (u < cell.H) {
+        pf_p[k] = *reinterpret_cast<const float4*>(cell.pre + ((int64_t)r * cell.H + u) * 4);
+        pf_c[k] = cell.c_prev[(int64_t)r * cell.H + u];
+      }
+    }
+  }
   RowStat a = {-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff};
   if (valid) {
+#pragma unroll 4
     for (int t = sub; t < n_vt; t += CMB_LANES) {
       const VocabPartial p = part[(int64_t)t * R + r];
       merge_stat(a, p.m, p.s, p.zval, p.zlogit, p.zidx, p.m, p.xidx, p.xtgt);
@@ -657,10 +675,45 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
       tok_final = (int)tok;
     }
   }
-  if (cell.pre != nullptr && tok_out != nullptr) {
+  if (do_cell) {
     // the row's 32 lanes: lane k owns hidden units k, k + 32, ... (coalesced)
     const int tk = __shfl(tok_final, (int)(threadIdx.x & 63) & ~(CMB_LANES - 1), 64);
-    if (valid) {
+    if (valid && pf) {
+      const int H = cell.H;
+      const float* trow = cell.ptab + (int64_t)tk * 4 * H;
+      const float inv_keep = cell.drop_p > 0.f ? 1.f / (1.f - cell.drop_p) : 1.f;
+      float4 x[CELL_PF];
+#pragma unroll
+      for (int k = 0; k < CELL_PF; ++k) {
+        const int u = sub + k * CMB_LANES;
+        if (u < H) x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
+      }
+#pragma unroll
+      for (int k = 0; k < CELL_PF; ++k) {
+        const int u = sub + k * CMB_LANES;
+        if (u < H) {
+          const float4 p = pf_p[k];
+          const float gi = sigmoidf_(p.x + x[k].x), gf = sigmoidf_(p.y + x[k].y);
+          const float gg = tanhf_(p.z + x[k].z), go = sigmoidf_(p.w + x[k].w);
+          const int64_t o = (int64_t)r * H + u;
+          const float c = gf * pf_c[k] + gi * gg;
+          const float hv = go * tanhf_(c);
+          cell.c_out[o] = c;
+          cell.h_out[o] = f2bf(hv);
+          if (cell.hdrop_out) {
+            const bool keep =
+                cell.drop_p <= 0.f || dropout_keep(cell.seed, cell.step, r, u, cell.drop_p);
+            cell.hdrop_out[(int64_t)r * cell.ldh + u] = f2bf(keep ? hv * inv_keep : 0.f);
+          }
+          if (cell.gates_out) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(gi) | ((uint32_t)f2bf(gf) << 16);
+            pk.y = (uint32_t)f2bf(gg) | ((uint32_t)f2bf(go) << 16);
+            *reinterpret_cast<uint2*>(cell.gates_out + (int64_t)r * 4 * H + 4 * u) = pk;
+          }
+        }
+      }
+    } else if (valid) {
       const int H = cell.H;
       const float* prow = cell.pre + (int64_t)r * 4 * H;
       const float* trow = cell.ptab + (int64_t)tk * 4 * H;
@@ -716,38 +769,48 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
 
 // DS_ROWS rows of the [T*R][ldl] buffer per block.  Each thread owns the same
 // 8-column chunks in every row, so the bias gradient (column sums of dS) is
-// accumulated in registers and written once per block as a partial row.
+// accumulated in registers and written once per block as a partial row.  The
+// per-row scalars are staged in LDS up front (no dependent scalar loads in
+// the row loop); NCH = chunks per thread is a compile-time constant.
 constexpr int DS_ROWS = 64, DS_MAXCH = 8;  // V <= DS_MAXCH * 2048
 
+template <int NCH>
 __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
     uint16_t* __restrict__ buf, int64_t ldl, int V, int R, int T, int T_sel,
     const float* __restrict__ lse, const int64_t* __restrict__ y_sel, int64_t ysel_rs,
     const float* __restrict__ dg_sel, int64_t dgsel_rs, const int64_t* __restrict__ y_xe,
     int64_t yxe_rs, const float* __restrict__ dg_xe, int64_t dgxe_rs,
     float* __restrict__ colsum_part, int64_t row_begin, int64_t row_end) {
-  const int64_t nrows = row_end;
   const int64_t row0 = row_begin + (int64_t)blockIdx.x * DS_ROWS;
   const int64_t blk = row0 / DS_ROWS;  // global block index (row_begin % DS_ROWS == 0)
   const int nvec = V >> 3;
-  float cs[DS_MAXCH][8];
-#pragma unroll
-  for (int c = 0; c < DS_MAXCH; ++c)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cs[c][k] = 0.f;
-  for (int rr = 0; rr < DS_ROWS; ++rr) {
-    const int64_t rowid = row0 + rr;
-    if (rowid >= nrows) break;
+  const int nr = (int)min((int64_t)DS_ROWS, row_end - row0);
+  __shared__ float s_a[DS_ROWS], s_b[DS_ROWS], s_L[DS_ROWS];
+  __shared__ int s_ys[DS_ROWS], s_yx[DS_ROWS];
+  if ((int)threadIdx.x < nr) {
+    const int64_t rowid = row0 + threadIdx.x;
     const int t = (int)(rowid / R), r = (int)(rowid % R);
     const bool has_sel = dg_sel != nullptr && t < T_sel;
-    const float a = has_sel ? dg_sel[(int64_t)r * dgsel_rs + t] : 0.f;
-    const float bb = dg_xe ? dg_xe[(int64_t)r * dgxe_rs + t] : 0.f;
-    const int ys = has_sel ? (int)y_sel[(int64_t)r * ysel_rs + t] : -1;
-    const int yx = dg_xe ? (int)y_xe[(int64_t)r * yxe_rs + t] : -1;
-    const float L = lse[rowid];
+    s_a[threadIdx.x] = has_sel ? dg_sel[(int64_t)r * dgsel_rs + t] : 0.f;
+    s_b[threadIdx.x] = dg_xe ? dg_xe[(int64_t)r * dgxe_rs + t] : 0.f;
+    s_ys[threadIdx.x] = has_sel ? (int)y_sel[(int64_t)r * ysel_rs + t] : -1;
+    s_yx[threadIdx.x] = dg_xe ? (int)y_xe[(int64_t)r * yxe_rs + t] : -1;
+    s_L[threadIdx.x] = lse[rowid];
+  }
+  __syncthreads();
+  float cs[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs[c][k] = 0.f;
+  for (int rr = 0; rr < nr; ++rr) {
+    const int64_t rowid = row0 + rr;
+    const float a = s_a[rr], bb = s_b[rr], L = s_L[rr];
+    const int ys = s_ys[rr], yx = s_yx[rr];
     const float ab = a + bb;
     uint16_t* row = buf + rowid * ldl;
 #pragma unroll
-    for (int c = 0; c < DS_MAXCH; ++c) {
+    for (int c = 0; c < NCH; ++c) {
       const int i = threadIdx.x + c * 256;
       if (i < nvec) {
         uint4 x = *reinterpret_cast<const uint4*>(row + i * 8);
@@ -775,22 +838,18 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
   }
   float* out = colsum_part + blk * V;
 #pragma unroll
-  for (int c = 0; c < DS_MAXCH; ++c) {
+  for (int c = 0; c < NCH; ++c) {
     const int i = threadIdx.x + c * 256;
     if (i < nvec) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) out[i * 8 + k] = cs[c][k];
+      for (int k = 0; k < 8; ++k) out[i * 8 + k] = cs[c][k];  // row stride V: unaligned
     }
   }
   // tail columns: re-sum from the (already converted) buffer
   if (threadIdx.x < (V & 7)) {
     const int v = (nvec << 3) + threadIdx.x;
     float acc = 0.f;
-    for (int rr = 0; rr < DS_ROWS; ++rr) {
-      const int64_t rowid = row0 + rr;
-      if (rowid >= nrows) break;
-      acc += bf2f(buf[rowid * ldl + v]);
-    }
+    for (int rr = 0; rr < nr; ++rr) acc += bf2f(buf[(row0 + rr) * ldl + v]);
     out[v] = acc;
   }
 }
@@ -961,9 +1020,22 @@ void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_
                          int64_t row_begin, int64_t row_end, hipStream_t stream) {
   if (row_end <= row_begin) return;
   const int nb = (int)((row_end - row_begin + DS_ROWS - 1) / DS_ROWS);
-  hipLaunchKernelGGL(vocab_bwd_ds_kernel, dim3(nb), dim3(256), 0, stream, buf, ldl, V, R, T,
-                     T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe, yxe_rs, dg_xe, dgxe_rs,
-                     colsum_part, row_begin, row_end);
+  const int nch = ((V >> 3) + 255) / 256;
+#define DS_LAUNCH(N)                                                                          \
+  hipLaunchKernelGGL(vocab_bwd_ds_kernel<N>, dim3(nb), dim3(256), 0, stream, buf, ldl, V, R, T, \
+                     T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe, yxe_rs, dg_xe, dgxe_rs, \
+                     colsum_part, row_begin, row_end)
+  switch (nch) {
+    case 1: DS_LAUNCH(1); break;
+    case 2: DS_LAUNCH(2); break;
+    case 3: DS_LAUNCH(3); break;
+    case 4: DS_LAUNCH(4); break;
+    case 5: DS_LAUNCH(5); break;
+    case 6: DS_LAUNCH(6); break;
+    case 7: DS_LAUNCH(7); break;
+    default: DS_LAUNCH(8); break;
+  }
+#undef DS_LAUNCH
 }
 
 }  // namespace cst

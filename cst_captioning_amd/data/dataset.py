@@ -220,18 +220,53 @@ class CaptionLoader:
         return np.array(take, dtype=np.int64)
 
     def _caption_rows(self, vids):
+        """``seq_per_img`` label rows per video (dataloader.py:119-131): all
+        captions in order plus uniform random repeats when ncap <= S, a
+        uniformly random subset in random order when ncap > S.  Vectorised
+        over the batch (the per-video Python loop cost ~0.5 ms per step)."""
         S = self.seq_per_img
-        rows = np.empty((len(vids), S), dtype=np.int64)
-        for i, v in enumerate(vids):
-            s, e = self.ds.label_start_ix[v], self.ds.label_end_ix[v]
-            ncap = e - s
-            if ncap <= S:
-                pick = np.concatenate([np.arange(ncap),
-                                       self._cap_rng.randint(ncap, size=S - ncap)])
-            else:
-                pick = self._cap_rng.permutation(ncap)[:S]
-            rows[i] = s + pick
-        return rows.reshape(-1)
+        st = self.ds.label_start_ix[vids].astype(np.int64)
+        ncap = self.ds.label_end_ix[vids].astype(np.int64) - st
+        j = np.arange(S, dtype=np.int64)[None, :]
+        pick = np.broadcast_to(j, (len(vids), S)).copy()
+        short = ncap < S
+        if short.any():
+            nc = ncap[short][:, None]
+            rep = (self._cap_rng.random_sample((int(short.sum()), S)) * nc).astype(np.int64)
+            pick[short] = np.where(j < nc, j, np.minimum(rep, nc - 1))
+        long_ = ncap > S
+        if long_.any():
+            nc = ncap[long_][:, None]
+            keys = self._cap_rng.random_sample((int(long_.sum()), int(nc.max())))
+            keys[np.arange(keys.shape[1])[None, :] >= nc] = np.inf
+            pick[long_] = np.argsort(keys, axis=1)[:, :S]
+        return (st[:, None] + pick).reshape(-1)
+
+    def _to_device(self, *arrays):
+        """int64 host arrays -> device tensors through one pinned staging
+        buffer and one asynchronous copy (pageable copies block the host)."""
+        if self.device.type != 'cuda':
+            return [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
+        sizes = [len(a) for a in arrays]
+        n = sum(sizes)
+        if getattr(self, '_pin', None) is None or self._pin.numel() < n:
+            self._pin = torch.empty(max(n, 1 << 16), dtype=torch.int64).pin_memory()
+            self._pin_event = None
+        if self._pin_event is not None:
+            self._pin_event.synchronize()  # previous copy out of the buffer is done
+        host = self._pin.numpy()
+        off = 0
+        for a, k in zip(arrays, sizes):
+            host[off:off + k] = a
+            off += k
+        dev = self._pin[:n].to(self.device, non_blocking=True)
+        self._pin_event = torch.cuda.Event()
+        self._pin_event.record()
+        out, off = [], 0
+        for k in sizes:
+            out.append(dev[off:off + k])
+            off += k
+        return out
 
     def get_batch(self):
         return self._assemble(self._next_videos())
@@ -247,13 +282,15 @@ class CaptionLoader:
 
     def _assemble(self, vids):
         dev = self.ds.device_tensors(self.device)
-        vid_t = torch.from_numpy(vids).to(self.device, non_blocking=True)
+        rows = self._caption_rows(vids) if self.has_label else None
+        if rows is not None:
+            vid_t, rows_t = self._to_device(vids, rows)
+        else:
+            vid_t, = self._to_device(vids)
         data = {'video_index': vid_t, 'vids': vids,
                 'ids': self.ds.video_ids[vids].tolist(),
                 'feats': [f.index_select(0, vid_t) for f in dev['feats']]}
         if self.has_label:
-            rows = self._caption_rows(vids)
-            rows_t = torch.from_numpy(rows).to(self.device, non_blocking=True)
             labels = dev['labels'].index_select(0, rows_t)
             n = (labels != 0).sum(1, keepdim=True) + 1
             pos = torch.arange(labels.shape[1], device=labels.device)[None, :]

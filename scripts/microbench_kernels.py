@@ -36,4 +36,14 @@ for R in (1280, 64):
                                    flags, save, 50)
             res['R%d_v%d_%s' % (R, var, name)] = round(us, 2)
 C.set_vocab_variant(4)
+if os.environ.get('DS', '1') == '1':
+    n, R = 28, 1280
+    ldl = (V + 7) // 8 * 8
+    lg = (torch.randn(n, R, ldl, device=dev) * 2).half()
+    lse = torch.full((n, R), 12.0, device=dev)
+    seq = torch.randint(0, V, (R, n), device=dev)
+    dg = torch.randn(R, n, device=dev) * 1e-3
+    us = C.vocab_bwd_ds_bench(lg, lse, seq, dg, 10)
+    res['ds_T28_R1280_us'] = round(us, 1)
+    res['ds_TBps'] = round(2 * lg.numel() * 2 / us / 1e6, 2)
 print(json.dumps(res))

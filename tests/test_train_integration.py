@@ -47,8 +47,8 @@ def _setup(extra, seed=0):
 def test_xe_loss_decreases():
     opt, tr, _ = _setup(['--max_epochs', '100'])
     data = tr.train_loader.get_batch()
-    losses = [float(tr.train_step(data, 0)['loss']) for _ in range(40)]
-    assert losses[-1] < 0.7 * losses[0]
+    losses = [float(tr.train_step(data, 0)["loss"]) for _ in range(60)]
+    assert losses[-1] < 0.75 * losses[0]
 
 
 @pytest.mark.parametrize('recipe', [
