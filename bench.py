@@ -53,6 +53,8 @@ def parse():
     p.add_argument('--vocab', type=int, default=10509)
     p.add_argument('--seed', type=int, default=123)
     p.add_argument('--json_out', default='')
+    p.add_argument('--profile_phases', type=int, default=0,
+                   help='print the mean per-phase GPU time (HIP events) of the timed steps')
     p.add_argument('--sync_debug', type=int, default=0,
                    help='after warmup: report host-synchronising calls and host enqueue time of one step')
     return p.parse_args()
@@ -82,7 +84,8 @@ def main():
         use_rl=1 if a.mode != 'xe' else 0, use_rl_after=0, use_cst=1 if a.mode == 'cst' else 0,
         use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=2, scb_captions=S,
         impl=a.impl, precision=a.precision, reward_device=a.reward,
-        dedupe_greedy=a.dedupe_greedy, seed=a.seed, loglevel='WARNING', save_last=0)
+        dedupe_greedy=a.dedupe_greedy, seed=a.seed, loglevel='WARNING', save_last=0,
+        profile_phases=a.profile_phases)
     opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
     opt.vocab_size = ds.vocab_size
     opt.seq_length = ds.seq_length
@@ -120,8 +123,12 @@ def main():
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
+    phases = {}
     for _ in range(a.steps):
         out = step()
+        if a.profile_phases:  # reads the events: synchronises, diagnostic only
+            for k, v in trainer.timer.summary().items():
+                phases[k] = phases.get(k, 0.0) + v / a.steps
     sync()
     ctx.barrier()
     sync()
@@ -151,6 +158,8 @@ def main():
                    'dedupe_greedy': a.dedupe_greedy},
         'final_loss': loss, 'datagen_s': round(t_gen, 1),
     }
+    if phases:
+        rec['phases_ms'] = {k: round(v, 3) for k, v in phases.items()}
     if ctx.is_main:
         line = json.dumps(rec)
         print(line, flush=True)

@@ -233,7 +233,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor hdrop_all, at::Tensor gates_all,
                                          at::Tensor c_all, at::Tensor h_all, at::Tensor seq,
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
-                                         at::Tensor dg_xe, double drop_p, int64_t seed) {
+                                         at::Tensor dg_xe, double drop_p, int64_t seed,
+                                         at::Tensor out_wlog, at::Tensor out_blog,
+                                         int64_t comm_stream) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -259,7 +261,19 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor dS = logits16.view(at::kBFloat16).view({NR, ldl}).narrow(1, 0, V);
   at::Tensor hd2 = hdrop_all.view({NR, H + HAUG}).narrow(1, 0, H);
   at::Tensor dHd = at::empty({NR, H}, f32);
-  at::Tensor dWlog = at::empty({V, H}, f32);
+  // early gradients (DP overlap): dWlog / dblog written straight into the
+  // caller's gradient buffers on the side stream, and the caller's
+  // communication stream made to wait for them, so their all-reduce runs
+  // under the reverse LSTM loop
+  const bool early = out_wlog.defined() && out_wlog.numel() > 0;
+  if (early) {
+    TORCH_CHECK(out_wlog.scalar_type() == at::kFloat && out_wlog.is_contiguous() &&
+                    out_wlog.size(0) == V && out_wlog.size(1) == H,
+                "out_wlog must be a contiguous fp32 (V, H) tensor");
+    TORCH_CHECK(out_blog.scalar_type() == at::kFloat && out_blog.numel() == V, "out_blog shape");
+  }
+  at::Tensor dWlog = early ? out_wlog : at::empty({V, H}, f32);
+  at::Tensor dblog;
   const int64_t DR = vocab_bwd_ds_rows();
   static const int max_chunks = [] {
     const char* e = std::getenv("CSTCAP_BWD_CHUNKS");  // A/B knob for the pipeline depth
@@ -297,7 +311,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       (void)hipEventRecord(ev[c], side.stream());
     }
     at::mm_out(dWlog, dS.t(), hd2, at::kFloat);
+    if (early) {
+      dblog = out_blog.view({V});
+      at::sum_out(dblog, colsum, {0});
+    }
     (void)hipEventRecord(ev_done, side.stream());
+    if (early && comm_stream != 0)
+      (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
   }
   at::Tensor dG_all = at::empty({n_steps, R, H4}, wx.options());
   at::Tensor dc = at::zeros({R, H}, f32);
@@ -317,7 +337,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), st);
   }
   while (waited > 0) (void)hipStreamWaitEvent(st, ev[--waited], 0);
-  at::Tensor dblog = colsum.sum(0);                                     // (V)
+  if (!early) dblog = colsum.sum(0);                                    // (V)
   // 4. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
   //    reductions run as batched GEMMs over groups of steps (many more output
   //    tiles in flight than one K = 35k GEMM), summed afterwards.

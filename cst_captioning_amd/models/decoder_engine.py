@@ -88,11 +88,20 @@ class _DecoderFn(torch.autograd.Function):
         # input token of every step: it_0 = BOS / labels[:, 0], it_t = seq[:, t-1]
         first = labels[:, :1] if labels is not None else bos.view(-1, 1)
         toks = torch.cat([first, seq[:, :n_steps - 1]], 1).t().reshape(-1)
+        # DP overlap: the vocab-head weight gradients go straight into their
+        # flat-bucket slots and are all-reduced during the reverse LSTM loop
+        hook = getattr(eng, 'early_grad_hook', None)
+        early = hook is not None and hook.active
+        out_w, out_b, comm = (hook.out_wlog, hook.out_blog, hook.comm_ptr) if early \
+            else (empty, empty, 0)
         dWx, dWlog, dblog, d_emb, dvg = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
-            ctx.drop_p, ctx.seed)
+            ctx.drop_p, ctx.seed, out_w, out_b, comm)
+        if early:
+            hook.launch()
+            dWlog = dblog = None  # already in the gradient buffers
         E = eng.E
         d_orig = dWx.index_select(0, eng.inv_perm)
         w_ih_shape, emb_shape = ctx.shapes

@@ -118,13 +118,18 @@ def init_distributed(device_type=None, timeout_s=600):
     if device_type is None:
         device_type = 'cuda' if torch.cuda.is_available() else 'cpu'
     if device_type == 'cuda':
+        # one GPU per local rank; CSTCAP_SHARE_GPU=1 folds ranks onto the visible
+        # devices (multi-rank tests on a one-GPU box, with the gloo backend)
+        if os.environ.get('CSTCAP_SHARE_GPU') == '1':
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device('cuda', local)
     else:
         device = torch.device('cpu')
     backend = None
     if world > 1:
-        backend = 'nccl' if device_type == 'cuda' else 'gloo'
+        backend = os.environ.get('CSTCAP_DIST_BACKEND') or ('nccl' if device_type == 'cuda'
+                                                            else 'gloo')
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         kw = {}
         if backend == 'nccl':
@@ -132,6 +137,47 @@ def init_distributed(device_type=None, timeout_s=600):
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistContext(rank, world, local, device, backend)
+
+
+class EarlyAllReduce:
+    """Overlap of the gradient all-reduce with the backward (C2).
+
+    The fused decoder's backward produces the vocabulary-head gradients
+    (logit weight + bias, ~26 % of the parameters) before its reverse LSTM
+    loop (~0.5-0.8 ms).  With this hook the engine writes them straight into
+    their slots of the flat bucket (which places them first), makes
+    ``comm_stream`` wait for them, and :meth:`launch` starts their
+    all-reduce there -- it runs under the LSTM loop.  The rest of the bucket
+    is reduced after ``backward()`` and :meth:`FlatGradBucket.all_reduce`
+    joins both.
+    """
+
+    def __init__(self, ctx, bucket, params):
+        self.ctx = ctx
+        self.bucket = bucket
+        self.n = bucket.prefix_numel(params)
+        self.out_wlog, self.out_blog = (p.grad for p in params)
+        self.stream = torch.cuda.Stream(device=ctx.device) if ctx.device.type == 'cuda' else None
+        self.comm_ptr = self.stream.cuda_stream if self.stream is not None else 0
+        self.active = ctx.enabled
+        self.work = None
+
+    def launch(self):
+        view = self.bucket.grad[:self.n]
+        if self.stream is not None:
+            with torch.cuda.stream(self.stream):  # waits on the engine's event
+                self.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True)
+        else:
+            self.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True)
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            if self.stream is not None:
+                torch.cuda.current_stream(self.ctx.device).wait_stream(self.stream)
+            self.work = None
+            return True
+        return False
 
 
 class FlatGradBucket:
@@ -143,8 +189,14 @@ class FlatGradBucket:
     clip + Adam kernel cover every parameter.
     """
 
-    def __init__(self, params):
-        self.params = [p for p in params if p.requires_grad]
+    def __init__(self, params, first=()):
+        """``first``: parameters placed at the start of the buffer (the ones
+        an :class:`EarlyAllReduce` reduces ahead of the rest)."""
+        params = [p for p in params if p.requires_grad]
+        first_ids = {id(p) for p in first}
+        self.params = [p for p in params if id(p) in first_ids] + \
+            [p for p in params if id(p) not in first_ids]
+        self.early = None
         if not self.params:
             raise ValueError('no trainable parameters')
         dev = self.params[0].device
@@ -169,10 +221,20 @@ class FlatGradBucket:
             if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
                 p.grad = self.grad[off:off + n].view_as(p)
 
+    def prefix_numel(self, params):
+        """Elements of the leading slots holding exactly ``params``."""
+        n = 0
+        for p, want in zip(self.params, params):
+            if p is not want:
+                raise ValueError('parameters are not the leading slots of the bucket')
+            n += p.numel()
+        return n
+
     def all_reduce(self, ctx):
         if ctx.enabled:
-            if ctx.backend == 'nccl':
-                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
-            else:
-                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+            early = self.early is not None and self.early.work is not None
+            rest = self.grad[self.early.n:] if early else self.grad
+            dist.all_reduce(rest, op=dist.ReduceOp.SUM)
+            if early:
+                self.early.wait()
             self.grad.div_(ctx.world_size)

@@ -86,7 +86,12 @@ class Trainer:
         self.xe_criterion = CrossEntropyCriterion()
         self.rl_criterion = RewardCriterion()
         self.ctx.broadcast_module(model)
-        self.bucket = FlatGradBucket(model.parameters())
+        early = [model.logit.weight, model.logit.bias]
+        self.bucket = FlatGradBucket(model.parameters(), first=early)
+        if engine is not None and self.ctx.enabled and not getattr(opt, 'no_early_allreduce', 0):
+            from ..parallel.dist import EarlyAllReduce
+            self.bucket.early = EarlyAllReduce(self.ctx, self.bucket, early)
+            engine.early_grad_hook = self.bucket.early
         if getattr(opt, 'honor_optim_flags', 0):
             betas, eps = (opt.optim_alpha, opt.optim_beta), opt.optim_epsilon
         else:

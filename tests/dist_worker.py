@@ -1,6 +1,7 @@
 """Worker for tests/test_dist.py, launched by torchrun (gloo on CPU, or RCCL
 on GPUs): one XE gradient all-reduce, two optimizer steps, and a sharded
 validation.  Writes rank 0's results to ``argv[1]`` (torch.save)."""
+import os
 import sys
 
 import torch
@@ -12,10 +13,11 @@ from cst_captioning_amd.parallel import init_distributed
 from cst_captioning_amd.train.trainer import Trainer
 
 ARGS = ['--synthetic', 'msvd', '--synthetic_videos', '24', '--synthetic_vocab', '40',
-        '--seq_length', '10', '--rnn_size', '32', '--input_encoding_size', '32',
+        '--seq_length', '10', '--rnn_size', '64', '--input_encoding_size', '64',
         '--feat_dims', '16', '8', '--batch_size', '4', '--train_seq_per_img', '3',
         '--test_batch_size', '3', '--test_seq_per_img', '3', '--beam_size', '2',
-        '--impl', 'torch', '--loglevel', 'WARNING', '--drop_prob_lm', '0',
+        '--impl', os.environ.get('CSTCAP_TEST_IMPL', 'torch'), '--loglevel', 'WARNING',
+        '--drop_prob_lm', '0',
         '--learning_rate', '1e-3', '--language_eval', '0']
 
 
