@@ -52,6 +52,9 @@ def parse():
     p.add_argument('--videos', type=int, default=6513)
     p.add_argument('--vocab', type=int, default=10509)
     p.add_argument('--seed', type=int, default=123)
+    p.add_argument('--num_chunks', type=int, default=1,
+                   help='frames per video; > 1 enables temporal attention (the reference '
+                        'default, and the headline config, is 1: mean-pooled features)')
     p.add_argument('--json_out', default='')
     p.add_argument('--profile_phases', type=int, default=0,
                    help='print the mean per-phase GPU time (HIP events) of the timed steps')
@@ -74,13 +77,14 @@ def main():
         os.environ['CSTCAP_ALLOW_TORCH_FALLBACK'] = '1'
     seed_everything(a.seed, ctx.rank)
     t_gen = time.time()
-    ds = make_synthetic('msrvtt', num_videos=a.videos, vocab_size=a.vocab, seed=a.seed)
+    ds = make_synthetic('msrvtt', num_videos=a.videos, vocab_size=a.vocab, seed=a.seed,
+                        num_chunks=a.num_chunks)
     t_gen = time.time() - t_gen
     S = 20
     opt = default_opts(
         batch_size=a.batch_size, train_seq_per_img=S, test_seq_per_img=S, rnn_size=512,
         input_encoding_size=512, drop_prob_lm=0.5, learning_rate=1e-4, grad_clip=0.25,
-        model_type='concat', eval_metric='CIDEr', max_epochs=10 ** 9, print_log_interval=0,
+        model_type='concat', num_chunks=a.num_chunks, eval_metric='CIDEr', max_epochs=10 ** 9, print_log_interval=0,
         use_rl=1 if a.mode != 'xe' else 0, use_rl_after=0, use_cst=1 if a.mode == 'cst' else 0,
         use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=2, scb_captions=S,
         impl=a.impl, precision=a.precision, reward_device=a.reward,
@@ -155,7 +159,8 @@ def main():
                    'videos_per_gpu': a.batch_size, 'seq_per_img': S, 'seq_len': 30,
                    'parallelism': 'dp%d' % ctx.world_size, 'impl': a.impl,
                    'reward': a.reward, 'mode': a.mode, 'params': n_params,
-                   'dedupe_greedy': a.dedupe_greedy},
+                   'dedupe_greedy': a.dedupe_greedy,
+                   'temporal_attention_frames': a.num_chunks if a.num_chunks > 1 else None},
         'final_loss': loss, 'datagen_s': round(t_gen, 1),
     }
     if phases:

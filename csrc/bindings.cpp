@@ -12,7 +12,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         std::vector<int64_t> modes, double ss_prob,
                                         double drop_p, double temperature, int64_t seed,
                                         bool save, bool want_xe, bool use_counts,
-                                        bool use_unfinished);
+                                        bool use_unfinished, std::vector<at::Tensor> att);
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -20,10 +20,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
                                          at::Tensor dg_xe, double drop_p, int64_t seed,
                                          at::Tensor out_wlog, at::Tensor out_blog,
-                                         int64_t comm_stream);
+                                         int64_t comm_stream, std::vector<at::Tensor> att);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
-                                    int64_t K, int64_t T, int64_t bos_index);
+                                    int64_t K, int64_t T, int64_t bos_index,
+                                    std::vector<at::Tensor> att);
 double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
                           int64_t iters);
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,

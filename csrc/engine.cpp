@@ -53,16 +53,19 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         std::vector<int64_t> modes, double ss_prob,
                                         double drop_p, double temperature, int64_t seed,
                                         bool save, bool want_xe, bool use_counts,
-                                        bool use_unfinished) {
+                                        bool use_unfinished, std::vector<at::Tensor> att) {
   check_cuda(wx, "wx");
   check_cuda(emb, "emb");
   check_cuda(wlog, "wlog");
   check_cuda(blog, "blog");
-  check_cuda(vgate, "vgate");
+  // temporal attention (num_chunks > 1): att = {Gv (Bv, C, 4H) f32 packed gates,
+  // P (Bv, C, A) f32, W_q (A, H) bf16, w_a (A) f32, b_a (1) f32}; vgate unused
+  const bool has_att = !att.empty();
+  if (!has_att) check_cuda(vgate, "vgate");
   TORCH_CHECK(wx.scalar_type() == at::kBFloat16 && emb.scalar_type() == at::kBFloat16 &&
                   wlog.scalar_type() == at::kBFloat16,
               "decoder weights must be bf16");
-  TORCH_CHECK(vgate.scalar_type() == at::kFloat, "vgate must be fp32");
+  if (!has_att) TORCH_CHECK(vgate.scalar_type() == at::kFloat, "vgate must be fp32");
   check_cuda(ptab, "ptab");
   check_cuda(whh, "whh");
   TORCH_CHECK(ptab.scalar_type() == at::kFloat && ptab.size(0) == emb.size(0) &&
@@ -73,7 +76,27 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   TORCH_CHECK(wx.size(1) == E + H, "wx must be (4H, E+H)");
   TORCH_CHECK(E % 64 == 0 && H % 64 == 0, "E and H must be multiples of 64");
   TORCH_CHECK(wlog.size(1) == H && blog.numel() == V, "logit weight shape");
-  TORCH_CHECK(vgate.size(1) == H4 && vgate.size(0) * vgate_div >= R, "vgate shape");
+  if (!has_att)
+    TORCH_CHECK(vgate.size(1) == H4 && vgate.size(0) * vgate_div >= R, "vgate shape");
+  at::Tensor a_gv, a_pre, a_wq, a_wa, a_ba;
+  int64_t Bv = 0, C = 0, A = 0;
+  if (has_att) {
+    TORCH_CHECK(att.size() == 5, "att = {Gv, P, W_q, w_a, b_a}");
+    a_gv = att[0], a_pre = att[1], a_wq = att[2], a_wa = att[3], a_ba = att[4];
+    for (auto* t : {&a_gv, &a_pre, &a_wq, &a_wa, &a_ba}) check_cuda(*t, "attention operand");
+    Bv = a_gv.size(0), C = a_gv.size(1), A = a_pre.size(2);
+    TORCH_CHECK(a_gv.scalar_type() == at::kFloat && a_gv.dim() == 3 && a_gv.size(2) == H4,
+                "Gv must be fp32 (Bv, C, 4H)");
+    TORCH_CHECK(a_pre.scalar_type() == at::kFloat && a_pre.dim() == 3 && a_pre.size(0) == Bv &&
+                    a_pre.size(1) == C, "P must be fp32 (Bv, C, A)");
+    TORCH_CHECK(A % 64 == 0 && C >= 1 && C <= 32 && att_lds_need((int)C, (int)A) <= att_max_lds(),
+                "attention: A % 64 == 0, C <= 32 and the frame tile must fit in LDS");
+    TORCH_CHECK(a_wq.scalar_type() == at::kBFloat16 && a_wq.size(0) == A && a_wq.size(1) == H,
+                "W_q must be bf16 (A, H)");
+    TORCH_CHECK(a_wa.scalar_type() == at::kFloat && a_wa.numel() == A && a_ba.numel() == 1 &&
+                    a_ba.scalar_type() == at::kFloat, "w_a (A) / b_a (1) fp32");
+    TORCH_CHECK(Bv * vgate_div == R, "attention needs R == videos x rows per video");
+  }
   TORCH_CHECK(T >= 2 && (int64_t)modes.size() >= T - 1, "modes must cover T-1 steps");
   const bool have_labels = labels.defined() && labels.numel() > 0;
   int64_t L = 0;
@@ -141,6 +164,34 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor zeros_h = at::zeros({R, H}, bf), zeros_c = at::zeros({R, H}, f32);
   at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
 
+  // Attention of step t: query q_t = W_q h_{t-1} (hipBLASLt, fp32 out; q_0 = 0),
+  // then the attention kernel writes the per-row video gate term vg_rows.
+  at::Tensor vg_rows, q_all, alpha_all, q_tmp;
+  if (has_att) {
+    vg_rows = at::empty({R, H4}, f32);
+    if (save) {
+      q_all = at::zeros({n_steps, R, A}, f32);
+      alpha_all = at::empty({n_steps, R, C}, f32);
+    } else {
+      q_tmp = at::empty({R, A}, f32);
+    }
+  }
+  auto h_tensor = [&](int64_t t) -> at::Tensor { return save ? h_all[t] : (t & 1 ? h_b : h_a); };
+  auto run_att = [&](int64_t t) {
+    const float* qp = nullptr;
+    if (t > 0) {
+      at::Tensor qo = save ? q_all[t] : q_tmp;
+      at::mm_out(qo, h_tensor(t - 1), a_wq.t(), at::kFloat);
+      qp = qo.data_ptr<float>();
+    }
+    launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), qp, nullptr,
+                   a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv, (int)vgate_div,
+                   (int)C, (int)A, (int)H4, vg_rows.data_ptr<float>(),
+                   save ? alpha_all[t].data_ptr<float>() : nullptr, st);
+  };
+  const float* VG = has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>();
+  const int VDIV = has_att ? 1 : (int)vgate_div;
+
   static const bool merged = [] {
     const char* e = std::getenv("CSTCAP_FWD_MERGED");  // A/B knob (default on)
     return e == nullptr || std::atoi(e) != 0;
@@ -150,10 +201,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       const int64_t* tok = t == 0 ? (have_labels ? LAB : bos.data_ptr<int64_t>())
                                   : seq.data_ptr<int64_t>() + (t - 1);
       const int64_t tok_stride = t == 0 ? (have_labels ? L : 1) : T - 1;
+      if (has_att) run_att(t);
       launch_lstm_step_fwd(tok, tok_stride, ptab.data_ptr<float>(),
                            t == 0 ? reinterpret_cast<uint16_t*>(zeros_h.data_ptr()) : h_buf(t - 1),
                            t == 0 ? zeros_c.data_ptr<float>() : c_buf(t - 1),
-                           vgate.data_ptr<float>(), (int)vgate_div, (int)R, (int)H, WHH, h_buf(t),
+                           VG, VDIV, (int)R, (int)H, WHH, h_buf(t),
                            c_buf(t), hd_buf(t), (int)(H + HAUG), (float)drop_p, seed_drop, (int)t,
                            gates_buf(t), st);
       uint16_t* hd = hd_buf(t);
@@ -176,9 +228,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     }
   }
   // step 0: fused LSTM step (h_{-1} = c_{-1} = 0)
+  if (merged && has_att) run_att(0);
   if (merged) launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
                        ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(zeros_h.data_ptr()),
-                       zeros_c.data_ptr<float>(), vgate.data_ptr<float>(), (int)vgate_div, (int)R,
+                       zeros_c.data_ptr<float>(), VG, VDIV, (int)R,
                        (int)H, WHH, h_buf(0), c_buf(0), hd_buf(0), (int)(H + HAUG), (float)drop_p,
                        seed_drop, 0, gates_buf(0), st);
   // Steps t >= 0: ONE launch runs the vocab projection of step t together with
@@ -194,10 +247,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
     const int vflags = do_sample | ((choose && mode == SEL_GREEDY_H) ? 2 : 0);
     const int64_t* tgt = (have_labels && t + 1 < L) ? LAB + (t + 1) : nullptr;
+    if (has_att && next) run_att(t + 1);  // vgate of step t+1 from h_t
     launch_vocab_lstm_fwd(vin, ldh, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
                           save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
                           part.data_ptr(), tgt, L, vflags, inv_temp, seed_samp, (int)t,
-                          h_buf(t), WHH, vgate.data_ptr<float>(), (int)vgate_div,
+                          h_buf(t), WHH, VG, VDIV,
                           next ? pre.data_ptr<float>() : nullptr, st);
     CellLaunch cl{};
     if (next) {
@@ -222,11 +276,17 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     out.push_back(gates_all);
     out.push_back(c_all);
     out.push_back(h_all);
+    if (has_att) {
+      out.push_back(alpha_all);
+      out.push_back(q_all);
+    }
   }
   return out;
 }
 
-// Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), d_emb (V, E), dvg_rows (R, 4H)}.
+// Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), d_emb (V, E), dvg_rows (R, 4H)}
+// (+ {dGv (Bv, C, 4H), dP (Bv, C, A), dw_a (A), db_a (1), dW_q (A, H)} with attention,
+// att = {Gv, P, W_q bf16, w_a, alpha_all (n, R, C), q_all (n, R, A)}; dvg_rows empty).
 // toks: (n_steps*R) input token of every (step, row), step-major.
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
@@ -235,7 +295,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
                                          at::Tensor dg_xe, double drop_p, int64_t seed,
                                          at::Tensor out_wlog, at::Tensor out_blog,
-                                         int64_t comm_stream) {
+                                         int64_t comm_stream, std::vector<at::Tensor> att) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -248,6 +308,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   if (has_xe) TORCH_CHECK(dg_xe.is_contiguous() && labels.defined(), "dg_xe needs labels");
   TORCH_CHECK(toks.numel() == n_steps * R, "toks must hold one token per (step, row)");
   const uint32_t seed_drop = (uint32_t)(seed * 2654435761u + 17u);
+  const bool has_att = !att.empty();
+  at::Tensor a_gv, a_pre, a_wq, a_wa, a_alpha, a_q;
+  int64_t Bv = 0, C = 0, A = 0, vdiv = 1;
+  if (has_att) {
+    TORCH_CHECK(att.size() == 6, "att = {Gv, P, W_q, w_a, alpha_all, q_all}");
+    a_gv = att[0], a_pre = att[1], a_wq = att[2], a_wa = att[3], a_alpha = att[4], a_q = att[5];
+    Bv = a_gv.size(0), C = a_gv.size(1), A = a_pre.size(2);
+    vdiv = R / Bv;
+    TORCH_CHECK(Bv * vdiv == R && a_alpha.size(0) == n_steps && a_alpha.size(2) == C &&
+                    a_q.size(2) == A && a_wq.size(0) == A && a_wq.size(1) == H,
+                "attention operand shapes");
+  }
+  // dG rows: 4H gate gradients (+ A columns of dq with attention)
+  const int64_t KD = H4 + A;
 
   // 1-3. Vocab head + reverse recurrence, pipelined over row chunks.
   //    Side stream, last chunk first: dS = dG (onehot - softmax) in place
@@ -319,10 +393,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     if (early && comm_stream != 0)
       (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
   }
-  at::Tensor dG_all = at::empty({n_steps, R, H4}, wx.options());
+  at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
   at::Tensor dc = at::zeros({R, H}, f32);
-  // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel
-  at::Tensor whhT = wx.narrow(1, E, H).t().contiguous();
+  // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel; with
+  // attention [W_hh^T | W_q^T] (H, 4H + A), so the step GEMM over
+  // [dG_{t+1} | dq_{t+1}] also adds dq_{t+1} W_q (q_{t+1} = W_q h_t) into dh_t
+  at::Tensor whhT = has_att ? at::cat({wx.narrow(1, E, H).t(), a_wq.t()}, 1).contiguous()
+                            : wx.narrow(1, E, H).t().contiguous();
+  at::Tensor dpre_part, dwa_part, dba_part;
+  if (has_att) {
+    const int64_t nwg = Bv * att_groups((int)vdiv);
+    dpre_part = at::zeros({nwg, C, A}, f32);
+    dwa_part = at::zeros({nwg, A}, f32);
+    dba_part = at::zeros({nwg}, f32);
+  }
   int waited = n_chunks;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     int need = 0;  // chunk holding the first row of step t (chunks finish high to low)
@@ -334,15 +418,24 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
         c_all[t].data_ptr<float>(), t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R,
         (int)H, (float)drop_p, seed_drop, (int)t,
-        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), st);
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st);
+    if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
+      launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
+                     a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
+                     t > 0 ? a_q[t].data_ptr<float>() : nullptr, a_alpha[t].data_ptr<float>(),
+                     a_wa.data_ptr<float>(), (int)Bv, (int)vdiv, (int)C, (int)A, (int)H4,
+                     t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
+                     dba_part.data_ptr<float>(), st);
   }
   while (waited > 0) (void)hipStreamWaitEvent(st, ev[--waited], 0);
   if (!early) dblog = colsum.sum(0);                                    // (V)
   // 4. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
   //    reductions run as batched GEMMs over groups of steps (many more output
   //    tiles in flight than one K = 35k GEMM), summed afterwards.
-  at::Tensor dG2 = dG_all.view({n_steps * R, H4});
+  at::Tensor dGx = dG_all.view({n_steps * R, KD});  // [dG | dq] rows
+  at::Tensor dG2 = dGx.narrow(1, 0, H4);
   at::Tensor dWx = at::empty({H4, E + H}, f32);
+  at::Tensor dWq;
   auto grouped_wgrad = [&](at::Tensor a_rows, at::Tensor b_rows, int64_t nsteps) {
     int64_t G = 1;  // steps per group: largest divisor <= 7
     for (int64_t g = 7; g >= 1; --g)
@@ -355,11 +448,15 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor x_in = emb.index_select(0, toks);                            // (n*R, E) bf16
   dWx.narrow(1, 0, E).copy_(grouped_wgrad(dG2, x_in, n_steps));
   if (n_steps > 1) {
-    dWx.narrow(1, E, H).copy_(grouped_wgrad(dG2.narrow(0, R, (n_steps - 1) * R),
-                                            h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
-                                            n_steps - 1));
+    // with attention the extra rows of [dG | dq]^T h_prev are dW_q
+    at::Tensor wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
+                                  h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
+                                  n_steps - 1);
+    dWx.narrow(1, E, H).copy_(wh.narrow(0, 0, H4));
+    if (has_att) dWq = wh.narrow(0, H4, A).contiguous();
   } else {
     dWx.narrow(1, E, H).zero_();
+    if (has_att) dWq = at::zeros({A, H}, f32);
   }
   //    embedding: dX = dG W_ie, then a sorted segmented sum into d_emb
   TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
@@ -369,10 +466,25 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor d_emb = at::zeros({V, E}, f32);
   launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int64_t>(),
                         srow.data_ptr<int64_t>(), (int)(n_steps * R), d_emb.data_ptr<float>(), st);
-  at::Tensor dvg = dG_all.sum(0, false, at::kFloat);                   // (R, 4H), sum over time
+  at::Tensor dvg;
+  std::vector<at::Tensor> res;
+  if (!has_att) {
+    dvg = dG_all.sum(0, false, at::kFloat);                              // (R, 4H), sum over time
+  } else {
+    // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r]: one batched GEMM
+    // per (step, video), K = rows per video, summed over steps
+    at::Tensor al = a_alpha.to(at::kBFloat16).view({n_steps * Bv, vdiv, C}).transpose(1, 2);
+    at::Tensor dgv = dG_all.view({n_steps * Bv, vdiv, KD}).narrow(2, 0, H4);
+    at::Tensor dGv = at::bmm(al, dgv, at::kFloat).view({n_steps, Bv, C, H4}).sum(0);
+    const int64_t ng = att_groups((int)vdiv);
+    res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0),
+           dba_part.sum(0).view({1}), dWq};
+  }
   (void)hipStreamWaitEvent(st, ev_done, 0);  // join the side stream (dWlog)
   for (auto& e : ev) (void)hipEventDestroy(e);
-  return {dWx, dWlog, dblog, d_emb, dvg};
+  std::vector<at::Tensor> out = {dWx, dWlog, dblog, d_emb, dvg};
+  out.insert(out.end(), res.begin(), res.end());
+  return out;
 }
 
 // On-GPU CIDEr-D scores of N hypotheses.
@@ -415,13 +527,26 @@ at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v
 // padded with zeros like the reference.
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
-                                    int64_t K, int64_t T, int64_t bos_index) {
+                                    int64_t K, int64_t T, int64_t bos_index,
+                                    std::vector<at::Tensor> att) {
   check_cuda(wx, "wx");
   check_cuda(vgate, "vgate");
   TORCH_CHECK(get_vocab_variant() >= 4, "beam search needs a transposed-epilogue vocab variant");
   TORCH_CHECK(K >= 1 && K <= 16, "beam_size must be in [1, 16]");
   const int64_t H4 = wx.size(0), H = H4 / 4, V = wlog.size(0), B = vgate.size(0), R = B * K;
   TORCH_CHECK(K <= V, "beam_size > vocab_size");
+  // temporal attention: att = {Gv, P, W_q, w_a, b_a} as in decoder_forward; the
+  // query of a beam row comes from its parent's h (q rows gathered by parent)
+  const bool has_att = !att.empty();
+  int64_t C = 0, A = 0;
+  at::Tensor vg_rows, qb;
+  if (has_att) {
+    TORCH_CHECK(att.size() == 5 && att[0].size(0) == B && att[0].size(2) == H4,
+                "att = {Gv (B, C, 4H), P, W_q, w_a, b_a}");
+    C = att[0].size(1), A = att[1].size(2);
+    TORCH_CHECK(A % 64 == 0 && C <= 32 && att_lds_need((int)C, (int)A) <= att_max_lds() &&
+                    att[2].size(0) == A && att[2].size(1) == H, "attention shapes");
+  }
   auto dev = wx.device();
   auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
   auto i64 = at::TensorOptions().dtype(at::kLong).device(dev);
@@ -446,6 +571,10 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   at::Tensor c[2] = {at::zeros({R, H}, f32), at::empty({R, H}, f32)};
   const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
+  if (has_att) {
+    vg_rows = at::empty({R, H4}, f32);
+    qb = at::empty({R, A}, f32);
+  }
   for (int64_t t = 0; t < T - 1; ++t) {
     if (t >= 1) {
       launch_beam_topk(logits.data_ptr<float>(), ldl, (int)V, (int)R, (int)K,
@@ -461,9 +590,17 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
     const at::Tensor& cp = c[t & 1];
     at::Tensor& ho = h[(t + 1) & 1];
     at::Tensor& co = c[(t + 1) & 1];
+    if (has_att) {
+      if (t >= 1) at::mm_out(qb, hp, att[2].t(), at::kFloat);
+      launch_att_fwd(att[0].data_ptr<float>(), att[1].data_ptr<float>(),
+                     t >= 1 ? qb.data_ptr<float>() : nullptr, t >= 1 ? parent.data_ptr<int>() : nullptr,
+                     att[3].data_ptr<float>(), att[4].data_ptr<float>(), (int)B, (int)K, (int)C,
+                     (int)A, (int)H4, vg_rows.data_ptr<float>(), nullptr, st);
+    }
     launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, ptab.data_ptr<float>(),
                          reinterpret_cast<const uint16_t*>(hp.data_ptr()), cp.data_ptr<float>(),
-                         vgate.data_ptr<float>(), (int)K, (int)R, (int)H, WHH,
+                         has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>(),
+                         has_att ? 1 : (int)K, (int)R, (int)H, WHH,
                          reinterpret_cast<uint16_t*>(ho.data_ptr()), co.data_ptr<float>(), nullptr,
                          (int)H, 0.f, 0u, (int)t, nullptr, st,
                          t >= 1 ? parent.data_ptr<int>() : nullptr);

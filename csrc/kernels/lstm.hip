@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
     const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
-    uint16_t* __restrict__ dG) {
+    uint16_t* __restrict__ dG, int KD) {
   using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
   const int ut = b / n_rt, rt = b % n_rt;
   const int r0 = rt * BM, u0 = ut * 64;
   const int H4 = 4 * H;
-  const int nk = dg_next != nullptr ? H4 / 64 : 0;
+  const int nk = dg_next != nullptr ? KD / 64 : 0;  // KD = 4H (+ A with attention)
   const int tid = threadIdx.x, u = tid & 63, rg = tid >> 6;
   const int hu = u0 + u;
   constexpr int RPT = BM / 4;
@@ -213,20 +213,20 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     DmaSrc<BM / 32> a;
     DmaSrc<64 / 32> bsrc;
-    a.r0 = a.r1 = make_rsrc(dg_next ? dg_next : whhT, (int64_t)R * H4 * 2);
+    a.r0 = a.r1 = make_rsrc(dg_next ? dg_next : whhT, (int64_t)R * KD * 2);
     a.ksplit = nk;
 #pragma unroll
     for (int i = 0; i < BM / 32; ++i) {
       const int row = dma_row(w, i, lane);
-      a.voff0[i] = min(r0 + row, R - 1) * H4 * 2 + dma_chunk(row, lane) * 16;
+      a.voff0[i] = min(r0 + row, R - 1) * KD * 2 + dma_chunk(row, lane) * 16;
       a.voff1[i] = a.voff0[i];
     }
-    bsrc.r0 = bsrc.r1 = make_rsrc(whhT, (int64_t)H * H4 * 2);
+    bsrc.r0 = bsrc.r1 = make_rsrc(whhT, (int64_t)H * KD * 2);
     bsrc.ksplit = nk;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = dma_row(w, i, lane);
-      bsrc.voff0[i] = (u0 + row) * H4 * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff0[i] = (u0 + row) * KD * 2 + dma_chunk(row, lane) * 16;
       bsrc.voff1[i] = bsrc.voff0[i];
     }
     gemm_nt_mainloop<TL>(nk, a, bsrc, lds, acc);
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
       uint2 pk;
       pk.x = (uint32_t)f2bf(dpi) | ((uint32_t)f2bf(dpf) << 16);
       pk.y = (uint32_t)f2bf(dpg) | ((uint32_t)f2bf(dpo) << 16);
-      *reinterpret_cast<uint2*>(dG + (int64_t)r * H4 + 4 * hu) = pk;
+      *reinterpret_cast<uint2*>(dG + (int64_t)r * KD + 4 * hu) = pk;
     }
   }
 }
@@ -268,7 +268,7 @@ static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT
                                    const float* dh_logit, float* dc_carry,
                                    const uint16_t* gates, const float* c_t, const float* c_prev,
                                    int R, int H, float drop_p, uint32_t seed, int step,
-                                   uint16_t* dG, hipStream_t stream) {
+                                   uint16_t* dG, int KD, hipStream_t stream) {
   using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -279,15 +279,15 @@ static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT
   const int n = (H / 64) * ((R + BM - 1) / BM);
   hipLaunchKernelGGL(lstm_step_bwd_kernel<BM>, dim3(n), dim3(256), TL::LDS_BYTES, stream,
                      dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
-                     step, dG);
+                     step, dG, KD);
 }
 
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, uint32_t seed,
-                          int step, uint16_t* dG, hipStream_t stream) {
+                          int step, uint16_t* dG, int KD, hipStream_t stream) {
   launch_lstm_step_bwd_t<64>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                             drop_p, seed, step, dG, stream);
+                             drop_p, seed, step, dG, KD, stream);
 }
 
 static int g_lstm_fwd_variant = 0;

@@ -78,10 +78,24 @@ void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_
                           int H, float drop_p, uint32_t seed, int step, uint16_t* dG,
                           hipStream_t stream);
 
+// dg_next / dG rows have stride KD: 4H gate columns (+ A attention-query
+// columns, matched by extra whhT columns [W_hh^T | W_q^T] of width KD)
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, uint32_t seed,
-                          int step, uint16_t* dG, hipStream_t stream);
+                          int step, uint16_t* dG, int KD, hipStream_t stream);
+
+// attention.hip (temporal attention over num_chunks frames)
+int att_groups(int vdiv);
+size_t att_lds_need(int C, int A);
+size_t att_max_lds();
+void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
+                    const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
+                    float* vg_out, float* alpha_out, hipStream_t stream);
+void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,
+                    const float* alpha, const float* wa, int Bv, int vdiv, int C, int A, int G4,
+                    int write_dq, float* dpre_part, float* dwa_part, float* dba_part,
+                    hipStream_t stream);
 
 // embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows sorted by token; C <= 1024)
 void launch_token_rows_sum(const float* x, int C, const int64_t* stok, const int64_t* srow, int N,

@@ -64,7 +64,7 @@ def build_model(opt, device, impl=None):
     if impl == 'hip':
         from .models.decoder_engine import DecoderEngine, engine_supports
         if not engine_supports(opt):
-            logger.warning('fused HIP decoder supports lstm/1-layer/concat/num_chunks=1; '
+            logger.warning('fused HIP decoder supports lstm/1-layer/concat (num_chunks <= 32); '
                            'using the PyTorch decoder path for this configuration')
             return model, None
         engine = DecoderEngine(model, opt)

@@ -20,6 +20,14 @@ reference feeds the same video vector at every step to 20 identical rows,
 ``model.py:84-86,278``), whose gradient the engine returns summed over time
 and rows.
 
+Temporal attention (``num_chunks > 1``, the extension of the reference's
+declared-only ``--num_chunks``, ``opts.py:241-245``): autograd computes, once
+per batch, the per-frame gate table ``Gv[b, c] = W_ih[:, E:] . v_c`` and the
+projected frames ``P = f_feat(v)``; every decode step runs the attention
+kernel of ``csrc/kernels/attention.hip`` (scores from ``W_q h_{t-1}``,
+softmax over frames, ``vgate_r = sum_c alpha_c Gv[b, c]``), and the backward
+returns ``dGv, dP, dW_q, dw_a, db_a``.
+
 Semantics match :class:`CaptionModel`'s PyTorch path (reference
 ``model.py:218-367``) with two documented differences that are
 distribution-identical, not value-identical:
@@ -28,8 +36,8 @@ distribution-identical, not value-identical:
   * precision: bf16 MFMA operands, fp32 accumulation, cell state and
     softmax statistics in fp32.
 Supported configuration: ``rnn_type lstm``, ``num_layers 1``, ``model_type
-concat``, ``num_chunks 1`` (the reference default); other configurations use
-the PyTorch path (``build_model`` decides).
+concat`` with or without temporal attention; other configurations use the
+PyTorch path (``build_model`` decides).
 """
 import torch
 import torch.nn.functional as F
@@ -39,33 +47,57 @@ from ..utils.text import BOS
 
 SEL_GT, SEL_SAMPLE, SEL_GREEDY, SEL_SS = 0, 1, 2, 3
 
+ATT_MAX_CHUNKS = 32
+ATT_LDS_LIMIT = 64 * 1024
+
+
+def att_lds_bytes(C, A):
+    """LDS of the attention backward kernel (csrc/kernels/attention.hip)."""
+    maxc = 8 if C <= 8 else 16 if C <= 16 else 32
+    return 4 * (C * A + 4 * A + A + 5 * 4 * maxc)
+
 
 def engine_supports(opt):
-    return (getattr(opt, 'rnn_type', 'lstm') == 'lstm' and getattr(opt, 'num_layers', 1) == 1
-            and getattr(opt, 'model_type', 'concat') == 'concat'
-            and getattr(opt, 'num_chunks', 1) == 1
-            and opt.input_encoding_size % 64 == 0 and opt.input_encoding_size <= 1024
-            and opt.rnn_size % 64 == 0)
+    ok = (getattr(opt, 'rnn_type', 'lstm') == 'lstm' and getattr(opt, 'num_layers', 1) == 1
+          and getattr(opt, 'model_type', 'concat') == 'concat'
+          and opt.input_encoding_size % 64 == 0 and opt.input_encoding_size <= 1024
+          and opt.rnn_size % 64 == 0)
+    C = getattr(opt, 'num_chunks', 1)
+    if ok and C > 1:  # attention size == rnn_size (TemporalAttention)
+        ok = C <= ATT_MAX_CHUNKS and att_lds_bytes(C, opt.rnn_size) <= ATT_LDS_LIMIT
+    return ok
 
 
 class _DecoderFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, vgate, w_ih, w_hh, emb_w, logit_w, logit_b, eng, labels, bos, R, T, modes,
-                ss_prob, drop_p, temperature, seed, vdiv, want_xe, use_counts, use_unfinished,
-                save):
+    def forward(ctx, vgate, w_ih, w_hh, emb_w, logit_w, logit_b, att_gv, att_pre, att_wq,
+                att_wa, att_ba, eng, labels, bos, R, T, modes, ss_prob, drop_p, temperature, seed,
+                vdiv, want_xe, use_counts, use_unfinished, save):
+        has_att = att_gv is not None
+        dev = logit_b.device
+        att = []
+        if has_att:
+            att = [att_gv.detach().float().contiguous(), att_pre.detach().float().contiguous(),
+                   eng.wq, att_wa.detach().float().contiguous().view(-1),
+                   att_ba.detach().float().contiguous().view(-1)]
+        vg_in = torch.empty(0, device=dev) if has_att else vgate.detach().float().contiguous()
         outs = _ext.ops().decoder_forward(
             eng.wx, eng.emb, eng.ptab, eng.whh, eng.wlog, logit_b.detach().float().contiguous(),
-            vgate.detach().float().contiguous(), vdiv,
+            vg_in, vdiv,
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
-            drop_p, temperature, seed, save, want_xe, use_counts, use_unfinished)
+            drop_p, temperature, seed, save, want_xe, use_counts, use_unfinished, att)
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
         ctx.eng = eng
         ctx.drop_p, ctx.seed = drop_p, seed
         ctx.shapes = (w_ih.shape, emb_w.shape)
+        ctx.has_att = has_att
+        ctx.att_saved = None
         if save:
-            ctx.saved = (lse, *outs[4:], seq, labels, bos)
+            ctx.saved = (lse, *outs[4:9], seq, labels, bos)
+            if has_att:  # Gv, P, W_q, w_a, alpha_all, q_all
+                ctx.att_saved = (att[0], att[1], att[2], att[3], outs[9], outs[10])
         else:
             ctx.saved = None
         ctx.mark_non_differentiable(seq)
@@ -81,6 +113,8 @@ class _DecoderFn(torch.autograd.Function):
         eng = ctx.eng
         lse, logits16, hdrop, gates, c_all, h_all, seq, labels, bos = ctx.saved
         ctx.saved = None  # logits buffer is overwritten in place by dS
+        att = list(ctx.att_saved) if ctx.has_att else []
+        ctx.att_saved = None
         g_sel = dg_sel.contiguous() if dg_sel is not None else None
         g_xe = dg_xe.contiguous() if (want_xe and dg_xe is not None and dg_xe.numel()) else None
         empty = torch.empty(0, device=lse.device)
@@ -94,11 +128,12 @@ class _DecoderFn(torch.autograd.Function):
         early = hook is not None and hook.active
         out_w, out_b, comm = (hook.out_wlog, hook.out_blog, hook.comm_ptr) if early \
             else (empty, empty, 0)
-        dWx, dWlog, dblog, d_emb, dvg = _ext.ops().decoder_backward(
+        res = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
-            ctx.drop_p, ctx.seed, out_w, out_b, comm)
+            ctx.drop_p, ctx.seed, out_w, out_b, comm, att)
+        dWx, dWlog, dblog, d_emb, dvg = res[:5]
         if early:
             hook.launch()
             dWlog = dblog = None  # already in the gradient buffers
@@ -108,20 +143,26 @@ class _DecoderFn(torch.autograd.Function):
         d_wih = torch.zeros(w_ih_shape, dtype=torch.float32, device=dWx.device)
         d_wih[:, :E] = d_orig[:, :E]
         d_whh = d_orig[:, E:].contiguous()
+        if ctx.has_att:
+            d_gv, d_pre, d_wa, d_ba, d_wq = res[5:10]
+            return (None, d_wih, d_whh, d_emb, dWlog, dblog, d_gv, d_pre, d_wq, d_wa,
+                    d_ba) + (None,) * 15
         nv = R // vdiv
         d_vgate = dvg.view(nv, vdiv, -1).sum(1)
-        return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 15
+        return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 20
 
 
 class DecoderEngine:
     def __init__(self, model, opt):
         if not engine_supports(opt):
-            raise ValueError('fused engine supports lstm/1 layer/concat/num_chunks=1')
+            raise ValueError('fused engine supports lstm / 1 layer / concat '
+                             '(num_chunks <= %d with attention)' % ATT_MAX_CHUNKS)
         if not _ext.available():
             raise RuntimeError('HIP extension not available')
         self.H = model.rnn_size
         self.E = model.input_encoding_size
         self.V = model.vocab_size
+        self.attention = getattr(model, 'num_chunks', 1) > 1
         dev = model.embed.weight.device
         H = self.H
         # packed gate row 4u+g  <-  original row g*H+u
@@ -145,6 +186,8 @@ class DecoderEngine:
         # input-token gate table P = emb . W_ie^T (V x 4H, packed gate order):
         # one GEMM per optimizer step instead of K=E of work in every decode step
         self.ptab = torch.mm(self.emb, self.wx[:, :E].t(), out_dtype=torch.float32)
+        if self.attention:
+            self.wq = m.temporal_att.f_h.weight.detach().to(torch.bfloat16).contiguous()
 
     def attach_optimizer(self, trainer):
         self.refresh_weights()  # params were re-homed into the flat buffer
@@ -161,9 +204,25 @@ class DecoderEngine:
         vg = F.linear(fc, w_iv)
         return vg.index_select(1, self.perm), fc.size(0)
 
+    def _att_inputs(self, model, feats):
+        """Per-batch attention operands: per-frame gate table Gv (B, C, 4H)
+        in packed gate order, projected frames P (B, C, A), and the scorer
+        parameters (W_q, w_a, b_a) as autograd inputs of the Function."""
+        frames = model.encode(feats)  # (B, C, F*H), FeatPool dropout in train mode
+        ta = model.temporal_att
+        w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
+        gv = F.linear(frames, w_iv).index_select(2, self.perm)
+        pre = ta.precompute(frames)
+        return (gv, pre, ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), frames.size(0)
+
     def _run(self, model, feats, labels, modes, want_xe, use_counts, use_unfinished,
              expand=True, ss_prob=0.0, drop=True, temperature=1.0, bos_rows=None):
-        vg, B = self._vgate(model, feats, expand)
+        if self.attention:
+            att, B = self._att_inputs(model, feats)
+            vg = None
+        else:
+            vg, B = self._vgate(model, feats, expand)
+            att = (None,) * 5
         S = model.feat_expander.n if expand else 1
         R = labels.size(0) if labels is not None else B * S
         if labels is not None:
@@ -171,14 +230,15 @@ class DecoderEngine:
             bos = None
         else:
             T = model.seq_length - 1
-            bos = torch.full((R,), BOS, dtype=torch.long, device=vg.device)
+            bos = torch.full((R,), BOS, dtype=torch.long, device=model.logit.bias.device)
         drop_p = model.drop_prob_lm if (model.training and drop) else 0.0
         m = model
         ws = (m.core.rnn.weight_ih_l0, m.core.rnn.weight_hh_l0, m.embed.weight, m.logit.weight,
               m.logit.bias)
         # (inside Function.forward grad mode is off, so decide here)
-        save = torch.is_grad_enabled() and (vg.requires_grad or any(w.requires_grad for w in ws))
-        return _DecoderFn.apply(vg, *ws, self,
+        diff_in = [t for t in (vg,) + tuple(att) if t is not None] + list(ws)
+        save = torch.is_grad_enabled() and any(t.requires_grad for t in diff_in)
+        return _DecoderFn.apply(vg, *ws, *att, self,
                                 labels.contiguous() if labels is not None else None, bos, R, T,
                                 modes, float(ss_prob), float(drop_p), float(temperature),
                                 self._seed(), S, want_xe, use_counts, use_unfinished, save)
@@ -248,9 +308,16 @@ class DecoderEngine:
                 return model.sample_beam(feats, opt)
             finally:
                 model.impl = 'hip'
-        vg, _ = self._vgate(model, feats, False)
+        att = []
+        if self.attention:
+            (gv, pre, _, wa, ba), _ = self._att_inputs(model, feats)
+            att = [gv.float().contiguous(), pre.float().contiguous(), self.wq,
+                   wa.float().contiguous(), ba.float().contiguous()]
+            vg = gv[:, 0]  # only its row count is read when attention is on
+        else:
+            vg, _ = self._vgate(model, feats, False)
         seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog,
                                          model.logit.bias.detach().float().contiguous(),
                                          vg.detach().float().contiguous(), K, model.seq_length,
-                                         BOS)
+                                         BOS, att)
         return seq, lp

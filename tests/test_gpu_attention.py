@@ -1,0 +1,129 @@
+"""Temporal attention (num_chunks > 1) on the fused HIP engine vs the PyTorch
+CaptionModel path (fp32 reference of the same model): teacher-forced
+log-probs and every parameter gradient (attention scorer, frame projection,
+LSTM, vocab head, FeatPool), REINFORCE gradients through a rollout, greedy
+decoding and beam search.  Kernels: csrc/kernels/attention.hip
+(att_fwd_kernel / att_bwd_kernel) plus the K = 4H + A recurrent backward GEMM.
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def _tiny(C=4, V=300, H=64, feat_dims=(48, 32), S=5, B=6, L=12, seed=0):
+    from cst_captioning_amd.config import default_opts
+    from cst_captioning_amd.data import make_synthetic, CaptionLoader
+    from cst_captioning_amd.models import CaptionModel
+    ds = make_synthetic('msrvtt', num_videos=40, vocab_size=V, seq_length=L,
+                        feat_dims=list(feat_dims), num_chunks=C, seed=seed)
+    opt = default_opts(vocab_size=V, seq_length=L, feat_dims=list(feat_dims),
+                       train_seq_per_img=S, rnn_size=H, input_encoding_size=H,
+                       drop_prob_lm=0.0, num_chunks=C)
+    torch.manual_seed(seed)
+    model = CaptionModel(opt).to(DEV)
+    with torch.no_grad():  # non-trivial decoder and attention
+        model.logit.weight.mul_(3.0)
+        model.core.rnn.weight_hh_l0.mul_(2.0)
+        model.temporal_att.align.weight.mul_(4.0)
+    loader = CaptionLoader(ds, B, S, 'train', DEV, seed=seed)
+    return ds, opt, model, loader
+
+
+def _engine(model, opt):
+    from cst_captioning_amd.models.decoder_engine import DecoderEngine, engine_supports
+    assert engine_supports(opt)
+    return DecoderEngine(model, opt)
+
+
+def _grad_errors(model, ref):
+    out = {}
+    for (name, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+        if name == 'temporal_att.align.bias':
+            # softmax is shift-invariant: the exact gradient is 0 (both sides
+            # hold rounding noise only)
+            assert p.grad is None or float(p.grad.abs().max()) < 1e-3
+            continue
+        if q.grad is None or q.grad.norm() == 0:
+            continue
+        out[name] = float((p.grad - q.grad).norm() / (q.grad.norm() + 1e-12))
+    return out
+
+
+@pytest.mark.parametrize('C', [4, 8, 12])
+def test_attention_teacher_forced_matches_torch(C):
+    ds, opt, model, loader = _tiny(C=C)
+    eng = _engine(model, opt)
+    model.train()
+    data = loader.get_batch()
+    labels = data['labels']
+    assert data['feats'][0].dim() == 3 and data['feats'][0].size(1) == C
+    ref = copy.deepcopy(model)
+    ref.impl = 'torch'
+    pred = ref(data['feats'], labels)[0]
+    tgt = labels[:, 1:1 + pred.size(1)]
+    ref_lp = pred.gather(2, tgt.unsqueeze(2)).squeeze(2)
+    g_xe = eng.teacher_forced(model, data['feats'], labels)
+    n = pred.size(1)
+    m = data['masks'][:, 1:1 + n] > 0
+    assert (g_xe[:, :n][m] - ref_lp[m]).abs().max() < 0.08
+    from cst_captioning_amd.models import CrossEntropyCriterion
+    crit = CrossEntropyCriterion()
+    crit(pred, labels[:, 1:], data['masks'][:, 1:]).backward()
+    crit(g_xe, labels[:, 1:], data['masks'][:, 1:]).backward()
+    errs = _grad_errors(model, ref)
+    for k in ('temporal_att.f_h.weight', 'temporal_att.f_feat.weight',
+              'temporal_att.align.weight', 'core.rnn.weight_ih_l0', 'core.rnn.weight_hh_l0'):
+        assert k in errs, (k, sorted(errs))
+    bad = {k: v for k, v in errs.items() if v > 0.06}
+    assert not bad, bad
+
+
+def test_attention_rollout_gradient_matches_torch():
+    ds, opt, model, loader = _tiny(C=6, seed=2)
+    eng = _engine(model, opt)
+    model.train()
+    model.set_mixer_from(1)
+    data = loader.get_batch()
+    seq, g_sel, _ = eng.rollout(model, data['feats'], data['labels'])
+    w = torch.randn(seq.size(0), device=DEV)
+    from cst_captioning_amd.models import RewardCriterion
+    RewardCriterion()(seq, g_sel, w).backward()
+    ref = copy.deepcopy(model)
+    ref.impl = 'torch'
+    ref.zero_grad(set_to_none=True)
+    ref.set_mixer_from(0)
+    lab = torch.cat([data['labels'][:, :1], seq, torch.zeros_like(seq[:, :1])], 1)
+    pred = ref(data['feats'], lab)[0]
+    lp_ref = pred[:, :seq.size(1)].gather(2, seq[:, :pred.size(1)].unsqueeze(2)).squeeze(2)
+    k = lp_ref.size(1)
+    assert (g_sel[:, :k] - lp_ref).abs().max() < 0.08
+    RewardCriterion()(seq[:, :k], lp_ref, w).backward()
+    bad = {n: v for n, v in _grad_errors(model, ref).items() if v > 0.08}
+    assert not bad, bad
+
+
+def test_attention_greedy_and_beam_match_torch():
+    ds, opt, model, loader = _tiny(C=5, seed=3)
+    with torch.no_grad():
+        model.logit.weight.mul_(3.0)  # peaked distributions: few near-ties
+    eng = _engine(model, opt)
+    model.eval()
+    data = loader.get_batch()
+    ref = copy.deepcopy(model)
+    ref.impl = 'torch'
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(p.bfloat16().float())
+    seq_ref, _ = ref.sample(data['feats'], {'sample_max': 1})
+    seq, _ = eng.sample(model, data['feats'], {'sample_max': 1})
+    assert (seq[:, :4] == seq_ref[:, :4]).float().mean().item() > 0.9
+    for K in (2, 4):
+        b_ref, _ = ref.sample(data['feats'], {'beam_size': K})
+        b, _ = eng.sample_beam(model, data['feats'], {'beam_size': K})
+        assert b.shape == b_ref.shape
+        assert (b == b_ref).all(1).float().mean().item() >= 0.8, (K, b, b_ref)
