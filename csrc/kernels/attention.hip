@@ -16,11 +16,15 @@
 //     packed gate order) ONCE per batch; per step the kernel forms
 //     vgate_r = sum_c alpha_c Gv[b, c] (C x 4H FMAs per row) instead of a
 //     (R x F*H) . (F*H x 4H) GEMM -- 4H/C times less work per step;
-//   * one workgroup owns ATT_RPW rows of ONE video: the video's projected
-//     frame tile P[b] (C x A), the rows' queries and w_a are staged in LDS
-//     once and every (row, frame) score is a wave-wide dot product out of
-//     LDS; the Gv[b] rows stream from L2 (shared by the video's row groups)
-//     as float4;
+//   * one workgroup owns ATT_RPW rows of ONE video.  Thread t owns the
+//     attention units a = t + 256 j: it reads its own columns of the video's
+//     projected frame tile P[b] (C x A) and of the rows' queries (coalesced),
+//     accumulates the partial scores of all RPW x C (row, frame) pairs in
+//     registers, and a butterfly all-reduce (N - 1 shuffles for N values,
+//     instead of 6 per value) plus a cross-wave LDS sum finishes every score
+//     at once; the video's Gv[b] rows (L2-resident, shared by its row groups)
+//     are prefetched into registers at kernel start, so their latency hides
+//     under the scores;
 //   * backward (per reverse step, after the fused LSTM step backward has
 //     produced dG_t): dalpha = dG_t . Gv[b]^T, softmax backward, and the
 //     tanh-scorer backward.  dq_t is written as bf16 into the tail columns
@@ -33,64 +37,135 @@
 
 namespace cst {
 
-constexpr int ATT_THREADS = 256, ATT_RPW = 4;
+constexpr int ATT_THREADS = 256, ATT_RPW = 4, ATT_WAVES = ATT_THREADS / WAVE;
 
-__device__ __forceinline__ void att_stage(float* s_pre, float* s_q, float* s_wa,
-                                          const float* __restrict__ pre,
-                                          const float* __restrict__ q,
-                                          const int* __restrict__ q_rowmap,
-                                          const float* __restrict__ wa, int b, int r0, int nr,
-                                          int C, int A) {
-  const int tid = threadIdx.x, A4 = A >> 2;
-  const float4* src = reinterpret_cast<const float4*>(pre + (int64_t)b * C * A);
-  for (int i = tid; i < C * A4; i += ATT_THREADS) reinterpret_cast<float4*>(s_pre)[i] = src[i];
-  for (int i = tid; i < ATT_RPW * A4; i += ATT_THREADS) {
-    const int s = i / A4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q != nullptr && s < nr) {
-      const int r = r0 + s, qr = q_rowmap ? q_rowmap[r] : r;
-      v = reinterpret_cast<const float4*>(q + (int64_t)qr * A)[i - s * A4];
+// Butterfly all-reduce of N (32 or 64) per-lane partial sums across the 64
+// lanes of a wave in log2(64) exchange steps: each step a lane keeps half of
+// its values and adds the partner's copy of them, so the wave spends N-1
+// shuffles instead of 6 N for N separate reductions.  Afterwards lane l holds
+// the total of value index (l >> (6 - log2 N)) in v[0].
+template <int N, int M>
+struct Bfly {
+  static __device__ __forceinline__ void run(float* v, int lane) {
+    constexpr int H = N / 2;
+    const bool up = (lane & M) != 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      const float send = up ? v[i] : v[i + H];
+      const float keep = up ? v[i + H] : v[i];
+      v[i] = keep + __shfl_xor(send, M, WAVE);
     }
-    reinterpret_cast<float4*>(s_q)[i] = v;
+    Bfly<H, M / 2>::run(v, lane);
   }
-  for (int i = tid; i < A; i += ATT_THREADS) s_wa[i] = wa[i];
+};
+template <int M>
+struct Bfly<1, M> {
+  static __device__ __forceinline__ void run(float* v, int lane) {
+    v[0] += __shfl_xor(v[0], M, WAVE);
+    Bfly<1, M / 2>::run(v, lane);
+  }
+};
+template <>
+struct Bfly<1, 0> {
+  static __device__ __forceinline__ void run(float*, int) {}
+};
+
+// Sum of RPW x MAXC per-thread partials over the whole block -> s_out
+// (index s * MAXC + c); s_red holds ATT_WAVES x RPW x MAXC floats.
+template <int MAXC>
+__device__ __forceinline__ void block_sum_partials(float (&part)[ATT_RPW][MAXC], float* s_red,
+                                                   float* s_out) {
+  constexpr int N = ATT_RPW * MAXC;
+  constexpr int CH = N < 64 ? N : 64;  // butterfly chunk
+  constexpr int SH = CH == 32 ? 1 : 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* flat = &part[0][0];
+#pragma unroll
+  for (int c0 = 0; c0 < N; c0 += CH) {
+    Bfly<CH, 32>::run(flat + c0, lane);
+    if ((lane & ((1 << SH) - 1)) == 0) s_red[w * N + c0 + (lane >> SH)] = flat[c0];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += ATT_THREADS) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < ATT_WAVES; ++k) t += s_red[k * N + i];
+    s_out[i] = t;
+  }
+  __syncthreads();
 }
 
+// Column groups (float4) of the 4H gate vector a thread prefetches into
+// registers: 2 x 256 threads x 4 = 2048 = 4H at H = 512 (larger H loops).
+constexpr int ATT_GPF = 2;
+
 // grid: Bv * ngroups blocks; block (b, g) owns rows b*vdiv + g*RPW ... (< (b+1)*vdiv)
+// Scores: thread t owns attention units a = t + 256 j and accumulates the
+// partial dot products of all RPW x C (row, frame) pairs over them (its own
+// columns of P[b] and q: coalesced loads, no LDS staging), then one butterfly
+// + cross-wave sum finishes every score at once.
+template <int MAXC>
 __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
     const float* __restrict__ gv, const float* __restrict__ pre, const float* __restrict__ q,
     const int* __restrict__ q_rowmap, const float* __restrict__ wa, const float* __restrict__ ba,
     int vdiv, int ngroups, int C, int A, int G4, float* __restrict__ vg_out,
-    float* __restrict__ alpha_out) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* s_pre = sm;
-  float* s_q = s_pre + C * A;
-  float* s_wa = s_q + ATT_RPW * A;
-  float* s_e = s_wa + A;  // ATT_RPW x C
+    float* __restrict__ alpha_out, int accumulate) {
+  __shared__ float s_red[ATT_WAVES * ATT_RPW * MAXC];
+  __shared__ float s_e[ATT_RPW * MAXC];
   const int b = blockIdx.x / ngroups, g = blockIdx.x % ngroups;
   const int r0 = b * vdiv + g * ATT_RPW, nr = min(ATT_RPW, vdiv - g * ATT_RPW);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  att_stage(s_pre, s_q, s_wa, pre, q, q_rowmap, wa, b, r0, nr, C, A);
-  __syncthreads();
-  // scores: one wave per (row, frame) pair, lanes stride the attention dim
-  const float bias = ba[0];
-  for (int p = w; p < nr * C; p += ATT_THREADS / WAVE) {
-    const int s = p / C, c = p - s * C;
-    const float* pc = s_pre + c * A;
-    const float* qs = s_q + s * A;
-    float acc = 0.f;
-    for (int a = lane; a < A; a += WAVE) acc += s_wa[a] * tanhf_(pc[a] + qs[a]);
-    acc = wave_sum(acc);
-    if (lane == 0) s_e[s * C + c] = acc + bias;
+  const int tid = threadIdx.x;
+  const float4* G = reinterpret_cast<const float4*>(gv + (int64_t)b * C * G4);
+  const int G44 = G4 >> 2;
+  // the video's frame gate rows (L2-resident, shared by its row groups) are
+  // requested first: their latency hides under the scores
+  // (register prefetch only for C <= 8: 2 x 8 float4 = 64 VGPRs)
+  const bool gpf = MAXC <= 8 && G44 <= ATT_GPF * ATT_THREADS;
+  float4 gr[ATT_GPF][MAXC];
+  if (gpf) {
+#pragma unroll
+    for (int j = 0; j < ATT_GPF; ++j)
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        gr[j][c] = (c < C && tid + j * ATT_THREADS < G44)
+                       ? G[(int64_t)c * G44 + tid + j * ATT_THREADS]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  __syncthreads();
+  int qrow[ATT_RPW];
+#pragma unroll
+  for (int s = 0; s < ATT_RPW; ++s) {
+    const int r = r0 + min(s, nr - 1);
+    qrow[s] = q_rowmap ? q_rowmap[r] : r;
+  }
+  float part[ATT_RPW][MAXC];
+#pragma unroll
+  for (int s = 0; s < ATT_RPW; ++s)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) part[s][c] = 0.f;
+  const float* P = pre + (int64_t)b * C * A;
+  for (int a = tid; a < A; a += ATT_THREADS) {
+    const float wa_a = wa[a];
+    float qv[ATT_RPW];
+#pragma unroll
+    for (int s = 0; s < ATT_RPW; ++s) qv[s] = q != nullptr ? q[(int64_t)qrow[s] * A + a] : 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < C) {
+        const float pc = P[(int64_t)c * A + a];
+#pragma unroll
+        for (int s = 0; s < ATT_RPW; ++s) part[s][c] += wa_a * tanhf_(pc + qv[s]);
+      }
+    }
+  }
+  block_sum_partials<MAXC>(part, s_red, s_e);
   if (tid < nr) {  // softmax over frames, one thread per row
-    float* e = s_e + tid * C;
+    float* e = s_e + tid * MAXC;
+    const float bias = ba[0];
     float m = -INFINITY;
-    for (int c = 0; c < C; ++c) m = fmaxf(m, e[c]);
+    for (int c = 0; c < C; ++c) m = fmaxf(m, e[c] + bias);
     float sum = 0.f;
     for (int c = 0; c < C; ++c) {
-      const float x = __expf(e[c] - m);
+      const float x = __expf(e[c] + bias - m);
       e[c] = x;
       sum += x;
     }
@@ -102,26 +177,48 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
   }
   __syncthreads();
   // vgate_r = sum_c alpha_rc Gv[b, c]: each thread owns float4 column groups
-  const float4* G = reinterpret_cast<const float4*>(gv + (int64_t)b * C * G4);
-  const int G44 = G4 >> 2;
-  for (int cg = tid; cg < G44; cg += ATT_THREADS) {
+  auto emit = [&](int cg, const float4* gcol) {
     float4 acc[ATT_RPW];
 #pragma unroll
     for (int s = 0; s < ATT_RPW; ++s) acc[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int c = 0; c < C; ++c) {
-      const float4 v = G[(int64_t)c * G44 + cg];
 #pragma unroll
-      for (int s = 0; s < ATT_RPW; ++s) {
-        const float al = s_e[min(s, nr - 1) * C + c];
-        acc[s].x += al * v.x;
-        acc[s].y += al * v.y;
-        acc[s].z += al * v.z;
-        acc[s].w += al * v.w;
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < C) {
+        const float4 v = gcol[c];
+#pragma unroll
+        for (int s = 0; s < ATT_RPW; ++s) {
+          const float al = s_e[min(s, nr - 1) * MAXC + c];
+          acc[s].x += al * v.x;
+          acc[s].y += al * v.y;
+          acc[s].z += al * v.z;
+          acc[s].w += al * v.w;
+        }
       }
     }
 #pragma unroll
-    for (int s = 0; s < ATT_RPW; ++s)
-      if (s < nr) reinterpret_cast<float4*>(vg_out + (int64_t)(r0 + s) * G4)[cg] = acc[s];
+    for (int s = 0; s < ATT_RPW; ++s) {
+      if (s < nr) {
+        float4* dst = reinterpret_cast<float4*>(vg_out + (int64_t)(r0 + s) * G4) + cg;
+        if (accumulate) {
+          const float4 o = *dst;
+          acc[s].x += o.x, acc[s].y += o.y, acc[s].z += o.z, acc[s].w += o.w;
+        }
+        *dst = acc[s];
+      }
+    }
+  };
+  if (gpf) {
+#pragma unroll
+    for (int j = 0; j < ATT_GPF; ++j)
+      if (tid + j * ATT_THREADS < G44) emit(tid + j * ATT_THREADS, gr[j]);
+  } else {
+    for (int cg = tid; cg < G44; cg += ATT_THREADS) {
+      float4 gcol[MAXC];
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        gcol[c] = c < C ? G[(int64_t)c * G44 + cg] : make_float4(0.f, 0.f, 0.f, 0.f);
+      emit(cg, gcol);
+    }
   }
 }
 
@@ -133,16 +230,35 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     const float* __restrict__ pre, const float* __restrict__ q, const float* __restrict__ alpha,
     const float* __restrict__ wa, int vdiv, int ngroups, int C, int A, int G4, int write_dq,
     float* __restrict__ dpre_part, float* __restrict__ dwa_part, float* __restrict__ dba_part) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* s_pre = sm;
-  float* s_q = s_pre + C * A;
-  float* s_wa = s_q + ATT_RPW * A;
-  float* s_red = s_wa + A;                                   // 4 waves x RPW x MAXC
-  float* s_de = s_red + (ATT_THREADS / WAVE) * ATT_RPW * MAXC;  // RPW x MAXC
+  __shared__ float s_red[ATT_WAVES * ATT_RPW * MAXC];
+  __shared__ float s_da[ATT_RPW * MAXC];
   const int b = blockIdx.x / ngroups, g = blockIdx.x % ngroups;
   const int r0 = b * vdiv + g * ATT_RPW, nr = min(ATT_RPW, vdiv - g * ATT_RPW);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  att_stage(s_pre, s_q, s_wa, pre, q, nullptr, wa, b, r0, nr, C, A);
+  const int tid = threadIdx.x;
+  // this block's accumulator slots of dP / dw_a (read-modify-write every
+  // reverse step) and its columns of P / q: requested up front, so the loads
+  // overlap phase 1
+  constexpr int AJ = 2;  // attention units per thread held in registers (A <= 512)
+  const bool apf = MAXC <= 8 && A <= AJ * ATT_THREADS;  // (register budget)
+  float acc_dp[AJ][MAXC], acc_dw[AJ], pv[AJ][MAXC], qv[AJ][ATT_RPW];
+  float* dpp = dpre_part + (int64_t)blockIdx.x * C * A;
+  float* dwp = dwa_part + (int64_t)blockIdx.x * A;
+  const float* P = pre + (int64_t)b * C * A;
+  if (apf) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int a = tid + j * ATT_THREADS;
+      acc_dw[j] = a < A ? dwp[a] : 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        acc_dp[j][c] = (a < A && c < C) ? dpp[c * A + a] : 0.f;
+        pv[j][c] = (a < A && c < C) ? P[c * A + a] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < ATT_RPW; ++s)
+        qv[j][s] = (a < A && q != nullptr && s < nr) ? q[(int64_t)(r0 + s) * A + a] : 0.f;
+    }
+  }
 
   // 1. dalpha[s][c] = dG_r . Gv[b, c]
   float part[ATT_RPW][MAXC];
@@ -173,34 +289,23 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
       }
     }
   }
-#pragma unroll
-  for (int s = 0; s < ATT_RPW; ++s)
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c < C) {
-        const float v = wave_sum(part[s][c]);
-        if (lane == 0) s_red[(w * ATT_RPW + s) * MAXC + c] = v;
-      }
-    }
-  __syncthreads();
-  // 2. softmax backward: de_c = alpha_c (dalpha_c - sum_k alpha_k dalpha_k)
+  block_sum_partials<MAXC>(part, s_red, s_da);
+  // 2. softmax backward: de_c = alpha_c (dalpha_c - sum_k alpha_k dalpha_k), in place
   if (tid < nr) {
     const float* al = alpha + (int64_t)(r0 + tid) * C;
-    float da[MAXC], sa = 0.f;
+    float* da = s_da + tid * MAXC;
+    float av[MAXC], sa = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      da[c] = 0.f;
-      if (c < C) {
-#pragma unroll
-        for (int k = 0; k < ATT_THREADS / WAVE; ++k) da[c] += s_red[(k * ATT_RPW + tid) * MAXC + c];
-        sa += al[c] * da[c];
-      }
+      av[c] = c < C ? al[c] : 0.f;
+      sa += c < C ? av[c] * da[c] : 0.f;
     }
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
-      if (c < C) s_de[tid * MAXC + c] = al[c] * (da[c] - sa);
+      if (c < C) da[c] = av[c] * (da[c] - sa);
   }
   __syncthreads();
+  const float* s_de = s_da;
   if (tid == 0) {
     float sb = 0.f;
     for (int s = 0; s < nr; ++s)
@@ -209,55 +314,81 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   }
   // 3. scorer backward, thread per attention unit a:
   //    dz = de_c w_a (1 - u^2), u = tanh(P_c + q_s); dq_s = sum_c dz; dP_c = sum_s dz
-  for (int a = tid; a < A; a += ATT_THREADS) {
-    const float wa_a = s_wa[a];
+  auto unit = [&](int a, const float* pa, const float* qa, float (&dp)[MAXC], float& dwa) {
+    const float wa_a = wa[a];
     float dq[ATT_RPW];
 #pragma unroll
     for (int s = 0; s < ATT_RPW; ++s) dq[s] = 0.f;
-    float dwa = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const float pc = s_pre[c * A + a];
-      float dp = 0.f;
 #pragma unroll
-      for (int s = 0; s < ATT_RPW; ++s) {
-        if (s < nr) {
-          const float u = tanhf_(pc + s_q[s * A + a]);
-          const float de = s_de[s * MAXC + c];
-          dwa += de * u;
-          const float dz = de * wa_a * (1.f - u * u);
-          dq[s] += dz;
-          dp += dz;
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < C) {
+#pragma unroll
+        for (int s = 0; s < ATT_RPW; ++s) {
+          if (s < nr) {
+            const float u = tanhf_(pa[c] + qa[s]);
+            const float de = s_de[s * MAXC + c];
+            dwa += de * u;
+            const float dz = de * wa_a * (1.f - u * u);
+            dq[s] += dz;
+            dp[c] += dz;
+          }
         }
       }
-      dpre_part[((int64_t)blockIdx.x * C + c) * A + a] += dp;
     }
-    dwa_part[(int64_t)blockIdx.x * A + a] += dwa;
     if (write_dq) {
 #pragma unroll
       for (int s = 0; s < ATT_RPW; ++s)
         if (s < nr) dG[(int64_t)(r0 + s) * ldg + G4 + a] = f2bf(dq[s]);
+    }
+  };
+  if (apf) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int a = tid + j * ATT_THREADS;
+      if (a < A) {
+        unit(a, pv[j], qv[j], acc_dp[j], acc_dw[j]);
+        dwp[a] = acc_dw[j];
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+          if (c < C) dpp[c * A + a] = acc_dp[j][c];
+      }
+    }
+  } else {
+    for (int a = tid; a < A; a += ATT_THREADS) {
+      float dp[MAXC], pa[MAXC], qa[ATT_RPW], dw = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        dp[c] = 0.f;
+        pa[c] = c < C ? P[c * A + a] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < ATT_RPW; ++s)
+        qa[s] = (q != nullptr && s < nr) ? q[(int64_t)(r0 + s) * A + a] : 0.f;
+      unit(a, pa, qa, dp, dw);
+      dwp[a] += dw;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < C) dpp[c * A + a] += dp[c];
     }
   }
 }
 
 int att_groups(int vdiv) { return (vdiv + ATT_RPW - 1) / ATT_RPW; }
 
-static size_t att_lds_bytes(int C, int A, int maxc) {
-  return sizeof(float) * ((size_t)C * A + ATT_RPW * A + A +
-                          (size_t)(ATT_THREADS / WAVE + 1) * ATT_RPW * maxc);
-}
-
-size_t att_max_lds() { return 64 * 1024; }
-
-size_t att_lds_need(int C, int A) { return att_lds_bytes(C, A, C <= 8 ? 8 : C <= 16 ? 16 : 32); }
-
 void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
                     const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
-                    float* vg_out, float* alpha_out, hipStream_t stream) {
+                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate) {
   const int ng = att_groups(vdiv);
-  const size_t lds = sizeof(float) * ((size_t)C * A + ATT_RPW * A + A + ATT_RPW * C);
-  hipLaunchKernelGGL(att_fwd_kernel, dim3(Bv * ng), dim3(ATT_THREADS), lds, stream, gv, pre, q,
-                     q_rowmap, wa, ba, vdiv, ng, C, A, G4, vg_out, alpha_out);
+#define ATT_FWD(M)                                                                          \
+  hipLaunchKernelGGL(att_fwd_kernel<M>, dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, gv, pre, \
+                     q, q_rowmap, wa, ba, vdiv, ng, C, A, G4, vg_out, alpha_out, accumulate)
+  if (C <= 8)
+    ATT_FWD(8);
+  else if (C <= 16)
+    ATT_FWD(16);
+  else
+    ATT_FWD(32);
+#undef ATT_FWD
 }
 
 template <int MAXC>
@@ -266,9 +397,9 @@ static void launch_att_bwd_t(uint16_t* dG, int ldg, const float* gv, const float
                              int C, int A, int G4, int write_dq, float* dpre_part, float* dwa_part,
                              float* dba_part, hipStream_t stream) {
   const int ng = att_groups(vdiv);
-  hipLaunchKernelGGL(att_bwd_kernel<MAXC>, dim3(Bv * ng), dim3(ATT_THREADS),
-                     att_lds_bytes(C, A, MAXC), stream, dG, ldg, gv, pre, q, alpha, wa, vdiv, ng,
-                     C, A, G4, write_dq, dpre_part, dwa_part, dba_part);
+  hipLaunchKernelGGL(att_bwd_kernel<MAXC>, dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, dG, ldg,
+                     gv, pre, q, alpha, wa, vdiv, ng, C, A, G4, write_dq, dpre_part, dwa_part,
+                     dba_part);
 }
 
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,

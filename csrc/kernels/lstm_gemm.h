@@ -3,7 +3,11 @@
 //
 //   pre_{t+1}[r][n] = sum_k h_t[r][k] W_hh[n][k] + vgate[r / vdiv][n]
 //
-// (packed gate order, fp32 out).  It depends only on h_t, not on the token
+// (packed gate order, fp32 out).  With temporal attention the weight operand
+// carries NQ = A extra rows (W_q): those tiles write the attention query of
+// step t+1, q_{t+1} = h_t W_q^T, to q_out instead, and vgate is nullptr (the
+// attention kernel adds the per-row video term into pre afterwards).
+//  It depends only on h_t, not on the token
 // sampled at step t, so it runs CONCURRENTLY with vocab_t; the input-token
 // term P[tok_{t+1}] and the cell nonlinearity are applied by the combine
 // kernel once the token is known (vocab_combine_kernel's cell epilogue).
@@ -21,15 +25,16 @@ __device__ __forceinline__ int xcd_remap_g(int bid, int nwg) {
 constexpr int LG_BM = 128, LG_BN = 64, LG_STAGES = 3;
 using LGTile = Tile<LG_BM, LG_BN, LG_STAGES>;
 
-__host__ __device__ constexpr int lstm_gemm_blocks(int R, int H) {
-  return ((4 * H) / LG_BN) * ((R + LG_BM - 1) / LG_BM);
+__host__ __device__ constexpr int lstm_gemm_blocks(int R, int H, int NQ = 0) {
+  return ((4 * H + NQ) / LG_BN) * ((R + LG_BM - 1) / LG_BM);
 }
 
 __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restrict__ h, int R,
                                                 int H, const uint16_t* __restrict__ whh,
                                                 const float* __restrict__ vgate, int vdiv,
-                                                float* __restrict__ pre, char* lds) {
-  const int n_nt = (4 * H) / LG_BN, n_rt = (R + LG_BM - 1) / LG_BM;
+                                                float* __restrict__ pre, char* lds,
+                                                int NQ = 0, float* __restrict__ q_out = nullptr) {
+  const int n_nt = (4 * H + NQ) / LG_BN, n_rt = (R + LG_BM - 1) / LG_BM;
   const int b = xcd_remap_g(bid, n_nt * n_rt);
   const int nt = b / n_rt, rt = b % n_rt;
   const int r0 = rt * LG_BM, n0 = nt * LG_BN;
@@ -47,7 +52,7 @@ __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restr
       a.voff0[i] = min(r0 + row, R - 1) * H * 2 + dma_chunk(row, lane) * 16;
       a.voff1[i] = a.voff0[i];
     }
-    bsrc.r0 = bsrc.r1 = make_rsrc(whh, (int64_t)4 * H * H * 2);
+    bsrc.r0 = bsrc.r1 = make_rsrc(whh, (int64_t)(4 * H + NQ) * H * 2);
     bsrc.ksplit = nk;
 #pragma unroll
     for (int i = 0; i < LG_BN / 32; ++i) {
@@ -62,15 +67,22 @@ __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restr
   __syncthreads();
   // 16 lanes per row x 4 columns: 256-byte coalesced fp32 rows
   const int u = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const bool qtile = n0 >= 4 * H;
 #pragma unroll 4
   for (int i = 0; i < LG_BM / 16; ++i) {
     const int row = rg + 16 * i, r = r0 + row;
     if (r < R) {
       const float4 x = *reinterpret_cast<const float4*>(C + row * LGTile::CSTRIDE + 4 * u);
-      const float4 vg =
-          *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * (4 * H) + n0 + 4 * u);
-      *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) =
-          make_float4(x.x + vg.x, x.y + vg.y, x.z + vg.z, x.w + vg.w);
+      if (qtile) {
+        *reinterpret_cast<float4*>(q_out + (int64_t)r * NQ + (n0 - 4 * H) + 4 * u) = x;
+      } else if (vgate != nullptr) {
+        const float4 vg =
+            *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * (4 * H) + n0 + 4 * u);
+        *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) =
+            make_float4(x.x + vg.x, x.y + vg.y, x.z + vg.z, x.w + vg.w);
+      } else {
+        *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) = x;
+      }
     }
   }
 }

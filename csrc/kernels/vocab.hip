@@ -532,11 +532,12 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(VOCAB_TR_PARAMS)
 template <int BN, int STAGES, int OCC>
 __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
     VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
-    const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad) {
+    const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad, int NQ,
+    float* __restrict__ q_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   if ((int)blockIdx.x < n_lstm_pad) {
-    if ((int)blockIdx.x < lstm_gemm_blocks(R, H))
-      lstm_gemm_block(blockIdx.x, h_t, R, H, whh, vgate, vdiv, pre, lds);
+    if ((int)blockIdx.x < lstm_gemm_blocks(R, H, NQ))
+      lstm_gemm_block(blockIdx.x, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
     return;
   }
   vocab_tr_block<BN, STAGES>(blockIdx.x - n_lstm_pad, lds, VOCAB_TR_ARGS);
@@ -977,14 +978,14 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
                                 float inv_temp, uint32_t seed, int step, const uint16_t* h_t,
                                 const uint16_t* whh, const float* vgate, int vdiv, float* pre,
-                                hipStream_t stream) {
+                                int NQ, float* q_out, hipStream_t stream) {
   using TL = Tile<VT_V, BN, STAGES>;
   constexpr int LV = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
                          ? TL::STAGES * TL::STAGE_BYTES
                          : 4 * BN * (int)sizeof(GroupStat);
   constexpr int LDS = LV > LGTile::LDS_BYTES ? LV : LGTile::LDS_BYTES;
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
-  const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H) + 7) / 8 * 8 : 0;
+  const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H, NQ) + 7) / 8 * 8 : 0;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC>,
@@ -993,21 +994,24 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   }
   hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC>), dim3(n_l + n_vt * n_rt), dim3(256),
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
-                     tgt, tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, n_l);
+                     tgt, tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, n_l,
+                     NQ, q_out);
 }
 
 void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                            const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                            uint32_t seed, int step, const uint16_t* h_t, const uint16_t* whh,
-                           const float* vgate, int vdiv, float* pre, hipStream_t stream) {
+                           const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
+                           float* q_out) {
   if (R <= 64)
     launch_vocab_lstm_t<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
-                                  flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, stream);
+                                  flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, NQ,
+                                  q_out, stream);
   else
     launch_vocab_lstm_t<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
                                    tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv,
-                                   pre, stream);
+                                   pre, NQ, q_out, stream);
 }
 
 int vocab_bwd_ds_blocks(int T, int R) { return (int)(((int64_t)T * R + DS_ROWS - 1) / DS_ROWS); }

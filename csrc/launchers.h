@@ -50,12 +50,15 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           float ss_prob, uint32_t seed, int step, int* counts, int count_step,
                           uint8_t* unfinished, hipStream_t stream, const CellLaunch* cell = nullptr);
 // vocab projection of step t + recurrent GEMM of step t+1 in one launch
-// (transposed-epilogue vocab kernel; pre == nullptr: vocab only)
+// (transposed-epilogue vocab kernel; pre == nullptr: vocab only).  NQ > 0:
+// whh has 4H + NQ rows, the last NQ (W_q) produce the attention query q_out
+// (R x NQ) and vgate must be nullptr.
 void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                            const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                            uint32_t seed, int step, const uint16_t* h_t, const uint16_t* whh,
-                           const float* vgate, int vdiv, float* pre, hipStream_t stream);
+                           const float* vgate, int vdiv, float* pre, hipStream_t stream,
+                           int NQ = 0, float* q_out = nullptr);
 int vocab_bwd_ds_blocks(int T, int R);
 // rows [row_begin, row_end) of the (T*R, ldl) buffer; row_begin % vocab_bwd_ds_rows() == 0
 void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
@@ -87,11 +90,10 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
 
 // attention.hip (temporal attention over num_chunks frames)
 int att_groups(int vdiv);
-size_t att_lds_need(int C, int A);
-size_t att_max_lds();
+// vg_out[r] = sum_c alpha_rc Gv[b, c]  (+= when accumulate: adds into pre)
 void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
                     const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
-                    float* vg_out, float* alpha_out, hipStream_t stream);
+                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate = 0);
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,
                     const float* alpha, const float* wa, int Bv, int vdiv, int C, int A, int G4,
                     int write_dq, float* dpre_part, float* dwa_part, float* dba_part,

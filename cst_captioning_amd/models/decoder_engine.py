@@ -47,14 +47,7 @@ from ..utils.text import BOS
 
 SEL_GT, SEL_SAMPLE, SEL_GREEDY, SEL_SS = 0, 1, 2, 3
 
-ATT_MAX_CHUNKS = 32
-ATT_LDS_LIMIT = 64 * 1024
-
-
-def att_lds_bytes(C, A):
-    """LDS of the attention backward kernel (csrc/kernels/attention.hip)."""
-    maxc = 8 if C <= 8 else 16 if C <= 16 else 32
-    return 4 * (C * A + 4 * A + A + 5 * 4 * maxc)
+ATT_MAX_CHUNKS = 32  # frames per video supported by csrc/kernels/attention.hip
 
 
 def engine_supports(opt):
@@ -64,7 +57,7 @@ def engine_supports(opt):
           and opt.rnn_size % 64 == 0)
     C = getattr(opt, 'num_chunks', 1)
     if ok and C > 1:  # attention size == rnn_size (TemporalAttention)
-        ok = C <= ATT_MAX_CHUNKS and att_lds_bytes(C, opt.rnn_size) <= ATT_LDS_LIMIT
+        ok = C <= ATT_MAX_CHUNKS
     return ok
 
 
@@ -82,7 +75,8 @@ class _DecoderFn(torch.autograd.Function):
                    att_ba.detach().float().contiguous().view(-1)]
         vg_in = torch.empty(0, device=dev) if has_att else vgate.detach().float().contiguous()
         outs = _ext.ops().decoder_forward(
-            eng.wx, eng.emb, eng.ptab, eng.whh, eng.wlog, logit_b.detach().float().contiguous(),
+            eng.wx, eng.emb, eng.ptab, eng.whh_q if has_att else eng.whh, eng.wlog,
+            logit_b.detach().float().contiguous(),
             vg_in, vdiv,
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
@@ -188,6 +182,9 @@ class DecoderEngine:
         self.ptab = torch.mm(self.emb, self.wx[:, :E].t(), out_dtype=torch.float32)
         if self.attention:
             self.wq = m.temporal_att.f_h.weight.detach().to(torch.bfloat16).contiguous()
+            # [W_hh; W_q]: the decode step's recurrent GEMM also projects the
+            # next step's attention query
+            self.whh_q = torch.cat([self.whh, self.wq], 0).contiguous()
 
     def attach_optimizer(self, trainer):
         self.refresh_weights()  # params were re-homed into the flat buffer
