@@ -19,6 +19,7 @@ image, so this module re-implements the metrics from their definitions:
 
 Tokenisation approximates the PTB tokenizer + coco punctuation removal.
 """
+import logging
 import math
 import os
 import re
@@ -137,6 +138,9 @@ def _porter_light(w):
     return w
 
 
+_METEOR_WARNED = False
+
+
 class Meteor:
     alpha, beta, gamma = 0.85, 0.2, 0.6
     w_exact, w_stem = 1.0, 0.6
@@ -145,6 +149,12 @@ class Meteor:
         jar = os.environ.get('METEOR_JAR')
         self.java = bool(jar and os.path.isfile(jar) and shutil.which('java'))
         self.jar = jar
+        global _METEOR_WARNED
+        if not self.java and not _METEOR_WARNED:
+            _METEOR_WARNED = True
+            logging.getLogger(__name__).warning(
+                'METEOR: java or $METEOR_JAR missing -- using the native approximation '
+                '(parity with coco-caption METEOR unpinned)')
 
     def _align(self, h, r):
         used = [False] * len(r)
