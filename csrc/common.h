@@ -10,8 +10,54 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <stdexcept>
+#include <string>
 
 namespace cst {
+
+// ---- debugging aids -------------------------------------------
+// Device-side bounds checks, compiled in by the debug build
+// (CSTCAP_KERNEL_DEBUG=1 python setup.py build_ext --inplace, which adds
+// -DCST_KERNEL_DEBUG): a failed check prints the condition and the block /
+// thread and execution continues on the kernel's own clamped index (no trap:
+// a trapping wave can take the whole node down on the shared pool).
+#ifdef CST_KERNEL_DEBUG
+#define CST_DCHECK(cond)                                                               \
+  do {                                                                                 \
+    if (!(cond))                                                                       \
+      printf("CST_DCHECK failed %s:%d: %s (block %d, thread %d)\n", __FILE__, __LINE__, \
+             #cond, (int)blockIdx.x, (int)threadIdx.x);                                \
+  } while (0)
+#else
+#define CST_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
+// Host-side launch checking, after every kernel launch of the runtime:
+// CSTCAP_LAUNCH_CHECK=1 -> hipGetLastError (bad grid / LDS / arguments);
+// CSTCAP_LAUNCH_CHECK=2 -> also synchronise the stream, so an asynchronous
+// fault is reported against the kernel that caused it (HIP_LAUNCH_BLOCKING
+// for this runtime only).  Raises std::runtime_error (RuntimeError in Python).
+inline int launch_check_mode() {
+  static const int mode = [] {
+    const char* e = getenv("CSTCAP_LAUNCH_CHECK");
+    return e ? atoi(e) : 0;
+  }();
+  return mode;
+}
+inline void post_launch(const char* kernel, hipStream_t stream) {
+  const int mode = launch_check_mode();
+  if (mode == 0) return;
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && mode > 1) e = hipStreamSynchronize(stream);
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("HIP error after ") + kernel + ": " +
+                             hipGetErrorString(e));
+}
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));

@@ -111,10 +111,12 @@ void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, f
   int blocks = (int)std::min<int64_t>(ADAM_MAX_PARTIALS, std::max<int64_t>(1, (n / 4 + 255) / 256));
   hipLaunchKernelGGL(adam_sumsq_kernel, dim3(blocks), dim3(ADAM_THREADS), 0, stream, g, n,
                      partials);
+  post_launch("adam_sumsq_kernel", stream);
   int ublocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n / 4 + 255) / 256));
   hipLaunchKernelGGL(adam_update_kernel, dim3(ublocks), dim3(ADAM_THREADS), 0, stream, p, g, m,
                      v, n, partials, blocks, skip, scal, lr / bc1, b1, b2, eps,
                      1.f / sqrtf(bc2), clip);
+  post_launch("adam_update_kernel", stream);
 }
 
 }  // namespace cst

@@ -136,7 +136,9 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
   for (int s = 0; s < ATT_RPW; ++s) {
     const int r = r0 + min(s, nr - 1);
     qrow[s] = q_rowmap ? q_rowmap[r] : r;
+    CST_DCHECK(qrow[s] >= 0 && qrow[s] < (int)(gridDim.x / ngroups) * vdiv);
   }
+  CST_DCHECK(nr >= 1 && g * ATT_RPW + nr <= vdiv);
   float part[ATT_RPW][MAXC];
 #pragma unroll
   for (int s = 0; s < ATT_RPW; ++s)
@@ -389,6 +391,7 @@ void launch_att_fwd(const float* gv, const float* pre, const float* q, const int
   else
     ATT_FWD(32);
 #undef ATT_FWD
+  post_launch("att_fwd_kernel", stream);
 }
 
 template <int MAXC>
@@ -400,6 +403,7 @@ static void launch_att_bwd_t(uint16_t* dG, int ldg, const float* gv, const float
   hipLaunchKernelGGL(att_bwd_kernel<MAXC>, dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, dG, ldg,
                      gv, pre, q, alpha, wa, vdiv, ng, C, A, G4, write_dq, dpre_part, dwa_part,
                      dba_part);
+  post_launch("att_bwd_kernel", stream);
 }
 
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,

@@ -173,6 +173,7 @@ void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, con
                       float* top_v, int* top_i, hipStream_t stream) {
   hipLaunchKernelGGL(beam_topk_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, logits, ldl, V,
                      R, K, lse, top_v, top_i);
+  post_launch("beam_topk_kernel", stream);
 }
 
 void launch_beam_step(const float* top_v, const int* top_i, int B, int K, int T, int t,
@@ -182,6 +183,7 @@ void launch_beam_step(const float* top_v, const int* top_i, int B, int K, int T,
   hipLaunchKernelGGL(beam_step_kernel, dim3(B), dim3(64), 0, stream, top_v, top_i, B, K, T, t,
                      beam_sum, seq_hist, lp_hist, best_ppl, best_seq, best_lp, tok_out,
                      parent_out);
+  post_launch("beam_step_kernel", stream);
 }
 
 }  // namespace cst

@@ -155,6 +155,7 @@ void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
   hipLaunchKernelGGL(cider_d_kernel, grid, block, 0, stream, hyps, T, hyp_video, N, ht_keys,
                      ht_vals, ht_cap, vid_ref_off, ref_ng_off, ref_norm, ref_len, ng_key,
                      ng_val, log_ref_len, use_eos, out);
+  post_launch("cider_d_kernel", stream);
 }
 
 }  // namespace cst

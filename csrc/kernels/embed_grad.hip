@@ -24,6 +24,7 @@ __global__ __launch_bounds__(256) void token_rows_sum_kernel(
   if ((int)threadIdx.x < n) {
     s_tok[threadIdx.x] = (int)stok[i0 + threadIdx.x];
     s_row[threadIdx.x] = (int)srow[i0 + threadIdx.x];
+    CST_DCHECK(s_tok[threadIdx.x] >= 0 && s_row[threadIdx.x] >= 0 && s_row[threadIdx.x] < N);
   }
   __syncthreads();
   const int nj = (C + 255) >> 8;
@@ -68,6 +69,7 @@ void launch_token_rows_sum(const float* x, int C, const int64_t* stok, const int
                            float* out, hipStream_t stream) {
   hipLaunchKernelGGL(token_rows_sum_kernel, dim3((N + EG_ROWS - 1) / EG_ROWS), dim3(256), 0,
                      stream, x, C, stok, srow, N, out);
+  post_launch("token_rows_sum_kernel", stream);
 }
 
 }  // namespace cst

@@ -70,6 +70,8 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     pre_px[i] = *reinterpret_cast<const float4*>(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u);
     pre_vg[i] = *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
     pre_c[i] = c_prev[(int64_t)(row_map ? row_map[r] : r) * H + hu];
+    CST_DCHECK(s_tok[row] >= 0);
+    CST_DCHECK(row_map == nullptr || (row_map[r] >= 0 && row_map[r] < R));
   }
 
   f32x16 acc[LTile::TM][LTile::TN];
@@ -280,6 +282,7 @@ static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT
   hipLaunchKernelGGL(lstm_step_bwd_kernel<BM>, dim3(n), dim3(256), TL::LDS_BYTES, stream,
                      dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
                      step, dG, KD);
+  post_launch("lstm_step_bwd_kernel", stream);
 }
 
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
@@ -312,6 +315,7 @@ static void launch_lstm_step_fwd_t(const int64_t* tok, int64_t tok_stride, const
   hipLaunchKernelGGL((lstm_step_fwd_kernel<BM, STAGES>), dim3(n_nt * n_rt), dim3(256), LDS,
                      stream, tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh,
                      h_out, c_out, hdrop_out, ldh, drop_p, seed, step, gates_out, row_map);
+  post_launch("lstm_step_fwd_kernel", stream);
 }
 
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
@@ -339,6 +343,7 @@ void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_
   hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream, dh_logit, dh_rec, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
                      step, dG);
+  post_launch("lstm_cell_bwd_kernel", stream);
 }
 
 }  // namespace cst

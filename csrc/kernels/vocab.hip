@@ -670,6 +670,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
         unfinished[r] = u;
         if (!u) tok = 0;
       }
+      CST_DCHECK(tok >= 0 && tok < (int64_t)n_vt * VT_V);
       tok_out[(int64_t)r * tok_stride] = tok;
       if (g_sel) g_sel[(int64_t)r * gsel_stride] = tl - lse;
       if (counts != nullptr && tok != 0) atomicAdd(&s_nonzero, 1);
@@ -881,6 +882,7 @@ static void launch_vocab_fwd_t(const uint16_t* hd, int ldh, int R, int H, const 
   hipLaunchKernelGGL((vocab_fwd_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256),
                      TL::LDS_BYTES, stream, hd, ldh, R, H, W, bias, V, logits16, ldl,
                      (VocabPartial*)part, tgt, tgt_stride, do_sample, inv_temp, seed, step);
+  post_launch("vocab_fwd_kernel", stream);
 }
 
 template <int BN, int STAGES, int OCC>
@@ -902,6 +904,7 @@ static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const
   hipLaunchKernelGGL((vocab_fwd_tr_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256), LDS,
                      stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt,
                      tgt_stride, flags, inv_temp, seed, step);
+  post_launch("vocab_fwd_tr_kernel", stream);
 }
 
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
@@ -970,6 +973,7 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                      (const VocabPartial*)part, n_vt, R, lse_out, tok_out, tok_stride, g_sel,
                      gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode, ss_prob, seed, step,
                      counts, count_step, unfinished, cell);
+  post_launch("vocab_combine_kernel", stream);
 }
 
 template <int BN, int STAGES, int OCC>
@@ -996,6 +1000,7 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
                      tgt, tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, n_l,
                      NQ, q_out);
+  post_launch("vocab_lstm_fwd_kernel", stream);
 }
 
 void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
@@ -1040,6 +1045,7 @@ void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_
     default: DS_LAUNCH(8); break;
   }
 #undef DS_LAUNCH
+  post_launch("vocab_bwd_ds_kernel", stream);
 }
 
 }  // namespace cst

@@ -28,6 +28,12 @@ OBJ_DIR = os.path.join(HERE, 'build', 'hip_objs')
 HIP_SOURCES = sorted(glob.glob(os.path.join(HERE, 'csrc', 'kernels', '*.hip')))
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-munsafe-fp-atomics',
              '-I' + os.path.join(HERE, 'csrc')]
+# Debug build of the kernels: CSTCAP_KERNEL_DEBUG=1 compiles the
+# device-side CST_DCHECK bounds checks in (separate object directory).  Pair it
+# with CSTCAP_LAUNCH_CHECK=2 at run time to synchronise after every launch.
+if os.environ.get('CSTCAP_KERNEL_DEBUG') == '1':
+    HIP_FLAGS += ['-DCST_KERNEL_DEBUG', '-g']
+    OBJ_DIR = os.path.join(HERE, 'build', 'hip_objs_debug')
 
 
 def hip_objects():
