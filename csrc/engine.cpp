@@ -120,6 +120,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor g_sel = at::zeros({R, T - 1}, f32);
   at::Tensor g_xe = want_xe ? at::zeros({R, T}, f32) : at::Tensor();
   at::Tensor lse = at::empty({n_steps, R}, f32);
+  static const bool merged = [] {
+    const char* e = std::getenv("CSTCAP_FWD_MERGED");  // A/B knob (default on)
+    return e == nullptr || std::atoi(e) != 0;
+  }();
   const int n_vt = vocab_num_tiles((int)V);
   at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4}, f32);
   at::Tensor counts = at::zeros({T + 1}, at::TensorOptions().dtype(at::kInt).device(dev));
@@ -192,10 +196,6 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   const float* VG = has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>();
   const int VDIV = has_att ? 1 : (int)vgate_div;
 
-  static const bool merged = [] {
-    const char* e = std::getenv("CSTCAP_FWD_MERGED");  // A/B knob (default on)
-    return e == nullptr || std::atoi(e) != 0;
-  }();
   if (!merged) {  // reference structure: LSTM step -> vocab -> combine, per step
     for (int64_t t = 0; t < n_steps; ++t) {
       const int64_t* tok = t == 0 ? (have_labels ? LAB : bos.data_ptr<int64_t>())
@@ -417,6 +417,18 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dwa_part = at::zeros({nwg, A}, f32);
     dba_part = at::zeros({nwg}, f32);
   }
+  // split-K of the fused backward step (CSTCAP_BWD_SPLITK, default 1).  On
+  // MI355X S = 2..4 measured SLOWER (73 vs 29.5 us per step, bench 6.5 vs
+  // 5.0 ms): the reverse loop shares the GPU with the side stream's dWlog
+  // GEMM, and the extra blocks queue behind it instead of filling idle CUs
+  static const int splitk = [] {
+    const char* e = std::getenv("CSTCAP_BWD_SPLITK");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
+  }();
+  const int64_t n_bt = lstm_bwd_tiles((int)R, (int)H);
+  at::Tensor bwd_ws = splitk > 1 ? at::empty({n_bt * splitk * 64 * 64}, f32) : at::Tensor();
+  at::Tensor bwd_cnt = splitk > 1 ? at::zeros({n_bt}, at::TensorOptions().dtype(at::kInt).device(dev))
+                                  : at::Tensor();
   int waited = n_chunks;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     int need = 0;  // chunk holding the first row of step t (chunks finish high to low)
@@ -428,7 +440,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
         c_all[t].data_ptr<float>(), t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R,
         (int)H, (float)drop_p, seed_drop, (int)t,
-        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st);
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, splitk,
+        splitk > 1 ? bwd_ws.data_ptr<float>() : nullptr,
+        splitk > 1 ? bwd_cnt.data_ptr<int>() : nullptr);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),

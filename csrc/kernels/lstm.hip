@@ -176,39 +176,62 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
 //   dh     = dh_rec + mask * dh_logit / (1 - p)
 //   cell backward of step t in the epilogue -> dG_t (bf16, packed gates),
 //   dc_carry <- dc * f.
-// One block owns BM rows x 64 hidden units; every epilogue operand is
-// prefetched before the main loop.
+// One tile = BM rows x 64 hidden units: only (R/BM) x (H/64) = 160 tiles at
+// R = 1280, H = 512 -- fewer than the 256 CUs, each a 32-deep K loop.  So the
+// K = 4H (+A) reduction is split S ways (split-K): S blocks per tile each
+// reduce a K range, publish their fp32 partial tile to `ws`, and the LAST of
+// them to arrive (per-tile atomic counter, reset by that block for the next
+// launch) sums the partials and runs the cell epilogue.  S = 1 keeps the
+// original single-pass kernel with every epilogue operand prefetched before
+// the main loop.
+template <int BM>
+__device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, int hu,
+                                                  const uint16_t* __restrict__ gates,
+                                                  const float* __restrict__ c_t,
+                                                  const float* __restrict__ c_prev,
+                                                  const float* __restrict__ dc_carry,
+                                                  const float* __restrict__ dh_logit,
+                                                  uint2* pg, float* pc, float* pcp, float* pdc,
+                                                  float* pdl) {
+  constexpr int RPT = BM / 4;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = min(r0 + rg + 4 * i, R - 1);
+    const int64_t o = (int64_t)r * H + hu;
+    pg[i] = *reinterpret_cast<const uint2*>(gates + (int64_t)r * 4 * H + 4 * hu);
+    pc[i] = c_t[o];
+    pcp[i] = c_prev ? c_prev[o] : 0.f;
+    pdc[i] = dc_carry[o];
+    pdl[i] = dh_logit[o];
+  }
+}
+
 template <int BM>
 __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
     const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
     const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
-    uint16_t* __restrict__ dG, int KD) {
+    uint16_t* __restrict__ dG, int KD, int S, float* __restrict__ ws, int* __restrict__ tile_cnt) {
   using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int n_ut = H / 64, n_rt = (R + BM - 1) / BM;
-  const int b = xcd_remap_l(blockIdx.x, n_ut * n_rt);
+  __shared__ int s_last;
+  const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
+  const int tile = blockIdx.x % n_tiles, split = blockIdx.x / n_tiles;
+  const int b = xcd_remap_l(tile, n_tiles);
   const int ut = b / n_rt, rt = b % n_rt;
   const int r0 = rt * BM, u0 = ut * 64;
-  const int H4 = 4 * H;
-  const int nk = dg_next != nullptr ? KD / 64 : 0;  // KD = 4H (+ A with attention)
+  const int nk_all = dg_next != nullptr ? KD / 64 : 0;  // KD = 4H (+ A with attention)
+  const int k0 = split * nk_all / S, nk = (split + 1) * nk_all / S - k0;
   const int tid = threadIdx.x, u = tid & 63, rg = tid >> 6;
   const int hu = u0 + u;
   constexpr int RPT = BM / 4;
 
   uint2 pg[RPT];
   float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int r = min(r0 + rg + 4 * i, R - 1);
-    const int64_t o = (int64_t)r * H + hu;
-    pg[i] = *reinterpret_cast<const uint2*>(gates + (int64_t)r * H4 + 4 * hu);
-    pc[i] = c_t[o];
-    pcp[i] = c_prev ? c_prev[o] : 0.f;
-    pdc[i] = dc_carry[o];
-    pdl[i] = dh_logit[o];
-  }
+  if (S == 1)  // single pass: the epilogue operands' latency hides under the GEMM
+    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, pg, pc, pcp,
+                          pdc, pdl);
 
   f32x16 acc[TL::TM][TL::TN];
   {
@@ -220,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < BM / 32; ++i) {
       const int row = dma_row(w, i, lane);
-      a.voff0[i] = min(r0 + row, R - 1) * KD * 2 + dma_chunk(row, lane) * 16;
+      a.voff0[i] = min(r0 + row, R - 1) * KD * 2 + k0 * 128 + dma_chunk(row, lane) * 16;
       a.voff1[i] = a.voff0[i];
     }
     bsrc.r0 = bsrc.r1 = make_rsrc(whhT, (int64_t)H * KD * 2);
@@ -228,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = dma_row(w, i, lane);
-      bsrc.voff0[i] = (u0 + row) * KD * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff0[i] = (u0 + row) * KD * 2 + k0 * 128 + dma_chunk(row, lane) * 16;
       bsrc.voff1[i] = bsrc.voff0[i];
     }
     gemm_nt_mainloop<TL>(nk, a, bsrc, lds, acc);
@@ -236,6 +259,47 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
   float* C = reinterpret_cast<float*>(lds);
   store_acc_to_lds<TL>(acc, C, [](int) { return 0.f; });
   __syncthreads();
+
+  if (S > 1) {
+    constexpr int TE = BM * 64;
+    float* mine = ws + ((int64_t)tile * S + split) * TE;
+    for (int i = 4 * tid; i < TE; i += 4 * 256) {
+      const float* c = C + (i >> 6) * TL::CSTRIDE + (i & 63);
+      *reinterpret_cast<float4*>(mine + i) = make_float4(c[0], c[1], c[2], c[3]);
+    }
+    __threadfence();  // release: the partial is visible device-wide before the count
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(&tile_cnt[tile], 1) == S - 1;
+    __syncthreads();
+    if (!s_last) return;
+    // acquire: the device-scope fence also invalidates this CU's L1, so the
+    // plain (batched, non-serialised) loads below see the other blocks' partials
+    __threadfence();
+    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, pg, pc, pcp,
+                          pdc, pdl);
+    const float4* wsv = reinterpret_cast<const float4*>(ws + (int64_t)tile * S * TE);
+    constexpr int PER = TE / 4 / 256;  // float4 per thread per partial
+    float4 sum[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) sum[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < S; ++k) {
+      if (k == split) continue;
+      float4 v[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) v[j] = wsv[k * (TE / 4) + tid + 256 * j];
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        sum[j].x += v[j].x, sum[j].y += v[j].y, sum[j].z += v[j].z, sum[j].w += v[j].w;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = 4 * (tid + 256 * j);
+      float* c = C + (i >> 6) * TL::CSTRIDE + (i & 63);
+      c[0] += sum[j].x, c[1] += sum[j].y, c[2] += sum[j].z, c[3] += sum[j].w;
+    }
+    if (tid == 0) tile_cnt[tile] = 0;  // ready for the next launch
+    __syncthreads();
+  }
 
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
 #pragma unroll
@@ -264,13 +328,15 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
   }
 }
 
+int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
 template <int BM>
 static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT,
                                    const float* dh_logit, float* dc_carry,
                                    const uint16_t* gates, const float* c_t, const float* c_prev,
                                    int R, int H, float drop_p, uint32_t seed, int step,
-                                   uint16_t* dG, int KD, hipStream_t stream) {
+                                   uint16_t* dG, int KD, int S, float* ws, int* tile_cnt,
+                                   hipStream_t stream) {
   using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -278,19 +344,21 @@ static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT
                               hipFuncAttributeMaxDynamicSharedMemorySize, TL::LDS_BYTES);
     attr_set = true;
   }
-  const int n = (H / 64) * ((R + BM - 1) / BM);
+  if (dg_next == nullptr || ws == nullptr || tile_cnt == nullptr) S = 1;  // no K to split
+  const int n = (H / 64) * ((R + BM - 1) / BM) * S;
   hipLaunchKernelGGL(lstm_step_bwd_kernel<BM>, dim3(n), dim3(256), TL::LDS_BYTES, stream,
                      dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
-                     step, dG, KD);
+                     step, dG, KD, S, ws, tile_cnt);
   post_launch("lstm_step_bwd_kernel", stream);
 }
 
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, uint32_t seed,
-                          int step, uint16_t* dG, int KD, hipStream_t stream) {
+                          int step, uint16_t* dG, int KD, hipStream_t stream, int S, float* ws,
+                          int* tile_cnt) {
   launch_lstm_step_bwd_t<64>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                             drop_p, seed, step, dG, KD, stream);
+                             drop_p, seed, step, dG, KD, S, ws, tile_cnt, stream);
 }
 
 static int g_lstm_fwd_variant = 0;
