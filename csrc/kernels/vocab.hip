@@ -605,25 +605,40 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   const int r = blockIdx.x * CMB_ROWS + (threadIdx.x / CMB_LANES);
   const bool valid = r < R;
   if (threadIdx.x == 0) s_nonzero = 0;
-  // The cell epilogue's token-independent operands (pre-activations of the
-  // row, c_{t}) are loaded first, so their latency overlaps the merge below.
-  constexpr int CELL_PF = 16;  // units per lane held in registers (H <= 512)
-  const bool do_cell = cell.pre != nullptr && tok_out != nullptr;
-  const bool pf = do_cell && cell.H <= CMB_LANES * CELL_PF;
-  float4 pf_p[CELL_PF];
-  float pf_c[CELL_PF];
-  if (pf && valid) {
+  // The row's tile partials are loaded unconditionally (clamped index,
+  // neutralised in the merge) so they issue back to back: one memory round
+  // trip instead of one per merge step.  The cell epilogue's operands are
+  // loaded afterwards in one batch (pre-activations, c_t and the token's
+  // table row together): the vector-memory counter retires loads in order,
+  // so prefetching them before the partials made the merge wait for them.
+  constexpr int CMB_MAXP = 4;  // n_vt <= 128: V <= 16384 at 128-wide tiles
+  const bool fastp = n_vt <= CMB_MAXP * CMB_LANES;
+  VocabPartial pp[CMB_MAXP];
+  if (valid && fastp) {
 #pragma unroll
-    for (int k = 0; k < CELL_PF; ++k) {
-      const int u = sub + k * CMB_LANES;
-      if (u < cell.H) {
-        pf_p[k] = *reinterpret_cast<const float4*>(cell.pre + ((int64_t)r * cell.H + u) * 4);
-        pf_c[k] = cell.c_prev[(int64_t)r * cell.H + u];
-      }
-    }
+    for (int k = 0; k < CMB_MAXP; ++k)
+      pp[k] = part[(int64_t)min(sub + k * CMB_LANES, n_vt - 1) * R + r];
+  }
+  const bool do_cell = cell.pre != nullptr && tok_out != nullptr;
+  // the selecting lane's other inputs, requested now (they do not depend on
+  // the merge): ground-truth token, previous step's non-EOS count, row mask
+  int64_t gt_pre = 0;
+  bool dead_pre = false, unf_pre = true;
+  if (valid && sub == 0 && tok_out != nullptr) {
+    gt_pre = gt ? gt[(int64_t)r * gt_stride] : 0;
+    dead_pre = counts != nullptr && count_step > 1 && counts[count_step - 1] == 0;
+    unf_pre = unfinished == nullptr || unfinished[r] != 0;
   }
   RowStat a = {-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff};
-  if (valid) {
+  if (valid && fastp) {
+#pragma unroll
+    for (int k = 0; k < CMB_MAXP; ++k) {
+      if (sub + k * CMB_LANES < n_vt) {
+        const VocabPartial& p = pp[k];
+        merge_stat(a, p.m, p.s, p.zval, p.zlogit, p.zidx, p.m, p.xidx, p.xtgt);
+      }
+    }
+  } else if (valid) {
 #pragma unroll 4
     for (int t = sub; t < n_vt; t += CMB_LANES) {
       const VocabPartial p = part[(int64_t)t * R + r];
@@ -642,7 +657,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     if (lse_out) lse_out[r] = lse;
     if (g_xe) g_xe[(int64_t)r * gxe_stride] = a.xt - lse;
     if (tok_out != nullptr) {
-      const int64_t gt_tok = gt ? gt[(int64_t)r * gt_stride] : 0;
+      const int64_t gt_tok = gt_pre;
       int64_t tok;
       float tl;
       switch (mode) {
@@ -657,16 +672,15 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
         }
         default: tok = gt_tok; tl = a.xt; break;
       }
-      // reference forward(): once every row emitted EOS at one step, decoding stops
-      if (counts != nullptr) {
-        bool dead = false;
-        for (int k = 1; k < count_step; ++k) dead |= (counts[k] == 0);
-        if (dead) tok = 0;
-      }
+      // reference forward(): once every row emitted EOS at one step, decoding
+      // stops.  Sticky on the device: after such a step every token is forced
+      // to 0, so the count of the previous step alone decides (one load, not a
+      // dependent scan over all earlier steps)
+      if (dead_pre) tok = 0;
       // per-row finished mask: reference sample(), or forward() with the
       // --mask_after_eos fix
       if (unfinished != nullptr) {
-        const uint8_t u = unfinished[r] && (tok > 0);
+        const uint8_t u = unf_pre && (tok > 0);
         unfinished[r] = u;
         if (!u) tok = 0;
       }
@@ -680,50 +694,15 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   if (do_cell) {
     // the row's 32 lanes: lane k owns hidden units k, k + 32, ... (coalesced)
     const int tk = __shfl(tok_final, (int)(threadIdx.x & 63) & ~(CMB_LANES - 1), 64);
-    if (valid && pf) {
-      const int H = cell.H;
-      const float* trow = cell.ptab + (int64_t)tk * 4 * H;
-      const float inv_keep = cell.drop_p > 0.f ? 1.f / (1.f - cell.drop_p) : 1.f;
-      float4 x[CELL_PF];
-#pragma unroll
-      for (int k = 0; k < CELL_PF; ++k) {
-        const int u = sub + k * CMB_LANES;
-        if (u < H) x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
-      }
-#pragma unroll
-      for (int k = 0; k < CELL_PF; ++k) {
-        const int u = sub + k * CMB_LANES;
-        if (u < H) {
-          const float4 p = pf_p[k];
-          const float gi = sigmoidf_(p.x + x[k].x), gf = sigmoidf_(p.y + x[k].y);
-          const float gg = tanhf_(p.z + x[k].z), go = sigmoidf_(p.w + x[k].w);
-          const int64_t o = (int64_t)r * H + u;
-          const float c = gf * pf_c[k] + gi * gg;
-          const float hv = go * tanhf_(c);
-          cell.c_out[o] = c;
-          cell.h_out[o] = f2bf(hv);
-          if (cell.hdrop_out) {
-            const bool keep =
-                cell.drop_p <= 0.f || dropout_keep(cell.seed, cell.step, r, u, cell.drop_p);
-            cell.hdrop_out[(int64_t)r * cell.ldh + u] = f2bf(keep ? hv * inv_keep : 0.f);
-          }
-          if (cell.gates_out) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(gi) | ((uint32_t)f2bf(gf) << 16);
-            pk.y = (uint32_t)f2bf(gg) | ((uint32_t)f2bf(go) << 16);
-            *reinterpret_cast<uint2*>(cell.gates_out + (int64_t)r * 4 * H + 4 * u) = pk;
-          }
-        }
-      }
-    } else if (valid) {
+    if (valid) {
       const int H = cell.H;
       const float* prow = cell.pre + (int64_t)r * 4 * H;
       const float* trow = cell.ptab + (int64_t)tk * 4 * H;
       const float inv_keep = cell.drop_p > 0.f ? 1.f / (1.f - cell.drop_p) : 1.f;
-      // batches of CELL_U units: every load of a batch is issued before the
-      // first store (the stores could alias the inputs as far as the
-      // compiler knows, which would serialise each unit's loads)
-      constexpr int CELL_U = 8;
+      // batches of CELL_U units (all of H = 512 in one): every load of a
+      // batch is issued before the first store (the stores could alias the
+      // inputs as far as the compiler knows, which would serialise the loads)
+      constexpr int CELL_U = 16;
       for (int u0 = sub; u0 < H; u0 += CMB_LANES * CELL_U) {
         float4 p[CELL_U], x[CELL_U];
         float cp[CELL_U];
