@@ -41,8 +41,14 @@ def _captions_for(rng, topic_perm, n_words, ncap, mean_len, max_words, zipf_a):
 
 def make_synthetic(kind='msrvtt', num_videos=None, vocab_size=10509, seq_length=30,
                    feat_dims=None, num_chunks=1, n_topics=64, seed=0, mean_len=9.3,
-                   with_consensus=False, split='train', start_video_id=0, consensus_cols=20):
+                   with_consensus=False, split='train', start_video_id=0, consensus_cols=20,
+                   world_seed=None):
+    """``world_seed``: seed of the generative "world" (topic word
+    distributions, topic feature embeddings); splits that share it are
+    different videos of the same world, so a model trained on one
+    generalises to the others.  None: drawn from ``seed`` (one stream)."""
     rng = np.random.RandomState(seed)
+    wrng = rng if world_seed is None else np.random.RandomState(world_seed)
     if kind == 'msrvtt':
         num_videos = num_videos or 6513
         feat_dims = feat_dims or MSRVTT_FEAT_DIMS
@@ -58,7 +64,7 @@ def make_synthetic(kind='msrvtt', num_videos=None, vocab_size=10509, seq_length=
         raise ValueError('vocab_size too small')
     # topic structure: a shared Zipf head + topic-specific tails
     topic_perm = [np.concatenate([np.arange(min(32, n_words)),
-                                  rng.permutation(np.arange(min(32, n_words), n_words))])
+                                  wrng.permutation(np.arange(min(32, n_words), n_words))])
                   for _ in range(n_topics)]
     topics = rng.randint(n_topics, size=num_videos)
     # Every word appears in the vocab: word ids are w0..w{n_words-1}, and the
@@ -75,7 +81,7 @@ def make_synthetic(kind='msrvtt', num_videos=None, vocab_size=10509, seq_length=
     # features: topic embedding + noise (+ per-chunk jitter)
     feats = []
     for d in feat_dims:
-        emb = rng.normal(0, 1, size=(n_topics, d)).astype(np.float32)
+        emb = wrng.normal(0, 1, size=(n_topics, d)).astype(np.float32)
         base = emb[topics] + 0.5 * rng.normal(0, 1, size=(num_videos, d)).astype(np.float32)
         f = np.repeat(base[:, None, :], num_chunks, axis=1)
         if num_chunks > 1:
@@ -103,13 +109,17 @@ def make_splits(kind='msrvtt', vocab_size=10509, seq_length=30, feat_dims=None,
                 num_chunks=1, train_videos=None, eval_videos=None, seed=0,
                 with_consensus=False, seq_per_img=20):
     """(train, val, test) synthetic splits sharing one vocabulary."""
+    # one generative world (topic vocabularies / feature embeddings) for all
+    # three splits, different videos in each
+    world = 10007 + seed
     tr = make_synthetic(kind, train_videos, vocab_size, seq_length, feat_dims, num_chunks,
-                        seed=seed, with_consensus=with_consensus, consensus_cols=seq_per_img)
+                        seed=seed, with_consensus=with_consensus, consensus_cols=seq_per_img,
+                        world_seed=world)
     n_eval = eval_videos or max(8, (train_videos or 600) // 10)
     va = make_synthetic(kind, n_eval, vocab_size, seq_length, feat_dims, num_chunks,
-                        seed=seed + 1, start_video_id=10 ** 6)
+                        seed=seed + 1, start_video_id=10 ** 6, world_seed=world)
     te = make_synthetic(kind, n_eval, vocab_size, seq_length, feat_dims, num_chunks,
-                        seed=seed + 2, start_video_id=2 * 10 ** 6)
+                        seed=seed + 2, start_video_id=2 * 10 ** 6, world_seed=world)
     # train df is the one used for CIDEr-D rewards on every split
     va.df = te.df = tr.df
     return tr, va, te
