@@ -152,7 +152,9 @@ def main():
         'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': round(ms, 3),
         'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': round(caps / baseline, 3) if (baseline and a.mode == 'scst') else None,
-        'dtype': a.precision, 'data': 'synthetic (MSR-VTT-shaped, random-init weights)',
+        # effective compute dtype: the fused engine is bf16, the PyTorch path fp32
+        'dtype': 'bf16' if engine is not None else 'fp32',
+        'data': 'synthetic (MSR-VTT-shaped, random-init weights)',
         'config': {'model': 'CaptionModel concat LSTM-512 (resnet+c3d+mfcc+category, '
                             'V=%d, L=30)' % a.vocab,
                    'global_batch': a.batch_size * S * ctx.world_size,

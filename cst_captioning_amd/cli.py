@@ -61,6 +61,11 @@ def build_model(opt, device, impl=None):
     engine = None
     if impl == 'auto':
         impl = 'hip' if device.type == 'cuda' else 'torch'
+    if impl == 'hip' and getattr(opt, 'precision', 'bf16') == 'fp32':
+        # the fused engine computes with bf16 MFMA operands; fp32 means the
+        # plain PyTorch path
+        logger.warning('--precision fp32: using the PyTorch decoder path (the HIP engine is bf16)')
+        return model, None
     if impl == 'hip':
         from .models.decoder_engine import DecoderEngine, engine_supports
         if not engine_supports(opt):

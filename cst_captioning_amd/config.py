@@ -98,7 +98,8 @@ def build_parser():
     add('--impl', type=str, default='auto', choices=['auto', 'hip', 'torch'],
         help='decoder implementation: fused HIP engine, or plain PyTorch ops')
     add('--precision', type=str, default='bf16', choices=['bf16', 'fp32'],
-        help='compute precision of the decoder GEMMs (master weights stay fp32)')
+        help='decoder compute precision: bf16 = fused HIP engine (bf16 MFMA operands, fp32 '
+             'accumulation / master weights); fp32 = PyTorch path in fp32')
     add('--reward_device', type=str, default='gpu', choices=['gpu', 'cpu'],
         help='CIDEr-D reward: on-GPU HIP kernel, or the CPU scorer (reference semantics)')
     add('--mask_after_eos', type=int, default=0,
