@@ -46,7 +46,10 @@ def parse():
     p.add_argument('--impl', default='hip', choices=['hip', 'torch'])
     p.add_argument('--reward', default='gpu', choices=['gpu', 'cpu'])
     p.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
-    p.add_argument('--mode', default='scst', choices=['scst', 'cst', 'xe'])
+    p.add_argument('--mode', default='scst', choices=['scst', 'cst', 'xe', 'beam'],
+                   help='beam: evaluation decode throughput (beam search, --beam_size) '
+                        'instead of a training step')
+    p.add_argument('--beam_size', type=int, default=5)
     p.add_argument('--dedupe_greedy', type=int, default=1)
     p.add_argument('--batch_size', type=int, default=64)
     p.add_argument('--videos', type=int, default=6513)
@@ -103,6 +106,11 @@ def main():
 
     def step():
         data = loader.get_batch()
+        if a.mode == 'beam':  # BASELINE config 5: beam-5 evaluation decode
+            model.eval()
+            with torch.no_grad():
+                seq, _ = model.sample(data['feats'], {'beam_size': a.beam_size})
+            return {'loss': seq.float().mean()}
         return trainer.train_step(data, 0)
 
     sync = torch.cuda.synchronize if dev.type == 'cuda' else (lambda: None)
@@ -141,14 +149,23 @@ def main():
     loss = float(out['loss'])
     ms = dt / a.steps * 1e3
     caps = a.batch_size * S * ctx.world_size * a.steps / dt
+    vids = a.batch_size * ctx.world_size * a.steps / dt
     baseline = None
     if os.path.exists(BASELINE_FILE):
         with open(BASELINE_FILE) as f:
             baseline = json.load(f).get('value')
+    if a.mode == 'beam':
+        metric, value, unit = 'beam-%d evaluation decode videos/sec (whole job)' % a.beam_size, \
+            vids, 'videos/s'
+    elif a.mode == 'scst':
+        metric, value, unit = ('SCST training captions/sec (whole node), MSR-VTT LSTM-attn at '
+                               '1/2/4/8 MI355X', caps, 'captions/s')
+    else:
+        metric, value, unit = '%s training captions/sec (whole job)' % a.mode.upper(), caps, \
+            'captions/s'
     rec = {
-        'metric': 'SCST training captions/sec (whole node), MSR-VTT LSTM-attn at 1/2/4/8 MI355X'
-        if a.mode == 'scst' else '%s training captions/sec (whole job)' % a.mode.upper(),
-        'value': round(caps, 2), 'unit': 'captions/s', 'n_gpus': ctx.world_size,
+        'metric': metric,
+        'value': round(value, 2), 'unit': unit, 'n_gpus': ctx.world_size,
         'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': round(ms, 3),
         'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': round(caps / baseline, 3) if (baseline and a.mode == 'scst') else None,
@@ -157,7 +174,7 @@ def main():
         'data': 'synthetic (MSR-VTT-shaped, random-init weights)',
         'config': {'model': 'CaptionModel concat LSTM-512 (resnet+c3d+mfcc+category, '
                             'V=%d, L=30)' % a.vocab,
-                   'global_batch': a.batch_size * S * ctx.world_size,
+                   'global_batch': a.batch_size * (1 if a.mode == 'beam' else S) * ctx.world_size,
                    'videos_per_gpu': a.batch_size, 'seq_per_img': S, 'seq_len': 30,
                    'parallelism': 'dp%d' % ctx.world_size, 'impl': a.impl,
                    'reward': a.reward, 'mode': a.mode, 'params': n_params,
