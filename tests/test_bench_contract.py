@@ -1,0 +1,48 @@
+"""bench.py output contract (the driver runs it under torch.distributed.run
+with N ranks): ONE JSON line from rank 0 with the whole-job value, n_gpus,
+steps / warmup, the config and the timing fields.  Exercised on the CPU with
+the gloo backend and the PyTorch decoder path at tiny sizes."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize('world', [1, 2])
+def test_bench_json_line(world):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES='', OMP_NUM_THREADS='1')
+    args = ['bench.py', '--gpus', str(world), '--impl', 'torch', '--steps', '2', '--warmup', '1',
+            '--videos', '48', '--vocab', '300', '--batch_size', '4']
+    if world > 1:
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node',
+               str(world), '--master-addr', '127.0.0.1', '--master-port', str(_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    rec = json.loads(lines[0])
+    for k in ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+              'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data', 'config'):
+        assert k in rec, k
+    assert rec['n_gpus'] == world and rec['steps'] == 2 and rec['warmup'] == 1
+    assert rec['scaling'] == 'weak' and rec['higher_is_better'] is True
+    assert rec['dtype'] == 'fp32'  # the PyTorch path computes in fp32
+    assert rec['config']['global_batch'] == 4 * 20 * world
+    assert rec['config']['parallelism'] == 'dp%d' % world
+    # whole-job value = global captions / step time
+    assert abs(rec['value'] - 4 * 20 * world / (rec['ms_per_step'] / 1e3)) < 0.02 * rec['value']

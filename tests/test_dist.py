@@ -1,5 +1,5 @@
 """Data parallelism without a cluster (SURVEY.md §4.2 "Distributed"):
-torchrun with the gloo backend, world sizes 1 and 2 on the CPU.
+torchrun with the gloo backend, world sizes 1, 2 and 4 on the CPU.
 
   * C1: rank 0's parameters are broadcast (ranks start from different seeds);
   * C2: the all-reduced gradient equals the gradient of the mean of the
@@ -43,7 +43,7 @@ def _run(world, out):
 @pytest.fixture(scope='module')
 def runs(tmp_path_factory):
     d = tmp_path_factory.mktemp('dist')
-    return {w: _run(w, str(d / ('w%d.pt' % w))) for w in (1, 2)}
+    return {w: _run(w, str(d / ('w%d.pt' % w))) for w in (1, 2, 4)}
 
 
 def _reference_grad(world):
@@ -77,10 +77,17 @@ def test_broadcast_and_allreduce(runs):
     assert r2['same_after_steps']
 
 
+def test_allreduce_world4(runs):
+    r4 = runs[4]
+    _, ref = _reference_grad(4)
+    torch.testing.assert_close(r4['grad'], ref, rtol=1e-5, atol=1e-7)
+    assert r4['same_after_steps']
+
+
 def test_sharded_validation_matches_single_rank(runs):
     p1, p2 = runs[1]['predictions'], runs[2]['predictions']
     assert len(p1) == 8  # synthetic val split: max(8, 24 // 10) videos
-    assert p1 == p2  # same ids, same order, same captions
+    assert p1 == p2 == runs[4]['predictions']  # same ids, same order, same captions
     # (the XE 'Loss' depends on which seq_per_img captions each rank draws, as in
     # the reference's random caption selection, so only the beam outputs are compared)
     assert runs[1]['world'] == 1 and runs[2]['world'] == 2
