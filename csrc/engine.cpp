@@ -126,7 +126,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   }();
   const int n_vt = vocab_num_tiles((int)V);
   at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4}, f32);
-  at::Tensor counts = at::zeros({T + 1}, at::TensorOptions().dtype(at::kInt).device(dev));
+  at::Tensor counts = at::zeros({(T + 1) * combine_count_ints_per_step()},
+                                at::TensorOptions().dtype(at::kInt).device(dev));
   at::Tensor unfinished =
       use_unfinished ? at::ones({R}, at::TensorOptions().dtype(at::kByte).device(dev))
                      : at::Tensor();

@@ -551,6 +551,10 @@ enum SelMode : int { SEL_GT = 0, SEL_SAMPLE = 1, SEL_GREEDY = 2, SEL_SS = 3 };
 // 64-thread blocks (2 rows): 640 blocks at R = 1280 spread the combine and
 // the cell epilogue's 33 MB of traffic over every CU.
 constexpr int CMB_LANES = 32, CMB_THREADS = 64, CMB_ROWS = CMB_THREADS / CMB_LANES;
+// end-of-sequence flags: per decode step CMB_CNT_SLOTS slots, one 128-byte
+// line apart (see vocab_combine_kernel)
+constexpr int CMB_CNT_SLOTS = CMB_LANES, CMB_CNT_STRIDE = 32;
+int combine_count_ints_per_step() { return CMB_CNT_SLOTS * CMB_CNT_STRIDE; }
 
 // Cell epilogue of the NEXT decode step, applied as soon as its input token
 // is chosen (see lstm_gemm.h): gates = pre + P[tok] -> i, f, g, o -> c, h.
@@ -623,12 +627,21 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   // the selecting lane's other inputs, requested now (they do not depend on
   // the merge): ground-truth token, previous step's non-EOS count, row mask
   int64_t gt_pre = 0;
-  bool dead_pre = false, unf_pre = true;
+  bool unf_pre = true;
   if (valid && sub == 0 && tok_out != nullptr) {
     gt_pre = gt ? gt[(int64_t)r * gt_stride] : 0;
-    dead_pre = counts != nullptr && count_step > 1 && counts[count_step - 1] == 0;
     unf_pre = unfinished == nullptr || unfinished[r] != 0;
   }
+  // "some row emitted a non-EOS token at the previous step": one flag slot
+  // per lane of the half-wave (CMB_CNT_SLOTS cache-line-strided slots, written
+  // by the blocks of that step), OR-reduced across the 32 lanes
+  int nz_prev = 1;
+  if (counts != nullptr && count_step > 1 && tok_out != nullptr) {
+    nz_prev = counts[((count_step - 1) * CMB_CNT_SLOTS + sub) * CMB_CNT_STRIDE];
+#pragma unroll
+    for (int o = 1; o < CMB_LANES; o <<= 1) nz_prev |= __shfl_xor(nz_prev, o, 64);
+  }
+  const bool dead_pre = nz_prev == 0;
   RowStat a = {-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff};
   if (valid && fastp) {
 #pragma unroll
@@ -744,7 +757,10 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   }
   if (counts != nullptr && tok_out != nullptr) {
     __syncthreads();
-    if (threadIdx.x == 0 && s_nonzero > 0) atomicAdd(&counts[count_step], s_nonzero);
+    // idempotent flag store into this block's slot: no same-address atomics
+    // from all 640 blocks (those cost ~5 us per decode step)
+    if (threadIdx.x == 0 && s_nonzero > 0)
+      counts[(count_step * CMB_CNT_SLOTS + blockIdx.x % CMB_CNT_SLOTS) * CMB_CNT_STRIDE] = 1;
   }
 }
 

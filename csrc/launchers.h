@@ -44,6 +44,8 @@ struct CellLaunch {
   uint32_t seed;
   int step;
 };
+// size of the end-of-sequence flag area per decode step (ints) of `counts`
+int combine_count_ints_per_step();
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
