@@ -25,6 +25,10 @@
 //     at once; the video's Gv[b] rows (L2-resident, shared by its row groups)
 //     are prefetched into registers at kernel start, so their latency hides
 //     under the scores;
+//   * in the rollout the query q_{t+1} = W_q h_t comes from extra W_q tiles of
+//     the merged decode launch's recurrent GEMM (lstm_gemm.h), and the kernel
+//     adds each row's vgate straight into that GEMM's pre-activations
+//     (accumulate = 1), which the combine kernel's cell epilogue consumes;
 //   * backward (per reverse step, after the fused LSTM step backward has
 //     produced dG_t): dalpha = dG_t . Gv[b]^T, softmax backward, and the
 //     tanh-scorer backward.  dq_t is written as bf16 into the tail columns
