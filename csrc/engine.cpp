@@ -371,14 +371,52 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   hipEvent_t ev_ready = ev[n_chunks], ev_done = ev[n_chunks + 1];
   (void)hipEventRecord(ev_ready, st);
-  {
-    // one persistent side stream per device: pool streams rotate, and every
-    // new stream pays hipBLASLt handle/workspace setup on first use
-    static std::map<int, c10::hip::HIPStream> side_streams;
-    auto it = side_streams.find(dev.index());
+  // persistent side streams per device (slot 0: vocab head, slot 1: token
+  // sort / embedding gradient): pool streams rotate, and every new stream
+  // pays hipBLASLt handle/workspace setup on first use
+  static std::map<std::pair<int, int>, c10::hip::HIPStream> side_streams;
+  auto side_stream = [&](int slot) {
+    auto key = std::make_pair((int)dev.index(), slot);
+    auto it = side_streams.find(key);
     if (it == side_streams.end())
-      it = side_streams.emplace(dev.index(), c10::hip::getStreamFromPool(false, dev.index())).first;
-    auto side = it->second;
+      it = side_streams.emplace(key, c10::hip::getStreamFromPool(false, dev.index())).first;
+    return it->second;
+  };
+  // Where to build the operands that depend only on the tokens (sorted token
+  // order for the embedding gradient, gathered input embeddings for dW_ie)
+  // off the critical path?  CSTCAP_BWD_AUX (A/B knob): 0 (default) = on the
+  // main stream after the loop; 1 = on the vocab-head side stream after dHd,
+  // i.e. under the reverse loop (within noise of 0); 2 = on a third stream that also takes the
+  // embedding-gradient GEMM concurrently with the weight GEMMs (measured
+  // 5.21 vs 4.87 ms per step: more streams than hardware queues).  The
+  // outputs are allocated here on the main stream so their memory is ordered
+  // by it.
+  TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
+  at::Tensor stok = at::empty_like(toks), srow = at::empty_like(toks);
+  at::Tensor x_in = at::empty({n_steps * R, E}, emb.options());     // (n*R, E) bf16
+  at::Tensor d_emb = at::empty({V, E}, f32);
+  static const int aux_mode = [] {
+    const char* e = std::getenv("CSTCAP_BWD_AUX");
+    return e ? std::atoi(e) : 0;
+  }();
+  auto main_stream = at::hip::getCurrentHIPStream();
+  auto aux = aux_mode == 2 ? side_stream(1) : main_stream;  // embedding-gradient tail
+  hipEvent_t ev_aux, ev_tail;
+  (void)hipEventCreateWithFlags(&ev_aux, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming);
+  auto token_prep = [&](c10::hip::HIPStream s) {
+    c10::hip::HIPStreamGuard guard(s);
+    at::sort_out(stok, srow, toks);
+    at::index_select_out(x_in, emb, 0, toks);
+    d_emb.zero_();
+    (void)hipEventRecord(ev_aux, s.stream());
+  };
+  if (aux_mode == 2) {
+    (void)hipStreamWaitEvent(aux.stream(), ev_ready, 0);
+    token_prep(aux);
+  }
+  {
+    auto side = side_stream(0);
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
     for (int c = n_chunks - 1; c >= 0; --c) {
@@ -395,6 +433,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       at::mm_out(out, dS.narrow(0, cb[c], cb[c + 1] - cb[c]), wlog, at::kFloat);
       (void)hipEventRecord(ev[c], side.stream());
     }
+    if (aux_mode == 1) token_prep(side);
     at::mm_out(dWlog, dS.t(), hd2, at::kFloat);
     if (early) {
       dblog = out_blog.view({V});
@@ -470,7 +509,21 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     at::Tensor b = b_rows.reshape({nc, G * R, b_rows.size(1)});
     return at::bmm(a, b, at::kFloat).sum(0);
   };
-  at::Tensor x_in = emb.index_select(0, toks);                            // (n*R, E) bf16
+  if (aux_mode == 0) token_prep(main_stream);
+  (void)hipStreamWaitEvent(st, ev_aux, 0);
+  // embedding gradient: dX = dG W_ie, then a sorted segmented sum into d_emb
+  // (mode 2: on the third stream, concurrently with the weight GEMMs below;
+  // dX is allocated and consumed on that stream)
+  (void)hipEventRecord(ev_tail, st);
+  (void)hipStreamWaitEvent(aux.stream(), ev_tail, 0);
+  {
+    c10::hip::HIPStreamGuard guard(aux);
+    at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);      // (n*R, E)
+    launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int64_t>(),
+                          srow.data_ptr<int64_t>(), (int)(n_steps * R), d_emb.data_ptr<float>(),
+                          aux.stream());
+    (void)hipEventRecord(ev_aux, aux.stream());
+  }
   dWx.narrow(1, 0, E).copy_(grouped_wgrad(dG2, x_in, n_steps));
   if (n_steps > 1) {
     // with attention the extra rows of [dG | dq]^T h_prev are dW_q
@@ -483,14 +536,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dWx.narrow(1, E, H).zero_();
     if (has_att) dWq = at::zeros({A, H}, f32);
   }
-  //    embedding: dX = dG W_ie, then a sorted segmented sum into d_emb
-  TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
-  at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);        // (n*R, E)
-  auto sorted = at::sort(toks);
-  at::Tensor stok = std::get<0>(sorted), srow = std::get<1>(sorted);
-  at::Tensor d_emb = at::zeros({V, E}, f32);
-  launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int64_t>(),
-                        srow.data_ptr<int64_t>(), (int)(n_steps * R), d_emb.data_ptr<float>(), st);
   at::Tensor dvg;
   std::vector<at::Tensor> res;
   if (!has_att) {
@@ -506,7 +551,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
            dba_part.sum(0).view({1}), dWq};
   }
   (void)hipStreamWaitEvent(st, ev_done, 0);  // join the side stream (dWlog)
+  (void)hipStreamWaitEvent(st, ev_aux, 0);   // join the embedding-gradient stream
   for (auto& e : ev) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(ev_aux);
+  (void)hipEventDestroy(ev_tail);
   std::vector<at::Tensor> out = {dWx, dWlog, dblog, d_emb, dvg};
   out.insert(out.end(), res.begin(), res.end());
   return out;
