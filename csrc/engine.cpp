@@ -388,7 +388,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // main stream after the loop; 1 = on the vocab-head side stream after dHd,
   // i.e. under the reverse loop (within noise of 0); 2 = on a third stream that also takes the
   // embedding-gradient GEMM concurrently with the weight GEMMs (measured
-  // 5.21 vs 4.87 ms per step: more streams than hardware queues).  The
+  // 5.21 vs 4.87 ms per step, also with GPU_MAX_HW_QUEUES=8: the two GEMMs
+  // slow each other down more than the overlap saves).  The
   // outputs are allocated here on the main stream so their memory is ordered
   // by it.
   TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
