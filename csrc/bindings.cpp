@@ -27,6 +27,9 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     std::vector<at::Tensor> att);
 double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
                           int64_t iters);
+double vocab_bwd_dhd_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
+                           at::Tensor wT, int64_t V, int64_t splits, int64_t dbg, int64_t iters);
+void set_bwd_fused(int64_t on);
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
                        int64_t flags, bool save, int64_t iters);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
@@ -96,6 +99,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_vocab_variant", &cst::set_vocab_variant);
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
   m.def("vocab_bwd_ds_bench", &cst::vocab_bwd_ds_bench);
+  m.def("vocab_bwd_dhd_bench", &cst::vocab_bwd_dhd_bench);
+  m.def("set_bwd_fused", &cst::set_bwd_fused);
   m.def("beam_search", &cst::beam_search);
   m.def("set_lstm_fwd_variant", &cst::set_lstm_fwd_variant);
 }

@@ -45,6 +45,12 @@ static void check_cuda(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+static int g_bwd_fused = [] {
+  const char* e = std::getenv("CSTCAP_BWD_FUSED");
+  return e ? std::atoi(e) : 0;
+}();
+void set_bwd_fused(int64_t on) { g_bwd_fused = (int)on; }
+
 // modes[t] = token-selection mode for token t+1 (see SelModeHost)
 std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor ptab,
                                         at::Tensor whh, at::Tensor wlog,
@@ -131,7 +137,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor unfinished =
       use_unfinished ? at::ones({R}, at::TensorOptions().dtype(at::kByte).device(dev))
                      : at::Tensor();
-  const int64_t ldl = (V + 7) / 8 * 8;
+  // saved-logit rows padded to 128 bytes: the fused backward writes dS back
+  // in whole cache lines
+  const int64_t ldl = (V + 63) / 64 * 64;
   at::Tensor logits16, hdrop_all, gates_all, c_all, h_all;
   if (save) {
     logits16 = at::empty({n_steps, R, ldl}, at::TensorOptions().dtype(at::kHalf).device(dev));
@@ -342,10 +350,28 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   //    it starts as soon as the last chunk is ready and overlaps the rest.
   TORCH_CHECK(V <= 8 * 2048, "vocab larger than the dS kernel's register tiling");
   const int64_t NR = n_steps * R;
-  at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n_steps, (int)R), V}, f32);
+  // Fused route (vocab_bwd.hip; CSTCAP_BWD_FUSED=1 or set_bwd_fused(1)): one
+  // kernel forms dS from the fp16 logits and multiplies it into dHd (split-K
+  // over the vocabulary into CSTCAP_BWD_DHD_SPLIT partials, 1 or 2), writing
+  // dS in place and the bias-gradient column sums.  Measured slower on
+  // MI355X (1.0 ms vs 0.43 + 0.45 ms for the dS pass + BLAS GEMM, see
+  // profiles/README.md), so the two-pass route is the default.
+  const int fused_env = g_bwd_fused;
+  static const int dhd_split = [] {
+    const char* e = std::getenv("CSTCAP_BWD_DHD_SPLIT");
+    return e ? std::max(1, std::min(2, std::atoi(e))) : 2;
+  }();
+  const bool fused = fused_env != 0 && H == 512 && ldl % 8 == 0;
+  const int n_part = fused ? dhd_split : 1;
+  at::Tensor colsum =
+      at::empty({fused ? vocab_bwd_dhd_colsum_rows(NR) : vocab_bwd_ds_blocks((int)n_steps, (int)R), V},
+                f32);
   at::Tensor dS = logits16.view(at::kBFloat16).view({NR, ldl}).narrow(1, 0, V);
   at::Tensor hd2 = hdrop_all.view({NR, H + HAUG}).narrow(1, 0, H);
-  at::Tensor dHd = at::empty({NR, H}, f32);
+  at::Tensor dHd_all = at::empty({n_part, NR, H}, f32);
+  at::Tensor dHd = dHd_all[0];
+  const int64_t ldw = fused ? (V + vocab_bwd_dhd_kpad() - 1) / vocab_bwd_dhd_kpad() * vocab_bwd_dhd_kpad() : 0;
+  at::Tensor wT = fused ? at::zeros({H, ldw}, wlog.options()) : at::Tensor();  // W_logit^T, padded
   // early gradients (DP overlap): dWlog / dblog written straight into the
   // caller's gradient buffers on the side stream, and the caller's
   // communication stream made to wait for them, so their all-reduce runs
@@ -364,7 +390,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     const char* e = std::getenv("CSTCAP_BWD_CHUNKS");  // A/B knob for the pipeline depth
     return e ? std::max(1, std::atoi(e)) : 1;
   }();
-  const int n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(max_chunks, NR / (8 * DR)));
+  const int n_chunks =
+      fused ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(max_chunks, NR / (8 * DR)));
   std::vector<int64_t> cb(n_chunks + 1);
   for (int c = 0; c <= n_chunks; ++c) cb[c] = c == n_chunks ? NR : (NR * c / n_chunks) / DR * DR;
   std::vector<hipEvent_t> ev(n_chunks + 2);
@@ -420,7 +447,21 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     auto side = side_stream(0);
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
-    for (int c = n_chunks - 1; c >= 0; --c) {
+    if (fused) {
+      wT.narrow(1, 0, V).copy_(wlog.t());
+      launch_vocab_bwd_dhd(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
+                           (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
+                           has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
+                           has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
+                           has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
+                           has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
+                           has_xe ? dg_xe.size(1) : 0,
+                           reinterpret_cast<const uint16_t*>(wT.data_ptr()), (int)ldw, (int)H,
+                           n_part, dHd_all.data_ptr<float>(), colsum.data_ptr<float>(),
+                           side.stream());
+      (void)hipEventRecord(ev[0], side.stream());
+    }
+    for (int c = fused ? -1 : n_chunks - 1; c >= 0; --c) {
       launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
                           (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
                           has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
@@ -483,7 +524,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         (int)H, (float)drop_p, seed_drop, (int)t,
         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, splitk,
         splitk > 1 ? bwd_ws.data_ptr<float>() : nullptr,
-        splitk > 1 ? bwd_cnt.data_ptr<int>() : nullptr);
+        splitk > 1 ? bwd_cnt.data_ptr<int>() : nullptr,
+        n_part > 1 ? dHd_all[1].data_ptr<float>() + t * R * H : nullptr);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
@@ -737,6 +779,38 @@ double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, a
                         (int)n, (int)T_sel, lse.data_ptr<float>(), seq.data_ptr<int64_t>(), T_sel,
                         dg_sel.data_ptr<float>(), T_sel, nullptr, 0, nullptr, 0,
                         colsum.data_ptr<float>(), 0, n * R, st);
+  };
+  launch();
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < iters; ++i) launch();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 1000.0 * ms / (double)iters;
+}
+
+// fused dS + dHd kernel alone (synthetic RL-shaped inputs), us per launch;
+// dbg = ablation bits of vocab_bwd_dhd_kernel
+double vocab_bwd_dhd_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
+                           at::Tensor wT, int64_t V, int64_t splits, int64_t dbg, int64_t iters) {
+  const int64_t n = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
+  const int64_t T_sel = seq.size(1), H = wT.size(0), NR = n * R;
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(logits16.device());
+  at::Tensor dhd = at::empty({splits, NR, H}, f32);
+  at::Tensor colsum = at::empty({vocab_bwd_dhd_colsum_rows(NR), V}, f32);
+  hipStream_t st = cur_stream();
+  auto launch = [&]() {
+    launch_vocab_bwd_dhd(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
+                         (int)n, (int)T_sel, lse.data_ptr<float>(), seq.data_ptr<int64_t>(), T_sel,
+                         dg_sel.data_ptr<float>(), T_sel, nullptr, 0, nullptr, 0,
+                         reinterpret_cast<const uint16_t*>(wT.data_ptr()), (int)wT.size(1), (int)H,
+                         (int)splits, dhd.data_ptr<float>(), colsum.data_ptr<float>(), st, (int)dbg);
   };
   launch();
   hipEvent_t e0, e1;

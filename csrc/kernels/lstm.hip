@@ -191,6 +191,7 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
                                                   const float* __restrict__ c_prev,
                                                   const float* __restrict__ dc_carry,
                                                   const float* __restrict__ dh_logit,
+                                                  const float* __restrict__ dh_logit2,
                                                   uint2* pg, float* pc, float* pcp, float* pdc,
                                                   float* pdl) {
   constexpr int RPT = BM / 4;
@@ -202,17 +203,18 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
     pc[i] = c_t[o];
     pcp[i] = c_prev ? c_prev[o] : 0.f;
     pdc[i] = dc_carry[o];
-    pdl[i] = dh_logit[o];
+    pdl[i] = dh_logit[o] + (dh_logit2 ? dh_logit2[o] : 0.f);  // split-K partials of dHd
   }
 }
 
 template <int BM>
 __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
-    const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
-    const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
-    const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
-    uint16_t* __restrict__ dG, int KD, int S, float* __restrict__ ws, int* __restrict__ tile_cnt) {
+    const float* __restrict__ dh_logit, const float* __restrict__ dh_logit2,
+    float* __restrict__ dc_carry, const uint16_t* __restrict__ gates,
+    const float* __restrict__ c_t, const float* __restrict__ c_prev, int R, int H, float drop_p,
+    uint32_t seed, int step, uint16_t* __restrict__ dG, int KD, int S, float* __restrict__ ws,
+    int* __restrict__ tile_cnt) {
   using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ int s_last;
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
   uint2 pg[RPT];
   float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
   if (S == 1)  // single pass: the epilogue operands' latency hides under the GEMM
-    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, pg, pc, pcp,
+    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, dh_logit2, pg, pc, pcp,
                           pdc, pdl);
 
   f32x16 acc[TL::TM][TL::TN];
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     // acquire: the device-scope fence also invalidates this CU's L1, so the
     // plain (batched, non-serialised) loads below see the other blocks' partials
     __threadfence();
-    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, pg, pc, pcp,
+    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, dh_logit2, pg, pc, pcp,
                           pdc, pdl);
     const float4* wsv = reinterpret_cast<const float4*>(ws + (int64_t)tile * S * TE);
     constexpr int PER = TE / 4 / 256;  // float4 per thread per partial
@@ -332,7 +334,7 @@ int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
 template <int BM>
 static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT,
-                                   const float* dh_logit, float* dc_carry,
+                                   const float* dh_logit, const float* dh_logit2, float* dc_carry,
                                    const uint16_t* gates, const float* c_t, const float* c_prev,
                                    int R, int H, float drop_p, uint32_t seed, int step,
                                    uint16_t* dG, int KD, int S, float* ws, int* tile_cnt,
@@ -347,7 +349,8 @@ static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT
   if (dg_next == nullptr || ws == nullptr || tile_cnt == nullptr) S = 1;  // no K to split
   const int n = (H / 64) * ((R + BM - 1) / BM) * S;
   hipLaunchKernelGGL(lstm_step_bwd_kernel<BM>, dim3(n), dim3(256), TL::LDS_BYTES, stream,
-                     dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
+                     dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
+                     drop_p, seed,
                      step, dG, KD, S, ws, tile_cnt);
   post_launch("lstm_step_bwd_kernel", stream);
 }
@@ -356,8 +359,8 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, uint32_t seed,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int S, float* ws,
-                          int* tile_cnt) {
-  launch_lstm_step_bwd_t<64>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
+                          int* tile_cnt, const float* dh_logit2) {
+  launch_lstm_step_bwd_t<64>(dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
                              drop_p, seed, step, dG, KD, S, ws, tile_cnt, stream);
 }
 

@@ -69,6 +69,18 @@ void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_
                          int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
                          int64_t row_begin, int64_t row_end, hipStream_t stream);
 int vocab_bwd_ds_rows();
+// fused dS + dHd (vocab_bwd.hip): H == 512; wT = W_logit^T (H x ldw bf16,
+// zero-padded, ldw % vocab_bwd_dhd_kpad() == 0); dhd = splits partials of
+// (T*R, H) fp32; colsum = (vocab_bwd_dhd_colsum_rows(T*R), V) bias-gradient partials
+int vocab_bwd_dhd_mblocks(int64_t NR);
+int vocab_bwd_dhd_colsum_rows(int64_t NR);  // rows of the colsum partial buffer
+int vocab_bwd_dhd_kpad();
+void launch_vocab_bwd_dhd(uint16_t* logits, int64_t ldl, int V, int R, int T, int T_sel,
+                          const float* lse, const int64_t* y_sel, int64_t ysel_rs,
+                          const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
+                          int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, const uint16_t* wT,
+                          int ldw, int H, int splits, float* dhd, float* colsum,
+                          hipStream_t stream, int dbg = 0);
 
 // lstm.hip
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
@@ -92,7 +104,8 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, uint32_t seed,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int S = 1,
-                          float* ws = nullptr, int* tile_cnt = nullptr);
+                          float* ws = nullptr, int* tile_cnt = nullptr,
+                          const float* dh_logit2 = nullptr);  // second dHd partial (or null)
 
 // attention.hip (temporal attention over num_chunks frames)
 int att_groups(int vdiv);

@@ -111,8 +111,29 @@ def test_flat_adam_skip_flag():
     torch.testing.assert_close(p.detach(), before)
 
 
-def test_teacher_forced_logprobs_and_grads_match_torch():
-    ds, opt, model, loader = _tiny()
+# fused=True: the fused dS + dHd backward kernel (vocab_bwd.hip, H = 512
+# only); V = 1299 is not a multiple of its 32-wide K tile and 330 rows not of
+# its 128-row tile
+_SHAPES = [dict(), dict(V=1299, H=512), dict(V=1299, H=512, fused=True)]
+_SHAPE_IDS = ['h64', 'h512', 'h512_fused']
+
+
+def _tiny_shape(seed=0, fused=False, **shape):
+    _ext().set_bwd_fused(1 if fused else 0)
+    return _tiny(seed=seed, **shape)
+
+
+@pytest.fixture(autouse=True)
+def _fused_off():
+    yield
+    from cst_captioning_amd import _ext as ext
+    if ext.available():
+        ext.ops().set_bwd_fused(0)
+
+
+@pytest.mark.parametrize('shape', _SHAPES, ids=_SHAPE_IDS)
+def test_teacher_forced_logprobs_and_grads_match_torch(shape):
+    ds, opt, model, loader = _tiny_shape(**shape)
     eng = _engine(model, opt)
     model.train()  # dropout is 0 in this config; MIOpen RNN backward needs train mode
     data = loader.get_batch()
@@ -185,9 +206,10 @@ def test_beam_search_kernel_matches_torch(K):
     assert ((lp - lp_ref).abs()[same] < 0.05).all()
 
 
-def test_rl_rollout_gradient_matches_torch():
+@pytest.mark.parametrize('shape', _SHAPES, ids=_SHAPE_IDS)
+def test_rl_rollout_gradient_matches_torch(shape):
     """REINFORCE gradient through the sampled-token path (y_sel)."""
-    ds, opt, model, loader = _tiny(seed=2)
+    ds, opt, model, loader = _tiny_shape(seed=2, **shape)
     eng = _engine(model, opt)
     model.train()  # dropout is 0 in this config
     model.set_mixer_from(1)
