@@ -207,7 +207,7 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
   }
 }
 
-template <int BM>
+template <int BM, int STAGES = LSTM_BWD_STAGES>
 __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
     const float* __restrict__ dh_logit, const float* __restrict__ dh_logit2,
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     const float* __restrict__ c_t, const float* __restrict__ c_prev, int R, int H, float drop_p,
     uint32_t seed, int step, uint16_t* __restrict__ dG, int KD, int S, float* __restrict__ ws,
     int* __restrict__ tile_cnt) {
-  using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
+  using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ int s_last;
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
@@ -332,23 +332,23 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
 
 int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
-template <int BM>
+template <int BM, int STAGES>
 static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT,
                                    const float* dh_logit, const float* dh_logit2, float* dc_carry,
                                    const uint16_t* gates, const float* c_t, const float* c_prev,
                                    int R, int H, float drop_p, uint32_t seed, int step,
                                    uint16_t* dG, int KD, int S, float* ws, int* tile_cnt,
                                    hipStream_t stream) {
-  using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
+  using TL = Tile<BM, 64, STAGES>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM>,
+    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, STAGES>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, TL::LDS_BYTES);
     attr_set = true;
   }
   if (dg_next == nullptr || ws == nullptr || tile_cnt == nullptr) S = 1;  // no K to split
   const int n = (H / 64) * ((R + BM - 1) / BM) * S;
-  hipLaunchKernelGGL(lstm_step_bwd_kernel<BM>, dim3(n), dim3(256), TL::LDS_BYTES, stream,
+  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES>), dim3(n), dim3(256), TL::LDS_BYTES, stream,
                      dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
                      drop_p, seed,
                      step, dG, KD, S, ws, tile_cnt);
@@ -360,7 +360,16 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           const float* c_prev, int R, int H, float drop_p, uint32_t seed,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int S, float* ws,
                           int* tile_cnt, const float* dh_logit2) {
-  launch_lstm_step_bwd_t<64>(dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
+  // pipeline depth (A/B knob CSTCAP_BWD_STAGES: 3 or 6 LDS stages)
+  static const int stages = [] {
+    const char* e = std::getenv("CSTCAP_BWD_STAGES");
+    return e && std::atoi(e) >= 6 ? 6 : 3;
+  }();
+  if (stages == 6)
+  launch_lstm_step_bwd_t<64, 6>(dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
+                             drop_p, seed, step, dG, KD, S, ws, tile_cnt, stream);
+  else
+  launch_lstm_step_bwd_t<64, 3>(dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
                              drop_p, seed, step, dG, KD, S, ws, tile_cnt, stream);
 }
 
