@@ -416,7 +416,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // i.e. under the reverse loop (within noise of 0); 2 = on a third stream that also takes the
   // embedding-gradient GEMM concurrently with the weight GEMMs (measured
   // 5.21 vs 4.87 ms per step, also with GPU_MAX_HW_QUEUES=8: the two GEMMs
-  // slow each other down more than the overlap saves).  The
+  // slow each other down more than the overlap saves); 3 = on the main
+  // stream before the reverse loop, under the dS pass (interleaved A/B:
+  // 4.67-4.78 vs 4.76-4.86 ms with one 6.4 ms outlier, kept opt-in).  The
   // outputs are allocated here on the main stream so their memory is ordered
   // by it.
   TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
@@ -442,6 +444,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   if (aux_mode == 2) {
     (void)hipStreamWaitEvent(aux.stream(), ev_ready, 0);
     token_prep(aux);
+  } else if (aux_mode == 3) {
+    // main stream, before the reverse loop: it idles there until the first
+    // dHd chunk is ready, so the sort/gather ride under the dS pass instead
+    // of queueing behind the full-chip dW_logit GEMM after the loop
+    token_prep(main_stream);
   }
   {
     auto side = side_stream(0);
