@@ -201,8 +201,15 @@ class FlatGradBucket:
             raise ValueError('no trainable parameters')
         dev = self.params[0].device
         total = sum(p.numel() for p in self.params)
-        self.data = torch.empty(total, dtype=torch.float32, device=dev)
-        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        # one status slot after the parameters (padded to 64 elements): a
+        # rank's "skip this step" flag rides the gradient all-reduce instead of
+        # a collective of its own.  It is zero in every healthy step, so it adds
+        # nothing to the gradient norm and Adam leaves its (zero) parameter
+        # slot at zero.
+        padded = (total + 1 + 63) // 64 * 64
+        self.data = torch.zeros(padded, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(padded, dtype=torch.float32, device=dev)
+        self.flag = self.grad[total:total + 1]
         self.slices = []
         off = 0
         for p in self.params:
@@ -213,6 +220,16 @@ class FlatGradBucket:
             self.slices.append((off, n))
             off += n
         self.numel = total
+
+    def set_flag(self, bad):
+        """Store this rank's skip flag (0-dim bool device tensor) in the
+        status slot before :meth:`all_reduce`."""
+        self.flag.copy_(bad.reshape(1))
+
+    def flag_any(self):
+        """After :meth:`all_reduce`: true on every rank when any rank set its
+        flag (0-dim bool device tensor, no host sync)."""
+        return self.flag[0] > 0
 
     def zero_grad(self):
         self.grad.zero_()

@@ -217,16 +217,16 @@ class Trainer:
             loss, extra = self.xe_loss(data)
         loss.backward()
         self.timer.mark('backward')
+        skip = None
+        guard = getattr(opt, 'nan_guard', 1)
+        if guard:
+            skip = ~torch.isfinite(loss.detach())
+            if self.ctx.enabled:  # every rank must skip together: the flag
+                self.bucket.set_flag(skip)  # rides the gradient all-reduce
         self.bucket.all_reduce(self.ctx)
         self.timer.mark('allreduce')
-        skip = None
-        if getattr(opt, 'nan_guard', 1):
-            bad = ~torch.isfinite(loss.detach())
-            if self.ctx.enabled:  # every rank must skip together
-                b = bad.float().reshape(1)
-                self.ctx.all_reduce_(b)
-                bad = b[0] > 0
-            skip = bad
+        if guard and self.ctx.enabled:
+            skip = self.bucket.flag_any()
         self.optimizer.step(skip)
         if self.engine is not None:
             self.engine.after_step()

@@ -53,8 +53,16 @@ def main(out):
     flat = tr.bucket.data.detach().cpu().clone()
     allp = ctx.all_gather_object(flat)
     same = all(torch.equal(allp[0], p) for p in allp)
+    # NaN guard: only the last rank's loss is NaN; its skip flag rides the
+    # gradient all-reduce, so every rank must skip the update
+    data = loader.get_batch()
+    if ctx.rank == ctx.world_size - 1:
+        data['masks'] = data['masks'] * float('nan')
+    tr.train_step(data, 0)
+    after = tr.bucket.data.detach().cpu().clone()
+    nan_skip = all(ctx.all_gather_object(torch.equal(after, flat)))
     if ctx.is_main:
-        torch.save({'init': init, 'grad': grad, 'same_after_steps': same,
+        torch.save({'init': init, 'grad': grad, 'same_after_steps': same, 'nan_skip_all': nan_skip,
                     'predictions': res['predictions'], 'loss': res['scores']['Loss'],
                     'world': ctx.world_size}, out)
     ctx.destroy()

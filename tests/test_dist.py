@@ -84,6 +84,11 @@ def test_allreduce_world4(runs):
     assert r4['same_after_steps']
 
 
+def test_nan_on_one_rank_skips_everywhere(runs):
+    # the skip flag travels in the gradient bucket's status slot
+    assert runs[1]['nan_skip_all'] and runs[2]['nan_skip_all'] and runs[4]['nan_skip_all']
+
+
 def test_sharded_validation_matches_single_rank(runs):
     p1, p2 = runs[1]['predictions'], runs[2]['predictions']
     assert len(p1) == 8  # synthetic val split: max(8, 24 // 10) videos
