@@ -495,7 +495,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     const char* e = std::getenv("CSTCAP_BWD_DWLOG_LATE");
     return e ? std::atoi(e) : -1;
   }();
-  const bool dwlog_late = dwlog_env >= 0 ? dwlog_env != 0 : !early;
+  // direct writes without a communication stream (one GPU) keep the late
+  // schedule: nothing waits on the slots before the optimizer
+  const bool dwlog_late = dwlog_env >= 0 ? dwlog_env != 0 : (!early || comm_stream == 0);
   auto launch_dwlog = [&]() {
     auto side = side_stream(0);
     c10::hip::HIPStreamGuard guard(side);

@@ -120,8 +120,15 @@ class _DecoderFn(torch.autograd.Function):
         # flat-bucket slots and are all-reduced during the reverse LSTM loop
         hook = getattr(eng, 'early_grad_hook', None)
         early = hook is not None and hook.active
-        out_w, out_b, comm = (hook.out_wlog, hook.out_blog, hook.comm_ptr) if early \
-            else (empty, empty, 0)
+        # without DP the same slots are written directly too (no autograd
+        # accumulate pass over the V x H gradient), on the late schedule
+        direct = getattr(eng, 'direct_grad_slots', None)
+        if early:
+            out_w, out_b, comm = hook.out_wlog, hook.out_blog, hook.comm_ptr
+        elif direct is not None:
+            (out_w, out_b), comm = direct, 0
+        else:
+            out_w, out_b, comm = empty, empty, 0
         res = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
@@ -130,6 +137,7 @@ class _DecoderFn(torch.autograd.Function):
         dWx, dWlog, dblog, d_emb, dvg = res[:5]
         if early:
             hook.launch()
+        if early or direct is not None:
             dWlog = dblog = None  # already in the gradient buffers
         E = eng.E
         d_orig = dWx.index_select(0, eng.inv_perm)

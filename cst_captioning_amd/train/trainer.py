@@ -92,6 +92,13 @@ class Trainer:
             from ..parallel.dist import EarlyAllReduce
             self.bucket.early = EarlyAllReduce(self.ctx, self.bucket, early)
             engine.early_grad_hook = self.bucket.early
+        if engine is not None:
+            # the fused backward writes the vocab-head gradients straight into
+            # their bucket slots (one backward per step: overwrite == accumulate
+            # onto the zeroed buffer)
+            engine.direct_grad_slots = tuple(
+                self.bucket.grad[off:off + n].view_as(p)
+                for p, (off, n) in zip(early, self.bucket.slices[:2]))
         if getattr(opt, 'honor_optim_flags', 0):
             betas, eps = (opt.optim_alpha, opt.optim_beta), opt.optim_epsilon
         else:
