@@ -20,7 +20,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
                                          at::Tensor dg_xe, double drop_p, int64_t seed,
                                          at::Tensor out_wlog, at::Tensor out_blog,
-                                         int64_t comm_stream, std::vector<at::Tensor> att);
+                                         int64_t comm_stream, std::vector<at::Tensor> att,
+                                         at::Tensor out_emb);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,

@@ -314,7 +314,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
                                          at::Tensor dg_xe, double drop_p, int64_t seed,
                                          at::Tensor out_wlog, at::Tensor out_blog,
-                                         int64_t comm_stream, std::vector<at::Tensor> att) {
+                                         int64_t comm_stream, std::vector<at::Tensor> att,
+                                         at::Tensor out_emb) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -424,7 +425,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
   at::Tensor stok = at::empty_like(toks), srow = at::empty_like(toks);
   at::Tensor x_in = at::empty({n_steps * R, E}, emb.options());     // (n*R, E) bf16
-  at::Tensor d_emb = at::empty({V, E}, f32);
+  // out_emb: the embedding's gradient slot (written directly, zeroed here)
+  const bool emb_direct = out_emb.defined() && out_emb.numel() > 0;
+  if (emb_direct)
+    TORCH_CHECK(out_emb.is_contiguous() && out_emb.scalar_type() == at::kFloat &&
+                    out_emb.size(0) == V && out_emb.size(1) == E,
+                "out_emb must be a contiguous fp32 (V, E) tensor");
+  at::Tensor d_emb = emb_direct ? out_emb : at::empty({V, E}, f32);
   static const int aux_mode = [] {
     const char* e = std::getenv("CSTCAP_BWD_AUX");
     return e ? std::atoi(e) : 0;

@@ -126,19 +126,23 @@ class _DecoderFn(torch.autograd.Function):
         if early:
             out_w, out_b, comm = hook.out_wlog, hook.out_blog, hook.comm_ptr
         elif direct is not None:
-            (out_w, out_b), comm = direct, 0
+            (out_w, out_b), comm = direct[:2], 0
         else:
             out_w, out_b, comm = empty, empty, 0
+        emb_direct = direct is not None and len(direct) > 2
+        out_emb = direct[2] if emb_direct else empty
         res = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
-            ctx.drop_p, ctx.seed, out_w, out_b, comm, att)
+            ctx.drop_p, ctx.seed, out_w, out_b, comm, att, out_emb)
         dWx, dWlog, dblog, d_emb, dvg = res[:5]
         if early:
             hook.launch()
         if early or direct is not None:
             dWlog = dblog = None  # already in the gradient buffers
+        if emb_direct:
+            d_emb = None
         E = eng.E
         d_orig = dWx.index_select(0, eng.inv_perm)
         w_ih_shape, emb_shape = ctx.shapes

@@ -96,9 +96,12 @@ class Trainer:
             # the fused backward writes the vocab-head gradients straight into
             # their bucket slots (one backward per step: overwrite == accumulate
             # onto the zeroed buffer)
+            slot = {id(p): (off, n) for p, (off, n) in zip(self.bucket.params, self.bucket.slices)}
             engine.direct_grad_slots = tuple(
-                self.bucket.grad[off:off + n].view_as(p)
-                for p, (off, n) in zip(early, self.bucket.slices[:2]))
+                self.bucket.grad[slot[id(p)][0]:slot[id(p)][0] + slot[id(p)][1]].view_as(p)
+                for p in early + [model.embed.weight])
+            if os.environ.get('CSTCAP_DIRECT_EMB', '1') == '0':  # A/B knob
+                engine.direct_grad_slots = engine.direct_grad_slots[:2]
         if getattr(opt, 'honor_optim_flags', 0):
             betas, eps = (opt.optim_alpha, opt.optim_beta), opt.optim_epsilon
         else:
