@@ -126,11 +126,15 @@ class _DecoderFn(torch.autograd.Function):
         if early:
             out_w, out_b, comm = hook.out_wlog, hook.out_blog, hook.comm_ptr
         elif direct is not None:
-            (out_w, out_b), comm = direct[:2], 0
+            out_w, out_b, comm = direct['wlog'], direct['blog'], 0
         else:
             out_w, out_b, comm = empty, empty, 0
-        emb_direct = direct is not None and len(direct) > 2
-        out_emb = direct[2] if emb_direct else empty
+        # embedding / LSTM weight slots: written here instead of returned, which
+        # saves autograd's zero-fill + accumulate passes over them.  The video
+        # columns of W_ih still arrive through autograd (the gate-table path),
+        # and add onto these disjoint token columns in either order.
+        emb_direct = direct is not None and 'emb' in direct
+        out_emb = direct['emb'] if emb_direct else empty
         res = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
@@ -146,9 +150,14 @@ class _DecoderFn(torch.autograd.Function):
         E = eng.E
         d_orig = dWx.index_select(0, eng.inv_perm)
         w_ih_shape, emb_shape = ctx.shapes
-        d_wih = torch.zeros(w_ih_shape, dtype=torch.float32, device=dWx.device)
-        d_wih[:, :E] = d_orig[:, :E]
-        d_whh = d_orig[:, E:].contiguous()
+        if emb_direct:
+            direct['wih'][:, :E].copy_(d_orig[:, :E])
+            direct['whh'].copy_(d_orig[:, E:])
+            d_wih = d_whh = None
+        else:
+            d_wih = torch.zeros(w_ih_shape, dtype=torch.float32, device=dWx.device)
+            d_wih[:, :E] = d_orig[:, :E]
+            d_whh = d_orig[:, E:].contiguous()
         if ctx.has_att:
             d_gv, d_pre, d_wa, d_ba, d_wq = res[5:10]
             return (None, d_wih, d_whh, d_emb, dWlog, dblog, d_gv, d_pre, d_wq, d_wa,

@@ -97,11 +97,14 @@ class Trainer:
             # their bucket slots (one backward per step: overwrite == accumulate
             # onto the zeroed buffer)
             slot = {id(p): (off, n) for p, (off, n) in zip(self.bucket.params, self.bucket.slices)}
-            engine.direct_grad_slots = tuple(
-                self.bucket.grad[slot[id(p)][0]:slot[id(p)][0] + slot[id(p)][1]].view_as(p)
-                for p in early + [model.embed.weight])
+            rnn = model.core.rnn
+            named = {'wlog': model.logit.weight, 'blog': model.logit.bias,
+                     'emb': model.embed.weight, 'wih': rnn.weight_ih_l0, 'whh': rnn.weight_hh_l0}
             if os.environ.get('CSTCAP_DIRECT_EMB', '1') == '0':  # A/B knob
-                engine.direct_grad_slots = engine.direct_grad_slots[:2]
+                named = {k: named[k] for k in ('wlog', 'blog')}
+            engine.direct_grad_slots = {
+                k: self.bucket.grad[slot[id(p)][0]:slot[id(p)][0] + slot[id(p)][1]].view_as(p)
+                for k, p in named.items()}
         if getattr(opt, 'honor_optim_flags', 0):
             betas, eps = (opt.optim_alpha, opt.optim_beta), opt.optim_epsilon
         else:

@@ -329,3 +329,35 @@ def test_wide_tile_decode_matches_torch(C):
     lp_ref = pr[:, :k].gather(2, seq[:, :k].unsqueeze(2)).squeeze(2)
     alive = torch.cumprod((seq[:, :k] > 0).long(), 1) > 0
     assert (g_sel[:, :k] - lp_ref).abs()[alive].max() < 0.08
+
+
+def test_trainer_direct_gradient_slots_match_torch():
+    """Through the Trainer the fused backward writes the vocab-head, embedding
+    and LSTM weight gradients straight into the flat bucket (no autograd
+    accumulate); the video columns of W_ih still arrive through autograd.
+    The bucket must hold the same gradient as the PyTorch decoder's."""
+    from cst_captioning_amd.models import CrossEntropyCriterion
+    from cst_captioning_amd.parallel import DistContext
+    from cst_captioning_amd.train.trainer import Trainer
+    ds, opt, model, loader = _tiny(seed=4)
+    ref_model = copy.deepcopy(model)
+    ref_model.impl = 'torch'
+    eng = _engine(model, opt)
+    opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
+    tr = Trainer(opt, model, loader, None, DistContext(device=torch.device(DEV)), eng)
+    assert set(eng.direct_grad_slots) == {'wlog', 'blog', 'emb', 'wih', 'whh'}
+    model.train()
+    ref_model.train()
+    data = loader.get_batch()
+    tr.optimizer.zero_grad()
+    model.set_seq_per_img(5)
+    loss, _ = tr.xe_loss(data)
+    loss.backward()
+    ref_model.set_seq_per_img(5)
+    pred = ref_model(data['feats'], data['labels'])[0]
+    CrossEntropyCriterion()(pred, data['labels'][:, 1:], data['masks'][:, 1:]).backward()
+    for (name, p), (_, q) in zip(model.named_parameters(), ref_model.named_parameters()):
+        if q.grad is None:
+            continue
+        err = (p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)
+        assert err < 0.06, (name, float(err))
