@@ -123,6 +123,13 @@ class _DecoderFn(torch.autograd.Function):
         # without DP the same slots are written directly too (no autograd
         # accumulate pass over the V x H gradient), on the late schedule
         direct = getattr(eng, 'direct_grad_slots', None)
+        if direct is not None:
+            # the slots are overwritten, so only one fused backward may feed
+            # them between two zero_grad() calls
+            if eng.direct_used:
+                raise RuntimeError('second fused backward before zero_grad(): direct '
+                                   'gradient slots would be overwritten')
+            eng.direct_used = True
         if early:
             out_w, out_b, comm = hook.out_wlog, hook.out_blog, hook.comm_ptr
         elif direct is not None:

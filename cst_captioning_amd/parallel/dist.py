@@ -197,6 +197,7 @@ class FlatGradBucket:
         self.params = [p for p in params if id(p) in first_ids] + \
             [p for p in params if id(p) not in first_ids]
         self.early = None
+        self.on_zero = None
         if not self.params:
             raise ValueError('no trainable parameters')
         dev = self.params[0].device
@@ -233,6 +234,8 @@ class FlatGradBucket:
 
     def zero_grad(self):
         self.grad.zero_()
+        if self.on_zero is not None:  # e.g. re-arm the fused engine's direct slots
+            self.on_zero()
         # autograd may have replaced a view (e.g. after set_to_none); re-point
         for p, (off, n) in zip(self.params, self.slices):
             if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():

@@ -105,6 +105,8 @@ class Trainer:
             engine.direct_grad_slots = {
                 k: self.bucket.grad[slot[id(p)][0]:slot[id(p)][0] + slot[id(p)][1]].view_as(p)
                 for k, p in named.items()}
+            engine.direct_used = False
+            self.bucket.on_zero = lambda: setattr(engine, 'direct_used', False)
         if getattr(opt, 'honor_optim_flags', 0):
             betas, eps = (opt.optim_alpha, opt.optim_beta), opt.optim_epsilon
         else:
