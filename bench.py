@@ -22,9 +22,11 @@ Modes:
                reference semantics (PyTorch ops, CPU CIDEr-D in Python):
                the baseline BASELINE.md asks to beat.
 
-Launch: ``python bench.py`` (1 GPU) or
+Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (starts
+the PyTorch launcher with N ranks as a child process), or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1
---master-port P bench.py --gpus N``.
+--master-port P bench.py --gpus N``.  Every rank checks that the job's world
+size equals ``--gpus`` and exits non-zero otherwise.
 """
 import argparse
 import json
@@ -66,8 +68,32 @@ def parse():
     return p.parse_args()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def relaunch_if_needed(a):
+    """``python bench.py --gpus N`` with no torchrun environment: start the
+    PyTorch launcher with N ranks as a CHILD process and exit with its code.
+    This runs before torch is imported, so the parent never touches the GPU
+    (no exec from a process that initialised HIP)."""
+    if a.gpus <= 1 or 'WORLD_SIZE' in os.environ:
+        return
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(a.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     a = parse()
+    relaunch_if_needed(a)
     import torch
     from cst_captioning_amd.config import default_opts
     from cst_captioning_amd.data import CaptionLoader, make_synthetic
@@ -76,6 +102,11 @@ def main():
     from cst_captioning_amd.train.trainer import Trainer
 
     ctx = init_distributed()
+    if ctx.world_size != a.gpus:
+        print('bench.py: --gpus %d but the job has %d rank(s) (WORLD_SIZE=%s)'
+              % (a.gpus, ctx.world_size, os.environ.get('WORLD_SIZE')), file=sys.stderr)
+        ctx.destroy()
+        sys.exit(3)
     if a.impl == 'torch':
         os.environ['CSTCAP_ALLOW_TORCH_FALLBACK'] = '1'
     seed_everything(a.seed, ctx.rank)
@@ -181,6 +212,7 @@ def main():
                    'dedupe_greedy': a.dedupe_greedy,
                    'temporal_attention_frames': a.num_chunks if a.num_chunks > 1 else None},
         'final_loss': loss, 'datagen_s': round(t_gen, 1),
+        'world_size_seen': ctx.world_size, 'backend': ctx.backend or 'none',
     }
     if phases:
         rec['phases_ms'] = {k: round(v, 3) for k, v in phases.items()}

@@ -19,7 +19,7 @@
 //     h_{t-1} . W_hh^T (K = H);
 //   * training mode also emits, for the backward: post-activation gates, c_t,
 //     h_t, and h after dropout (the input of the vocabulary projection; mask
-//     from Philox, regenerated in backward).
+//     from the mix32 counter hash dropout_keep(), regenerated in backward).
 #include "gemm_tile.h"
 
 namespace cst {

@@ -31,8 +31,12 @@ returns ``dGv, dP, dW_q, dw_a, db_a``.
 Semantics match :class:`CaptionModel`'s PyTorch path (reference
 ``model.py:218-367``) with two documented differences that are
 distribution-identical, not value-identical:
-  * RNG: multinomial sampling is Gumbel-max with Philox counters (exact
-    samples from the same softmax), dropout masks come from Philox;
+  * RNG: multinomial sampling is an exact two-level inverse-CDF draw
+    (tile chosen by its probability mass, then a token inside the tile)
+    driven by a murmur3-finaliser counter hash of (seed, row, step); dropout
+    keep-masks come from the same kind of counter hash of (seed, step, row,
+    column), regenerated in the backward (``csrc/common.h`` ``mix32``,
+    ``dropout_keep``); the scheduled-sampling coin uses Philox4x32-10;
   * precision: bf16 MFMA operands, fp32 accumulation, cell state and
     softmax statistics in fp32.
 Supported configuration: ``rnn_type lstm``, ``num_layers 1``, ``model_type

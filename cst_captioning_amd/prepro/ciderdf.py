@@ -92,16 +92,16 @@ def save_df(path_pkl, packed_df, ref_len, write_pickle=True):
 def load_packed_df(path):
     """(keys uint64, values float32, ref_len) from a df file.
 
-    ``.npz`` is read without pickle.  A ``.pkl`` must be one written by this
-    framework (pickles execute code; never load a foreign one)."""
+    ``.npz`` is read without pickle.  A reference-format ``.pkl`` goes
+    through the restricted unpickler (plain containers and numbers only)."""
     if path.endswith('.pkl'):
         npz = path[:-4] + '.npz'
         try:
             z = np.load(npz, allow_pickle=False)
             return z['keys'], z['values'], int(z['ref_len'])
         except FileNotFoundError:
-            with open(path, 'rb') as f:
-                d = pickle.load(f)
+            from ..utils.safe_pickle import safe_load
+            d = safe_load(path)
             keys = np.array([pack_ngram([int(t) for t in g]) for g in d['document_frequency']],
                             dtype=np.uint64)
             vals = np.array(list(d['document_frequency'].values()), dtype=np.float32)

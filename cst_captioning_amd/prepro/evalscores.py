@@ -12,6 +12,7 @@ Results are saved as ``.npz`` (no pickle needed to read them back); a
 ``.pkl`` path also gets the reference-format pickle.
 """
 import argparse
+import os
 import pickle
 
 import numpy as np
@@ -58,8 +59,16 @@ def save_scores(path, scores):
 
 def load_scores(path, metric='CIDEr'):
     """One metric's (N, S) matrix, read from the ``.npz`` written beside a
-    ``.pkl`` (no unpickling)."""
+    ``.pkl`` (no unpickling).  A reference-written ``.pkl`` with no ``.npz``
+    beside it goes through the restricted unpickler (arrays and containers
+    only)."""
     npz = path[:-4] + '.npz' if path.endswith('.pkl') else path
+    if path.endswith('.pkl') and not os.path.exists(npz):
+        from ..utils.safe_pickle import safe_load
+        z = safe_load(path)
+        if metric == 'CIDEr' and metric not in z and 'cider' in z:
+            metric = 'cider'
+        return np.asarray(z[metric], dtype=np.float64)
     z = np.load(npz, allow_pickle=False)
     if metric == 'CIDEr' and metric not in z.files and 'cider' in z.files:
         metric = 'cider'  # dataloader.py:70-71

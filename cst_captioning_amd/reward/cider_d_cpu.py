@@ -21,10 +21,11 @@ is "parity unpinned" (the package is not available in this image); the GPU
 kernel is tested against this oracle.
 """
 import math
-import pickle
 from collections import defaultdict
 
 import numpy as np
+
+from ..utils.safe_pickle import safe_load
 
 NGRAM_N = 4
 SIGMA = 6.0
@@ -163,10 +164,9 @@ def load_df_file(path):
     """Load a df table.
 
     ``.npz`` (written by this framework: keys/values arrays) is read with
-    ``allow_pickle=False``.  A reference-format ``.pkl`` is a pickle of
-    python tuples: it is only loaded when it was produced by *this*
-    framework's prepro (callers pass ``trusted=True`` implicitly by choosing
-    the file); never point this at an untrusted file.
+    ``allow_pickle=False``.  A reference-format ``.pkl`` (tuples of strings
+    -> floats) goes through the restricted unpickler, which resolves no
+    globals beyond plain containers and numbers.
     """
     if str(path).endswith('.npz'):
         z = np.load(path, allow_pickle=False)
@@ -174,5 +174,4 @@ def load_df_file(path):
         keys = unpack_ngram_keys(z['keys'])
         return {'document_frequency': dict(zip(keys, z['values'].tolist())),
                 'ref_len': int(z['ref_len'])}
-    with open(path, 'rb') as f:
-        return pickle.load(f)
+    return safe_load(path)

@@ -10,6 +10,7 @@ Additions: ``<model>_last.pth`` holding optimizer, RNG and
 loader state so a killed run continues bit-exactly (``save_last``), written
 atomically (temp file + rename).
 """
+import argparse
 import json
 import logging
 import os
@@ -30,18 +31,55 @@ def save_checkpoint(model, infos, opt, path):
     d = os.path.dirname(path)
     if d:
         os.makedirs(d, exist_ok=True)
-    _atomic_save({'model': model.state_dict(), 'infos': infos, 'opt': opt}, path)
+    _atomic_save({'model': model.state_dict(), 'infos': _encode(infos), 'opt': _encode(opt)},
+                 path)
     logger.info('Wrote checkpoint to: %s', path)
 
 
-def load_checkpoint(path, map_location='cpu', trusted=True):
-    """Load a checkpoint.  Reference checkpoints pickle an argparse Namespace,
-    so they need ``weights_only=False``: only do that for files this
-    framework (or a trusted reference run) wrote.  ``trusted=False`` loads
-    with ``weights_only=True`` and returns only what that allows."""
-    if not trusted:
-        return torch.load(path, map_location=map_location, weights_only=True)
-    return torch.load(path, map_location=map_location, weights_only=False)
+def _encode(obj):
+    """Make a state tree loadable with ``weights_only=True``: numpy arrays
+    become tagged tensors, numpy scalars Python numbers, numpy RNG state
+    tuples tagged dicts."""
+    if isinstance(obj, np.ndarray):
+        return {'__ndarray__': torch.from_numpy(np.ascontiguousarray(obj))}
+    if isinstance(obj, np.generic):
+        return obj.item()
+    if isinstance(obj, tuple) and len(obj) == 5 and obj[0] == 'MT19937':
+        return {'__np_rng__': [obj[0], torch.from_numpy(obj[1].astype(np.int64)), int(obj[2]),
+                               int(obj[3]), float(obj[4])]}
+    if isinstance(obj, argparse.Namespace):
+        return argparse.Namespace(**_encode(vars(obj)))
+    if isinstance(obj, dict):
+        return {k: _encode(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_encode(v) for v in obj)
+    return obj
+
+
+def _decode(obj):
+    if isinstance(obj, argparse.Namespace):
+        return argparse.Namespace(**_decode(vars(obj)))
+    if isinstance(obj, dict):
+        if set(obj) == {'__ndarray__'}:
+            return obj['__ndarray__'].cpu().numpy()
+        if set(obj) == {'__np_rng__'}:
+            name, keys, pos, has_gauss, cached = obj['__np_rng__']
+            return (name, keys.cpu().numpy().astype(np.uint32), pos, has_gauss, cached)
+        return {k: _decode(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_decode(v) for v in obj)
+    return obj
+
+
+def load_checkpoint(path, map_location='cpu'):
+    """Load a checkpoint with ``torch.load(weights_only=True)`` -- nothing in
+    the file is executed.  The reference pickles an ``argparse.Namespace`` as
+    ``opt`` (``/root/reference/train.py:87-91``), so that one class is on the
+    allow-list; files this framework writes hold only tensors, containers and
+    numbers (numpy state is tagged by :func:`_encode`)."""
+    with torch.serialization.safe_globals([argparse.Namespace]):
+        s = torch.load(path, map_location=map_location, weights_only=True)
+    return _decode(s)
 
 
 def resolve_start_from(start_from, model_file):
@@ -63,15 +101,20 @@ def rng_state(extra=None):
             'extra': extra}
 
 
-def save_last(path, model, optimizer, infos, opt, loader, rng_extra=None, per_rank=None):
+def save_last(path, model, optimizer, infos, opt, loader, rng_extra=None, per_rank=None,
+              extra=None):
     """``per_rank``: optional list (one entry per DP rank) of
-    ``{'loader': state, 'rng': state}``; rank r resumes from entry r."""
+    ``{'loader': state, 'rng': state}``; rank r resumes from entry r.
+    ``extra``: trainer state beyond ``infos`` (history, resolved schedule
+    epochs)."""
     state = {'model': model.state_dict(), 'infos': infos, 'opt': opt,
              'optimizer': optimizer.state_dict(), 'loader': loader.state_dict(),
              'rng': rng_state(rng_extra)}
     if per_rank is not None:
         state['per_rank'] = per_rank
-    _atomic_save(state, path)
+    if extra is not None:
+        state['extra'] = extra
+    _atomic_save(_encode(state), path)
 
 
 def restore_rng(rng):

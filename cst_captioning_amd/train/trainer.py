@@ -262,12 +262,18 @@ class Trainer:
             if pr is not None and len(pr) == self.ctx.world_size:
                 self.train_loader.load_state_dict(pr[self.ctx.rank]['loader'])
                 ckpt.restore_rng(pr[self.ctx.rank]['rng'])
+                if self.val_loader is not None and 'val_loader' in pr[self.ctx.rank]:
+                    self.val_loader.load_state_dict(pr[self.ctx.rank]['val_loader'])
             else:  # written by a run with another world size: shared state only
                 self.train_loader.load_state_dict(s['loader'])
                 ckpt.restore_rng(s['rng'])
             self.infos = s['infos']
+            extra = s.get('extra') or {}
+            self.history = extra.get('history', {})
+            self._exact_resume = extra
             logger.info('Resumed exactly from %s (iter %d)', last, self.infos['iter'])
-            return True
+            # the sidecar records whether that epoch's validation already ran
+            return extra.get('checked', True)
         if path and os.path.exists(path):
             logger.info('Loading state from: %s', path)
             s = ckpt.load_checkpoint(path, map_location=self.device)
@@ -278,15 +284,41 @@ class Trainer:
         logger.info('No checkpoint found! Training from the scratch')
         return False
 
+    def _save_last(self, checked):
+        """Exact-resume sidecar: weights, optimizer, infos, history, the
+        resolved RL/CST start epochs and every rank's loader position and RNG
+        streams (gathered, written by rank 0)."""
+        opt = self.opt
+        if not (opt.model_file and getattr(opt, 'save_last', 1)):
+            return
+        mine = {'loader': self.train_loader.state_dict(), 'rng': ckpt.rng_state()}
+        if self.val_loader is not None:  # its caption draws continue too
+            mine['val_loader'] = self.val_loader.state_dict()
+        per_rank = self.ctx.all_gather_object(mine)
+        if self.ctx.is_main:
+            extra = {'history': self.history, 'checked': checked,
+                     'use_rl_after': opt.use_rl_after,
+                     'use_cst_after': getattr(opt, 'use_cst_after', 0)}
+            ckpt.save_last(ckpt.last_path(opt.model_file), self.model, self.optimizer,
+                           self.infos, opt, self.train_loader, per_rank=per_rank, extra=extra)
+        self.ctx.barrier()
+
     def train(self):
         opt, infos = self.opt, None
+        self._exact_resume = None
         checked = self.resume()
         infos = self.infos
         if opt.model_file and self.ctx.is_main and not os.path.exists(opt.model_file):
             logger.info('>>> No model file found. Write a base checkpoint.')
             ckpt.save_checkpoint(self.model, infos, opt, opt.model_file)
         self.ctx.barrier()
-        if opt.use_rl == 1 and opt.use_rl_after == 0:
+        if self._exact_resume is not None and 'use_rl_after' in self._exact_resume:
+            # exact resume: keep the schedule origin of the interrupted run, so
+            # MIXER / SCB annealing continues where it was
+            opt.use_rl_after = self._exact_resume['use_rl_after']
+            opt.use_cst_after = self._exact_resume['use_cst_after']
+        elif opt.use_rl == 1 and opt.use_rl_after == 0:
+            # train.py:95-98: RL starts at the (warm-start) resume epoch
             opt.use_rl_after = infos['epoch']
             opt.use_cst_after = infos['epoch']
             self.train_loader.set_current_epoch(infos['epoch'])
@@ -306,15 +338,7 @@ class Trainer:
                 lr = schedules.adjust_learning_rate(opt, self.optimizer,
                                                     infos['epoch'] - infos['start_epoch'])
                 logger.info('===> Learning rate: %f: ', lr)
-                if opt.model_file and getattr(opt, 'save_last', 1):
-                    # every rank's loader position and RNG streams, written by rank 0
-                    per_rank = self.ctx.all_gather_object(
-                        {'loader': self.train_loader.state_dict(), 'rng': ckpt.rng_state()})
-                    if self.ctx.is_main:
-                        ckpt.save_last(ckpt.last_path(opt.model_file), self.model,
-                                       self.optimizer, infos, opt, self.train_loader,
-                                       per_rank=per_rank)
-                    self.ctx.barrier()
+                self._save_last(checked=False)
             if (self.val_loader is not None and infos['epoch'] >= opt.save_checkpoint_from
                     and infos['epoch'] % opt.save_checkpoint_every == 0 and not checked):
                 results = self.validate(self.val_loader)
@@ -324,21 +348,38 @@ class Trainer:
                 infos.update(results['scores'])
                 self.check_model()
                 checked = True
+                # re-save with the validated best score / epoch and history
+                self._save_last(checked=True)
             if infos['epoch'] >= opt.max_epochs or \
                     infos['epoch'] - infos['best_epoch'] > opt.max_patience:
                 logger.info('>>> Terminating...')
                 break
         return infos
 
+    def reduce_log_scalars(self, out):
+        """C3: the logged scalars averaged over the ranks -- ONE small
+        all-reduce, on log iterations only, before the host conversion.
+        Returns ``[loss, reward mean, m, b]`` (the RL entries only in RL mode)
+        as Python floats."""
+        vals = [out['loss']]
+        if self.rl_training:
+            vals += [out['reward'].float().mean(), out['m'], out['b']]
+        dev = self.ctx.comm_device if self.ctx.enabled else self.device
+        t = torch.stack([torch.as_tensor(v).detach().to(dev, torch.float64).reshape(())
+                         for v in vals])
+        self.ctx.all_reduce_(t, average=True)
+        return t.tolist()
+
     def _log(self, out, elapsed):
         opt, infos = self.opt, self.infos
-        loss = float(out['loss'])
+        vals = self.reduce_log_scalars(out)
+        loss = vals[0]
         infos['TrainLoss'] = loss
         items = [('Epoch', infos['epoch']), ('Iter', infos['iter']), ('Loss', loss)]
         if self.rl_training:
-            items += [('Reward', float(out['reward'].float().mean())),
-                      ('{} (m)'.format(opt.eval_metric), float(out['m'])),
-                      ('{} (b)'.format(opt.eval_metric), float(out['b']))]
+            items += [('Reward', vals[1]),
+                      ('{} (m)'.format(opt.eval_metric), vals[2]),
+                      ('{} (b)'.format(opt.eval_metric), vals[3])]
         if opt.use_ss == 1:
             items.append(('ss_prob', opt.ss_prob))
         if opt.use_mixer == 1:
@@ -346,6 +387,18 @@ class Trainer:
         if opt.use_cst == 1:
             items.append(('scb_captions', out['scb_captions']))
         items.append(('Time', elapsed))
+        # throughput since the previous log line (the scalar reduction above
+        # synchronised the device, so the wall clock covers finished work)
+        now = time.perf_counter()
+        last = getattr(self, '_last_log', None)
+        self._last_log = (now, infos['iter'])
+        if last is not None and infos['iter'] > last[1]:
+            rows = self.train_loader.get_batch_size() * self.train_loader.get_seq_per_img()
+            items.append(('Captions/s', round(rows * self.ctx.world_size * (infos['iter'] - last[1])
+                                              / (now - last[0]), 1)))
+        if self.device.type == 'cuda':
+            items.append(('HBM_GB', round(torch.cuda.max_memory_allocated(self.device) / 2 ** 30,
+                                          2)))
         ph = self.timer.summary()
         if ph:
             items.append(('phases_ms', ','.join('%s=%.2f' % kv for kv in ph.items())))
@@ -404,7 +457,14 @@ class Trainer:
             gl = sorted((x for g in gathered for x in g['gt_avglogp']), key=lambda x: x[0])
             gt = np.array([v for _, l in gl for v in l]).reshape(-1, S)
             if ctx.is_main and opt.model_file:
-                np.save(opt.model_file.replace('.pth', '_gt_avglogps.npy', 1), gt)
+                # train.py:367-373: the (N, S) array pickled beside the model
+                # (plus an .npy twin that loads without unpickling)
+                import pickle
+                path = opt.model_file.replace('.pth', '_gt_avglogps.pkl', 1)
+                with open(path, 'wb') as f:
+                    pickle.dump(gt, f, protocol=pickle.HIGHEST_PROTOCOL)
+                np.save(path[:-4] + '.npy', gt)
+                logger.info('Wrote GT logp to: %s', path)
         results['scores'] = ctx.broadcast_object(scores)
         m.train()
         return results

@@ -61,10 +61,21 @@ def main(out):
     tr.train_step(data, 0)
     after = tr.bucket.data.detach().cpu().clone()
     nan_skip = all(ctx.all_gather_object(torch.equal(after, flat)))
+    # C3: logged scalars are the mean over ranks (rank r logs loss r + 1,
+    # reward row means r, m = 2r, b = -r)
+    r = float(ctx.rank)
+    tr.rl_training = True
+    logged = tr.reduce_log_scalars({'loss': torch.tensor(r + 1.0),
+                                    'reward': torch.full((6,), r), 'm': 2 * r, 'b': -r})
+    step_out = tr.train_step(loader.get_batch(), 0)
+    tr.rl_training = False
+    xe_logged = tr.reduce_log_scalars(step_out)
+    xe_losses = ctx.all_gather_object(float(step_out['loss']))
     if ctx.is_main:
         torch.save({'init': init, 'grad': grad, 'same_after_steps': same, 'nan_skip_all': nan_skip,
                     'predictions': res['predictions'], 'loss': res['scores']['Loss'],
-                    'world': ctx.world_size}, out)
+                    'world': ctx.world_size, 'logged': logged, 'xe_logged': xe_logged,
+                    'xe_losses': xe_losses}, out)
     ctx.destroy()
 
 

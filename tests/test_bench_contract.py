@@ -21,12 +21,16 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize('world', [1, 2])
-def test_bench_json_line(world):
+@pytest.mark.parametrize('world,launcher', [(1, False), (2, True), (2, False)])
+def test_bench_json_line(world, launcher):
+    """launcher=False with world 2 is the driver's ``python bench.py --gpus 2``
+    shape: bench.py starts the ranks itself."""
     env = dict(os.environ, CUDA_VISIBLE_DEVICES='', OMP_NUM_THREADS='1')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK'):
+        env.pop(k, None)
     args = ['bench.py', '--gpus', str(world), '--impl', 'torch', '--steps', '2', '--warmup', '1',
             '--videos', '48', '--vocab', '300', '--batch_size', '4']
-    if world > 1:
+    if launcher:
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node',
                str(world), '--master-addr', '127.0.0.1', '--master-port', str(_port())] + args
     else:
@@ -44,5 +48,20 @@ def test_bench_json_line(world):
     assert rec['dtype'] == 'fp32'  # the PyTorch path computes in fp32
     assert rec['config']['global_batch'] == 4 * 20 * world
     assert rec['config']['parallelism'] == 'dp%d' % world
+    assert rec['world_size_seen'] == world
+    assert rec['backend'] == ('gloo' if world > 1 else 'none')
     # whole-job value = global captions / step time
     assert abs(rec['value'] - 4 * 20 * world / (rec['ms_per_step'] / 1e3)) < 0.02 * rec['value']
+
+
+def test_bench_world_size_mismatch_fails():
+    """A rank whose job size differs from --gpus exits non-zero."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES='', OMP_NUM_THREADS='1', WORLD_SIZE='1',
+               RANK='0', LOCAL_RANK='0')
+    r = subprocess.run([sys.executable, 'bench.py', '--gpus', '2', '--impl', 'torch', '--steps',
+                        '1', '--warmup', '0', '--videos', '48', '--vocab', '300',
+                        '--batch_size', '4'], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode != 0
+    assert 'rank(s)' in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith('{')]

@@ -89,6 +89,18 @@ def test_nan_on_one_rank_skips_everywhere(runs):
     assert runs[1]['nan_skip_all'] and runs[2]['nan_skip_all'] and runs[4]['nan_skip_all']
 
 
+def test_log_scalars_are_rank_means(runs):
+    """C3: the log line's loss / reward / m / b are averaged over ranks."""
+    for w in (1, 2, 4):
+        mean = (w - 1) / 2.0
+        assert runs[w]['logged'] == pytest.approx([mean + 1, mean, 2 * mean, -mean])
+        # a real step: the logged XE loss is the mean of the per-rank losses
+        xl = runs[w]['xe_losses']
+        assert len(xl) == w
+        assert runs[w]['xe_logged'] == pytest.approx([sum(xl) / w], rel=1e-6)
+    assert len(set(runs[4]['xe_losses'])) > 1  # shards differ, so the test has teeth
+
+
 def test_sharded_validation_matches_single_rank(runs):
     p1, p2 = runs[1]['predictions'], runs[2]['predictions']
     assert len(p1) == 8  # synthetic val split: max(8, 24 // 10) videos
