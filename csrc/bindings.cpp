@@ -10,7 +10,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         at::Tensor blog, at::Tensor vgate, int64_t vgate_div,
                                         at::Tensor labels, at::Tensor bos, int64_t R, int64_t T,
                                         std::vector<int64_t> modes, double ss_prob,
-                                        double drop_p, double temperature, int64_t seed,
+                                        double drop_p, double temperature, at::Tensor rng,
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att);
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
@@ -18,7 +18,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor hdrop_all, at::Tensor gates_all,
                                          at::Tensor c_all, at::Tensor h_all, at::Tensor seq,
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
-                                         at::Tensor dg_xe, double drop_p, int64_t seed,
+                                         at::Tensor dg_xe, double drop_p, at::Tensor rng,
                                          at::Tensor out_wlog, at::Tensor out_blog,
                                          int64_t comm_stream, std::vector<at::Tensor> att,
                                          at::Tensor out_emb);
@@ -28,16 +28,17 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     std::vector<at::Tensor> att);
 double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
                           int64_t iters);
-double vocab_bwd_dhd_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
-                           at::Tensor wT, int64_t V, int64_t splits, int64_t dbg, int64_t iters);
-void set_bwd_fused(int64_t on);
+double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
+std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V);
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
                        int64_t flags, bool save, int64_t iters);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
                        double log_ref_len, int64_t use_eos);
 at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
-                          at::Tensor partials, at::Tensor scal, at::Tensor skip, double lr,
-                          double b1, double b2, double eps, double clip, double bc1, double bc2);
+                          at::Tensor partials, at::Tensor scal, at::Tensor skip, at::Tensor hyper,
+                          double b1, double b2, double eps, double clip, at::Tensor shadow_meta,
+                          std::vector<at::Tensor> shadow_dst);
+void refresh_shadows(at::Tensor p, at::Tensor shadow_meta, std::vector<at::Tensor> shadow_dst);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -97,11 +98,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cider_score", &cst::cider_score);
   m.def("cider_score_cpu", &cst::cider_score_cpu);
   m.def("flat_adam_step", &cst::flat_adam_step);
-  m.def("set_vocab_variant", &cst::set_vocab_variant);
+  m.def("refresh_shadows", &cst::refresh_shadows);
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
   m.def("vocab_bwd_ds_bench", &cst::vocab_bwd_ds_bench);
-  m.def("vocab_bwd_dhd_bench", &cst::vocab_bwd_dhd_bench);
-  m.def("set_bwd_fused", &cst::set_bwd_fused);
+  m.def("token_sort_bench", &cst::token_sort_bench);
+  m.def("token_sort", &cst::token_sort);
   m.def("beam_search", &cst::beam_search);
-  m.def("set_lstm_fwd_variant", &cst::set_lstm_fwd_variant);
 }

@@ -151,6 +151,16 @@ enum RngStream : uint32_t {
   RNG_SS = 3,         // scheduled-sampling coin per row
 };
 
+// Per-pass RNG seeds live in DEVICE memory (int32[2], drawn by the caller with
+// torch.randint on the GPU), not in kernel arguments: a captured HIP graph
+// replays its kernel arguments verbatim, so seeds passed by value would repeat
+// the same dropout masks and samples on every replay.  The backward reads the
+// same two words as its forward, so it regenerates the forward's masks.
+enum RngSlot : int { RNG_SLOT_DROPOUT = 0, RNG_SLOT_SAMPLE = 1 };
+__device__ __forceinline__ uint32_t rng_seed(const uint32_t* rng, int slot) {
+  return rng != nullptr ? rng[slot] : 0u;
+}
+
 // Keep-mask of dropout on element (row, col) of step t: a counter hash, so the
 // backward regenerates exactly the forward's mask.
 __device__ __forceinline__ bool dropout_keep(uint32_t seed, int step, int row, int col,

@@ -45,11 +45,35 @@ static void check_cuda(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
-static int g_bwd_fused = [] {
-  const char* e = std::getenv("CSTCAP_BWD_FUSED");
-  return e ? std::atoi(e) : 0;
-}();
-void set_bwd_fused(int64_t on) { g_bwd_fused = (int)on; }
+// rng: int32[2] device tensor {dropout seed, sampling seed} (or undefined /
+// empty: seeds 0).  Kernels read it from device memory, so a captured HIP
+// graph draws fresh masks and samples on every replay.
+static const uint32_t* rng_ptr(const at::Tensor& rng) {
+  if (!rng.defined() || rng.numel() == 0) return nullptr;
+  TORCH_CHECK(rng.is_cuda() && rng.scalar_type() == at::kInt && rng.numel() >= 2 &&
+                  rng.is_contiguous(),
+              "rng must be a contiguous int32[2] GPU tensor");
+  return reinterpret_cast<const uint32_t*>(rng.data_ptr());
+}
+
+// Events and side streams are created once per device and reused: nothing
+// is created or destroyed while a HIP graph is being captured.
+struct DeviceAux {
+  std::vector<hipEvent_t> ev;
+  c10::hip::HIPStream side[2];
+};
+static DeviceAux& device_aux(int dev_index) {
+  static std::map<int, DeviceAux*> aux;
+  auto it = aux.find(dev_index);
+  if (it == aux.end()) {
+    auto* a = new DeviceAux{{}, {c10::hip::getStreamFromPool(false, dev_index),
+                                 c10::hip::getStreamFromPool(false, dev_index)}};
+    a->ev.resize(6);
+    for (auto& e : a->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    it = aux.emplace(dev_index, a).first;
+  }
+  return *it->second;
+}
 
 // modes[t] = token-selection mode for token t+1 (see SelModeHost)
 std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor ptab,
@@ -57,7 +81,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         at::Tensor blog, at::Tensor vgate, int64_t vgate_div,
                                         at::Tensor labels, at::Tensor bos, int64_t R, int64_t T,
                                         std::vector<int64_t> modes, double ss_prob,
-                                        double drop_p, double temperature, int64_t seed,
+                                        double drop_p, double temperature, at::Tensor rng,
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att) {
   check_cuda(wx, "wx");
@@ -126,10 +150,6 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor g_sel = at::zeros({R, T - 1}, f32);
   at::Tensor g_xe = want_xe ? at::zeros({R, T}, f32) : at::Tensor();
   at::Tensor lse = at::empty({n_steps, R}, f32);
-  static const bool merged = [] {
-    const char* e = std::getenv("CSTCAP_FWD_MERGED");  // A/B knob (default on)
-    return e == nullptr || std::atoi(e) != 0;
-  }();
   const int n_vt = vocab_num_tiles((int)V);
   at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4}, f32);
   at::Tensor counts = at::zeros({(T + 1) * combine_count_ints_per_step()},
@@ -152,8 +172,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor c_a = at::zeros({R, H}, f32), c_b = at::empty({R, H}, f32);
   at::Tensor hd_tmp = (!save && drop_p > 0) ? at::empty({R, H + HAUG}, bf) : at::Tensor();
 
-  const uint32_t seed_drop = (uint32_t)(seed * 2654435761u + 17u);
-  const uint32_t seed_samp = (uint32_t)(seed * 40503u + 0x9E37u);
+  const uint32_t* RNG = rng_ptr(rng);
   const float inv_temp = (float)(1.0 / temperature);
   const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
@@ -205,48 +224,17 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   const float* VG = has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>();
   const int VDIV = has_att ? 1 : (int)vgate_div;
 
-  if (!merged) {  // reference structure: LSTM step -> vocab -> combine, per step
-    for (int64_t t = 0; t < n_steps; ++t) {
-      const int64_t* tok = t == 0 ? (have_labels ? LAB : bos.data_ptr<int64_t>())
-                                  : seq.data_ptr<int64_t>() + (t - 1);
-      const int64_t tok_stride = t == 0 ? (have_labels ? L : 1) : T - 1;
-      if (has_att) run_att(t);
-      launch_lstm_step_fwd(tok, tok_stride, ptab.data_ptr<float>(),
-                           t == 0 ? reinterpret_cast<uint16_t*>(zeros_h.data_ptr()) : h_buf(t - 1),
-                           t == 0 ? zeros_c.data_ptr<float>() : c_buf(t - 1),
-                           VG, VDIV, (int)R, (int)H, WHH, h_buf(t),
-                           c_buf(t), hd_buf(t), (int)(H + HAUG), (float)drop_p, seed_drop, (int)t,
-                           gates_buf(t), st);
-      uint16_t* hd = hd_buf(t);
-      const bool choose = t < T - 1;
-      const int mode = choose ? (int)modes[t] : SEL_GT_H;
-      const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
-      const int vflags = do_sample | ((choose && mode == SEL_GREEDY_H) ? 2 : 0);
-      const int64_t* tgt = (have_labels && t + 1 < L) ? LAB + (t + 1) : nullptr;
-      launch_vocab_fwd(hd ? hd : h_buf(t), hd ? (int)(H + HAUG) : (int)H, (int)R, (int)H, W,
-                       blog.data_ptr<float>(), (int)V,
-                       save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
-                       part.data_ptr(), tgt, L, vflags, inv_temp, seed_samp, (int)t, st);
-      launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
-                           choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
-                           choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,
-                           want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
-                           (float)ss_prob, seed_samp, (int)t,
-                           use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
-                           use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st);
-    }
-  }
   // step 0: fused LSTM step (h_{-1} = c_{-1} = 0)
-  if (merged && has_att) run_att(0);
-  if (merged) launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
+  if (has_att) run_att(0);
+  launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
                        ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(zeros_h.data_ptr()),
                        zeros_c.data_ptr<float>(), VG, VDIV, (int)R,
                        (int)H, WHH, h_buf(0), c_buf(0), hd_buf(0), (int)(H + HAUG), (float)drop_p,
-                       seed_drop, 0, gates_buf(0), st);
+                       RNG, 0, gates_buf(0), st);
   // Steps t >= 0: ONE launch runs the vocab projection of step t together with
   // the recurrent GEMM of step t+1 (pre = h_t W_hh^T + vgate), then the combine
   // picks token t+1 and applies step t+1's cell epilogue (pre + P[token]).
-  for (int64_t t = 0; merged && t < n_steps; ++t) {
+  for (int64_t t = 0; t < n_steps; ++t) {
     const bool next = t + 1 < n_steps;
     uint16_t* hd = hd_buf(t);
     const uint16_t* vin = hd ? hd : h_buf(t);
@@ -263,7 +251,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     if (has_att && next) q_next = save ? q_all[t + 1] : q_tmp;
     launch_vocab_lstm_fwd(vin, ldh, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
                           save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
-                          part.data_ptr(), tgt, L, vflags, inv_temp, seed_samp, (int)t,
+                          part.data_ptr(), tgt, L, vflags, inv_temp, RNG, (int)t,
                           h_buf(t), WHH, has_att ? nullptr : VG, VDIV,
                           next ? pre.data_ptr<float>() : nullptr, st, has_att ? (int)A : 0,
                           has_att && next ? q_next.data_ptr<float>() : nullptr);
@@ -277,13 +265,13 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       TORCH_CHECK(choose, "internal: a next step needs a chosen token");
       cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_buf(t), c_buf(t + 1),
                       h_buf(t + 1), hd_buf(t + 1), (int)(H + HAUG), gates_buf(t + 1), (int)H,
-                      (float)drop_p, seed_drop, (int)(t + 1)};
+                      (float)drop_p, (int)(t + 1)};
     }
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                          choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
                          choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,
                          want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
-                         (float)ss_prob, seed_samp, (int)t,
+                         (float)ss_prob, RNG, (int)t,
                          use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
                          use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st,
                          next ? &cl : nullptr);
@@ -307,12 +295,26 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 // (+ {dGv (Bv, C, 4H), dP (Bv, C, A), dw_a (A), db_a (1), dW_q (A, H)} with attention,
 // att = {Gv, P, W_q bf16, w_a, alpha_all (n, R, C), q_all (n, R, A)}; dvg_rows empty).
 // toks: (n_steps*R) input token of every (step, row), step-major.
+//
+// Schedule (streams):
+//   side 0 : dS = dG (onehot - softmax) in place of the fp16 logits (plus
+//            bias-gradient column partials), then dHd = dS W_logit (one BLAS
+//            GEMM over all T*R rows);
+//   main   : waits for dHd, runs the reverse LSTM loop (one fused kernel per
+//            step: recurrent GEMM + cell backward), then the token counting
+//            sort / embedding gather, the embedding-gradient GEMM + grouped
+//            row sums and the batched weight-gradient GEMMs;
+//   side 0 : dW_logit = dS^T Hd -- after the loop on one GPU (run concurrently
+//            the BLAS GEMM takes every CU and delays the loop's first step by
+//            ~370 us), concurrently with the loop under data parallelism so
+//            the vocab head's all-reduce (comm_stream waits on it) hides under
+//            the loop.
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
                                          at::Tensor c_all, at::Tensor h_all, at::Tensor seq,
                                          at::Tensor labels, at::Tensor toks, at::Tensor dg_sel,
-                                         at::Tensor dg_xe, double drop_p, int64_t seed,
+                                         at::Tensor dg_xe, double drop_p, at::Tensor rng,
                                          at::Tensor out_wlog, at::Tensor out_blog,
                                          int64_t comm_stream, std::vector<at::Tensor> att,
                                          at::Tensor out_emb) {
@@ -322,12 +324,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   hipStream_t st = cur_stream();
   auto dev = wx.device();
   auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+  auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
   const bool has_sel = dg_sel.defined() && dg_sel.numel() > 0;
   const bool has_xe = dg_xe.defined() && dg_xe.numel() > 0;
   if (has_sel) TORCH_CHECK(dg_sel.is_contiguous() && dg_sel.size(1) == T_sel, "dg_sel shape");
   if (has_xe) TORCH_CHECK(dg_xe.is_contiguous() && labels.defined(), "dg_xe needs labels");
   TORCH_CHECK(toks.numel() == n_steps * R, "toks must hold one token per (step, row)");
-  const uint32_t seed_drop = (uint32_t)(seed * 2654435761u + 17u);
+  const uint32_t* RNG = rng_ptr(rng);
   const bool has_att = !att.empty();
   at::Tensor a_gv, a_pre, a_wq, a_wa, a_alpha, a_q;
   int64_t Bv = 0, C = 0, A = 0, vdiv = 1;
@@ -342,41 +345,18 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   }
   // dG rows: 4H gate gradients (+ A columns of dq with attention)
   const int64_t KD = H4 + A;
-
-  // 1-3. Vocab head + reverse recurrence, pipelined over row chunks.
-  //    Side stream, last chunk first: dS = dG (onehot - softmax) in place
-  //    (fp16 logits -> bf16 dS, plus per-block column sums for the bias), then
-  //    dHd = dS W for the chunk; finally dWlog = dS^T Hd.
-  //    Main stream: the reverse LSTM loop, which needs dHd of step t only, so
-  //    it starts as soon as the last chunk is ready and overlaps the rest.
   TORCH_CHECK(V <= 8 * 2048, "vocab larger than the dS kernel's register tiling");
+  TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
   const int64_t NR = n_steps * R;
-  // Fused route (vocab_bwd.hip; CSTCAP_BWD_FUSED=1 or set_bwd_fused(1)): one
-  // kernel forms dS from the fp16 logits and multiplies it into dHd (split-K
-  // over the vocabulary into CSTCAP_BWD_DHD_SPLIT partials, 1 or 2), writing
-  // dS in place and the bias-gradient column sums.  Measured slower on
-  // MI355X (1.0 ms vs 0.43 + 0.45 ms for the dS pass + BLAS GEMM, see
-  // profiles/README.md), so the two-pass route is the default.
-  const int fused_env = g_bwd_fused;
-  static const int dhd_split = [] {
-    const char* e = std::getenv("CSTCAP_BWD_DHD_SPLIT");
-    return e ? std::max(1, std::min(2, std::atoi(e))) : 2;
-  }();
-  const bool fused = fused_env != 0 && H == 512 && ldl % 8 == 0;
-  const int n_part = fused ? dhd_split : 1;
-  at::Tensor colsum =
-      at::empty({fused ? vocab_bwd_dhd_colsum_rows(NR) : vocab_bwd_ds_blocks((int)n_steps, (int)R), V},
-                f32);
+  DeviceAux& aux = device_aux((int)dev.index());
+  hipEvent_t ev_ready = aux.ev[0], ev_dhd = aux.ev[1], ev_done = aux.ev[2];
+  c10::hip::HIPStream side = aux.side[0];
+
+  // 1-2. vocab head on the side stream: dS in place, dHd = dS W
+  at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n_steps, (int)R), V}, f32);
   at::Tensor dS = logits16.view(at::kBFloat16).view({NR, ldl}).narrow(1, 0, V);
   at::Tensor hd2 = hdrop_all.view({NR, H + HAUG}).narrow(1, 0, H);
-  at::Tensor dHd_all = at::empty({n_part, NR, H}, f32);
-  at::Tensor dHd = dHd_all[0];
-  const int64_t ldw = fused ? (V + vocab_bwd_dhd_kpad() - 1) / vocab_bwd_dhd_kpad() * vocab_bwd_dhd_kpad() : 0;
-  at::Tensor wT = fused ? at::zeros({H, ldw}, wlog.options()) : at::Tensor();  // W_logit^T, padded
-  // early gradients (DP overlap): dWlog / dblog written straight into the
-  // caller's gradient buffers on the side stream, and the caller's
-  // communication stream made to wait for them, so their all-reduce runs
-  // under the reverse LSTM loop
+  at::Tensor dHd = at::empty({NR, H}, f32);
   const bool early = out_wlog.defined() && out_wlog.numel() > 0;
   if (early) {
     TORCH_CHECK(out_wlog.scalar_type() == at::kFloat && out_wlog.is_contiguous() &&
@@ -385,139 +365,35 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     TORCH_CHECK(out_blog.scalar_type() == at::kFloat && out_blog.numel() == V, "out_blog shape");
   }
   at::Tensor dWlog = early ? out_wlog : at::empty({V, H}, f32);
-  at::Tensor dblog;
-  const int64_t DR = vocab_bwd_ds_rows();
-  static const int max_chunks = [] {
-    const char* e = std::getenv("CSTCAP_BWD_CHUNKS");  // A/B knob for the pipeline depth
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
-  const int n_chunks =
-      fused ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(max_chunks, NR / (8 * DR)));
-  std::vector<int64_t> cb(n_chunks + 1);
-  for (int c = 0; c <= n_chunks; ++c) cb[c] = c == n_chunks ? NR : (NR * c / n_chunks) / DR * DR;
-  std::vector<hipEvent_t> ev(n_chunks + 2);
-  for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  hipEvent_t ev_ready = ev[n_chunks], ev_done = ev[n_chunks + 1];
+  at::Tensor dblog = early ? out_blog.view({V}) : at::empty({V}, f32);
   (void)hipEventRecord(ev_ready, st);
-  // persistent side streams per device (slot 0: vocab head, slot 1: token
-  // sort / embedding gradient): pool streams rotate, and every new stream
-  // pays hipBLASLt handle/workspace setup on first use
-  static std::map<std::pair<int, int>, c10::hip::HIPStream> side_streams;
-  auto side_stream = [&](int slot) {
-    auto key = std::make_pair((int)dev.index(), slot);
-    auto it = side_streams.find(key);
-    if (it == side_streams.end())
-      it = side_streams.emplace(key, c10::hip::getStreamFromPool(false, dev.index())).first;
-    return it->second;
-  };
-  // Where to build the operands that depend only on the tokens (sorted token
-  // order for the embedding gradient, gathered input embeddings for dW_ie)
-  // off the critical path?  CSTCAP_BWD_AUX (A/B knob): 0 (default) = on the
-  // main stream after the loop; 1 = on the vocab-head side stream after dHd,
-  // i.e. under the reverse loop (within noise of 0); 2 = on a third stream that also takes the
-  // embedding-gradient GEMM concurrently with the weight GEMMs (measured
-  // 5.21 vs 4.87 ms per step, also with GPU_MAX_HW_QUEUES=8: the two GEMMs
-  // slow each other down more than the overlap saves); 3 = on the main
-  // stream before the reverse loop, under the dS pass (interleaved A/B:
-  // 4.67-4.78 vs 4.76-4.86 ms with one 6.4 ms outlier, kept opt-in).  The
-  // outputs are allocated here on the main stream so their memory is ordered
-  // by it.
-  TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
-  at::Tensor stok = at::empty_like(toks), srow = at::empty_like(toks);
-  at::Tensor x_in = at::empty({n_steps * R, E}, emb.options());     // (n*R, E) bf16
-  // out_emb: the embedding's gradient slot (written directly, zeroed here)
-  const bool emb_direct = out_emb.defined() && out_emb.numel() > 0;
-  if (emb_direct)
-    TORCH_CHECK(out_emb.is_contiguous() && out_emb.scalar_type() == at::kFloat &&
-                    out_emb.size(0) == V && out_emb.size(1) == E,
-                "out_emb must be a contiguous fp32 (V, E) tensor");
-  at::Tensor d_emb = emb_direct ? out_emb : at::empty({V, E}, f32);
-  static const int aux_mode = [] {
-    const char* e = std::getenv("CSTCAP_BWD_AUX");
-    return e ? std::atoi(e) : 0;
-  }();
-  auto main_stream = at::hip::getCurrentHIPStream();
-  auto aux = aux_mode == 2 ? side_stream(1) : main_stream;  // embedding-gradient tail
-  hipEvent_t ev_aux, ev_tail;
-  (void)hipEventCreateWithFlags(&ev_aux, hipEventDisableTiming);
-  (void)hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming);
-  auto token_prep = [&](c10::hip::HIPStream s) {
-    c10::hip::HIPStreamGuard guard(s);
-    at::sort_out(stok, srow, toks);
-    at::index_select_out(x_in, emb, 0, toks);
-    d_emb.zero_();
-    (void)hipEventRecord(ev_aux, s.stream());
-  };
-  if (aux_mode == 2) {
-    (void)hipStreamWaitEvent(aux.stream(), ev_ready, 0);
-    token_prep(aux);
-  } else if (aux_mode == 3) {
-    // main stream, before the reverse loop: it idles there until the first
-    // dHd chunk is ready, so the sort/gather ride under the dS pass instead
-    // of queueing behind the full-chip dW_logit GEMM after the loop
-    token_prep(main_stream);
-  }
+  (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
   {
-    auto side = side_stream(0);
-    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
-    if (fused) {
-      wT.narrow(1, 0, V).copy_(wlog.t());
-      launch_vocab_bwd_dhd(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
-                           (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
-                           has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
-                           has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
-                           has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
-                           has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                           has_xe ? dg_xe.size(1) : 0,
-                           reinterpret_cast<const uint16_t*>(wT.data_ptr()), (int)ldw, (int)H,
-                           n_part, dHd_all.data_ptr<float>(), colsum.data_ptr<float>(),
-                           side.stream());
-      (void)hipEventRecord(ev[0], side.stream());
-    }
-    for (int c = fused ? -1 : n_chunks - 1; c >= 0; --c) {
-      launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
-                          (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
-                          has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
-                          has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
-                          has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
-                          has_xe ? labels.size(1) : 0,
-                          has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                          has_xe ? dg_xe.size(1) : 0, colsum.data_ptr<float>(), cb[c], cb[c + 1],
-                          side.stream());
-      at::Tensor out = dHd.narrow(0, cb[c], cb[c + 1] - cb[c]);
-      at::mm_out(out, dS.narrow(0, cb[c], cb[c + 1] - cb[c]), wlog, at::kFloat);
-      (void)hipEventRecord(ev[c], side.stream());
-    }
-    if (aux_mode == 1) token_prep(side);
+    launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
+                        (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
+                        has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
+                        has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
+                        has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
+                        has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
+                        has_xe ? dg_xe.size(1) : 0, colsum.data_ptr<float>(), 0, NR,
+                        side.stream());
+    at::mm_out(dHd, dS, wlog, at::kFloat);
+    (void)hipEventRecord(ev_dhd, side.stream());
   }
-  // dWlog = dS^T Hd (+ the early bias gradient) on the side stream.  BLAS
-  // fills every CU with it, so run concurrently with the reverse LSTM loop it
-  // delays the loop's first step until it ends; late (CSTCAP_BWD_DWLOG_LATE=1)
-  // enqueues it after the loop instead, beside the weight-gradient tail:
-  // 4.74 vs 4.77 ms per step on one GPU.  Under data parallelism (early
-  // gradients) the default stays concurrent, so the vocab head's all-reduce
-  // still hides under the reverse loop.
-  static const int dwlog_env = [] {
-    const char* e = std::getenv("CSTCAP_BWD_DWLOG_LATE");
-    return e ? std::atoi(e) : -1;
-  }();
-  // direct writes without a communication stream (one GPU) keep the late
-  // schedule: nothing waits on the slots before the optimizer
-  const bool dwlog_late = dwlog_env >= 0 ? dwlog_env != 0 : (!early || comm_stream == 0);
+  // 3. dW_logit = dS^T Hd and the bias gradient (column sums of dS), side stream
+  const bool dwlog_late = !early || comm_stream == 0;
   auto launch_dwlog = [&]() {
-    auto side = side_stream(0);
     c10::hip::HIPStreamGuard guard(side);
     at::mm_out(dWlog, dS.t(), hd2, at::kFloat);
-    if (early) {
-      dblog = out_blog.view({V});
-      at::sum_out(dblog, colsum, {0});
-    }
+    at::sum_out(dblog, colsum, {0});
     (void)hipEventRecord(ev_done, side.stream());
     if (early && comm_stream != 0)
       (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
   };
   if (!dwlog_late) launch_dwlog();
+
+  // 4. reverse LSTM loop on the main stream
   at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
   at::Tensor dc = at::zeros({R, H}, f32);
   // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel; with
@@ -532,33 +408,15 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dwa_part = at::zeros({nwg, A}, f32);
     dba_part = at::zeros({nwg}, f32);
   }
-  // split-K of the fused backward step (CSTCAP_BWD_SPLITK, default 1).  On
-  // MI355X S = 2..4 measured SLOWER (73 vs 29.5 us per step, bench 6.5 vs
-  // 5.0 ms): the reverse loop shares the GPU with the side stream's dWlog
-  // GEMM, and the extra blocks queue behind it instead of filling idle CUs
-  static const int splitk = [] {
-    const char* e = std::getenv("CSTCAP_BWD_SPLITK");
-    return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
-  }();
-  const int64_t n_bt = lstm_bwd_tiles((int)R, (int)H);
-  at::Tensor bwd_ws = splitk > 1 ? at::empty({n_bt * splitk * 64 * 64}, f32) : at::Tensor();
-  at::Tensor bwd_cnt = splitk > 1 ? at::zeros({n_bt}, at::TensorOptions().dtype(at::kInt).device(dev))
-                                  : at::Tensor();
-  int waited = n_chunks;
+  (void)hipStreamWaitEvent(st, ev_dhd, 0);
   for (int64_t t = n_steps - 1; t >= 0; --t) {
-    int need = 0;  // chunk holding the first row of step t (chunks finish high to low)
-    while (need + 1 < n_chunks && cb[need + 1] <= t * R) ++need;
-    while (waited > need) (void)hipStreamWaitEvent(st, ev[--waited], 0);
     launch_lstm_step_bwd(
         t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
         reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dHd.data_ptr<float>() + t * R * H,
         dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
         c_all[t].data_ptr<float>(), t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R,
-        (int)H, (float)drop_p, seed_drop, (int)t,
-        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, splitk,
-        splitk > 1 ? bwd_ws.data_ptr<float>() : nullptr,
-        splitk > 1 ? bwd_cnt.data_ptr<int>() : nullptr,
-        n_part > 1 ? dHd_all[1].data_ptr<float>() + t * R * H : nullptr);
+        (int)H, (float)drop_p, RNG, (int)t, reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()),
+        (int)KD, st);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
@@ -567,18 +425,37 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
                      dba_part.data_ptr<float>(), st);
   }
-  while (waited > 0) (void)hipStreamWaitEvent(st, ev[--waited], 0);
   if (dwlog_late) {
     (void)hipEventRecord(ev_ready, st);  // reverse loop done
-    (void)hipStreamWaitEvent(side_stream(0).stream(), ev_ready, 0);
+    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     launch_dwlog();
   }
-  if (!early) dblog = colsum.sum(0);                                    // (V)
-  // 4. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
+
+  // 5. embedding gradient: rows grouped by input token (counting sort), dX =
+  //    dG W_ie, grouped row sums into d_emb; input-weight gradient from the
+  //    gathered input embeddings
+  const bool emb_direct = out_emb.defined() && out_emb.numel() > 0;
+  if (emb_direct)
+    TORCH_CHECK(out_emb.is_contiguous() && out_emb.scalar_type() == at::kFloat &&
+                    out_emb.size(0) == V && out_emb.size(1) == E,
+                "out_emb must be a contiguous fp32 (V, E) tensor");
+  at::Tensor d_emb = emb_direct ? out_emb : at::empty({V, E}, f32);
+  at::Tensor sort_ws = at::empty({2 * V}, i32);
+  at::Tensor stok = at::empty({NR}, i32), srow = at::empty({NR}, i32);
+  launch_token_sort(toks.data_ptr<int64_t>(), (int)NR, (int)V, sort_ws.data_ptr<int>(),
+                    stok.data_ptr<int>(), srow.data_ptr<int>(), st);
+  at::Tensor x_in = at::index_select(emb, 0, toks);  // (n*R, E) bf16
+  d_emb.zero_();
+  at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
+  at::Tensor dG2 = dGx.narrow(1, 0, H4);
+  {
+    at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);  // (n*R, E)
+    launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int>(),
+                          srow.data_ptr<int>(), (int)NR, d_emb.data_ptr<float>(), st);
+  }
+  // 6. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
   //    reductions run as batched GEMMs over groups of steps (many more output
   //    tiles in flight than one K = 35k GEMM), summed afterwards.
-  at::Tensor dGx = dG_all.view({n_steps * R, KD});  // [dG | dq] rows
-  at::Tensor dG2 = dGx.narrow(1, 0, H4);
   at::Tensor dWx = at::empty({H4, E + H}, f32);
   at::Tensor dWq;
   auto grouped_wgrad = [&](at::Tensor a_rows, at::Tensor b_rows, int64_t nsteps) {
@@ -590,21 +467,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     at::Tensor b = b_rows.reshape({nc, G * R, b_rows.size(1)});
     return at::bmm(a, b, at::kFloat).sum(0);
   };
-  if (aux_mode == 0) token_prep(main_stream);
-  (void)hipStreamWaitEvent(st, ev_aux, 0);
-  // embedding gradient: dX = dG W_ie, then a sorted segmented sum into d_emb
-  // (mode 2: on the third stream, concurrently with the weight GEMMs below;
-  // dX is allocated and consumed on that stream)
-  (void)hipEventRecord(ev_tail, st);
-  (void)hipStreamWaitEvent(aux.stream(), ev_tail, 0);
-  {
-    c10::hip::HIPStreamGuard guard(aux);
-    at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);      // (n*R, E)
-    launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int64_t>(),
-                          srow.data_ptr<int64_t>(), (int)(n_steps * R), d_emb.data_ptr<float>(),
-                          aux.stream());
-    (void)hipEventRecord(ev_aux, aux.stream());
-  }
   dWx.narrow(1, 0, E).copy_(grouped_wgrad(dG2, x_in, n_steps));
   if (n_steps > 1) {
     // with attention the extra rows of [dG | dq]^T h_prev are dW_q
@@ -620,7 +482,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor dvg;
   std::vector<at::Tensor> res;
   if (!has_att) {
-    dvg = dG_all.sum(0, false, at::kFloat);                              // (R, 4H), sum over time
+    dvg = dG_all.sum(0, false, at::kFloat);  // (R, 4H), sum over time
   } else {
     // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r]: one batched GEMM
     // per (step, video), K = rows per video, summed over steps
@@ -631,11 +493,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0),
            dba_part.sum(0).view({1}), dWq};
   }
-  (void)hipStreamWaitEvent(st, ev_done, 0);  // join the side stream (dWlog)
-  (void)hipStreamWaitEvent(st, ev_aux, 0);   // join the embedding-gradient stream
-  for (auto& e : ev) (void)hipEventDestroy(e);
-  (void)hipEventDestroy(ev_aux);
-  (void)hipEventDestroy(ev_tail);
+  // join the side stream (dW_logit): every tensor it touched was allocated
+  // on the main stream and is released after this point
+  (void)hipStreamWaitEvent(st, ev_done, 0);
   std::vector<at::Tensor> out = {dWx, dWlog, dblog, d_emb, dvg};
   out.insert(out.end(), res.begin(), res.end());
   return out;
@@ -661,16 +521,66 @@ at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::stri
   return out;
 }
 
+// Shadow-copy segments from Python: meta = int64 CPU (n, 7) rows {off, n,
+// kind, cols, H, E, ld2}; dsts = 2 tensors per row (dst, dst2; undefined or
+// empty when unused).
+static ShadowSegs make_shadow_segs(const at::Tensor& meta, const std::vector<at::Tensor>& dsts) {
+  ShadowSegs ss{};
+  if (!meta.defined() || meta.numel() == 0) return ss;
+  TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.dim() == 2 &&
+                  meta.size(1) == 7 && meta.size(0) <= SHADOW_MAX_SEGS,
+              "shadow meta must be an int64 CPU (n <= ", SHADOW_MAX_SEGS, ", 7) tensor");
+  TORCH_CHECK((int64_t)dsts.size() == 2 * meta.size(0), "two destination tensors per segment");
+  auto m = meta.accessor<int64_t, 2>();
+  ss.n = (int)meta.size(0);
+  for (int k = 0; k < ss.n; ++k) {
+    ShadowSeg& g = ss.s[k];
+    g.off = m[k][0], g.n = m[k][1], g.kind = (int)m[k][2], g.cols = (int)m[k][3];
+    g.H = (int)m[k][4], g.E = (int)m[k][5], g.ld2 = (int)m[k][6];
+    const at::Tensor& d = dsts[2 * k];
+    const at::Tensor& d2 = dsts[2 * k + 1];
+    TORCH_CHECK(d.is_cuda() && d.scalar_type() == at::kBFloat16, "shadow dst must be bf16 GPU");
+    g.dst = reinterpret_cast<uint16_t*>(d.data_ptr());
+    g.dst2 = d2.defined() && d2.numel() ? reinterpret_cast<uint16_t*>(d2.data_ptr()) : nullptr;
+    if (g.kind == SHADOW_PLAIN) {
+      TORCH_CHECK(d.numel() >= g.n, "plain shadow too small");
+    } else {
+      TORCH_CHECK(g.H > 0 && g.cols > 0 && g.n % g.cols == 0 && g.n / g.cols == 4 * g.H &&
+                      d.numel() >= 4 * (int64_t)g.H * (g.E + g.H),
+                  "LSTM shadow segment shape");
+      if (g.kind == SHADOW_LSTM_HH)
+        TORCH_CHECK(g.dst2 != nullptr && g.cols == g.H && d2.numel() >= 4 * (int64_t)g.H * g.ld2,
+                    "W_hh shadow needs its packed copy");
+    }
+  }
+  return ss;
+}
+
+// hyper (device fp32): [lr, step]; the caller increments step before the call
 at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
-                          at::Tensor partials, at::Tensor scal, at::Tensor skip, double lr,
-                          double b1, double b2, double eps, double clip, double bc1, double bc2) {
+                          at::Tensor partials, at::Tensor scal, at::Tensor skip, at::Tensor hyper,
+                          double b1, double b2, double eps, double clip, at::Tensor shadow_meta,
+                          std::vector<at::Tensor> shadow_dst) {
   check_cuda(p, "p");
   TORCH_CHECK(partials.numel() >= 1024 && scal.numel() >= 2, "workspace too small");
+  TORCH_CHECK(hyper.is_cuda() && hyper.scalar_type() == at::kFloat && hyper.numel() >= 2,
+              "hyper must be fp32 [lr, step] on the GPU");
+  const ShadowSegs ss = make_shadow_segs(shadow_meta, shadow_dst);
+  for (int k = 0; k < ss.n; ++k)
+    TORCH_CHECK(ss.s[k].off >= 0 && ss.s[k].off + ss.s[k].n <= p.numel(), "shadow range");
   launch_flat_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                    v.data_ptr<float>(), p.numel(), partials.data_ptr<float>(),
-                   skip.data_ptr<bool>(), scal.data_ptr<float>(), (float)lr, (float)b1,
-                   (float)b2, (float)eps, (float)clip, (float)bc1, (float)bc2, cur_stream());
+                   skip.data_ptr<bool>(), scal.data_ptr<float>(), hyper.data_ptr<float>(),
+                   (float)b1, (float)b2, (float)eps, (float)clip, ss, cur_stream());
   return scal.narrow(0, 0, 1).squeeze(0);
+}
+
+void refresh_shadows(at::Tensor p, at::Tensor shadow_meta, std::vector<at::Tensor> shadow_dst) {
+  check_cuda(p, "p");
+  const ShadowSegs ss = make_shadow_segs(shadow_meta, shadow_dst);
+  for (int k = 0; k < ss.n; ++k)
+    TORCH_CHECK(ss.s[k].off >= 0 && ss.s[k].off + ss.s[k].n <= p.numel(), "shadow range");
+  launch_shadow_refresh(p.data_ptr<float>(), ss, cur_stream());
 }
 
 // Batched beam search (reference sample_beam, model.py:369-512) for B videos
@@ -685,7 +595,6 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     std::vector<at::Tensor> att) {
   check_cuda(wx, "wx");
   check_cuda(vgate, "vgate");
-  TORCH_CHECK(get_vocab_variant() >= 4, "beam search needs a transposed-epilogue vocab variant");
   TORCH_CHECK(K >= 1 && K <= 16, "beam_size must be in [1, 16]");
   const int64_t H4 = wx.size(0), H = H4 / 4, V = wlog.size(0), B = vgate.size(0), R = B * K;
   TORCH_CHECK(K <= V, "beam_size > vocab_size");
@@ -756,14 +665,14 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                          has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>(),
                          has_att ? 1 : (int)K, (int)R, (int)H, WHH,
                          reinterpret_cast<uint16_t*>(ho.data_ptr()), co.data_ptr<float>(), nullptr,
-                         (int)H, 0.f, 0u, (int)t, nullptr, st,
+                         (int)H, 0.f, nullptr, (int)t, nullptr, st,
                          t >= 1 ? parent.data_ptr<int>() : nullptr);
     launch_vocab_fwd(reinterpret_cast<const uint16_t*>(ho.data_ptr()), (int)H, (int)R, (int)H, W,
                      blog.data_ptr<float>(), (int)V,
                      reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl, part.data_ptr(),
-                     nullptr, 0, /*flags=*/8, 1.f, 0u, (int)t, st);
+                     nullptr, 0, /*flags=*/8, 1.f, nullptr, (int)t, st);
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse.data_ptr<float>(), nullptr, 0,
-                         nullptr, 0, nullptr, 0, nullptr, 0, SEL_GT_H, 0.f, 0u, (int)t, nullptr,
+                         nullptr, 0, nullptr, 0, nullptr, 0, SEL_GT_H, 0.f, nullptr, (int)t, nullptr,
                          0, nullptr, st);
   }
   return {best_seq, best_lp};
@@ -771,24 +680,8 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
 
 // Microbenchmarks of single kernels (scripts/microbench_kernels.py): mean
 // microseconds per launch over `iters` back-to-back launches, HIP events.
-double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
-                       int64_t flags, bool save, int64_t iters) {
-  const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
-  TORCH_CHECK(H % 64 == 0 && wlog.size(1) == H && blog.numel() == V, "shapes");
-  auto dev = hd.device();
-  const int64_t ldl = (V + 7) / 8 * 8;
-  at::Tensor logits = save ? at::empty({R, ldl}, hd.options().dtype(at::kHalf)) : at::Tensor();
-  const int n_vt = vocab_num_tiles((int)V);
-  at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4},
-                              at::TensorOptions().dtype(at::kFloat).device(dev));
-  const int64_t* tg = tgt.defined() && tgt.numel() ? tgt.data_ptr<int64_t>() : nullptr;
-  hipStream_t st = cur_stream();
-  auto launch = [&](int i) {
-    launch_vocab_fwd(reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R, (int)H,
-                     reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
-                     (int)V, save ? reinterpret_cast<uint16_t*>(logits.data_ptr()) : nullptr,
-                     ldl, part.data_ptr(), tg, 1, (int)flags, 1.f, 1234u, i, st);
-  };
+template <class F>
+static double time_launches(F&& launch, int64_t iters, hipStream_t st) {
   launch(0);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
@@ -804,6 +697,30 @@ double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tens
   return 1000.0 * ms / (double)iters;
 }
 
+double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
+                       int64_t flags, bool save, int64_t iters) {
+  const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
+  TORCH_CHECK(H % 64 == 0 && wlog.size(1) == H && blog.numel() == V, "shapes");
+  auto dev = hd.device();
+  const int64_t ldl = (V + 7) / 8 * 8;
+  at::Tensor logits = save ? at::empty({R, ldl}, hd.options().dtype(at::kHalf)) : at::Tensor();
+  const int n_vt = vocab_num_tiles((int)V);
+  at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4},
+                              at::TensorOptions().dtype(at::kFloat).device(dev));
+  at::Tensor rng = at::full({2}, 1234, at::TensorOptions().dtype(at::kInt).device(dev));
+  const int64_t* tg = tgt.defined() && tgt.numel() ? tgt.data_ptr<int64_t>() : nullptr;
+  hipStream_t st = cur_stream();
+  return time_launches(
+      [&](int i) {
+        launch_vocab_fwd(reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R,
+                         (int)H, reinterpret_cast<const uint16_t*>(wlog.data_ptr()),
+                         blog.data_ptr<float>(), (int)V,
+                         save ? reinterpret_cast<uint16_t*>(logits.data_ptr()) : nullptr, ldl,
+                         part.data_ptr(), tg, 1, (int)flags, 1.f, rng_ptr(rng), i, st);
+      },
+      iters, st);
+}
+
 double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
                           int64_t iters) {
   const int64_t n = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
@@ -812,57 +729,41 @@ double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, a
   auto f32 = at::TensorOptions().dtype(at::kFloat).device(logits16.device());
   at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n, (int)R), V}, f32);
   hipStream_t st = cur_stream();
-  auto launch = [&]() {
-    launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
-                        (int)n, (int)T_sel, lse.data_ptr<float>(), seq.data_ptr<int64_t>(), T_sel,
-                        dg_sel.data_ptr<float>(), T_sel, nullptr, 0, nullptr, 0,
-                        colsum.data_ptr<float>(), 0, n * R, st);
-  };
-  launch();
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0);
-  (void)hipEventCreate(&e1);
-  (void)hipEventRecord(e0, st);
-  for (int i = 0; i < iters; ++i) launch();
-  (void)hipEventRecord(e1, st);
-  (void)hipEventSynchronize(e1);
-  float ms = 0.f;
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  return 1000.0 * ms / (double)iters;
+  return time_launches(
+      [&](int) {
+        launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V,
+                            (int)R, (int)n, (int)T_sel, lse.data_ptr<float>(),
+                            seq.data_ptr<int64_t>(), T_sel, dg_sel.data_ptr<float>(), T_sel,
+                            nullptr, 0, nullptr, 0, colsum.data_ptr<float>(), 0, n * R, st);
+      },
+      iters, st);
 }
 
-// fused dS + dHd kernel alone (synthetic RL-shaped inputs), us per launch;
-// dbg = ablation bits of vocab_bwd_dhd_kernel
-double vocab_bwd_dhd_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
-                           at::Tensor wT, int64_t V, int64_t splits, int64_t dbg, int64_t iters) {
-  const int64_t n = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
-  const int64_t T_sel = seq.size(1), H = wT.size(0), NR = n * R;
-  auto f32 = at::TensorOptions().dtype(at::kFloat).device(logits16.device());
-  at::Tensor dhd = at::empty({splits, NR, H}, f32);
-  at::Tensor colsum = at::empty({vocab_bwd_dhd_colsum_rows(NR), V}, f32);
+// counting sort of n token ids < V (the embedding-gradient grouping)
+double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters) {
+  check_cuda(toks, "toks");
+  const int64_t N = toks.numel();
+  auto i32 = at::TensorOptions().dtype(at::kInt).device(toks.device());
+  at::Tensor ws = at::empty({2 * V}, i32), stok = at::empty({N}, i32), srow = at::empty({N}, i32);
   hipStream_t st = cur_stream();
-  auto launch = [&]() {
-    launch_vocab_bwd_dhd(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
-                         (int)n, (int)T_sel, lse.data_ptr<float>(), seq.data_ptr<int64_t>(), T_sel,
-                         dg_sel.data_ptr<float>(), T_sel, nullptr, 0, nullptr, 0,
-                         reinterpret_cast<const uint16_t*>(wT.data_ptr()), (int)wT.size(1), (int)H,
-                         (int)splits, dhd.data_ptr<float>(), colsum.data_ptr<float>(), st, (int)dbg);
-  };
-  launch();
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0);
-  (void)hipEventCreate(&e1);
-  (void)hipEventRecord(e0, st);
-  for (int i = 0; i < iters; ++i) launch();
-  (void)hipEventRecord(e1, st);
-  (void)hipEventSynchronize(e1);
-  float ms = 0.f;
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  return 1000.0 * ms / (double)iters;
+  return time_launches(
+      [&](int) {
+        launch_token_sort(toks.data_ptr<int64_t>(), (int)N, (int)V, ws.data_ptr<int>(),
+                          stok.data_ptr<int>(), srow.data_ptr<int>(), st);
+      },
+      iters, st);
+}
+
+// the counting sort itself, for tests: returns {stok, srow} (int32)
+std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V) {
+  check_cuda(toks, "toks");
+  TORCH_CHECK(toks.scalar_type() == at::kLong, "int64 token ids");
+  const int64_t N = toks.numel();
+  auto i32 = at::TensorOptions().dtype(at::kInt).device(toks.device());
+  at::Tensor ws = at::empty({2 * V}, i32), stok = at::empty({N}, i32), srow = at::empty({N}, i32);
+  launch_token_sort(toks.data_ptr<int64_t>(), (int)N, (int)V, ws.data_ptr<int>(),
+                    stok.data_ptr<int>(), srow.data_ptr<int>(), cur_stream());
+  return {stok, srow};
 }
 
 }  // namespace cst

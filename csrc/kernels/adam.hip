@@ -12,8 +12,19 @@
 //           PyTorch's Adam update with the clipped gradient; an optional
 //           device-side skip flag (non-finite loss) turns the step into a
 //           no-op without a host round trip.
-// Memory-bound: 5 x 4 B read + 3 x 4 B write per parameter.
+// Learning rate and step count are read from device memory (hyper[0] = lr,
+// hyper[1] = step, already incremented), so the bias corrections of a
+// replayed HIP graph follow the live step count and an LR decay between
+// replays needs no re-capture.
+//
+// The update pass also refreshes the bf16 shadow copies of the decoder
+// weights that the MFMA kernels read (ShadowSegs: vocab head, embedding, and
+// the LSTM weights re-packed into the gate-interleaved [W_ie | W_hh] layout),
+// so no separate conversion / cat / gather pass runs after the optimizer.
+// Memory-bound: 5 x 4 B read + 3 x 4 B write per parameter (+ 2 B per
+// shadowed parameter).
 #include "../common.h"
+#include "../launchers.h"
 
 namespace cst {
 
@@ -51,6 +62,41 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_sumsq_kernel(const float* _
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
+// packed gate row of original LSTM weight row g*H + u: 4u + g
+__device__ __forceinline__ int64_t packed_gate_row(int64_t row, int H) {
+  return (row % H) * 4 + row / H;
+}
+
+__device__ __forceinline__ void shadow_store(const ShadowSegs& ss, int64_t e, float val) {
+#pragma unroll
+  for (int k = 0; k < SHADOW_MAX_SEGS; ++k) {
+    if (k >= ss.n) break;
+    const ShadowSeg& g = ss.s[k];
+    const int64_t j = e - g.off;
+    if (j < 0 || j >= g.n) continue;
+    const uint16_t b = f2bf(val);
+    if (g.kind == SHADOW_PLAIN) {
+      g.dst[j] = b;
+    } else {
+      const int64_t row = j / g.cols, col = j - row * g.cols;
+      const int64_t pr = packed_gate_row(row, g.H);
+      if (g.kind == SHADOW_LSTM_IH) {
+        if (col < g.E) g.dst[pr * (g.E + g.H) + col] = b;
+      } else {  // SHADOW_LSTM_HH
+        g.dst[pr * (g.E + g.H) + g.E + col] = b;
+        g.dst2[pr * g.ld2 + col] = b;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* __restrict__ p,
+                                                             ShadowSegs ss, int seg) {
+  const ShadowSeg& g = ss.s[seg];
+  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < g.n; j += (int64_t)gridDim.x * 256)
+    shadow_store(ss, g.off + j, p[g.off + j]);
+}
+
 __device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, float coef,
                                          float lr_bc1, float b1, float b2, float eps,
                                          float inv_sqrt_bc2) {
@@ -64,10 +110,13 @@ __device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, 
 __global__ __launch_bounds__(ADAM_THREADS) void adam_update_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, int64_t n, const float* __restrict__ partials, int nparts,
-    const bool* __restrict__ skip, float* __restrict__ scal, float lr_bc1, float b1, float b2,
-    float eps, float inv_sqrt_bc2, float clip) {
+    const bool* __restrict__ skip, float* __restrict__ scal, const float* __restrict__ hyper,
+    float b1, float b2, float eps, float clip, ShadowSegs ss) {
   __shared__ float sh[ADAM_THREADS / 64];
   __shared__ float s_coef;
+  const float t = hyper[1];
+  const float lr_bc1 = hyper[0] / (1.f - powf(b1, t));
+  const float inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(b2, t));
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += ADAM_THREADS) acc += partials[i];
   const float tot = block_sum(acc, sh);
@@ -98,25 +147,40 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_update_kernel(
     p4[i] = pp;
     m4[i] = mm;
     v4[i] = vv;
+    if (ss.n > 0) {
+      shadow_store(ss, 4 * i, pp.x);
+      shadow_store(ss, 4 * i + 1, pp.y);
+      shadow_store(ss, 4 * i + 2, pp.z);
+      shadow_store(ss, 4 * i + 3, pp.w);
+    }
   }
   if (blockIdx.x == 0) {
-    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += ADAM_THREADS)
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += ADAM_THREADS) {
       adam_one(p[i], m[i], v[i], g[i], coef, lr_bc1, b1, b2, eps, inv_sqrt_bc2);
+      if (ss.n > 0) shadow_store(ss, i, p[i]);
+    }
   }
 }
 
 void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float* partials,
-                      const bool* skip, float* scal, float lr, float b1, float b2, float eps,
-                      float clip, float bc1, float bc2, hipStream_t stream) {
+                      const bool* skip, float* scal, const float* hyper, float b1, float b2,
+                      float eps, float clip, const ShadowSegs& ss, hipStream_t stream) {
   int blocks = (int)std::min<int64_t>(ADAM_MAX_PARTIALS, std::max<int64_t>(1, (n / 4 + 255) / 256));
   hipLaunchKernelGGL(adam_sumsq_kernel, dim3(blocks), dim3(ADAM_THREADS), 0, stream, g, n,
                      partials);
   post_launch("adam_sumsq_kernel", stream);
   int ublocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n / 4 + 255) / 256));
   hipLaunchKernelGGL(adam_update_kernel, dim3(ublocks), dim3(ADAM_THREADS), 0, stream, p, g, m,
-                     v, n, partials, blocks, skip, scal, lr / bc1, b1, b2, eps,
-                     1.f / sqrtf(bc2), clip);
+                     v, n, partials, blocks, skip, scal, hyper, b1, b2, eps, clip, ss);
   post_launch("adam_update_kernel", stream);
+}
+
+void launch_shadow_refresh(const float* p, const ShadowSegs& ss, hipStream_t stream) {
+  for (int k = 0; k < ss.n; ++k) {
+    const int blocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (ss.s[k].n + 255) / 256));
+    hipLaunchKernelGGL(shadow_refresh_kernel, dim3(blocks), dim3(256), 0, stream, p, ss, k);
+    post_launch("shadow_refresh_kernel", stream);
+  }
 }
 
 }  // namespace cst

@@ -41,8 +41,8 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
     const float* __restrict__ vgate, int vgate_div, int R, int H,
     const uint16_t* __restrict__ whh, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
-    uint16_t* __restrict__ hdrop_out, int ldh, float drop_p, uint32_t seed, int step,
-    uint16_t* __restrict__ gates_out, const int* __restrict__ row_map) {
+    uint16_t* __restrict__ hdrop_out, int ldh, float drop_p, const uint32_t* __restrict__ rng,
+    int step, uint16_t* __restrict__ gates_out, const int* __restrict__ row_map) {
   using LTile = Tile<BM, LB_N, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_nt = (4 * H) / LB_N, n_rt = (R + BM - 1) / BM;
@@ -104,6 +104,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
   __syncthreads();
 
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int row = rg + 16 * i, r = r0 + row;
@@ -133,42 +134,6 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
       }
     }
   }
-}
-
-// Cell backward of one step; one thread per (row, hidden unit).
-//   dh = dh_rec + mask * dh_logit / (1 - p)
-//   dc = dc_carry + dh * o * (1 - tanh(c)^2);  dc_carry <- dc * f
-//   dpre = [dc*g*i(1-i), dc*c_prev*f(1-f), dc*i*(1-g^2), dh*tanh(c)*o(1-o)]
-__global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(
-    const float* __restrict__ dh_logit, const float* __restrict__ dh_rec,
-    float* __restrict__ dc_carry, const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
-    const float* __restrict__ c_prev, int R, int H, float drop_p, uint32_t seed, int step,
-    uint16_t* __restrict__ dG) {
-  const int64_t idx = blockIdx.x * 256ll + threadIdx.x;
-  if (idx >= (int64_t)R * H) return;
-  const int r = (int)(idx / H), u = (int)(idx % H);
-  float dh = dh_rec ? dh_rec[idx] : 0.f;
-  if (dh_logit) {
-    const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, u, drop_p);
-    if (keep) dh += dh_logit[idx] * (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
-  }
-  const int64_t go_ = (int64_t)r * 4 * H + 4 * u;
-  const uint2 gp = *reinterpret_cast<const uint2*>(gates + go_);
-  const float4 g4 = make_float4(bf2f(gp.x & 0xffff), bf2f(gp.x >> 16), bf2f(gp.y & 0xffff),
-                                bf2f(gp.y >> 16));
-  const float c = c_t[idx];
-  const float tc = tanhf_(c);
-  const float dc = dc_carry[idx] + dh * g4.w * (1.f - tc * tc);
-  const float cp = c_prev ? c_prev[idx] : 0.f;
-  const float dpi = dc * g4.z * g4.x * (1.f - g4.x);
-  const float dpf = dc * cp * g4.y * (1.f - g4.y);
-  const float dpg = dc * g4.x * (1.f - g4.z * g4.z);
-  const float dpo = dh * tc * g4.w * (1.f - g4.w);
-  dc_carry[idx] = dc * g4.y;
-  uint2 pk;
-  pk.x = (uint32_t)f2bf(dpi) | ((uint32_t)f2bf(dpf) << 16);
-  pk.y = (uint32_t)f2bf(dpg) | ((uint32_t)f2bf(dpo) << 16);
-  *reinterpret_cast<uint2*>(dG + go_) = pk;
 }
 
 // Fused backward step (replaces cell backward + a separate recurrent GEMM):
@@ -213,8 +178,8 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
     const float* __restrict__ dh_logit, const float* __restrict__ dh_logit2,
     float* __restrict__ dc_carry, const uint16_t* __restrict__ gates,
     const float* __restrict__ c_t, const float* __restrict__ c_prev, int R, int H, float drop_p,
-    uint32_t seed, int step, uint16_t* __restrict__ dG, int KD, int S, float* __restrict__ ws,
-    int* __restrict__ tile_cnt) {
+    const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int S,
+    float* __restrict__ ws, int* __restrict__ tile_cnt) {
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ int s_last;
@@ -304,6 +269,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
   }
 
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int row = rg + 4 * i, r = r0 + row;
@@ -332,58 +298,35 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
 
 int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
-template <int BM, int STAGES>
-static void launch_lstm_step_bwd_t(const uint16_t* dg_next, const uint16_t* whhT,
-                                   const float* dh_logit, const float* dh_logit2, float* dc_carry,
-                                   const uint16_t* gates, const float* c_t, const float* c_prev,
-                                   int R, int H, float drop_p, uint32_t seed, int step,
-                                   uint16_t* dG, int KD, int S, float* ws, int* tile_cnt,
-                                   hipStream_t stream) {
-  using TL = Tile<BM, 64, STAGES>;
+void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
+                          float* dc_carry, const uint16_t* gates, const float* c_t,
+                          const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
+                          int step, uint16_t* dG, int KD, hipStream_t stream, int S, float* ws,
+                          int* tile_cnt, const float* dh_logit2) {
+  constexpr int BM = 64;
+  using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, STAGES>,
+    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, LSTM_BWD_STAGES>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, TL::LDS_BYTES);
     attr_set = true;
   }
   if (dg_next == nullptr || ws == nullptr || tile_cnt == nullptr) S = 1;  // no K to split
   const int n = (H / 64) * ((R + BM - 1) / BM) * S;
-  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES>), dim3(n), dim3(256), TL::LDS_BYTES, stream,
-                     dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
-                     drop_p, seed,
-                     step, dG, KD, S, ws, tile_cnt);
+  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, LSTM_BWD_STAGES>), dim3(n), dim3(256),
+                     TL::LDS_BYTES, stream, dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates,
+                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, S, ws, tile_cnt);
   post_launch("lstm_step_bwd_kernel", stream);
 }
 
-void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
-                          float* dc_carry, const uint16_t* gates, const float* c_t,
-                          const float* c_prev, int R, int H, float drop_p, uint32_t seed,
-                          int step, uint16_t* dG, int KD, hipStream_t stream, int S, float* ws,
-                          int* tile_cnt, const float* dh_logit2) {
-  // pipeline depth (A/B knob CSTCAP_BWD_STAGES: 3 or 6 LDS stages)
-  static const int stages = [] {
-    const char* e = std::getenv("CSTCAP_BWD_STAGES");
-    return e && std::atoi(e) >= 6 ? 6 : 3;
-  }();
-  if (stages == 6)
-  launch_lstm_step_bwd_t<64, 6>(dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
-                             drop_p, seed, step, dG, KD, S, ws, tile_cnt, stream);
-  else
-  launch_lstm_step_bwd_t<64, 3>(dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates, c_t, c_prev, R, H,
-                             drop_p, seed, step, dG, KD, S, ws, tile_cnt, stream);
-}
-
-static int g_lstm_fwd_variant = 0;
-void set_lstm_fwd_variant(int v) { g_lstm_fwd_variant = v; }
-
-template <int BM, int STAGES>
-static void launch_lstm_step_fwd_t(const int64_t* tok, int64_t tok_stride, const float* ptab,
-                                   const uint16_t* h_prev, const float* c_prev,
-                                   const float* vgate, int vgate_div, int R, int H,
-                                   const uint16_t* whh, uint16_t* h_out, float* c_out,
-                                   uint16_t* hdrop_out, int ldh, float drop_p, uint32_t seed,
-                                   int step, uint16_t* gates_out, const int* row_map,
-                                   hipStream_t stream) {
+// 128-row tiles x 64 packed gate columns, 3 LDS stages (72 KB, 2 blocks per CU)
+void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
+                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
+                          int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
+                          float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
+                          const uint32_t* rng, int step, uint16_t* gates_out, hipStream_t stream,
+                          const int* row_map) {
+  constexpr int BM = 128, STAGES = 3;
   constexpr int LDS = Tile<BM, LB_N, STAGES>::LDS_BYTES + BM * 4;  // + staged token ids
   const int n_nt = (4 * H) / LB_N, n_rt = (R + BM - 1) / BM;
   static bool attr_set = false;
@@ -394,36 +337,8 @@ static void launch_lstm_step_fwd_t(const int64_t* tok, int64_t tok_stride, const
   }
   hipLaunchKernelGGL((lstm_step_fwd_kernel<BM, STAGES>), dim3(n_nt * n_rt), dim3(256), LDS,
                      stream, tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh,
-                     h_out, c_out, hdrop_out, ldh, drop_p, seed, step, gates_out, row_map);
+                     h_out, c_out, hdrop_out, ldh, drop_p, rng, step, gates_out, row_map);
   post_launch("lstm_step_fwd_kernel", stream);
-}
-
-void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
-                          const uint16_t* h_prev, const float* c_prev, const float* vgate,
-                          int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
-                          float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
-                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream,
-                          const int* row_map) {
-#define LSTM_FWD_ARGS tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh, h_out, \
-    c_out, hdrop_out, ldh, drop_p, seed, step, gates_out, row_map, stream
-  switch (g_lstm_fwd_variant) {
-    case 1: launch_lstm_step_fwd_t<128, 4>(LSTM_FWD_ARGS); break;  // 96 KB, 1 block/CU
-    case 2: launch_lstm_step_fwd_t<64, 4>(LSTM_FWD_ARGS); break;   // 64 KB, 2 blocks/CU
-    case 3: launch_lstm_step_fwd_t<64, 3>(LSTM_FWD_ARGS); break;   // 48 KB, 3 blocks/CU
-    default: launch_lstm_step_fwd_t<128, 3>(LSTM_FWD_ARGS);        // 72 KB, 2 blocks/CU
-  }
-#undef LSTM_FWD_ARGS
-}
-
-void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
-                          const uint16_t* gates, const float* c_t, const float* c_prev, int R,
-                          int H, float drop_p, uint32_t seed, int step, uint16_t* dG,
-                          hipStream_t stream) {
-  const int64_t n = (int64_t)R * H;
-  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     stream, dh_logit, dh_rec, dc_carry, gates, c_t, c_prev, R, H, drop_p, seed,
-                     step, dG);
-  post_launch("lstm_cell_bwd_kernel", stream);
 }
 
 }  // namespace cst

@@ -8,8 +8,10 @@
 // Here one launch computes the logits tile by MFMA and reduces it in the
 // epilogue, so no R x V log-prob tensor is ever formed:
 //
-// vocab_fwd_kernel  (grid: V/128 vocab tiles x R/128 row tiles, XCD-aware)
-//   * C = h_drop(R x H) . W(V x H)^T + b  with v_mfma_f32_32x32x16_bf16;
+// vocab_fwd_tr_kernel / vocab_lstm_fwd_kernel (grid: V/128 vocab tiles x
+// R/128 row tiles, XCD-aware; the latter also carries the next step's
+// recurrent GEMM tiles)
+//   * C^T = W(V x H) . h_drop(R x H)^T + b  with v_mfma_f32_32x32x16_bf16;
 //   * optional fp16 copy of the logits (the backward's softmax input, so
 //     the backward never recomputes the 0.4 TFLOP projection);
 //   * per (row, tile) partials: max, sum(exp(x - max)), a multinomial draw
@@ -17,7 +19,8 @@
 //     the tile over the exp() weights kept in registers, and an exponential
 //     race across tiles (key log(tile mass) - log(E), E ~ Exp(1)) --, both
 //     driven by counter hashes of (seed, step, row, tile), so no per-element
-//     random numbers;
+//     random numbers (the seed is read from device memory, so a replayed
+//     HIP graph draws fresh samples);
 //     greedy argmax, and the logit of the row's target token.
 // vocab_combine_kernel (one wavefront per row)
 //   * merges the tile partials: LSE, sampled / greedy / target token and
@@ -47,8 +50,6 @@ struct VocabPartial {  // 32 bytes per (tile, row)
   float pad;
 };
 
-constexpr int VB_M = 128;
-
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch),
 // so consecutive ids of the remapped index land on the same XCD's L2.  Vocab
 // tiles are the outer index: the 8 XCDs each stream a contiguous 1/8 of W
@@ -59,204 +60,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
-template <int VB_N, int STAGES, int OCC>
-__global__ __launch_bounds__(256, OCC) void vocab_fwd_kernel(
-    const uint16_t* __restrict__ hd, int ldh, int R, int H, const uint16_t* __restrict__ W,
-    const float* __restrict__ bias, int V, uint16_t* __restrict__ logits16, int64_t ldl,
-    VocabPartial* __restrict__ part, const int64_t* __restrict__ tgt, int64_t tgt_stride,
-    int do_sample, float inv_temp, uint32_t seed, int step) {
-  using VTile = Tile<VB_M, VB_N, STAGES>;
-  constexpr int NG = VB_N / 8;  // 4-column groups per thread (2 threads per row)
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int n_vt = (V + VB_N - 1) / VB_N, n_rt = (R + VB_M - 1) / VB_M;
-  const int b = xcd_remap(blockIdx.x, n_vt * n_rt);
-  const int vt = b / n_rt, rt = b % n_rt;
-  const int r0 = rt * VB_M, v0 = vt * VB_N;
-  const int nk = H / 64;
-
-  // epilogue operands prefetched before the main loop (latency hides under it)
-  float pre_bias[VTile::TN];
-  {
-    const int lane = threadIdx.x & 63, wc = (threadIdx.x >> 6) & 1;
-#pragma unroll
-    for (int j = 0; j < VTile::TN; ++j) {
-      const int v = v0 + wc * VTile::WN + j * 32 + (lane & 31);
-      pre_bias[j] = v < V ? bias[v] : 0.f;
-    }
-  }
-  const int target = tgt != nullptr
-                         ? (int)tgt[(int64_t)min(r0 + (int)(threadIdx.x >> 1), R - 1) * tgt_stride]
-                         : -1;
-
-  f32x16 acc[VTile::TM][VTile::TN];
-  {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    DmaSrc<VB_M / 32> a;
-    DmaSrc<VB_N / 32> bsrc;
-    a.r0 = a.r1 = make_rsrc(hd, (int64_t)R * ldh * 2);
-    a.ksplit = nk;
-#pragma unroll
-    for (int i = 0; i < VB_M / 32; ++i) {
-      const int row = dma_row(w, i, lane);
-      a.voff0[i] = min(r0 + row, R - 1) * ldh * 2 + dma_chunk(row, lane) * 16;
-      a.voff1[i] = a.voff0[i];
-    }
-    bsrc.r0 = bsrc.r1 = make_rsrc(W, (int64_t)V * H * 2);
-    bsrc.ksplit = nk;
-#pragma unroll
-    for (int i = 0; i < VB_N / 32; ++i) {
-      const int row = dma_row(w, i, lane);
-      bsrc.voff0[i] = min(v0 + row, V - 1) * H * 2 + dma_chunk(row, lane) * 16;
-      bsrc.voff1[i] = bsrc.voff0[i];
-    }
-    gemm_nt_mainloop<VTile>(nk, a, bsrc, lds, acc);
-  }
-
-  float* C = reinterpret_cast<float*>(lds);
-  store_acc_to_lds<VTile>(acc, C, [&](int col) {
-    return pre_bias[(col % VTile::WN) / 32];  // col = wc*WN + j*32 + lane%32
-  });
-  __syncthreads();
-  const int tid = threadIdx.x;
-
-  // (a) fp16 logits: lane l of a wave stores columns 4(l&31)..+3 of one row
-  //     (32 lanes = one 256-byte row segment, coalesced); each 16-lane group
-  //     reads 256 contiguous LDS bytes (bank-conflict free).
-  if (logits16 != nullptr) {
-    constexpr int LPR = VB_N / 4;  // lanes per row
-#pragma unroll 4
-    for (int i = 0; i < (VB_M * VB_N / 4) / 256; ++i) {
-      const int idx = tid + i * 256, row = idx / LPR, c4 = (idx % LPR) * 4;
-      const int r = r0 + row, v = v0 + c4;
-      if (r < R && v < V) {
-        const float4 x = *reinterpret_cast<const float4*>(C + row * VTile::CSTRIDE + c4);
-        uint16_t* dst = logits16 + (int64_t)r * ldl + v;
-        if (v + 4 <= V) {
-          uint2 pk;
-          pk.x = (uint32_t)f2h(x.x) | ((uint32_t)f2h(x.y) << 16);
-          pk.y = (uint32_t)f2h(x.z) | ((uint32_t)f2h(x.w) << 16);
-          *reinterpret_cast<uint2*>(dst) = pk;
-        } else {
-          const float xs[4] = {x.x, x.y, x.z, x.w};
-          for (int e = 0; e < V - v; ++e) dst[e] = f2h(xs[e]);
-        }
-      }
-    }
-  }
-
-  // (b) per-row statistics: 2 threads per row (adjacent lanes), interleaved
-  //     4-column groups (thread h owns groups 2j+h).
-  const int row = tid >> 1, h = tid & 1;
-  const int r = r0 + row;
-  const int rr = min(r, R - 1);
-  const float* Crow = C + row * VTile::CSTRIDE;
-  // pass 1: max and first argmax
-  float m = -INFINITY;
-  int xidx = 0x7fffffff;
-#pragma unroll
-  for (int j = 0; j < NG; ++j) {
-    const int c0 = 4 * (2 * j + h);
-    const float4 x = *reinterpret_cast<const float4*>(Crow + c0);
-    const int v = v0 + c0;
-    const float xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (v + e < V && xs[e] > m) {
-        m = xs[e];
-        xidx = v + e;
-      }
-  }
-  {
-    const float m2 = __shfl_xor(m, 1, 64);
-    const int xi2 = __shfl_xor(xidx, 1, 64);
-    if (m2 > m || (m2 == m && xi2 < xidx)) xidx = xi2;
-    m = fmaxf(m, m2);  // row max of the tile, shared by both threads
-  }
-  // pass 2: exp weights kept in registers; softmax sum; target logit
-  const bool temp1 = inv_temp == 1.f;
-  float ev[NG][4];
-  float s = 0.f, sw = 0.f, xtgt = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < NG; ++j) {
-    const int c0 = 4 * (2 * j + h);
-    const float4 x = *reinterpret_cast<const float4*>(Crow + c0);
-    const int v = v0 + c0;
-    const float xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bool ok = v + e < V;
-      const float ex = ok ? __expf(xs[e] - m) : 0.f;
-      s += ex;
-      if (v + e == target) xtgt = xs[e];
-      const float wv = (temp1 || !ok) ? ex : __expf((xs[e] - m) * inv_temp);
-      ev[j][e] = wv;
-      sw += wv;
-    }
-  }
-  const float s_other = __shfl_xor(s, 1, 64);
-  const float sw_other = __shfl_xor(sw, 1, 64);
-  const float S = s + s_other;
-  // pass 3 (sampling): exact two-level multinomial draw.  Within the tile:
-  // inverse CDF over the register-resident weights (thread 0's columns first);
-  // across tiles (in the combine): exponential race with key
-  // z = m/temp + log(sum_w) - log(E),  E ~ Exp(1)  => tile chosen w.p. ~ mass.
-  float zval = -INFINITY, zlogit = 0.f;
-  int zidx = 0x7fffffff;
-  if (do_sample) {
-    const uint32_t key = mix32(seed ^ mix32((uint32_t)rr * 0x9E3779B1u + (uint32_t)step * 0x85EBCA77u) ^
-                               (uint32_t)vt * 0xC2B2AE3Du);
-    const float u = ((float)(key >> 8) + 0.5f) * (1.0f / 16777216.0f);
-    const float sw0 = h == 0 ? sw : sw_other;  // thread 0's mass
-    const float tot = sw + sw_other;
-    float tgt_mass = u * tot - (h == 0 ? 0.f : sw0);
-    int cand = -1;
-    float cum = 0.f;
-    int last = -1;
-#pragma unroll
-    for (int j = 0; j < NG; ++j) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int v = v0 + 4 * (2 * j + h) + e;
-        if (v < V) {
-          cum += ev[j][e];
-          last = v;
-          if (cand < 0 && cum > tgt_mass) cand = v;
-        }
-      }
-    }
-    // thread 0 wins if the target falls in its mass; rounding: fall back to last
-    const bool mine = (h == 0) ? (u * tot < sw0) : !(u * tot < sw0);
-    const int pick = cand >= 0 ? cand : last;
-    const int pick2 = __shfl_xor(pick, 1, 64);
-    const int chosen = mine ? pick : pick2;
-    const uint32_t key2 = mix32(key ^ 0x68E31DA4u);
-    const float u2 = ((float)(key2 >> 8) + 0.5f) * (1.0f / 16777216.0f);
-    zidx = chosen;
-    zval = (tot > 0.f && chosen >= 0) ? m * inv_temp + __logf(tot) - __logf(-__logf(u2))
-                                      : -INFINITY;
-  }
-  // logit of the sampled token: read it back from the C tile (a row's two
-  // threads agree on zidx)
-  if (do_sample && zidx >= v0 && zidx < v0 + VB_N) zlogit = Crow[zidx - v0];
-  {
-    const float xt2 = __shfl_xor(xtgt, 1, 64);
-    if (h == 0 && r < R) {
-      VocabPartial p;
-      p.m = m;
-      p.s = S;
-      p.zval = zval;
-      p.zlogit = zlogit;
-      p.zidx = zidx;
-      p.xidx = xidx;
-      p.xtgt = fmaxf(xtgt, xt2);
-      p.pad = 0.f;
-      part[(int64_t)vt * R + r] = p;
-    }
-  }
-}
-
 // -------------------------------------------------------------------------------
-// Transposed-epilogue variant: the MFMA computes C^T = W . h_drop^T (vocab rows
+// Transposed epilogue: the MFMA computes C^T = W . h_drop^T (vocab rows
 // as the M operand, caption rows as N).  In the 32x32 MFMA output layout lane l
 // then holds, for caption row (l & 31) of each 32-row sub-tile, 16 vocabulary
 // entries per 32-vocab sub-tile: the lane's 32 (TM = 2) logits of one row sit
@@ -283,9 +88,9 @@ struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS
   const uint16_t *__restrict__ hd, int ldh, int R, int H, const uint16_t *__restrict__ W,    \
       const float *__restrict__ bias, int V, uint16_t *__restrict__ logits16, int64_t ldl,   \
       VocabPartial *__restrict__ part, const int64_t *__restrict__ tgt, int64_t tgt_stride, \
-      int flags, float inv_temp, uint32_t seed, int step
+      int flags, float inv_temp, const uint32_t *__restrict__ rng, int step
 #define VOCAB_TR_ARGS \
-  hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, seed, step
+  hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, rng, step
 
 template <int BN, int STAGES>
 __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARAMS) {
@@ -453,6 +258,7 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
           for (int k = 0; k < 16; ++k) sw += __builtin_amdgcn_exp2f(fmaf(x[i][k], wsc, -wl));
       }
       const uint32_t rr = (uint32_t)min(r, R - 1);
+      const uint32_t seed = rng_seed(rng, RNG_SLOT_SAMPLE);
       const uint32_t key = mix32(seed ^ mix32(rr * 0x9E3779B1u + (uint32_t)step * 0x85EBCA77u) ^
                                  (uint32_t)(vt * 4 + g) * 0xC2B2AE3Du);
       const float u = ((float)(key >> 8) + 0.5f) * (1.0f / 16777216.0f);
@@ -569,7 +375,6 @@ struct CellArgs {
   uint16_t* gates_out;  // nullable (training: saved for the backward)
   int H;
   float drop_p;
-  uint32_t seed;
   int step;  // decode step of the cell (dropout mask index)
 };
 
@@ -601,7 +406,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     int64_t* __restrict__ tok_out, int64_t tok_stride, float* __restrict__ g_sel,
     int64_t gsel_stride, float* __restrict__ g_xe, int64_t gxe_stride,
     const int64_t* __restrict__ gt, int64_t gt_stride, int mode, float ss_prob,
-    uint32_t seed, int step, int* __restrict__ counts, int count_step,
+    const uint32_t* __restrict__ rng, int step, int* __restrict__ counts, int count_step,
     uint8_t* __restrict__ unfinished, CellArgs cell) {
   __shared__ int s_nonzero;
   int tok_final = 0;
@@ -677,7 +482,8 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
         case SEL_SAMPLE: tok = a.zi; tl = a.zl; break;
         case SEL_GREEDY: tok = a.xi; tl = a.xm; break;
         case SEL_SS: {
-          const u32x4 u = philox4x32({(uint32_t)r, RNG_SS, (uint32_t)step, 0u}, seed, 0x68E31DA4u);
+          const u32x4 u = philox4x32({(uint32_t)r, RNG_SS, (uint32_t)step, 0u},
+                                     rng_seed(rng, RNG_SLOT_SAMPLE), 0x68E31DA4u);
           const bool use_sample = u01(u.x) < ss_prob;
           tok = use_sample ? (int64_t)a.zi : gt_tok;
           tl = use_sample ? a.zl : a.xt;
@@ -712,6 +518,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
       const float* prow = cell.pre + (int64_t)r * 4 * H;
       const float* trow = cell.ptab + (int64_t)tk * 4 * H;
       const float inv_keep = cell.drop_p > 0.f ? 1.f / (1.f - cell.drop_p) : 1.f;
+      const uint32_t dseed = rng_seed(rng, RNG_SLOT_DROPOUT);
       // batches of CELL_U units (all of H = 512 in one): every load of a
       // batch is issued before the first store (the stores could alias the
       // inputs as far as the compiler knows, which would serialise the loads)
@@ -741,7 +548,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
             cell.h_out[o] = f2bf(hv);
             if (cell.hdrop_out) {
               const bool keep =
-                  cell.drop_p <= 0.f || dropout_keep(cell.seed, cell.step, r, u, cell.drop_p);
+                  cell.drop_p <= 0.f || dropout_keep(dseed, cell.step, r, u, cell.drop_p);
               cell.hdrop_out[(int64_t)r * cell.ldh + u] = f2bf(keep ? hv * inv_keep : 0.f);
             }
             if (cell.gates_out) {
@@ -764,11 +571,14 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   }
 }
 
-// DS_ROWS rows of the [T*R][ldl] buffer per block.  Each thread owns the same
-// 8-column chunks in every row, so the bias gradient (column sums of dS) is
-// accumulated in registers and written once per block as a partial row.  The
-// per-row scalars are staged in LDS up front (no dependent scalar loads in
-// the row loop); NCH = chunks per thread is a compile-time constant.
+// DS_ROWS rows of the [T*R][ldl] buffer per block; the 8-column chunks of a
+// row are split over gridDim.y blocks (column split), so the grid has enough
+// blocks to keep HBM busy (560 row blocks alone left the CUs at ~2 waves
+// each) without adding bias-gradient partial rows.  Each thread owns the same
+// chunks in every row, so the bias gradient (column sums of dS) is
+// accumulated in registers and written once per block.  The per-row scalars
+// are staged in LDS up front; NCH = chunks per thread is a compile-time
+// constant.
 constexpr int DS_ROWS = 64, DS_MAXCH = 8;  // V <= DS_MAXCH * 2048
 
 template <int NCH>
@@ -781,6 +591,10 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
   const int64_t row0 = row_begin + (int64_t)blockIdx.x * DS_ROWS;
   const int64_t blk = row0 / DS_ROWS;  // global block index (row_begin % DS_ROWS == 0)
   const int nvec = V >> 3;
+  // this block's chunk range [c_lo, c_hi) of the row
+  const int per = (nvec + gridDim.y - 1) / gridDim.y;
+  const int c_lo = blockIdx.y * per, c_hi = min(nvec, c_lo + per);
+  const bool tail_blk = blockIdx.y == gridDim.y - 1;
   const int nr = (int)min((int64_t)DS_ROWS, row_end - row0);
   __shared__ float s_a[DS_ROWS], s_b[DS_ROWS], s_L[DS_ROWS];
   __shared__ int s_ys[DS_ROWS], s_yx[DS_ROWS];
@@ -806,12 +620,17 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
     const int ys = s_ys[rr], yx = s_yx[rr];
     const float ab = a + bb;
     uint16_t* row = buf + rowid * ldl;
+    uint4 xv[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {  // the row's loads in flight together
+      const int i = c_lo + threadIdx.x + c * 256;
+      if (i < c_hi) xv[c] = *reinterpret_cast<const uint4*>(row + i * 8);
+    }
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int i = threadIdx.x + c * 256;
-      if (i < nvec) {
-        uint4 x = *reinterpret_cast<const uint4*>(row + i * 8);
-        uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+      const int i = c_lo + threadIdx.x + c * 256;
+      if (i < c_hi) {
+        uint32_t ws[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int v = i * 8 + 2 * k;
@@ -827,7 +646,7 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
         *reinterpret_cast<uint4*>(row + i * 8) = make_uint4(ws[0], ws[1], ws[2], ws[3]);
       }
     }
-    if (threadIdx.x < (V & 7)) {  // ragged tail columns
+    if (tail_blk && threadIdx.x < (V & 7)) {  // ragged tail columns
       const int v = (nvec << 3) + threadIdx.x;
       const float d = -ab * __expf(h2f(row[v]) - L) + (v == ys ? a : 0.f) + (v == yx ? bb : 0.f);
       row[v] = f2bf(d);  // column sum added after the row loop
@@ -836,14 +655,14 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
   float* out = colsum_part + blk * V;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int i = threadIdx.x + c * 256;
-    if (i < nvec) {
+    const int i = c_lo + threadIdx.x + c * 256;
+    if (i < c_hi) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) out[i * 8 + k] = cs[c][k];  // row stride V: unaligned
     }
   }
   // tail columns: re-sum from the (already converted) buffer
-  if (threadIdx.x < (V & 7)) {
+  if (tail_blk && threadIdx.x < (V & 7)) {
     const int v = (nvec << 3) + threadIdx.x;
     float acc = 0.f;
     for (int rr = 0; rr < nr; ++rr) acc += bf2f(buf[(row0 + rr) * ldl + v]);
@@ -852,39 +671,15 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
 }
 
 // -------------------------------------------------------------------------------
-// Tile-shape variants (A/B-tested on MI355X, see profiles/); the partial
-// record layout depends on the vocab tile width, so the choice is global.
-static int g_vocab_variant = 4;  // transposed epilogue (fastest on MI355X, profiles/)
-void set_vocab_variant(int v) { g_vocab_variant = v; }
-int get_vocab_variant() { return g_vocab_variant; }
-static int vocab_bn() { return g_vocab_variant == 1 || g_vocab_variant == 3 ? 64 : 128; }
-static bool vocab_tr() { return g_vocab_variant >= 4; }
-
-template <int BN, int STAGES, int OCC>
-static void launch_vocab_fwd_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
-                               const float* bias, int V, uint16_t* logits16, int64_t ldl,
-                               void* part, const int64_t* tgt, int64_t tgt_stride,
-                               int do_sample, float inv_temp, uint32_t seed, int step,
-                               hipStream_t stream) {
-  using TL = Tile<VB_M, BN, STAGES>;
-  const int n_vt = (V + BN - 1) / BN, n_rt = (R + VB_M - 1) / VB_M;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_fwd_kernel<BN, STAGES, OCC>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, TL::LDS_BYTES);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((vocab_fwd_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256),
-                     TL::LDS_BYTES, stream, hd, ldh, R, H, W, bias, V, logits16, ldl,
-                     (VocabPartial*)part, tgt, tgt_stride, do_sample, inv_temp, seed, step);
-  post_launch("vocab_fwd_kernel", stream);
-}
-
+// Launchers.  Tiles: 128 vocab x 128 caption rows, 2 LDS stages (64 KB, 2
+// blocks per CU); 64-row tiles when there are only 64 rows (the greedy
+// baseline decodes one row per video).
 template <int BN, int STAGES, int OCC>
 static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
-                                float inv_temp, uint32_t seed, int step, hipStream_t stream) {
+                                float inv_temp, const uint32_t* rng, int step,
+                                hipStream_t stream) {
   using TL = Tile<VT_V, BN, STAGES>;
   constexpr int LDS = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
                           ? TL::STAGES * TL::STAGE_BYTES
@@ -898,75 +693,40 @@ static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const
   }
   hipLaunchKernelGGL((vocab_fwd_tr_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256), LDS,
                      stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt,
-                     tgt_stride, flags, inv_temp, seed, step);
+                     tgt_stride, flags, inv_temp, rng, step);
   post_launch("vocab_fwd_tr_kernel", stream);
 }
 
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                       const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                       const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
-                      uint32_t seed, int step, hipStream_t stream) {
-  const int do_sample = flags & VF_SAMPLE;
-  switch (g_vocab_variant) {
-    case 4:  // transposed epilogue, 128 vocab x 128 rows, 2 stages (64 KB, 2 blocks/CU);
-             // 64-row tiles when there are only 64 rows (greedy baseline: one per video)
-      if (R <= 64)
-        launch_vocab_fwd_tr<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                      tgt_stride, flags, inv_temp, seed, step, stream);
-      else
-        launch_vocab_fwd_tr<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                       tgt_stride, flags, inv_temp, seed, step, stream);
-      break;
-    case 5:  // transposed epilogue, 128 vocab x 64 rows, 3 stages (72 KB, 2 blocks/CU)
-      launch_vocab_fwd_tr<64, 3, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                    tgt_stride, flags, inv_temp, seed, step, stream);
-      break;
-    case 6:  // transposed epilogue, 128 vocab x 64 rows, 2 stages (48 KB)
-      launch_vocab_fwd_tr<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                    tgt_stride, flags, inv_temp, seed, step, stream);
-      break;
-    case 7:  // transposed epilogue, 128 x 128, 3 stages (96 KB, 1 block/CU)
-      launch_vocab_fwd_tr<128, 3, 1>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                     tgt_stride, flags, inv_temp, seed, step, stream);
-      break;
-    case 1:  // 128x64 tile, 3 stages (72 KB LDS, 2 blocks/CU)
-      launch_vocab_fwd_t<64, 3, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                   tgt_stride, do_sample, inv_temp, seed, step, stream);
-      break;
-    case 2:  // 128x128 tile, 3 stages (96 KB LDS, 1 block/CU)
-      launch_vocab_fwd_t<128, 3, 1>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                    tgt_stride, do_sample, inv_temp, seed, step, stream);
-      break;
-    case 3:  // 128x64 tile, 2 stages
-      launch_vocab_fwd_t<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                   tgt_stride, do_sample, inv_temp, seed, step, stream);
-      break;
-    default:  // 128x128 tile, 2 stages (70 KB LDS incl. C tile, 2 blocks/CU)
-      launch_vocab_fwd_t<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                    tgt_stride, do_sample, inv_temp, seed, step, stream);
-  }
+                      const uint32_t* rng, int step, hipStream_t stream) {
+  if (R <= 64)
+    launch_vocab_fwd_tr<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
+                                  flags, inv_temp, rng, step, stream);
+  else
+    launch_vocab_fwd_tr<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                   tgt_stride, flags, inv_temp, rng, step, stream);
 }
 
-int vocab_num_tiles(int V) {
-  const int bn = vocab_tr() ? VT_V : vocab_bn();
-  return (V + bn - 1) / bn;
-}
+int vocab_num_tiles(int V) { return (V + VT_V - 1) / VT_V; }
 int vocab_partial_bytes() { return (int)sizeof(VocabPartial); }
 
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
-                          float ss_prob, uint32_t seed, int step, int* counts, int count_step,
-                          uint8_t* unfinished, hipStream_t stream, const CellLaunch* cl) {
+                          float ss_prob, const uint32_t* rng, int step, int* counts,
+                          int count_step, uint8_t* unfinished, hipStream_t stream,
+                          const CellLaunch* cl) {
   CellArgs cell{};
   if (cl != nullptr) {
     cell = CellArgs{cl->pre, cl->ptab, cl->c_prev, cl->c_out, cl->h_out, cl->hdrop_out,
-                    cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->seed, cl->step};
+                    cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step};
   }
   hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + CMB_ROWS - 1) / CMB_ROWS), dim3(CMB_THREADS), 0,
                      stream,
                      (const VocabPartial*)part, n_vt, R, lse_out, tok_out, tok_stride, g_sel,
-                     gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode, ss_prob, seed, step,
+                     gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode, ss_prob, rng, step,
                      counts, count_step, unfinished, cell);
   post_launch("vocab_combine_kernel", stream);
 }
@@ -975,7 +735,7 @@ template <int BN, int STAGES, int OCC>
 static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
-                                float inv_temp, uint32_t seed, int step, const uint16_t* h_t,
+                                float inv_temp, const uint32_t* rng, int step, const uint16_t* h_t,
                                 const uint16_t* whh, const float* vgate, int vdiv, float* pre,
                                 int NQ, float* q_out, hipStream_t stream) {
   using TL = Tile<VT_V, BN, STAGES>;
@@ -993,7 +753,7 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   }
   hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC>), dim3(n_l + n_vt * n_rt), dim3(256),
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
-                     tgt, tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, n_l,
+                     tgt, tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate, vdiv, pre, n_l,
                      NQ, q_out);
   post_launch("vocab_lstm_fwd_kernel", stream);
 }
@@ -1001,16 +761,16 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
 void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                            const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
-                           uint32_t seed, int step, const uint16_t* h_t, const uint16_t* whh,
+                           const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
                            float* q_out) {
   if (R <= 64)
     launch_vocab_lstm_t<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
-                                  flags, inv_temp, seed, step, h_t, whh, vgate, vdiv, pre, NQ,
+                                  flags, inv_temp, rng, step, h_t, whh, vgate, vdiv, pre, NQ,
                                   q_out, stream);
   else
     launch_vocab_lstm_t<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                   tgt_stride, flags, inv_temp, seed, step, h_t, whh, vgate, vdiv,
+                                   tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate, vdiv,
                                    pre, NQ, q_out, stream);
 }
 
@@ -1024,11 +784,15 @@ void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_
                          int64_t row_begin, int64_t row_end, hipStream_t stream) {
   if (row_end <= row_begin) return;
   const int nb = (int)((row_end - row_begin + DS_ROWS - 1) / DS_ROWS);
-  const int nch = ((V >> 3) + 255) / 256;
+  const int nvec = V >> 3;
+  // column split: >= ~6 blocks per CU (256 CUs), each thread >= 1 chunk
+  int split = 1;
+  while (split < 4 && nb * split < 1536 && (nvec + 2 * split - 1) / (2 * split) >= 256) split *= 2;
+  const int nch = ((nvec + split - 1) / split + 255) / 256;
 #define DS_LAUNCH(N)                                                                          \
-  hipLaunchKernelGGL(vocab_bwd_ds_kernel<N>, dim3(nb), dim3(256), 0, stream, buf, ldl, V, R, T, \
-                     T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe, yxe_rs, dg_xe, dgxe_rs, \
-                     colsum_part, row_begin, row_end)
+  hipLaunchKernelGGL(vocab_bwd_ds_kernel<N>, dim3(nb, split), dim3(256), 0, stream, buf, ldl, V, \
+                     R, T, T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe, yxe_rs, dg_xe,    \
+                     dgxe_rs, colsum_part, row_begin, row_end)
   switch (nch) {
     case 1: DS_LAUNCH(1); break;
     case 2: DS_LAUNCH(2); break;

@@ -15,20 +15,38 @@ void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
                     hipStream_t stream);
 
 // adam.hip
+// bf16 shadow copies of decoder weights written by the optimizer pass
+enum ShadowKind : int { SHADOW_PLAIN = 0, SHADOW_LSTM_IH = 1, SHADOW_LSTM_HH = 2 };
+constexpr int SHADOW_MAX_SEGS = 6;
+struct ShadowSeg {
+  int64_t off, n;   // range of the flat parameter buffer
+  int kind;         // ShadowKind
+  int cols;         // row length of the source matrix (LSTM kinds)
+  int H, E;         // LSTM sizes: packed wx is (4H, E + H)
+  uint16_t* dst;    // PLAIN: dst[j]; LSTM kinds: packed wx
+  uint16_t* dst2;   // LSTM_HH: packed W_hh copy (row stride ld2)
+  int ld2;
+};
+struct ShadowSegs {
+  ShadowSeg s[SHADOW_MAX_SEGS];
+  int n;
+};
+// hyper (device): [lr, step]; the step must already count this update
 void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float* partials,
-                      const bool* skip, float* scal, float lr, float b1, float b2, float eps,
-                      float clip, float bc1, float bc2, hipStream_t stream);
+                      const bool* skip, float* scal, const float* hyper, float b1, float b2,
+                      float eps, float clip, const ShadowSegs& ss, hipStream_t stream);
+void launch_shadow_refresh(const float* p, const ShadowSegs& ss, hipStream_t stream);
 
 // vocab.hip
 enum SelModeHost : int { SEL_GT_H = 0, SEL_SAMPLE_H = 1, SEL_GREEDY_H = 2, SEL_SS_H = 3 };
 int vocab_num_tiles(int V);
-void set_vocab_variant(int v);
 int vocab_partial_bytes();
+// rng (device, nullable): int32[2] seeds {dropout, sampling}, see common.h
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                       const float* bias,
                       int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
-                      int64_t tgt_stride, int flags, float inv_temp, uint32_t seed, int step,
-                      hipStream_t stream);  // flags: 1 = sample, 2 = argmax
+                      int64_t tgt_stride, int flags, float inv_temp, const uint32_t* rng,
+                      int step, hipStream_t stream);  // flags: 1 = sample, 2 = argmax, 8 = fp32 logits
 // Cell epilogue of the next step, fused into the combine (see lstm_gemm.h).
 struct CellLaunch {
   const float* pre;
@@ -41,7 +59,6 @@ struct CellLaunch {
   uint16_t* gates_out;
   int H;
   float drop_p;
-  uint32_t seed;
   int step;
 };
 // size of the end-of-sequence flag area per decode step (ints) of `counts`
@@ -49,7 +66,7 @@ int combine_count_ints_per_step();
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
-                          float ss_prob, uint32_t seed, int step, int* counts, int count_step,
+                          float ss_prob, const uint32_t* rng, int step, int* counts, int count_step,
                           uint8_t* unfinished, hipStream_t stream, const CellLaunch* cell = nullptr);
 // vocab projection of step t + recurrent GEMM of step t+1 in one launch
 // (transposed-epilogue vocab kernel; pre == nullptr: vocab only).  NQ > 0:
@@ -58,7 +75,7 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
 void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                            const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
-                           uint32_t seed, int step, const uint16_t* h_t, const uint16_t* whh,
+                           const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream,
                            int NQ = 0, float* q_out = nullptr);
 int vocab_bwd_ds_blocks(int T, int R);
@@ -69,31 +86,14 @@ void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_
                          int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
                          int64_t row_begin, int64_t row_end, hipStream_t stream);
 int vocab_bwd_ds_rows();
-// fused dS + dHd (vocab_bwd.hip): H == 512; wT = W_logit^T (H x ldw bf16,
-// zero-padded, ldw % vocab_bwd_dhd_kpad() == 0); dhd = splits partials of
-// (T*R, H) fp32; colsum = (vocab_bwd_dhd_colsum_rows(T*R), V) bias-gradient partials
-int vocab_bwd_dhd_mblocks(int64_t NR);
-int vocab_bwd_dhd_colsum_rows(int64_t NR);  // rows of the colsum partial buffer
-int vocab_bwd_dhd_kpad();
-void launch_vocab_bwd_dhd(uint16_t* logits, int64_t ldl, int V, int R, int T, int T_sel,
-                          const float* lse, const int64_t* y_sel, int64_t ysel_rs,
-                          const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
-                          int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, const uint16_t* wT,
-                          int ldw, int H, int splits, float* dhd, float* colsum,
-                          hipStream_t stream, int dbg = 0);
 
 // lstm.hip
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
                           const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
-                          uint32_t seed, int step, uint16_t* gates_out, hipStream_t stream,
+                          const uint32_t* rng, int step, uint16_t* gates_out, hipStream_t stream,
                           const int* row_map = nullptr);  // row_map: h/c source row (beam)
-void set_lstm_fwd_variant(int v);
-void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_carry,
-                          const uint16_t* gates, const float* c_t, const float* c_prev, int R,
-                          int H, float drop_p, uint32_t seed, int step, uint16_t* dG,
-                          hipStream_t stream);
 
 // dg_next / dG rows have stride KD: 4H gate columns (+ A attention-query
 // columns, matched by extra whhT columns [W_hh^T | W_q^T] of width KD)
@@ -102,7 +102,7 @@ void launch_lstm_cell_bwd(const float* dh_logit, const float* dh_rec, float* dc_
 int lstm_bwd_tiles(int R, int H);
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
-                          const float* c_prev, int R, int H, float drop_p, uint32_t seed,
+                          const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int S = 1,
                           float* ws = nullptr, int* tile_cnt = nullptr,
                           const float* dh_logit2 = nullptr);  // second dHd partial (or null)
@@ -118,14 +118,16 @@ void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, co
                     int write_dq, float* dpre_part, float* dwa_part, float* dba_part,
                     hipStream_t stream);
 
-// embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows sorted by token; C <= 1024)
-void launch_token_rows_sum(const float* x, int C, const int64_t* stok, const int64_t* srow, int N,
+// embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows grouped by token; C <= 1024)
+void launch_token_rows_sum(const float* x, int C, const int* stok, const int* srow, int N,
                            float* out, hipStream_t stream);
+// counting sort of N token ids (< V <= 65536) into (stok, srow); ws: 2V ints
+void launch_token_sort(const int64_t* toks, int N, int V, int* ws, int* stok, int* srow,
+                       hipStream_t stream);
 
 // beam.hip
 void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,
                       float* top_v, int* top_i, hipStream_t stream);
-int get_vocab_variant();
 void launch_beam_step(const float* top_v, const int* top_i, int B, int K, int T, int t,
                       float* beam_sum, int64_t* seq_hist, float* lp_hist, float* best_ppl,
                       int64_t* best_seq, float* best_lp, int64_t* tok_out, int* parent_out,

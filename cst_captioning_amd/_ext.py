@@ -25,8 +25,6 @@ def _load():
         import torch  # noqa: F401  (libtorch must be loaded first)
         from . import _C  # type: ignore
         _mod = _C
-        if os.environ.get('CSTCAP_VOCAB_VARIANT'):  # kernel A/B testing
-            _C.set_vocab_variant(int(os.environ['CSTCAP_VOCAB_VARIANT']))
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e
 

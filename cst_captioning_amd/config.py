@@ -119,6 +119,9 @@ def build_parser():
     add('--save_last', type=int, default=1,
         help='write a _last.pth sidecar with optimizer/RNG/loader state for exact resume')
     add('--nan_guard', type=int, default=1, help='skip a step whose loss is not finite')
+    add('--cuda_graph', type=int, default=1,
+        help='replay the fused-engine training step as a captured HIP graph (1) or enqueue '
+             'it eagerly every step (0)')
     add('--profile_phases', type=int, default=0, help='log per-phase HIP-event timings')
     return p
 

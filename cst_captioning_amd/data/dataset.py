@@ -281,27 +281,68 @@ class CaptionLoader:
         return self._assemble(self.index[lo:hi].astype(np.int64))
 
     def _assemble(self, vids):
-        dev = self.ds.device_tensors(self.device)
         rows = self._caption_rows(vids) if self.has_label else None
-        if rows is not None:
-            vid_t, rows_t = self._to_device(vids, rows)
-        else:
-            vid_t, = self._to_device(vids)
-        data = {'video_index': vid_t, 'vids': vids,
-                'ids': self.ds.video_ids[vids].tolist(),
-                'feats': [f.index_select(0, vid_t) for f in dev['feats']]}
-        if self.has_label:
+        idx = self._to_device(vids, rows) if rows is not None else self._to_device(vids)
+        return Batch(self, vids, idx)
+
+    def gather(self, vid_t, rows_t=None):
+        """Device part of a batch from its index tensors: features, labels,
+        masks (``nonzeros + 1``, ``dataloader.py:158-163``) and consensus
+        scores -- gathers only, so it can run inside a captured HIP graph."""
+        dev = self.ds.device_tensors(self.device)
+        out = {'feats': [f.index_select(0, vid_t) for f in dev['feats']]}
+        if rows_t is not None:
             labels = dev['labels'].index_select(0, rows_t)
             n = (labels != 0).sum(1, keepdim=True) + 1
             pos = torch.arange(labels.shape[1], device=labels.device)[None, :]
-            data['labels'] = labels
-            data['masks'] = (pos < n).float()
-            data['gts'] = _LazyGts(self.ds, vids)
-            if 'bcmrscores' in dev:
-                data['bcmrscores'] = dev['bcmrscores'].index_select(0, vid_t)
-            else:
-                data['bcmrscores'] = None
-        return data
+            out['labels'] = labels
+            out['masks'] = (pos < n).float()
+            out['bcmrscores'] = dev['bcmrscores'].index_select(0, vid_t) \
+                if 'bcmrscores' in dev else None
+        return out
+
+
+class Batch(dict):
+    """One batch: ``video_index`` / ``vids`` / ``ids`` / ``gts`` eagerly, the
+    device gathers (``feats``, ``labels``, ``masks``, ``bcmrscores``) on first
+    access.  ``index_tensors()`` exposes the gather indices, so the trainer's
+    HIP-graph step copies only them and gathers inside the graph."""
+
+    _DEVICE_KEYS = ('feats', 'labels', 'masks', 'bcmrscores')
+
+    def __init__(self, loader, vids, idx):
+        super().__init__()
+        self._loader = loader
+        self._idx = idx  # [vid_t] or [vid_t, rows_t]
+        self['video_index'] = idx[0]
+        self['vids'] = vids
+        self['ids'] = loader.ds.video_ids[vids].tolist()
+        if loader.has_label:
+            self['gts'] = _LazyGts(loader.ds, vids)
+
+    def index_tensors(self):
+        """The gather indices, or None once the device part was materialised
+        (the caller may have modified it, so only an eager step is exact)."""
+        return None if 'feats' in self.keys() else list(self._idx)
+
+    def _materialise(self):
+        if 'feats' not in self.keys():
+            self.update(self._loader.gather(*self._idx))
+
+    def __getitem__(self, k):
+        if k in self._DEVICE_KEYS:
+            self._materialise()
+        return super().__getitem__(k)
+
+    def get(self, k, default=None):
+        if k in self._DEVICE_KEYS:
+            self._materialise()
+        return super().get(k, default)
+
+    def __contains__(self, k):
+        if k in self._DEVICE_KEYS:
+            self._materialise()
+        return super().__contains__(k)
 
 
 class _LazyGts:

@@ -68,7 +68,7 @@ def engine_supports(opt):
 class _DecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, vgate, w_ih, w_hh, emb_w, logit_w, logit_b, att_gv, att_pre, att_wq,
-                att_wa, att_ba, eng, labels, bos, R, T, modes, ss_prob, drop_p, temperature, seed,
+                att_wa, att_ba, eng, labels, bos, R, T, modes, ss_prob, drop_p, temperature, rng,
                 vdiv, want_xe, use_counts, use_unfinished, save):
         has_att = att_gv is not None
         dev = logit_b.device
@@ -84,11 +84,11 @@ class _DecoderFn(torch.autograd.Function):
             vg_in, vdiv,
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
-            drop_p, temperature, seed, save, want_xe, use_counts, use_unfinished, att)
+            drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att)
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
         ctx.eng = eng
-        ctx.drop_p, ctx.seed = drop_p, seed
+        ctx.drop_p, ctx.rng = drop_p, rng
         ctx.shapes = (w_ih.shape, emb_w.shape)
         ctx.has_att = has_att
         ctx.att_saved = None
@@ -128,12 +128,7 @@ class _DecoderFn(torch.autograd.Function):
         # accumulate pass over the V x H gradient), on the late schedule
         direct = getattr(eng, 'direct_grad_slots', None)
         if direct is not None:
-            # the slots are overwritten, so only one fused backward may feed
-            # them between two zero_grad() calls
-            if eng.direct_used:
-                raise RuntimeError('second fused backward before zero_grad(): direct '
-                                   'gradient slots would be overwritten')
-            eng.direct_used = True
+            eng.check_direct_slots()
         if early:
             out_w, out_b, comm = hook.out_wlog, hook.out_blog, hook.comm_ptr
         elif direct is not None:
@@ -150,7 +145,7 @@ class _DecoderFn(torch.autograd.Function):
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
-            ctx.drop_p, ctx.seed, out_w, out_b, comm, att, out_emb)
+            ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb)
         dWx, dWlog, dblog, d_emb, dvg = res[:5]
         if early:
             hook.launch()
@@ -190,42 +185,115 @@ class DecoderEngine:
         self.V = model.vocab_size
         self.attention = getattr(model, 'num_chunks', 1) > 1
         dev = model.embed.weight.device
-        H = self.H
+        H, E, V = self.H, self.E, self.V
         # packed gate row 4u+g  <-  original row g*H+u
         self.perm = torch.arange(4 * H, device=dev).view(4, H).t().reshape(-1).contiguous()
         self.inv_perm = torch.argsort(self.perm)
         self.model = model
+        # bf16 shadow weights read by the kernels.  Persistent buffers, updated
+        # IN PLACE (by the fused Adam pass, or refresh_weights()), so a captured
+        # HIP graph always reads the live weights.
+        A = model.temporal_att.f_h.weight.size(0) if self.attention else 0
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.wx = torch.empty(4 * H, E + H, **bf)       # [W_ie | W_hh], packed gate rows
+        self.whh_q = torch.empty(4 * H + A, H, **bf)    # [W_hh; W_q] (recurrent GEMM operand)
+        self.whh = self.whh_q[:4 * H]
+        self.wq = self.whh_q[4 * H:] if self.attention else None
+        self.emb = torch.empty(V, E, **bf)
+        self.wlog = torch.empty(V, H, **bf)
+        self.ptab = torch.empty(V, 4 * H, dtype=torch.float32, device=dev)
+        self.fused_refresh = False  # True once an optimizer writes the shadows
+        self.direct_grad_slots = None
+        self.direct_params = None
+        self.direct_armed = False
         self.refresh_weights()
 
-    # -- bf16 shadow weights (refreshed after every optimizer step) -----------
+    # -- bf16 shadow weights ------------------------------------------------------
+    def shadow_spec(self, bucket):
+        """Shadow-copy segments of the flat parameter buffer for the fused
+        Adam pass: (int64 CPU meta (n, 7), [dst, dst2] * n)."""
+        m = self.model
+        slot = {id(p): (off, n) for p, (off, n) in zip(bucket.params, bucket.slices)}
+        rnn = m.core.rnn
+        H, E = self.H, self.E
+        empty = torch.empty(0, dtype=torch.bfloat16, device=self.wx.device)
+        segs = [(m.logit.weight, 0, 0, self.wlog, empty, 0),
+                (m.embed.weight, 0, 0, self.emb, empty, 0),
+                (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx, empty, 0),
+                (rnn.weight_hh_l0, 2, H, self.wx, self.whh_q, H)]
+        if self.attention:
+            segs.append((m.temporal_att.f_h.weight, 0, 0, self.wq, empty, 0))
+        meta, dsts = [], []
+        for p, kind, cols, d, d2, ld2 in segs:
+            off, n = slot[id(p)]
+            meta.append([off, n, kind, cols, H, E, ld2])
+            dsts += [d, d2]
+        return torch.tensor(meta, dtype=torch.int64), dsts
+
     @torch.no_grad()
     def refresh_weights(self):
+        """Rewrite every shadow from the fp32 parameters (after init or a
+        checkpoint load; the optimizer keeps them fresh during training)."""
         m = self.model
         E = self.E
         w_ih = m.core.rnn.weight_ih_l0
         w_hh = m.core.rnn.weight_hh_l0
-        self.wx = torch.cat([w_ih[:, :E], w_hh], 1).index_select(0, self.perm) \
-            .to(torch.bfloat16).contiguous()
-        self.whh = self.wx[:, E:].contiguous()
-        self.emb = m.embed.weight.detach().to(torch.bfloat16).contiguous()
-        self.wlog = m.logit.weight.detach().to(torch.bfloat16).contiguous()
+        self.wx[:, :E].copy_(w_ih[:, :E].index_select(0, self.perm))
+        self.wx[:, E:].copy_(w_hh.index_select(0, self.perm))
+        self.whh.copy_(self.wx[:, E:])
+        self.emb.copy_(m.embed.weight)
+        self.wlog.copy_(m.logit.weight)
+        if self.attention:
+            self.wq.copy_(m.temporal_att.f_h.weight)
+        self.update_ptab()
+
+    @torch.no_grad()
+    def update_ptab(self):
         # input-token gate table P = emb . W_ie^T (V x 4H, packed gate order):
         # one GEMM per optimizer step instead of K=E of work in every decode step
-        self.ptab = torch.mm(self.emb, self.wx[:, :E].t(), out_dtype=torch.float32)
-        if self.attention:
-            self.wq = m.temporal_att.f_h.weight.detach().to(torch.bfloat16).contiguous()
-            # [W_hh; W_q]: the decode step's recurrent GEMM also projects the
-            # next step's attention query
-            self.whh_q = torch.cat([self.whh, self.wq], 0).contiguous()
+        torch.mm(self.emb, self.wx[:, :self.E].t(), out_dtype=torch.float32, out=self.ptab)
 
     def attach_optimizer(self, trainer):
+        """The trainer's flat Adam writes the bf16 shadows in its update pass."""
+        opt = trainer.optimizer
+        if getattr(opt, 'supports_shadows', False):
+            opt.set_shadows(*self.shadow_spec(trainer.bucket))
+            self.fused_refresh = True
         self.refresh_weights()  # params were re-homed into the flat buffer
 
     def after_step(self):
-        self.refresh_weights()
+        if self.fused_refresh:
+            self.update_ptab()
+        else:
+            self.refresh_weights()
 
-    def _seed(self):
-        return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+    # -- gradient slots written by the fused backward -------------------------------
+    def set_direct_slots(self, slots, params):
+        self.direct_grad_slots = slots
+        self.direct_params = params
+        self.direct_armed = True
+
+    def arm_direct_slots(self):
+        self.direct_armed = True
+
+    def check_direct_slots(self):
+        """The fused backward OVERWRITES the gradient slots: one backward per
+        zero_grad(), and the slots must still be the parameters' .grad."""
+        if not self.direct_armed:
+            raise RuntimeError('second fused backward before the gradient bucket was zeroed: '
+                               'direct gradient slots would be overwritten')
+        for k, slot in self.direct_grad_slots.items():
+            g = self.direct_params[k].grad
+            if g is None or g.data_ptr() != slot.data_ptr():
+                raise RuntimeError('parameter %r no longer has its flat-bucket slot as .grad '
+                                   '(zero_grad(set_to_none=True) or a replaced .grad?); use the '
+                                   'trainer bucket\'s zero_grad()' % k)
+        self.direct_armed = False
+
+    def _rng(self, dev):
+        # per-pass seeds {dropout, sampling} drawn ON the device (graph-safe:
+        # a replayed graph advances the generator's offset)
+        return torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev)
 
     def _vgate(self, model, feats, expand):
         fc = model.encode(feats)  # (B, F*H), FeatPool dropout in train mode
@@ -270,7 +338,8 @@ class DecoderEngine:
         return _DecoderFn.apply(vg, *ws, *att, self,
                                 labels.contiguous() if labels is not None else None, bos, R, T,
                                 modes, float(ss_prob), float(drop_p), float(temperature),
-                                self._seed(), S, want_xe, use_counts, use_unfinished, save)
+                                self._rng(m.logit.bias.device), S, want_xe, use_counts,
+                                use_unfinished, save)
 
     # -- public entry points ------------------------------------------------------
     def rollout(self, model, feats, labels):

@@ -8,9 +8,13 @@ buffers of :class:`..parallel.FlatGradBucket`:
   * pass 1: sum of squares of the gradient (one block-reduction kernel);
   * pass 2: ``coef = min(1, clip / (norm + 1e-6))`` is computed ON DEVICE
     and applied inside the Adam update, which also refreshes the bf16
-    shadow copies of the decoder weights used by the MFMA kernels.
+    shadow copies of the decoder weights used by the MFMA kernels
+    (:meth:`set_shadows`).
 
-No host synchronisation.  The math is PyTorch's Adam:
+No host synchronisation.  Learning rate and step count live in a device
+tensor (``[lr, step]``): the bias corrections follow the device step, so a
+captured HIP graph replays correct updates, and :meth:`sync_lr` (outside
+any capture) publishes an LR change made through ``param_groups``.  The math is PyTorch's Adam:
 ``denom = sqrt(v) / sqrt(1 - b2^t) + eps``,
 ``p -= lr / (1 - b1^t) * m / denom``.
 
@@ -36,9 +40,27 @@ class FlatAdam:
         self.param_groups = [{'lr': lr}]  # for adjust_learning_rate()
         self.last_norm = None
         self._use_hip = _ext.available() and bucket.data.is_cuda
+        self.supports_shadows = self._use_hip
+        self._shadow = (torch.empty(0, dtype=torch.int64), [])
         if self._use_hip:
-            self._partials = torch.empty(1024, dtype=torch.float32, device=bucket.data.device)
-            self._scal = torch.empty(2, dtype=torch.float32, device=bucket.data.device)
+            dev = bucket.data.device
+            self._partials = torch.empty(1024, dtype=torch.float32, device=dev)
+            self._scal = torch.empty(2, dtype=torch.float32, device=dev)
+            self._hyper = torch.tensor([float(lr), 0.0], dtype=torch.float32, device=dev)
+            self._no_skip = torch.zeros((), dtype=torch.bool, device=dev)
+            self._lr_synced = float(lr)
+
+    def set_shadows(self, meta, dsts):
+        """bf16 shadow copies the update pass writes (see csrc/kernels/adam.hip)."""
+        self._shadow = (meta, list(dsts))
+
+    def sync_lr(self):
+        """Publish ``param_groups[0]['lr']`` to the device (no-op if unchanged).
+        Call outside graph capture."""
+        lr = float(self.param_groups[0]['lr'])
+        if self._use_hip and lr != self._lr_synced:
+            self._hyper[0].fill_(lr)
+            self._lr_synced = lr
 
     def zero_grad(self):
         self.bucket.zero_grad()
@@ -49,16 +71,18 @@ class FlatAdam:
         self.lr = self.param_groups[0]['lr']
         self.step_count += 1
         b1, b2 = self.betas
-        bc1 = 1 - b1 ** self.step_count
-        bc2 = 1 - b2 ** self.step_count
         g, p = self.bucket.grad, self.bucket.data
         if self._use_hip:
+            if not torch.cuda.is_current_stream_capturing():
+                self.sync_lr()
+            self._hyper[1:].add_(1.0)
             self.last_norm = _ext.ops().flat_adam_step(
                 p, g, self.exp_avg, self.exp_avg_sq, self._partials, self._scal,
-                skip if skip is not None else torch.zeros((), dtype=torch.bool, device=p.device),
-                float(self.lr), float(b1), float(b2), float(self.eps),
-                float(self.grad_clip), float(bc1), float(bc2))
+                skip if skip is not None else self._no_skip, self._hyper,
+                float(b1), float(b2), float(self.eps), float(self.grad_clip), *self._shadow)
             return self.last_norm
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
         norm = torch.linalg.vector_norm(g)
         self.last_norm = norm
         coef = torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0)
@@ -79,12 +103,20 @@ class FlatAdam:
             p.copy_(torch.where(keep, p - upd, p))
         return norm
 
+    def _steps(self):
+        # graph replays advance only the device counter
+        return int(self._hyper[1].item()) if self._use_hip else self.step_count
+
     def state_dict(self):
-        return {'step': self.step_count, 'exp_avg': self.exp_avg, 'exp_avg_sq': self.exp_avg_sq,
-                'lr': self.param_groups[0]['lr'], 'betas': self.betas, 'eps': self.eps}
+        return {'step': self._steps(), 'exp_avg': self.exp_avg,
+                'exp_avg_sq': self.exp_avg_sq, 'lr': self.param_groups[0]['lr'],
+                'betas': self.betas, 'eps': self.eps}
 
     def load_state_dict(self, s):
         self.step_count = s['step']
         self.exp_avg.copy_(s['exp_avg'])
         self.exp_avg_sq.copy_(s['exp_avg_sq'])
         self.param_groups[0]['lr'] = s['lr']
+        if self._use_hip:
+            self._hyper[1].fill_(float(s['step']))
+            self.sync_lr()

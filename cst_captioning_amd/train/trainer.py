@@ -88,25 +88,27 @@ class Trainer:
         self.ctx.broadcast_module(model)
         early = [model.logit.weight, model.logit.bias]
         self.bucket = FlatGradBucket(model.parameters(), first=early)
-        if engine is not None and self.ctx.enabled and not getattr(opt, 'no_early_allreduce', 0):
+        # Early all-reduce of the vocab-head gradients under the reverse loop:
+        # eager steps only.  With HIP graphs every step (eager warm-up or
+        # replay) issues the same single bucket all-reduce, so ranks can never
+        # disagree on the collective sequence.
+        if (engine is not None and self.ctx.enabled and not getattr(opt, 'no_early_allreduce', 0)
+                and not getattr(opt, 'cuda_graph', 1)):
             from ..parallel.dist import EarlyAllReduce
             self.bucket.early = EarlyAllReduce(self.ctx, self.bucket, early)
             engine.early_grad_hook = self.bucket.early
         if engine is not None:
-            # the fused backward writes the vocab-head gradients straight into
-            # their bucket slots (one backward per step: overwrite == accumulate
-            # onto the zeroed buffer)
+            # the fused backward writes the vocab-head, embedding and LSTM
+            # weight gradients straight into their bucket slots (one backward
+            # per step: overwrite == accumulate onto the zeroed buffer)
             slot = {id(p): (off, n) for p, (off, n) in zip(self.bucket.params, self.bucket.slices)}
             rnn = model.core.rnn
             named = {'wlog': model.logit.weight, 'blog': model.logit.bias,
                      'emb': model.embed.weight, 'wih': rnn.weight_ih_l0, 'whh': rnn.weight_hh_l0}
-            if os.environ.get('CSTCAP_DIRECT_EMB', '1') == '0':  # A/B knob
-                named = {k: named[k] for k in ('wlog', 'blog')}
-            engine.direct_grad_slots = {
-                k: self.bucket.grad[slot[id(p)][0]:slot[id(p)][0] + slot[id(p)][1]].view_as(p)
-                for k, p in named.items()}
-            engine.direct_used = False
-            self.bucket.on_zero = lambda: setattr(engine, 'direct_used', False)
+            engine.set_direct_slots(
+                {k: self.bucket.grad[slot[id(p)][0]:slot[id(p)][0] + slot[id(p)][1]].view_as(p)
+                 for k, p in named.items()}, named)
+            self.bucket.on_zero = engine.arm_direct_slots
         if getattr(opt, 'honor_optim_flags', 0):
             betas, eps = (opt.optim_alpha, opt.optim_beta), opt.optim_epsilon
         else:
@@ -120,6 +122,11 @@ class Trainer:
                       'best_iter': 0, 'best_epoch': opt.max_epochs}
         self.history = {}
         self.rl_training = False
+        # HIP-graph step (see graph_step): captured step per schedule key
+        self._graph = None
+        self._graph_key = None
+        self._graph_warm = {}
+        self._ev_inputs = None
 
     # ------------------------------------------------------------------ RL ---
     def _ensure_scorer(self):
@@ -163,10 +170,13 @@ class Trainer:
             # the small greedy decode (measured equal to greedy-first, 4.87 ms
             # per step: the step is GPU-bound).
             if getattr(self, '_side_stream', None) is None:
+                # (a high-priority stream for the greedy decode measured 4.5 ->
+                # 8.7 ms per step: the queue priority throttles the rollout)
                 self._side_stream = torch.cuda.Stream(device=self.device)
+                self._ev_inputs = torch.cuda.Event()
             side = self._side_stream
             main = torch.cuda.current_stream(self.device)
-            inputs_ready = torch.cuda.Event()
+            inputs_ready = self._ev_inputs
             inputs_ready.record(main)
         model_res, logprobs, _ = self._decode_rollout(data)
         if side is not None:
@@ -193,7 +203,7 @@ class Trainer:
                                                        opt.scb_baseline)
         self.timer.mark('reward')
         loss = self.rl_criterion(model_res, logprobs, reward.detach().to(logprobs.dtype))
-        return loss, {'reward': reward, 'm': m_score, 'b': b_score}
+        return loss, {'reward': reward, 'm': m_score, 'b': b_score, 'seq': model_res}
 
     def xe_loss(self, data):
         if self.engine is not None:
@@ -205,11 +215,10 @@ class Trainer:
         return self.xe_criterion(pred, data['labels'][:, 1:], data['masks'][:, 1:]), {}
 
     # --------------------------------------------------------------- step ---
-    def train_step(self, data, epoch):
-        opt, m, infos = self.opt, self.model, self.infos
-        self.timer.reset()
-        self.timer.mark('start')
-        m.train()
+    def _schedules(self, epoch):
+        """Host-side per-epoch schedules (train.py:109-162): scheduled
+        sampling, RL switch, MIXER start, SCB count.  Returns (mixer_from, scb)."""
+        opt, m = self.opt, self.model
         ssp = schedules.ss_prob(opt, epoch)
         opt.ss_prob = ssp
         if ssp > 0 or opt.use_ss == 1:
@@ -224,6 +233,13 @@ class Trainer:
         scb = opt.scb_captions
         if opt.use_cst == 1 and self.rl_training:
             scb = schedules.scb_captions(opt, epoch, self.train_loader.get_seq_per_img())
+        return mixer_from, scb
+
+    def _forward_backward(self, data, mixer_from, scb):
+        """zero_grad -> forward -> loss -> backward (+ the NaN-guard flag).
+        Device work only: no host synchronisation (graph-capturable)."""
+        opt, m = self.opt, self.model
+        m.train()
         self.optimizer.zero_grad()
         m.set_seq_per_img(self.train_loader.get_seq_per_img())
         if self.rl_training:
@@ -233,21 +249,106 @@ class Trainer:
         loss.backward()
         self.timer.mark('backward')
         skip = None
-        guard = getattr(opt, 'nan_guard', 1)
-        if guard:
+        if getattr(opt, 'nan_guard', 1):
             skip = ~torch.isfinite(loss.detach())
             if self.ctx.enabled:  # every rank must skip together: the flag
                 self.bucket.set_flag(skip)  # rides the gradient all-reduce
-        self.bucket.all_reduce(self.ctx)
-        self.timer.mark('allreduce')
-        if guard and self.ctx.enabled:
+        extra.update(loss=loss.detach(), mixer_from=mixer_from, scb_captions=scb)
+        return extra, skip
+
+    def _apply_update(self, skip):
+        """(after the gradient all-reduce) clip + Adam + weight shadows."""
+        if getattr(self.opt, 'nan_guard', 1) and self.ctx.enabled:
             skip = self.bucket.flag_any()
         self.optimizer.step(skip)
         if self.engine is not None:
             self.engine.after_step()
         self.timer.mark('optimizer')
-        extra.update(loss=loss.detach(), mixer_from=mixer_from, scb_captions=scb)
+
+    def train_step(self, data, epoch):
+        self.timer.reset()
+        self.timer.mark('start')
+        mixer_from, scb = self._schedules(epoch)
+        if self._graph_enabled():
+            out = self._graph_step(data, mixer_from, scb)
+            if out is not None:
+                return out
+        extra, skip = self._forward_backward(data, mixer_from, scb)
+        self.bucket.all_reduce(self.ctx)
+        self.timer.mark('allreduce')
+        self._apply_update(skip)
         return extra
+
+    # ------------------------------------------------------------ HIP graph ---
+    # One training step replayed as ONE captured HIP graph (torch.cuda.CUDAGraph
+    # is hipGraph on ROCm): feature encoder, rollout, concurrent greedy
+    # baseline (second stream, joined by events), on-GPU CIDEr-D, reward,
+    # backward (vocab head on a side stream), clip + Adam + bf16 weight shadows
+    # and the input-token table.  The host then enqueues one graph launch per
+    # step instead of ~600 kernel launches.  What makes the replay correct:
+    #   * inputs are copied into static buffers before each replay;
+    #   * RNG seeds are drawn on the device (graph-safe Philox offsets), the
+    #     kernels read them from memory;
+    #   * Adam's lr / step live on the device; the bf16 weight shadows and the
+    #     token table are persistent buffers updated in place;
+    #   * schedules that change the captured work (RL switch, MIXER start, SCB
+    #     count, scheduled-sampling probability, batch shapes) key the graph:
+    #     a new key is run eagerly once, then captured.
+    # Under data parallelism the gradient all-reduce stays an eager RCCL call
+    # between two graphs (forward/backward, then update).
+    def _graph_enabled(self):
+        return (self.engine is not None and self.device.type == 'cuda'
+                and bool(getattr(self.opt, 'cuda_graph', 1)) and not self.timer.enabled)
+
+    def _graph_signature(self, idx, mixer_from, scb):
+        return (self.rl_training, mixer_from, scb, float(self.model.ss_prob),
+                self.train_loader.get_seq_per_img(), tuple(tuple(t.shape) for t in idx))
+
+    def _graph_step(self, data, mixer_from, scb):
+        """Replay the captured step on this batch; None = run it eagerly."""
+        idx = data.index_tensors() if hasattr(data, 'index_tensors') else None
+        if idx is None:
+            return None
+        key = self._graph_signature(idx, mixer_from, scb)
+        if key != self._graph_key:
+            if self._graph_warm.get(key, 0) < 1:  # run a new schedule eagerly once
+                self._graph_warm[key] = self._graph_warm.get(key, 0) + 1
+                return None
+            self._capture(data._loader, idx, key, mixer_from, scb)
+        for dst, src in zip(self._static_idx, idx):
+            dst.copy_(src, non_blocking=True)
+        self.optimizer.sync_lr()
+        g_a, g_b = self._graph
+        g_a.replay()
+        if g_b is not None:  # data parallel: eager all-reduce between the graphs
+            self.bucket.all_reduce(self.ctx)
+            g_b.replay()
+        return self._graph_out
+
+    def _capture(self, loader, idx, key, mixer_from, scb):
+        """Capture one step (batch gather + forward + backward [+ update]).
+        Callers must not keep an earlier autograd graph alive (e.g. an
+        un-freed loss tensor): its AccumulateGrad nodes stay bound to the
+        default stream, and the cross-stream wait they add breaks the capture."""
+        self._graph = self._graph_out = None
+        torch.cuda.synchronize(self.device)
+        self._static_idx = [t.clone() for t in idx]
+        pool = torch.cuda.graph_pool_handle()
+        g_a = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_a, pool=pool):
+            batch = loader.gather(*self._static_idx)  # the batch gather is captured too
+            batch['video_index'] = self._static_idx[0]
+            extra, skip = self._forward_backward(batch, mixer_from, scb)
+            if not self.ctx.enabled:
+                self._apply_update(skip)
+        g_b = None
+        if self.ctx.enabled:
+            g_b = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_b, pool=pool):
+                self._apply_update(skip)
+        self._graph, self._graph_key, self._graph_out = (g_a, g_b), key, extra
+        logger.info('captured the training step as a HIP graph (%s)',
+                    'two graphs around the all-reduce' if g_b is not None else 'one graph')
 
     # --------------------------------------------------------------- loop ---
     def resume(self):

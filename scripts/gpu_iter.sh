@@ -1,19 +1,16 @@
 #!/bin/bash
-# iteration loop: tests -> bench -> decoder microbench -> PMC (VALU/MFMA/waits)
+# iteration check: graph + kernel GPU tests first, then the whole GPU suite,
+# the headline bench with and without the HIP graph, and a kernel profile
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc
-CSTCAP_VOCAB_VARIANT=${TEST_VARIANT:-4} timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-[ $rc -eq 0 ] || exit $rc
-CSTCAP_VOCAB_VARIANT=${TEST_VARIANT:-4} timeout -k 10 400 python bench.py --steps 20 --warmup 5 --json_out gpurun_out/bench_hip.json > gpurun_out/bench_hip.log 2>&1 || exit $?
-VARIANTS=${VARIANTS:-0,3} timeout -k 10 300 python scripts/microbench_decoder.py > gpurun_out/microbench.log 2>&1 || exit $?
-[ -n "$SKIP_PMC" ] && exit 0
-VARIANTS=0 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/p1 -o p1 \
-  --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS \
-  -- python scripts/microbench_decoder.py > gpurun_out/pmc/p1.log 2>&1 || exit $?
-VARIANTS=0 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/p2 -o p2 \
-  --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
-  -- python scripts/microbench_decoder.py > gpurun_out/pmc/p2.log 2>&1
-echo "rc=$?"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_graph.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_graph.log 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --steps 40 --warmup 5 --json_out gpurun_out/bench_hip.json > gpurun_out/bench_hip.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --steps 40 --warmup 5 --cuda_graph 0 --json_out gpurun_out/bench_eager.json > gpurun_out/bench_eager.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --steps 30 --warmup 5 --num_chunks 8 --json_out gpurun_out/bench_att8.json > gpurun_out/bench_att8.log 2>&1 || exit $?
+rm -rf gpurun_out/prof_rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_rc -o rc -- python bench.py --steps 5 --warmup 3 > gpurun_out/prof_rc.log 2>&1 || exit $?
+python scripts/prof_summary.py gpurun_out/prof_rc/rc_kernel_trace.csv 5 45 > gpurun_out/prof_rc_summary.txt
+python scripts/step_timeline.py gpurun_out/prof_rc/rc_kernel_trace.csv 1 > gpurun_out/step_timeline_rc.txt

@@ -1,7 +1,7 @@
 """Single-kernel microbenchmarks (HIP-event timed, back-to-back launches).
 
 vocab_fwd at the rollout shape (R = 1280 rows) and the greedy shape (R = 64),
-per tile variant, with the epilogue pieces switched on one at a time:
+with the epilogue pieces switched on one at a time:
   mainloop = GEMM only; stats = max/LSE (+target); sample; sample+save
   (fp16 logits for the backward); argmax.
 """
@@ -20,22 +20,18 @@ dev = 'cuda'
 V, H = 10509, 512
 W = (torch.randn(V, H, device=dev) * 0.05).bfloat16()
 b = torch.randn(V, device=dev) * 0.1
-variants = [int(x) for x in os.environ.get('VARIANTS', '0,4,5,6,7').split(',')]
 res = {}
 for R in (1280, 64):
     hd = torch.randn(R, H, device=dev).bfloat16()
     tgt = torch.randint(0, V, (R,), device=dev)
-    for var in variants:
-        C.set_vocab_variant(var)
-        for name, flags, save, t in (('mainloop', 4, False, None), ('stats', 0, False, tgt),
-                                     ('sample', 1, False, None), ('sample_save', 1, True, None),
-                                     ('argmax', 2, False, None)):
-            if var < 4 and flags == 4:
-                continue
-            us = C.vocab_fwd_bench(hd, W, b, t if t is not None else torch.empty(0, dtype=torch.long, device=dev),
-                                   flags, save, 50)
-            res['R%d_v%d_%s' % (R, var, name)] = round(us, 2)
-C.set_vocab_variant(4)
+    for name, flags, save, t in (('mainloop', 4, False, None), ('stats', 0, False, tgt),
+                                 ('sample', 1, False, None), ('sample_save', 1, True, None),
+                                 ('argmax', 2, False, None)):
+        us = C.vocab_fwd_bench(hd, W, b, t if t is not None else torch.empty(0, dtype=torch.long, device=dev),
+                               flags, save, 50)
+        res['R%d_%s' % (R, name)] = round(us, 2)
+toks = torch.randint(0, V, (28 * 1280,), device=dev)
+res['token_sort_us'] = round(C.token_sort_bench(toks, V, 50), 2)
 if os.environ.get('DS', '1') == '1':
     n, R = 28, 1280
     ldl = (V + 7) // 8 * 8

@@ -17,7 +17,7 @@ ARGS = ['--synthetic', 'msvd', '--synthetic_videos', '24', '--synthetic_vocab', 
         '--feat_dims', '16', '8', '--batch_size', '4', '--train_seq_per_img', '3',
         '--test_batch_size', '3', '--test_seq_per_img', '3', '--beam_size', '2',
         '--impl', os.environ.get('CSTCAP_TEST_IMPL', 'torch'), '--loglevel', 'WARNING',
-        '--drop_prob_lm', '0',
+        '--drop_prob_lm', '0', '--cuda_graph', os.environ.get('CSTCAP_TEST_GRAPH', '1'),
         '--learning_rate', '1e-3', '--language_eval', '0']
 
 
@@ -45,6 +45,9 @@ def main(out):
     tr.optimizer.zero_grad()
     loss, _ = tr.xe_loss(data)
     loss.backward()
+    # drop the autograd graph: a graph kept alive across the HIP-graph capture
+    # of the next train_step pins AccumulateGrad nodes to the default stream
+    del loss
     tr.bucket.all_reduce(ctx)
     grad = tr.bucket.grad.detach().cpu().clone()
     # two full steps: parameters must stay identical on every rank

@@ -26,10 +26,11 @@ def _free_port():
     return p
 
 
-def _run(world, out):
-    env = dict(os.environ)
+def _run(world, out, graph):
+    env = dict(os.environ, CSTCAP_TEST_GRAPH=str(graph))
     env.update(PYTHONPATH=ROOT + os.pathsep + env.get('PYTHONPATH', ''), CSTCAP_SHARE_GPU='1',
-               CSTCAP_DIST_BACKEND='gloo', CSTCAP_TEST_IMPL='hip', OMP_NUM_THREADS='4')
+               CSTCAP_DIST_BACKEND='gloo', CSTCAP_TEST_IMPL='hip', OMP_NUM_THREADS='4',
+               PYTHONFAULTHANDLER='1')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node',
            str(world), '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
            os.path.join(HERE, 'dist_worker.py'), out]
@@ -38,10 +39,14 @@ def _run(world, out):
     return torch.load(out, weights_only=False)
 
 
-def test_engine_dp_allreduce_matches_single_process(tmp_path):
+@pytest.mark.parametrize('graph', [1, 0], ids=['hip_graph', 'eager_early_allreduce'])
+def test_engine_dp_allreduce_matches_single_process(tmp_path, graph):
+    """graph=1: steps replayed as HIP graphs around one bucket all-reduce;
+    graph=0: eager steps with the vocab-head all-reduce started under the
+    reverse LSTM loop (EarlyAllReduce)."""
     os.environ['CSTCAP_TEST_IMPL'] = 'hip'
-    r2 = _run(2, str(tmp_path / 'w2.pt'))
-    r1 = _run(1, str(tmp_path / 'w1.pt'))
+    r2 = _run(2, str(tmp_path / 'w2.pt'), graph)
+    r1 = _run(1, str(tmp_path / 'w1.pt'), graph)
     sys.path.insert(0, HERE)
     import dist_worker as W
     from cst_captioning_amd.parallel import DistContext

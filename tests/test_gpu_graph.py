@@ -1,0 +1,113 @@
+"""The HIP-graph training step and the pieces that make its replay correct
+(``Trainer._graph_step``): device-side RNG seeds, device-side Adam lr/step,
+bf16 weight shadows written by the Adam pass, and the counting sort of the
+backward's input tokens."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def _setup(rl, seed=0, V=500, H=128, drop=0.0, graph=1):
+    from cst_captioning_amd.config import default_opts
+    from cst_captioning_amd.data import make_synthetic, CaptionLoader
+    from cst_captioning_amd.cli import build_model
+    from cst_captioning_amd.parallel import DistContext
+    from cst_captioning_amd.train.trainer import Trainer
+    ds = make_synthetic('msrvtt', num_videos=48, vocab_size=V, seq_length=12,
+                        feat_dims=[64, 32], seed=seed)
+    opt = default_opts(vocab_size=V, seq_length=12, feat_dims=[64, 32], train_seq_per_img=5,
+                       batch_size=8, rnn_size=H, input_encoding_size=H, drop_prob_lm=drop,
+                       use_rl=int(rl), use_rl_after=0, use_cst=0, use_mixer=1, mixer_from=1,
+                       use_eos=1, impl='hip', cuda_graph=graph, learning_rate=1e-3)
+    opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
+    torch.manual_seed(seed)
+    dev = torch.device(DEV)
+    model, engine = build_model(opt, dev, 'hip')
+    assert engine is not None
+    loader = CaptionLoader(ds, 8, 5, 'train', dev, seed=seed)
+    tr = Trainer(opt, model, loader, None, DistContext(device=dev), engine)
+    tr.rl_training = bool(rl)
+    return tr, loader
+
+
+def _flat(model):
+    return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+
+
+def test_graph_xe_steps_match_eager():
+    """XE without dropout is deterministic up to summation order: 6 steps
+    through the captured graph equal 6 eager steps on the same batches."""
+    a, la = _setup(rl=False, graph=0)
+    b, lb = _setup(rl=False, graph=1)
+    torch.testing.assert_close(_flat(a.model), _flat(b.model), rtol=0, atol=0)
+    for _ in range(6):
+        da, db = la.get_batch(), lb.get_batch()
+        oa = a.train_step(da, 0)
+        ob = b.train_step(db, 0)
+        torch.testing.assert_close(float(oa['loss']), float(ob['loss']), rtol=1e-4, atol=1e-5)
+    assert b._graph is not None, 'the graph path was never captured'
+    pa, pb = _flat(a.model), _flat(b.model)
+    assert ((pa - pb).norm() / pa.norm()).item() < 1e-4
+    # the optimizer's device step counter advanced on every replay
+    assert b.optimizer.state_dict()['step'] == 6
+
+
+def test_graph_replays_draw_fresh_samples():
+    """The same batch replayed twice gives different rollouts (seeds are
+    drawn on the device inside the graph), and the weights keep training."""
+    tr, loader = _setup(rl=True, drop=0.5)
+    seqs = []
+    for _ in range(4):
+        before = _flat(tr.model).clone()
+        out = tr.train_step(loader.get_batch_at(0), 0)  # the same videos every step
+        torch.cuda.synchronize()
+        assert torch.isfinite(out['loss']).item()
+        assert not torch.equal(before, _flat(tr.model))
+        seqs.append(out['seq'].clone() if tr._graph is not None else None)
+    assert tr._graph is not None
+    assert seqs[-1] is not None and seqs[-2] is not None
+    assert not torch.equal(seqs[-1], seqs[-2])
+
+
+def test_adam_pass_writes_the_bf16_shadows():
+    """After training steps the engine's shadow buffers (written by the fused
+    Adam pass) equal a from-scratch refresh of the fp32 parameters."""
+    tr, loader = _setup(rl=True, drop=0.5)
+    for _ in range(4):
+        tr.train_step(loader.get_batch(), 0)
+    eng = tr.engine
+    got = [t.clone() for t in (eng.wx, eng.whh_q, eng.emb, eng.wlog, eng.ptab)]
+    eng.refresh_weights()
+    for g, r in zip(got, (eng.wx, eng.whh_q, eng.emb, eng.wlog)):
+        assert torch.equal(g, r)
+    torch.testing.assert_close(got[4], eng.ptab, rtol=1e-5, atol=1e-5)
+
+
+def test_token_counting_sort():
+    from cst_captioning_amd import _ext
+    V = 10509
+    toks = torch.randint(0, V, (28 * 1280,), device=DEV)
+    toks[:5000] = 0  # a heavy bucket (EOS)
+    stok, srow = _ext.ops().token_sort(toks, V)
+    st, sr = stok.cpu().numpy(), srow.cpu().numpy()
+    t = toks.cpu().numpy()
+    assert (np.diff(st) >= 0).all()                  # grouped by token
+    assert np.array_equal(np.sort(sr), np.arange(t.size))  # a permutation of the rows
+    assert np.array_equal(t[sr], st)                 # each row under its own token
+
+
+def test_lr_change_reaches_the_graph():
+    """An LR decay between replays (adjust_learning_rate) takes effect
+    without a re-capture: with lr = 0 the weights stop moving."""
+    tr, loader = _setup(rl=False)
+    for _ in range(3):
+        tr.train_step(loader.get_batch(), 0)
+    assert tr._graph is not None
+    tr.optimizer.param_groups[0]['lr'] = 0.0
+    before = _flat(tr.model).clone()
+    tr.train_step(loader.get_batch(), 0)
+    torch.testing.assert_close(_flat(tr.model), before, rtol=0, atol=0)

@@ -111,24 +111,14 @@ def test_flat_adam_skip_flag():
     torch.testing.assert_close(p.detach(), before)
 
 
-# fused=True: the fused dS + dHd backward kernel (vocab_bwd.hip, H = 512
-# only); V = 1299 is not a multiple of its 32-wide K tile and 330 rows not of
-# its 128-row tile
-_SHAPES = [dict(), dict(V=1299, H=512), dict(V=1299, H=512, fused=True)]
-_SHAPE_IDS = ['h64', 'h512', 'h512_fused']
+# V = 1299 is not a multiple of the 128-wide vocab tile, 330 rows not of the
+# 128-row tile
+_SHAPES = [dict(), dict(V=1299, H=512)]
+_SHAPE_IDS = ['h64', 'h512']
 
 
-def _tiny_shape(seed=0, fused=False, **shape):
-    _ext().set_bwd_fused(1 if fused else 0)
+def _tiny_shape(seed=0, **shape):
     return _tiny(seed=seed, **shape)
-
-
-@pytest.fixture(autouse=True)
-def _fused_off():
-    yield
-    from cst_captioning_amd import _ext as ext
-    if ext.available():
-        ext.ops().set_bwd_fused(0)
 
 
 @pytest.mark.parametrize('shape', _SHAPES, ids=_SHAPE_IDS)
