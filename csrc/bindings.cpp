@@ -30,6 +30,9 @@ double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, a
                           int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
 std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V);
+std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
+                                     at::Tensor rng, int64_t mode, double temperature,
+                                     int64_t step);
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
                        int64_t flags, bool save, int64_t iters);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
@@ -103,5 +106,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vocab_bwd_ds_bench", &cst::vocab_bwd_ds_bench);
   m.def("token_sort_bench", &cst::token_sort_bench);
   m.def("token_sort", &cst::token_sort);
+  m.def("vocab_select", &cst::vocab_select);
   m.def("beam_search", &cst::beam_search);
 }

@@ -754,6 +754,36 @@ double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters) {
       iters, st);
 }
 
+// the vocab projection + sampler/argmax + combine alone (tests of the exact
+// two-level sampler): rows hd (R, H) bf16 -> {token (R) int64, lse (R)}.
+// mode: SEL_SAMPLE_H (1) or SEL_GREEDY_H (2).
+std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
+                                     at::Tensor rng, int64_t mode, double temperature,
+                                     int64_t step) {
+  check_cuda(hd, "hd");
+  check_cuda(wlog, "wlog");
+  TORCH_CHECK(hd.scalar_type() == at::kBFloat16 && wlog.scalar_type() == at::kBFloat16 &&
+                  blog.scalar_type() == at::kFloat, "bf16 hd / W, fp32 bias");
+  TORCH_CHECK(mode == SEL_SAMPLE_H || mode == SEL_GREEDY_H, "mode: 1 sample, 2 greedy");
+  const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
+  TORCH_CHECK(H % 64 == 0 && wlog.size(1) == H && blog.numel() == V, "shapes");
+  auto dev = hd.device();
+  const int n_vt = vocab_num_tiles((int)V);
+  at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4},
+                              at::TensorOptions().dtype(at::kFloat).device(dev));
+  at::Tensor tok = at::zeros({R, 1}, at::TensorOptions().dtype(at::kLong).device(dev));
+  at::Tensor lse = at::empty({R}, at::TensorOptions().dtype(at::kFloat).device(dev));
+  hipStream_t st = cur_stream();
+  launch_vocab_fwd(reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R, (int)H,
+                   reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
+                   (int)V, nullptr, 0, part.data_ptr(), nullptr, 0, mode == SEL_SAMPLE_H ? 1 : 2,
+                   (float)(1.0 / temperature), rng_ptr(rng), (int)step, st);
+  launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse.data_ptr<float>(),
+                       tok.data_ptr<int64_t>(), 1, nullptr, 0, nullptr, 0, nullptr, 0, (int)mode,
+                       0.f, rng_ptr(rng), (int)step, nullptr, 0, nullptr, st);
+  return {tok.view({R}), lse};
+}
+
 // the counting sort itself, for tests: returns {stok, srow} (int32)
 std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V) {
   check_cuda(toks, "toks");

@@ -351,3 +351,4 @@ def test_trainer_direct_gradient_slots_match_torch():
             continue
         err = (p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)
         assert err < 0.06, (name, float(err))
+
