@@ -21,6 +21,10 @@ Modes:
   --impl torch --reward cpu --precision fp32 --dedupe_greedy 0
                reference semantics (PyTorch ops, CPU CIDEr-D in Python):
                the baseline BASELINE.md asks to beat.
+  --impl torch --precision bf16
+               same-precision PyTorch baseline: PyTorch decoder ops under bf16
+               autocast with the on-GPU CIDEr-D reward, so the kernels'
+               speed-up is separated from the precision change.
 
 Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (starts
 the PyTorch launcher with N ranks as a child process), or
@@ -202,8 +206,9 @@ def main():
         'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': round(ms, 3),
         'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': round(caps / baseline, 3) if (baseline and a.mode == 'scst') else None,
-        # effective compute dtype: the fused engine is bf16, the PyTorch path fp32
-        'dtype': 'bf16' if engine is not None else 'fp32',
+        # effective compute dtype: the fused engine is bf16; the PyTorch path is
+        # bf16 under autocast with --precision bf16 on a GPU, else fp32
+        'dtype': 'bf16' if (engine is not None or trainer.autocast_bf16) else 'fp32',
         'data': 'synthetic (MSR-VTT-shaped, random-init weights)',
         'config': {'model': 'CaptionModel concat LSTM-512 (resnet+c3d+mfcc+category, '
                             'V=%d, L=30)' % a.vocab,

@@ -317,7 +317,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor dg_xe, double drop_p, at::Tensor rng,
                                          at::Tensor out_wlog, at::Tensor out_blog,
                                          int64_t comm_stream, std::vector<at::Tensor> att,
-                                         at::Tensor out_emb) {
+                                         at::Tensor out_emb, at::Tensor ds_bias) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -366,11 +366,17 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   }
   at::Tensor dWlog = early ? out_wlog : at::empty({V, H}, f32);
   at::Tensor dblog = early ? out_blog.view({V}) : at::empty({V}, f32);
+  // ds_bias given: the caller already wrote a dense dS (bf16) into the logits
+  // buffer (full log-prob API) and passes the bias gradient (its column sums)
+  const bool ds_ready = ds_bias.defined() && ds_bias.numel() > 0;
+  if (ds_ready)
+    TORCH_CHECK(ds_bias.is_cuda() && ds_bias.scalar_type() == at::kFloat && ds_bias.numel() == V,
+                "ds_bias must be fp32 (V)");
   (void)hipEventRecord(ev_ready, st);
   (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
   {
     c10::hip::HIPStreamGuard guard(side);
-    launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
+    if (!ds_ready) launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
                         (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
                         has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
                         has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
@@ -386,7 +392,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   auto launch_dwlog = [&]() {
     c10::hip::HIPStreamGuard guard(side);
     at::mm_out(dWlog, dS.t(), hd2, at::kFloat);
-    at::sum_out(dblog, colsum, {0});
+    if (ds_ready)
+      dblog.copy_(ds_bias);
+    else
+      at::sum_out(dblog, colsum, {0});
     (void)hipEventRecord(ev_done, side.stream());
     if (early && comm_stream != 0)
       (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);

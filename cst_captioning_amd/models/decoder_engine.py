@@ -87,6 +87,12 @@ class _DecoderFn(torch.autograd.Function):
             drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att)
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
+        full = None
+        if want_full:
+            # full (R, T, V) log-probs for the model(feats, seq) API, from the
+            # logits the backward keeps anyway (fp16) and the fp32 LSE
+            V = logit_b.numel()
+            full = (outs[4][:, :, :V].float() - lse.unsqueeze(2)).permute(1, 0, 2).contiguous()
         ctx.eng = eng
         ctx.drop_p, ctx.rng = drop_p, rng
         ctx.shapes = (w_ih.shape, emb_w.shape)
@@ -101,10 +107,12 @@ class _DecoderFn(torch.autograd.Function):
         ctx.mark_non_differentiable(seq)
         if g_xe is None:
             g_xe = torch.zeros(0, device=g_sel.device)
-        return seq, g_sel, g_xe
+        if full is None:
+            full = torch.zeros(0, device=g_sel.device)
+        return seq, g_sel, g_xe, full
 
     @staticmethod
-    def backward(ctx, dseq, dg_sel, dg_xe):
+    def backward(ctx, dseq, dg_sel, dg_xe, dfull):
         if ctx.saved is None:
             raise RuntimeError('decoder forward ran without saving activations')
         R, T, vdiv, want_xe = ctx.save_dims
@@ -117,6 +125,25 @@ class _DecoderFn(torch.autograd.Function):
         g_xe = dg_xe.contiguous() if (want_xe and dg_xe is not None and dg_xe.numel()) else None
         empty = torch.empty(0, device=lse.device)
         n_steps = logits16.shape[0]
+        ds_bias = empty
+        if dfull is not None and dfull.numel():
+            # gradient w.r.t. the full log-probs: dense dS = G - p * sum_v G
+            # (+ the gathered terms), written as bf16 into the logits buffer
+            V = logit_b_numel = eng.V
+            n_sel = g_sel.size(1) if g_sel is not None else 0
+            G = dfull.permute(1, 0, 2).float()  # (n, R, V)
+            if g_sel is not None:
+                G[:n_sel].scatter_add_(2, seq.t()[:n_sel].unsqueeze(2), g_sel.t().unsqueeze(2))
+            if g_xe is not None:
+                tgt = labels[:, 1:1 + n_steps].t().unsqueeze(2)
+                G.scatter_add_(2, tgt, g_xe.t()[:n_steps].unsqueeze(2))
+            p = torch.exp(logits16[:, :, :V].float() - lse.unsqueeze(2))
+            dS = G - p * G.sum(2, keepdim=True)
+            logits16.view(torch.bfloat16)[:, :, :V].copy_(dS)
+            ds_bias = dS.to(torch.bfloat16).float().sum((0, 1))
+            del G, p, dS
+            g_sel = g_xe = None
+            del logit_b_numel
         # input token of every step: it_0 = BOS / labels[:, 0], it_t = seq[:, t-1]
         first = labels[:, :1] if labels is not None else bos.view(-1, 1)
         toks = torch.cat([first, seq[:, :n_steps - 1]], 1).t().reshape(-1)
@@ -145,7 +172,7 @@ class _DecoderFn(torch.autograd.Function):
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
-            ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb)
+            ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias)
         dWx, dWlog, dblog, d_emb, dvg = res[:5]
         if early:
             hook.launch()
@@ -167,10 +194,10 @@ class _DecoderFn(torch.autograd.Function):
         if ctx.has_att:
             d_gv, d_pre, d_wa, d_ba, d_wq = res[5:10]
             return (None, d_wih, d_whh, d_emb, dWlog, dblog, d_gv, d_pre, d_wq, d_wa,
-                    d_ba) + (None,) * 15
+                    d_ba) + (None,) * 16
         nv = R // vdiv
         d_vgate = dvg.view(nv, vdiv, -1).sum(1)
-        return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 20
+        return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 21
 
 
 class DecoderEngine:
@@ -313,7 +340,8 @@ class DecoderEngine:
         return (gv, pre, ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), frames.size(0)
 
     def _run(self, model, feats, labels, modes, want_xe, use_counts, use_unfinished,
-             expand=True, ss_prob=0.0, drop=True, temperature=1.0, bos_rows=None):
+             expand=True, ss_prob=0.0, drop=True, temperature=1.0, bos_rows=None,
+             want_full=False):
         if self.attention:
             att, B = self._att_inputs(model, feats)
             vg = None
@@ -334,12 +362,12 @@ class DecoderEngine:
               m.logit.bias)
         # (inside Function.forward grad mode is off, so decide here)
         diff_in = [t for t in (vg,) + tuple(att) if t is not None] + list(ws)
-        save = torch.is_grad_enabled() and any(t.requires_grad for t in diff_in)
+        save = want_full or (torch.is_grad_enabled() and any(t.requires_grad for t in diff_in))
         return _DecoderFn.apply(vg, *ws, *att, self,
                                 labels.contiguous() if labels is not None else None, bos, R, T,
                                 modes, float(ss_prob), float(drop_p), float(temperature),
                                 self._rng(m.logit.bias.device), S, want_xe, use_counts,
-                                use_unfinished, save)
+                                use_unfinished, save, want_full)
 
     # -- public entry points ------------------------------------------------------
     def rollout(self, model, feats, labels):
@@ -348,8 +376,8 @@ class DecoderEngine:
         T = labels.size(1) - 1
         modes = self._modes(model, T)
         mask_eos = getattr(model, 'mask_after_eos', False)
-        seq, g_sel, _ = self._run(model, feats, labels, modes, want_xe=False, use_counts=True,
-                                  use_unfinished=mask_eos, ss_prob=model.ss_prob)
+        seq, g_sel, _, _ = self._run(model, feats, labels, modes, want_xe=False, use_counts=True,
+                                     use_unfinished=mask_eos, ss_prob=model.ss_prob)
         return seq, g_sel, None
 
     def teacher_forced(self, model, feats, labels):
@@ -357,8 +385,8 @@ class DecoderEngine:
         what CrossEntropyCriterion needs.  Honours scheduled sampling."""
         T = labels.size(1) - 1
         modes = self._modes(model, T, rl=False)
-        _, _, g_xe = self._run(model, feats, labels, modes, want_xe=True, use_counts=True,
-                               use_unfinished=False, ss_prob=model.ss_prob)
+        _, _, g_xe, _ = self._run(model, feats, labels, modes, want_xe=True, use_counts=True,
+                                  use_unfinished=False, ss_prob=model.ss_prob)
         return g_xe
 
     def _modes(self, model, T, rl=True):
@@ -374,13 +402,21 @@ class DecoderEngine:
         return modes
 
     def forward_full(self, model, feats, seq):
-        """``model(feats, seq)`` API: full (R, T, V) log-probs need the plain
-        path; delegate to it."""
-        model.impl = 'torch'
-        try:
-            return model(feats, seq)
-        finally:
-            model.impl = 'hip'
+        """Reference ``forward(feats, seq)`` (``model.py:218-289``) on the
+        engine: (log-probs (R, T, V), sample_seq (R, T-1), sample_logprobs
+        (R, T-1)) with teacher forcing / scheduled sampling / MIXER sampling as
+        the model's setters select.  The log-probs are the kernels' logits
+        (kept in fp16 for the backward) minus the fp32 LSE; gradients w.r.t.
+        them flow through the fused backward as a dense dS.  Difference: when
+        every row has emitted EOS the reference stops early; here the
+        remaining steps are computed on EOS inputs (tokens stay 0)."""
+        T = seq.size(1) - 1
+        modes = self._modes(model, T)
+        mask_eos = getattr(model, 'mask_after_eos', False)
+        s_seq, g_sel, _, full = self._run(model, feats, seq, modes, want_xe=True,
+                                          use_counts=True, use_unfinished=mask_eos,
+                                          ss_prob=model.ss_prob, want_full=True)
+        return full, s_seq, g_sel
 
     @torch.no_grad()
     def sample(self, model, feats, opt):
@@ -389,9 +425,9 @@ class DecoderEngine:
         expand = opt.get('expand_feat', 0) == 1
         T = model.seq_length - 1
         modes = [SEL_GREEDY if sample_max == 1 else SEL_SAMPLE] * (T - 1)
-        seq, lp, _ = self._run(model, feats, None, modes, want_xe=False, use_counts=False,
-                               use_unfinished=True, expand=expand, drop=False,
-                               temperature=temperature)
+        seq, lp, _, _ = self._run(model, feats, None, modes, want_xe=False, use_counts=False,
+                                  use_unfinished=True, expand=expand, drop=False,
+                                  temperature=temperature)
         return seq, lp
 
     @torch.no_grad()

@@ -117,6 +117,10 @@ class Trainer:
         if engine is not None:
             engine.attach_optimizer(self)
         self.scorer = None
+        # PyTorch decoder path at --precision bf16: torch autocast (bf16 GEMMs /
+        # LSTM, fp32 softmax), the same-precision baseline of the fused engine
+        self.autocast_bf16 = (engine is None and self.device.type == 'cuda'
+                              and getattr(opt, 'precision', 'bf16') == 'bf16')
         self.timer = PhaseTimer(enabled=bool(getattr(opt, 'profile_phases', 0)))
         self.infos = {'iter': 0, 'epoch': 0, 'start_epoch': 0, 'best_score': float('-inf'),
                       'best_iter': 0, 'best_epoch': opt.max_epochs}
@@ -242,10 +246,11 @@ class Trainer:
         m.train()
         self.optimizer.zero_grad()
         m.set_seq_per_img(self.train_loader.get_seq_per_img())
-        if self.rl_training:
-            loss, extra = self.rl_loss(data, scb)
-        else:
-            loss, extra = self.xe_loss(data)
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=self.autocast_bf16):
+            if self.rl_training:
+                loss, extra = self.rl_loss(data, scb)
+            else:
+                loss, extra = self.xe_loss(data)
         loss.backward()
         self.timer.mark('backward')
         skip = None

@@ -352,3 +352,33 @@ def test_trainer_direct_gradient_slots_match_torch():
         err = (p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)
         assert err < 0.06, (name, float(err))
 
+
+
+def test_forward_full_logprobs_and_gradient_match_torch():
+    """``model(feats, seq)`` on the engine: full (R, T, V) log-probs and the
+    gradient of an arbitrary function of them (dense dS through the fused
+    backward) vs the PyTorch path."""
+    ds, opt, model, loader = _tiny(V=700, H=128, seed=6)
+    model.impl = 'hip'
+    model._engine = _engine(model, opt)
+    model.train()
+    model.set_seq_per_img(5)
+    data = loader.get_batch()
+    labels = data['labels']
+    ref = copy.deepcopy(model)
+    ref.impl = 'torch'
+    ref._engine = None
+    full, s_seq, s_lp = model(data['feats'], labels)
+    pr, r_seq, r_lp = ref(data['feats'], labels)
+    n = pr.size(1)
+    assert full.shape[0] == pr.shape[0] and full.shape[2] == pr.shape[2]
+    assert (full[:, :n] - pr).abs().max().item() < 0.08
+    assert torch.equal(s_seq[:, :r_seq.size(1)], r_seq)
+    wgt = torch.randn_like(pr) * (torch.rand_like(pr) < 0.05)  # sparse-ish dense weights
+    (full[:, :n] * wgt).sum().backward()
+    (pr * wgt).sum().backward()
+    for (name, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+        if q.grad is None or q.grad.norm() == 0:
+            continue
+        err = (p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)
+        assert err < 0.06, (name, float(err))
