@@ -87,11 +87,15 @@ struct DmaSrc {
   int ksplit;
 };
 
+// tid: thread index within the 256-thread group that owns this main loop
+// (a block may run several groups on disjoint LDS, e.g. an in-block split-K;
+// every group must run the same number of K-tiles: the barriers are
+// block-wide).
 template <class TL>
-__device__ __forceinline__ void gemm_nt_mainloop(int nk, const DmaSrc<TL::BM / 32>& a,
-                                                 const DmaSrc<TL::BN / 32>& b, char* lds,
-                                                 f32x16 (&acc)[TL::TM][TL::TN]) {
-  const int tid = threadIdx.x, lane = tid & 63;
+__device__ __forceinline__ void gemm_nt_mainloop_g(int tid, int nk, const DmaSrc<TL::BM / 32>& a,
+                                                   const DmaSrc<TL::BN / 32>& b, char* lds,
+                                                   f32x16 (&acc)[TL::TM][TL::TN]) {
+  const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
 
@@ -156,11 +160,20 @@ __device__ __forceinline__ void gemm_nt_mainloop(int nk, const DmaSrc<TL::BM / 3
   __syncthreads();  // all waves done with the staging buffers (epilogue reuses LDS)
 }
 
+template <class TL>
+__device__ __forceinline__ void gemm_nt_mainloop(int nk, const DmaSrc<TL::BM / 32>& a,
+                                                 const DmaSrc<TL::BN / 32>& b, char* lds,
+                                                 f32x16 (&acc)[TL::TM][TL::TN]) {
+  gemm_nt_mainloop_g<TL>((int)threadIdx.x, nk, a, b, lds, acc);
+}
+
 // Accumulators -> fp32 C tile in LDS (row stride TL::CSTRIDE), adding colbias(col).
 template <class TL, class ColBias>
 __device__ __forceinline__ void store_acc_to_lds(const f32x16 (&acc)[TL::TM][TL::TN],
-                                                 float* C, ColBias colbias) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+                                                 float* C, ColBias colbias,
+                                                 int tid = -1) {
+  if (tid < 0) tid = (int)threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
 #pragma unroll
   for (int j = 0; j < TL::TN; ++j) {

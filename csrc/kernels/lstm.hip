@@ -25,8 +25,8 @@
 namespace cst {
 
 constexpr int LB_M = 128, LB_N = 64;
-// backward step pipeline depth (48 KB of LDS: co-resides with the dWlog GEMM
-// that runs concurrently on a side stream; 6 stages measured no faster)
+// backward step pipeline depth per K group (48 KB of LDS each; 6 stages
+// measured no faster)
 constexpr int LSTM_BWD_STAGES = 3;
 
 __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
@@ -142,71 +142,68 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
 //   cell backward of step t in the epilogue -> dG_t (bf16, packed gates),
 //   dc_carry <- dc * f.
 // One tile = BM rows x 64 hidden units: only (R/BM) x (H/64) = 160 tiles at
-// R = 1280, H = 512 -- fewer than the 256 CUs, each a 32-deep K loop.  So the
-// K = 4H (+A) reduction is split S ways (split-K): S blocks per tile each
-// reduce a K range, publish their fp32 partial tile to `ws`, and the LAST of
-// them to arrive (per-tile atomic counter, reset by that block for the next
-// launch) sums the partials and runs the cell epilogue.  S = 1 keeps the
-// original single-pass kernel with every epilogue operand prefetched before
-// the main loop.
-template <int BM>
+// R = 1280, H = 512 -- fewer than the 256 CUs, each a 32-deep K loop (the
+// reverse loop is latency-bound).  So each block runs GROUPS = 2 groups of 4
+// waves that split the tile's K range (in-block split-K): both groups stream
+// their half of K through their own LDS pipeline, leave their fp32 partial
+// tiles in LDS, and all 8 waves run the cell epilogue on the sum.  No global
+// workspace, no atomics, and every epilogue operand is prefetched before the
+// main loop.
+template <int BM, int GROUPS>
 __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, int hu,
                                                   const uint16_t* __restrict__ gates,
                                                   const float* __restrict__ c_t,
                                                   const float* __restrict__ c_prev,
                                                   const float* __restrict__ dc_carry,
                                                   const float* __restrict__ dh_logit,
-                                                  const float* __restrict__ dh_logit2,
                                                   uint2* pg, float* pc, float* pcp, float* pdc,
                                                   float* pdl) {
-  constexpr int RPT = BM / 4;
+  constexpr int RG = 4 * GROUPS, RPT = BM / RG;
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
-    const int r = min(r0 + rg + 4 * i, R - 1);
+    const int r = min(r0 + rg + RG * i, R - 1);
     const int64_t o = (int64_t)r * H + hu;
     pg[i] = *reinterpret_cast<const uint2*>(gates + (int64_t)r * 4 * H + 4 * hu);
     pc[i] = c_t[o];
     pcp[i] = c_prev ? c_prev[o] : 0.f;
     pdc[i] = dc_carry[o];
-    pdl[i] = dh_logit[o] + (dh_logit2 ? dh_logit2[o] : 0.f);  // split-K partials of dHd
+    pdl[i] = dh_logit[o];
   }
 }
 
-template <int BM, int STAGES = LSTM_BWD_STAGES>
-__global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
+template <int BM, int STAGES, int GROUPS>
+__global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
-    const float* __restrict__ dh_logit, const float* __restrict__ dh_logit2,
-    float* __restrict__ dc_carry, const uint16_t* __restrict__ gates,
-    const float* __restrict__ c_t, const float* __restrict__ c_prev, int R, int H, float drop_p,
-    const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int S,
-    float* __restrict__ ws, int* __restrict__ tile_cnt) {
+    const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
+    const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
+    const float* __restrict__ c_prev, int R, int H, float drop_p,
+    const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD) {
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  __shared__ int s_last;
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
-  const int tile = blockIdx.x % n_tiles, split = blockIdx.x / n_tiles;
-  const int b = xcd_remap_l(tile, n_tiles);
+  const int b = xcd_remap_l(blockIdx.x, n_tiles);
   const int ut = b / n_rt, rt = b % n_rt;
   const int r0 = rt * BM, u0 = ut * 64;
   const int nk_all = dg_next != nullptr ? KD / 64 : 0;  // KD = 4H (+ A with attention)
-  const int k0 = split * nk_all / S, nk = (split + 1) * nk_all / S - k0;
+  const int grp = threadIdx.x >> 8, gtid = threadIdx.x & 255;
+  const int nkg = nk_all / GROUPS, k0 = grp * nkg;  // (launcher: nk_all % GROUPS == 0)
   const int tid = threadIdx.x, u = tid & 63, rg = tid >> 6;
   const int hu = u0 + u;
-  constexpr int RPT = BM / 4;
+  constexpr int RG = 4 * GROUPS, RPT = BM / RG;
 
   uint2 pg[RPT];
   float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
-  if (S == 1)  // single pass: the epilogue operands' latency hides under the GEMM
-    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, dh_logit2, pg, pc, pcp,
-                          pdc, pdl);
+  // the epilogue operands' latency hides under the GEMM
+  lstm_bwd_load_epi<BM, GROUPS>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, pg,
+                                pc, pcp, pdc, pdl);
 
   f32x16 acc[TL::TM][TL::TN];
-  {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (nkg > 0) {
+    const int lane = gtid & 63, w = gtid >> 6;
     DmaSrc<BM / 32> a;
     DmaSrc<64 / 32> bsrc;
-    a.r0 = a.r1 = make_rsrc(dg_next ? dg_next : whhT, (int64_t)R * KD * 2);
-    a.ksplit = nk;
+    a.r0 = a.r1 = make_rsrc(dg_next, (int64_t)R * KD * 2);
+    a.ksplit = nkg;
 #pragma unroll
     for (int i = 0; i < BM / 32; ++i) {
       const int row = dma_row(w, i, lane);
@@ -214,68 +211,36 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
       a.voff1[i] = a.voff0[i];
     }
     bsrc.r0 = bsrc.r1 = make_rsrc(whhT, (int64_t)H * KD * 2);
-    bsrc.ksplit = nk;
+    bsrc.ksplit = nkg;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = dma_row(w, i, lane);
       bsrc.voff0[i] = (u0 + row) * KD * 2 + k0 * 128 + dma_chunk(row, lane) * 16;
       bsrc.voff1[i] = bsrc.voff0[i];
     }
-    gemm_nt_mainloop<TL>(nk, a, bsrc, lds, acc);
+    gemm_nt_mainloop_g<TL>(gtid, nkg, a, bsrc, lds + grp * TL::STAGES * TL::STAGE_BYTES, acc);
+  } else {
+#pragma unroll
+    for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TL::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   }
-  float* C = reinterpret_cast<float*>(lds);
-  store_acc_to_lds<TL>(acc, C, [](int) { return 0.f; });
+  float* C = reinterpret_cast<float*>(lds);  // GROUPS partial tiles of BM x CSTRIDE
+  store_acc_to_lds<TL>(acc, C + grp * BM * TL::CSTRIDE, [](int) { return 0.f; }, gtid);
   __syncthreads();
-
-  if (S > 1) {
-    constexpr int TE = BM * 64;
-    float* mine = ws + ((int64_t)tile * S + split) * TE;
-    for (int i = 4 * tid; i < TE; i += 4 * 256) {
-      const float* c = C + (i >> 6) * TL::CSTRIDE + (i & 63);
-      *reinterpret_cast<float4*>(mine + i) = make_float4(c[0], c[1], c[2], c[3]);
-    }
-    __threadfence();  // release: the partial is visible device-wide before the count
-    __syncthreads();
-    if (tid == 0) s_last = atomicAdd(&tile_cnt[tile], 1) == S - 1;
-    __syncthreads();
-    if (!s_last) return;
-    // acquire: the device-scope fence also invalidates this CU's L1, so the
-    // plain (batched, non-serialised) loads below see the other blocks' partials
-    __threadfence();
-    lstm_bwd_load_epi<BM>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, dh_logit2, pg, pc, pcp,
-                          pdc, pdl);
-    const float4* wsv = reinterpret_cast<const float4*>(ws + (int64_t)tile * S * TE);
-    constexpr int PER = TE / 4 / 256;  // float4 per thread per partial
-    float4 sum[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) sum[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < S; ++k) {
-      if (k == split) continue;
-      float4 v[PER];
-#pragma unroll
-      for (int j = 0; j < PER; ++j) v[j] = wsv[k * (TE / 4) + tid + 256 * j];
-#pragma unroll
-      for (int j = 0; j < PER; ++j)
-        sum[j].x += v[j].x, sum[j].y += v[j].y, sum[j].z += v[j].z, sum[j].w += v[j].w;
-    }
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = 4 * (tid + 256 * j);
-      float* c = C + (i >> 6) * TL::CSTRIDE + (i & 63);
-      c[0] += sum[j].x, c[1] += sum[j].y, c[2] += sum[j].z, c[3] += sum[j].w;
-    }
-    if (tid == 0) tile_cnt[tile] = 0;  // ready for the next launch
-    __syncthreads();
-  }
 
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
-    const int row = rg + 4 * i, r = r0 + row;
+    const int row = rg + RG * i, r = r0 + row;
     if (r < R) {
       const int64_t o = (int64_t)r * H + hu;
-      float dh = C[row * TL::CSTRIDE + u];
+      float dh = 0.f;
+#pragma unroll
+      for (int g = 0; g < GROUPS; ++g) dh += C[(g * BM + row) * TL::CSTRIDE + u];
       const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
       if (keep) dh += pdl[i] * inv_keep;
       const uint2 gp = pg[i];
@@ -298,25 +263,43 @@ __global__ __launch_bounds__(256, 2) void lstm_step_bwd_kernel(
 
 int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
+template <int GROUPS, int STAGES = LSTM_BWD_STAGES>
+static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT,
+                                   const float* dh_logit, float* dc_carry, const uint16_t* gates,
+                                   const float* c_t, const float* c_prev, int R, int H,
+                                   float drop_p, const uint32_t* rng, int step, uint16_t* dG,
+                                   int KD, hipStream_t stream) {
+  constexpr int BM = 64;
+  using TL = Tile<BM, 64, STAGES>;
+  constexpr int LDS = GROUPS * TL::STAGES * TL::STAGE_BYTES > GROUPS * BM * TL::CSTRIDE * 4
+                          ? GROUPS * TL::STAGES * TL::STAGE_BYTES
+                          : GROUPS * BM * TL::CSTRIDE * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, STAGES, GROUPS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  const int n = (H / 64) * ((R + BM - 1) / BM);
+  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS>), dim3(n),
+                     dim3(256 * GROUPS), LDS, stream, dg_next, whhT, dh_logit, dc_carry, gates,
+                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD);
+  post_launch("lstm_step_bwd_kernel", stream);
+}
+
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
-                          int step, uint16_t* dG, int KD, hipStream_t stream, int S, float* ws,
-                          int* tile_cnt, const float* dh_logit2) {
-  constexpr int BM = 64;
-  using TL = Tile<BM, 64, LSTM_BWD_STAGES>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, LSTM_BWD_STAGES>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, TL::LDS_BYTES);
-    attr_set = true;
-  }
-  if (dg_next == nullptr || ws == nullptr || tile_cnt == nullptr) S = 1;  // no K to split
-  const int n = (H / 64) * ((R + BM - 1) / BM) * S;
-  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, LSTM_BWD_STAGES>), dim3(n), dim3(256),
-                     TL::LDS_BYTES, stream, dg_next, whhT, dh_logit, dh_logit2, dc_carry, gates,
-                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, S, ws, tile_cnt);
-  post_launch("lstm_step_bwd_kernel", stream);
+                          int step, uint16_t* dG, int KD, hipStream_t stream) {
+  // two K groups per block when the K-tiles split evenly
+  // (measured per step: 1 group 4.66 ms, 2 groups 4.54 ms, 4 groups with 2
+  // LDS stages each 4.51 vs 4.47 ms for 2 groups on another box)
+  if ((KD / 64) % 2 == 0)
+    launch_lstm_step_bwd_g<2>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
+                              drop_p, rng, step, dG, KD, stream);
+  else
+    launch_lstm_step_bwd_g<1>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
+                              drop_p, rng, step, dG, KD, stream);
 }
 
 // 128-row tiles x 64 packed gate columns, 3 LDS stages (72 KB, 2 blocks per CU)

@@ -97,15 +97,11 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* p
 
 // dg_next / dG rows have stride KD: 4H gate columns (+ A attention-query
 // columns, matched by extra whhT columns [W_hh^T | W_q^T] of width KD)
-// S > 1: split-K over S blocks per tile; ws holds lstm_bwd_tiles(R, H) * S * 64 * 64
-// floats and tile_cnt lstm_bwd_tiles(R, H) zero-initialised ints (self-resetting).
 int lstm_bwd_tiles(int R, int H);
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
-                          int step, uint16_t* dG, int KD, hipStream_t stream, int S = 1,
-                          float* ws = nullptr, int* tile_cnt = nullptr,
-                          const float* dh_logit2 = nullptr);  // second dHd partial (or null)
+                          int step, uint16_t* dG, int KD, hipStream_t stream);
 
 // attention.hip (temporal attention over num_chunks frames)
 int att_groups(int vdiv);

@@ -69,7 +69,7 @@ class _DecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, vgate, w_ih, w_hh, emb_w, logit_w, logit_b, att_gv, att_pre, att_wq,
                 att_wa, att_ba, eng, labels, bos, R, T, modes, ss_prob, drop_p, temperature, rng,
-                vdiv, want_xe, use_counts, use_unfinished, save):
+                vdiv, want_xe, use_counts, use_unfinished, save, want_full):
         has_att = att_gv is not None
         dev = logit_b.device
         att = []
