@@ -161,6 +161,81 @@ __device__ __forceinline__ uint32_t rng_seed(const uint32_t* rng, int slot) {
   return rng != nullptr ? rng[slot] : 0u;
 }
 
+// ---- recurrent cells ------------------------------------------------------------
+// Every cell is computed from 4 packed pre-activation slots per hidden unit
+// (packed row 4u + g of the gate GEMMs; the caller packs the weights):
+//   LSTM (PyTorch i, f, g, o):  c = f c' + i g,  h = o tanh(c)
+//   GRU  (PyTorch r, z, n):     slots (r, z, n_x, n_h) -- the input part of n
+//        (x / video terms) and its recurrent part (W_hn h) stay separate:
+//        n = tanh(n_x + r n_h),  h = (1 - z) n + z h'
+//   RNN  (tanh):                slot 0 only, h = tanh(a0)
+// The "c" state buffers carry h in fp32 for GRU / RNN.  Saved gate slots
+// (bf16) for the backward: LSTM (i, f, g, o); GRU (r, z, n, n_h); RNN (h, -).
+enum CellType : int { CELL_LSTM = 0, CELL_GRU = 1, CELL_RNN_TANH = 2 };
+
+struct CellFwd {
+  float h, c, s0, s1, s2, s3;
+};
+__device__ __forceinline__ CellFwd cell_fwd(int cell, float a0, float a1, float a2, float a3,
+                                            float cp) {
+  CellFwd o;
+  if (cell == CELL_LSTM) {
+    const float gi = sigmoidf_(a0), gf = sigmoidf_(a1), gg = tanhf_(a2), go = sigmoidf_(a3);
+    o.c = gf * cp + gi * gg;
+    o.h = go * tanhf_(o.c);
+    o.s0 = gi, o.s1 = gf, o.s2 = gg, o.s3 = go;
+  } else if (cell == CELL_GRU) {
+    const float r = sigmoidf_(a0), z = sigmoidf_(a1);
+    const float n = tanhf_(a2 + r * a3);
+    o.h = (1.f - z) * n + z * cp;
+    o.c = o.h;
+    o.s0 = r, o.s1 = z, o.s2 = n, o.s3 = a3;
+  } else {
+    o.h = tanhf_(a0);
+    o.c = o.h;
+    o.s0 = o.h, o.s1 = o.s2 = o.s3 = 0.f;
+  }
+  return o;
+}
+
+// Cell backward: dh = gradient reaching h_t (recurrent GEMM + logit path),
+// carry = the state gradient carried from step t+1 (LSTM: into c_t; GRU /
+// RNN: into h_t); c_t / cp = this / previous step's state.  Returns the
+// 4 packed slot gradients and the carry for step t-1.
+struct CellBwd {
+  float d0, d1, d2, d3, carry;
+};
+__device__ __forceinline__ CellBwd cell_bwd(int cell, float dh, float carry, float s0, float s1,
+                                            float s2, float s3, float c_t, float cp) {
+  CellBwd o;
+  if (cell == CELL_LSTM) {
+    const float tc = tanhf_(c_t);
+    const float dc = carry + dh * s3 * (1.f - tc * tc);
+    o.d0 = dc * s2 * s0 * (1.f - s0);
+    o.d1 = dc * cp * s1 * (1.f - s1);
+    o.d2 = dc * s0 * (1.f - s2 * s2);
+    o.d3 = dh * tc * s3 * (1.f - s3);
+    o.carry = dc * s1;
+  } else if (cell == CELL_GRU) {
+    const float r = s0, z = s1, n = s2, nh = s3;
+    const float d = dh + carry;
+    const float dz = d * (cp - n);
+    const float da2 = d * (1.f - z) * (1.f - n * n);
+    const float dr = da2 * nh;
+    o.d0 = dr * r * (1.f - r);
+    o.d1 = dz * z * (1.f - z);
+    o.d2 = da2;
+    o.d3 = da2 * r;
+    o.carry = d * z;
+  } else {
+    const float d = dh + carry;
+    o.d0 = d * (1.f - s0 * s0);
+    o.d1 = o.d2 = o.d3 = 0.f;
+    o.carry = 0.f;
+  }
+  return o;
+}
+
 // Keep-mask of dropout on element (row, col) of step t: a counter hash, so the
 // backward regenerates exactly the forward's mask.
 __device__ __forceinline__ bool dropout_keep(uint32_t seed, int step, int row, int col,

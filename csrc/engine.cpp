@@ -83,8 +83,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         std::vector<int64_t> modes, double ss_prob,
                                         double drop_p, double temperature, at::Tensor rng,
                                         bool save, bool want_xe, bool use_counts,
-                                        bool use_unfinished, std::vector<at::Tensor> att) {
+                                        bool use_unfinished, std::vector<at::Tensor> att,
+                                        int64_t cell) {
   check_cuda(wx, "wx");
+  TORCH_CHECK(cell >= 0 && cell <= 2, "cell: 0 lstm, 1 gru, 2 rnn (tanh)");  // CellType (common.h)
   check_cuda(emb, "emb");
   check_cuda(wlog, "wlog");
   check_cuda(blog, "blog");
@@ -230,7 +232,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                        ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(zeros_h.data_ptr()),
                        zeros_c.data_ptr<float>(), VG, VDIV, (int)R,
                        (int)H, WHH, h_buf(0), c_buf(0), hd_buf(0), (int)(H + HAUG), (float)drop_p,
-                       RNG, 0, gates_buf(0), st);
+                       RNG, 0, gates_buf(0), st, nullptr, (int)cell);
   // Steps t >= 0: ONE launch runs the vocab projection of step t together with
   // the recurrent GEMM of step t+1 (pre = h_t W_hh^T + vgate), then the combine
   // picks token t+1 and applies step t+1's cell epilogue (pre + P[token]).
@@ -265,7 +267,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       TORCH_CHECK(choose, "internal: a next step needs a chosen token");
       cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_buf(t), c_buf(t + 1),
                       h_buf(t + 1), hd_buf(t + 1), (int)(H + HAUG), gates_buf(t + 1), (int)H,
-                      (float)drop_p, (int)(t + 1)};
+                      (float)drop_p, (int)(t + 1), (int)cell};
     }
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                          choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
@@ -317,7 +319,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor dg_xe, double drop_p, at::Tensor rng,
                                          at::Tensor out_wlog, at::Tensor out_blog,
                                          int64_t comm_stream, std::vector<at::Tensor> att,
-                                         at::Tensor out_emb, at::Tensor ds_bias) {
+                                         at::Tensor out_emb, at::Tensor ds_bias, int64_t cell) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -450,7 +452,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
         c_all[t].data_ptr<float>(), t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R,
         (int)H, (float)drop_p, RNG, (int)t, reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()),
-        (int)KD, st);
+        (int)KD, st, (int)cell);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
@@ -543,22 +545,22 @@ at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::stri
   return out;
 }
 
-// Shadow-copy segments from Python: meta = int64 CPU (n, 7) rows {off, n,
-// kind, cols, H, E, ld2}; dsts = 2 tensors per row (dst, dst2; undefined or
+// Shadow-copy segments from Python: meta = int64 CPU (n, 8) rows {off, n,
+// kind, cols, H, E, ld2, slots}; dsts = 2 tensors per row (dst, dst2; undefined or
 // empty when unused).
 static ShadowSegs make_shadow_segs(const at::Tensor& meta, const std::vector<at::Tensor>& dsts) {
   ShadowSegs ss{};
   if (!meta.defined() || meta.numel() == 0) return ss;
   TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.dim() == 2 &&
-                  meta.size(1) == 7 && meta.size(0) <= SHADOW_MAX_SEGS,
-              "shadow meta must be an int64 CPU (n <= ", SHADOW_MAX_SEGS, ", 7) tensor");
+                  meta.size(1) == 8 && meta.size(0) <= SHADOW_MAX_SEGS,
+              "shadow meta must be an int64 CPU (n <= ", SHADOW_MAX_SEGS, ", 8) tensor");
   TORCH_CHECK((int64_t)dsts.size() == 2 * meta.size(0), "two destination tensors per segment");
   auto m = meta.accessor<int64_t, 2>();
   ss.n = (int)meta.size(0);
   for (int k = 0; k < ss.n; ++k) {
     ShadowSeg& g = ss.s[k];
     g.off = m[k][0], g.n = m[k][1], g.kind = (int)m[k][2], g.cols = (int)m[k][3];
-    g.H = (int)m[k][4], g.E = (int)m[k][5], g.ld2 = (int)m[k][6];
+    g.H = (int)m[k][4], g.E = (int)m[k][5], g.ld2 = (int)m[k][6], g.slots = (int)m[k][7];
     const at::Tensor& d = dsts[2 * k];
     const at::Tensor& d2 = dsts[2 * k + 1];
     TORCH_CHECK(d.is_cuda() && d.scalar_type() == at::kBFloat16, "shadow dst must be bf16 GPU");
@@ -567,10 +569,17 @@ static ShadowSegs make_shadow_segs(const at::Tensor& meta, const std::vector<at:
     if (g.kind == SHADOW_PLAIN) {
       TORCH_CHECK(d.numel() >= g.n, "plain shadow too small");
     } else {
-      TORCH_CHECK(g.H > 0 && g.cols > 0 && g.n % g.cols == 0 && g.n / g.cols == 4 * g.H &&
+      const int64_t rows = g.cols > 0 ? g.n / g.cols : 0;
+      const int64_t gates = g.H > 0 ? rows / g.H : 0;
+      TORCH_CHECK(g.H > 0 && g.cols > 0 && g.n % g.cols == 0 && rows % g.H == 0 &&
+                      (gates == 1 || gates == 3 || gates == 4) &&
                       d.numel() >= 4 * (int64_t)g.H * (g.E + g.H),
-                  "LSTM shadow segment shape");
-      if (g.kind == SHADOW_LSTM_HH)
+                  "gate-weight shadow segment shape");
+      for (int q = 0; q < gates; ++q)
+        for (int q2 = 0; q2 < q; ++q2)
+          TORCH_CHECK(((g.slots >> (2 * q)) & 3) != ((g.slots >> (2 * q2)) & 3),
+                      "gate slot map must be injective");
+      if (g.kind == SHADOW_GATES_HH)
         TORCH_CHECK(g.dst2 != nullptr && g.cols == g.H && d2.numel() >= 4 * (int64_t)g.H * g.ld2,
                     "W_hh shadow needs its packed copy");
     }
@@ -614,7 +623,7 @@ void refresh_shadows(at::Tensor p, at::Tensor shadow_meta, std::vector<at::Tenso
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,
-                                    std::vector<at::Tensor> att) {
+                                    std::vector<at::Tensor> att, int64_t cell) {
   check_cuda(wx, "wx");
   check_cuda(vgate, "vgate");
   TORCH_CHECK(K >= 1 && K <= 16, "beam_size must be in [1, 16]");
@@ -688,7 +697,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                          has_att ? 1 : (int)K, (int)R, (int)H, WHH,
                          reinterpret_cast<uint16_t*>(ho.data_ptr()), co.data_ptr<float>(), nullptr,
                          (int)H, 0.f, nullptr, (int)t, nullptr, st,
-                         t >= 1 ? parent.data_ptr<int>() : nullptr);
+                         t >= 1 ? parent.data_ptr<int>() : nullptr, (int)cell);
     launch_vocab_fwd(reinterpret_cast<const uint16_t*>(ho.data_ptr()), (int)H, (int)R, (int)H, W,
                      blog.data_ptr<float>(), (int)V,
                      reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl, part.data_ptr(),

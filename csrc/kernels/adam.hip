@@ -62,9 +62,12 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_sumsq_kernel(const float* _
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
-// packed gate row of original LSTM weight row g*H + u: 4u + g
-__device__ __forceinline__ int64_t packed_gate_row(int64_t row, int H) {
-  return (row % H) * 4 + row / H;
+// packed gate row of source weight row g*H + u: 4u + slot(g), slot(g) = bits
+// [2g, 2g + 2) of the segment's slot map (LSTM 0xE4: i,f,g,o -> 0,1,2,3; GRU
+// W_ih 0x24: r,z,n -> 0,1,2; GRU W_hh 0x34: r,z,n -> 0,1,3; RNN 0x0)
+__device__ __forceinline__ int64_t packed_gate_row(int64_t row, int H, int slots) {
+  const int g = (int)(row / H);
+  return (row - (int64_t)g * H) * 4 + ((slots >> (2 * g)) & 3);
 }
 
 __device__ __forceinline__ void shadow_store(const ShadowSegs& ss, int64_t e, float val) {
@@ -79,10 +82,10 @@ __device__ __forceinline__ void shadow_store(const ShadowSegs& ss, int64_t e, fl
       g.dst[j] = b;
     } else {
       const int64_t row = j / g.cols, col = j - row * g.cols;
-      const int64_t pr = packed_gate_row(row, g.H);
-      if (g.kind == SHADOW_LSTM_IH) {
+      const int64_t pr = packed_gate_row(row, g.H, g.slots);
+      if (g.kind == SHADOW_GATES_IH) {
         if (col < g.E) g.dst[pr * (g.E + g.H) + col] = b;
-      } else {  // SHADOW_LSTM_HH
+      } else {  // SHADOW_GATES_HH
         g.dst[pr * (g.E + g.H) + g.E + col] = b;
         g.dst2[pr * g.ld2 + col] = b;
       }

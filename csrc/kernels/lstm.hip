@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     const float* __restrict__ vgate, int vgate_div, int R, int H,
     const uint16_t* __restrict__ whh, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
     uint16_t* __restrict__ hdrop_out, int ldh, float drop_p, const uint32_t* __restrict__ rng,
-    int step, uint16_t* __restrict__ gates_out, const int* __restrict__ row_map) {
+    int step, uint16_t* __restrict__ gates_out, const int* __restrict__ row_map, int cell) {
   using LTile = Tile<BM, LB_N, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_nt = (4 * H) / LB_N, n_rt = (R + BM - 1) / BM;
@@ -111,14 +111,11 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     if (r < R) {
       const float4 pre = *reinterpret_cast<const float4*>(C + row * LTile::CSTRIDE + 4 * u);
       const float4 vg = pre_vg[i], px = pre_px[i];
-      const float gi = sigmoidf_(pre.x + vg.x + px.x);
-      const float gf = sigmoidf_(pre.y + vg.y + px.y);
-      const float gg = tanhf_(pre.z + vg.z + px.z);
-      const float go = sigmoidf_(pre.w + vg.w + px.w);
+      const CellFwd cf = cell_fwd(cell, pre.x + vg.x + px.x, pre.y + vg.y + px.y,
+                                  pre.z + vg.z + px.z, pre.w + vg.w + px.w, pre_c[i]);
       const int64_t o = (int64_t)r * H + hu;
-      const float c = gf * pre_c[i] + gi * gg;
-      const float hv = go * tanhf_(c);
-      c_out[o] = c;
+      const float hv = cf.h;
+      c_out[o] = cf.c;
       h_out[o] = f2bf(hv);
       if (hdrop_out) {
         const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
@@ -128,8 +125,8 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
       }
       if (gates_out) {
         uint2 pk;
-        pk.x = (uint32_t)f2bf(gi) | ((uint32_t)f2bf(gf) << 16);
-        pk.y = (uint32_t)f2bf(gg) | ((uint32_t)f2bf(go) << 16);
+        pk.x = (uint32_t)f2bf(cf.s0) | ((uint32_t)f2bf(cf.s1) << 16);
+        pk.y = (uint32_t)f2bf(cf.s2) | ((uint32_t)f2bf(cf.s3) << 16);
         *reinterpret_cast<uint2*>(gates_out + (int64_t)r * 4 * H + n0 + 4 * u) = pk;
       }
     }
@@ -177,7 +174,7 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
     const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p,
-    const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD) {
+    const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int cell) {
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
@@ -244,18 +241,12 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
       const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
       if (keep) dh += pdl[i] * inv_keep;
       const uint2 gp = pg[i];
-      const float gi = bf2f(gp.x & 0xffff), gf = bf2f(gp.x >> 16);
-      const float gg = bf2f(gp.y & 0xffff), go = bf2f(gp.y >> 16);
-      const float tc = tanhf_(pc[i]);
-      const float dc = pdc[i] + dh * go * (1.f - tc * tc);
-      const float dpi = dc * gg * gi * (1.f - gi);
-      const float dpf = dc * pcp[i] * gf * (1.f - gf);
-      const float dpg = dc * gi * (1.f - gg * gg);
-      const float dpo = dh * tc * go * (1.f - go);
-      dc_carry[o] = dc * gf;
+      const CellBwd cb = cell_bwd(cell, dh, pdc[i], bf2f(gp.x & 0xffff), bf2f(gp.x >> 16),
+                                  bf2f(gp.y & 0xffff), bf2f(gp.y >> 16), pc[i], pcp[i]);
+      dc_carry[o] = cb.carry;
       uint2 pk;
-      pk.x = (uint32_t)f2bf(dpi) | ((uint32_t)f2bf(dpf) << 16);
-      pk.y = (uint32_t)f2bf(dpg) | ((uint32_t)f2bf(dpo) << 16);
+      pk.x = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
+      pk.y = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
       *reinterpret_cast<uint2*>(dG + (int64_t)r * KD + 4 * hu) = pk;
     }
   }
@@ -268,7 +259,7 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
                                    const float* dh_logit, float* dc_carry, const uint16_t* gates,
                                    const float* c_t, const float* c_prev, int R, int H,
                                    float drop_p, const uint32_t* rng, int step, uint16_t* dG,
-                                   int KD, hipStream_t stream) {
+                                   int KD, hipStream_t stream, int cell) {
   constexpr int BM = 64;
   using TL = Tile<BM, 64, STAGES>;
   constexpr int LDS = GROUPS * TL::STAGES * TL::STAGE_BYTES > GROUPS * BM * TL::CSTRIDE * 4
@@ -283,23 +274,23 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
   const int n = (H / 64) * ((R + BM - 1) / BM);
   hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS>), dim3(n),
                      dim3(256 * GROUPS), LDS, stream, dg_next, whhT, dh_logit, dc_carry, gates,
-                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD);
+                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell);
   post_launch("lstm_step_bwd_kernel", stream);
 }
 
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
-                          int step, uint16_t* dG, int KD, hipStream_t stream) {
+                          int step, uint16_t* dG, int KD, hipStream_t stream, int cell) {
   // two K groups per block when the K-tiles split evenly
   // (measured per step: 1 group 4.66 ms, 2 groups 4.54 ms, 4 groups with 2
   // LDS stages each 4.51 vs 4.47 ms for 2 groups on another box)
   if ((KD / 64) % 2 == 0)
     launch_lstm_step_bwd_g<2>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream);
+                              drop_p, rng, step, dG, KD, stream, cell);
   else
     launch_lstm_step_bwd_g<1>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream);
+                              drop_p, rng, step, dG, KD, stream, cell);
 }
 
 // 128-row tiles x 64 packed gate columns, 3 LDS stages (72 KB, 2 blocks per CU)
@@ -308,7 +299,7 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* p
                           int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
                           const uint32_t* rng, int step, uint16_t* gates_out, hipStream_t stream,
-                          const int* row_map) {
+                          const int* row_map, int cell) {
   constexpr int BM = 128, STAGES = 3;
   constexpr int LDS = Tile<BM, LB_N, STAGES>::LDS_BYTES + BM * 4;  // + staged token ids
   const int n_nt = (4 * H) / LB_N, n_rt = (R + BM - 1) / BM;
@@ -320,7 +311,7 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* p
   }
   hipLaunchKernelGGL((lstm_step_fwd_kernel<BM, STAGES>), dim3(n_nt * n_rt), dim3(256), LDS,
                      stream, tok, tok_stride, ptab, h_prev, c_prev, vgate, vgate_div, R, H, whh,
-                     h_out, c_out, hdrop_out, ldh, drop_p, rng, step, gates_out, row_map);
+                     h_out, c_out, hdrop_out, ldh, drop_p, rng, step, gates_out, row_map, cell);
   post_launch("lstm_step_fwd_kernel", stream);
 }
 

@@ -376,6 +376,7 @@ struct CellArgs {
   int H;
   float drop_p;
   int step;  // decode step of the cell (dropout mask index)
+  int cell;  // CellType
 };
 
 struct RowStat {
@@ -539,12 +540,11 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
         for (int k = 0; k < CELL_U; ++k) {
           const int u = u0 + k * CMB_LANES;
           if (u < H) {
-            const float gi = sigmoidf_(p[k].x + x[k].x), gf = sigmoidf_(p[k].y + x[k].y);
-            const float gg = tanhf_(p[k].z + x[k].z), go = sigmoidf_(p[k].w + x[k].w);
+            const CellFwd cf = cell_fwd(cell.cell, p[k].x + x[k].x, p[k].y + x[k].y,
+                                        p[k].z + x[k].z, p[k].w + x[k].w, cp[k]);
             const int64_t o = (int64_t)r * H + u;
-            const float c = gf * cp[k] + gi * gg;
-            const float hv = go * tanhf_(c);
-            cell.c_out[o] = c;
+            const float hv = cf.h;
+            cell.c_out[o] = cf.c;
             cell.h_out[o] = f2bf(hv);
             if (cell.hdrop_out) {
               const bool keep =
@@ -553,8 +553,8 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
             }
             if (cell.gates_out) {
               uint2 pk;
-              pk.x = (uint32_t)f2bf(gi) | ((uint32_t)f2bf(gf) << 16);
-              pk.y = (uint32_t)f2bf(gg) | ((uint32_t)f2bf(go) << 16);
+              pk.x = (uint32_t)f2bf(cf.s0) | ((uint32_t)f2bf(cf.s1) << 16);
+              pk.y = (uint32_t)f2bf(cf.s2) | ((uint32_t)f2bf(cf.s3) << 16);
               *reinterpret_cast<uint2*>(cell.gates_out + (int64_t)r * 4 * H + 4 * u) = pk;
             }
           }
@@ -721,7 +721,7 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   CellArgs cell{};
   if (cl != nullptr) {
     cell = CellArgs{cl->pre, cl->ptab, cl->c_prev, cl->c_out, cl->h_out, cl->hdrop_out,
-                    cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step};
+                    cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step, cl->cell};
   }
   hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + CMB_ROWS - 1) / CMB_ROWS), dim3(CMB_THREADS), 0,
                      stream,

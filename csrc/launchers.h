@@ -16,16 +16,19 @@ void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
 
 // adam.hip
 // bf16 shadow copies of decoder weights written by the optimizer pass
-enum ShadowKind : int { SHADOW_PLAIN = 0, SHADOW_LSTM_IH = 1, SHADOW_LSTM_HH = 2 };
+// (GATES kinds: a recurrent cell's W_ih / W_hh, rows scattered into the packed
+// 4-slot gate layout, see common.h "recurrent cells")
+enum ShadowKind : int { SHADOW_PLAIN = 0, SHADOW_GATES_IH = 1, SHADOW_GATES_HH = 2 };
 constexpr int SHADOW_MAX_SEGS = 6;
 struct ShadowSeg {
   int64_t off, n;   // range of the flat parameter buffer
   int kind;         // ShadowKind
-  int cols;         // row length of the source matrix (LSTM kinds)
-  int H, E;         // LSTM sizes: packed wx is (4H, E + H)
-  uint16_t* dst;    // PLAIN: dst[j]; LSTM kinds: packed wx
-  uint16_t* dst2;   // LSTM_HH: packed W_hh copy (row stride ld2)
+  int cols;         // row length of the source matrix (GATES kinds)
+  int H, E;         // cell sizes: packed wx is (4H, E + H)
+  uint16_t* dst;    // PLAIN: dst[j]; GATES kinds: packed wx
+  uint16_t* dst2;   // GATES_HH: packed W_hh copy (row stride ld2)
   int ld2;
+  int slots;        // GATES kinds: packed slot of source gate g = bits [2g, 2g + 2)
 };
 struct ShadowSegs {
   ShadowSeg s[SHADOW_MAX_SEGS];
@@ -60,6 +63,7 @@ struct CellLaunch {
   int H;
   float drop_p;
   int step;
+  int cell;  // CellType (common.h)
 };
 // size of the end-of-sequence flag area per decode step (ints) of `counts`
 int combine_count_ints_per_step();
@@ -93,7 +97,7 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* p
                           int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,
                           const uint32_t* rng, int step, uint16_t* gates_out, hipStream_t stream,
-                          const int* row_map = nullptr);  // row_map: h/c source row (beam)
+                          const int* row_map, int cell);  // row_map: h/c source row (beam)
 
 // dg_next / dG rows have stride KD: 4H gate columns (+ A attention-query
 // columns, matched by extra whhT columns [W_hh^T | W_q^T] of width KD)
@@ -101,7 +105,7 @@ int lstm_bwd_tiles(int R, int H);
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
-                          int step, uint16_t* dG, int KD, hipStream_t stream);
+                          int step, uint16_t* dG, int KD, hipStream_t stream, int cell);
 
 // attention.hip (temporal attention over num_chunks frames)
 int att_groups(int vdiv);

@@ -39,9 +39,17 @@ distribution-identical, not value-identical:
     ``dropout_keep``); the scheduled-sampling coin uses Philox4x32-10;
   * precision: bf16 MFMA operands, fp32 accumulation, cell state and
     softmax statistics in fp32.
-Supported configuration: ``rnn_type lstm``, ``num_layers 1``, ``model_type
-concat`` with or without temporal attention; other configurations use the
-PyTorch path (``build_model`` decides).
+Cells (``--rnn_type``, reference ``opts.py`` / ``model.py:93-116``): LSTM,
+GRU and tanh RNN share every kernel; only the cell epilogues differ
+(``csrc/common.h`` ``cell_fwd`` / ``cell_bwd``).  All three are packed into
+4 pre-activation slots per hidden unit (packed gate row ``4u + slot``):
+LSTM (i, f, g, o); GRU (r, z, n_x, n_h), where the input-side weights fill
+slots r, z, n_x and the recurrent ones r, z, n_h, because GRU's candidate is
+``tanh(n_x + r * n_h)``; RNN slot 0 only.  Unused slots are zero rows.
+
+Supported configuration: ``rnn_type lstm | gru | rnn``, ``num_layers 1``,
+``model_type concat`` with or without temporal attention; other
+configurations use the PyTorch path (``build_model`` decides).
 """
 import torch
 import torch.nn.functional as F
@@ -51,11 +59,17 @@ from ..utils.text import BOS
 
 SEL_GT, SEL_SAMPLE, SEL_GREEDY, SEL_SS = 0, 1, 2, 3
 
+# cell id of csrc/common.h CellType, gate groups of the PyTorch weights, and
+# the packed slot of each gate group on the input / recurrent side
+CELLS = {'lstm': (0, 4, (0, 1, 2, 3), (0, 1, 2, 3)),
+         'gru': (1, 3, (0, 1, 2), (0, 1, 3)),
+         'rnn': (2, 1, (0,), (0,))}
+
 ATT_MAX_CHUNKS = 32  # frames per video supported by csrc/kernels/attention.hip
 
 
 def engine_supports(opt):
-    ok = (getattr(opt, 'rnn_type', 'lstm') == 'lstm' and getattr(opt, 'num_layers', 1) == 1
+    ok = (getattr(opt, 'rnn_type', 'lstm') in CELLS and getattr(opt, 'num_layers', 1) == 1
           and getattr(opt, 'model_type', 'concat') == 'concat'
           and opt.input_encoding_size % 64 == 0 and opt.input_encoding_size <= 1024
           and opt.rnn_size % 64 == 0)
@@ -63,6 +77,25 @@ def engine_supports(opt):
     if ok and C > 1:  # attention size == rnn_size (TemporalAttention)
         ok = C <= ATT_MAX_CHUNKS
     return ok
+
+
+def gate_maps(rnn_type, H):
+    """Packing of a cell's gate-major PyTorch weights (rows ``g*H + u``) into
+    packed gate rows ``4u + slot``, for the input and the recurrent side:
+    (src (4H,) PyTorch row of each packed row, ``G*H`` = a zero row;
+    dst (G*H,) packed row of each PyTorch row; slot code for the Adam
+    shadow pass, 2 bits per gate group, ``csrc/kernels/adam.hip``)."""
+    _, G, slots_ie, slots_hh = CELLS[rnn_type]
+    u = torch.arange(H)
+    out = []
+    for slots in (slots_ie, slots_hh):
+        src = torch.full((H, 4), G * H, dtype=torch.long)
+        dst = torch.empty(G * H, dtype=torch.long)
+        for g, k in enumerate(slots):
+            src[:, k] = g * H + u
+            dst[g * H:(g + 1) * H] = 4 * u + k
+        out.append((src.view(-1), dst, sum(k << (2 * g) for g, k in enumerate(slots))))
+    return out
 
 
 class _DecoderFn(torch.autograd.Function):
@@ -84,7 +117,7 @@ class _DecoderFn(torch.autograd.Function):
             vg_in, vdiv,
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
-            drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att)
+            drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell)
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
         full = None
@@ -172,7 +205,7 @@ class _DecoderFn(torch.autograd.Function):
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
-            ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias)
+            ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell)
         dWx, dWlog, dblog, d_emb, dvg = res[:5]
         if early:
             hook.launch()
@@ -181,16 +214,18 @@ class _DecoderFn(torch.autograd.Function):
         if emb_direct:
             d_emb = None
         E = eng.E
-        d_orig = dWx.index_select(0, eng.inv_perm)
+        # packed gate rows -> the PyTorch weights' rows (unused slots dropped)
+        d_ie = dWx[:, :E].index_select(0, eng.dst_ie)
+        d_hh = dWx[:, E:].index_select(0, eng.dst_hh)
         w_ih_shape, emb_shape = ctx.shapes
         if emb_direct:
-            direct['wih'][:, :E].copy_(d_orig[:, :E])
-            direct['whh'].copy_(d_orig[:, E:])
+            direct['wih'][:, :E].copy_(d_ie)
+            direct['whh'].copy_(d_hh)
             d_wih = d_whh = None
         else:
             d_wih = torch.zeros(w_ih_shape, dtype=torch.float32, device=dWx.device)
-            d_wih[:, :E] = d_orig[:, :E]
-            d_whh = d_orig[:, E:].contiguous()
+            d_wih[:, :E] = d_ie
+            d_whh = d_hh
         if ctx.has_att:
             d_gv, d_pre, d_wa, d_ba, d_wq = res[5:10]
             return (None, d_wih, d_whh, d_emb, dWlog, dblog, d_gv, d_pre, d_wq, d_wa,
@@ -203,7 +238,7 @@ class _DecoderFn(torch.autograd.Function):
 class DecoderEngine:
     def __init__(self, model, opt):
         if not engine_supports(opt):
-            raise ValueError('fused engine supports lstm / 1 layer / concat '
+            raise ValueError('fused engine supports lstm, gru, rnn / 1 layer / concat '
                              '(num_chunks <= %d with attention)' % ATT_MAX_CHUNKS)
         if not _ext.available():
             raise RuntimeError('HIP extension not available')
@@ -213,9 +248,10 @@ class DecoderEngine:
         self.attention = getattr(model, 'num_chunks', 1) > 1
         dev = model.embed.weight.device
         H, E, V = self.H, self.E, self.V
-        # packed gate row 4u+g  <-  original row g*H+u
-        self.perm = torch.arange(4 * H, device=dev).view(4, H).t().reshape(-1).contiguous()
-        self.inv_perm = torch.argsort(self.perm)
+        self.cell, G, _, _ = CELLS[model.rnn_type]
+        self.gates = G
+        (self.src_ie, self.dst_ie, self.slots_ie), (self.src_hh, self.dst_hh, self.slots_hh) = \
+            [(a.to(dev), b.to(dev), c) for a, b, c in gate_maps(model.rnn_type, H)]
         self.model = model
         # bf16 shadow weights read by the kernels.  Persistent buffers, updated
         # IN PLACE (by the fused Adam pass, or refresh_weights()), so a captured
@@ -238,22 +274,23 @@ class DecoderEngine:
     # -- bf16 shadow weights ------------------------------------------------------
     def shadow_spec(self, bucket):
         """Shadow-copy segments of the flat parameter buffer for the fused
-        Adam pass: (int64 CPU meta (n, 7), [dst, dst2] * n)."""
+        Adam pass: (int64 CPU meta (n, 8), [dst, dst2] * n).  The fused pass
+        never writes the unused (zero) gate slots."""
         m = self.model
         slot = {id(p): (off, n) for p, (off, n) in zip(bucket.params, bucket.slices)}
         rnn = m.core.rnn
         H, E = self.H, self.E
         empty = torch.empty(0, dtype=torch.bfloat16, device=self.wx.device)
-        segs = [(m.logit.weight, 0, 0, self.wlog, empty, 0),
-                (m.embed.weight, 0, 0, self.emb, empty, 0),
-                (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx, empty, 0),
-                (rnn.weight_hh_l0, 2, H, self.wx, self.whh_q, H)]
+        segs = [(m.logit.weight, 0, 0, self.wlog, empty, 0, 0),
+                (m.embed.weight, 0, 0, self.emb, empty, 0, 0),
+                (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx, empty, 0, self.slots_ie),
+                (rnn.weight_hh_l0, 2, H, self.wx, self.whh_q, H, self.slots_hh)]
         if self.attention:
-            segs.append((m.temporal_att.f_h.weight, 0, 0, self.wq, empty, 0))
+            segs.append((m.temporal_att.f_h.weight, 0, 0, self.wq, empty, 0, 0))
         meta, dsts = [], []
-        for p, kind, cols, d, d2, ld2 in segs:
+        for p, kind, cols, d, d2, ld2, slots in segs:
             off, n = slot[id(p)]
-            meta.append([off, n, kind, cols, H, E, ld2])
+            meta.append([off, n, kind, cols, H, E, ld2, slots])
             dsts += [d, d2]
         return torch.tensor(meta, dtype=torch.int64), dsts
 
@@ -265,14 +302,21 @@ class DecoderEngine:
         E = self.E
         w_ih = m.core.rnn.weight_ih_l0
         w_hh = m.core.rnn.weight_hh_l0
-        self.wx[:, :E].copy_(w_ih[:, :E].index_select(0, self.perm))
-        self.wx[:, E:].copy_(w_hh.index_select(0, self.perm))
+        self.wx[:, :E].copy_(self.pack_rows(w_ih[:, :E], self.src_ie))
+        self.wx[:, E:].copy_(self.pack_rows(w_hh, self.src_hh))
         self.whh.copy_(self.wx[:, E:])
         self.emb.copy_(m.embed.weight)
         self.wlog.copy_(m.logit.weight)
         if self.attention:
             self.wq.copy_(m.temporal_att.f_h.weight)
         self.update_ptab()
+
+    @staticmethod
+    def pack_rows(w, src, dim=0):
+        """rows (``dim``) of a gate-major PyTorch tensor in packed gate order,
+        zeros in the unused slots (differentiable)"""
+        pad = [0, 0] * (w.dim() - 1 - dim % w.dim()) + [0, 1]
+        return F.pad(w, pad).index_select(dim, src)
 
     @torch.no_grad()
     def update_ptab(self):
@@ -326,7 +370,7 @@ class DecoderEngine:
         fc = model.encode(feats)  # (B, F*H), FeatPool dropout in train mode
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
         vg = F.linear(fc, w_iv)
-        return vg.index_select(1, self.perm), fc.size(0)
+        return self.pack_rows(vg, self.src_ie, 1), fc.size(0)
 
     def _att_inputs(self, model, feats):
         """Per-batch attention operands: per-frame gate table Gv (B, C, 4H)
@@ -335,7 +379,7 @@ class DecoderEngine:
         frames = model.encode(feats)  # (B, C, F*H), FeatPool dropout in train mode
         ta = model.temporal_att
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
-        gv = F.linear(frames, w_iv).index_select(2, self.perm)
+        gv = self.pack_rows(F.linear(frames, w_iv), self.src_ie, 2)
         pre = ta.precompute(frames)
         return (gv, pre, ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), frames.size(0)
 
@@ -453,5 +497,5 @@ class DecoderEngine:
         seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog,
                                          model.logit.bias.detach().float().contiguous(),
                                          vg.detach().float().contiguous(), K, model.seq_length,
-                                         BOS, att)
+                                         BOS, att, self.cell)
         return seq, lp

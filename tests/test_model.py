@@ -254,3 +254,42 @@ def test_temporal_attention_model_runs():
     with torch.no_grad():
         s, _ = m.eval().sample(_feats(2, chunks=4), {'beam_size': 3})
     assert s.shape == (2, L)
+
+
+@pytest.mark.parametrize('cell', ['lstm', 'gru', 'rnn'])
+def test_engine_gate_packing_maps(cell):
+    """Packed gate layout of the fused engine (decoder_engine.gate_maps): src
+    and dst are inverse on the used rows, unused slots read the zero row, the
+    slot code decodes (as csrc/kernels/adam.hip packed_gate_row does) to the
+    same packed rows, and a packed GEMM reproduces the cell's pre-activations
+    slot by slot (GRU: n_x and n_h kept apart)."""
+    from cst_captioning_amd.models.decoder_engine import CELLS, DecoderEngine, gate_maps
+    H, K = 8, 5
+    _, G, _, _ = CELLS[cell]
+    (src_ie, dst_ie, code_ie), (src_hh, dst_hh, code_hh) = gate_maps(cell, H)
+    for src, dst, code in ((src_ie, dst_ie, code_ie), (src_hh, dst_hh, code_hh)):
+        assert src.shape == (4 * H,) and dst.shape == (G * H,)
+        assert torch.equal(src[dst], torch.arange(G * H))
+        assert (src == G * H).sum() == (4 - G) * H
+        rows = torch.arange(G * H)
+        g = rows // H
+        assert torch.equal(dst, (rows - g * H) * 4 + ((code >> (2 * g)) & 3))
+    torch.manual_seed(0)
+    w_ih, w_hh = torch.randn(G * H, K), torch.randn(G * H, H)
+    x, h = torch.randn(3, K), torch.randn(3, H)
+    a_x = (x @ DecoderEngine.pack_rows(w_ih, src_ie).t()).view(3, H, 4)
+    a_h = (h @ DecoderEngine.pack_rows(w_hh, src_hh).t()).view(3, H, 4)
+    px, ph = (x @ w_ih.t()).view(3, G, H), (h @ w_hh.t()).view(3, G, H)
+    if cell == 'gru':  # slots r, z, n_x, n_h
+        torch.testing.assert_close((a_x + a_h)[..., :2], (px + ph)[:, :2].transpose(1, 2))
+        torch.testing.assert_close((a_x + a_h)[..., 2], px[:, 2])
+        torch.testing.assert_close((a_x + a_h)[..., 3], ph[:, 2])
+    else:
+        torch.testing.assert_close((a_x + a_h)[..., :G], (px + ph).transpose(1, 2))
+        assert (a_x[..., G:] == 0).all() and (a_h[..., G:] == 0).all()
+    # pack_rows along another dim (the video gate table (B, C, G*H))
+    gv = torch.randn(2, 3, G * H, requires_grad=True)
+    pk = DecoderEngine.pack_rows(gv, src_ie, 2)
+    assert pk.shape == (2, 3, 4 * H)
+    pk.sum().backward()
+    assert torch.equal(gv.grad, torch.ones_like(gv))
