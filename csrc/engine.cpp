@@ -84,14 +84,15 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         double drop_p, double temperature, at::Tensor rng,
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att,
-                                        int64_t cell) {
+                                        int64_t cell, std::vector<at::Tensor> state0) {
   check_cuda(wx, "wx");
   TORCH_CHECK(cell >= 0 && cell <= 2, "cell: 0 lstm, 1 gru, 2 rnn (tanh)");  // CellType (common.h)
   check_cuda(emb, "emb");
   check_cuda(wlog, "wlog");
   check_cuda(blog, "blog");
   // temporal attention (num_chunks > 1): att = {Gv (Bv, C, 4H) f32 packed gates,
-  // P (Bv, C, A) f32, W_q (A, H) bf16, w_a (A) f32, b_a (1) f32}; vgate unused
+  // P (Bv, C, A) f32, W_q (A, H) bf16, w_a (A) f32, b_a (1) f32}; vgate unused.
+  // MANet (modal attention over the C modality blocks): w_a (C, A), b_a (C)
   const bool has_att = !att.empty();
   if (!has_att) check_cuda(vgate, "vgate");
   TORCH_CHECK(wx.scalar_type() == at::kBFloat16 && emb.scalar_type() == at::kBFloat16 &&
@@ -112,6 +113,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     TORCH_CHECK(vgate.size(1) == H4 && vgate.size(0) * vgate_div >= R, "vgate shape");
   at::Tensor a_gv, a_pre, a_wq, a_wa, a_ba;
   int64_t Bv = 0, C = 0, A = 0;
+  int per_frame = 0;
   if (has_att) {
     TORCH_CHECK(att.size() == 5, "att = {Gv, P, W_q, w_a, b_a}");
     a_gv = att[0], a_pre = att[1], a_wq = att[2], a_wa = att[3], a_ba = att[4];
@@ -125,9 +127,12 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     TORCH_CHECK(a_wq.scalar_type() == at::kBFloat16 && a_wq.size(0) == A && a_wq.size(1) == H,
                 "W_q must be bf16 (A, H)");
     TORCH_CHECK(whh.size(0) == H4 + A, "with attention whh must be [W_hh; W_q] (4H + A, H)");
-    TORCH_CHECK(a_wa.scalar_type() == at::kFloat && a_wa.numel() == A && a_ba.numel() == 1 &&
-                    a_ba.scalar_type() == at::kFloat, "w_a (A) / b_a (1) fp32");
+    TORCH_CHECK(a_wa.scalar_type() == at::kFloat && a_ba.scalar_type() == at::kFloat &&
+                    ((a_wa.numel() == A && a_ba.numel() == 1) ||
+                     (C > 1 && C <= 8 && a_wa.numel() == C * A && a_ba.numel() == C)),
+                "w_a (A) / b_a (1), or per frame (C, A) / (C), fp32");
     TORCH_CHECK(Bv * vgate_div == R, "attention needs R == videos x rows per video");
+    per_frame = a_wa.numel() == C * A && C > 1 ? 1 : 0;
   }
   TORCH_CHECK(T >= 2 && (int64_t)modes.size() >= T - 1, "modes must cover T-1 steps");
   const bool have_labels = labels.defined() && labels.numel() > 0;
@@ -195,7 +200,21 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   auto gates_buf = [&](int64_t t) -> uint16_t* {
     return save ? reinterpret_cast<uint16_t*>(gates_all[t].data_ptr()) : nullptr;
   };
-  at::Tensor zeros_h = at::zeros({R, H}, bf), zeros_c = at::zeros({R, H}, f32);
+  // initial state (model_type 'standard': the state after the video step;
+  // otherwise zero): state0 = {h0 bf16 (R, H), c0 fp32 (R, H)}
+  at::Tensor h0, c0;
+  if (!state0.empty()) {
+    TORCH_CHECK(state0.size() == 2 && !has_att, "state0 = {h0, c0}, without attention");
+    h0 = state0[0], c0 = state0[1];
+    check_cuda(h0, "h0");
+    check_cuda(c0, "c0");
+    TORCH_CHECK(h0.scalar_type() == at::kBFloat16 && h0.is_contiguous() && h0.size(0) == R &&
+                    h0.size(1) == H && c0.scalar_type() == at::kFloat && c0.is_contiguous() &&
+                    c0.size(0) == R && c0.size(1) == H,
+                "h0 bf16 / c0 fp32, contiguous (R, H)");
+  } else {
+    h0 = at::zeros({R, H}, bf), c0 = at::zeros({R, H}, f32);
+  }
   at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
 
   // Attention of step t: query q_t = W_q h_{t-1} (hipBLASLt, fp32 out; q_0 = 0),
@@ -221,16 +240,16 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), qp, nullptr,
                    a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv, (int)vgate_div,
                    (int)C, (int)A, (int)H4, vg_rows.data_ptr<float>(),
-                   save ? alpha_all[t].data_ptr<float>() : nullptr, st);
+                   save ? alpha_all[t].data_ptr<float>() : nullptr, st, 0, per_frame);
   };
   const float* VG = has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>();
   const int VDIV = has_att ? 1 : (int)vgate_div;
 
-  // step 0: fused LSTM step (h_{-1} = c_{-1} = 0)
+  // step 0: fused cell step from (h_{-1}, c_{-1}) = (h0, c0)
   if (has_att) run_att(0);
   launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
-                       ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(zeros_h.data_ptr()),
-                       zeros_c.data_ptr<float>(), VG, VDIV, (int)R,
+                       ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(h0.data_ptr()),
+                       c0.data_ptr<float>(), VG, VDIV, (int)R,
                        (int)H, WHH, h_buf(0), c_buf(0), hd_buf(0), (int)(H + HAUG), (float)drop_p,
                        RNG, 0, gates_buf(0), st, nullptr, (int)cell);
   // Steps t >= 0: ONE launch runs the vocab projection of step t together with
@@ -261,7 +280,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), q_next.data_ptr<float>(),
                      nullptr, a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv,
                      (int)vgate_div, (int)C, (int)A, (int)H4, pre.data_ptr<float>(),
-                     save ? alpha_all[t + 1].data_ptr<float>() : nullptr, st, /*accumulate=*/1);
+                     save ? alpha_all[t + 1].data_ptr<float>() : nullptr, st, /*accumulate=*/1,
+                     per_frame);
     CellLaunch cl{};
     if (next) {
       TORCH_CHECK(choose, "internal: a next step needs a chosen token");
@@ -295,7 +315,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 
 // Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), d_emb (V, E), dvg_rows (R, 4H)}
 // (+ {dGv (Bv, C, 4H), dP (Bv, C, A), dw_a (A), db_a (1), dW_q (A, H)} with attention,
-// att = {Gv, P, W_q bf16, w_a, alpha_all (n, R, C), q_all (n, R, A)}; dvg_rows empty).
+// att = {Gv, P, W_q bf16, w_a, alpha_all (n, R, C), q_all (n, R, A)}; dvg_rows empty)
+// (+ {dh0 (R, H) through W_hh, dc0 (R, H) the state carry} with an initial
+// state, state0 = {h0, c0} of the forward).
 // toks: (n_steps*R) input token of every (step, row), step-major.
 //
 // Schedule (streams):
@@ -319,7 +341,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor dg_xe, double drop_p, at::Tensor rng,
                                          at::Tensor out_wlog, at::Tensor out_blog,
                                          int64_t comm_stream, std::vector<at::Tensor> att,
-                                         at::Tensor out_emb, at::Tensor ds_bias, int64_t cell) {
+                                         at::Tensor out_emb, at::Tensor ds_bias, int64_t cell,
+                                         std::vector<at::Tensor> state0) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -344,9 +367,18 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     TORCH_CHECK(Bv * vdiv == R && a_alpha.size(0) == n_steps && a_alpha.size(2) == C &&
                     a_q.size(2) == A && a_wq.size(0) == A && a_wq.size(1) == H,
                 "attention operand shapes");
+    TORCH_CHECK(a_wa.numel() == A || (C > 1 && a_wa.numel() == C * A), "w_a shape");
   }
+  const int per_frame = has_att && C > 1 && a_wa.numel() == C * A ? 1 : 0;
+  const int64_t NWA = per_frame ? C : 1;  // scorer-weight rows
   // dG rows: 4H gate gradients (+ A columns of dq with attention)
   const int64_t KD = H4 + A;
+  const bool has_s0 = !state0.empty();
+  if (has_s0)
+    TORCH_CHECK(state0.size() == 2 && !has_att && state0[0].size(0) == R &&
+                    state0[0].scalar_type() == at::kBFloat16 && state0[1].size(0) == R &&
+                    state0[1].scalar_type() == at::kFloat,
+                "state0 = {h0 bf16, c0 fp32} (R, H)");
   TORCH_CHECK(V <= 8 * 2048, "vocab larger than the dS kernel's register tiling");
   TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
   const int64_t NR = n_steps * R;
@@ -441,8 +473,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   if (has_att) {
     const int64_t nwg = Bv * att_groups((int)vdiv);
     dpre_part = at::zeros({nwg, C, A}, f32);
-    dwa_part = at::zeros({nwg, A}, f32);
-    dba_part = at::zeros({nwg}, f32);
+    dwa_part = at::zeros({nwg, NWA * A}, f32);
+    dba_part = at::zeros({nwg, NWA}, f32);
   }
   (void)hipStreamWaitEvent(st, ev_dhd, 0);
   for (int64_t t = n_steps - 1; t >= 0; --t) {
@@ -450,7 +482,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
         reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dHd.data_ptr<float>() + t * R * H,
         dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
-        c_all[t].data_ptr<float>(), t > 0 ? c_all[t - 1].data_ptr<float>() : nullptr, (int)R,
+        c_all[t].data_ptr<float>(),
+        t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
+        (int)R,
         (int)H, (float)drop_p, RNG, (int)t, reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()),
         (int)KD, st, (int)cell);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
@@ -459,7 +493,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      t > 0 ? a_q[t].data_ptr<float>() : nullptr, a_alpha[t].data_ptr<float>(),
                      a_wa.data_ptr<float>(), (int)Bv, (int)vdiv, (int)C, (int)A, (int)H4,
                      t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
-                     dba_part.data_ptr<float>(), st);
+                     dba_part.data_ptr<float>(), st, per_frame);
   }
   if (dwlog_late) {
     (void)hipEventRecord(ev_ready, st);  // reverse loop done
@@ -503,6 +537,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dWx.narrow(1, E, H).zero_();
     if (has_att) dWq = at::zeros({A, H}, f32);
   }
+  at::Tensor dh0;
+  if (has_s0) {  // step 0's recurrent input h0: dW_hh += dG_0^T h0, dh0 = dG_0 W_hh
+    at::Tensor dG0 = dG2.narrow(0, 0, R);
+    dWx.narrow(1, E, H).add_(at::mm(dG0.t(), state0[0], at::kFloat));
+    dh0 = at::mm(dG0, wx.narrow(1, E, H), at::kFloat);
+  }
   at::Tensor dvg;
   std::vector<at::Tensor> res;
   if (!has_att) {
@@ -514,14 +554,18 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     at::Tensor dgv = dG_all.view({n_steps * Bv, vdiv, KD}).narrow(2, 0, H4);
     at::Tensor dGv = at::bmm(al, dgv, at::kFloat).view({n_steps, Bv, C, H4}).sum(0);
     const int64_t ng = att_groups((int)vdiv);
-    res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0),
-           dba_part.sum(0).view({1}), dWq};
+    res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0).view_as(a_wa),
+           dba_part.sum(0).view({NWA}), dWq};
   }
   // join the side stream (dW_logit): every tensor it touched was allocated
   // on the main stream and is released after this point
   (void)hipStreamWaitEvent(st, ev_done, 0);
   std::vector<at::Tensor> out = {dWx, dWlog, dblog, d_emb, dvg};
   out.insert(out.end(), res.begin(), res.end());
+  if (has_s0) {
+    out.push_back(dh0);
+    out.push_back(dc);  // carry into step -1 (LSTM: dc0; GRU / RNN: direct dh0 term)
+  }
   return out;
 }
 
@@ -623,7 +667,8 @@ void refresh_shadows(at::Tensor p, at::Tensor shadow_meta, std::vector<at::Tenso
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,
-                                    std::vector<at::Tensor> att, int64_t cell) {
+                                    std::vector<at::Tensor> att, int64_t cell,
+                                    std::vector<at::Tensor> state0) {
   check_cuda(wx, "wx");
   check_cuda(vgate, "vgate");
   TORCH_CHECK(K >= 1 && K <= 16, "beam_size must be in [1, 16]");
@@ -640,7 +685,10 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
     C = att[0].size(1), A = att[1].size(2);
     TORCH_CHECK(A % 64 == 0 && C >= 1 && C <= 32 &&
                     att[2].size(0) == A && att[2].size(1) == H, "attention shapes");
+    TORCH_CHECK(att[3].numel() == A || (C > 1 && C <= 8 && att[3].numel() == C * A &&
+                                        att[4].numel() == C), "w_a / b_a shapes");
   }
+  const int per_frame = has_att && C > 1 && att[3].numel() == C * A ? 1 : 0;
   auto dev = wx.device();
   auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
   auto i64 = at::TensorOptions().dtype(at::kLong).device(dev);
@@ -663,6 +711,13 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   at::Tensor parent = at::empty({R}, i32);
   at::Tensor h[2] = {at::zeros({R, H}, wx.options()), at::empty({R, H}, wx.options())};
   at::Tensor c[2] = {at::zeros({R, H}, f32), at::empty({R, H}, f32)};
+  if (!state0.empty()) {  // per-video initial state {h0 (B, H), c0 (B, H)}, one copy per beam
+    TORCH_CHECK(state0.size() == 2 && !has_att && state0[0].size(0) == B &&
+                    state0[1].size(0) == B && state0[0].size(1) == H && state0[1].size(1) == H,
+                "state0 = {h0, c0} (B, H), without attention");
+    h[0].copy_(state0[0].repeat_interleave(K, 0));
+    c[0].copy_(state0[1].repeat_interleave(K, 0));
+  }
   const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
   if (has_att) {
@@ -689,7 +744,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
       launch_att_fwd(att[0].data_ptr<float>(), att[1].data_ptr<float>(),
                      t >= 1 ? qb.data_ptr<float>() : nullptr, t >= 1 ? parent.data_ptr<int>() : nullptr,
                      att[3].data_ptr<float>(), att[4].data_ptr<float>(), (int)B, (int)K, (int)C,
-                     (int)A, (int)H4, vg_rows.data_ptr<float>(), nullptr, st);
+                     (int)A, (int)H4, vg_rows.data_ptr<float>(), nullptr, st, 0, per_frame);
     }
     launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, ptab.data_ptr<float>(),
                          reinterpret_cast<const uint16_t*>(hp.data_ptr()), cp.data_ptr<float>(),

@@ -9,6 +9,12 @@
 // h_{t-1}:
 //     e_c   = w_a . tanh(P[b, c] + q_r) + b_a,  P = W_f v_c + b_f,  q_r = W_q h_{t-1, r}
 //     alpha = softmax_c(e),  ctx_r = sum_c alpha_c v_c,  gates += W_iv ctx_r.
+// The same kernels run the reference's modal attention MANet
+// (/root/reference/model.py:119-142) with the F modality blocks of the video
+// vector as the "frames": there the scorer weights differ per frame,
+//     e_f = A_m[f] . tanh(p + W_hm h_{t-1}) + b_m[f],  p = W_fm v + b_fm + b_hm,
+// i.e. per-frame rows w_a[c] (wa_ld = A) and biases b_a[c] (ba_ld = 1) over a
+// P that is the same for every frame (the caller expands it).
 //
 // MI355X design:
 //   * ctx only enters the LSTM through W_iv, which is linear, so the caller
@@ -38,6 +44,7 @@
 //     free.  dP / dw_a / db_a accumulate in per-workgroup slots (the grid
 //     shape is the same every step, so no atomics and a deterministic sum).
 #include "../common.h"
+#include "../launchers.h"
 
 namespace cst {
 
@@ -112,7 +119,7 @@ template <int MAXC>
 __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
     const float* __restrict__ gv, const float* __restrict__ pre, const float* __restrict__ q,
     const int* __restrict__ q_rowmap, const float* __restrict__ wa, const float* __restrict__ ba,
-    int vdiv, int ngroups, int C, int A, int G4, float* __restrict__ vg_out,
+    int wa_ld, int ba_ld, int vdiv, int ngroups, int C, int A, int G4, float* __restrict__ vg_out,
     float* __restrict__ alpha_out, int accumulate) {
   __shared__ float s_red[ATT_WAVES * ATT_RPW * MAXC];
   __shared__ float s_e[ATT_RPW * MAXC];
@@ -150,13 +157,13 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
     for (int c = 0; c < MAXC; ++c) part[s][c] = 0.f;
   const float* P = pre + (int64_t)b * C * A;
   for (int a = tid; a < A; a += ATT_THREADS) {
-    const float wa_a = wa[a];
     float qv[ATT_RPW];
 #pragma unroll
     for (int s = 0; s < ATT_RPW; ++s) qv[s] = q != nullptr ? q[(int64_t)qrow[s] * A + a] : 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       if (c < C) {
+        const float wa_a = wa[c * wa_ld + a];
         const float pc = P[(int64_t)c * A + a];
 #pragma unroll
         for (int s = 0; s < ATT_RPW; ++s) part[s][c] += wa_a * tanhf_(pc + qv[s]);
@@ -166,12 +173,14 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
   block_sum_partials<MAXC>(part, s_red, s_e);
   if (tid < nr) {  // softmax over frames, one thread per row
     float* e = s_e + tid * MAXC;
-    const float bias = ba[0];
     float m = -INFINITY;
-    for (int c = 0; c < C; ++c) m = fmaxf(m, e[c] + bias);
+    for (int c = 0; c < C; ++c) {
+      e[c] += ba[c * ba_ld];
+      m = fmaxf(m, e[c]);
+    }
     float sum = 0.f;
     for (int c = 0; c < C; ++c) {
-      const float x = __expf(e[c] + bias - m);
+      const float x = __expf(e[c] - m);
       e[c] = x;
       sum += x;
     }
@@ -229,8 +238,9 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
 }
 
 // dG: (R, ldg) bf16 rows, gate gradients in columns [0, G4); dq_t is written
-// as bf16 into columns [G4, G4 + A) when write_dq.
-template <int MAXC>
+// as bf16 into columns [G4, G4 + A) when write_dq.  PERC: per-frame scorer
+// weights (MANet): dw_a / db_a slots are (C, A) / (C) per workgroup.
+template <int MAXC, bool PERC>
 __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     uint16_t* __restrict__ dG, int ldg, const float* __restrict__ gv,
     const float* __restrict__ pre, const float* __restrict__ q, const float* __restrict__ alpha,
@@ -245,16 +255,18 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   // reverse step) and its columns of P / q: requested up front, so the loads
   // overlap phase 1
   constexpr int AJ = 2;  // attention units per thread held in registers (A <= 512)
+  constexpr int NW = PERC ? MAXC : 1;  // scorer-weight rows
   const bool apf = MAXC <= 8 && A <= AJ * ATT_THREADS;  // (register budget)
-  float acc_dp[AJ][MAXC], acc_dw[AJ], pv[AJ][MAXC], qv[AJ][ATT_RPW];
+  float acc_dp[AJ][MAXC], acc_dw[AJ][NW], pv[AJ][MAXC], qv[AJ][ATT_RPW];
   float* dpp = dpre_part + (int64_t)blockIdx.x * C * A;
-  float* dwp = dwa_part + (int64_t)blockIdx.x * A;
+  float* dwp = dwa_part + (int64_t)blockIdx.x * (PERC ? C : 1) * A;
   const float* P = pre + (int64_t)b * C * A;
   if (apf) {
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
       const int a = tid + j * ATT_THREADS;
-      acc_dw[j] = a < A ? dwp[a] : 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) acc_dw[j][w] = (a < A && w < C) ? dwp[w * A + a] : 0.f;
 #pragma unroll
       for (int c = 0; c < MAXC; ++c) {
         acc_dp[j][c] = (a < A && c < C) ? dpp[c * A + a] : 0.f;
@@ -312,7 +324,13 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   }
   __syncthreads();
   const float* s_de = s_da;
-  if (tid == 0) {
+  if (PERC) {
+    if (tid < C) {
+      float sb = 0.f;
+      for (int s = 0; s < nr; ++s) sb += s_de[s * MAXC + tid];
+      dba_part[(int64_t)blockIdx.x * C + tid] += sb;
+    }
+  } else if (tid == 0) {
     float sb = 0.f;
     for (int s = 0; s < nr; ++s)
       for (int c = 0; c < C; ++c) sb += s_de[s * MAXC + c];
@@ -320,20 +338,20 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   }
   // 3. scorer backward, thread per attention unit a:
   //    dz = de_c w_a (1 - u^2), u = tanh(P_c + q_s); dq_s = sum_c dz; dP_c = sum_s dz
-  auto unit = [&](int a, const float* pa, const float* qa, float (&dp)[MAXC], float& dwa) {
-    const float wa_a = wa[a];
+  auto unit = [&](int a, const float* pa, const float* qa, float (&dp)[MAXC], float (&dwa)[NW]) {
     float dq[ATT_RPW];
 #pragma unroll
     for (int s = 0; s < ATT_RPW; ++s) dq[s] = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       if (c < C) {
+        const float wa_a = wa[PERC ? c * A + a : a];
 #pragma unroll
         for (int s = 0; s < ATT_RPW; ++s) {
           if (s < nr) {
             const float u = tanhf_(pa[c] + qa[s]);
             const float de = s_de[s * MAXC + c];
-            dwa += de * u;
+            dwa[PERC ? c : 0] += de * u;
             const float dz = de * wa_a * (1.f - u * u);
             dq[s] += dz;
             dp[c] += dz;
@@ -353,7 +371,9 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
       const int a = tid + j * ATT_THREADS;
       if (a < A) {
         unit(a, pv[j], qv[j], acc_dp[j], acc_dw[j]);
-        dwp[a] = acc_dw[j];
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+          if (w < C) dwp[w * A + a] = acc_dw[j][w];
 #pragma unroll
         for (int c = 0; c < MAXC; ++c)
           if (c < C) dpp[c * A + a] = acc_dp[j][c];
@@ -361,7 +381,9 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     }
   } else {
     for (int a = tid; a < A; a += ATT_THREADS) {
-      float dp[MAXC], pa[MAXC], qa[ATT_RPW], dw = 0.f;
+      float dp[MAXC], pa[MAXC], qa[ATT_RPW], dw[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) dw[w] = 0.f;
 #pragma unroll
       for (int c = 0; c < MAXC; ++c) {
         dp[c] = 0.f;
@@ -371,7 +393,9 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
       for (int s = 0; s < ATT_RPW; ++s)
         qa[s] = (q != nullptr && s < nr) ? q[(int64_t)(r0 + s) * A + a] : 0.f;
       unit(a, pa, qa, dp, dw);
-      dwp[a] += dw;
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if (w < C) dwp[w * A + a] += dw[w];
 #pragma unroll
       for (int c = 0; c < MAXC; ++c)
         if (c < C) dpp[c * A + a] += dp[c];
@@ -383,11 +407,14 @@ int att_groups(int vdiv) { return (vdiv + ATT_RPW - 1) / ATT_RPW; }
 
 void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
                     const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
-                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate) {
+                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate,
+                    int per_frame) {
   const int ng = att_groups(vdiv);
+  const int wa_ld = per_frame ? A : 0, ba_ld = per_frame ? 1 : 0;
 #define ATT_FWD(M)                                                                          \
   hipLaunchKernelGGL(att_fwd_kernel<M>, dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, gv, pre, \
-                     q, q_rowmap, wa, ba, vdiv, ng, C, A, G4, vg_out, alpha_out, accumulate)
+                     q, q_rowmap, wa, ba, wa_ld, ba_ld, vdiv, ng, C, A, G4, vg_out, alpha_out,  \
+                     accumulate)
   if (C <= 8)
     ATT_FWD(8);
   else if (C <= 16)
@@ -398,13 +425,13 @@ void launch_att_fwd(const float* gv, const float* pre, const float* q, const int
   post_launch("att_fwd_kernel", stream);
 }
 
-template <int MAXC>
+template <int MAXC, bool PERC>
 static void launch_att_bwd_t(uint16_t* dG, int ldg, const float* gv, const float* pre,
                              const float* q, const float* alpha, const float* wa, int Bv, int vdiv,
                              int C, int A, int G4, int write_dq, float* dpre_part, float* dwa_part,
                              float* dba_part, hipStream_t stream) {
   const int ng = att_groups(vdiv);
-  hipLaunchKernelGGL(att_bwd_kernel<MAXC>, dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, dG, ldg,
+  hipLaunchKernelGGL((att_bwd_kernel<MAXC, PERC>), dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, dG, ldg,
                      gv, pre, q, alpha, wa, vdiv, ng, C, A, G4, write_dq, dpre_part, dwa_part,
                      dba_part);
   post_launch("att_bwd_kernel", stream);
@@ -413,16 +440,21 @@ static void launch_att_bwd_t(uint16_t* dG, int ldg, const float* gv, const float
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,
                     const float* alpha, const float* wa, int Bv, int vdiv, int C, int A, int G4,
                     int write_dq, float* dpre_part, float* dwa_part, float* dba_part,
-                    hipStream_t stream) {
-  if (C <= 8)
-    launch_att_bwd_t<8>(dG, ldg, gv, pre, q, alpha, wa, Bv, vdiv, C, A, G4, write_dq, dpre_part,
-                        dwa_part, dba_part, stream);
-  else if (C <= 16)
-    launch_att_bwd_t<16>(dG, ldg, gv, pre, q, alpha, wa, Bv, vdiv, C, A, G4, write_dq, dpre_part,
-                         dwa_part, dba_part, stream);
-  else
-    launch_att_bwd_t<32>(dG, ldg, gv, pre, q, alpha, wa, Bv, vdiv, C, A, G4, write_dq, dpre_part,
-                         dwa_part, dba_part, stream);
+                    hipStream_t stream, int per_frame) {
+#define ATT_BWD(M, PF)                                                                        \
+  launch_att_bwd_t<M, PF>(dG, ldg, gv, pre, q, alpha, wa, Bv, vdiv, C, A, G4, write_dq, dpre_part, \
+                          dwa_part, dba_part, stream)
+  if (per_frame) {  // MANet: C = number of modalities
+    if (C > 8) throw std::runtime_error("per-frame attention weights: at most 8 frames");
+    ATT_BWD(8, true);
+  } else if (C <= 8) {
+    ATT_BWD(8, false);
+  } else if (C <= 16) {
+    ATT_BWD(16, false);
+  } else {
+    ATT_BWD(32, false);
+  }
+#undef ATT_BWD
 }
 
 }  // namespace cst

@@ -107,16 +107,19 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell);
 
-// attention.hip (temporal attention over num_chunks frames)
+// attention.hip (temporal attention over num_chunks frames; MANet modal
+// attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
 int att_groups(int vdiv);
 // vg_out[r] = sum_c alpha_rc Gv[b, c]  (+= when accumulate: adds into pre)
 void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
                     const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
-                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate = 0);
+                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate,
+                    int per_frame);
+// dwa_part / dba_part: per-workgroup slots of (A) / (1), or (C, A) / (C) per_frame
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,
                     const float* alpha, const float* wa, int Bv, int vdiv, int C, int A, int G4,
                     int write_dq, float* dpre_part, float* dwa_part, float* dba_part,
-                    hipStream_t stream);
+                    hipStream_t stream, int per_frame);
 
 // embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows grouped by token; C <= 1024)
 void launch_token_rows_sum(const float* x, int C, const int* stok, const int* srow, int N,

@@ -47,9 +47,22 @@ LSTM (i, f, g, o); GRU (r, z, n_x, n_h), where the input-side weights fill
 slots r, z, n_x and the recurrent ones r, z, n_h, because GRU's candidate is
 ``tanh(n_x + r * n_h)``; RNN slot 0 only.  Unused slots are zero rows.
 
+Model types (reference ``model.py:273-278``): ``concat`` (the video vector
+enters every step's gates through ``vgate``), ``standard`` (the video
+vector is the input of an extra step -1: autograd runs that one cell step
+per video, and the engine starts from its state, returning the gradient
+w.r.t. that initial state), and ``manet`` (modal attention,
+``model.py:119-142``): the F modality blocks of the video vector are the
+attention "frames" of the same kernels -- gate table ``Gv[b, f] =
+W_iv[:, block f] . v_f``, projected input ``p = W_fm v + b_fm + b_hm``
+(shared by every frame), query ``W_hm h_{t-1}`` and per-frame scorer rows
+``A_m[f]`` / ``b_m[f]``; the scorer width F is zero-padded to 64 (the
+query's GEMM tile), and the padded units contribute nothing.
+
 Supported configuration: ``rnn_type lstm | gru | rnn``, ``num_layers 1``,
-``model_type concat`` with or without temporal attention; other
-configurations use the PyTorch path (``build_model`` decides).
+``model_type concat | standard | manet`` (manet: at most 8 modalities),
+temporal attention with ``concat``; other configurations use the PyTorch
+path (``build_model`` decides).
 """
 import torch
 import torch.nn.functional as F
@@ -66,16 +79,19 @@ CELLS = {'lstm': (0, 4, (0, 1, 2, 3), (0, 1, 2, 3)),
          'rnn': (2, 1, (0,), (0,))}
 
 ATT_MAX_CHUNKS = 32  # frames per video supported by csrc/kernels/attention.hip
+MANET_MAX_FEATS = 8  # modalities with per-frame scorer weights (attention.hip)
 
 
 def engine_supports(opt):
     ok = (getattr(opt, 'rnn_type', 'lstm') in CELLS and getattr(opt, 'num_layers', 1) == 1
-          and getattr(opt, 'model_type', 'concat') == 'concat'
+          and getattr(opt, 'model_type', 'concat') in ('concat', 'standard', 'manet')
           and opt.input_encoding_size % 64 == 0 and opt.input_encoding_size <= 1024
           and opt.rnn_size % 64 == 0)
     C = getattr(opt, 'num_chunks', 1)
+    if ok and getattr(opt, 'model_type', 'concat') == 'manet':
+        ok = C == 1 and len(getattr(opt, 'feat_dims', [])) <= MANET_MAX_FEATS
     if ok and C > 1:  # attention size == rnn_size (TemporalAttention)
-        ok = C <= ATT_MAX_CHUNKS
+        ok = C <= ATT_MAX_CHUNKS and getattr(opt, 'model_type', 'concat') == 'concat'
     return ok
 
 
@@ -101,8 +117,8 @@ def gate_maps(rnn_type, H):
 class _DecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, vgate, w_ih, w_hh, emb_w, logit_w, logit_b, att_gv, att_pre, att_wq,
-                att_wa, att_ba, eng, labels, bos, R, T, modes, ss_prob, drop_p, temperature, rng,
-                vdiv, want_xe, use_counts, use_unfinished, save, want_full):
+                att_wa, att_ba, h0, c0, eng, labels, bos, R, T, modes, ss_prob, drop_p,
+                temperature, rng, vdiv, want_xe, use_counts, use_unfinished, save, want_full):
         has_att = att_gv is not None
         dev = logit_b.device
         att = []
@@ -111,13 +127,17 @@ class _DecoderFn(torch.autograd.Function):
                    eng.wq, att_wa.detach().float().contiguous().view(-1),
                    att_ba.detach().float().contiguous().view(-1)]
         vg_in = torch.empty(0, device=dev) if has_att else vgate.detach().float().contiguous()
+        state0 = []
+        if h0 is not None:  # bf16 h (the recurrent GEMM operand), fp32 c
+            state0 = [h0.detach().bfloat16().contiguous(), c0.detach().float().contiguous()]
         outs = _ext.ops().decoder_forward(
             eng.wx, eng.emb, eng.ptab, eng.whh_q if has_att else eng.whh, eng.wlog,
             logit_b.detach().float().contiguous(),
             vg_in, vdiv,
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
-            drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell)
+            drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell,
+            state0)
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
         full = None
@@ -130,6 +150,7 @@ class _DecoderFn(torch.autograd.Function):
         ctx.drop_p, ctx.rng = drop_p, rng
         ctx.shapes = (w_ih.shape, emb_w.shape)
         ctx.has_att = has_att
+        ctx.state0 = state0 if save else []
         ctx.att_saved = None
         if save:
             ctx.saved = (lse, *outs[4:9], seq, labels, bos)
@@ -137,6 +158,7 @@ class _DecoderFn(torch.autograd.Function):
                 ctx.att_saved = (att[0], att[1], att[2], att[3], outs[9], outs[10])
         else:
             ctx.saved = None
+        ctx.att_shapes = (att_wa.shape, att_ba.shape) if has_att else None
         ctx.mark_non_differentiable(seq)
         if g_xe is None:
             g_xe = torch.zeros(0, device=g_sel.device)
@@ -205,7 +227,13 @@ class _DecoderFn(torch.autograd.Function):
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
-            ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell)
+            ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell,
+            ctx.state0)
+        d_state = (None, None)
+        if ctx.state0:
+            d_state = (res[-2], res[-1])  # through W_hh, and the state carry
+            res = res[:-2]
+        ctx.state0 = []
         dWx, dWlog, dblog, d_emb, dvg = res[:5]
         if early:
             hook.launch()
@@ -228,11 +256,13 @@ class _DecoderFn(torch.autograd.Function):
             d_whh = d_hh
         if ctx.has_att:
             d_gv, d_pre, d_wa, d_ba, d_wq = res[5:10]
+            d_wa, d_ba = d_wa.view(ctx.att_shapes[0]), d_ba.view(ctx.att_shapes[1])
             return (None, d_wih, d_whh, d_emb, dWlog, dblog, d_gv, d_pre, d_wq, d_wa,
-                    d_ba) + (None,) * 16
+                    d_ba) + (None,) * 18
         nv = R // vdiv
         d_vgate = dvg.view(nv, vdiv, -1).sum(1)
-        return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 21
+        return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 5 + d_state + \
+            (None,) * 16
 
 
 class DecoderEngine:
@@ -245,7 +275,10 @@ class DecoderEngine:
         self.H = model.rnn_size
         self.E = model.input_encoding_size
         self.V = model.vocab_size
-        self.attention = getattr(model, 'num_chunks', 1) > 1
+        self.manet = getattr(model, 'model_type', 'concat') == 'manet'
+        # the attention kernels run temporal attention and MANet
+        self.attention = getattr(model, 'num_chunks', 1) > 1 or self.manet
+        self.standard = getattr(model, 'model_type', 'concat') == 'standard'
         dev = model.embed.weight.device
         H, E, V = self.H, self.E, self.V
         self.cell, G, _, _ = CELLS[model.rnn_type]
@@ -256,7 +289,12 @@ class DecoderEngine:
         # bf16 shadow weights read by the kernels.  Persistent buffers, updated
         # IN PLACE (by the fused Adam pass, or refresh_weights()), so a captured
         # HIP graph always reads the live weights.
-        A = model.temporal_att.f_h.weight.size(0) if self.attention else 0
+        A = 0
+        if self.manet:  # scorer width F, zero-padded to the 64-row GEMM tile
+            A = (model.num_feats + 63) // 64 * 64
+        elif self.attention:
+            A = model.temporal_att.f_h.weight.size(0)
+        self.att_dim = A
         bf = dict(dtype=torch.bfloat16, device=dev)
         self.wx = torch.empty(4 * H, E + H, **bf)       # [W_ie | W_hh], packed gate rows
         self.whh_q = torch.empty(4 * H + A, H, **bf)    # [W_hh; W_q] (recurrent GEMM operand)
@@ -285,8 +323,8 @@ class DecoderEngine:
                 (m.embed.weight, 0, 0, self.emb, empty, 0, 0),
                 (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx, empty, 0, self.slots_ie),
                 (rnn.weight_hh_l0, 2, H, self.wx, self.whh_q, H, self.slots_hh)]
-        if self.attention:
-            segs.append((m.temporal_att.f_h.weight, 0, 0, self.wq, empty, 0, 0))
+        if self.attention:  # (MANet: the first F rows of the padded W_q)
+            segs.append((self._query_weight(), 0, 0, self.wq, empty, 0, 0))
         meta, dsts = [], []
         for p, kind, cols, d, d2, ld2, slots in segs:
             off, n = slot[id(p)]
@@ -308,7 +346,8 @@ class DecoderEngine:
         self.emb.copy_(m.embed.weight)
         self.wlog.copy_(m.logit.weight)
         if self.attention:
-            self.wq.copy_(m.temporal_att.f_h.weight)
+            q = self._query_weight()
+            self.wq.copy_(F.pad(q, (0, 0, 0, self.att_dim - q.size(0))))
         self.update_ptab()
 
     @staticmethod
@@ -366,16 +405,58 @@ class DecoderEngine:
         # a replayed graph advances the generator's offset)
         return torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev)
 
+    def _initial_state(self, model, feats):
+        """model_type 'standard': one cell step per video on the video vector
+        from a zero state (plain autograd ops, so it captures in a HIP graph;
+        W_hh does not enter it).  Returns (h0, c0) per video, c0 = h0 for
+        GRU / RNN (the kernels' state buffer)."""
+        fc = model.encode(feats)  # (B, E), FeatPool dropout in train mode
+        a = F.linear(fc, model.core.rnn.weight_ih_l0)
+        if self.cell == 0:  # LSTM i, f, g, o with c' = 0
+            i, _, g, o = a.chunk(4, 1)
+            c = torch.sigmoid(i) * torch.tanh(g)
+            return torch.sigmoid(o) * torch.tanh(c), c
+        if self.cell == 1:  # GRU r, z, n with h' = 0
+            _, z, n = a.chunk(3, 1)
+            h = (1 - torch.sigmoid(z)) * torch.tanh(n)
+        else:
+            h = torch.tanh(a)
+        return h, h
+
     def _vgate(self, model, feats, expand):
+        if self.standard:  # no per-step video term
+            B = feats[0].size(0)
+            return model.logit.bias.new_zeros(B, 4 * self.H), B
         fc = model.encode(feats)  # (B, F*H), FeatPool dropout in train mode
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
         vg = F.linear(fc, w_iv)
         return self.pack_rows(vg, self.src_ie, 1), fc.size(0)
 
+    def _query_weight(self):
+        m = self.model
+        return m.manet.f_h_m.weight if self.manet else m.temporal_att.f_h.weight
+
+    def _manet_inputs(self, model, feats):
+        """MANet as attention over the F modality blocks (module docstring)."""
+        x = model.encode(feats)  # (B, F*blk), FeatPool dropout in train mode
+        B, Fm = x.size(0), model.num_feats
+        blk = x.size(1) // Fm
+        w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
+        gv = torch.einsum('bfk,gfk->bfg', x.view(B, Fm, blk), w_iv.view(-1, Fm, blk))
+        gv = self.pack_rows(gv, self.src_ie, 2)
+        mn, pad = model.manet, self.att_dim - Fm
+        p = F.pad(mn.f_feat_m(x) + mn.f_h_m.bias, (0, pad))
+        pre = p.unsqueeze(1).expand(B, Fm, self.att_dim)
+        wq = F.pad(mn.f_h_m.weight, (0, 0, 0, pad))
+        wa = F.pad(mn.align_m.weight, (0, pad))
+        return (gv, pre, wq, wa, mn.align_m.bias), B
+
     def _att_inputs(self, model, feats):
         """Per-batch attention operands: per-frame gate table Gv (B, C, 4H)
         in packed gate order, projected frames P (B, C, A), and the scorer
         parameters (W_q, w_a, b_a) as autograd inputs of the Function."""
+        if self.manet:
+            return self._manet_inputs(model, feats)
         frames = model.encode(feats)  # (B, C, F*H), FeatPool dropout in train mode
         ta = model.temporal_att
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
@@ -393,6 +474,11 @@ class DecoderEngine:
             vg, B = self._vgate(model, feats, expand)
             att = (None,) * 5
         S = model.feat_expander.n if expand else 1
+        h0 = c0 = None
+        if self.standard:
+            h0, c0 = self._initial_state(model, feats)
+            if S > 1:
+                h0, c0 = h0.repeat_interleave(S, 0), c0.repeat_interleave(S, 0)
         R = labels.size(0) if labels is not None else B * S
         if labels is not None:
             T = labels.size(1) - 1
@@ -405,9 +491,9 @@ class DecoderEngine:
         ws = (m.core.rnn.weight_ih_l0, m.core.rnn.weight_hh_l0, m.embed.weight, m.logit.weight,
               m.logit.bias)
         # (inside Function.forward grad mode is off, so decide here)
-        diff_in = [t for t in (vg,) + tuple(att) if t is not None] + list(ws)
+        diff_in = [t for t in (vg, h0, c0) + tuple(att) if t is not None] + list(ws)
         save = want_full or (torch.is_grad_enabled() and any(t.requires_grad for t in diff_in))
-        return _DecoderFn.apply(vg, *ws, *att, self,
+        return _DecoderFn.apply(vg, *ws, *att, h0, c0, self,
                                 labels.contiguous() if labels is not None else None, bos, R, T,
                                 modes, float(ss_prob), float(drop_p), float(temperature),
                                 self._rng(m.logit.bias.device), S, want_xe, use_counts,
@@ -494,8 +580,12 @@ class DecoderEngine:
             vg = gv[:, 0]  # only its row count is read when attention is on
         else:
             vg, _ = self._vgate(model, feats, False)
+        state0 = []
+        if self.standard:
+            h0, c0 = self._initial_state(model, feats)
+            state0 = [h0.bfloat16().contiguous(), c0.float().contiguous()]
         seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog,
                                          model.logit.bias.detach().float().contiguous(),
                                          vg.detach().float().contiguous(), K, model.seq_length,
-                                         BOS, att, self.cell)
+                                         BOS, att, self.cell, state0)
         return seq, lp

@@ -1,10 +1,12 @@
 """GRU and tanh-RNN decoders (``--rnn_type gru | rnn``, reference
-``opts.py`` / ``model.py:93-116``) through the fused HIP engine, against the
-PyTorch ``nn.GRU`` / ``nn.RNN`` path of :class:`CaptionModel`: teacher-forced
-log-probs and XE gradients, REINFORCE gradients of a MIXER rollout, greedy
-decoding, the GPU beam search, temporal attention, and the graph-captured
-training step whose Adam pass writes the packed bf16 shadows (unused gate
-slots stay zero)."""
+``opts.py`` / ``model.py:93-116``) and the ``standard`` and ``manet`` model types
+(video vector as the input of step -1; modal attention, ``model.py:119-142,
+273-278``) through the fused HIP
+engine, against the PyTorch ``nn.GRU`` / ``nn.RNN`` / ``nn.LSTM`` path of
+:class:`CaptionModel`: teacher-forced log-probs and XE gradients, REINFORCE
+gradients of a MIXER rollout, greedy decoding, the GPU beam search, temporal
+attention, and the graph-captured training step whose Adam pass writes the
+packed bf16 shadows (unused gate slots stay zero)."""
 import copy
 
 import pytest
@@ -13,10 +15,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 DEV = 'cuda'
-CELLS = ['gru', 'rnn']
+# (rnn_type, model_type): standard feeds the video (F*H = 2H wide) as the
+# step -1 input, so its input encoding size is 2H
+VARIANTS = [('gru', 'concat'), ('rnn', 'concat'), ('lstm', 'standard'), ('gru', 'standard'),
+            ('lstm', 'manet'), ('gru', 'manet')]
+VIDS = ['%s-%s' % v for v in VARIANTS]
 
 
-def _tiny(cell, V=300, H=64, S=5, B=6, L=12, seed=0, C=1):
+def _tiny(cell, V=300, H=64, S=5, B=6, L=12, seed=0, C=1, model_type='concat'):
     from cst_captioning_amd.config import default_opts
     from cst_captioning_amd.data import make_synthetic, CaptionLoader
     from cst_captioning_amd.models import CaptionModel
@@ -24,8 +30,8 @@ def _tiny(cell, V=300, H=64, S=5, B=6, L=12, seed=0, C=1):
     ds = make_synthetic('msrvtt', num_videos=40, vocab_size=V, seq_length=L,
                         feat_dims=[48, 32], num_chunks=C, seed=seed)
     opt = default_opts(vocab_size=V, seq_length=L, feat_dims=[48, 32], train_seq_per_img=S,
-                       rnn_size=H, input_encoding_size=H, drop_prob_lm=0.0, rnn_type=cell,
-                       num_chunks=C)
+                       rnn_size=H, input_encoding_size=2 * H if model_type == 'standard' else H,
+                       drop_prob_lm=0.0, rnn_type=cell, num_chunks=C, model_type=model_type)
     torch.manual_seed(seed)
     model = CaptionModel(opt).to(DEV)
     with torch.no_grad():  # make the decoder non-trivial
@@ -34,6 +40,16 @@ def _tiny(cell, V=300, H=64, S=5, B=6, L=12, seed=0, C=1):
     eng = DecoderEngine(model, opt)
     loader = CaptionLoader(ds, B, S, 'train', DEV, seed=seed)
     return ds, opt, model, eng, loader
+
+
+def _tol(name, base=0.06):
+    """MANet's scorer biases get the sum over every row and step of
+    softmax-backward terms that cancel (a row's score gradients sum to zero
+    over the modalities), computed from the bf16 gate gradients: their
+    relative error is the cancelled sum's, not the terms'."""
+    if name.startswith('manet.') and name.endswith('bias'):
+        return 0.2
+    return base
 
 
 def _grad_errs(model, ref, skip=()):
@@ -46,11 +62,12 @@ def _grad_errs(model, ref, skip=()):
 
 
 @pytest.mark.parametrize('H', [64, 256])
-@pytest.mark.parametrize('cell', CELLS)
-def test_cell_teacher_forced_logprobs_and_grads_match_torch(cell, H):
+@pytest.mark.parametrize('variant', VARIANTS, ids=VIDS)
+def test_cell_teacher_forced_logprobs_and_grads_match_torch(variant, H):
     from cst_captioning_amd.models import CrossEntropyCriterion
-    ds, opt, model, eng, loader = _tiny(cell, V=1299 if H > 64 else 300, H=H)
-    assert eng.cell == {'gru': 1, 'rnn': 2}[cell]
+    cell, mt = variant
+    ds, opt, model, eng, loader = _tiny(cell, V=1299 if H > 64 else 300, H=H, model_type=mt)
+    assert eng.cell == {'lstm': 0, 'gru': 1, 'rnn': 2}[cell] and eng.standard == (mt == 'standard')
     model.train()
     data = loader.get_batch()
     labels = data['labels']
@@ -70,14 +87,14 @@ def test_cell_teacher_forced_logprobs_and_grads_match_torch(cell, H):
     crit(g_xe, labels[:, 1:], data['masks'][:, 1:]).backward()
     errs = _grad_errs(model, ref)
     assert {'core.rnn.weight_ih_l0', 'core.rnn.weight_hh_l0', 'embed.weight'} <= set(errs)
-    bad = {k: v for k, v in errs.items() if v > 0.06}
+    bad = {k: v for k, v in errs.items() if v > _tol(k)}
     assert not bad, errs
 
 
-@pytest.mark.parametrize('cell', CELLS)
-def test_cell_rollout_reinforce_gradient_matches_torch(cell):
+@pytest.mark.parametrize('variant', VARIANTS, ids=VIDS)
+def test_cell_rollout_reinforce_gradient_matches_torch(variant):
     from cst_captioning_amd.models import RewardCriterion
-    ds, opt, model, eng, loader = _tiny(cell, seed=2)
+    ds, opt, model, eng, loader = _tiny(variant[0], seed=2, model_type=variant[1])
     model.train()
     model.set_mixer_from(1)
     model.set_seq_per_img(5)
@@ -97,13 +114,14 @@ def test_cell_rollout_reinforce_gradient_matches_torch(cell):
     assert (g_sel[:, :k] - lp_ref).abs()[alive].max() < 0.08
     RewardCriterion()(seq[:, :k], lp_ref, w).backward()
     errs = _grad_errs(model, ref)
-    bad = {k: v for k, v in errs.items() if v > 0.08}
+    bad = {k: v for k, v in errs.items() if v > _tol(k, 0.08)}
     assert not bad, errs
 
 
-@pytest.mark.parametrize('cell', CELLS)
-def test_cell_greedy_and_beam_match_torch(cell):
-    ds, opt, model, eng, loader = _tiny(cell, seed=1)
+@pytest.mark.parametrize('variant', VARIANTS, ids=VIDS)
+def test_cell_greedy_and_beam_match_torch(variant):
+    # 24 videos: a single bf16 near-tie flip is < 5% of the rows
+    ds, opt, model, eng, loader = _tiny(variant[0], seed=1, model_type=variant[1], B=24)
     with torch.no_grad():
         model.logit.weight.mul_(3.0)  # peaked distributions: few near-ties
     eng.refresh_weights()
@@ -150,8 +168,8 @@ def test_gru_temporal_attention_matches_torch():
     assert not bad, errs
 
 
-@pytest.mark.parametrize('cell', CELLS)
-def test_cell_graph_training_keeps_packed_shadows(cell):
+@pytest.mark.parametrize('variant', VARIANTS, ids=VIDS)
+def test_cell_graph_training_keeps_packed_shadows(variant):
     """Graph-captured SCST steps: the weights train, and the shadows the Adam
     pass wrote equal a fresh packing of the fp32 parameters, zero slots
     included."""
@@ -160,17 +178,20 @@ def test_cell_graph_training_keeps_packed_shadows(cell):
     from cst_captioning_amd.cli import build_model
     from cst_captioning_amd.parallel import DistContext
     from cst_captioning_amd.train.trainer import Trainer
+    cell, mt = variant
     ds = make_synthetic('msrvtt', num_videos=48, vocab_size=500, seq_length=12,
                         feat_dims=[64, 32], seed=0)
     opt = default_opts(vocab_size=500, seq_length=12, feat_dims=[64, 32], train_seq_per_img=5,
-                       batch_size=8, rnn_size=128, input_encoding_size=128, drop_prob_lm=0.5,
+                       batch_size=8, rnn_size=128,
+                       input_encoding_size=256 if mt == 'standard' else 128, drop_prob_lm=0.5,
                        use_rl=1, use_rl_after=0, use_cst=0, use_mixer=1, mixer_from=1,
-                       use_eos=1, impl='hip', cuda_graph=1, learning_rate=1e-3, rnn_type=cell)
+                       use_eos=1, impl='hip', cuda_graph=1, learning_rate=1e-3, rnn_type=cell,
+                       model_type=mt)
     opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
     torch.manual_seed(0)
     dev = torch.device(DEV)
     model, eng = build_model(opt, dev, 'hip')
-    assert eng is not None and eng.cell == {'gru': 1, 'rnn': 2}[cell]
+    assert eng is not None and eng.cell == {'lstm': 0, 'gru': 1, 'rnn': 2}[cell]
     loader = CaptionLoader(ds, 8, 5, 'train', dev, seed=0)
     tr = Trainer(opt, model, loader, None, DistContext(device=dev), eng)
     tr.rl_training = True
@@ -188,5 +209,5 @@ def test_cell_graph_training_keeps_packed_shadows(cell):
     E = eng.E
     unused_ie = eng.src_ie == eng.gates * eng.H
     unused_hh = eng.src_hh == eng.gates * eng.H
-    assert unused_ie.any() and unused_hh.any()
+    assert unused_ie.any() == unused_hh.any() == (cell != 'lstm')
     assert (eng.wx[unused_ie, :E] == 0).all() and (eng.wx[unused_hh, E:] == 0).all()
