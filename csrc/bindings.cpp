@@ -13,7 +13,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         double drop_p, double temperature, at::Tensor rng,
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att,
-                                        int64_t cell, std::vector<at::Tensor> state0);
+                                        int64_t cell, std::vector<at::Tensor> state0,
+                                        std::vector<at::Tensor> up);
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -23,12 +24,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor out_wlog, at::Tensor out_blog,
                                          int64_t comm_stream, std::vector<at::Tensor> att,
                                          at::Tensor out_emb, at::Tensor ds_bias, int64_t cell,
-                                         std::vector<at::Tensor> state0);
+                                         std::vector<at::Tensor> state0,
+                                         std::vector<at::Tensor> up);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,
                                     std::vector<at::Tensor> att, int64_t cell,
-                                    std::vector<at::Tensor> state0);
+                                    std::vector<at::Tensor> state0, std::vector<at::Tensor> up);
 double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
                           int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);

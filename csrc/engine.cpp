@@ -17,6 +17,7 @@
 //                   reverse LSTM recurrence (cell kernel + one GEMM per step),
 //                   then the batched weight-gradient GEMMs.
 #include <torch/extension.h>
+#include <array>
 #include <cstdlib>
 #include <map>
 #include <ATen/hip/HIPContext.h>
@@ -28,12 +29,6 @@
 namespace cst {
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
-
-// h_drop rows may carry HAUG extra columns [1, 0, ...] (written by the LSTM
-// kernel) so that one GEMM dS^T [h | 1] also yields the bias gradient.  The
-// MI355X measurement (hipBLASLt at N=528 vs 512) made the dS kernel's
-// column-sum partials the faster route, so HAUG = 0.
-constexpr int64_t HAUG = 0;
 
 template <class T>
 static T* ptr_or_null(const at::Tensor& t) {
@@ -84,7 +79,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         double drop_p, double temperature, at::Tensor rng,
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att,
-                                        int64_t cell, std::vector<at::Tensor> state0) {
+                                        int64_t cell, std::vector<at::Tensor> state0,
+                                        std::vector<at::Tensor> up) {
   check_cuda(wx, "wx");
   TORCH_CHECK(cell >= 0 && cell <= 2, "cell: 0 lstm, 1 gru, 2 rnn (tanh)");  // CellType (common.h)
   check_cuda(emb, "emb");
@@ -167,17 +163,65 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   // saved-logit rows padded to 128 bytes: the fused backward writes dS back
   // in whole cache lines
   const int64_t ldl = (V + 63) / 64 * 64;
-  at::Tensor logits16, hdrop_all, gates_all, c_all, h_all;
-  if (save) {
-    logits16 = at::empty({n_steps, R, ldl}, at::TensorOptions().dtype(at::kHalf).device(dev));
-    hdrop_all = at::empty({n_steps, R, H + HAUG}, bf);  // [h_drop | 1 | 0...]
-    gates_all = at::empty({n_steps, R, H4}, bf);
-    c_all = at::empty({n_steps, R, H}, f32);
-    h_all = at::empty({n_steps, R, H}, bf);
+  // Stacked layers (num_layers > 1): layer 0 is the fused pipeline below;
+  // layer l >= 1 runs after it in every step: x_l = dropout(h_{l-1}) W_ih_l^T
+  // (hipBLASLt, fp32) enters the step kernel as its per-row input term, the
+  // kernel adds h_l W_hh_l^T and applies the cell.  Dropout between layers
+  // (nn.LSTM's inter-layer dropout) and before the vocab projection share the
+  // counter hash, keyed by step + 65536 * (layers above).
+  TORCH_CHECK(up.size() % 2 == 0, "up = {[W_ih | W_hh] (4H, 2H), W_hh (4H, H)} per upper layer");
+  const int64_t NL = 1 + (int64_t)up.size() / 2;
+  if (NL > 1) TORCH_CHECK(!has_att && state0.empty(), "stacked layers: no attention / initial state");
+  for (int64_t l = 1; l < NL; ++l) {
+    const at::Tensor &wu = up[2 * (l - 1)], &wh = up[2 * (l - 1) + 1];
+    check_cuda(wu, "upper-layer weights");
+    check_cuda(wh, "upper-layer W_hh");
+    TORCH_CHECK(wu.scalar_type() == at::kBFloat16 && wu.is_contiguous() && wu.size(0) == H4 &&
+                    wu.size(1) == 2 * H && wh.scalar_type() == at::kBFloat16 &&
+                    wh.is_contiguous() && wh.size(0) == H4 && wh.size(1) == H,
+                "upper layer: [W_ih | W_hh] bf16 (4H, 2H) and W_hh bf16 (4H, H)");
   }
-  at::Tensor h_a = at::zeros({R, H}, bf), h_b = at::empty({R, H}, bf);
-  at::Tensor c_a = at::zeros({R, H}, f32), c_b = at::empty({R, H}, f32);
-  at::Tensor hd_tmp = (!save && drop_p > 0) ? at::empty({R, H + HAUG}, bf) : at::Tensor();
+  auto key = [&](int64_t l, int64_t t) -> int { return (int)(t + 65536 * (NL - 1 - l)); };
+
+  // Per-layer buffers: h_t / c_t / gates_t saved per step in training (else
+  // ping-pong), hd_t = dropout(h_t) (the next layer's input; the top layer's
+  // is the vocab input)
+  at::Tensor logits16;
+  std::vector<at::Tensor> Hs(NL), Cs(NL), Gs(NL), HDs(NL);
+  std::vector<std::array<at::Tensor, 2>> hpp(NL), cpp(NL);
+  if (save)
+    logits16 = at::empty({n_steps, R, ldl}, at::TensorOptions().dtype(at::kHalf).device(dev));
+  for (int64_t l = 0; l < NL; ++l) {
+    if (save) {
+      Hs[l] = at::empty({n_steps, R, H}, bf);
+      Cs[l] = at::empty({n_steps, R, H}, f32);
+      Gs[l] = at::empty({n_steps, R, H4}, bf);
+      HDs[l] = at::empty({n_steps, R, H}, bf);
+    } else {
+      hpp[l] = {at::empty({R, H}, bf), at::empty({R, H}, bf)};
+      cpp[l] = {at::empty({R, H}, f32), at::empty({R, H}, f32)};
+      if (drop_p > 0) HDs[l] = at::empty({R, H}, bf);
+    }
+  }
+  auto h_tensor = [&](int64_t l, int64_t t) -> at::Tensor {
+    return save ? Hs[l][t] : hpp[l][t & 1];
+  };
+  auto h_buf = [&](int64_t l, int64_t t) -> uint16_t* {
+    return reinterpret_cast<uint16_t*>(h_tensor(l, t).data_ptr());
+  };
+  auto c_buf = [&](int64_t l, int64_t t) -> float* {
+    return save ? Cs[l][t].data_ptr<float>() : cpp[l][t & 1].data_ptr<float>();
+  };
+  auto hd_buf = [&](int64_t l, int64_t t) -> uint16_t* {
+    if (!HDs[l].defined()) return nullptr;
+    return reinterpret_cast<uint16_t*>((save ? HDs[l][t] : HDs[l]).data_ptr());
+  };
+  auto out_tensor = [&](int64_t l, int64_t t) -> at::Tensor {  // layer l's output fed upward
+    return HDs[l].defined() ? (save ? HDs[l][t] : HDs[l]) : h_tensor(l, t);
+  };
+  auto gates_buf = [&](int64_t l, int64_t t) -> uint16_t* {
+    return save ? reinterpret_cast<uint16_t*>(Gs[l][t].data_ptr()) : nullptr;
+  };
 
   const uint32_t* RNG = rng_ptr(rng);
   const float inv_temp = (float)(1.0 / temperature);
@@ -185,21 +229,6 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
   const int64_t* LAB = have_labels ? labels.data_ptr<int64_t>() : nullptr;
 
-  // Step t's buffers: h_t / c_t (saved per step in training, else ping-pong),
-  // hd_t = dropout(h_t) (the vocab input).
-  auto h_buf = [&](int64_t t) -> uint16_t* {
-    return reinterpret_cast<uint16_t*>(save ? h_all[t].data_ptr() : (t & 1 ? h_b : h_a).data_ptr());
-  };
-  auto c_buf = [&](int64_t t) -> float* {
-    return save ? c_all[t].data_ptr<float>() : (t & 1 ? c_b : c_a).data_ptr<float>();
-  };
-  auto hd_buf = [&](int64_t t) -> uint16_t* {
-    if (save) return reinterpret_cast<uint16_t*>(hdrop_all[t].data_ptr());
-    return drop_p > 0 ? reinterpret_cast<uint16_t*>(hd_tmp.data_ptr()) : nullptr;
-  };
-  auto gates_buf = [&](int64_t t) -> uint16_t* {
-    return save ? reinterpret_cast<uint16_t*>(gates_all[t].data_ptr()) : nullptr;
-  };
   // initial state (model_type 'standard': the state after the video step;
   // otherwise zero): state0 = {h0 bf16 (R, H), c0 fp32 (R, H)}
   at::Tensor h0, c0;
@@ -216,6 +245,20 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     h0 = at::zeros({R, H}, bf), c0 = at::zeros({R, H}, f32);
   }
   at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
+  at::Tensor xin = NL > 1 ? at::empty({R, H4}, f32) : at::Tensor();
+
+  // layer l >= 1 at step t (its zero initial state is h0 / c0's zeros)
+  auto upper_step = [&](int64_t l, int64_t t) {
+    const at::Tensor& wu = up[2 * (l - 1)];
+    at::mm_out(xin, out_tensor(l - 1, t), wu.narrow(1, 0, H).t(), at::kFloat);
+    launch_lstm_step_fwd(nullptr, 0, nullptr,
+                         t > 0 ? h_buf(l, t - 1) : reinterpret_cast<uint16_t*>(h0.data_ptr()),
+                         t > 0 ? c_buf(l, t - 1) : c0.data_ptr<float>(), xin.data_ptr<float>(), 1,
+                         (int)R, (int)H,
+                         reinterpret_cast<const uint16_t*>(up[2 * (l - 1) + 1].data_ptr()),
+                         h_buf(l, t), c_buf(l, t), hd_buf(l, t), (int)H, (float)drop_p, RNG,
+                         key(l, t), gates_buf(l, t), st, nullptr, (int)cell);
+  };
 
   // Attention of step t: query q_t = W_q h_{t-1} (hipBLASLt, fp32 out; q_0 = 0),
   // then the attention kernel writes the per-row video gate term vg_rows.
@@ -229,12 +272,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       q_tmp = at::empty({R, A}, f32);
     }
   }
-  auto h_tensor = [&](int64_t t) -> at::Tensor { return save ? h_all[t] : (t & 1 ? h_b : h_a); };
   auto run_att = [&](int64_t t) {
     const float* qp = nullptr;
     if (t > 0) {
       at::Tensor qo = save ? q_all[t] : q_tmp;
-      at::mm_out(qo, h_tensor(t - 1), a_wq.t(), at::kFloat);
+      at::mm_out(qo, h_tensor(0, t - 1), a_wq.t(), at::kFloat);
       qp = qo.data_ptr<float>();
     }
     launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), qp, nullptr,
@@ -249,17 +291,18 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   if (has_att) run_att(0);
   launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
                        ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(h0.data_ptr()),
-                       c0.data_ptr<float>(), VG, VDIV, (int)R,
-                       (int)H, WHH, h_buf(0), c_buf(0), hd_buf(0), (int)(H + HAUG), (float)drop_p,
-                       RNG, 0, gates_buf(0), st, nullptr, (int)cell);
+                       c0.data_ptr<float>(), VG, VDIV, (int)R, (int)H, WHH, h_buf(0, 0),
+                       c_buf(0, 0), hd_buf(0, 0), (int)H, (float)drop_p, RNG, key(0, 0),
+                       gates_buf(0, 0), st, nullptr, (int)cell);
+  for (int64_t l = 1; l < NL; ++l) upper_step(l, 0);
   // Steps t >= 0: ONE launch runs the vocab projection of step t together with
-  // the recurrent GEMM of step t+1 (pre = h_t W_hh^T + vgate), then the combine
-  // picks token t+1 and applies step t+1's cell epilogue (pre + P[token]).
+  // the recurrent GEMM of step t+1 (pre = h_t W_hh^T + vgate, layer 0), then
+  // the combine picks token t+1 and applies step t+1's cell epilogue (pre +
+  // P[token]); the upper layers of step t+1 follow.
   for (int64_t t = 0; t < n_steps; ++t) {
     const bool next = t + 1 < n_steps;
-    uint16_t* hd = hd_buf(t);
-    const uint16_t* vin = hd ? hd : h_buf(t);
-    const int ldh = hd ? (int)(H + HAUG) : (int)H;
+    uint16_t* hd = hd_buf(NL - 1, t);
+    const uint16_t* vin = hd ? hd : h_buf(NL - 1, t);
     const bool choose = t < T - 1;
     const int mode = choose ? (int)modes[t] : SEL_GT_H;
     const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
@@ -270,10 +313,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     // adds each row's video term into pre before the combine's cell epilogue
     at::Tensor q_next;
     if (has_att && next) q_next = save ? q_all[t + 1] : q_tmp;
-    launch_vocab_lstm_fwd(vin, ldh, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
+    launch_vocab_lstm_fwd(vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
                           save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
                           part.data_ptr(), tgt, L, vflags, inv_temp, RNG, (int)t,
-                          h_buf(t), WHH, has_att ? nullptr : VG, VDIV,
+                          h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
                           next ? pre.data_ptr<float>() : nullptr, st, has_att ? (int)A : 0,
                           has_att && next ? q_next.data_ptr<float>() : nullptr);
     if (has_att && next)
@@ -285,9 +328,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     CellLaunch cl{};
     if (next) {
       TORCH_CHECK(choose, "internal: a next step needs a chosen token");
-      cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_buf(t), c_buf(t + 1),
-                      h_buf(t + 1), hd_buf(t + 1), (int)(H + HAUG), gates_buf(t + 1), (int)H,
-                      (float)drop_p, (int)(t + 1), (int)cell};
+      cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_buf(0, t), c_buf(0, t + 1),
+                      h_buf(0, t + 1), hd_buf(0, t + 1), (int)H, gates_buf(0, t + 1), (int)H,
+                      (float)drop_p, key(0, t + 1), (int)cell};
     }
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                          choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
@@ -297,17 +340,27 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                          use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
                          use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st,
                          next ? &cl : nullptr);
+    if (next)
+      for (int64_t l = 1; l < NL; ++l) upper_step(l, t + 1);
   }
+  // saved: {logits16, hd of the top layer (vocab input), layer 0's gates, c, h}
+  // (+ {alpha_all, q_all}) (+ {h, c, gates of layer l, hd of layer l-1} per l >= 1)
   std::vector<at::Tensor> out = {seq, g_sel, want_xe ? g_xe : at::Tensor(), lse};
   if (save) {
     out.push_back(logits16);
-    out.push_back(hdrop_all);
-    out.push_back(gates_all);
-    out.push_back(c_all);
-    out.push_back(h_all);
+    out.push_back(HDs[NL - 1]);
+    out.push_back(Gs[0]);
+    out.push_back(Cs[0]);
+    out.push_back(Hs[0]);
     if (has_att) {
       out.push_back(alpha_all);
       out.push_back(q_all);
+    }
+    for (int64_t l = 1; l < NL; ++l) {
+      out.push_back(Hs[l]);
+      out.push_back(Cs[l]);
+      out.push_back(Gs[l]);
+      out.push_back(HDs[l - 1]);
     }
   }
   return out;
@@ -317,7 +370,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 // (+ {dGv (Bv, C, 4H), dP (Bv, C, A), dw_a (A), db_a (1), dW_q (A, H)} with attention,
 // att = {Gv, P, W_q bf16, w_a, alpha_all (n, R, C), q_all (n, R, A)}; dvg_rows empty)
 // (+ {dh0 (R, H) through W_hh, dc0 (R, H) the state carry} with an initial
-// state, state0 = {h0, c0} of the forward).
+// state, state0 = {h0, c0} of the forward)
+// (+ {dW_up_l (4H, 2H) packed [W_ih | W_hh]} per upper layer; up = {[W_ih |
+// W_hh] bf16, h_all, c_all, gates_all of layer l, hd_all of layer l-1} each).
 // toks: (n_steps*R) input token of every (step, row), step-major.
 //
 // Schedule (streams):
@@ -342,7 +397,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor out_wlog, at::Tensor out_blog,
                                          int64_t comm_stream, std::vector<at::Tensor> att,
                                          at::Tensor out_emb, at::Tensor ds_bias, int64_t cell,
-                                         std::vector<at::Tensor> state0) {
+                                         std::vector<at::Tensor> state0,
+                                         std::vector<at::Tensor> up) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -373,6 +429,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const int64_t NWA = per_frame ? C : 1;  // scorer-weight rows
   // dG rows: 4H gate gradients (+ A columns of dq with attention)
   const int64_t KD = H4 + A;
+  TORCH_CHECK(up.size() % 5 == 0, "up = {W, h_all, c_all, gates_all, hd_in} per upper layer");
+  const int64_t NL = 1 + (int64_t)up.size() / 5;
+  if (NL > 1) TORCH_CHECK(!has_att && state0.empty(), "stacked layers: no attention / initial state");
+  auto upw = [&](int64_t l, int k) -> const at::Tensor& { return up[5 * (l - 1) + k]; };
+  for (int64_t l = 1; l < NL; ++l)
+    TORCH_CHECK(upw(l, 0).size(0) == H4 && upw(l, 0).size(1) == 2 * H &&
+                    upw(l, 1).size(0) == n_steps && upw(l, 2).size(0) == n_steps &&
+                    upw(l, 3).size(0) == n_steps && upw(l, 4).size(0) == n_steps,
+                "upper-layer operand shapes");
+  auto key = [&](int64_t l, int64_t t) -> int { return (int)(t + 65536 * (NL - 1 - l)); };
   const bool has_s0 = !state0.empty();
   if (has_s0)
     TORCH_CHECK(state0.size() == 2 && !has_att && state0[0].size(0) == R &&
@@ -389,7 +455,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // 1-2. vocab head on the side stream: dS in place, dHd = dS W
   at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n_steps, (int)R), V}, f32);
   at::Tensor dS = logits16.view(at::kBFloat16).view({NR, ldl}).narrow(1, 0, V);
-  at::Tensor hd2 = hdrop_all.view({NR, H + HAUG}).narrow(1, 0, H);
+  at::Tensor hd2 = hdrop_all.view({NR, H});
   at::Tensor dHd = at::empty({NR, H}, f32);
   const bool early = out_wlog.defined() && out_wlog.numel() > 0;
   if (early) {
@@ -476,17 +542,46 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dwa_part = at::zeros({nwg, NWA * A}, f32);
     dba_part = at::zeros({nwg, NWA}, f32);
   }
+  // upper layers: W_hh_l^T (K-contiguous B operands), gate gradients, carries
+  std::vector<at::Tensor> whhT_up(NL), dG_up(NL), dc_up(NL);
+  at::Tensor dX_up = NL > 1 ? at::empty({R, H}, f32) : at::Tensor();
+  for (int64_t l = 1; l < NL; ++l) {
+    whhT_up[l] = upw(l, 0).narrow(1, H, H).t().contiguous();
+    dG_up[l] = at::empty({n_steps, R, H4}, wx.options());
+    dc_up[l] = at::zeros({R, H}, f32);
+  }
   (void)hipStreamWaitEvent(st, ev_dhd, 0);
   for (int64_t t = n_steps - 1; t >= 0; --t) {
+    // top layer first: its h gradient comes from the vocab head (dHd, with the
+    // vocab dropout mask); layer l < top gets dG_{l+1, t} W_ih_{l+1} through
+    // the inter-layer dropout mask of layer l's output
+    for (int64_t l = NL - 1; l >= 1; --l) {
+      const float* dh_in = dHd.data_ptr<float>() + t * R * H;
+      if (l < NL - 1) {
+        at::mm_out(dX_up, dG_up[l + 1][t], upw(l + 1, 0).narrow(1, 0, H), at::kFloat);
+        dh_in = dX_up.data_ptr<float>();
+      }
+      launch_lstm_step_bwd(
+          t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_up[l][t + 1].data_ptr()) : nullptr,
+          reinterpret_cast<const uint16_t*>(whhT_up[l].data_ptr()), dh_in,
+          dc_up[l].data_ptr<float>(), reinterpret_cast<const uint16_t*>(upw(l, 3)[t].data_ptr()),
+          upw(l, 2)[t].data_ptr<float>(), t > 0 ? upw(l, 2)[t - 1].data_ptr<float>() : nullptr,
+          (int)R, (int)H, (float)drop_p, RNG, key(l, t),
+          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell);
+    }
+    const float* dh0_in = dHd.data_ptr<float>() + t * R * H;
+    if (NL > 1) {
+      at::mm_out(dX_up, dG_up[1][t], upw(1, 0).narrow(1, 0, H), at::kFloat);
+      dh0_in = dX_up.data_ptr<float>();
+    }
     launch_lstm_step_bwd(
         t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
-        reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dHd.data_ptr<float>() + t * R * H,
+        reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dh0_in,
         dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
         c_all[t].data_ptr<float>(),
         t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
-        (int)R,
-        (int)H, (float)drop_p, RNG, (int)t, reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()),
-        (int)KD, st, (int)cell);
+        (int)R, (int)H, (float)drop_p, RNG, key(0, t),
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
@@ -565,6 +660,18 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   if (has_s0) {
     out.push_back(dh0);
     out.push_back(dc);  // carry into step -1 (LSTM: dc0; GRU / RNN: direct dh0 term)
+  }
+  for (int64_t l = 1; l < NL; ++l) {  // dW_l = dG_l^T [hd_{l-1, t} | h_{l, t-1}]
+    at::Tensor dWu = at::empty({H4, 2 * H}, f32);
+    at::Tensor dGl = dG_up[l].view({NR, H4});
+    dWu.narrow(1, 0, H).copy_(grouped_wgrad(dGl, upw(l, 4).reshape({NR, H}), n_steps));
+    if (n_steps > 1)
+      dWu.narrow(1, H, H).copy_(grouped_wgrad(
+          dGl.narrow(0, R, (n_steps - 1) * R),
+          upw(l, 1).narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}), n_steps - 1));
+    else
+      dWu.narrow(1, H, H).zero_();
+    out.push_back(dWu);
   }
   return out;
 }
@@ -668,7 +775,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,
                                     std::vector<at::Tensor> att, int64_t cell,
-                                    std::vector<at::Tensor> state0) {
+                                    std::vector<at::Tensor> state0, std::vector<at::Tensor> up) {
   check_cuda(wx, "wx");
   check_cuda(vgate, "vgate");
   TORCH_CHECK(K >= 1 && K <= 16, "beam_size must be in [1, 16]");
@@ -709,8 +816,18 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   at::Tensor best_lp = at::zeros({B, T}, f32);
   at::Tensor tok = at::full({R}, bos_index, i64);
   at::Tensor parent = at::empty({R}, i32);
-  at::Tensor h[2] = {at::zeros({R, H}, wx.options()), at::empty({R, H}, wx.options())};
-  at::Tensor c[2] = {at::zeros({R, H}, f32), at::empty({R, H}, f32)};
+  // stacked layers: up = {[W_ih | W_hh] (4H, 2H), W_hh (4H, H)} per upper layer
+  TORCH_CHECK(up.size() % 2 == 0, "up = {[W_ih | W_hh], W_hh} per upper layer");
+  const int64_t NL = 1 + (int64_t)up.size() / 2;
+  if (NL > 1) TORCH_CHECK(!has_att && state0.empty(), "stacked layers: no attention / initial state");
+  std::vector<std::array<at::Tensor, 2>> hl(NL), cl(NL);
+  for (int64_t l = 0; l < NL; ++l) {
+    hl[l] = {at::zeros({R, H}, wx.options()), at::empty({R, H}, wx.options())};
+    cl[l] = {at::zeros({R, H}, f32), at::empty({R, H}, f32)};
+  }
+  at::Tensor xin = NL > 1 ? at::empty({R, H4}, f32) : at::Tensor();
+  at::Tensor* h = hl[0].data();
+  at::Tensor* c = cl[0].data();
   if (!state0.empty()) {  // per-video initial state {h0 (B, H), c0 (B, H)}, one copy per beam
     TORCH_CHECK(state0.size() == 2 && !has_att && state0[0].size(0) == B &&
                     state0[1].size(0) == B && state0[0].size(1) == H && state0[1].size(1) == H,
@@ -753,7 +870,19 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                          reinterpret_cast<uint16_t*>(ho.data_ptr()), co.data_ptr<float>(), nullptr,
                          (int)H, 0.f, nullptr, (int)t, nullptr, st,
                          t >= 1 ? parent.data_ptr<int>() : nullptr, (int)cell);
-    launch_vocab_fwd(reinterpret_cast<const uint16_t*>(ho.data_ptr()), (int)H, (int)R, (int)H, W,
+    for (int64_t l = 1; l < NL; ++l) {  // upper layers: their state follows the parent beam too
+      at::mm_out(xin, hl[l - 1][(t + 1) & 1], up[2 * (l - 1)].narrow(1, 0, H).t(), at::kFloat);
+      launch_lstm_step_fwd(nullptr, 0, nullptr,
+                           reinterpret_cast<const uint16_t*>(hl[l][t & 1].data_ptr()),
+                           cl[l][t & 1].data_ptr<float>(), xin.data_ptr<float>(), 1, (int)R,
+                           (int)H, reinterpret_cast<const uint16_t*>(up[2 * (l - 1) + 1].data_ptr()),
+                           reinterpret_cast<uint16_t*>(hl[l][(t + 1) & 1].data_ptr()),
+                           cl[l][(t + 1) & 1].data_ptr<float>(), nullptr, (int)H, 0.f, nullptr,
+                           (int)t, nullptr, st, t >= 1 ? parent.data_ptr<int>() : nullptr,
+                           (int)cell);
+    }
+    const at::Tensor& htop = hl[NL - 1][(t + 1) & 1];
+    launch_vocab_fwd(reinterpret_cast<const uint16_t*>(htop.data_ptr()), (int)H, (int)R, (int)H, W,
                      blog.data_ptr<float>(), (int)V,
                      reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl, part.data_ptr(),
                      nullptr, 0, /*flags=*/8, 1.f, nullptr, (int)t, st);

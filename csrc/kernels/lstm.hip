@@ -51,10 +51,11 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
   const int r0 = rt * BM, n0 = nt * LB_N;
   const int nk = H / 64;
 
-  // token ids of this row tile (used by the epilogue's table gather)
+  // token ids of this row tile (used by the epilogue's table gather; upper
+  // layers of a stacked decoder have no token term: tok = ptab = null)
   int* s_tok = reinterpret_cast<int*>(lds + LTile::LDS_BYTES);
   if (threadIdx.x < BM)
-    s_tok[threadIdx.x] = (int)tok[(int64_t)min(r0 + (int)threadIdx.x, R - 1) * tok_stride];
+    s_tok[threadIdx.x] = tok ? (int)tok[(int64_t)min(r0 + (int)threadIdx.x, R - 1) * tok_stride] : 0;
   __syncthreads();
 
   // Epilogue operands are gathered BEFORE the main loop, so their latency
@@ -67,7 +68,8 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int row = rg + 16 * i, r = min(r0 + row, R - 1);
-    pre_px[i] = *reinterpret_cast<const float4*>(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u);
+    pre_px[i] = ptab ? *reinterpret_cast<const float4*>(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
     pre_vg[i] = *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
     pre_c[i] = c_prev[(int64_t)(row_map ? row_map[r] : r) * H + hu];
     CST_DCHECK(s_tok[row] >= 0);
@@ -120,8 +122,6 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
       if (hdrop_out) {
         const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
         hdrop_out[(int64_t)r * ldh + hu] = f2bf(keep ? hv * inv_keep : 0.f);
-        // augmented columns [H, ldh): a 1 then zeros (bias-gradient GEMM trick)
-        if (nt == 0 && u < ldh - H) hdrop_out[(int64_t)r * ldh + H + u] = u == 0 ? 0x3f80 : 0;
       }
       if (gates_out) {
         uint2 pk;

@@ -19,7 +19,7 @@ void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
 // (GATES kinds: a recurrent cell's W_ih / W_hh, rows scattered into the packed
 // 4-slot gate layout, see common.h "recurrent cells")
 enum ShadowKind : int { SHADOW_PLAIN = 0, SHADOW_GATES_IH = 1, SHADOW_GATES_HH = 2 };
-constexpr int SHADOW_MAX_SEGS = 6;
+constexpr int SHADOW_MAX_SEGS = 12;
 struct ShadowSeg {
   int64_t off, n;   // range of the flat parameter buffer
   int kind;         // ShadowKind

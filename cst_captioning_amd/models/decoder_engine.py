@@ -59,10 +59,17 @@ W_iv[:, block f] . v_f``, projected input ``p = W_fm v + b_fm + b_hm``
 ``A_m[f]`` / ``b_m[f]``; the scorer width F is zero-padded to 64 (the
 query's GEMM tile), and the padded units contribute nothing.
 
-Supported configuration: ``rnn_type lstm | gru | rnn``, ``num_layers 1``,
-``model_type concat | standard | manet`` (manet: at most 8 modalities),
-temporal attention with ``concat``; other configurations use the PyTorch
-path (``build_model`` decides).
+Stacked layers (``num_layers > 1``, ``model.py:93-116``): layer 0 is the
+fused pipeline above; each upper layer ``l`` runs one hipBLASLt GEMM
+``dropout(h_{l-1}) W_ih_l^T`` and one step kernel (recurrent GEMM + cell) per
+step, its weights packed as ``[W_ih_l | W_hh_l]`` (4H, 2H).  nn.LSTM's
+inter-layer dropout uses the same counter hash as the vocab dropout, keyed
+per layer, so the backward regenerates it.
+
+Supported configuration: ``rnn_type lstm | gru | rnn``, ``model_type concat
+| standard | manet`` (manet: at most 8 modalities), temporal attention with
+``concat``, ``num_layers >= 1`` (> 1 with concat, no attention); other
+configurations use the PyTorch path (``build_model`` decides).
 """
 import torch
 import torch.nn.functional as F
@@ -80,14 +87,18 @@ CELLS = {'lstm': (0, 4, (0, 1, 2, 3), (0, 1, 2, 3)),
 
 ATT_MAX_CHUNKS = 32  # frames per video supported by csrc/kernels/attention.hip
 MANET_MAX_FEATS = 8  # modalities with per-frame scorer weights (attention.hip)
+MAX_LAYERS = 5  # bf16 shadow segments of the fused Adam pass (SHADOW_MAX_SEGS)
 
 
 def engine_supports(opt):
-    ok = (getattr(opt, 'rnn_type', 'lstm') in CELLS and getattr(opt, 'num_layers', 1) == 1
+    layers = getattr(opt, 'num_layers', 1)
+    ok = (getattr(opt, 'rnn_type', 'lstm') in CELLS and 1 <= layers <= MAX_LAYERS
           and getattr(opt, 'model_type', 'concat') in ('concat', 'standard', 'manet')
           and opt.input_encoding_size % 64 == 0 and opt.input_encoding_size <= 1024
           and opt.rnn_size % 64 == 0)
     C = getattr(opt, 'num_chunks', 1)
+    if ok and layers > 1:
+        ok = getattr(opt, 'model_type', 'concat') == 'concat' and C == 1
     if ok and getattr(opt, 'model_type', 'concat') == 'manet':
         ok = C == 1 and len(getattr(opt, 'feat_dims', [])) <= MANET_MAX_FEATS
     if ok and C > 1:  # attention size == rnn_size (TemporalAttention)
@@ -118,7 +129,8 @@ class _DecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, vgate, w_ih, w_hh, emb_w, logit_w, logit_b, att_gv, att_pre, att_wq,
                 att_wa, att_ba, h0, c0, eng, labels, bos, R, T, modes, ss_prob, drop_p,
-                temperature, rng, vdiv, want_xe, use_counts, use_unfinished, save, want_full):
+                temperature, rng, vdiv, want_xe, use_counts, use_unfinished, save, want_full,
+                *up_w):
         has_att = att_gv is not None
         dev = logit_b.device
         att = []
@@ -137,7 +149,7 @@ class _DecoderFn(torch.autograd.Function):
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
             drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell,
-            state0)
+            state0, eng.upper_operands())
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
         full = None
@@ -156,6 +168,7 @@ class _DecoderFn(torch.autograd.Function):
             ctx.saved = (lse, *outs[4:9], seq, labels, bos)
             if has_att:  # Gv, P, W_q, w_a, alpha_all, q_all
                 ctx.att_saved = (att[0], att[1], att[2], att[3], outs[9], outs[10])
+            ctx.up_saved = outs[11 if has_att else 9:]  # (h, c, gates, hd_in) per upper layer
         else:
             ctx.saved = None
         ctx.att_shapes = (att_wa.shape, att_ba.shape) if has_att else None
@@ -228,7 +241,15 @@ class _DecoderFn(torch.autograd.Function):
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
             ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell,
-            ctx.state0)
+            ctx.state0, eng.upper_operands(ctx.up_saved))
+        ctx.up_saved = None
+        d_up = []
+        if eng.layers > 1:  # packed [W_ih | W_hh] of each upper layer
+            H = eng.H
+            for dwu in res[len(res) - (eng.layers - 1):]:
+                d_up += [dwu[:, :H].index_select(0, eng.dst_ie),
+                         dwu[:, H:].index_select(0, eng.dst_hh)]
+            res = res[:len(res) - (eng.layers - 1)]
         d_state = (None, None)
         if ctx.state0:
             d_state = (res[-2], res[-1])  # through W_hh, and the state carry
@@ -262,7 +283,7 @@ class _DecoderFn(torch.autograd.Function):
         nv = R // vdiv
         d_vgate = dvg.view(nv, vdiv, -1).sum(1)
         return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 5 + d_state + \
-            (None,) * 16
+            (None,) * 16 + tuple(d_up)
 
 
 class DecoderEngine:
@@ -303,6 +324,11 @@ class DecoderEngine:
         self.emb = torch.empty(V, E, **bf)
         self.wlog = torch.empty(V, H, **bf)
         self.ptab = torch.empty(V, 4 * H, dtype=torch.float32, device=dev)
+        # upper layers of a stacked decoder: packed [W_ih_l | W_hh_l] and a
+        # contiguous copy of W_hh_l (the step kernel's B operand)
+        self.layers = getattr(model, 'num_layers', 1)
+        self.wup = [torch.empty(4 * H, 2 * H, **bf) for _ in range(self.layers - 1)]
+        self.whh_up = [torch.empty(4 * H, H, **bf) for _ in range(self.layers - 1)]
         self.fused_refresh = False  # True once an optimizer writes the shadows
         self.direct_grad_slots = None
         self.direct_params = None
@@ -319,16 +345,22 @@ class DecoderEngine:
         rnn = m.core.rnn
         H, E = self.H, self.E
         empty = torch.empty(0, dtype=torch.bfloat16, device=self.wx.device)
-        segs = [(m.logit.weight, 0, 0, self.wlog, empty, 0, 0),
-                (m.embed.weight, 0, 0, self.emb, empty, 0, 0),
-                (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx, empty, 0, self.slots_ie),
-                (rnn.weight_hh_l0, 2, H, self.wx, self.whh_q, H, self.slots_hh)]
+        segs = [(m.logit.weight, 0, 0, self.wlog, empty, 0, 0, E),
+                (m.embed.weight, 0, 0, self.emb, empty, 0, 0, E),
+                (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx, empty, 0, self.slots_ie,
+                 E),
+                (rnn.weight_hh_l0, 2, H, self.wx, self.whh_q, H, self.slots_hh, E)]
         if self.attention:  # (MANet: the first F rows of the padded W_q)
-            segs.append((self._query_weight(), 0, 0, self.wq, empty, 0, 0))
+            segs.append((self._query_weight(), 0, 0, self.wq, empty, 0, 0, E))
+        for k in range(1, self.layers):  # packed [W_ih_k | W_hh_k]: "E" = H
+            segs += [(getattr(rnn, 'weight_ih_l%d' % k), 1, H, self.wup[k - 1], empty, 0,
+                      self.slots_ie, H),
+                     (getattr(rnn, 'weight_hh_l%d' % k), 2, H, self.wup[k - 1],
+                      self.whh_up[k - 1], H, self.slots_hh, H)]
         meta, dsts = [], []
-        for p, kind, cols, d, d2, ld2, slots in segs:
+        for p, kind, cols, d, d2, ld2, slots, e in segs:
             off, n = slot[id(p)]
-            meta.append([off, n, kind, cols, H, E, ld2, slots])
+            meta.append([off, n, kind, cols, H, e, ld2, slots])
             dsts += [d, d2]
         return torch.tensor(meta, dtype=torch.int64), dsts
 
@@ -348,6 +380,14 @@ class DecoderEngine:
         if self.attention:
             q = self._query_weight()
             self.wq.copy_(F.pad(q, (0, 0, 0, self.att_dim - q.size(0))))
+        H = self.H
+        for k in range(1, self.layers):
+            rnn = m.core.rnn
+            self.wup[k - 1][:, :H].copy_(self.pack_rows(getattr(rnn, 'weight_ih_l%d' % k),
+                                                        self.src_ie))
+            self.wup[k - 1][:, H:].copy_(self.pack_rows(getattr(rnn, 'weight_hh_l%d' % k),
+                                                        self.src_hh))
+            self.whh_up[k - 1].copy_(self.wup[k - 1][:, H:])
         self.update_ptab()
 
     @staticmethod
@@ -432,6 +472,18 @@ class DecoderEngine:
         vg = F.linear(fc, w_iv)
         return self.pack_rows(vg, self.src_ie, 1), fc.size(0)
 
+    def upper_operands(self, saved=None):
+        """Upper-layer operands of the native calls: forward / beam
+        {[W_ih | W_hh], W_hh} per layer; backward {[W_ih | W_hh], h, c, gates,
+        hd_in} per layer from the forward's saved tensors."""
+        out = []
+        for k in range(self.layers - 1):
+            if saved is None:
+                out += [self.wup[k], self.whh_up[k]]
+            else:
+                out += [self.wup[k], *saved[4 * k:4 * k + 4]]
+        return out
+
     def _query_weight(self):
         m = self.model
         return m.manet.f_h_m.weight if self.manet else m.temporal_att.f_h.weight
@@ -490,14 +542,17 @@ class DecoderEngine:
         m = model
         ws = (m.core.rnn.weight_ih_l0, m.core.rnn.weight_hh_l0, m.embed.weight, m.logit.weight,
               m.logit.bias)
+        ups = []
+        for k in range(1, self.layers):
+            ups += [getattr(m.core.rnn, 'weight_ih_l%d' % k), getattr(m.core.rnn, 'weight_hh_l%d' % k)]
         # (inside Function.forward grad mode is off, so decide here)
-        diff_in = [t for t in (vg, h0, c0) + tuple(att) if t is not None] + list(ws)
+        diff_in = [t for t in (vg, h0, c0) + tuple(att) if t is not None] + list(ws) + ups
         save = want_full or (torch.is_grad_enabled() and any(t.requires_grad for t in diff_in))
         return _DecoderFn.apply(vg, *ws, *att, h0, c0, self,
                                 labels.contiguous() if labels is not None else None, bos, R, T,
                                 modes, float(ss_prob), float(drop_p), float(temperature),
                                 self._rng(m.logit.bias.device), S, want_xe, use_counts,
-                                use_unfinished, save, want_full)
+                                use_unfinished, save, want_full, *ups)
 
     # -- public entry points ------------------------------------------------------
     def rollout(self, model, feats, labels):
@@ -587,5 +642,5 @@ class DecoderEngine:
         seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog,
                                          model.logit.bias.detach().float().contiguous(),
                                          vg.detach().float().contiguous(), K, model.seq_length,
-                                         BOS, att, self.cell, state0)
+                                         BOS, att, self.cell, state0, self.upper_operands())
         return seq, lp
