@@ -66,6 +66,8 @@ def parse():
                         'default, and the headline config, is 1: mean-pooled features)')
     p.add_argument('--cuda_graph', type=int, default=1,
                    help='replay the training step as a captured HIP graph (fused engine)')
+    p.add_argument('--grad_wire', default='fp32', choices=['fp32', 'bf16'],
+                   help='DP gradient reduction: fp32 all-reduce or bf16 wire / fp32 accumulation')
     p.add_argument('--json_out', default='')
     p.add_argument('--profile_phases', type=int, default=0,
                    help='print the mean per-phase GPU time (HIP events) of the timed steps')
@@ -129,7 +131,7 @@ def main():
         use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=2, scb_captions=S,
         impl=a.impl, precision=a.precision, reward_device=a.reward,
         dedupe_greedy=a.dedupe_greedy, seed=a.seed, loglevel='WARNING', save_last=0,
-        profile_phases=a.profile_phases, cuda_graph=a.cuda_graph)
+        profile_phases=a.profile_phases, cuda_graph=a.cuda_graph, grad_wire=a.grad_wire)
     opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
     opt.vocab_size = ds.vocab_size
     opt.seq_length = ds.seq_length
@@ -218,6 +220,7 @@ def main():
                    'reward': a.reward, 'mode': a.mode, 'params': n_params,
                    'dedupe_greedy': a.dedupe_greedy,
                    'cuda_graph': int(trainer._graph is not None),
+                   'grad_wire': a.grad_wire,
                    'temporal_attention_frames': a.num_chunks if a.num_chunks > 1 else None},
         'final_loss': loss, 'datagen_s': round(t_gen, 1),
         'world_size_seen': ctx.world_size, 'backend': ctx.backend or 'none',

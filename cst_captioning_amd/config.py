@@ -122,6 +122,9 @@ def build_parser():
     add('--cuda_graph', type=int, default=1,
         help='replay the fused-engine training step as a captured HIP graph (1) or enqueue '
              'it eagerly every step (0)')
+    add('--grad_wire', type=str, default='fp32', choices=['fp32', 'bf16'],
+        help='data-parallel gradient reduction: fp32 all-reduce, or bf16 on the wire with '
+             'fp32 accumulation (all-to-all + all-gather, half the bytes)')
     add('--profile_phases', type=int, default=0, help='log per-phase HIP-event timings')
     return p
 

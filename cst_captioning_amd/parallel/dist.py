@@ -189,9 +189,14 @@ class FlatGradBucket:
     clip + Adam kernel cover every parameter.
     """
 
-    def __init__(self, params, first=()):
+    def __init__(self, params, first=(), world_size=1, wire='fp32'):
         """``first``: parameters placed at the start of the buffer (the ones
-        an :class:`EarlyAllReduce` reduces ahead of the rest)."""
+        an :class:`EarlyAllReduce` reduces ahead of the rest).  ``wire``:
+        'fp32' (one all-reduce) or 'bf16' (see :meth:`all_reduce`); the buffer
+        is padded so it splits into ``world_size`` equal chunks."""
+        if wire not in ('fp32', 'bf16'):
+            raise ValueError('wire must be fp32 or bf16')
+        self.wire = wire
         params = [p for p in params if p.requires_grad]
         first_ids = {id(p) for p in first}
         self.params = [p for p in params if id(p) in first_ids] + \
@@ -207,7 +212,8 @@ class FlatGradBucket:
         # a collective of its own.  It is zero in every healthy step, so it adds
         # nothing to the gradient norm and Adam leaves its (zero) parameter
         # slot at zero.
-        padded = (total + 1 + 63) // 64 * 64
+        quantum = 64 * max(1, world_size)
+        padded = (total + 1 + quantum - 1) // quantum * quantum
         self.data = torch.zeros(padded, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(padded, dtype=torch.float32, device=dev)
         self.flag = self.grad[total:total + 1]
@@ -251,6 +257,28 @@ class FlatGradBucket:
         return n
 
     def all_reduce(self, ctx):
+        """Sum the gradient over ranks and divide by the world size.
+
+        wire 'fp32': one RCCL ring all-reduce of the fp32 buffer (plus the
+        early vocab-head slice, if one was launched).  wire 'bf16': half the
+        bytes on xGMI with fp32 accumulation -- every rank sends chunk j of its
+        gradient as bf16 to rank j (all-to-all), sums the N received chunks in
+        fp32, and the reduced chunks are all-gathered as bf16.  Per rank that
+        moves (N-1)/N of the buffer in bf16 twice, half of the fp32 ring's
+        2 (N-1)/N x 4 bytes; the applied gradient carries one bf16 rounding of
+        each input and of the sum (relative 2^-9), which Adam's normalised
+        update tolerates.  The skip flag (0 / 1) is exact in bf16."""
+        if ctx.enabled and self.wire == 'bf16':
+            N = ctx.world_size
+            chunk = self.grad.numel() // N
+            send = self.grad.view(N, chunk).to(torch.bfloat16)
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send)
+            mine = recv.float().sum(0).div_(N).to(torch.bfloat16)
+            out = torch.empty(N * chunk, dtype=torch.bfloat16, device=self.grad.device)
+            dist.all_gather_into_tensor(out, mine)
+            self.grad.copy_(out)
+            return
         if ctx.enabled:
             early = self.early is not None and self.early.work is not None
             rest = self.grad[self.early.n:] if early else self.grad

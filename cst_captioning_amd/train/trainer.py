@@ -87,13 +87,15 @@ class Trainer:
         self.rl_criterion = RewardCriterion()
         self.ctx.broadcast_module(model)
         early = [model.logit.weight, model.logit.bias]
-        self.bucket = FlatGradBucket(model.parameters(), first=early)
+        self.bucket = FlatGradBucket(model.parameters(), first=early,
+                                     world_size=self.ctx.world_size,
+                                     wire=getattr(opt, 'grad_wire', 'fp32'))
         # Early all-reduce of the vocab-head gradients under the reverse loop:
         # eager steps only.  With HIP graphs every step (eager warm-up or
         # replay) issues the same single bucket all-reduce, so ranks can never
         # disagree on the collective sequence.
         if (engine is not None and self.ctx.enabled and not getattr(opt, 'no_early_allreduce', 0)
-                and not getattr(opt, 'cuda_graph', 1)):
+                and not getattr(opt, 'cuda_graph', 1) and self.bucket.wire == 'fp32'):
             from ..parallel.dist import EarlyAllReduce
             self.bucket.early = EarlyAllReduce(self.ctx, self.bucket, early)
             engine.early_grad_hook = self.bucket.early

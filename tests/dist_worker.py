@@ -18,7 +18,8 @@ ARGS = ['--synthetic', 'msvd', '--synthetic_videos', '24', '--synthetic_vocab', 
         '--test_batch_size', '3', '--test_seq_per_img', '3', '--beam_size', '2',
         '--impl', os.environ.get('CSTCAP_TEST_IMPL', 'torch'), '--loglevel', 'WARNING',
         '--drop_prob_lm', '0', '--cuda_graph', os.environ.get('CSTCAP_TEST_GRAPH', '1'),
-        '--learning_rate', '1e-3', '--language_eval', '0']
+        '--learning_rate', '1e-3', '--language_eval', '0',
+        '--grad_wire', os.environ.get('CSTCAP_TEST_WIRE', 'fp32')]
 
 
 def build(rank, world, device):

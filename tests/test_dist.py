@@ -5,7 +5,9 @@ torchrun with the gloo backend, world sizes 1, 2 and 4 on the CPU.
   * C2: the all-reduced gradient equals the gradient of the mean of the
     per-shard losses computed in one process;
   * parameters stay bit-identical across ranks after optimizer steps;
-  * C4: sharded validation + all-gather reproduces the single-rank result.
+  * C4: sharded validation + all-gather reproduces the single-rank result;
+  * the bf16-wire reduction (all-to-all + fp32 sum + all-gather) matches the
+    reference gradient to bf16 rounding and keeps the ranks in lock-step.
 """
 import os
 import socket
@@ -27,8 +29,9 @@ def _free_port():
     return p
 
 
-def _run(world, out):
+def _run(world, out, wire='fp32'):
     env = dict(os.environ)
+    env['CSTCAP_TEST_WIRE'] = wire
     env['PYTHONPATH'] = ROOT + os.pathsep + env.get('PYTHONPATH', '')
     env['CUDA_VISIBLE_DEVICES'] = ''  # CPU ranks (gloo)
     env['OMP_NUM_THREADS'] = '1'
@@ -46,15 +49,22 @@ def runs(tmp_path_factory):
     return {w: _run(w, str(d / ('w%d.pt' % w))) for w in (1, 2, 4)}
 
 
-def _reference_grad(world):
-    """Gradient of mean_k(loss on shard k), one process."""
+@pytest.fixture(scope='module')
+def runs_bf16(tmp_path_factory):
+    d = tmp_path_factory.mktemp('dist_bf16')
+    return {w: _run(w, str(d / ('w%d.pt' % w)), 'bf16') for w in (2, 4)}
+
+
+def _reference_grad(world, with_abs=False):
+    """Gradient of mean_k(loss on shard k), one process (and, with_abs, the
+    mean of the per-shard gradients' magnitudes)."""
     sys.path.insert(0, HERE)
     import dist_worker as W
     from cst_captioning_amd.parallel import DistContext
     from cst_captioning_amd.train.trainer import Trainer
     dev = torch.device('cpu')
     opt, model, engine, _, _ = W.build(0, world, dev)
-    grads = None
+    grads = mags = None
     for k in range(world):
         _, _, _, loader, _ = W.build(k, world, dev)
         tr = Trainer(opt, model, loader, None, DistContext(device=dev), engine)
@@ -63,6 +73,9 @@ def _reference_grad(world):
         loss.backward()
         g = tr.bucket.grad.clone() / world
         grads = g if grads is None else grads + g
+        mags = g.abs() if mags is None else mags + g.abs()
+    if with_abs:
+        return model, grads, mags
     return model, grads
 
 
@@ -73,14 +86,15 @@ def test_broadcast_and_allreduce(runs):
     # with the same seed, so its init matches
     init_ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
     torch.testing.assert_close(r2['init'], init_ref, rtol=0, atol=0)
-    torch.testing.assert_close(r2['grad'], ref, rtol=1e-5, atol=1e-7)
+    # (the bucket's zero padding depends on the world size)
+    torch.testing.assert_close(r2['grad'][:ref.numel()], ref, rtol=1e-5, atol=1e-7)
     assert r2['same_after_steps']
 
 
 def test_allreduce_world4(runs):
     r4 = runs[4]
     _, ref = _reference_grad(4)
-    torch.testing.assert_close(r4['grad'], ref, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(r4['grad'][:ref.numel()], ref, rtol=1e-5, atol=1e-7)
     assert r4['same_after_steps']
 
 
@@ -108,3 +122,20 @@ def test_sharded_validation_matches_single_rank(runs):
     # (the XE 'Loss' depends on which seq_per_img captions each rank draws, as in
     # the reference's random caption selection, so only the beam outputs are compared)
     assert runs[1]['world'] == 1 and runs[2]['world'] == 2
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_bf16_wire_reduction(runs_bf16, world):
+    r = runs_bf16[world]
+    _, ref, mag = _reference_grad(world, with_abs=True)
+    g = r['grad']
+    assert g.numel() % (64 * world) == 0  # the buffer splits into equal chunks
+    n = min(ref.numel(), g.numel())
+    ref, mag = ref[:n], mag[:n]
+    # one bf16 rounding (relative 2^-9) of every rank's input and of the sum
+    err = (g[:n] - ref).abs()
+    bound = 2 ** -8 * (mag + ref.abs()) + 1e-9
+    assert (err <= bound).all(), (err - bound).max()
+    assert err.max() > 0  # the wire really is bf16
+    assert r['same_after_steps'] and r['nan_skip_all']
+    assert r['xe_logged'] == pytest.approx([sum(r['xe_losses']) / world], rel=1e-6)
