@@ -39,7 +39,7 @@ std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor 
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
-                       int64_t flags, bool save, int64_t iters);
+                       int64_t flags, bool save, int64_t iters, int64_t variant);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
                        double log_ref_len, int64_t use_eos);
 at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,

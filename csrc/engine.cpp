@@ -913,7 +913,7 @@ static double time_launches(F&& launch, int64_t iters, hipStream_t st) {
 }
 
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
-                       int64_t flags, bool save, int64_t iters) {
+                       int64_t flags, bool save, int64_t iters, int64_t variant) {
   const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
   TORCH_CHECK(H % 64 == 0 && wlog.size(1) == H && blog.numel() == V, "shapes");
   auto dev = hd.device();
@@ -927,11 +927,12 @@ double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tens
   hipStream_t st = cur_stream();
   return time_launches(
       [&](int i) {
-        launch_vocab_fwd(reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R,
-                         (int)H, reinterpret_cast<const uint16_t*>(wlog.data_ptr()),
-                         blog.data_ptr<float>(), (int)V,
-                         save ? reinterpret_cast<uint16_t*>(logits.data_ptr()) : nullptr, ldl,
-                         part.data_ptr(), tg, 1, (int)flags, 1.f, rng_ptr(rng), i, st);
+        launch_vocab_fwd_variant((int)variant, reinterpret_cast<const uint16_t*>(hd.data_ptr()),
+                                 (int)H, (int)R, (int)H,
+                                 reinterpret_cast<const uint16_t*>(wlog.data_ptr()),
+                                 blog.data_ptr<float>(), (int)V,
+                                 save ? reinterpret_cast<uint16_t*>(logits.data_ptr()) : nullptr,
+                                 ldl, part.data_ptr(), tg, 1, (int)flags, 1.f, rng_ptr(rng), i, st);
       },
       iters, st);
 }

@@ -24,11 +24,13 @@ __device__ __forceinline__ int xcd_remap_g(int bid, int nwg) {
 
 constexpr int LG_BM = 128, LG_BN = 64, LG_STAGES = 3;
 using LGTile = Tile<LG_BM, LG_BN, LG_STAGES>;
+using LGTile2 = Tile<LG_BM, LG_BN, 2>;
 
 __host__ __device__ constexpr int lstm_gemm_blocks(int R, int H, int NQ = 0) {
   return ((4 * H + NQ) / LG_BN) * ((R + LG_BM - 1) / LG_BM);
 }
 
+template <class LT = LGTile>
 __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restrict__ h, int R,
                                                 int H, const uint16_t* __restrict__ whh,
                                                 const float* __restrict__ vgate, int vdiv,
@@ -39,7 +41,7 @@ __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restr
   const int nt = b / n_rt, rt = b % n_rt;
   const int r0 = rt * LG_BM, n0 = nt * LG_BN;
   const int nk = H / 64;
-  f32x16 acc[LGTile::TM][LGTile::TN];
+  f32x16 acc[LT::TM][LT::TN];
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     DmaSrc<LG_BM / 32> a;
@@ -60,10 +62,10 @@ __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restr
       bsrc.voff0[i] = (n0 + row) * H * 2 + dma_chunk(row, lane) * 16;
       bsrc.voff1[i] = bsrc.voff0[i];
     }
-    gemm_nt_mainloop<LGTile>(nk, a, bsrc, lds, acc);
+    gemm_nt_mainloop<LT>(nk, a, bsrc, lds, acc);
   }
   float* C = reinterpret_cast<float*>(lds);
-  store_acc_to_lds<LGTile>(acc, C, [](int) { return 0.f; });
+  store_acc_to_lds<LT>(acc, C, [](int) { return 0.f; });
   __syncthreads();
   // 16 lanes per row x 4 columns: 256-byte coalesced fp32 rows
   const int u = threadIdx.x & 15, rg = threadIdx.x >> 4;
@@ -72,7 +74,7 @@ __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restr
   for (int i = 0; i < LG_BM / 16; ++i) {
     const int row = rg + 16 * i, r = r0 + row;
     if (r < R) {
-      const float4 x = *reinterpret_cast<const float4*>(C + row * LGTile::CSTRIDE + 4 * u);
+      const float4 x = *reinterpret_cast<const float4*>(C + row * LT::CSTRIDE + 4 * u);
       if (qtile) {
         *reinterpret_cast<float4*>(q_out + (int64_t)r * NQ + (n0 - 4 * H) + 4 * u) = x;
       } else if (vgate != nullptr) {

@@ -214,11 +214,17 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       for (int k = 0; k < 16; ++k) m = fmaxf(m, x[i][k]);
     const float msafe = m == -INFINITY ? 0.f : m;
     const float ml = msafe * L2E;
+    // exp weights stay in registers for the sampler's inverse CDF (no second
+    // exp pass at temperature 1)
+    float ew[TM][16];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += __builtin_amdgcn_exp2f(fmaf(x[i][k], L2E, -ml));
+      for (int k = 0; k < 16; ++k) {
+        ew[i][k] = __builtin_amdgcn_exp2f(fmaf(x[i][k], L2E, -ml));
+        s += ew[i][k];
+      }
 
     GroupStat st;
     st.m = m;
@@ -255,7 +261,10 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int k = 0; k < 16; ++k) sw += __builtin_amdgcn_exp2f(fmaf(x[i][k], wsc, -wl));
+          for (int k = 0; k < 16; ++k) {
+            ew[i][k] = __builtin_amdgcn_exp2f(fmaf(x[i][k], wsc, -wl));
+            sw += ew[i][k];
+          }
       }
       const uint32_t rr = (uint32_t)min(r, R - 1);
       const uint32_t seed = rng_seed(rng, RNG_SLOT_SAMPLE);
@@ -271,8 +280,7 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          const float wv = temp1 ? __builtin_amdgcn_exp2f(fmaf(x[i][k], L2E, -ml))
-                                 : __builtin_amdgcn_exp2f(fmaf(x[i][k], wsc, -wl));
+          const float wv = ew[i][k];
           cum += wv;
           const bool hit = cand < 0 && cum >= tm && wv > 0.f;
           cand = hit ? vb + 32 * i + 8 * (k >> 2) + (k & 3) : cand;
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(VOCAB_TR_PARAMS)
 // tiles leave idle instead of running before it.  The first n_lstm_pad
 // blocks (a multiple of 8, so both halves keep their XCD-aware mapping) are
 // LSTM tiles.
-template <int BN, int STAGES, int OCC>
+template <int BN, int STAGES, int OCC, class LT>
 __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
     VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
     const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad, int NQ,
@@ -343,7 +351,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) char lds[];
   if ((int)blockIdx.x < n_lstm_pad) {
     if ((int)blockIdx.x < lstm_gemm_blocks(R, H, NQ))
-      lstm_gemm_block(blockIdx.x, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
+      lstm_gemm_block<LT>(blockIdx.x, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
     return;
   }
   vocab_tr_block<BN, STAGES>(blockIdx.x - n_lstm_pad, lds, VOCAB_TR_ARGS);
@@ -671,9 +679,8 @@ __global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
 }
 
 // -------------------------------------------------------------------------------
-// Launchers.  Tiles: 128 vocab x 128 caption rows, 2 LDS stages (64 KB, 2
-// blocks per CU); 64-row tiles when there are only 64 rows (the greedy
-// baseline decodes one row per video).
+// Launchers.  Tiles: 128 vocab x 64 caption rows, 2 LDS stages (48 KB, 3
+// blocks per CU).
 template <int BN, int STAGES, int OCC>
 static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
@@ -701,12 +708,31 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
                       const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                       const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                       const uint32_t* rng, int step, hipStream_t stream) {
-  if (R <= 64)
-    launch_vocab_fwd_tr<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
-                                  flags, inv_temp, rng, step, stream);
-  else
-    launch_vocab_fwd_tr<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                   tgt_stride, flags, inv_temp, rng, step, stream);
+  // (microbenchmark at V = 10,509: 31.0 vs 33.5 us at R = 1280, 8.7 vs 12.4
+  // us at R = 64 against 128-row tiles, 2 blocks per CU)
+  launch_vocab_fwd_tr<64, 2, 3>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
+                                flags, inv_temp, rng, step, stream);
+}
+
+// microbenchmark only (scripts/microbench_kernels.py): other tile / pipeline
+// shapes of the vocab kernel, <BN, STAGES, OCC>
+void launch_vocab_fwd_variant(int variant, const uint16_t* hd, int ldh, int R, int H,
+                              const uint16_t* W, const float* bias, int V, uint16_t* logits16,
+                              int64_t ldl, void* part, const int64_t* tgt, int64_t tgt_stride,
+                              int flags, float inv_temp, const uint32_t* rng, int step,
+                              hipStream_t stream) {
+#define VV(BN, ST, OC)                                                                          \
+  launch_vocab_fwd_tr<BN, ST, OC>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, \
+                                  flags, inv_temp, rng, step, stream)
+  switch (variant) {
+    case 1: VV(128, 3, 1); break;
+    case 2: VV(128, 4, 1); break;
+    case 3: VV(64, 3, 2); break;
+    case 5: VV(64, 4, 1); break;
+    case 6: VV(128, 2, 2); break;
+    default: VV(64, 2, 3); break;
+  }
+#undef VV
 }
 
 int vocab_num_tiles(int V) { return (V + VT_V - 1) / VT_V; }
@@ -731,7 +757,7 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   post_launch("vocab_combine_kernel", stream);
 }
 
-template <int BN, int STAGES, int OCC>
+template <int BN, int STAGES, int OCC, class LT = LGTile>
 static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
@@ -742,16 +768,16 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   constexpr int LV = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
                          ? TL::STAGES * TL::STAGE_BYTES
                          : 4 * BN * (int)sizeof(GroupStat);
-  constexpr int LDS = LV > LGTile::LDS_BYTES ? LV : LGTile::LDS_BYTES;
+  constexpr int LDS = LV > LT::LDS_BYTES ? LV : LT::LDS_BYTES;
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
   const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H, NQ) + 7) / 8 * 8 : 0;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC>,
+    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC>), dim3(n_l + n_vt * n_rt), dim3(256),
+  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT>), dim3(n_l + n_vt * n_rt), dim3(256),
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
                      tgt, tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate, vdiv, pre, n_l,
                      NQ, q_out);
@@ -764,14 +790,13 @@ void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
                            float* q_out) {
-  if (R <= 64)
-    launch_vocab_lstm_t<64, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
-                                  flags, inv_temp, rng, step, h_t, whh, vgate, vdiv, pre, NQ,
-                                  q_out, stream);
-  else
-    launch_vocab_lstm_t<128, 2, 2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                   tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate, vdiv,
-                                   pre, NQ, q_out, stream);
+  // 64-row tiles, 3 blocks per CU (48 KB of LDS each; the recurrent tiles use
+  // 2 stages to fit): one block's epilogue overlaps the others' main loops.
+  // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
+  // CU (3 interleaved rounds; profiles/r2/ab_vocab_tiles.txt)
+  launch_vocab_lstm_t<64, 2, 3, LGTile2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                         tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate,
+                                         vdiv, pre, NQ, q_out, stream);
 }
 
 int vocab_bwd_ds_blocks(int T, int R) { return (int)(((int64_t)T * R + DS_ROWS - 1) / DS_ROWS); }

@@ -43,6 +43,11 @@ void launch_shadow_refresh(const float* p, const ShadowSegs& ss, hipStream_t str
 // vocab.hip
 enum SelModeHost : int { SEL_GT_H = 0, SEL_SAMPLE_H = 1, SEL_GREEDY_H = 2, SEL_SS_H = 3 };
 int vocab_num_tiles(int V);
+void launch_vocab_fwd_variant(int variant, const uint16_t* hd, int ldh, int R, int H,
+                              const uint16_t* W, const float* bias, int V, uint16_t* logits16,
+                              int64_t ldl, void* part, const int64_t* tgt, int64_t tgt_stride,
+                              int flags, float inv_temp, const uint32_t* rng, int step,
+                              hipStream_t stream);
 int vocab_partial_bytes();
 // rng (device, nullable): int32[2] seeds {dropout, sampling}, see common.h
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,

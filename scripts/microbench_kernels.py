@@ -4,6 +4,8 @@ vocab_fwd at the rollout shape (R = 1280 rows) and the greedy shape (R = 64),
 with the epilogue pieces switched on one at a time:
   mainloop = GEMM only; stats = max/LSE (+target); sample; sample+save
   (fp16 logits for the backward); argmax.
+VARIANTS="0 1 2 ..." times other <BN, STAGES, OCC> shapes of the vocab kernel
+(launch_vocab_fwd_variant in csrc/kernels/vocab.hip).
 """
 import json
 import os
@@ -21,15 +23,17 @@ V, H = 10509, 512
 W = (torch.randn(V, H, device=dev) * 0.05).bfloat16()
 b = torch.randn(V, device=dev) * 0.1
 res = {}
+variants = [int(v) for v in os.environ.get('VARIANTS', '0').split()]
 for R in (1280, 64):
     hd = torch.randn(R, H, device=dev).bfloat16()
     tgt = torch.randint(0, V, (R,), device=dev)
-    for name, flags, save, t in (('mainloop', 4, False, None), ('stats', 0, False, tgt),
-                                 ('sample', 1, False, None), ('sample_save', 1, True, None),
-                                 ('argmax', 2, False, None)):
-        us = C.vocab_fwd_bench(hd, W, b, t if t is not None else torch.empty(0, dtype=torch.long, device=dev),
-                               flags, save, 50)
-        res['R%d_%s' % (R, name)] = round(us, 2)
+    none = torch.empty(0, dtype=torch.long, device=dev)
+    for var in variants:
+        for name, flags, save, t in (('mainloop', 4, False, None), ('stats', 0, False, tgt),
+                                     ('sample', 1, False, None), ('sample_save', 1, True, None),
+                                     ('argmax', 2, False, None)):
+            us = C.vocab_fwd_bench(hd, W, b, t if t is not None else none, flags, save, 50, var)
+            res['v%d_R%d_%s' % (var, R, name)] = round(us, 2)
 toks = torch.randint(0, V, (28 * 1280,), device=dev)
 res['token_sort_us'] = round(C.token_sort_bench(toks, V, 50), 2)
 if os.environ.get('DS', '1') == '1':
