@@ -142,6 +142,19 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
                        ? G[(int64_t)c * G44 + tid + j * ATT_THREADS]
                        : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // accumulate: the rows' current pre-activations (written by the previous
+  // launch) are requested up front too, so the final add does not wait on a
+  // second memory round trip
+  float4 acc0[ATT_GPF][ATT_RPW];
+  if (gpf && accumulate) {
+#pragma unroll
+    for (int j = 0; j < ATT_GPF; ++j)
+#pragma unroll
+      for (int s = 0; s < ATT_RPW; ++s)
+        acc0[j][s] = (s < nr && tid + j * ATT_THREADS < G44)
+                         ? reinterpret_cast<const float4*>(vg_out + (int64_t)(r0 + s) * G4)[tid + j * ATT_THREADS]
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   int qrow[ATT_RPW];
 #pragma unroll
   for (int s = 0; s < ATT_RPW; ++s) {
@@ -192,7 +205,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
   }
   __syncthreads();
   // vgate_r = sum_c alpha_rc Gv[b, c]: each thread owns float4 column groups
-  auto emit = [&](int cg, const float4* gcol) {
+  auto emit = [&](int cg, const float4* gcol, int pj) {  // pj: prefetched group, or -1
     float4 acc[ATT_RPW];
 #pragma unroll
     for (int s = 0; s < ATT_RPW; ++s) acc[s] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -215,7 +228,14 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
       if (s < nr) {
         float4* dst = reinterpret_cast<float4*>(vg_out + (int64_t)(r0 + s) * G4) + cg;
         if (accumulate) {
-          const float4 o = *dst;
+          float4 o;
+          if (pj >= 0) {
+#pragma unroll
+            for (int j = 0; j < ATT_GPF; ++j)
+              if (j == pj) o = acc0[j][s];
+          } else {
+            o = *dst;
+          }
           acc[s].x += o.x, acc[s].y += o.y, acc[s].z += o.z, acc[s].w += o.w;
         }
         *dst = acc[s];
@@ -225,14 +245,14 @@ __global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
   if (gpf) {
 #pragma unroll
     for (int j = 0; j < ATT_GPF; ++j)
-      if (tid + j * ATT_THREADS < G44) emit(tid + j * ATT_THREADS, gr[j]);
+      if (tid + j * ATT_THREADS < G44) emit(tid + j * ATT_THREADS, gr[j], j);
   } else {
     for (int cg = tid; cg < G44; cg += ATT_THREADS) {
       float4 gcol[MAXC];
 #pragma unroll
       for (int c = 0; c < MAXC; ++c)
         gcol[c] = c < C ? G[(int64_t)c * G44 + cg] : make_float4(0.f, 0.f, 0.f, 0.f);
-      emit(cg, gcol);
+      emit(cg, gcol, -1);
     }
   }
 }
@@ -278,7 +298,18 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     }
   }
 
-  // 1. dalpha[s][c] = dG_r . Gv[b, c]
+  // 1. dalpha[s][c] = dG_r . Gv[b, c]  (the first ATT_GPF column groups of the
+  // rows' dG are requested up front with the partial slots)
+  uint2 dgp[ATT_GPF][ATT_RPW];
+#pragma unroll
+  for (int j = 0; j < ATT_GPF; ++j)
+#pragma unroll
+    for (int s = 0; s < ATT_RPW; ++s) {
+      const int cg = tid + j * ATT_THREADS;
+      dgp[j][s] = (s < nr && cg < (G4 >> 2))
+                      ? *reinterpret_cast<const uint2*>(dG + (int64_t)(r0 + s) * ldg + 4 * cg)
+                      : make_uint2(0u, 0u);
+    }
   float part[ATT_RPW][MAXC];
 #pragma unroll
   for (int s = 0; s < ATT_RPW; ++s)
@@ -286,13 +317,14 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     for (int c = 0; c < MAXC; ++c) part[s][c] = 0.f;
   const float4* G = reinterpret_cast<const float4*>(gv + (int64_t)b * C * G4);
   const int G44 = G4 >> 2;
-  for (int cg = tid; cg < G44; cg += ATT_THREADS) {
+  for (int cg = tid, j = 0; cg < G44; cg += ATT_THREADS, ++j) {
     float4 d[ATT_RPW];
 #pragma unroll
     for (int s = 0; s < ATT_RPW; ++s) {
       d[s] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (s < nr) {
-        const uint2 raw = *reinterpret_cast<const uint2*>(dG + (int64_t)(r0 + s) * ldg + 4 * cg);
+        const uint2 raw = j < ATT_GPF ? dgp[j < ATT_GPF ? j : 0][s]
+                                      : *reinterpret_cast<const uint2*>(dG + (int64_t)(r0 + s) * ldg + 4 * cg);
         d[s] = make_float4(bf2f(raw.x & 0xffff), bf2f(raw.x >> 16), bf2f(raw.y & 0xffff),
                            bf2f(raw.y >> 16));
       }

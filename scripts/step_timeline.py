@@ -3,7 +3,7 @@
 usage: python scripts/step_timeline.py <kernel_trace.csv> [step_from_end]
 Consecutive launches of the same kernel on the same stream are merged into
 one line: start offset (us from the step start), span, count, summed busy
-time, stream id.  The step spans from the end of one adam_update kernel to
+time, hardware queue id.  The step spans from the end of one adam_update kernel to
 the end of the next.
 """
 import csv
@@ -13,7 +13,7 @@ path = sys.argv[1]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 rows = list(csv.DictReader(open(path)))
 ev = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'][:60],
-             r['Stream_Id']) for r in rows)
+             r['Queue_Id']) for r in rows)  # (graph replays: streams show as hardware queues)
 adam = [e for e in ev if 'adam_update' in e[2]]
 lo, hi = adam[-1 - k][1], adam[-k][1]
 ev = [e for e in ev if e[0] >= lo and e[1] <= hi]
