@@ -23,7 +23,10 @@ def _load():
         return
     try:
         import torch  # noqa: F401  (libtorch must be loaded first)
-        from . import _C  # type: ignore
+        if os.environ.get('CSTCAP_EXT') == 'san':  # host-sanitized build (setup.py)
+            from . import _C_san as _C  # type: ignore
+        else:
+            from . import _C  # type: ignore
         _mod = _C
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e

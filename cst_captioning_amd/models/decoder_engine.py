@@ -199,7 +199,9 @@ class _DecoderFn(torch.autograd.Function):
             # (+ the gathered terms), written as bf16 into the logits buffer
             V = logit_b_numel = eng.V
             n_sel = g_sel.size(1) if g_sel is not None else 0
-            G = dfull.permute(1, 0, 2).float()  # (n, R, V)
+            # (n, R, V); a private dense copy: the incoming gradient may be an
+            # expanded view (e.g. of full.sum()) or shared with other nodes
+            G = dfull.permute(1, 0, 2).float().clone(memory_format=torch.contiguous_format)
             if g_sel is not None:
                 G[:n_sel].scatter_add_(2, seq.t()[:n_sel].unsqueeze(2), g_sel.t().unsqueeze(2))
             if g_xe is not None:

@@ -66,12 +66,26 @@ class BuildWithHip(BuildExtension):
         super().run()
 
 
+# Host-sanitized variant of the same extension: the C++ host
+# runtime (decoder executor, bindings, CIDEr-D host code) under UBSan with
+# abort-on-error plus libstdc++ container bounds checks, linked against the
+# same gfx950 kernel objects.  CSTCAP_HOST_SANITIZE=1 python setup.py
+# build_ext --inplace builds cst_captioning_amd._C_san; CSTCAP_EXT=san loads it
+# instead of _C (tests/test_gpu_debug.py runs the engine through it).  UBSan
+# needs no preloaded runtime (libubsan is an ordinary shared-library
+# dependency), unlike ASan, which the host-only tests cover
+# (tests/test_native_sanitizers.py).
+SANITIZE = os.environ.get('CSTCAP_HOST_SANITIZE') == '1'
 ext = CppExtension(
-    'cst_captioning_amd._C',
+    'cst_captioning_amd._C_san' if SANITIZE else 'cst_captioning_amd._C',
     ['csrc/engine.cpp', 'csrc/bindings.cpp', 'csrc/host/cider_host.cpp'],
     include_dirs=[os.path.join(HERE, 'csrc')] + include_paths(device_type='cuda'),
-    define_macros=[('__HIP_PLATFORM_AMD__', '1'), ('USE_ROCM', '1')],
-    extra_compile_args=['-O3', '-std=c++17'],
+    define_macros=[('__HIP_PLATFORM_AMD__', '1'), ('USE_ROCM', '1')]
+    + ([('_GLIBCXX_ASSERTIONS', '1')] if SANITIZE else []),
+    extra_compile_args=(['-O1', '-g', '-std=c++17', '-fsanitize=undefined',
+                         '-fno-sanitize-recover=all', '-fno-omit-frame-pointer']
+                        if SANITIZE else ['-O3', '-std=c++17']),
+    extra_link_args=['-fsanitize=undefined'] if SANITIZE else [],
     extra_objects=hip_objects(),
     library_dirs=[os.path.join(ROCM, 'lib')],
     libraries=['amdhip64', 'c10_hip', 'torch_hip'],

@@ -54,3 +54,23 @@ def test_rollout_is_deterministic_for_a_seed(C):
     with torch.no_grad():
         seq2, _, _ = eng.rollout(model, data['feats'], data['labels'])
     assert not torch.equal(seq2, outs[0][0])  # a different seed draws different samples
+
+
+def test_engine_under_host_ubsan():
+    """The C++ host runtime (decoder executor, backward schedule, beam search,
+    shadow segments, graph-captured step) under UBSan with abort-on-error and
+    libstdc++ bounds checks (the ``_C_san`` build of setup.py): every decoder
+    configuration and a few captured training steps run clean."""
+    import glob
+    root = os.path.dirname(HERE)
+    if not glob.glob(os.path.join(root, 'cst_captioning_amd', '_C_san*.so')):
+        pytest.fail('host-sanitized extension not built: '
+                    'CSTCAP_HOST_SANITIZE=1 python setup.py build_ext --inplace')
+    env = dict(os.environ, CSTCAP_EXT='san',
+               UBSAN_OPTIONS='halt_on_error=1:print_stacktrace=1')
+    res = subprocess.run([sys.executable, os.path.join(HERE, 'gpu_san_worker.py')], env=env,
+                         capture_output=True, text=True, timeout=115)
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-4000:]
+    assert 'runtime error' not in out, out[-4000:]
+    assert out.count('ubsan ok') == 6, out[-2000:]
