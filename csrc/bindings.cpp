@@ -35,6 +35,11 @@ double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, a
                           int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
 std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V);
+at::Tensor featpool_forward(std::vector<at::Tensor> xs, std::vector<at::Tensor> ws,
+                            std::vector<at::Tensor> bs, double drop_p, at::Tensor rng);
+std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
+                                          std::vector<at::Tensor> xs,
+                                          std::vector<at::Tensor> ws, double drop_p);
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);
@@ -113,4 +118,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("token_sort", &cst::token_sort);
   m.def("vocab_select", &cst::vocab_select);
   m.def("beam_search", &cst::beam_search);
+  m.def("featpool_forward", &cst::featpool_forward);
+  m.def("featpool_backward", &cst::featpool_backward);
 }

@@ -676,6 +676,78 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   return out;
 }
 
+// FeatPool (csrc/kernels/featpool.hip): xs[f] (rows, d_f), ws[f] (H, d_f),
+// bs[f] (H), all fp32 contiguous GPU tensors; returns the concatenated
+// (rows, F*H) output after ReLU and dropout (mask from rng slot 0).
+static FeatPoolArgs featpool_args(const std::vector<at::Tensor>& xs,
+                                  const std::vector<at::Tensor>& ws,
+                                  const std::vector<at::Tensor>& bs) {
+  TORCH_CHECK(!xs.empty() && xs.size() <= FEATPOOL_MAX_F && ws.size() == xs.size() &&
+                  (bs.empty() || bs.size() == xs.size()),
+              "featpool: 1..", FEATPOOL_MAX_F, " modalities, one weight (and bias) each");
+  FeatPoolArgs a{};
+  a.nf = (int)xs.size();
+  a.rows = (int)xs[0].size(0);
+  a.H = (int)ws[0].size(0);
+  TORCH_CHECK(a.H % 64 == 0, "featpool: output size must be a multiple of 64");
+  for (int f = 0; f < a.nf; ++f) {
+    const at::Tensor &x = xs[f], &w = ws[f];
+    check_cuda(x, "featpool x");
+    check_cuda(w, "featpool w");
+    TORCH_CHECK(x.scalar_type() == at::kFloat && w.scalar_type() == at::kFloat && x.dim() == 2 &&
+                    w.dim() == 2 && x.size(0) == a.rows && w.size(0) == a.H &&
+                    x.size(1) == w.size(1) && x.size(1) % 4 == 0,
+                "featpool: fp32 x (rows, d) and w (H, d) with d % 4 == 0");
+    a.s[f].x = x.data_ptr<float>();
+    a.s[f].w = w.data_ptr<float>();
+    if (!bs.empty()) {
+      check_cuda(bs[f], "featpool b");
+      TORCH_CHECK(bs[f].scalar_type() == at::kFloat && bs[f].numel() == a.H, "featpool: bias (H)");
+      a.s[f].b = bs[f].data_ptr<float>();
+    }
+    a.s[f].d = (int)x.size(1);
+  }
+  featpool_layout(a);
+  return a;
+}
+
+at::Tensor featpool_forward(std::vector<at::Tensor> xs, std::vector<at::Tensor> ws,
+                            std::vector<at::Tensor> bs, double drop_p, at::Tensor rng) {
+  TORCH_CHECK(bs.size() == xs.size(), "featpool: one bias per modality");
+  FeatPoolArgs a = featpool_args(xs, ws, bs);
+  auto f32 = xs[0].options();
+  at::Tensor wsp = at::empty({(int64_t)a.fwd_blocks * 64 * 64}, f32);
+  at::Tensor out = at::empty({a.rows, (int64_t)a.nf * a.H}, f32);
+  launch_featpool_fwd(a, wsp.data_ptr<float>(), out.data_ptr<float>(), (float)drop_p,
+                      rng_ptr(rng), cur_stream());
+  return out;
+}
+
+// -> {dW_0 .. dW_{F-1}, db_0 .. db_{F-1}} given dL/d(out) and the forward's out
+std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
+                                          std::vector<at::Tensor> xs,
+                                          std::vector<at::Tensor> ws, double drop_p) {
+  FeatPoolArgs a = featpool_args(xs, ws, {});
+  check_cuda(dout, "featpool dout");
+  check_cuda(out, "featpool out");
+  TORCH_CHECK(dout.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat &&
+                  dout.numel() == (int64_t)a.rows * a.nf * a.H && out.numel() == dout.numel(),
+              "featpool: dout / out (rows, F*H) fp32");
+  std::vector<at::Tensor> res;
+  FeatPoolGrads g{};
+  for (int f = 0; f < a.nf; ++f) {
+    res.push_back(at::empty_like(ws[f]));
+    g.dw[f] = res.back().data_ptr<float>();
+  }
+  for (int f = 0; f < a.nf; ++f) {
+    res.push_back(at::empty({a.H}, ws[f].options()));
+    g.db[f] = res.back().data_ptr<float>();
+  }
+  launch_featpool_bwd(a, dout.data_ptr<float>(), out.data_ptr<float>(), (float)drop_p, g,
+                      cur_stream());
+  return res;
+}
+
 // On-GPU CIDEr-D scores of N hypotheses.
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
                        double log_ref_len, int64_t use_eos) {

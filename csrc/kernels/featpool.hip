@@ -1,0 +1,229 @@
+// P10 FeatPool, fused: per modality Linear -> ReLU -> Dropout, concatenated
+// (reference /root/reference/model.py:46-69), forward and weight backward.
+//
+// The reference (and the plain PyTorch path) runs, per modality, one small
+// GEMM (64 videos x 512 x d_f), a ReLU, a dropout and finally a concat -- ~15
+// latency-bound launches forward and as many backward, ~0.2 ms per SCST step
+// on MI355X.  Here:
+//   * forward: ONE launch of 64 x 64 output tiles for every modality at once,
+//     split over K (256-wide chunks) so ~240 workgroups fill the chip; fp32
+//     operands on the fp32 matrix cores (MFMA 32x32x2 f32: the module keeps
+//     the reference's fp32 precision -- bf16 operands would move ReLU
+//     decisions near zero and with them whole gradient terms); partial
+//     tiles go to a workspace and
+//     a second launch sums them, adds the bias, applies ReLU and the dropout
+//     mask (counter hash of (seed, row, column), like the decoder's dropout)
+//     and writes the concatenated (rows, F*H) output;
+//   * backward: ONE launch computes dW_f = dz^T x_f for every modality, with
+//     dz = dout * [out > 0] / (1 - p) formed while loading (ReLU and dropout
+//     backward from the saved output alone: out > 0 iff the unit was kept and
+//     its pre-activation was positive), and the bias gradient in the blocks
+//     of the first K tile.  The features need no gradient.
+#include "../common.h"
+#include "../launchers.h"
+
+namespace cst {
+
+constexpr int FP_T = 64;     // output tile (rows x units, or units x k)
+constexpr int FP_KS = 32;    // K step per LDS stage
+constexpr int FP_KCH = 256;  // forward split-K chunk
+constexpr int FP_LDA = FP_KS + 1;  // fp32 row stride in LDS (conflict-free column reads)
+constexpr int FEATPOOL_DROP_KEY = 0x46504C;  // dropout_keep "step" key of FeatPool
+
+// One 64x64 tile += A(64 x KS) B(64 x KS)^T from fp32 LDS tiles (row stride
+// FP_LDA): wave w owns the 32x32 quarter (w >> 1, w & 1); each MFMA takes
+// k = 2: lane l supplies row / column l % 32 at k = l / 32.
+__device__ __forceinline__ void fp_mfma_step(const float* As, const float* Bs, f32x16& acc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const float* ar = As + (wr * 32 + (lane & 31)) * FP_LDA + (lane >> 5);
+  const float* br = Bs + (wc * 32 + (lane & 31)) * FP_LDA + (lane >> 5);
+#pragma unroll
+  for (int s = 0; s < FP_KS / 2; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * s], br[2 * s], acc, 0, 0, 0);
+}
+
+// (row, col) of accumulator element r of lane `lane` in the 64x64 tile
+__device__ __forceinline__ int acc_row(int r, int lane, int wr) {
+  return wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+
+// ---- forward: partial tiles --------------------------------------------------
+// block -> (modality f, row tile, unit tile, K chunk); partial 64x64 tile to ws
+__global__ __launch_bounds__(256) void featpool_fwd_partial_kernel(FeatPoolArgs a, float* ws) {
+  __shared__ float As[2][FP_T * FP_LDA];
+  __shared__ float Bs[2][FP_T * FP_LDA];
+  int f = 0;
+  while (f + 1 < a.nf && (int)blockIdx.x >= a.s[f + 1].blk0) ++f;
+  const FeatPoolSeg& g = a.s[f];
+  int b = (int)blockIdx.x - g.blk0;
+  const int nkc = (g.d + FP_KCH - 1) / FP_KCH, nut = a.H / FP_T;
+  const int kc = b % nkc;
+  b /= nkc;
+  const int ut = b % nut, rt = b / nut;
+  const int r0 = rt * FP_T, u0 = ut * FP_T, k0 = kc * FP_KCH;
+  const int kend = min(g.d, k0 + FP_KCH);
+  const int tid = threadIdx.x;
+  // each thread stages 2 float4 of A and of B per K step: tile row tid/8 + 32 i,
+  // columns 4 (tid % 8)
+  float4 ra[2], rb[2];
+  auto load = [&](int k) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (tid >> 3) + 32 * i, kk = k + 4 * (tid & 7);
+      const bool kin = kk < kend;  // d % 4 == 0 (host check): a float4 is in or out
+      const int r = r0 + row;
+      ra[i] = (kin && r < a.rows) ? *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.d + kk)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[i] = kin ? *reinterpret_cast<const float4*>(g.w + (int64_t)(u0 + row) * g.d + kk)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (tid >> 3) + 32 * i, kk = 4 * (tid & 7);
+      float* pa = &As[buf][row * FP_LDA + kk];
+      float* pb = &Bs[buf][row * FP_LDA + kk];
+      pa[0] = ra[i].x, pa[1] = ra[i].y, pa[2] = ra[i].z, pa[3] = ra[i].w;
+      pb[0] = rb[i].x, pb[1] = rb[i].y, pb[2] = rb[i].z, pb[3] = rb[i].w;
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int nks = (kend - k0 + FP_KS - 1) / FP_KS;
+  load(k0);
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    stage(buf);
+    __syncthreads();
+    if (ks + 1 < nks) load(k0 + (ks + 1) * FP_KS);  // in flight under the MFMAs
+    fp_mfma_step(As[buf], Bs[buf], acc);
+  }
+  const int lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+  float* out = ws + (int64_t)blockIdx.x * FP_T * FP_T;
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    out[acc_row(r, lane, wr) * FP_T + wc * 32 + (lane & 31)] = acc[r];
+}
+
+// ---- forward: sum of the K chunks + bias + ReLU + dropout -> (rows, F*H) ------
+__global__ __launch_bounds__(256) void featpool_fwd_epilogue_kernel(FeatPoolArgs a, const float* ws,
+                                                                    float* out, float drop_p,
+                                                                    const uint32_t* rng) {
+  const int FH = a.nf * a.H;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)a.rows * FH) return;
+  const int r = (int)(i / FH), col = (int)(i % FH);
+  const int f = col / a.H, u = col % a.H;
+  const FeatPoolSeg& g = a.s[f];
+  const int nkc = (g.d + FP_KCH - 1) / FP_KCH, nut = a.H / FP_T;
+  const int rt = r / FP_T, ut = u / FP_T;
+  const int base = g.blk0 + (rt * nut + ut) * nkc;
+  float z = g.b[u];
+  for (int kc = 0; kc < nkc; ++kc)
+    z += ws[(int64_t)(base + kc) * FP_T * FP_T + (r % FP_T) * FP_T + (u % FP_T)];
+  float y = fmaxf(z, 0.f);
+  if (drop_p > 0.f) {
+    const bool keep = dropout_keep(rng_seed(rng, RNG_SLOT_DROPOUT), FEATPOOL_DROP_KEY, r, col, drop_p);
+    y = keep ? y * (1.f / (1.f - drop_p)) : 0.f;
+  }
+  out[i] = y;
+}
+
+// ---- backward: dW_f = dz^T x_f, db_f = sum_rows dz ----------------------------
+// block -> (modality f, unit tile, k tile); K = rows in steps of FP_KS
+__global__ __launch_bounds__(256) void featpool_bwd_kernel(FeatPoolArgs a, const float* dout,
+                                                           const float* outp, float inv_keep,
+                                                           FeatPoolGrads gr) {
+  __shared__ float As[FP_T * FP_LDA];  // dz^T: units x rows
+  __shared__ float Bs[FP_T * FP_LDA];  // x^T: k x rows
+  int f = 0;
+  while (f + 1 < a.nf && (int)blockIdx.x >= a.s[f + 1].bblk0) ++f;
+  const FeatPoolSeg& g = a.s[f];
+  int b = (int)blockIdx.x - g.bblk0;
+  const int nkt = (g.d + FP_T - 1) / FP_T;
+  const int kt = b % nkt, ut = b / nkt;
+  const int u0 = ut * FP_T, k0 = kt * FP_T, FH = a.nf * a.H;
+  const int tid = threadIdx.x;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float dbias = 0.f;  // kt == 0 blocks, thread tid < 64: unit u0 + tid
+  for (int rs = 0; rs < a.rows; rs += FP_KS) {
+    // 32 rows x 64 columns of dz and of x: 2 float4 of each per thread,
+    // written transposed (column-major = K-contiguous per unit / k)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = (tid >> 4) + 16 * i, c4 = 4 * (tid & 15), r = rs + rr;
+      float4 dz = make_float4(0.f, 0.f, 0.f, 0.f), xv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < a.rows) {
+        const int64_t o = (int64_t)r * FH + f * a.H + u0 + c4;
+        const float4 dy = *reinterpret_cast<const float4*>(dout + o);
+        const float4 y = *reinterpret_cast<const float4*>(outp + o);
+        dz = make_float4(y.x > 0.f ? dy.x * inv_keep : 0.f, y.y > 0.f ? dy.y * inv_keep : 0.f,
+                         y.z > 0.f ? dy.z * inv_keep : 0.f, y.w > 0.f ? dy.w * inv_keep : 0.f);
+        if (k0 + c4 < g.d) xv = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.d + k0 + c4);
+      }
+      As[(c4 + 0) * FP_LDA + rr] = dz.x;
+      As[(c4 + 1) * FP_LDA + rr] = dz.y;
+      As[(c4 + 2) * FP_LDA + rr] = dz.z;
+      As[(c4 + 3) * FP_LDA + rr] = dz.w;
+      Bs[(c4 + 0) * FP_LDA + rr] = xv.x;
+      Bs[(c4 + 1) * FP_LDA + rr] = xv.y;
+      Bs[(c4 + 2) * FP_LDA + rr] = xv.z;
+      Bs[(c4 + 3) * FP_LDA + rr] = xv.w;
+    }
+    __syncthreads();
+    fp_mfma_step(As, Bs, acc);
+    if (kt == 0 && tid < FP_T) {  // bias gradient in fp32 (L2-resident re-read)
+      for (int rr = 0; rr < FP_KS && rs + rr < a.rows; ++rr) {
+        const int64_t o = (int64_t)(rs + rr) * FH + f * a.H + u0 + tid;
+        dbias += outp[o] > 0.f ? dout[o] * inv_keep : 0.f;
+      }
+    }
+    __syncthreads();
+  }
+  const int lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+  float* dw = gr.dw[f];
+  const int k = k0 + wc * 32 + (lane & 31);
+  if (k < g.d) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dw[(int64_t)(u0 + acc_row(r, lane, wr)) * g.d + k] = acc[r];
+  }
+  if (kt == 0 && tid < FP_T) gr.db[f][u0 + tid] = dbias;
+}
+
+void featpool_layout(FeatPoolArgs& a) {
+  int blk = 0, bblk = 0;
+  const int nrt = (a.rows + FP_T - 1) / FP_T, nut = a.H / FP_T;
+  for (int f = 0; f < a.nf; ++f) {
+    a.s[f].blk0 = blk;
+    a.s[f].bblk0 = bblk;
+    blk += nrt * nut * ((a.s[f].d + FP_KCH - 1) / FP_KCH);
+    bblk += nut * ((a.s[f].d + FP_T - 1) / FP_T);
+  }
+  a.fwd_blocks = blk;
+  a.bwd_blocks = bblk;
+}
+
+void launch_featpool_fwd(const FeatPoolArgs& a, float* ws, float* out, float drop_p,
+                         const uint32_t* rng, hipStream_t stream) {
+  hipLaunchKernelGGL(featpool_fwd_partial_kernel, dim3(a.fwd_blocks), dim3(256), 0, stream, a, ws);
+  post_launch("featpool_fwd_partial_kernel", stream);
+  const int64_t n = (int64_t)a.rows * a.nf * a.H;
+  hipLaunchKernelGGL(featpool_fwd_epilogue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     stream, a, (const float*)ws, out, drop_p, rng);
+  post_launch("featpool_fwd_epilogue_kernel", stream);
+}
+
+void launch_featpool_bwd(const FeatPoolArgs& a, const float* dout, const float* out, float drop_p,
+                         const FeatPoolGrads& gr, hipStream_t stream) {
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  hipLaunchKernelGGL(featpool_bwd_kernel, dim3(a.bwd_blocks), dim3(256), 0, stream, a, dout, out,
+                     inv_keep, gr);
+  post_launch("featpool_bwd_kernel", stream);
+}
+
+}  // namespace cst

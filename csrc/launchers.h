@@ -126,6 +126,31 @@ void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, co
                     int write_dq, float* dpre_part, float* dwa_part, float* dba_part,
                     hipStream_t stream, int per_frame);
 
+// featpool.hip: FeatPool (per modality Linear -> ReLU -> Dropout, concat)
+constexpr int FEATPOOL_MAX_F = 8;
+struct FeatPoolSeg {
+  const float* x;  // (rows, d) features of modality f
+  const float* w;  // (H, d) weight
+  const float* b;  // (H) bias
+  int d;
+  int blk0, bblk0;  // first forward / backward workgroup of the modality
+};
+struct FeatPoolArgs {
+  FeatPoolSeg s[FEATPOOL_MAX_F];
+  int nf, rows, H;
+  int fwd_blocks, bwd_blocks;
+};
+struct FeatPoolGrads {
+  float* dw[FEATPOOL_MAX_F];
+  float* db[FEATPOOL_MAX_F];
+};
+void featpool_layout(FeatPoolArgs& a);  // fills blk0 / bblk0 / *_blocks
+// ws: fwd_blocks * 64 * 64 floats; out: (rows, nf * H)
+void launch_featpool_fwd(const FeatPoolArgs& a, float* ws, float* out, float drop_p,
+                         const uint32_t* rng, hipStream_t stream);
+void launch_featpool_bwd(const FeatPoolArgs& a, const float* dout, const float* out, float drop_p,
+                         const FeatPoolGrads& gr, hipStream_t stream);
+
 // embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows grouped by token; C <= 1024)
 void launch_token_rows_sum(const float* x, int C, const int* stok, const int* srow, int N,
                            float* out, hipStream_t stream);

@@ -447,12 +447,21 @@ class DecoderEngine:
         # a replayed graph advances the generator's offset)
         return torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev)
 
+    @staticmethod
+    def _encode(model, feats):
+        """FeatPool through the fused kernels (ops/featpool.py) when they
+        cover the configuration, else the PyTorch module."""
+        from ..ops.featpool import featpool, fused_ok
+        if fused_ok(model.feat_pool, feats):
+            return featpool(model.feat_pool, feats)
+        return model.encode(feats)
+
     def _initial_state(self, model, feats):
         """model_type 'standard': one cell step per video on the video vector
         from a zero state (plain autograd ops, so it captures in a HIP graph;
         W_hh does not enter it).  Returns (h0, c0) per video, c0 = h0 for
         GRU / RNN (the kernels' state buffer)."""
-        fc = model.encode(feats)  # (B, E), FeatPool dropout in train mode
+        fc = self._encode(model, feats)  # (B, E), FeatPool dropout in train mode
         a = F.linear(fc, model.core.rnn.weight_ih_l0)
         if self.cell == 0:  # LSTM i, f, g, o with c' = 0
             i, _, g, o = a.chunk(4, 1)
@@ -469,7 +478,7 @@ class DecoderEngine:
         if self.standard:  # no per-step video term
             B = feats[0].size(0)
             return model.logit.bias.new_zeros(B, 4 * self.H), B
-        fc = model.encode(feats)  # (B, F*H), FeatPool dropout in train mode
+        fc = self._encode(model, feats)  # (B, F*H), FeatPool dropout in train mode
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
         vg = F.linear(fc, w_iv)
         return self.pack_rows(vg, self.src_ie, 1), fc.size(0)
@@ -492,7 +501,7 @@ class DecoderEngine:
 
     def _manet_inputs(self, model, feats):
         """MANet as attention over the F modality blocks (module docstring)."""
-        x = model.encode(feats)  # (B, F*blk), FeatPool dropout in train mode
+        x = self._encode(model, feats)  # (B, F*blk), FeatPool dropout in train mode
         B, Fm = x.size(0), model.num_feats
         blk = x.size(1) // Fm
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
@@ -511,7 +520,7 @@ class DecoderEngine:
         parameters (W_q, w_a, b_a) as autograd inputs of the Function."""
         if self.manet:
             return self._manet_inputs(model, feats)
-        frames = model.encode(feats)  # (B, C, F*H), FeatPool dropout in train mode
+        frames = self._encode(model, feats)  # (B, C, F*H), FeatPool dropout in train mode
         ta = model.temporal_att
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
         gv = self.pack_rows(F.linear(frames, w_iv), self.src_ie, 2)

@@ -1,0 +1,60 @@
+"""Fused FeatPool (``csrc/kernels/featpool.hip``): every modality's
+``Linear -> ReLU -> Dropout`` and the concat in two launches forward and one
+backward, for the fused decoder engine (the PyTorch path keeps
+:class:`~cst_captioning_amd.models.modules.FeatPool`).
+
+Reference: ``/root/reference/model.py:46-69``.  Same function, parameters
+and fp32 precision (fp32 matrix cores); dropout masks come from a counter
+hash of (seed, row, column) drawn on the device (graph-safe),
+distribution-identical to ``nn.Dropout``.
+"""
+import torch
+
+from .. import _ext
+
+
+def fused_ok(pool, feats):
+    """The fused kernels cover this call (else use the PyTorch module)."""
+    if not feats or not feats[0].is_cuda or len(feats) > 8 or not _ext.host_available():
+        return False
+    lins = [m[0] for m in pool.feat_list]
+    ps = {m[2].p for m in pool.feat_list}
+    H = lins[0].out_features
+    return (len(ps) == 1 and H % 64 == 0 and all(l.out_features == H for l in lins)
+            and all(f.dtype == torch.float32 and f.size(-1) % 4 == 0 for f in feats)
+            and all(l.bias is not None for l in lins))
+
+
+class _FeatPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p, rng, nf, *args):
+        xs, ws, bs = args[:nf], args[nf:2 * nf], args[2 * nf:]
+        out = _ext.ops().featpool_forward(list(xs), [w.detach() for w in ws],
+                                          [b.detach() for b in bs], p, rng)
+        ctx.p, ctx.nf = p, nf
+        ctx.save_for_backward(out, *xs, *[w.detach() for w in ws])
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        out, *rest = ctx.saved_tensors
+        nf = ctx.nf
+        g = _ext.ops().featpool_backward(dout.contiguous(), out, list(rest[:nf]),
+                                         list(rest[nf:]), ctx.p)
+        return (None, None, None) + (None,) * nf + tuple(g[:nf]) + tuple(g[nf:])
+
+
+def featpool(pool, feats):
+    """``pool(feats)`` through the fused kernels: feats list of (N, C, d_f)
+    fp32 -> (N, F*H) for C == 1, else (N, C, F*H)."""
+    lins = [m[0] for m in pool.feat_list]
+    p = float(pool.feat_list[0][2].p) if pool.training else 0.0
+    dev = feats[0].device
+    rng = (torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev) if p > 0
+           else torch.zeros(2, dtype=torch.int32, device=dev))
+    xs = [f.reshape(-1, f.size(-1)).contiguous() for f in feats]
+    out = _FeatPoolFn.apply(p, rng, len(xs), *xs, *[l.weight for l in lins],
+                            *[l.bias for l in lins])
+    N, C = feats[0].shape[0], feats[0].shape[1]
+    out = out.view(N, C, -1)
+    return out.squeeze(1) if C == 1 else out

@@ -382,3 +382,56 @@ def test_forward_full_logprobs_and_gradient_match_torch():
             continue
         err = (p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)
         assert err < 0.06, (name, float(err))
+
+
+@pytest.mark.parametrize('rows', [64, 6, 520])
+def test_fused_featpool_matches_torch(rows):
+    """csrc/kernels/featpool.hip (all modalities' Linear -> ReLU -> Dropout
+    + concat, and the weight / bias backward) vs the PyTorch FeatPool in fp32:
+    the headline modality sizes (2048, 4096, 1024, 300), H = 512; rows that
+    are and are not multiples of the 64-row tile."""
+    from cst_captioning_amd.models.modules import FeatPool
+    from cst_captioning_amd.ops.featpool import featpool, fused_ok
+    torch.manual_seed(0)
+    dims = [2048, 4096, 1024, 300]
+    pool = FeatPool(dims, 512, 0.0).to(DEV).train()
+    feats = [torch.randn(rows, 1, d, device=DEV) for d in dims]
+    assert fused_ok(pool, feats)
+    ref_pool = copy.deepcopy(pool)
+    out = featpool(pool, feats)
+    ref = ref_pool(feats)
+    assert out.shape == ref.shape == (rows, 4 * 512)
+    # fp32 matrix cores: equal up to the summation order
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-5
+    assert ((out > 0) != (ref > 0)).float().mean().item() < 1e-4
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    # backward arithmetic vs fp32 on the fused forward's own ReLU mask (a
+    # flipped near-zero unit moves a whole g * x term between the two masks)
+    dz = g * (out.detach() > 0).float()
+    for f, m in enumerate(pool.feat_list):
+        x = feats[f].reshape(rows, -1)
+        dzf = dz[:, 512 * f:512 * (f + 1)]
+        ref_dw = dzf.t() @ x
+        err = ((m[0].weight.grad - ref_dw).norm() / ref_dw.norm()).item()
+        assert err < 1e-5, (f, err)
+        torch.testing.assert_close(m[0].bias.grad, dzf.sum(0), rtol=1e-4, atol=1e-4)
+    # dropout: about half the units kept, survivors scaled by 2, and the
+    # backward routes gradient exactly through the survivors
+    for m in pool.feat_list:
+        m[2].p = 0.5
+    pool.zero_grad()
+    outd = featpool(pool, feats)
+    kept = outd > 0
+    pos = out > 0
+    frac = (kept.float().sum() / pos.float().sum()).item()
+    assert 0.45 < frac < 0.55, frac
+    torch.testing.assert_close(outd[kept], 2 * out.detach()[kept], rtol=1e-5, atol=1e-5)
+    outd.sum().backward()
+    w0 = pool.feat_list[0][0]
+    x0 = feats[0].reshape(rows, -1)
+    dz = kept[:, :512].float() * 2.0
+    torch.testing.assert_close(w0.bias.grad, dz.sum(0), rtol=1e-4, atol=1e-4)
+    ref_dw = dz.t() @ x0
+    assert ((w0.weight.grad - ref_dw).norm() / ref_dw.norm()).item() < 1e-5
