@@ -39,7 +39,8 @@ at::Tensor featpool_forward(std::vector<at::Tensor> xs, std::vector<at::Tensor> 
                             std::vector<at::Tensor> bs, double drop_p, at::Tensor rng);
 std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
                                           std::vector<at::Tensor> xs,
-                                          std::vector<at::Tensor> ws, double drop_p);
+                                          std::vector<at::Tensor> ws, double drop_p,
+                                          std::vector<at::Tensor> outs);
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);

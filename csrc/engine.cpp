@@ -723,10 +723,13 @@ at::Tensor featpool_forward(std::vector<at::Tensor> xs, std::vector<at::Tensor> 
   return out;
 }
 
-// -> {dW_0 .. dW_{F-1}, db_0 .. db_{F-1}} given dL/d(out) and the forward's out
+// -> {dW_0 .. dW_{F-1}, db_0 .. db_{F-1}} given dL/d(out) and the forward's out;
+// written into `outs` (2F contiguous fp32 tensors, e.g. gradient-bucket
+// slots) when given
 std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
                                           std::vector<at::Tensor> xs,
-                                          std::vector<at::Tensor> ws, double drop_p) {
+                                          std::vector<at::Tensor> ws, double drop_p,
+                                          std::vector<at::Tensor> outs) {
   FeatPoolArgs a = featpool_args(xs, ws, {});
   check_cuda(dout, "featpool dout");
   check_cuda(out, "featpool out");
@@ -735,13 +738,23 @@ std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
               "featpool: dout / out (rows, F*H) fp32");
   std::vector<at::Tensor> res;
   FeatPoolGrads g{};
-  for (int f = 0; f < a.nf; ++f) {
-    res.push_back(at::empty_like(ws[f]));
-    g.dw[f] = res.back().data_ptr<float>();
+  if (!outs.empty()) {
+    TORCH_CHECK((int)outs.size() == 2 * a.nf, "featpool: outs = {dW_f} + {db_f}");
+    for (int f = 0; f < a.nf; ++f) {
+      TORCH_CHECK(outs[f].is_cuda() && outs[f].is_contiguous() &&
+                      outs[f].scalar_type() == at::kFloat && outs[f].numel() == ws[f].numel() &&
+                      outs[a.nf + f].is_cuda() && outs[a.nf + f].is_contiguous() &&
+                      outs[a.nf + f].scalar_type() == at::kFloat && outs[a.nf + f].numel() == a.H,
+                  "featpool: output slots must be contiguous fp32 (H, d) / (H)");
+    }
+    res = outs;
+  } else {
+    for (int f = 0; f < a.nf; ++f) res.push_back(at::empty_like(ws[f]));
+    for (int f = 0; f < a.nf; ++f) res.push_back(at::empty({a.H}, ws[f].options()));
   }
   for (int f = 0; f < a.nf; ++f) {
-    res.push_back(at::empty({a.H}, ws[f].options()));
-    g.db[f] = res.back().data_ptr<float>();
+    g.dw[f] = res[f].data_ptr<float>();
+    g.db[f] = res[a.nf + f].data_ptr<float>();
   }
   launch_featpool_bwd(a, dout.data_ptr<float>(), out.data_ptr<float>(), (float)drop_p, g,
                       cur_stream());

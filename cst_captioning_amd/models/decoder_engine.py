@@ -441,6 +441,18 @@ class DecoderEngine:
                                    '(zero_grad(set_to_none=True) or a replaced .grad?); use the '
                                    'trainer bucket\'s zero_grad()' % k)
         self.direct_armed = False
+        self._video_slots_ok = True
+
+    def take_video_slots(self):
+        """For the FeatPool / video-gate backward of the same pass (it runs
+        after the decoder's): the direct slots, once, if the decoder backward
+        verified them and the FeatPool parameters have slots too."""
+        ok = getattr(self, '_video_slots_ok', False)
+        self._video_slots_ok = False
+        d = self.direct_grad_slots
+        if not ok or d is None or 'fp_w0' not in d:
+            return None
+        return d
 
     def _rng(self, dev):
         # per-pass seeds {dropout, sampling} drawn ON the device (graph-safe:
@@ -478,6 +490,10 @@ class DecoderEngine:
         if self.standard:  # no per-step video term
             B = feats[0].size(0)
             return model.logit.bias.new_zeros(B, 4 * self.H), B
+        from ..ops.featpool import featpool_vgate, fused_ok
+        if fused_ok(model.feat_pool, feats) and feats[0].size(1) == 1:
+            vg = featpool_vgate(self, model, feats)  # one node: FeatPool + gate term
+            return vg, vg.size(0)
         fc = self._encode(model, feats)  # (B, F*H), FeatPool dropout in train mode
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
         vg = F.linear(fc, w_iv)

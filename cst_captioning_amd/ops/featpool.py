@@ -40,8 +40,63 @@ class _FeatPoolFn(torch.autograd.Function):
         out, *rest = ctx.saved_tensors
         nf = ctx.nf
         g = _ext.ops().featpool_backward(dout.contiguous(), out, list(rest[:nf]),
-                                         list(rest[nf:]), ctx.p)
+                                         list(rest[nf:]), ctx.p, [])
         return (None, None, None) + (None,) * nf + tuple(g[:nf]) + tuple(g[nf:])
+
+
+class _FeatPoolVgateFn(torch.autograd.Function):
+    """FeatPool + the video gate term of the fused engine in one node:
+    ``vg = pack(FeatPool(x) . W_ih[:, E:]^T)`` (packed gate slots, see
+    decoder_engine).  Backward: the FeatPool weight / bias gradients and the
+    video columns of ``W_ih``'s gradient are written straight into their
+    gradient-bucket slots when the trainer registered them (no autograd
+    zero-fill / accumulate passes), else returned."""
+
+    @staticmethod
+    def forward(ctx, eng, p, rng, nf, *args):
+        xs, ws, bs, w_ih = args[:nf], args[nf:2 * nf], args[2 * nf:3 * nf], args[3 * nf]
+        wsd = [w.detach() for w in ws]
+        fc = _ext.ops().featpool_forward(list(xs), wsd, [b.detach() for b in bs], p, rng)
+        w_iv = w_ih.detach()[:, eng.E:]
+        vg = eng.pack_rows(torch.mm(fc, w_iv.t()), eng.src_ie, 1)
+        ctx.eng, ctx.p, ctx.nf, ctx.wih_shape = eng, p, nf, w_ih.shape
+        ctx.save_for_backward(fc, *xs, *wsd)
+        return vg
+
+    @staticmethod
+    def backward(ctx, dvg):
+        eng, nf = ctx.eng, ctx.nf
+        fc, *rest = ctx.saved_tensors
+        xs, ws = list(rest[:nf]), list(rest[nf:])
+        E = eng.E
+        dvg_u = dvg.index_select(1, eng.dst_ie)  # (B, G*H), PyTorch gate order
+        w_iv = eng.model.core.rnn.weight_ih_l0.detach()[:, E:]
+        dfc = torch.mm(dvg_u, w_iv)
+        direct = eng.take_video_slots()
+        if direct is not None:  # the decoder backward wrote W_ih's token columns
+            torch.mm(dvg_u.t(), fc, out=direct['wih'][:, E:])
+            outs = [direct['fp_w%d' % f] for f in range(nf)] + \
+                   [direct['fp_b%d' % f] for f in range(nf)]
+            _ext.ops().featpool_backward(dfc, fc, xs, ws, ctx.p, outs)
+            return (None,) * (4 + 4 * nf)
+        d_wih = fc.new_zeros(ctx.wih_shape)
+        d_wih[:, E:] = dvg_u.t() @ fc
+        g = _ext.ops().featpool_backward(dfc, fc, xs, ws, ctx.p, [])
+        return (None,) * (4 + nf) + tuple(g[:nf]) + tuple(g[nf:]) + (d_wih,)
+
+
+def featpool_vgate(eng, model, feats):
+    """Packed video gate term (B, 4H) of the concat model through the fused
+    FeatPool (train-mode dropout as the module's)."""
+    pool = model.feat_pool
+    lins = [m[0] for m in pool.feat_list]
+    p = float(pool.feat_list[0][2].p) if pool.training else 0.0
+    dev = feats[0].device
+    rng = (torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev) if p > 0
+           else torch.zeros(2, dtype=torch.int32, device=dev))
+    xs = [f.reshape(-1, f.size(-1)).contiguous() for f in feats]
+    return _FeatPoolVgateFn.apply(eng, p, rng, len(xs), *xs, *[l.weight for l in lins],
+                                  *[l.bias for l in lins], model.core.rnn.weight_ih_l0)
 
 
 def featpool(pool, feats):

@@ -107,6 +107,9 @@ class Trainer:
             rnn = model.core.rnn
             named = {'wlog': model.logit.weight, 'blog': model.logit.bias,
                      'emb': model.embed.weight, 'wih': rnn.weight_ih_l0, 'whh': rnn.weight_hh_l0}
+            # FeatPool weights / biases: written by the fused FeatPool backward
+            for i, m in enumerate(model.feat_pool.feat_list):
+                named['fp_w%d' % i], named['fp_b%d' % i] = m[0].weight, m[0].bias
             engine.set_direct_slots(
                 {k: self.bucket.grad[slot[id(p)][0]:slot[id(p)][0] + slot[id(p)][1]].view_as(p)
                  for k, p in named.items()}, named)

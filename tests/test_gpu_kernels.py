@@ -335,7 +335,8 @@ def test_trainer_direct_gradient_slots_match_torch():
     eng = _engine(model, opt)
     opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
     tr = Trainer(opt, model, loader, None, DistContext(device=torch.device(DEV)), eng)
-    assert set(eng.direct_grad_slots) == {'wlog', 'blog', 'emb', 'wih', 'whh'}
+    assert set(eng.direct_grad_slots) == {'wlog', 'blog', 'emb', 'wih', 'whh',
+                                          'fp_w0', 'fp_b0', 'fp_w1', 'fp_b1'}
     model.train()
     ref_model.train()
     data = loader.get_batch()
