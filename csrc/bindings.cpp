@@ -35,6 +35,10 @@ double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, a
                           int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
 std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V);
+std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor sample,
+                                          at::Tensor greedy);
+at::Tensor scst_loss_backward(at::Tensor seq, at::Tensor reward, at::Tensor out,
+                              at::Tensor dloss);
 at::Tensor featpool_forward(std::vector<at::Tensor> xs, std::vector<at::Tensor> ws,
                             std::vector<at::Tensor> bs, double drop_p, at::Tensor rng);
 std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
@@ -120,5 +124,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vocab_select", &cst::vocab_select);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);
+  m.def("scst_loss_forward", &cst::scst_loss_forward);
+  m.def("scst_loss_backward", &cst::scst_loss_backward);
   m.def("featpool_backward", &cst::featpool_backward);
 }

@@ -70,6 +70,23 @@ static DeviceAux& device_aux(int dev_index) {
   return *it->second;
 }
 
+// Read-only zeros of at least n elements (initial decoder states): one
+// persistent buffer per (device, dtype), so a decode does not launch a fill
+// kernel per call.  Grown only outside graph capture; replaced buffers stay
+// alive (a captured graph may still read them).
+static at::Tensor zeros_view(const at::Device& dev, int64_t n, at::ScalarType dtype) {
+  static std::map<std::pair<int, int>, std::vector<at::Tensor>> bufs;
+  auto& v = bufs[std::make_pair((int)dev.index(), (int)dtype)];
+  if (v.empty() || v.back().numel() < n) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(cur_stream(), &cs);
+    auto opts = at::TensorOptions().dtype(dtype).device(dev);
+    if (cs != hipStreamCaptureStatusNone) return at::zeros({n}, opts);
+    v.push_back(at::zeros({std::max<int64_t>(n, 1 << 20)}, opts));
+  }
+  return v.back().narrow(0, 0, n);
+}
+
 // modes[t] = token-selection mode for token t+1 (see SelModeHost)
 std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tensor ptab,
                                         at::Tensor whh, at::Tensor wlog,
@@ -149,9 +166,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   auto i64 = at::TensorOptions().dtype(at::kLong).device(dev);
   hipStream_t st = cur_stream();
 
-  at::Tensor seq = at::zeros({R, T - 1}, i64);
-  at::Tensor g_sel = at::zeros({R, T - 1}, f32);
-  at::Tensor g_xe = want_xe ? at::zeros({R, T}, f32) : at::Tensor();
+  // (every entry is written by the combine of its step: no fill kernels)
+  at::Tensor seq = at::empty({R, T - 1}, i64);
+  at::Tensor g_sel = at::empty({R, T - 1}, f32);
+  at::Tensor g_xe = want_xe ? at::empty({R, T}, f32) : at::Tensor();
   at::Tensor lse = at::empty({n_steps, R}, f32);
   const int n_vt = vocab_num_tiles((int)V);
   at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4}, f32);
@@ -242,7 +260,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                     c0.size(0) == R && c0.size(1) == H,
                 "h0 bf16 / c0 fp32, contiguous (R, H)");
   } else {
-    h0 = at::zeros({R, H}, bf), c0 = at::zeros({R, H}, f32);
+    h0 = zeros_view(dev, R * H, at::kBFloat16).view({R, H});
+    c0 = zeros_view(dev, R * H, at::kFloat).view({R, H});
   }
   at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
   at::Tensor xin = NL > 1 ? at::empty({R, H4}, f32) : at::Tensor();
@@ -266,7 +285,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   if (has_att) {
     vg_rows = at::empty({R, H4}, f32);
     if (save) {
-      q_all = at::zeros({n_steps, R, A}, f32);
+      q_all = at::empty({n_steps, R, A}, f32);  // q_0 = 0 is never read
       alpha_all = at::empty({n_steps, R, C}, f32);
     } else {
       q_tmp = at::empty({R, A}, f32);
@@ -759,6 +778,39 @@ std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
   launch_featpool_bwd(a, dout.data_ptr<float>(), out.data_ptr<float>(), (float)drop_p, g,
                       cur_stream());
   return res;
+}
+
+// SCST loss (csrc/kernels/loss.hip): seq (R, T) int64, lp (R, T) fp32,
+// sample (R), greedy (R or R / gdiv) fp32 -> {loss (0-dim), out = [loss, m, b,
+// sum mask], reward (R)}
+std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor sample,
+                                          at::Tensor greedy) {
+  for (auto* t : {&seq, &lp, &sample, &greedy}) check_cuda(*t, "scst_loss operand");
+  const int64_t R = seq.size(0), T = seq.size(1);
+  TORCH_CHECK(seq.scalar_type() == at::kLong && lp.scalar_type() == at::kFloat &&
+                  lp.size(0) == R && lp.size(1) == T && sample.scalar_type() == at::kFloat &&
+                  sample.numel() == R && greedy.scalar_type() == at::kFloat &&
+                  greedy.numel() > 0 && R % greedy.numel() == 0,
+              "scst_loss: seq / lp (R, T), sample (R), greedy (R or R / rows per video)");
+  auto f32 = lp.options();
+  at::Tensor out = at::empty({4}, f32), reward = at::empty({R}, f32), loss = at::empty({}, f32);
+  launch_scst_loss_fwd(seq.data_ptr<int64_t>(), lp.data_ptr<float>(), (int)R, (int)T,
+                       sample.data_ptr<float>(), greedy.data_ptr<float>(),
+                       (int)(R / greedy.numel()), reward.data_ptr<float>(), out.data_ptr<float>(),
+                       loss.data_ptr<float>(), cur_stream());
+  return {loss, out, reward};
+}
+
+at::Tensor scst_loss_backward(at::Tensor seq, at::Tensor reward, at::Tensor out,
+                              at::Tensor dloss) {
+  for (auto* t : {&seq, &reward, &out, &dloss}) check_cuda(*t, "scst_loss operand");
+  TORCH_CHECK(dloss.scalar_type() == at::kFloat && dloss.numel() == 1, "dloss: fp32 scalar");
+  const int64_t R = seq.size(0), T = seq.size(1);
+  at::Tensor dlp = at::empty({R, T}, reward.options());
+  launch_scst_loss_bwd(seq.data_ptr<int64_t>(), reward.data_ptr<float>(), out.data_ptr<float>(),
+                       dloss.data_ptr<float>(), (int)R, (int)T, dlp.data_ptr<float>(),
+                       cur_stream());
+  return dlp;
 }
 
 // On-GPU CIDEr-D scores of N hypotheses.

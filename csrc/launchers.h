@@ -151,6 +151,14 @@ void launch_featpool_fwd(const FeatPoolArgs& a, float* ws, float* out, float dro
 void launch_featpool_bwd(const FeatPoolArgs& a, const float* dout, const float* out, float drop_p,
                          const FeatPoolGrads& gr, hipStream_t stream);
 
+// loss.hip: SCST reward + reward mask + REINFORCE loss (out = {loss, mean
+// sample, mean greedy, sum mask}), and its backward
+void launch_scst_loss_fwd(const int64_t* seq, const float* lp, int R, int T, const float* sample,
+                          const float* greedy, int gdiv, float* reward, float* out, float* loss,
+                          hipStream_t stream);
+void launch_scst_loss_bwd(const int64_t* seq, const float* reward, const float* out,
+                          const float* dloss, int R, int T, float* dlp, hipStream_t stream);
+
 // embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows grouped by token; C <= 1024)
 void launch_token_rows_sum(const float* x, int C, const int* stok, const int* srow, int N,
                            float* out, hipStream_t stream);

@@ -285,35 +285,76 @@ class CaptionLoader:
         idx = self._to_device(vids, rows) if rows is not None else self._to_device(vids)
         return Batch(self, vids, idx)
 
-    def gather(self, vid_t, rows_t=None):
+    def gather(self, vid_t, rows_t=None, keys=None):
         """Device part of a batch from its index tensors: features, labels,
         masks (``nonzeros + 1``, ``dataloader.py:158-163``) and consensus
-        scores -- gathers only, so it can run inside a captured HIP graph."""
+        scores -- gathers only, so it can run inside a captured HIP graph.
+        ``keys``: the subset to build (default: all)."""
         dev = self.ds.device_tensors(self.device)
-        out = {'feats': [f.index_select(0, vid_t) for f in dev['feats']]}
+        keys = set(keys) if keys is not None else {'feats', 'labels', 'masks', 'bcmrscores'}
+        out = {}
+        if 'feats' in keys:
+            out['feats'] = [f.index_select(0, vid_t) for f in dev['feats']]
         if rows_t is not None:
-            labels = dev['labels'].index_select(0, rows_t)
-            n = (labels != 0).sum(1, keepdim=True) + 1
-            pos = torch.arange(labels.shape[1], device=labels.device)[None, :]
-            out['labels'] = labels
-            out['masks'] = (pos < n).float()
-            out['bcmrscores'] = dev['bcmrscores'].index_select(0, vid_t) \
-                if 'bcmrscores' in dev else None
+            if keys & {'labels', 'masks'}:
+                labels = dev['labels'].index_select(0, rows_t)
+                out['labels'] = labels
+                if 'masks' in keys:
+                    n = (labels != 0).sum(1, keepdim=True) + 1
+                    pos = torch.arange(labels.shape[1], device=labels.device)[None, :]
+                    out['masks'] = (pos < n).float()
+            if 'bcmrscores' in keys:
+                out['bcmrscores'] = dev['bcmrscores'].index_select(0, vid_t) \
+                    if 'bcmrscores' in dev else None
         return out
 
 
-class Batch(dict):
-    """One batch: ``video_index`` / ``vids`` / ``ids`` / ``gts`` eagerly, the
-    device gathers (``feats``, ``labels``, ``masks``, ``bcmrscores``) on first
-    access.  ``index_tensors()`` exposes the gather indices, so the trainer's
-    HIP-graph step copies only them and gathers inside the graph."""
+class LazyGather(dict):
+    """The device part of a batch (``feats``, ``labels``, ``masks``,
+    ``bcmrscores``), each gathered on its first access: a step that never
+    reads the masks (SCST) never launches their kernels, also inside a
+    captured graph."""
 
     _DEVICE_KEYS = ('feats', 'labels', 'masks', 'bcmrscores')
 
-    def __init__(self, loader, vids, idx):
+    def __init__(self, loader, idx):
         super().__init__()
         self._loader = loader
         self._idx = idx  # [vid_t] or [vid_t, rows_t]
+        self._touched = False
+
+    def _materialise(self, k):
+        if not dict.__contains__(self, k):
+            self._touched = True
+            self.update(self._loader.gather(*self._idx, keys=[k]))
+            if not dict.__contains__(self, k):  # no labels in this split
+                dict.__setitem__(self, k, None)
+
+    def __getitem__(self, k):
+        if k in self._DEVICE_KEYS:
+            self._materialise(k)
+        return super().__getitem__(k)
+
+    def get(self, k, default=None):
+        if k in self._DEVICE_KEYS:
+            self._materialise(k)
+        return super().get(k, default)
+
+    def __contains__(self, k):
+        if k in self._DEVICE_KEYS:
+            self._materialise(k)
+            return super().get(k) is not None
+        return super().__contains__(k)
+
+
+class Batch(LazyGather):
+    """One batch: ``video_index`` / ``vids`` / ``ids`` / ``gts`` eagerly, the
+    device gathers on first access (:class:`LazyGather`).
+    ``index_tensors()`` exposes the gather indices, so the trainer's HIP-graph
+    step copies only them and gathers inside the graph."""
+
+    def __init__(self, loader, vids, idx):
+        super().__init__(loader, idx)
         self['video_index'] = idx[0]
         self['vids'] = vids
         self['ids'] = loader.ds.video_ids[vids].tolist()
@@ -321,28 +362,9 @@ class Batch(dict):
             self['gts'] = _LazyGts(loader.ds, vids)
 
     def index_tensors(self):
-        """The gather indices, or None once the device part was materialised
+        """The gather indices, or None once a device part was materialised
         (the caller may have modified it, so only an eager step is exact)."""
-        return None if 'feats' in self.keys() else list(self._idx)
-
-    def _materialise(self):
-        if 'feats' not in self.keys():
-            self.update(self._loader.gather(*self._idx))
-
-    def __getitem__(self, k):
-        if k in self._DEVICE_KEYS:
-            self._materialise()
-        return super().__getitem__(k)
-
-    def get(self, k, default=None):
-        if k in self._DEVICE_KEYS:
-            self._materialise()
-        return super().get(k, default)
-
-    def __contains__(self, k):
-        if k in self._DEVICE_KEYS:
-            self._materialise()
-        return super().__contains__(k)
+        return None if self._touched else list(self._idx)
 
 
 class _LazyGts:

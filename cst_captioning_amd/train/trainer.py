@@ -37,6 +37,7 @@ from ..parallel import FlatGradBucket
 from ..reward.rewards import cst_from_scores, scst_from_scores
 from ..utils import schedules
 from ..utils.text import decode_sequence, compute_avglogp
+from ..data.dataset import LazyGather
 from ..utils.timers import PhaseTimer
 from . import checkpoint as ckpt
 
@@ -151,15 +152,16 @@ class Trainer:
         pred, seq, lp = m(data['feats'], data['labels'])
         return seq, lp, pred
 
-    def _greedy_scores(self, data, scorer, S):
-        """SCST baseline scores, one per rewarded row (R,)."""
+    def _greedy_scores(self, data, scorer, S, per_video=False):
+        """SCST baseline scores, one per rewarded row (R,) (or, with
+        per_video and the deduplicated greedy decode, one per video)."""
         opt, m = self.opt, self.model
         vid = data['video_index']
         if opt.expand_feat == 1 and getattr(opt, 'dedupe_greedy', 1):
             with torch.no_grad():
                 g, _ = m.sample(data['feats'], {'sample_max': 1, 'expand_feat': 0})
             gs = scorer.score(g, vid)
-            return gs.repeat_interleave(S)
+            return gs if per_video else gs.repeat_interleave(S)
         with torch.no_grad():
             g, _ = m.sample(data['feats'], {'sample_max': 1, 'expand_feat': opt.expand_feat})
         gvid = vid.repeat_interleave(S) if opt.expand_feat == 1 else vid
@@ -187,11 +189,14 @@ class Trainer:
             main = torch.cuda.current_stream(self.device)
             inputs_ready = self._ev_inputs
             inputs_ready.record(main)
+        # fused engine: reward, mask and REINFORCE loss in one launch
+        # (ops/scst_loss.py), the greedy scores per video
+        fused = self.engine is not None and opt.use_cst == 0 and self.device.type == 'cuda'
         model_res, logprobs, _ = self._decode_rollout(data)
         if side is not None:
             side.wait_event(inputs_ready)
             with torch.cuda.stream(side):
-                greedy_scores = self._greedy_scores(data, scorer, S)
+                greedy_scores = self._greedy_scores(data, scorer, S, per_video=fused)
         self.timer.mark('rollout')
         if opt.use_cst == 0:
             sample_scores = scorer.score(model_res, vid_rows)
@@ -199,7 +204,13 @@ class Trainer:
                 main.wait_stream(side)
                 greedy_scores.record_stream(main)
             else:
-                greedy_scores = self._greedy_scores(data, scorer, S)
+                greedy_scores = self._greedy_scores(data, scorer, S, per_video=fused)
+            if fused:
+                from ..ops.scst_loss import scst_loss
+                loss, reward, m_score, b_score = scst_loss(model_res, logprobs, sample_scores,
+                                                           greedy_scores)
+                self.timer.mark('reward')
+                return loss, {'reward': reward, 'm': m_score, 'b': b_score, 'seq': model_res}
             reward, m_score, b_score = scst_from_scores(sample_scores.float(),
                                                         greedy_scores.float())
         else:
@@ -346,7 +357,8 @@ class Trainer:
         pool = torch.cuda.graph_pool_handle()
         g_a = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_a, pool=pool):
-            batch = loader.gather(*self._static_idx)  # the batch gather is captured too
+            # the batch gather is captured too, each part on first use
+            batch = LazyGather(loader, self._static_idx)
             batch['video_index'] = self._static_idx[0]
             extra, skip = self._forward_backward(batch, mixer_from, scb)
             if not self.ctx.enabled:

@@ -436,3 +436,32 @@ def test_fused_featpool_matches_torch(rows):
     torch.testing.assert_close(w0.bias.grad, dz.sum(0), rtol=1e-4, atol=1e-4)
     ref_dw = dz.t() @ x0
     assert ((w0.weight.grad - ref_dw).norm() / ref_dw.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize('per_video', [True, False])
+def test_fused_scst_loss_matches_torch(per_video):
+    """csrc/kernels/loss.hip vs scst_from_scores + RewardCriterion: loss,
+    reward, logged means and the gradient w.r.t. the sampled log-probs."""
+    from cst_captioning_amd.models import RewardCriterion
+    from cst_captioning_amd.ops.scst_loss import scst_loss
+    from cst_captioning_amd.reward.rewards import scst_from_scores
+    torch.manual_seed(0)
+    B, S, T = 64, 20, 28
+    R = B * S
+    seq = torch.randint(0, 50, (R, T), device=DEV)
+    seq[torch.rand(R, T, device=DEV) < 0.1] = 0  # EOS anywhere
+    lp = (-torch.rand(R, T, device=DEV) * 5).requires_grad_(True)
+    sample = torch.rand(R, device=DEV)
+    greedy_v = torch.rand(B, device=DEV)
+    greedy = greedy_v if per_video else greedy_v.repeat_interleave(S)
+    loss, reward, m, b = scst_loss(seq, lp, sample, greedy)
+    lp2 = lp.detach().clone().requires_grad_(True)
+    rref, mref, bref = scst_from_scores(sample, greedy_v.repeat_interleave(S))
+    ref = RewardCriterion()(seq, lp2, rref)
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(reward, rref, rtol=0, atol=0)
+    torch.testing.assert_close(m, mref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(b, bref, rtol=1e-6, atol=1e-6)
+    (3.0 * loss).backward()
+    (3.0 * ref).backward()
+    torch.testing.assert_close(lp.grad, lp2.grad, rtol=1e-5, atol=1e-8)
