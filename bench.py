@@ -66,6 +66,11 @@ def parse():
                         'default, and the headline config, is 1: mean-pooled features)')
     p.add_argument('--cuda_graph', type=int, default=1,
                    help='replay the training step as a captured HIP graph (fused engine)')
+    p.add_argument('--rnn_type', default='lstm', choices=['lstm', 'gru', 'rnn'],
+                   help='decoder cell (headline: lstm)')
+    p.add_argument('--model_type', default='concat', choices=['concat', 'standard', 'manet'],
+                   help="headline: concat; 'standard' uses input_encoding_size = F * 512")
+    p.add_argument('--num_layers', type=int, default=1)
     p.add_argument('--grad_wire', default='fp32', choices=['fp32', 'bf16'],
                    help='DP gradient reduction: fp32 all-reduce or bf16 wire / fp32 accumulation')
     p.add_argument('--json_out', default='')
@@ -125,8 +130,9 @@ def main():
     S = 20
     opt = default_opts(
         batch_size=a.batch_size, train_seq_per_img=S, test_seq_per_img=S, rnn_size=512,
-        input_encoding_size=512, drop_prob_lm=0.5, learning_rate=1e-4, grad_clip=0.25,
-        model_type='concat', num_chunks=a.num_chunks, eval_metric='CIDEr', max_epochs=10 ** 9, print_log_interval=0,
+        input_encoding_size=512 * len(ds.feat_dims) if a.model_type == 'standard' else 512,
+        drop_prob_lm=0.5, rnn_type=a.rnn_type, num_layers=a.num_layers, learning_rate=1e-4, grad_clip=0.25,
+        model_type=a.model_type, num_chunks=a.num_chunks, eval_metric='CIDEr', max_epochs=10 ** 9, print_log_interval=0,
         use_rl=1 if a.mode != 'xe' else 0, use_rl_after=0, use_cst=1 if a.mode == 'cst' else 0,
         use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=2, scb_captions=S,
         impl=a.impl, precision=a.precision, reward_device=a.reward,
@@ -212,8 +218,10 @@ def main():
         # bf16 under autocast with --precision bf16 on a GPU, else fp32
         'dtype': 'bf16' if (engine is not None or trainer.autocast_bf16) else 'fp32',
         'data': 'synthetic (MSR-VTT-shaped, random-init weights)',
-        'config': {'model': 'CaptionModel concat LSTM-512 (resnet+c3d+mfcc+category, '
-                            'V=%d, L=30)' % a.vocab,
+        'config': {'model': 'CaptionModel %s %s%s-512 (resnet+c3d+mfcc+category, '
+                            'V=%d, L=30)' % (a.model_type, a.rnn_type.upper(),
+                                             'x%d' % a.num_layers if a.num_layers > 1 else '',
+                                             a.vocab),
                    'global_batch': a.batch_size * (1 if a.mode == 'beam' else S) * ctx.world_size,
                    'videos_per_gpu': a.batch_size, 'seq_per_img': S, 'seq_len': 30,
                    'parallelism': 'dp%d' % ctx.world_size, 'impl': a.impl,

@@ -465,7 +465,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                     state0[1].scalar_type() == at::kFloat,
                 "state0 = {h0 bf16, c0 fp32} (R, H)");
   TORCH_CHECK(V <= 8 * 2048, "vocab larger than the dS kernel's register tiling");
-  TORCH_CHECK(E <= 1024, "embedding size must be <= 1024");
   const int64_t NR = n_steps * R;
   DeviceAux& aux = device_aux((int)dev.index());
   hipEvent_t ev_ready = aux.ev[0], ev_dhd = aux.ev[1], ev_done = aux.ev[2];

@@ -21,10 +21,10 @@
 
 namespace cst {
 
-constexpr int EG_ROWS = 64, EG_GROUP = 8, EG_MAXJ = 4;  // C <= 1024
+constexpr int EG_ROWS = 64, EG_GROUP = 8, EG_MAXJ = 4;  // <= 1024 columns per launch
 
 __global__ __launch_bounds__(256) void token_rows_sum_kernel(
-    const float* __restrict__ x, int C, const int* __restrict__ stok,
+    const float* __restrict__ x, int C, int ld, const int* __restrict__ stok,
     const int* __restrict__ srow, int N, float* __restrict__ out) {
   __shared__ int s_tok[EG_ROWS];
   __shared__ int s_row[EG_ROWS];
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void token_rows_sum_kernel(
 #pragma unroll
       for (int j = 0; j < EG_MAXJ; ++j)
         v[k][j] = (g + k < n && j < nj && tcol + 256 * j < C)
-                      ? x[(int64_t)s_row[g + k] * C + tcol + 256 * j]
+                      ? x[(int64_t)s_row[g + k] * ld + tcol + 256 * j]
                       : 0.f;
 #pragma unroll
     for (int k = 0; k < EG_GROUP; ++k) {
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void token_rows_sum_kernel(
 #pragma unroll
           for (int j = 0; j < EG_MAXJ; ++j)
             if (j < nj && tcol + 256 * j < C) {
-              atomicAdd(out + (int64_t)cur * C + tcol + 256 * j, acc[j]);
+              atomicAdd(out + (int64_t)cur * ld + tcol + 256 * j, acc[j]);
               acc[j] = 0.f;
             }
           cur = tk;
@@ -71,14 +71,18 @@ __global__ __launch_bounds__(256) void token_rows_sum_kernel(
   }
 #pragma unroll
   for (int j = 0; j < EG_MAXJ; ++j)
-    if (j < nj && tcol + 256 * j < C) atomicAdd(out + (int64_t)cur * C + tcol + 256 * j, acc[j]);
+    if (j < nj && tcol + 256 * j < C) atomicAdd(out + (int64_t)cur * ld + tcol + 256 * j, acc[j]);
 }
 
 void launch_token_rows_sum(const float* x, int C, const int* stok, const int* srow, int N,
                            float* out, hipStream_t stream) {
-  hipLaunchKernelGGL(token_rows_sum_kernel, dim3((N + EG_ROWS - 1) / EG_ROWS), dim3(256), 0,
-                     stream, x, C, stok, srow, N, out);
-  post_launch("token_rows_sum_kernel", stream);
+  // column chunks of <= 1024 (an embedding wider than that, e.g. the
+  // 'standard' model's E = F * H, takes several launches)
+  for (int c0 = 0; c0 < C; c0 += EG_MAXJ * 256) {
+    hipLaunchKernelGGL(token_rows_sum_kernel, dim3((N + EG_ROWS - 1) / EG_ROWS), dim3(256), 0,
+                       stream, x + c0, min(C - c0, EG_MAXJ * 256), C, stok, srow, N, out + c0);
+    post_launch("token_rows_sum_kernel", stream);
+  }
 }
 
 // ---- counting sort of the input tokens ----------------------------------------

@@ -94,7 +94,7 @@ def engine_supports(opt):
     layers = getattr(opt, 'num_layers', 1)
     ok = (getattr(opt, 'rnn_type', 'lstm') in CELLS and 1 <= layers <= MAX_LAYERS
           and getattr(opt, 'model_type', 'concat') in ('concat', 'standard', 'manet')
-          and opt.input_encoding_size % 64 == 0 and opt.input_encoding_size <= 1024
+          and opt.input_encoding_size % 64 == 0
           and opt.rnn_size % 64 == 0)
     C = getattr(opt, 'num_chunks', 1)
     if ok and layers > 1:

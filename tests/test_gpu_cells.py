@@ -229,3 +229,32 @@ def test_cell_graph_training_keeps_packed_shadows(variant):
     unused_hh = eng.src_hh == eng.gates * eng.H
     assert unused_ie.any() == unused_hh.any() == (cell != 'lstm')
     assert (eng.wx[unused_ie, :E] == 0).all() and (eng.wx[unused_hh, E:] == 0).all()
+
+
+def test_standard_with_embedding_wider_than_1024():
+    """'standard' feeds the F*H-wide video vector as the step -1 input, so its
+    embedding size is F*H: E = 1,152 here (the embedding-gradient row sums
+    run in 1,024-column chunks)."""
+    from cst_captioning_amd.models import CrossEntropyCriterion
+    ds, opt, model, eng, loader = _tiny('lstm', H=576, V=700, model_type='standard')
+    assert eng.E == 1152
+    model.train()
+    data = loader.get_batch()
+    labels = data['labels']
+    ref = copy.deepcopy(model)
+    ref.impl = 'torch'
+    model.set_seq_per_img(5)
+    ref.set_seq_per_img(5)
+    pred = ref(data['feats'], labels)[0]
+    n = pred.size(1)
+    ref_lp = pred.gather(2, labels[:, 1:1 + n].unsqueeze(2)).squeeze(2)
+    g_xe = eng.teacher_forced(model, data['feats'], labels)
+    m = data['masks'][:, 1:1 + n] > 0
+    assert (g_xe[:, :n] - ref_lp).abs()[m].max() < 0.08
+    crit = CrossEntropyCriterion()
+    crit(pred, labels[:, 1:], data['masks'][:, 1:]).backward()
+    crit(g_xe, labels[:, 1:], data['masks'][:, 1:]).backward()
+    errs = _grad_errs(model, ref)
+    assert 'embed.weight' in errs
+    bad = {k: v for k, v in errs.items() if v > _tol(k)}
+    assert not bad, errs
