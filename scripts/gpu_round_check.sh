@@ -13,3 +13,6 @@ rm -rf gpurun_out/prof_rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_rc -o rc -- python bench.py --steps 5 --warmup 2 > gpurun_out/prof_rc.log 2>&1 || exit $?
 python scripts/prof_summary.py gpurun_out/prof_rc/rc_kernel_trace.csv 7 40 > gpurun_out/prof_rc_summary.txt
 python scripts/step_timeline.py gpurun_out/prof_rc/rc_kernel_trace.csv 1 > gpurun_out/step_timeline_rc.txt
+rm -rf gpurun_out/prof_att8
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_att8 -o att8 -- python bench.py --steps 5 --warmup 2 --num_chunks 8 > gpurun_out/prof_att8.log 2>&1 || exit $?
+python scripts/prof_summary.py gpurun_out/prof_att8/att8_kernel_trace.csv 7 40 > gpurun_out/prof_att8_summary.txt
