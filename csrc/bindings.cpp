@@ -14,7 +14,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att,
                                         int64_t cell, std::vector<at::Tensor> state0,
-                                        std::vector<at::Tensor> up);
+                                        std::vector<at::Tensor> up, bool store_exp);
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -31,8 +31,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     int64_t K, int64_t T, int64_t bos_index,
                                     std::vector<at::Tensor> att, int64_t cell,
                                     std::vector<at::Tensor> state0, std::vector<at::Tensor> up);
-double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
-                          int64_t iters);
+double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
 std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V);
 std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor sample,
@@ -118,7 +117,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flat_adam_step", &cst::flat_adam_step);
   m.def("refresh_shadows", &cst::refresh_shadows);
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
-  m.def("vocab_bwd_ds_bench", &cst::vocab_bwd_ds_bench);
+  m.def("vgrad_colsum_bench", &cst::vgrad_colsum_bench);
   m.def("token_sort_bench", &cst::token_sort_bench);
   m.def("token_sort", &cst::token_sort);
   m.def("vocab_select", &cst::vocab_select);

@@ -11,11 +11,14 @@
 //
 // decoder_forward : teacher forcing / scheduled sampling / MIXER rollout /
 //                   greedy or multinomial sample(), optionally saving what the
-//                   backward needs (fp16 logits, dropped h, gates, c, [x;h]).
-// decoder_backward: batched vocab-head backward (dS in place, two
-//                   hipBLASLt GEMMs over all T*R rows at once), then the
-//                   reverse LSTM recurrence (cell kernel + one GEMM per step),
-//                   then the batched weight-gradient GEMMs.
+//                   backward needs (the exp store E = exp(logit - previous
+//                   LSE) in bf16, dropped h, gates, c, [x;h]).
+// decoder_backward: batched vocab-head backward without forming dS (two
+//                   hipBLASLt GEMMs over all T*R rows of E at once, row scales
+//                   and one-hot terms in kernels/vocab_grad.hip), then the
+//                   reverse LSTM recurrence (one fused kernel per step), then
+//                   the weight-gradient GEMMs (input-token ones over per-token
+//                   sums, V rows instead of T*R).
 #include <torch/extension.h>
 #include <array>
 #include <cstdlib>
@@ -97,7 +100,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att,
                                         int64_t cell, std::vector<at::Tensor> state0,
-                                        std::vector<at::Tensor> up) {
+                                        std::vector<at::Tensor> up, bool store_exp) {
   check_cuda(wx, "wx");
   TORCH_CHECK(cell >= 0 && cell <= 2, "cell: 0 lstm, 1 gru, 2 rnn (tanh)");  // CellType (common.h)
   check_cuda(emb, "emb");
@@ -178,8 +181,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor unfinished =
       use_unfinished ? at::ones({R}, at::TensorOptions().dtype(at::kByte).device(dev))
                      : at::Tensor();
-  // saved-logit rows padded to 128 bytes: the fused backward writes dS back
-  // in whole cache lines
+  // saved rows padded to 128 bytes (whole cache lines per row)
   const int64_t ldl = (V + 63) / 64 * 64;
   // Stacked layers (num_layers > 1): layer 0 is the fused pipeline below;
   // layer l >= 1 runs after it in every step: x_l = dropout(h_{l-1}) W_ih_l^T
@@ -207,8 +209,12 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor logits16;
   std::vector<at::Tensor> Hs(NL), Cs(NL), Gs(NL), HDs(NL);
   std::vector<std::array<at::Tensor, 2>> hpp(NL), cpp(NL);
+  // saved vocab rows: fp16 logits, or (store_exp) bf16 E = exp(x - lse of the
+  // previous step) for the dS-free backward (kernels/vocab_grad.hip)
   if (save)
-    logits16 = at::empty({n_steps, R, ldl}, at::TensorOptions().dtype(at::kHalf).device(dev));
+    logits16 = at::empty({n_steps, R, ldl}, at::TensorOptions()
+                                                .dtype(store_exp ? at::kBFloat16 : at::kHalf)
+                                                .device(dev));
   for (int64_t l = 0; l < NL; ++l) {
     if (save) {
       Hs[l] = at::empty({n_steps, R, H}, bf);
@@ -325,7 +331,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     const bool choose = t < T - 1;
     const int mode = choose ? (int)modes[t] : SEL_GT_H;
     const int do_sample = choose && (mode == SEL_SAMPLE_H || mode == SEL_SS_H);
-    const int vflags = do_sample | ((choose && mode == SEL_GREEDY_H) ? 2 : 0);
+    const bool exp_t = save && store_exp && t > 0;  // step 0: fp16, converted below
+    const int vflags = do_sample | ((choose && mode == SEL_GREEDY_H) ? 2 : 0) | (exp_t ? 16 : 0);
     const int64_t* tgt = (have_labels && t + 1 < L) ? LAB + (t + 1) : nullptr;
     // attention: the same launch also projects q_{t+1} = h_t W_q^T (extra
     // W_q tiles of the recurrent GEMM, no vgate add); the attention kernel then
@@ -337,7 +344,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                           part.data_ptr(), tgt, L, vflags, inv_temp, RNG, (int)t,
                           h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
                           next ? pre.data_ptr<float>() : nullptr, st, has_att ? (int)A : 0,
-                          has_att && next ? q_next.data_ptr<float>() : nullptr);
+                          has_att && next ? q_next.data_ptr<float>() : nullptr,
+                          exp_t ? lse[t - 1].data_ptr<float>() : nullptr);
     if (has_att && next)
       launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), q_next.data_ptr<float>(),
                      nullptr, a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv,
@@ -359,6 +367,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                          use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
                          use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st,
                          next ? &cl : nullptr);
+    if (save && store_exp && t == 0)
+      launch_vocab_exp_convert(reinterpret_cast<uint16_t*>(logits16[0].data_ptr()), ldl, (int)V,
+                               (int)R, lse[0].data_ptr<float>(), st);
     if (next)
       for (int64_t l = 1; l < NL; ++l) upper_step(l, t + 1);
   }
@@ -395,18 +406,18 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 // toks: (n_steps*R) input token of every (step, row), step-major.
 //
 // Schedule (streams):
-//   side 0 : dS = dG (onehot - softmax) in place of the fp16 logits (plus
-//            bias-gradient column partials), then dHd = dS W_logit (one BLAS
-//            GEMM over all T*R rows);
-//   main   : waits for dHd, runs the reverse LSTM loop (one fused kernel per
-//            step: recurrent GEMM + cell backward), then the token counting
-//            sort / embedding gather, the embedding-gradient GEMM + grouped
-//            row sums and the batched weight-gradient GEMMs;
-//   side 0 : dW_logit = dS^T Hd -- after the loop on one GPU (run concurrently
-//            the BLAS GEMM takes every CU and delays the loop's first step by
-//            ~370 us), concurrently with the loop under data parallelism so
-//            the vocab head's all-reduce (comm_stream waits on it) hides under
-//            the loop.
+//   side 0 : row weights alpha and the one-hot terms folded into E (dS =
+//            diag(alpha) E'), X = E' W_logit (one BLAS GEMM over all T*R
+//            rows), dHd = alpha X and the scaled rows alpha Hd in one pass;
+//   main   : the input-token counting sort (under the side stream's GEMM),
+//            then waits for dHd and runs the reverse LSTM loop (one fused
+//            kernel per step: recurrent GEMM + cell backward), then the
+//            per-token gate-gradient sums, the embedding / input-weight
+//            gradient GEMMs over them and the batched recurrent-weight GEMMs;
+//   side 0 : dW_logit = E'^T (alpha Hd) and the bias column sums -- after
+//            the loop on one GPU, concurrently with the loop under data
+//            parallelism so the vocab head's all-reduce (comm_stream waits
+//            on it) hides under the loop.
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -464,15 +475,28 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                     state0[0].scalar_type() == at::kBFloat16 && state0[1].size(0) == R &&
                     state0[1].scalar_type() == at::kFloat,
                 "state0 = {h0 bf16, c0 fp32} (R, H)");
-  TORCH_CHECK(V <= 8 * 2048, "vocab larger than the dS kernel's register tiling");
+  TORCH_CHECK(V < 65536, "vocab: token sort supports V < 65536");
   const int64_t NR = n_steps * R;
   DeviceAux& aux = device_aux((int)dev.index());
   hipEvent_t ev_ready = aux.ev[0], ev_dhd = aux.ev[1], ev_done = aux.ev[2];
   c10::hip::HIPStream side = aux.side[0];
 
-  // 1-2. vocab head on the side stream: dS in place, dHd = dS W
-  at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n_steps, (int)R), V}, f32);
-  at::Tensor dS = logits16.view(at::kBFloat16).view({NR, ldl}).narrow(1, 0, V);
+  // 1-2. vocab head on the side stream.  Exp store (training): X = E W, then
+  // one row pass turns X into dHd in place (row scale alpha + the one-hot
+  // rows of W) and writes alpha, the alpha-scaled Hd rows and the one-hot
+  // keys; kernels/vocab_grad.hip.  Dense dS given by the caller (full
+  // log-prob API, fp16-logits buffer rewritten as bf16 dS): dHd = dS W.
+  const bool ds_ready = ds_bias.defined() && ds_bias.numel() > 0;
+  if (ds_ready) {
+    TORCH_CHECK(ds_bias.is_cuda() && ds_bias.scalar_type() == at::kFloat && ds_bias.numel() == V,
+                "ds_bias must be fp32 (V)");
+  } else {
+    TORCH_CHECK(logits16.scalar_type() == at::kBFloat16,
+                "decoder_backward: the saved rows must be the exp store (forward store_exp) "
+                "unless a dense dS is given");
+  }
+  at::Tensor buf = logits16.scalar_type() == at::kBFloat16 ? logits16 : logits16.view(at::kBFloat16);
+  at::Tensor Ev = buf.view({NR, ldl}).narrow(1, 0, V);  // E (or dense dS), K = V columns
   at::Tensor hd2 = hdrop_all.view({NR, H});
   at::Tensor dHd = at::empty({NR, H}, f32);
   const bool early = out_wlog.defined() && out_wlog.numel() > 0;
@@ -484,66 +508,80 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   }
   at::Tensor dWlog = early ? out_wlog : at::empty({V, H}, f32);
   at::Tensor dblog = early ? out_blog.view({V}) : at::empty({V}, f32);
-  // ds_bias given: the caller already wrote a dense dS (bf16) into the logits
-  // buffer (full log-prob API) and passes the bias gradient (its column sums)
-  const bool ds_ready = ds_bias.defined() && ds_bias.numel() > 0;
-  if (ds_ready)
-    TORCH_CHECK(ds_bias.is_cuda() && ds_bias.scalar_type() == at::kFloat && ds_bias.numel() == V,
-                "ds_bias must be fp32 (V)");
+  at::Tensor alpha, hs, cs_part;
+  if (!ds_ready) {
+    alpha = at::empty({NR}, f32);
+    hs = at::empty({NR, H}, wx.options());
+    cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
+  }
+  auto launch_colsum = [&]() {
+    launch_vgrad_colsum(reinterpret_cast<const uint16_t*>(buf.data_ptr()), ldl, (int)V, NR,
+                        alpha.data_ptr<float>(), cs_part.data_ptr<float>(),
+                        dblog.data_ptr<float>(), side.stream());
+  };
+  // 3. dW_logit and the bias gradient: exp store: dW = E'^T (alpha Hd), db =
+  // sum_r alpha_r E'_r; dense dS: dW = dS^T Hd, db = ds_bias.  Neither needs
+  // the reverse loop.  One GPU: after the loop, concurrent with the input-token
+  // gradients (3.864-3.872 ms per step vs 3.961 before the loop, 3.889
+  // concurrent with it, 3.946 GEMM before / column sums during it;
+  // profiles/r2/ab_vh_sched.txt).  Data parallelism runs them concurrently
+  // with the loop, so the vocab head's all-reduce hides under it.
+  const bool early_comm = early && comm_stream != 0;
+  const int vh_sched = early_comm ? 2 : 0;
+  auto dw_gemm = [&]() {  // (current stream: side)
+    at::mm_out(dWlog, Ev.t(), ds_ready ? hd2 : hs, at::kFloat);
+  };
+  auto db_sums = [&]() {
+    if (ds_ready)
+      dblog.copy_(ds_bias);
+    else
+      launch_colsum();
+  };
+  auto dw_done = [&]() {
+    (void)hipEventRecord(ev_done, side.stream());
+    if (early_comm) (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
+  };
   (void)hipEventRecord(ev_ready, st);
   (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
   {
     c10::hip::HIPStreamGuard guard(side);
-    if (!ds_ready) launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V, (int)R,
-                        (int)n_steps, (int)T_sel, lse.data_ptr<float>(),
-                        has_sel ? seq.data_ptr<int64_t>() : nullptr, T_sel,
-                        has_sel ? dg_sel.data_ptr<float>() : nullptr, T_sel,
-                        has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
-                        has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                        has_xe ? dg_xe.size(1) : 0, colsum.data_ptr<float>(), 0, NR,
-                        side.stream());
-    at::mm_out(dHd, dS, wlog, at::kFloat);
+    if (!ds_ready) {  // alpha, one-hot terms folded into E (dS = diag(alpha) E')
+      VGradRows va{(int)R, (int)n_steps, (int)T_sel, (int)H, (int)V, lse.data_ptr<float>(),
+                   has_sel ? seq.data_ptr<int64_t>() : nullptr,
+                   has_sel ? dg_sel.data_ptr<float>() : nullptr,
+                   has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
+                   has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
+                   has_xe ? dg_xe.size(1) : 0};
+      launch_vgrad_onehot(va, reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl,
+                          alpha.data_ptr<float>(), side.stream());
+    }
+    at::mm_out(dHd, Ev, wlog, at::kFloat);
+    if (!ds_ready)
+      launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
+                        reinterpret_cast<const uint16_t*>(hd2.data_ptr()), dHd.data_ptr<float>(),
+                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
     (void)hipEventRecord(ev_dhd, side.stream());
+    if (vh_sched == 2) {
+      dw_gemm();
+      db_sums();
+      dw_done();
+    }
   }
-  // token-only operands of the embedding / input-weight gradients: rows grouped
-  // by input token (counting sort), the gathered input embeddings, the zeroed
-  // embedding-gradient slot
+  // token-only operands of the embedding / input-weight gradients: rows
+  // grouped by input token (counting sort), per-token sum scratch
   const bool emb_direct = out_emb.defined() && out_emb.numel() > 0;
   if (emb_direct)
     TORCH_CHECK(out_emb.is_contiguous() && out_emb.scalar_type() == at::kFloat &&
                     out_emb.size(0) == V && out_emb.size(1) == E,
                 "out_emb must be a contiguous fp32 (V, E) tensor");
   at::Tensor d_emb = emb_direct ? out_emb : at::empty({V, E}, f32);
-  at::Tensor sort_ws = at::empty({2 * V}, i32);
+  at::Tensor sort_ws = at::empty({2 * V + 1}, i32);
   at::Tensor stok = at::empty({NR}, i32), srow = at::empty({NR}, i32);
-  at::Tensor x_in = at::empty({NR, E}, emb.options());  // (n*R, E) bf16
-  auto token_prep = [&]() {
-    launch_token_sort(toks.data_ptr<int64_t>(), (int)NR, (int)V, sort_ws.data_ptr<int>(),
-                      stok.data_ptr<int>(), srow.data_ptr<int>(), st);
-    at::index_select_out(x_in, emb, 0, toks);
-    d_emb.zero_();
-  };
-  // on the main stream, under the side stream's dS pass (after the reverse
-  // loop its first launch queued behind the full-chip dW_logit GEMM: 4.56 vs
-  // 4.58 ms per step, 3 interleaved A/B rounds)
-  token_prep();
-
-  // 3. dW_logit = dS^T Hd and the bias gradient (column sums of dS), side stream
-  const bool dwlog_late = !early || comm_stream == 0;
-  auto launch_dwlog = [&]() {
-    // (on the main stream instead, serialised with the weight-gradient tail:
-    // 4.67 vs 4.58 ms per step)
-    c10::hip::HIPStreamGuard guard(side);
-    at::mm_out(dWlog, dS.t(), hd2, at::kFloat);
-    if (ds_ready)
-      dblog.copy_(ds_bias);
-    else
-      at::sum_out(dblog, colsum, {0});
-    (void)hipEventRecord(ev_done, side.stream());
-    if (early && comm_stream != 0)
-      (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
-  };
-  if (!dwlog_late) launch_dwlog();
+  at::Tensor S_tok = at::empty({V, H4}, wx.options());  // per-token gate-gradient sums
+  at::Tensor S32 = at::zeros({V, H4}, f32), s_flag = at::zeros({V}, i32);
+  // on the main stream, under the side stream's vocab-head GEMM
+  launch_token_sort(toks.data_ptr<int64_t>(), (int)NR, (int)V, sort_ws.data_ptr<int>(),
+                    stok.data_ptr<int>(), srow.data_ptr<int>(), st);
 
   // 4. reverse LSTM loop on the main stream
   at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
@@ -608,22 +646,26 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
                      dba_part.data_ptr<float>(), st, per_frame);
   }
-  if (dwlog_late) {
+  if (vh_sched == 0) {
     (void)hipEventRecord(ev_ready, st);  // reverse loop done
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
-    launch_dwlog();
+    c10::hip::HIPStreamGuard guard(side);
+    dw_gemm();
+    db_sums();
+    dw_done();
   }
 
-  // 5. embedding gradient: rows grouped by input token (counting sort), dX =
-  //    dG W_ie, grouped row sums into d_emb; input-weight gradient from the
-  //    gathered input embeddings
+  // 5. input-token gradients through the per-token sums S[v] = sum of the dG
+  //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
+  //    input-weight gradient S^T emb -- GEMMs over V rows instead of n*R
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
   at::Tensor dG2 = dGx.narrow(1, 0, H4);
-  {
-    at::Tensor dX = at::mm(dG2, wx.narrow(1, 0, E), at::kFloat);  // (n*R, E)
-    launch_token_rows_sum(dX.data_ptr<float>(), (int)E, stok.data_ptr<int>(),
-                          srow.data_ptr<int>(), (int)NR, d_emb.data_ptr<float>(), st);
-  }
+  launch_token_group_sum(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)H4, KD,
+                         stok.data_ptr<int>(), srow.data_ptr<int>(), (int)NR,
+                         sort_ws.data_ptr<int>(), (int)V,
+                         reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(),
+                         s_flag.data_ptr<int>(), st);
+  at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   // 6. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
   //    reductions run as batched GEMMs over groups of steps (many more output
   //    tiles in flight than one K = 35k GEMM), summed afterwards.
@@ -638,7 +680,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     at::Tensor b = b_rows.reshape({nc, G * R, b_rows.size(1)});
     return at::bmm(a, b, at::kFloat).sum(0);
   };
-  dWx.narrow(1, 0, E).copy_(grouped_wgrad(dG2, x_in, n_steps));
+  dWx.narrow(1, 0, E).copy_(at::mm(S_tok.t(), emb, at::kFloat));
   if (n_steps > 1) {
     // with attention the extra rows of [dG | dq]^T h_prev are dW_q
     at::Tensor wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
@@ -1073,20 +1115,18 @@ double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tens
       iters, st);
 }
 
-double vocab_bwd_ds_bench(at::Tensor logits16, at::Tensor lse, at::Tensor seq, at::Tensor dg_sel,
-                          int64_t iters) {
-  const int64_t n = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
-  const int64_t V = ldl;  // benchmark over the padded width
-  const int64_t T_sel = seq.size(1);
-  auto f32 = at::TensorOptions().dtype(at::kFloat).device(logits16.device());
-  at::Tensor colsum = at::empty({vocab_bwd_ds_blocks((int)n, (int)R), V}, f32);
+// bias-gradient column sums over the exp store: E (n, R, ldl) bf16, alpha (n*R)
+double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t iters) {
+  check_cuda(E, "E");
+  const int64_t NR = E.size(0) * E.size(1), ldl = E.size(2);
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(E.device());
+  at::Tensor part = at::empty({vgrad_colsum_blocks(NR), V}, f32), db = at::empty({V}, f32);
   hipStream_t st = cur_stream();
   return time_launches(
       [&](int) {
-        launch_vocab_bwd_ds(reinterpret_cast<uint16_t*>(logits16.data_ptr()), ldl, (int)V,
-                            (int)R, (int)n, (int)T_sel, lse.data_ptr<float>(),
-                            seq.data_ptr<int64_t>(), T_sel, dg_sel.data_ptr<float>(), T_sel,
-                            nullptr, 0, nullptr, 0, colsum.data_ptr<float>(), 0, n * R, st);
+        launch_vgrad_colsum(reinterpret_cast<const uint16_t*>(E.data_ptr()), ldl, (int)V, NR,
+                            alpha.data_ptr<float>(), part.data_ptr<float>(), db.data_ptr<float>(),
+                            st);
       },
       iters, st);
 }
@@ -1096,7 +1136,7 @@ double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters) {
   check_cuda(toks, "toks");
   const int64_t N = toks.numel();
   auto i32 = at::TensorOptions().dtype(at::kInt).device(toks.device());
-  at::Tensor ws = at::empty({2 * V}, i32), stok = at::empty({N}, i32), srow = at::empty({N}, i32);
+  at::Tensor ws = at::empty({2 * V + 1}, i32), stok = at::empty({N}, i32), srow = at::empty({N}, i32);
   hipStream_t st = cur_stream();
   return time_launches(
       [&](int) {
@@ -1142,7 +1182,7 @@ std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V) {
   TORCH_CHECK(toks.scalar_type() == at::kLong, "int64 token ids");
   const int64_t N = toks.numel();
   auto i32 = at::TensorOptions().dtype(at::kInt).device(toks.device());
-  at::Tensor ws = at::empty({2 * V}, i32), stok = at::empty({N}, i32), srow = at::empty({N}, i32);
+  at::Tensor ws = at::empty({2 * V + 1}, i32), stok = at::empty({N}, i32), srow = at::empty({N}, i32);
   launch_token_sort(toks.data_ptr<int64_t>(), (int)N, (int)V, ws.data_ptr<int>(),
                     stok.data_ptr<int>(), srow.data_ptr<int>(), cur_stream());
   return {stok, srow};

@@ -29,10 +29,9 @@
 //     reference's end-of-sequence rules (forward(): "all rows emitted EOS ->
 //     stop" through a device-side counter; sample(): per-row unfinished
 //     mask) without any host synchronisation.
-// vocab_bwd_ds_kernel
-//   * dlogits = dG_sel (onehot(y_sel) - p) + dG_xe (onehot(y_xe) - p),
-//     p = exp(x - lse), written as bf16 in place of the fp16 logits; the two
-//     plain GEMMs dH = dS W and dW = dS^T H then run on hipBLASLt.
+// vocab_exp_convert_kernel
+//   * step 0 of the exp store (see VF_EXP): fp16 logits -> bf16
+//     exp(x - lse) in place; the backward (vocab_grad.hip) never forms dS.
 #include "gemm_tile.h"
 #include "lstm_gemm.h"
 #include "../launchers.h"
@@ -76,7 +75,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // tiles in vocab_combine_kernel, and the union of independent races is the
 // race over all of V.
 constexpr int VT_V = 128;  // vocab entries per block
-enum VocabFlags : int { VF_SAMPLE = 1, VF_ARGMAX = 2, VF_BENCH_MAINLOOP = 4, VF_SAVE_F32 = 8 };
+// VF_EXP: the saved copy is E = exp(x - eoff[r]) in bf16 instead of fp16 x
+// (eoff = the row's LSE of the previous decode step), see vocab_grad.hip
+enum VocabFlags : int {
+  VF_SAMPLE = 1,
+  VF_ARGMAX = 2,
+  VF_BENCH_MAINLOOP = 4,
+  VF_SAVE_F32 = 8,
+  VF_EXP = 16
+};
 
 struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS
   float m, s, zkey, zlogit;
@@ -88,9 +95,10 @@ struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS
   const uint16_t *__restrict__ hd, int ldh, int R, int H, const uint16_t *__restrict__ W,    \
       const float *__restrict__ bias, int V, uint16_t *__restrict__ logits16, int64_t ldl,   \
       VocabPartial *__restrict__ part, const int64_t *__restrict__ tgt, int64_t tgt_stride, \
-      int flags, float inv_temp, const uint32_t *__restrict__ rng, int step
+      int flags, float inv_temp, const uint32_t *__restrict__ rng, int step,                 \
+      const float *__restrict__ eoff
 #define VOCAB_TR_ARGS \
-  hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, rng, step
+  hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, rng, step, eoff
 
 template <int BN, int STAGES>
 __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARAMS) {
@@ -124,10 +132,12 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       }
     }
   int tg[TN];
+  float ec[TN];  // exp-store offsets of the lane's rows
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int r = min(r0 + wc * TL::WN + 32 * j + (lane & 31), R - 1);
     tg[j] = tgt != nullptr ? (int)tgt[(int64_t)r * tgt_stride] : -1;
+    ec[j] = eoff != nullptr ? eoff[r] : 0.f;
   }
 
   f32x16 acc[TM][TN];
@@ -187,7 +197,7 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
               if (v + e < V) dst[v + e] = x[i][4 * q + e];
           }
         }
-    } else if (logits16 != nullptr && r < R) {
+    } else if (logits16 != nullptr && r < R && !(flags & VF_EXP)) {
       uint16_t* dst = logits16 + (int64_t)r * ldl;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -225,6 +235,31 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
         ew[i][k] = __builtin_amdgcn_exp2f(fmaf(x[i][k], L2E, -ml));
         s += ew[i][k];
       }
+    if ((flags & VF_EXP) && logits16 != nullptr && r < R) {
+      // E = exp(x - c) = exp(x - m) * exp(m - c): one multiply per entry on
+      // the weights already in registers (bf16: fp32's exponent range, so no
+      // overflow unless the row's max logit exceeds the previous step's LSE by
+      // ~88; that would surface as a non-finite gradient, which the optimizer's
+      // NaN guard skips)
+      const float f = __builtin_amdgcn_exp2f((msafe - ec[j]) * L2E);
+      uint16_t* dst = logits16 + (int64_t)r * ldl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int v = vb + 32 * i + 8 * q;
+          if (v + 4 <= V) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(ew[i][4 * q] * f) | ((uint32_t)f2bf(ew[i][4 * q + 1] * f) << 16);
+            pk.y = (uint32_t)f2bf(ew[i][4 * q + 2] * f) | ((uint32_t)f2bf(ew[i][4 * q + 3] * f) << 16);
+            *reinterpret_cast<uint2*>(dst + v) = pk;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (v + e < V) dst[v + e] = f2bf(ew[i][4 * q + e] * f);
+          }
+        }
+    }
 
     GroupStat st;
     st.m = m;
@@ -579,103 +614,29 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   }
 }
 
-// DS_ROWS rows of the [T*R][ldl] buffer per block; the 8-column chunks of a
-// row are split over gridDim.y blocks (column split), so the grid has enough
-// blocks to keep HBM busy (560 row blocks alone left the CUs at ~2 waves
-// each) without adding bias-gradient partial rows.  Each thread owns the same
-// chunks in every row, so the bias gradient (column sums of dS) is
-// accumulated in registers and written once per block.  The per-row scalars
-// are staged in LDS up front; NCH = chunks per thread is a compile-time
-// constant.
-constexpr int DS_ROWS = 64, DS_MAXCH = 8;  // V <= DS_MAXCH * 2048
-
-template <int NCH>
-__global__ __launch_bounds__(256) void vocab_bwd_ds_kernel(
-    uint16_t* __restrict__ buf, int64_t ldl, int V, int R, int T, int T_sel,
-    const float* __restrict__ lse, const int64_t* __restrict__ y_sel, int64_t ysel_rs,
-    const float* __restrict__ dg_sel, int64_t dgsel_rs, const int64_t* __restrict__ y_xe,
-    int64_t yxe_rs, const float* __restrict__ dg_xe, int64_t dgxe_rs,
-    float* __restrict__ colsum_part, int64_t row_begin, int64_t row_end) {
-  const int64_t row0 = row_begin + (int64_t)blockIdx.x * DS_ROWS;
-  const int64_t blk = row0 / DS_ROWS;  // global block index (row_begin % DS_ROWS == 0)
+// Exp-store conversion of one decode step's saved fp16 logits, in place:
+// E = bf16(exp(x - lse_r)).  Used for step 0 only, whose rows have no
+// previous-step LSE to offset by in the decode kernel (steps >= 1 write E
+// directly, VF_EXP).  One block per row, 8 entries (16 bytes) per thread and
+// iteration; the ragged tail (V % 8) scalar.
+__global__ __launch_bounds__(256) void vocab_exp_convert_kernel(uint16_t* __restrict__ buf,
+                                                                int64_t ldl, int V,
+                                                                const float* __restrict__ lse) {
+  const int r = blockIdx.x;
+  uint16_t* row = buf + (int64_t)r * ldl;
+  const float L = lse[r];
   const int nvec = V >> 3;
-  // this block's chunk range [c_lo, c_hi) of the row
-  const int per = (nvec + gridDim.y - 1) / gridDim.y;
-  const int c_lo = blockIdx.y * per, c_hi = min(nvec, c_lo + per);
-  const bool tail_blk = blockIdx.y == gridDim.y - 1;
-  const int nr = (int)min((int64_t)DS_ROWS, row_end - row0);
-  __shared__ float s_a[DS_ROWS], s_b[DS_ROWS], s_L[DS_ROWS];
-  __shared__ int s_ys[DS_ROWS], s_yx[DS_ROWS];
-  if ((int)threadIdx.x < nr) {
-    const int64_t rowid = row0 + threadIdx.x;
-    const int t = (int)(rowid / R), r = (int)(rowid % R);
-    const bool has_sel = dg_sel != nullptr && t < T_sel;
-    s_a[threadIdx.x] = has_sel ? dg_sel[(int64_t)r * dgsel_rs + t] : 0.f;
-    s_b[threadIdx.x] = dg_xe ? dg_xe[(int64_t)r * dgxe_rs + t] : 0.f;
-    s_ys[threadIdx.x] = has_sel ? (int)y_sel[(int64_t)r * ysel_rs + t] : -1;
-    s_yx[threadIdx.x] = dg_xe ? (int)y_xe[(int64_t)r * yxe_rs + t] : -1;
-    s_L[threadIdx.x] = lse[rowid];
+  for (int i = threadIdx.x; i < nvec; i += 256) {
+    uint4 x = *reinterpret_cast<const uint4*>(row + 8 * i);
+    uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = (uint32_t)f2bf(__expf(h2f(w[k] & 0xffff) - L)) |
+             ((uint32_t)f2bf(__expf(h2f(w[k] >> 16) - L)) << 16);
+    *reinterpret_cast<uint4*>(row + 8 * i) = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  __syncthreads();
-  float cs[NCH][8];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cs[c][k] = 0.f;
-  for (int rr = 0; rr < nr; ++rr) {
-    const int64_t rowid = row0 + rr;
-    const float a = s_a[rr], bb = s_b[rr], L = s_L[rr];
-    const int ys = s_ys[rr], yx = s_yx[rr];
-    const float ab = a + bb;
-    uint16_t* row = buf + rowid * ldl;
-    uint4 xv[NCH];
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {  // the row's loads in flight together
-      const int i = c_lo + threadIdx.x + c * 256;
-      if (i < c_hi) xv[c] = *reinterpret_cast<const uint4*>(row + i * 8);
-    }
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int i = c_lo + threadIdx.x + c * 256;
-      if (i < c_hi) {
-        uint32_t ws[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int v = i * 8 + 2 * k;
-          float lo = -ab * __expf(h2f(ws[k] & 0xffff) - L);
-          float hi = -ab * __expf(h2f(ws[k] >> 16) - L);
-          lo += (v == ys ? a : 0.f) + (v == yx ? bb : 0.f);
-          hi += (v + 1 == ys ? a : 0.f) + (v + 1 == yx ? bb : 0.f);
-          const uint16_t blo = f2bf(lo), bhi = f2bf(hi);
-          cs[c][2 * k] += bf2f(blo);  // sum what the GEMMs see (bf16 dS)
-          cs[c][2 * k + 1] += bf2f(bhi);
-          ws[k] = (uint32_t)blo | ((uint32_t)bhi << 16);
-        }
-        *reinterpret_cast<uint4*>(row + i * 8) = make_uint4(ws[0], ws[1], ws[2], ws[3]);
-      }
-    }
-    if (tail_blk && threadIdx.x < (V & 7)) {  // ragged tail columns
-      const int v = (nvec << 3) + threadIdx.x;
-      const float d = -ab * __expf(h2f(row[v]) - L) + (v == ys ? a : 0.f) + (v == yx ? bb : 0.f);
-      row[v] = f2bf(d);  // column sum added after the row loop
-    }
-  }
-  float* out = colsum_part + blk * V;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int i = c_lo + threadIdx.x + c * 256;
-    if (i < c_hi) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) out[i * 8 + k] = cs[c][k];  // row stride V: unaligned
-    }
-  }
-  // tail columns: re-sum from the (already converted) buffer
-  if (tail_blk && threadIdx.x < (V & 7)) {
-    const int v = (nvec << 3) + threadIdx.x;
-    float acc = 0.f;
-    for (int rr = 0; rr < nr; ++rr) acc += bf2f(buf[(row0 + rr) * ldl + v]);
-    out[v] = acc;
-  }
+  const int v = 8 * nvec + (int)threadIdx.x;
+  if (v < V) row[v] = f2bf(__expf(h2f(row[v]) - L));
 }
 
 // -------------------------------------------------------------------------------
@@ -686,7 +647,7 @@ static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
                                 float inv_temp, const uint32_t* rng, int step,
-                                hipStream_t stream) {
+                                hipStream_t stream, const float* eoff = nullptr) {
   using TL = Tile<VT_V, BN, STAGES>;
   constexpr int LDS = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
                           ? TL::STAGES * TL::STAGE_BYTES
@@ -700,18 +661,18 @@ static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const
   }
   hipLaunchKernelGGL((vocab_fwd_tr_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256), LDS,
                      stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt,
-                     tgt_stride, flags, inv_temp, rng, step);
+                     tgt_stride, flags, inv_temp, rng, step, eoff);
   post_launch("vocab_fwd_tr_kernel", stream);
 }
 
 void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                       const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                       const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
-                      const uint32_t* rng, int step, hipStream_t stream) {
+                      const uint32_t* rng, int step, hipStream_t stream, const float* eoff) {
   // (microbenchmark at V = 10,509: 31.0 vs 33.5 us at R = 1280, 8.7 vs 12.4
   // us at R = 64 against 128-row tiles, 2 blocks per CU)
   launch_vocab_fwd_tr<64, 2, 3>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
-                                flags, inv_temp, rng, step, stream);
+                                flags, inv_temp, rng, step, stream, eoff);
 }
 
 // microbenchmark only (scripts/microbench_kernels.py): other tile / pipeline
@@ -763,7 +724,7 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
                                 float inv_temp, const uint32_t* rng, int step, const uint16_t* h_t,
                                 const uint16_t* whh, const float* vgate, int vdiv, float* pre,
-                                int NQ, float* q_out, hipStream_t stream) {
+                                int NQ, float* q_out, hipStream_t stream, const float* eoff) {
   using TL = Tile<VT_V, BN, STAGES>;
   constexpr int LV = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
                          ? TL::STAGES * TL::STAGE_BYTES
@@ -779,7 +740,7 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   }
   hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT>), dim3(n_l + n_vt * n_rt), dim3(256),
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
-                     tgt, tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate, vdiv, pre, n_l,
+                     tgt, tgt_stride, flags, inv_temp, rng, step, eoff, h_t, whh, vgate, vdiv, pre, n_l,
                      NQ, q_out);
   post_launch("vocab_lstm_fwd_kernel", stream);
 }
@@ -789,47 +750,20 @@ void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
-                           float* q_out) {
+                           float* q_out, const float* eoff) {
   // 64-row tiles, 3 blocks per CU (48 KB of LDS each; the recurrent tiles use
   // 2 stages to fit): one block's epilogue overlaps the others' main loops.
   // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
   // CU (3 interleaved rounds; profiles/r2/ab_vocab_tiles.txt)
   launch_vocab_lstm_t<64, 2, 3, LGTile2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
                                          tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate,
-                                         vdiv, pre, NQ, q_out, stream);
+                                         vdiv, pre, NQ, q_out, stream, eoff);
 }
 
-int vocab_bwd_ds_blocks(int T, int R) { return (int)(((int64_t)T * R + DS_ROWS - 1) / DS_ROWS); }
-int vocab_bwd_ds_rows() { return DS_ROWS; }
-
-void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
-                         const float* lse, const int64_t* y_sel, int64_t ysel_rs,
-                         const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
-                         int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
-                         int64_t row_begin, int64_t row_end, hipStream_t stream) {
-  if (row_end <= row_begin) return;
-  const int nb = (int)((row_end - row_begin + DS_ROWS - 1) / DS_ROWS);
-  const int nvec = V >> 3;
-  // column split: >= ~6 blocks per CU (256 CUs), each thread >= 1 chunk
-  int split = 1;
-  while (split < 4 && nb * split < 1536 && (nvec + 2 * split - 1) / (2 * split) >= 256) split *= 2;
-  const int nch = ((nvec + split - 1) / split + 255) / 256;
-#define DS_LAUNCH(N)                                                                          \
-  hipLaunchKernelGGL(vocab_bwd_ds_kernel<N>, dim3(nb, split), dim3(256), 0, stream, buf, ldl, V, \
-                     R, T, T_sel, lse, y_sel, ysel_rs, dg_sel, dgsel_rs, y_xe, yxe_rs, dg_xe,    \
-                     dgxe_rs, colsum_part, row_begin, row_end)
-  switch (nch) {
-    case 1: DS_LAUNCH(1); break;
-    case 2: DS_LAUNCH(2); break;
-    case 3: DS_LAUNCH(3); break;
-    case 4: DS_LAUNCH(4); break;
-    case 5: DS_LAUNCH(5); break;
-    case 6: DS_LAUNCH(6); break;
-    case 7: DS_LAUNCH(7); break;
-    default: DS_LAUNCH(8); break;
-  }
-#undef DS_LAUNCH
-  post_launch("vocab_bwd_ds_kernel", stream);
+void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(vocab_exp_convert_kernel, dim3(R), dim3(256), 0, stream, buf, ldl, V, lse);
+  post_launch("vocab_exp_convert_kernel", stream);
 }
 
 }  // namespace cst

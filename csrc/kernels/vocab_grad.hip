@@ -1,0 +1,209 @@
+// K7: vocab-head backward from the exp store, without ever forming dS.
+//
+// Reference (/root/reference/model.py:281 log_softmax of the logit Linear,
+// criteria of /root/reference/train.py / utils.py): every loss of the
+// recipes is a per-row weighted log-prob of one chosen token, so for row
+// (t, r) with weights a (sampled / chosen token ys) and b (target token yx):
+//     dS_rv = a [v = ys] + b [v = yx] - (a + b) p_rv.
+// The decode kernel saved E_rv = exp(x_rv - c_r) (bf16, c_r = the row's LSE
+// of the previous step; step 0: its own LSE), so p_rv = s_r E_rv with
+// s_r = exp(c_r - lse_r).  With alpha_r = -(a + b) s_r the one-hot terms fold
+// into the row's own entries of E (vgrad_onehot: E'_{r,ys} = E_{r,ys} + a /
+// alpha_r, likewise yx; two scattered bf16 updates per row), so
+//     dS = diag(alpha) E'
+// exactly, and with plain hipBLASLt GEMMs over E':
+//     dHd = alpha . (E' W)          (vgrad_rows scales X = E' W in place)
+//     dW  = E'^T (alpha . Hd)       (vgrad_rows writes the scaled Hd rows)
+//     db  = sum_r alpha_r E'_r      (vgrad_colsum)
+// The former dS pass (read fp16 logits, write bf16 dS: 1.5 GB of HBM traffic,
+// ~0.44 ms per step) disappears.  A row whose weights cancel on two different
+// tokens (a + b = 0 with ys != yx, so dS_r = a (e_ys - e_yx)) keeps |alpha| >=
+// 2^-10 (|a| + |b|) s: its softmax part is then off by at most 2^-10 (|a| +
+// |b|) in total.
+#include "../common.h"
+#include "../launchers.h"
+
+namespace cst {
+
+struct RowW {
+  float a, b, s, al;
+  int ys, yx;
+};
+
+__device__ __forceinline__ RowW row_weights(const VGradRows& g, int64_t row) {
+  RowW w;
+  const int t = (int)(row / g.R), r = (int)(row % g.R);
+  const bool sel = g.dg_sel != nullptr && t < g.T_sel;
+  w.a = sel ? g.dg_sel[(int64_t)r * g.T_sel + t] : 0.f;
+  w.ys = sel ? (int)g.y_sel[(int64_t)r * g.T_sel + t] : -1;
+  w.b = g.dg_xe != nullptr ? g.dg_xe[(int64_t)r * g.dgxe_rs + t] : 0.f;
+  w.yx = g.dg_xe != nullptr ? (int)g.y_xe[(int64_t)r * g.yxe_rs + t] : -1;
+  w.s = t > 0 ? __expf(g.lse[(int64_t)(t - 1) * g.R + r] - g.lse[row]) : 1.f;
+  w.al = -(w.a + w.b) * w.s;
+  // weights that (nearly) cancel on two different tokens: keep alpha away from
+  // 0 so the one-hot terms stay representable (ys == yx cancels exactly)
+  if (w.a != 0.f && w.b != 0.f && w.ys >= 0 && w.yx >= 0 && w.ys != w.yx) {
+    const float floor_al = 0.0009765625f * (fabsf(w.a) + fabsf(w.b)) * w.s;
+    if (fabsf(w.al) < floor_al) w.al = w.al < 0.f ? -floor_al : floor_al;
+  }
+  return w;
+}
+
+// one thread per row: alpha, and the one-hot terms folded into E
+__global__ __launch_bounds__(256) void vgrad_onehot_kernel(VGradRows g, uint16_t* __restrict__ E,
+                                                           int64_t ldl,
+                                                           float* __restrict__ alpha) {
+  const int64_t NR = (int64_t)g.n_steps * g.R;
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= NR) return;
+  const RowW w = row_weights(g, row);
+  alpha[row] = w.al;
+  if (w.al == 0.f) return;  // no gradient through this row
+  uint16_t* e = E + row * ldl;
+  const float inv = 1.f / w.al;
+  const bool us = w.a != 0.f && w.ys >= 0, ux = w.b != 0.f && w.yx >= 0;
+  CST_DCHECK(!us || w.ys < g.V);
+  CST_DCHECK(!ux || w.yx < g.V);
+  if (us && ux && w.ys == w.yx) {
+    e[w.ys] = f2bf(bf2f(e[w.ys]) + (w.a + w.b) * inv);
+  } else {
+    if (us) e[w.ys] = f2bf(bf2f(e[w.ys]) + w.a * inv);
+    if (ux) e[w.yx] = f2bf(bf2f(e[w.yx]) + w.b * inv);
+  }
+}
+
+void launch_vgrad_onehot(const VGradRows& g, uint16_t* E, int64_t ldl, float* alpha,
+                         hipStream_t stream) {
+  const int64_t NR = (int64_t)g.n_steps * g.R;
+  hipLaunchKernelGGL(vgrad_onehot_kernel, dim3((unsigned)((NR + 255) / 256)), dim3(256), 0, stream,
+                     g, E, ldl, alpha);
+  post_launch("vgrad_onehot_kernel", stream);
+}
+
+constexpr int VG_THREADS = 256, VG_ROWS = VG_THREADS / WAVE;
+
+// One wavefront per rollout row, 8-column chunks per lane: dHd = alpha X in
+// place (X = E' W), hs = bf16(alpha Hd).
+__global__ __launch_bounds__(VG_THREADS) void vgrad_rows_kernel(
+    const float* __restrict__ alpha, int64_t NR, int H, const uint16_t* __restrict__ hd,
+    float* __restrict__ dhd, uint16_t* __restrict__ hs) {
+  const int64_t row = (int64_t)blockIdx.x * VG_ROWS + (threadIdx.x >> 6);
+  if (row >= NR) return;
+  const int lane = threadIdx.x & 63;
+  const float al = alpha[row];
+  for (int c = lane; 8 * c < H; c += WAVE) {
+    float4* xp = reinterpret_cast<float4*>(dhd + row * H + 8 * c);
+    float4 x0 = xp[0], x1 = xp[1];
+    const uint4 h = *reinterpret_cast<const uint4*>(hd + row * H + 8 * c);
+    x0.x *= al, x0.y *= al, x0.z *= al, x0.w *= al;
+    x1.x *= al, x1.y *= al, x1.z *= al, x1.w *= al;
+    xp[0] = x0;
+    xp[1] = x1;
+    const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+    uint32_t ho[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      ho[k] = (uint32_t)f2bf(al * bf2f(hw[k] & 0xffff)) |
+              ((uint32_t)f2bf(al * bf2f(hw[k] >> 16)) << 16);
+    *reinterpret_cast<uint4*>(hs + row * H + 8 * c) = make_uint4(ho[0], ho[1], ho[2], ho[3]);
+  }
+}
+
+void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd, float* dhd,
+                       uint16_t* hs, hipStream_t stream) {
+  if (H % 8 != 0) throw std::runtime_error("vgrad_rows: H must be a multiple of 8");
+  hipLaunchKernelGGL(vgrad_rows_kernel, dim3((unsigned)((NR + VG_ROWS - 1) / VG_ROWS)),
+                     dim3(VG_THREADS), 0, stream, alpha, NR, H, hd, dhd, hs);
+  post_launch("vgrad_rows_kernel", stream);
+}
+
+// Bias gradient, softmax part: db_v = sum_r alpha_r E_rv.  Block (i, j) owns
+// CS_ROWS rows and the 8-column chunks [256 j, 256 j + 256); each thread keeps
+// its chunk's 8 sums in registers over the rows (CS_UNROLL row loads in
+// flight) and writes one partial row per block; a second launch sums the
+// partials per column (deterministic, no atomics).
+constexpr int CS_ROWS = 128, CS_UNROLL = 8;
+
+int vgrad_colsum_blocks(int64_t NR) { return (int)((NR + CS_ROWS - 1) / CS_ROWS); }
+
+__global__ __launch_bounds__(256) void vgrad_colsum_kernel(const uint16_t* __restrict__ E,
+                                                           int64_t ldl, int V, int64_t NR,
+                                                           const float* __restrict__ alpha,
+                                                           float* __restrict__ part) {
+  __shared__ float s_al[CS_ROWS];
+  const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
+  const int nr = (int)min((int64_t)CS_ROWS, NR - r0);
+  if ((int)threadIdx.x < nr) s_al[threadIdx.x] = alpha[r0 + threadIdx.x];
+  __syncthreads();
+  const int ci = blockIdx.y * 256 + threadIdx.x;  // chunk
+  const int v0 = 8 * ci;
+  if (v0 >= V) return;
+  const int nv = min(8, V - v0);  // ragged last chunk: lanes >= nv are masked
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const uint16_t* base = E + r0 * ldl + v0;
+  for (int i = 0; i < nr; i += CS_UNROLL) {
+    uint4 x[CS_UNROLL];
+#pragma unroll
+    for (int u = 0; u < CS_UNROLL; ++u)
+      x[u] = i + u < nr ? *reinterpret_cast<const uint4*>(base + (int64_t)(i + u) * ldl)
+                        : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < CS_UNROLL; ++u) {
+      const float al = i + u < nr ? s_al[i + u] : 0.f;
+      const uint32_t w[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += al * bf2f(w[k] & 0xffff);
+        acc[2 * k + 1] += al * bf2f(w[k] >> 16);
+      }
+    }
+  }
+  float* out = part + (int64_t)blockIdx.x * V + v0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (k < nv) out[k] = acc[k];
+}
+
+// 64 columns per block, 4 groups of 64 threads splitting the partial rows
+// (8 loads in flight each), summed through LDS
+__global__ __launch_bounds__(256) void vgrad_colsum_reduce_kernel(const float* __restrict__ part,
+                                                                  int nb, int V,
+                                                                  float* __restrict__ db) {
+  __shared__ float s_p[4][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int v = blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (v < V) {
+    int b = g;
+    for (; b + 28 < nb; b += 32) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = part[(int64_t)(b + 4 * u) * V + v];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += x[u];
+    }
+    for (; b < nb; b += 4) s += part[(int64_t)b * V + v];
+  }
+  s_p[g][c] = s;
+  __syncthreads();
+  if (g == 0 && v < V) db[v] = s_p[0][c] + s_p[1][c] + s_p[2][c] + s_p[3][c];
+}
+
+void launch_vgrad_colsum(const uint16_t* E, int64_t ldl, int V, int64_t NR, const float* alpha,
+                         float* part, float* dblog, hipStream_t stream) {
+  // the ragged last chunk reads a whole 16-byte chunk: it must stay inside the row
+  if (ldl < (V + 7) / 8 * 8 || ldl % 8 != 0)
+    throw std::runtime_error("vgrad_colsum: row stride must cover V rounded up to 8");
+  const int nb = vgrad_colsum_blocks(NR);
+  const int nch = (V + 7) / 8;
+  hipLaunchKernelGGL(vgrad_colsum_kernel, dim3(nb, (nch + 255) / 256), dim3(256), 0, stream, E, ldl,
+                     V, NR, alpha, part);
+  post_launch("vgrad_colsum_kernel", stream);
+  hipLaunchKernelGGL(vgrad_colsum_reduce_kernel, dim3((V + 63) / 64), dim3(256), 0, stream, part,
+                     nb, V, dblog);
+  post_launch("vgrad_colsum_reduce_kernel", stream);
+}
+
+}  // namespace cst

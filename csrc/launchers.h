@@ -54,7 +54,8 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
                       const float* bias,
                       int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
                       int64_t tgt_stride, int flags, float inv_temp, const uint32_t* rng,
-                      int step, hipStream_t stream);  // flags: 1 = sample, 2 = argmax, 8 = fp32 logits
+                      int step, hipStream_t stream,
+                      const float* eoff = nullptr);  // flags: 1 = sample, 2 = argmax, 8 = fp32 logits, 16 = exp store
 // Cell epilogue of the next step, fused into the combine (see lstm_gemm.h).
 struct CellLaunch {
   const float* pre;
@@ -86,15 +87,35 @@ void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream,
-                           int NQ = 0, float* q_out = nullptr);
-int vocab_bwd_ds_blocks(int T, int R);
-// rows [row_begin, row_end) of the (T*R, ldl) buffer; row_begin % vocab_bwd_ds_rows() == 0
-void launch_vocab_bwd_ds(uint16_t* buf, int64_t ldl, int V, int R, int T, int T_sel,
-                         const float* lse, const int64_t* y_sel, int64_t ysel_rs,
-                         const float* dg_sel, int64_t dgsel_rs, const int64_t* y_xe,
-                         int64_t yxe_rs, const float* dg_xe, int64_t dgxe_rs, float* colsum_part,
-                         int64_t row_begin, int64_t row_end, hipStream_t stream);
-int vocab_bwd_ds_rows();
+                           int NQ = 0, float* q_out = nullptr, const float* eoff = nullptr);
+// exp store of step 0: fp16 logits rows -> bf16 exp(x - lse_r), in place
+void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,
+                              hipStream_t stream);
+
+// vocab_grad.hip: vocab-head backward from the exp store (see that file).
+// Row weights of the NR = n_steps * R rollout rows: sampled / chosen tokens
+// (weight dg_sel) and XE targets (weight dg_xe)
+struct VGradRows {
+  int R, n_steps, T_sel, H, V;
+  const float* lse;       // (n_steps, R)
+  const int64_t* y_sel;   // (R, T_sel) sampled / chosen tokens, nullable
+  const float* dg_sel;    // (R, T_sel), nullable
+  const int64_t* y_xe;    // labels + 1, row stride yxe_rs, nullable
+  int64_t yxe_rs;
+  const float* dg_xe;     // row stride dgxe_rs, nullable
+  int64_t dgxe_rs;
+};
+// alpha (NR) and the one-hot terms folded into E (NR rows, stride ldl), in place
+void launch_vgrad_onehot(const VGradRows& g, uint16_t* E, int64_t ldl, float* alpha,
+                         hipStream_t stream);
+// dhd = alpha . dhd in place (X = E' W -> dHd), hs = bf16(alpha . hd)
+void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd, float* dhd,
+                       uint16_t* hs, hipStream_t stream);
+// dblog = sum_r alpha_r E_rv (two launches: per-row-block partials, reduce);
+// part: vgrad_colsum_blocks(NR) * V floats
+int vgrad_colsum_blocks(int64_t NR);
+void launch_vgrad_colsum(const uint16_t* E, int64_t ldl, int V, int64_t NR, const float* alpha,
+                         float* part, float* dblog, hipStream_t stream);
 
 // lstm.hip
 void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
@@ -159,10 +180,15 @@ void launch_scst_loss_fwd(const int64_t* seq, const float* lp, int R, int T, con
 void launch_scst_loss_bwd(const int64_t* seq, const float* reward, const float* out,
                           const float* dloss, int R, int T, float* dlp, hipStream_t stream);
 
-// embed_grad.hip: out[stok[i]] += x[srow[i]] (fp32 rows grouped by token; C <= 1024)
-void launch_token_rows_sum(const float* x, int C, const int* stok, const int* srow, int N,
-                           float* out, hipStream_t stream);
-// counting sort of N token ids (< V <= 65536) into (stok, srow); ws: 2V ints
+// embed_grad.hip
+// per-token sums S[v] (bf16, V x C) of the bf16 rows x[srow[i]] (row stride ld)
+// over a token sort (ws = its workspace: counts, group ends); S32 (V x C fp32)
+// and flag (V ints) zeroed by the caller
+void launch_token_group_sum(const uint16_t* x, int C, int64_t ld, const int* stok,
+                            const int* srow, int N, const int* ws, int V, uint16_t* S, float* S32,
+                            int* flag, hipStream_t stream);
+// counting sort of N token ids (< V <= 65536) into (stok, srow); ws: 2V + 1 ints,
+// ws[2V] = number of sorted entries (ids outside [0, V) are left out)
 void launch_token_sort(const int64_t* toks, int N, int V, int* ws, int* stok, int* srow,
                        hipStream_t stream);
 

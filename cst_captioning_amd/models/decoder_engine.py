@@ -149,9 +149,12 @@ class _DecoderFn(torch.autograd.Function):
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
             drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell,
-            state0, eng.upper_operands())
+            state0, eng.upper_operands(), bool(save and not want_full))
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
+        # training rollouts save E = exp(logit - previous step's LSE) (bf16) for
+        # the dS-free backward; the full log-prob API keeps fp16 logits
+        ctx.store_exp = bool(save and not want_full)
         full = None
         if want_full:
             # full (R, T, V) log-probs for the model(feats, seq) API, from the
@@ -186,7 +189,7 @@ class _DecoderFn(torch.autograd.Function):
         R, T, vdiv, want_xe = ctx.save_dims
         eng = ctx.eng
         lse, logits16, hdrop, gates, c_all, h_all, seq, labels, bos = ctx.saved
-        ctx.saved = None  # logits buffer is overwritten in place by dS
+        ctx.saved = None  # (the fp16-logits buffer is overwritten in place by dS)
         att = list(ctx.att_saved) if ctx.has_att else []
         ctx.att_saved = None
         g_sel = dg_sel.contiguous() if dg_sel is not None else None
@@ -194,14 +197,18 @@ class _DecoderFn(torch.autograd.Function):
         empty = torch.empty(0, device=lse.device)
         n_steps = logits16.shape[0]
         ds_bias = empty
-        if dfull is not None and dfull.numel():
-            # gradient w.r.t. the full log-probs: dense dS = G - p * sum_v G
-            # (+ the gathered terms), written as bf16 into the logits buffer
+        if not ctx.store_exp:
+            # fp16 logits saved (full log-prob API): dense dS = G - p * sum_v G,
+            # G = the gradient w.r.t. the full log-probs (+ the gathered terms),
+            # written as bf16 into the logits buffer
             V = logit_b_numel = eng.V
             n_sel = g_sel.size(1) if g_sel is not None else 0
             # (n, R, V); a private dense copy: the incoming gradient may be an
             # expanded view (e.g. of full.sum()) or shared with other nodes
-            G = dfull.permute(1, 0, 2).float().clone(memory_format=torch.contiguous_format)
+            if dfull is not None and dfull.numel():
+                G = dfull.permute(1, 0, 2).float().clone(memory_format=torch.contiguous_format)
+            else:
+                G = torch.zeros(n_steps, R, V, device=lse.device)
             if g_sel is not None:
                 G[:n_sel].scatter_add_(2, seq.t()[:n_sel].unsqueeze(2), g_sel.t().unsqueeze(2))
             if g_xe is not None:

@@ -36,14 +36,12 @@ for R in (1280, 64):
             res['v%d_R%d_%s' % (var, R, name)] = round(us, 2)
 toks = torch.randint(0, V, (28 * 1280,), device=dev)
 res['token_sort_us'] = round(C.token_sort_bench(toks, V, 50), 2)
-if os.environ.get('DS', '1') == '1':
+if os.environ.get('CS', '1') == '1':  # bias-gradient column sums over the exp store
     n, R = 28, 1280
-    ldl = (V + 7) // 8 * 8
-    lg = (torch.randn(n, R, ldl, device=dev) * 2).half()
-    lse = torch.full((n, R), 12.0, device=dev)
-    seq = torch.randint(0, V, (R, n), device=dev)
-    dg = torch.randn(R, n, device=dev) * 1e-3
-    us = C.vocab_bwd_ds_bench(lg, lse, seq, dg, 10)
-    res['ds_T28_R1280_us'] = round(us, 1)
-    res['ds_TBps'] = round(2 * lg.numel() * 2 / us / 1e6, 2)
+    ldl = (V + 63) // 64 * 64
+    E = torch.rand(n, R, ldl, device=dev).bfloat16()
+    alpha = torch.randn(n * R, device=dev) * 1e-3
+    us = C.vgrad_colsum_bench(E, alpha, V, 10)
+    res['colsum_T28_R1280_us'] = round(us, 1)
+    res['colsum_TBps'] = round(n * R * V * 2 / us / 1e6, 2)
 print(json.dumps(res))
