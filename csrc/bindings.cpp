@@ -33,7 +33,10 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     std::vector<at::Tensor> state0, std::vector<at::Tensor> up);
 double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
+double att_bench(at::Tensor gv, at::Tensor P, at::Tensor q, at::Tensor wa, at::Tensor ba,
+                 int64_t R, int64_t which, int64_t iters);
 std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V);
+at::Tensor token_group_sum(at::Tensor x, at::Tensor toks, int64_t V);
 std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor sample,
                                           at::Tensor greedy);
 at::Tensor scst_loss_backward(at::Tensor seq, at::Tensor reward, at::Tensor out,
@@ -119,7 +122,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
   m.def("vgrad_colsum_bench", &cst::vgrad_colsum_bench);
   m.def("token_sort_bench", &cst::token_sort_bench);
+  m.def("att_bench", &cst::att_bench);
   m.def("token_sort", &cst::token_sort);
+  m.def("token_group_sum", &cst::token_group_sum);
   m.def("vocab_select", &cst::vocab_select);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);

@@ -408,12 +408,13 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 // Schedule (streams):
 //   side 0 : row weights alpha and the one-hot terms folded into E (dS =
 //            diag(alpha) E'), X = E' W_logit (one BLAS GEMM over all T*R
-//            rows), dHd = alpha X and the scaled rows alpha Hd in one pass;
+//            rows), then (under the loop) the scaled rows alpha Hd;
 //   main   : the input-token counting sort (under the side stream's GEMM),
-//            then waits for dHd and runs the reverse LSTM loop (one fused
-//            kernel per step: recurrent GEMM + cell backward), then the
-//            per-token gate-gradient sums, the embedding / input-weight
-//            gradient GEMMs over them and the batched recurrent-weight GEMMs;
+//            then waits for X and runs the reverse LSTM loop (one fused
+//            kernel per step: recurrent GEMM + cell backward; dHd = alpha X
+//            row-scaled as the step loads it), then the per-token
+//            gate-gradient sums, the embedding / input-weight gradient GEMMs
+//            over them and the batched recurrent-weight GEMMs;
 //   side 0 : dW_logit = E'^T (alpha Hd) and the bias column sums -- after
 //            the loop on one GPU, concurrently with the loop under data
 //            parallelism so the vocab head's all-reduce (comm_stream waits
@@ -481,11 +482,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   hipEvent_t ev_ready = aux.ev[0], ev_dhd = aux.ev[1], ev_done = aux.ev[2];
   c10::hip::HIPStream side = aux.side[0];
 
-  // 1-2. vocab head on the side stream.  Exp store (training): X = E W, then
-  // one row pass turns X into dHd in place (row scale alpha + the one-hot
-  // rows of W) and writes alpha, the alpha-scaled Hd rows and the one-hot
-  // keys; kernels/vocab_grad.hip.  Dense dS given by the caller (full
-  // log-prob API, fp16-logits buffer rewritten as bf16 dS): dHd = dS W.
+  // 1-2. vocab head on the side stream.  Exp store (training): alpha and the
+  // one-hot terms folded into E, X = E' W (dHd = alpha X, scaled by the
+  // loop), the alpha-scaled Hd rows for dW; kernels/vocab_grad.hip.  Dense
+  // dS given by the caller (full log-prob API, fp16-logits buffer rewritten
+  // as bf16 dS): dHd = dS W.
   const bool ds_ready = ds_bias.defined() && ds_bias.numel() > 0;
   if (ds_ready) {
     TORCH_CHECK(ds_bias.is_cuda() && ds_bias.scalar_type() == at::kFloat && ds_bias.numel() == V,
@@ -555,12 +556,15 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       launch_vgrad_onehot(va, reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl,
                           alpha.data_ptr<float>(), side.stream());
     }
+    // X = E' W; the reverse loop reads alpha X (row scales at load), so the
+    // loop starts right after the GEMM and the scaled Hd rows of the dW GEMM
+    // are formed under it
     at::mm_out(dHd, Ev, wlog, at::kFloat);
+    (void)hipEventRecord(ev_dhd, side.stream());
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
-                        reinterpret_cast<const uint16_t*>(hd2.data_ptr()), dHd.data_ptr<float>(),
+                        reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
                         reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
-    (void)hipEventRecord(ev_dhd, side.stream());
     if (vh_sched == 2) {
       dw_gemm();
       db_sums();
@@ -578,10 +582,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor sort_ws = at::empty({2 * V + 1}, i32);
   at::Tensor stok = at::empty({NR}, i32), srow = at::empty({NR}, i32);
   at::Tensor S_tok = at::empty({V, H4}, wx.options());  // per-token gate-gradient sums
-  at::Tensor S32 = at::zeros({V, H4}, f32), s_flag = at::zeros({V}, i32);
+  at::Tensor S32 = at::empty({V, H4}, f32);  // rows of long groups only (token_long_zero)
   // on the main stream, under the side stream's vocab-head GEMM
   launch_token_sort(toks.data_ptr<int64_t>(), (int)NR, (int)V, sort_ws.data_ptr<int>(),
                     stok.data_ptr<int>(), srow.data_ptr<int>(), st);
+  launch_token_long_zero(sort_ws.data_ptr<int>(), (int)V, (int)H4, S32.data_ptr<float>(), st);
 
   // 4. reverse LSTM loop on the main stream
   at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
@@ -606,6 +611,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dG_up[l] = at::empty({n_steps, R, H4}, wx.options());
     dc_up[l] = at::zeros({R, H}, f32);
   }
+  // the vocab head's gradient rows enter the loop as X = E' W with the row
+  // scales alpha applied at load (exp store); a dense dS gives dHd directly
+  auto dh_scale_t = [&](int64_t t) -> const float* {
+    return ds_ready ? nullptr : alpha.data_ptr<float>() + t * R;
+  };
   (void)hipStreamWaitEvent(st, ev_dhd, 0);
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     // top layer first: its h gradient comes from the vocab head (dHd, with the
@@ -613,9 +623,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // the inter-layer dropout mask of layer l's output
     for (int64_t l = NL - 1; l >= 1; --l) {
       const float* dh_in = dHd.data_ptr<float>() + t * R * H;
+      const float* dh_sc = dh_scale_t(t);
       if (l < NL - 1) {
         at::mm_out(dX_up, dG_up[l + 1][t], upw(l + 1, 0).narrow(1, 0, H), at::kFloat);
         dh_in = dX_up.data_ptr<float>();
+        dh_sc = nullptr;
       }
       launch_lstm_step_bwd(
           t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_up[l][t + 1].data_ptr()) : nullptr,
@@ -623,12 +635,14 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
           dc_up[l].data_ptr<float>(), reinterpret_cast<const uint16_t*>(upw(l, 3)[t].data_ptr()),
           upw(l, 2)[t].data_ptr<float>(), t > 0 ? upw(l, 2)[t - 1].data_ptr<float>() : nullptr,
           (int)R, (int)H, (float)drop_p, RNG, key(l, t),
-          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell);
+          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell, dh_sc);
     }
     const float* dh0_in = dHd.data_ptr<float>() + t * R * H;
+    const float* dh0_sc = dh_scale_t(t);
     if (NL > 1) {
       at::mm_out(dX_up, dG_up[1][t], upw(1, 0).narrow(1, 0, H), at::kFloat);
       dh0_in = dX_up.data_ptr<float>();
+      dh0_sc = nullptr;
     }
     launch_lstm_step_bwd(
         t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
@@ -637,7 +651,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         c_all[t].data_ptr<float>(),
         t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
         (int)R, (int)H, (float)drop_p, RNG, key(0, t),
-        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell);
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
@@ -646,6 +660,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
                      dba_part.data_ptr<float>(), st, per_frame);
   }
+  at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
   if (vh_sched == 0) {
     (void)hipEventRecord(ev_ready, st);  // reverse loop done
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
@@ -658,19 +673,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // 5. input-token gradients through the per-token sums S[v] = sum of the dG
   //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
   //    input-weight gradient S^T emb -- GEMMs over V rows instead of n*R
-  at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
   at::Tensor dG2 = dGx.narrow(1, 0, H4);
   launch_token_group_sum(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)H4, KD,
                          stok.data_ptr<int>(), srow.data_ptr<int>(), (int)NR,
                          sort_ws.data_ptr<int>(), (int)V,
-                         reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(),
-                         s_flag.data_ptr<int>(), st);
+                         reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   // 6. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
   //    reductions run as batched GEMMs over groups of steps (many more output
   //    tiles in flight than one K = 35k GEMM), summed afterwards.
   at::Tensor dWx = at::empty({H4, E + H}, f32);
-  at::Tensor dWq;
   auto grouped_wgrad = [&](at::Tensor a_rows, at::Tensor b_rows, int64_t nsteps) {
     int64_t G = 1;  // steps per group: largest divisor <= 7
     for (int64_t g = 7; g >= 1; --g)
@@ -680,6 +692,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     at::Tensor b = b_rows.reshape({nc, G * R, b_rows.size(1)});
     return at::bmm(a, b, at::kFloat).sum(0);
   };
+  at::Tensor dWq;
   dWx.narrow(1, 0, E).copy_(at::mm(S_tok.t(), emb, at::kFloat));
   if (n_steps > 1) {
     // with attention the extra rows of [dG | dq]^T h_prev are dW_q
@@ -1131,6 +1144,38 @@ double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t ite
       iters, st);
 }
 
+// temporal attention kernels alone (one decode / reverse step): Gv (Bv, C, 4H)
+// fp32, P (Bv, C, A), q (R, A), w_a (A), b_a (1); which = 0: forward
+// (accumulating into pre), 1: backward (dG rows (R, 4H + A) bf16, dq written)
+double att_bench(at::Tensor gv, at::Tensor P, at::Tensor q, at::Tensor wa, at::Tensor ba,
+                 int64_t R, int64_t which, int64_t iters) {
+  check_cuda(gv, "gv");
+  const int64_t Bv = gv.size(0), C = gv.size(1), H4 = gv.size(2), A = P.size(2);
+  TORCH_CHECK(R % Bv == 0 && q.size(0) == R && q.size(1) == A, "att_bench shapes");
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(gv.device());
+  const int vdiv = (int)(R / Bv);
+  at::Tensor pre = at::zeros({R, H4}, f32), alpha = at::full({R, C}, 1.f / C, f32);
+  at::Tensor dG = at::zeros({R, H4 + A}, gv.options().dtype(at::kBFloat16));
+  const int64_t nwg = Bv * att_groups(vdiv);
+  at::Tensor dpp = at::zeros({nwg, C, A}, f32), dwp = at::zeros({nwg, A}, f32),
+             dbp = at::zeros({nwg, 1}, f32);
+  hipStream_t st = cur_stream();
+  return time_launches(
+      [&](int) {
+        if (which == 0)
+          launch_att_fwd(gv.data_ptr<float>(), P.data_ptr<float>(), q.data_ptr<float>(), nullptr,
+                         wa.data_ptr<float>(), ba.data_ptr<float>(), (int)Bv, vdiv, (int)C, (int)A,
+                         (int)H4, pre.data_ptr<float>(), alpha.data_ptr<float>(), st, 1, 0);
+        else
+          launch_att_bwd(reinterpret_cast<uint16_t*>(dG.data_ptr()), (int)(H4 + A),
+                         gv.data_ptr<float>(), P.data_ptr<float>(), q.data_ptr<float>(),
+                         alpha.data_ptr<float>(), wa.data_ptr<float>(), (int)Bv, vdiv, (int)C,
+                         (int)A, (int)H4, 1, dpp.data_ptr<float>(), dwp.data_ptr<float>(),
+                         dbp.data_ptr<float>(), st, 0);
+      },
+      iters, st);
+}
+
 // counting sort of n token ids < V (the embedding-gradient grouping)
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters) {
   check_cuda(toks, "toks");
@@ -1186,6 +1231,28 @@ std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V) {
   launch_token_sort(toks.data_ptr<int64_t>(), (int)N, (int)V, ws.data_ptr<int>(),
                     stok.data_ptr<int>(), srow.data_ptr<int>(), cur_stream());
   return {stok, srow};
+}
+
+// per-token row sums for tests: x (N, C) bf16, toks (N) int64 -> S (V, C) bf16
+at::Tensor token_group_sum(at::Tensor x, at::Tensor toks, int64_t V) {
+  check_cuda(x, "x");
+  check_cuda(toks, "toks");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1, "x: (N, C) bf16");
+  TORCH_CHECK(toks.scalar_type() == at::kLong && toks.numel() == x.size(0), "toks: (N) int64");
+  const int64_t N = toks.numel(), C = x.size(1);
+  auto i32 = at::TensorOptions().dtype(at::kInt).device(toks.device());
+  at::Tensor ws = at::empty({2 * V + 1}, i32), stok = at::empty({N}, i32), srow = at::empty({N}, i32);
+  at::Tensor S = at::empty({V, C}, x.options());
+  at::Tensor S32 = at::empty({V, C}, x.options().dtype(at::kFloat));
+  hipStream_t st = cur_stream();
+  launch_token_sort(toks.data_ptr<int64_t>(), (int)N, (int)V, ws.data_ptr<int>(),
+                    stok.data_ptr<int>(), srow.data_ptr<int>(), st);
+  launch_token_long_zero(ws.data_ptr<int>(), (int)V, (int)C, S32.data_ptr<float>(), st);
+  launch_token_group_sum(reinterpret_cast<const uint16_t*>(x.data_ptr()), (int)C, x.stride(0),
+                         stok.data_ptr<int>(), srow.data_ptr<int>(), (int)N, ws.data_ptr<int>(),
+                         (int)V, reinterpret_cast<uint16_t*>(S.data_ptr()), S32.data_ptr<float>(),
+                         st);
+  return S;
 }
 
 }  // namespace cst

@@ -16,42 +16,62 @@ namespace cst {
 // sorted token stok[i] is v, as bf16 (V x C).  The embedding gradient is then
 // S W_ie and the input-weight gradient S^T emb: GEMMs over V rows instead of
 // the n*R rollout rows (3.4x fewer rows at V = 10.5k, R = 1280, 28 steps).
-// One 256-thread block per GS_CHUNK consecutive sorted entries, thread t
-// owning the 8-column chunks t + 256 j of every row (one 16-byte load per
-// thread and row, GS_PF rows in flight); the chunk's token / row indices are
-// staged in LDS.  A group that lies entirely in the chunk is stored directly
-// as bf16; a group that spans chunks (its first or last entry outside) is
-// added into the fp32 scratch S32 (zeroed by the caller) and flagged, and the
-// finalize pass converts flagged rows and zero-fills tokens without rows.
-// Atomics only at chunk boundaries, none per row.
-constexpr int GS_CHUNK = 64, GS_MAXJ = 2, GS_PF = 4;  // C <= 8 * 256 * GS_MAXJ = 4096
+//
+// Ownership instead of scratch: block b walks the sorted entries from the
+// start of the first group that begins in its chunk [GS_CHUNK b, GS_CHUNK (b +
+// 1)) to the END of the last such group, even past the chunk, so every group
+// of at most GS_LONG entries is summed by exactly one block, in a fixed order,
+// and stored once as bf16 (no atomics, no fp32 scratch).  Only
+// long groups (more than GS_LONG entries: the BOS token of step 0 has R of
+// them) are split at chunk boundaries; each chunk adds its part into the fp32
+// row S32[v] (zeroed by token_long_zero right after the sort, off the
+// critical path) and the finalize pass converts those rows and zero-fills the
+// tokens without entries.  (The former design zeroed a V x C fp32 scratch and
+// a flag array every step -- 86 MB -- and sent every chunk-spanning group
+// through atomics.)
+// Thread t owns the 8-column chunks t + 256 j of every row (one 16-byte load
+// per thread and row, GS_PF rows in flight); the block's entry indices are
+// staged in LDS.
+constexpr int GS_CHUNK = 64, GS_LONG = 192, GS_PF = 8;
+constexpr int GS_SPAN = GS_CHUNK + GS_LONG;  // entries one block can own
 
+template <int MAXJ>
 __global__ __launch_bounds__(256) void token_group_sum_kernel(
     const uint16_t* __restrict__ x, int C, int64_t ld, const int* __restrict__ stok,
-    const int* __restrict__ srow, int N, uint16_t* __restrict__ S, float* __restrict__ S32,
-    int* __restrict__ flag) {
-  __shared__ int s_tok[GS_CHUNK + 2];  // [0]: entry before the chunk, [n + 1]: after
-  __shared__ int s_row[GS_CHUNK];
+    const int* __restrict__ srow, const int* __restrict__ ws, int V, uint16_t* __restrict__ S,
+    float* __restrict__ S32) {
+  __shared__ int s_tok[GS_SPAN];
+  __shared__ int s_row[GS_SPAN];
+  const int* count = ws;
+  const int* gend = ws + V;  // after the scatter: end of each token's group
+  const int N = ws[2 * V];   // sorted entries
   const int c0 = blockIdx.x * GS_CHUNK;
-  const int n = min(GS_CHUNK, N - c0);
+  if (c0 >= N) return;
+  const int c1 = min(c0 + GS_CHUNK, N);
   const int tid = threadIdx.x;
-  if (tid < n) {
-    s_tok[tid + 1] = stok[c0 + tid];
-    s_row[tid] = srow[c0 + tid];
+  // owned range [lo, hi)
+  const int t0 = stok[c0], n0 = count[t0];
+  const int lo = (gend[t0] - n0 == c0 || n0 > GS_LONG) ? c0 : gend[t0];
+  const int tl = stok[c1 - 1], nl = count[tl];
+  const int hi = nl > GS_LONG ? c1 : (gend[tl] - nl >= c0 ? gend[tl] : c1);
+  const int n = hi - lo;
+  if (n <= 0) return;  // the chunk lies inside a short group begun earlier
+  CST_DCHECK(n <= GS_SPAN);
+  for (int i = tid; i < n; i += 256) {
+    s_tok[i] = stok[lo + i];
+    s_row[i] = srow[lo + i];
   }
-  if (tid == 64) s_tok[0] = c0 > 0 ? stok[c0 - 1] : -1;
-  if (tid == 65) s_tok[n + 1] = c0 + n < N ? stok[c0 + n] : -1;
   __syncthreads();
   const int nch = C >> 3;
-  float acc[GS_MAXJ][8];
+  float acc[MAXJ][8];
 #pragma unroll
-  for (int j = 0; j < GS_MAXJ; ++j)
+  for (int j = 0; j < MAXJ; ++j)
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
-  auto flush = [&](int v, bool inside) {
-    if (inside) {  // whole group in this chunk: final value
+  auto flush = [&](int v) {
+    if (count[v] <= GS_LONG) {  // whole group in this block: final value
 #pragma unroll
-      for (int j = 0; j < GS_MAXJ; ++j) {
+      for (int j = 0; j < MAXJ; ++j) {
         const int c = tid + 256 * j;
         if (c < nch) {
           uint4 o;
@@ -62,48 +82,45 @@ __global__ __launch_bounds__(256) void token_group_sum_kernel(
           *reinterpret_cast<uint4*>(S + (int64_t)v * C + 8 * c) = o;
         }
       }
-    } else {  // spans chunks: partial sum into the fp32 scratch
+    } else {  // this chunk's part of a long group
 #pragma unroll
-      for (int j = 0; j < GS_MAXJ; ++j) {
+      for (int j = 0; j < MAXJ; ++j) {
         const int c = tid + 256 * j;
         if (c < nch)
 #pragma unroll
           for (int k = 0; k < 8; ++k) atomicAdd(S32 + (int64_t)v * C + 8 * c + k, acc[j][k]);
       }
-      if (tid == 0) flag[v] = 1;
     }
 #pragma unroll
-    for (int j = 0; j < GS_MAXJ; ++j)
+    for (int j = 0; j < MAXJ; ++j)
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
   };
-  auto load = [&](int i, uint4 (&r)[GS_MAXJ]) {
+  auto load = [&](int i, uint4 (&r)[MAXJ]) {
     const uint16_t* row = x + (int64_t)s_row[i] * ld;
 #pragma unroll
-    for (int j = 0; j < GS_MAXJ; ++j) {
+    for (int j = 0; j < MAXJ; ++j) {
       const int c = tid + 256 * j;
       r[j] = c < nch ? *reinterpret_cast<const uint4*>(row + 8 * c) : make_uint4(0, 0, 0, 0);
     }
   };
-  uint4 buf[GS_PF][GS_MAXJ];
+  uint4 buf[GS_PF][MAXJ];
 #pragma unroll
   for (int p = 0; p < GS_PF; ++p)
     if (p < n) load(p, buf[p]);
-  int cur = s_tok[1];
-  bool first = true;  // cur is the chunk's first group
+  int cur = s_tok[0];
   for (int i0 = 0; i0 < n; i0 += GS_PF) {
 #pragma unroll
     for (int p = 0; p < GS_PF; ++p) {
       const int i = i0 + p;
       if (i < n) {
-        const int tk = s_tok[i + 1];
+        const int tk = s_tok[i];
         if (tk != cur) {
-          flush(cur, !first || s_tok[0] != cur);
+          flush(cur);
           cur = tk;
-          first = false;
         }
 #pragma unroll
-        for (int j = 0; j < GS_MAXJ; ++j) {
+        for (int j = 0; j < MAXJ; ++j) {
           const uint32_t w[4] = {buf[p][j].x, buf[p][j].y, buf[p][j].z, buf[p][j].w};
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -115,18 +132,29 @@ __global__ __launch_bounds__(256) void token_group_sum_kernel(
       }
     }
   }
-  flush(cur, (!first || s_tok[0] != cur) && s_tok[n + 1] != cur);
+  flush(cur);
+}
+
+// one wavefront per token: zero the fp32 rows of long groups (before the sums)
+__global__ __launch_bounds__(256) void token_long_zero_kernel(int V, int C,
+                                                              const int* __restrict__ count,
+                                                              float* __restrict__ S32) {
+  const int v = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (v >= V || count[v] <= GS_LONG) return;
+  for (int c = lane; c < (C >> 2); c += 64)
+    reinterpret_cast<float4*>(S32 + (int64_t)v * C)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // one wavefront per token: zero rows of tokens without entries, convert the
-// flagged (chunk-spanning) rows from the fp32 scratch
+// long groups' rows from the fp32 scratch
 __global__ __launch_bounds__(256) void token_group_finalize_kernel(
-    int V, int C, const int* __restrict__ count, const int* __restrict__ flag,
-    const float* __restrict__ S32, uint16_t* __restrict__ S) {
+    int V, int C, const int* __restrict__ count, const float* __restrict__ S32,
+    uint16_t* __restrict__ S) {
   const int v = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (v >= V) return;
-  const bool empty = count[v] == 0;
-  if (!empty && flag[v] == 0) return;
+  const int cnt = count[v];
+  if (cnt > 0 && cnt <= GS_LONG) return;
+  const bool empty = cnt == 0;
   for (int c = lane; c < (C >> 3); c += 64) {
     uint4 o = make_uint4(0, 0, 0, 0);
     if (!empty) {
@@ -141,16 +169,30 @@ __global__ __launch_bounds__(256) void token_group_finalize_kernel(
   }
 }
 
+void launch_token_long_zero(const int* ws, int V, int C, float* S32, hipStream_t stream) {
+  if (C % 4 != 0) throw std::runtime_error("token_long_zero: C must be a multiple of 4");
+  hipLaunchKernelGGL(token_long_zero_kernel, dim3((V + 3) / 4), dim3(256), 0, stream, V, C, ws,
+                     S32);
+  post_launch("token_long_zero_kernel", stream);
+}
+
 void launch_token_group_sum(const uint16_t* x, int C, int64_t ld, const int* stok,
                             const int* srow, int N, const int* ws, int V, uint16_t* S, float* S32,
-                            int* flag, hipStream_t stream) {
-  if (C % 8 != 0 || C > 256 * 8 * GS_MAXJ || ld % 8 != 0)
+                            hipStream_t stream) {
+  if (C % 8 != 0 || C > 256 * 8 * 2 || ld % 8 != 0)
     throw std::runtime_error("token_group_sum: C and ld multiples of 8, C <= 4096");
-  hipLaunchKernelGGL(token_group_sum_kernel, dim3((N + GS_CHUNK - 1) / GS_CHUNK), dim3(256), 0,
-                     stream, x, C, ld, stok, srow, N, S, S32, flag);
+  // grid over the N input entries (the sorted count ws[2V] <= N is read on
+  // the device; chunks past it exit)
+  const dim3 grid((N + GS_CHUNK - 1) / GS_CHUNK);
+  if (C <= 256 * 8)
+    hipLaunchKernelGGL(token_group_sum_kernel<1>, grid, dim3(256), 0, stream, x, C, ld, stok, srow,
+                       ws, V, S, S32);
+  else
+    hipLaunchKernelGGL(token_group_sum_kernel<2>, grid, dim3(256), 0, stream, x, C, ld, stok, srow,
+                       ws, V, S, S32);
   post_launch("token_group_sum_kernel", stream);
   hipLaunchKernelGGL(token_group_finalize_kernel, dim3((V + 3) / 4), dim3(256), 0, stream, V, C,
-                     ws, flag, S32, S);
+                     ws, S32, S);
   post_launch("token_group_finalize_kernel", stream);
 }
 

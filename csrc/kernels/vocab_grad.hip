@@ -12,7 +12,7 @@
 // alpha_r, likewise yx; two scattered bf16 updates per row), so
 //     dS = diag(alpha) E'
 // exactly, and with plain hipBLASLt GEMMs over E':
-//     dHd = alpha . (E' W)          (vgrad_rows scales X = E' W in place)
+//     dHd = alpha . (E' W)          (row scales applied by the reverse loop)
 //     dW  = E'^T (alpha . Hd)       (vgrad_rows writes the scaled Hd rows)
 //     db  = sum_r alpha_r E'_r      (vgrad_colsum)
 // The former dS pass (read fp16 logits, write bf16 dS: 1.5 GB of HBM traffic,
@@ -82,8 +82,10 @@ void launch_vgrad_onehot(const VGradRows& g, uint16_t* E, int64_t ldl, float* al
 
 constexpr int VG_THREADS = 256, VG_ROWS = VG_THREADS / WAVE;
 
-// One wavefront per rollout row, 8-column chunks per lane: dHd = alpha X in
-// place (X = E' W), hs = bf16(alpha Hd).
+// One wavefront per rollout row, 8-column chunks per lane: hs = bf16(alpha
+// Hd) (and dHd = alpha X in place when dhd is given; the engine instead lets
+// the reverse loop scale the rows it reads, so this pass leaves the critical
+// path).
 __global__ __launch_bounds__(VG_THREADS) void vgrad_rows_kernel(
     const float* __restrict__ alpha, int64_t NR, int H, const uint16_t* __restrict__ hd,
     float* __restrict__ dhd, uint16_t* __restrict__ hs) {
@@ -92,13 +94,15 @@ __global__ __launch_bounds__(VG_THREADS) void vgrad_rows_kernel(
   const int lane = threadIdx.x & 63;
   const float al = alpha[row];
   for (int c = lane; 8 * c < H; c += WAVE) {
-    float4* xp = reinterpret_cast<float4*>(dhd + row * H + 8 * c);
-    float4 x0 = xp[0], x1 = xp[1];
+    if (dhd != nullptr) {
+      float4* xp = reinterpret_cast<float4*>(dhd + row * H + 8 * c);
+      float4 x0 = xp[0], x1 = xp[1];
+      x0.x *= al, x0.y *= al, x0.z *= al, x0.w *= al;
+      x1.x *= al, x1.y *= al, x1.z *= al, x1.w *= al;
+      xp[0] = x0;
+      xp[1] = x1;
+    }
     const uint4 h = *reinterpret_cast<const uint4*>(hd + row * H + 8 * c);
-    x0.x *= al, x0.y *= al, x0.z *= al, x0.w *= al;
-    x1.x *= al, x1.y *= al, x1.z *= al, x1.w *= al;
-    xp[0] = x0;
-    xp[1] = x1;
     const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
     uint32_t ho[4];
 #pragma unroll

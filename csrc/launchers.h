@@ -108,7 +108,8 @@ struct VGradRows {
 // alpha (NR) and the one-hot terms folded into E (NR rows, stride ldl), in place
 void launch_vgrad_onehot(const VGradRows& g, uint16_t* E, int64_t ldl, float* alpha,
                          hipStream_t stream);
-// dhd = alpha . dhd in place (X = E' W -> dHd), hs = bf16(alpha . hd)
+// dhd = alpha . dhd in place (X = E' W -> dHd; dhd nullable: the consumer
+// scales the rows itself), hs = bf16(alpha . hd)
 void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd, float* dhd,
                        uint16_t* hs, hipStream_t stream);
 // dblog = sum_r alpha_r E_rv (two launches: per-row-block partials, reduce);
@@ -131,7 +132,8 @@ int lstm_bwd_tiles(int R, int H);
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
-                          int step, uint16_t* dG, int KD, hipStream_t stream, int cell);
+                          int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
+                          const float* dh_scale = nullptr);  // dh_logit row scales (nullable)
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal
 // attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
@@ -182,11 +184,12 @@ void launch_scst_loss_bwd(const int64_t* seq, const float* reward, const float* 
 
 // embed_grad.hip
 // per-token sums S[v] (bf16, V x C) of the bf16 rows x[srow[i]] (row stride ld)
-// over a token sort (ws = its workspace: counts, group ends); S32 (V x C fp32)
-// and flag (V ints) zeroed by the caller
+// over a token sort (ws = its workspace: counts, group ends); S32 (V x C fp32
+// scratch) must have been prepared by launch_token_long_zero after the sort
+void launch_token_long_zero(const int* ws, int V, int C, float* S32, hipStream_t stream);
 void launch_token_group_sum(const uint16_t* x, int C, int64_t ld, const int* stok,
                             const int* srow, int N, const int* ws, int V, uint16_t* S, float* S32,
-                            int* flag, hipStream_t stream);
+                            hipStream_t stream);
 // counting sort of N token ids (< V <= 65536) into (stok, srow); ws: 2V + 1 ints,
 // ws[2V] = number of sorted entries (ids outside [0, V) are left out)
 void launch_token_sort(const int64_t* toks, int N, int V, int* ws, int* stok, int* srow,

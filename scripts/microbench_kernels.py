@@ -44,4 +44,14 @@ if os.environ.get('CS', '1') == '1':  # bias-gradient column sums over the exp s
     us = C.vgrad_colsum_bench(E, alpha, V, 10)
     res['colsum_T28_R1280_us'] = round(us, 1)
     res['colsum_TBps'] = round(n * R * V * 2 / us / 1e6, 2)
+if os.environ.get('ATT', '1') == '1':  # temporal attention kernels, 8 frames
+    Bv, Cf, A = 64, 8, H
+    gv = torch.randn(Bv, Cf, 4 * H, device=dev) * 0.1
+    P = torch.randn(Bv, Cf, A, device=dev) * 0.5
+    wa = torch.randn(A, device=dev) * 0.1
+    ba = torch.zeros(1, device=dev)
+    for R in (1280, 64):
+        q = torch.randn(R, A, device=dev) * 0.5
+        res['att_fwd_R%d_us' % R] = round(C.att_bench(gv, P, q, wa, ba, R, 0, 50), 2)
+        res['att_bwd_R%d_us' % R] = round(C.att_bench(gv, P, q, wa, ba, R, 1, 50), 2)
 print(json.dumps(res))

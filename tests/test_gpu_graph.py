@@ -100,6 +100,31 @@ def test_token_counting_sort():
     assert np.array_equal(t[sr], st)                 # each row under its own token
 
 
+@pytest.mark.parametrize('C', [2048, 4096])
+def test_token_group_sums(C):
+    """Per-token row sums (embedding / input-weight gradient operand): short
+    groups summed by their owning block, long groups (the BOS / EOS buckets,
+    groups of 200-300 entries around the 192-entry split) through the fp32
+    scratch, and tokens without rows zero-filled -- against an fp32
+    index_add."""
+    from cst_captioning_amd import _ext
+    V, N = 10509, 28 * 1280
+    g = torch.Generator(device='cpu').manual_seed(3)
+    toks = torch.randint(1, V - 50, (N,), generator=g)
+    toks[:1280] = 0                     # step 0: BOS for every row
+    toks[5000:5250] = 7                 # long groups just above / below the split
+    toks[9000:9193] = 8
+    toks[12000:12192] = 9
+    toks = toks[torch.randperm(N, generator=g)].to(DEV)
+    x = torch.randn(N, C, generator=g).to(DEV, torch.bfloat16)
+    S = _ext.ops().token_group_sum(x, toks, V)
+    ref = torch.zeros(V, C, device=DEV).index_add_(0, toks, x.float())
+    assert S.dtype == torch.bfloat16 and S.shape == (V, C)
+    assert torch.all(S[V - 50:] == 0)   # tokens without rows
+    err = (S.float() - ref).norm() / ref.norm()
+    assert err < 4e-3, err
+
+
 def test_lr_change_reaches_the_graph():
     """An LR decay between replays (adjust_learning_rate) takes effect
     without a re-capture: with lr = 0 the weights stop moving."""
