@@ -1156,22 +1156,24 @@ double att_bench(at::Tensor gv, at::Tensor P, at::Tensor q, at::Tensor wa, at::T
   const int vdiv = (int)(R / Bv);
   at::Tensor pre = at::zeros({R, H4}, f32), alpha = at::full({R, C}, 1.f / C, f32);
   at::Tensor dG = at::zeros({R, H4 + A}, gv.options().dtype(at::kBFloat16));
-  const int64_t nwg = Bv * att_groups(vdiv);
+  const int rpw_b = which == 4 ? 2 : ATT_BWD_RPW;  // 1: backward, 4: backward at 2 rows
+  const int64_t nwg = Bv * att_groups(vdiv, rpw_b);
   at::Tensor dpp = at::zeros({nwg, C, A}, f32), dwp = at::zeros({nwg, A}, f32),
              dbp = at::zeros({nwg, 1}, f32);
   hipStream_t st = cur_stream();
   return time_launches(
       [&](int) {
-        if (which == 0)
+        if (which != 1 && which != 4)  // forward at 4 (0), 2 (2) or 1 (3) rows per workgroup
           launch_att_fwd(gv.data_ptr<float>(), P.data_ptr<float>(), q.data_ptr<float>(), nullptr,
                          wa.data_ptr<float>(), ba.data_ptr<float>(), (int)Bv, vdiv, (int)C, (int)A,
-                         (int)H4, pre.data_ptr<float>(), alpha.data_ptr<float>(), st, 1, 0);
+                         (int)H4, pre.data_ptr<float>(), alpha.data_ptr<float>(), st, 1, 0,
+                         which == 2 ? 2 : which == 3 ? 1 : 4);
         else
           launch_att_bwd(reinterpret_cast<uint16_t*>(dG.data_ptr()), (int)(H4 + A),
                          gv.data_ptr<float>(), P.data_ptr<float>(), q.data_ptr<float>(),
                          alpha.data_ptr<float>(), wa.data_ptr<float>(), (int)Bv, vdiv, (int)C,
                          (int)A, (int)H4, 1, dpp.data_ptr<float>(), dwp.data_ptr<float>(),
-                         dbp.data_ptr<float>(), st, 0);
+                         dbp.data_ptr<float>(), st, 0, rpw_b);
       },
       iters, st);
 }

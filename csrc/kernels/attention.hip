@@ -43,233 +43,29 @@
 //     the recurrence and the batched weight-gradient GEMM yields dW_q for
 //     free.  dP / dw_a / db_a accumulate in per-workgroup slots (the grid
 //     shape is the same every step, so no atomics and a deterministic sum).
-#include "../common.h"
+#include "att_fwd.h"
 #include "../launchers.h"
 
 namespace cst {
 
-constexpr int ATT_THREADS = 256, ATT_RPW = 4, ATT_WAVES = ATT_THREADS / WAVE;
-
-// Butterfly all-reduce of N (32 or 64) per-lane partial sums across the 64
-// lanes of a wave in log2(64) exchange steps: each step a lane keeps half of
-// its values and adds the partner's copy of them, so the wave spends N-1
-// shuffles instead of 6 N for N separate reductions.  Afterwards lane l holds
-// the total of value index (l >> (6 - log2 N)) in v[0].
-template <int N, int M>
-struct Bfly {
-  static __device__ __forceinline__ void run(float* v, int lane) {
-    constexpr int H = N / 2;
-    const bool up = (lane & M) != 0;
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      const float send = up ? v[i] : v[i + H];
-      const float keep = up ? v[i + H] : v[i];
-      v[i] = keep + __shfl_xor(send, M, WAVE);
-    }
-    Bfly<H, M / 2>::run(v, lane);
-  }
-};
-template <int M>
-struct Bfly<1, M> {
-  static __device__ __forceinline__ void run(float* v, int lane) {
-    v[0] += __shfl_xor(v[0], M, WAVE);
-    Bfly<1, M / 2>::run(v, lane);
-  }
-};
-template <>
-struct Bfly<1, 0> {
-  static __device__ __forceinline__ void run(float*, int) {}
-};
-
-// Sum of RPW x MAXC per-thread partials over the whole block -> s_out
-// (index s * MAXC + c); s_red holds ATT_WAVES x RPW x MAXC floats.
-template <int MAXC>
-__device__ __forceinline__ void block_sum_partials(float (&part)[ATT_RPW][MAXC], float* s_red,
-                                                   float* s_out) {
-  constexpr int N = ATT_RPW * MAXC;
-  constexpr int CH = N < 64 ? N : 64;  // butterfly chunk
-  constexpr int SH = CH == 32 ? 1 : 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float* flat = &part[0][0];
-#pragma unroll
-  for (int c0 = 0; c0 < N; c0 += CH) {
-    Bfly<CH, 32>::run(flat + c0, lane);
-    if ((lane & ((1 << SH) - 1)) == 0) s_red[w * N + c0 + (lane >> SH)] = flat[c0];
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < N; i += ATT_THREADS) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < ATT_WAVES; ++k) t += s_red[k * N + i];
-    s_out[i] = t;
-  }
-  __syncthreads();
-}
-
-// Column groups (float4) of the 4H gate vector a thread prefetches into
-// registers: 2 x 256 threads x 4 = 2048 = 4H at H = 512 (larger H loops).
-constexpr int ATT_GPF = 2;
-
-// grid: Bv * ngroups blocks; block (b, g) owns rows b*vdiv + g*RPW ... (< (b+1)*vdiv)
-// Scores: thread t owns attention units a = t + 256 j and accumulates the
-// partial dot products of all RPW x C (row, frame) pairs over them (its own
-// columns of P[b] and q: coalesced loads, no LDS staging), then one butterfly
-// + cross-wave sum finishes every score at once.
-template <int MAXC>
-__global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(
-    const float* __restrict__ gv, const float* __restrict__ pre, const float* __restrict__ q,
-    const int* __restrict__ q_rowmap, const float* __restrict__ wa, const float* __restrict__ ba,
-    int wa_ld, int ba_ld, int vdiv, int ngroups, int C, int A, int G4, float* __restrict__ vg_out,
-    float* __restrict__ alpha_out, int accumulate) {
-  __shared__ float s_red[ATT_WAVES * ATT_RPW * MAXC];
-  __shared__ float s_e[ATT_RPW * MAXC];
-  const int b = blockIdx.x / ngroups, g = blockIdx.x % ngroups;
-  const int r0 = b * vdiv + g * ATT_RPW, nr = min(ATT_RPW, vdiv - g * ATT_RPW);
-  const int tid = threadIdx.x;
-  const float4* G = reinterpret_cast<const float4*>(gv + (int64_t)b * C * G4);
-  const int G44 = G4 >> 2;
-  // the video's frame gate rows (L2-resident, shared by its row groups) are
-  // requested first: their latency hides under the scores
-  // (register prefetch only for C <= 8: 2 x 8 float4 = 64 VGPRs)
-  const bool gpf = MAXC <= 8 && G44 <= ATT_GPF * ATT_THREADS;
-  float4 gr[ATT_GPF][MAXC];
-  if (gpf) {
-#pragma unroll
-    for (int j = 0; j < ATT_GPF; ++j)
-#pragma unroll
-      for (int c = 0; c < MAXC; ++c)
-        gr[j][c] = (c < C && tid + j * ATT_THREADS < G44)
-                       ? G[(int64_t)c * G44 + tid + j * ATT_THREADS]
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  // accumulate: the rows' current pre-activations (written by the previous
-  // launch) are requested up front too, so the final add does not wait on a
-  // second memory round trip
-  float4 acc0[ATT_GPF][ATT_RPW];
-  if (gpf && accumulate) {
-#pragma unroll
-    for (int j = 0; j < ATT_GPF; ++j)
-#pragma unroll
-      for (int s = 0; s < ATT_RPW; ++s)
-        acc0[j][s] = (s < nr && tid + j * ATT_THREADS < G44)
-                         ? reinterpret_cast<const float4*>(vg_out + (int64_t)(r0 + s) * G4)[tid + j * ATT_THREADS]
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  int qrow[ATT_RPW];
-#pragma unroll
-  for (int s = 0; s < ATT_RPW; ++s) {
-    const int r = r0 + min(s, nr - 1);
-    qrow[s] = q_rowmap ? q_rowmap[r] : r;
-    CST_DCHECK(qrow[s] >= 0 && qrow[s] < (int)(gridDim.x / ngroups) * vdiv);
-  }
-  CST_DCHECK(nr >= 1 && g * ATT_RPW + nr <= vdiv);
-  float part[ATT_RPW][MAXC];
-#pragma unroll
-  for (int s = 0; s < ATT_RPW; ++s)
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) part[s][c] = 0.f;
-  const float* P = pre + (int64_t)b * C * A;
-  for (int a = tid; a < A; a += ATT_THREADS) {
-    float qv[ATT_RPW];
-#pragma unroll
-    for (int s = 0; s < ATT_RPW; ++s) qv[s] = q != nullptr ? q[(int64_t)qrow[s] * A + a] : 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c < C) {
-        const float wa_a = wa[c * wa_ld + a];
-        const float pc = P[(int64_t)c * A + a];
-#pragma unroll
-        for (int s = 0; s < ATT_RPW; ++s) part[s][c] += wa_a * tanhf_(pc + qv[s]);
-      }
-    }
-  }
-  block_sum_partials<MAXC>(part, s_red, s_e);
-  if (tid < nr) {  // softmax over frames, one thread per row
-    float* e = s_e + tid * MAXC;
-    float m = -INFINITY;
-    for (int c = 0; c < C; ++c) {
-      e[c] += ba[c * ba_ld];
-      m = fmaxf(m, e[c]);
-    }
-    float sum = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const float x = __expf(e[c] - m);
-      e[c] = x;
-      sum += x;
-    }
-    const float inv = 1.f / sum;
-    for (int c = 0; c < C; ++c) {
-      e[c] *= inv;
-      if (alpha_out) alpha_out[(int64_t)(r0 + tid) * C + c] = e[c];
-    }
-  }
-  __syncthreads();
-  // vgate_r = sum_c alpha_rc Gv[b, c]: each thread owns float4 column groups
-  auto emit = [&](int cg, const float4* gcol, int pj) {  // pj: prefetched group, or -1
-    float4 acc[ATT_RPW];
-#pragma unroll
-    for (int s = 0; s < ATT_RPW; ++s) acc[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c < C) {
-        const float4 v = gcol[c];
-#pragma unroll
-        for (int s = 0; s < ATT_RPW; ++s) {
-          const float al = s_e[min(s, nr - 1) * MAXC + c];
-          acc[s].x += al * v.x;
-          acc[s].y += al * v.y;
-          acc[s].z += al * v.z;
-          acc[s].w += al * v.w;
-        }
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < ATT_RPW; ++s) {
-      if (s < nr) {
-        float4* dst = reinterpret_cast<float4*>(vg_out + (int64_t)(r0 + s) * G4) + cg;
-        if (accumulate) {
-          float4 o;
-          if (pj >= 0) {
-#pragma unroll
-            for (int j = 0; j < ATT_GPF; ++j)
-              if (j == pj) o = acc0[j][s];
-          } else {
-            o = *dst;
-          }
-          acc[s].x += o.x, acc[s].y += o.y, acc[s].z += o.z, acc[s].w += o.w;
-        }
-        *dst = acc[s];
-      }
-    }
-  };
-  if (gpf) {
-#pragma unroll
-    for (int j = 0; j < ATT_GPF; ++j)
-      if (tid + j * ATT_THREADS < G44) emit(tid + j * ATT_THREADS, gr[j], j);
-  } else {
-    for (int cg = tid; cg < G44; cg += ATT_THREADS) {
-      float4 gcol[MAXC];
-#pragma unroll
-      for (int c = 0; c < MAXC; ++c)
-        gcol[c] = c < C ? G[(int64_t)c * G44 + cg] : make_float4(0.f, 0.f, 0.f, 0.f);
-      emit(cg, gcol, -1);
-    }
-  }
+template <int MAXC, int RPW>
+__global__ __launch_bounds__(ATT_THREADS) void att_fwd_kernel(AttFwdArgs args) {
+  att_fwd_block<MAXC, RPW>(blockIdx.x, args);
 }
 
 // dG: (R, ldg) bf16 rows, gate gradients in columns [0, G4); dq_t is written
 // as bf16 into columns [G4, G4 + A) when write_dq.  PERC: per-frame scorer
 // weights (MANet): dw_a / db_a slots are (C, A) / (C) per workgroup.
-template <int MAXC, bool PERC>
+template <int MAXC, bool PERC, int RPW>
 __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     uint16_t* __restrict__ dG, int ldg, const float* __restrict__ gv,
     const float* __restrict__ pre, const float* __restrict__ q, const float* __restrict__ alpha,
     const float* __restrict__ wa, int vdiv, int ngroups, int C, int A, int G4, int write_dq,
     float* __restrict__ dpre_part, float* __restrict__ dwa_part, float* __restrict__ dba_part) {
-  __shared__ float s_red[ATT_WAVES * ATT_RPW * MAXC];
-  __shared__ float s_da[ATT_RPW * MAXC];
+  __shared__ float s_red[ATT_WAVES * RPW * MAXC];
+  __shared__ float s_da[RPW * MAXC];
   const int b = blockIdx.x / ngroups, g = blockIdx.x % ngroups;
-  const int r0 = b * vdiv + g * ATT_RPW, nr = min(ATT_RPW, vdiv - g * ATT_RPW);
+  const int r0 = b * vdiv + g * RPW, nr = min(RPW, vdiv - g * RPW);
   const int tid = threadIdx.x;
   // this block's accumulator slots of dP / dw_a (read-modify-write every
   // reverse step) and its columns of P / q: requested up front, so the loads
@@ -277,7 +73,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   constexpr int AJ = 2;  // attention units per thread held in registers (A <= 512)
   constexpr int NW = PERC ? MAXC : 1;  // scorer-weight rows
   const bool apf = MAXC <= 8 && A <= AJ * ATT_THREADS;  // (register budget)
-  float acc_dp[AJ][MAXC], acc_dw[AJ][NW], pv[AJ][MAXC], qv[AJ][ATT_RPW];
+  float acc_dp[AJ][MAXC], acc_dw[AJ][NW], pv[AJ][MAXC], qv[AJ][RPW];
   float* dpp = dpre_part + (int64_t)blockIdx.x * C * A;
   float* dwp = dwa_part + (int64_t)blockIdx.x * (PERC ? C : 1) * A;
   const float* P = pre + (int64_t)b * C * A;
@@ -293,34 +89,41 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
         pv[j][c] = (a < A && c < C) ? P[c * A + a] : 0.f;
       }
 #pragma unroll
-      for (int s = 0; s < ATT_RPW; ++s)
+      for (int s = 0; s < RPW; ++s)
         qv[j][s] = (a < A && q != nullptr && s < nr) ? q[(int64_t)(r0 + s) * A + a] : 0.f;
     }
   }
 
+  // the softmax-backward thread's attention weights, requested now
+  float avp[MAXC <= 8 ? MAXC : 1];
+  if (MAXC <= 8 && tid < nr) {
+#pragma unroll
+    for (int c = 0; c < (MAXC <= 8 ? MAXC : 1); ++c)
+      avp[c] = c < C ? alpha[(int64_t)(r0 + tid) * C + c] : 0.f;
+  }
   // 1. dalpha[s][c] = dG_r . Gv[b, c]  (the first ATT_GPF column groups of the
   // rows' dG are requested up front with the partial slots)
-  uint2 dgp[ATT_GPF][ATT_RPW];
+  uint2 dgp[ATT_GPF][RPW];
 #pragma unroll
   for (int j = 0; j < ATT_GPF; ++j)
 #pragma unroll
-    for (int s = 0; s < ATT_RPW; ++s) {
+    for (int s = 0; s < RPW; ++s) {
       const int cg = tid + j * ATT_THREADS;
       dgp[j][s] = (s < nr && cg < (G4 >> 2))
                       ? *reinterpret_cast<const uint2*>(dG + (int64_t)(r0 + s) * ldg + 4 * cg)
                       : make_uint2(0u, 0u);
     }
-  float part[ATT_RPW][MAXC];
+  float part[RPW][MAXC];
 #pragma unroll
-  for (int s = 0; s < ATT_RPW; ++s)
+  for (int s = 0; s < RPW; ++s)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) part[s][c] = 0.f;
   const float4* G = reinterpret_cast<const float4*>(gv + (int64_t)b * C * G4);
   const int G44 = G4 >> 2;
   for (int cg = tid, j = 0; cg < G44; cg += ATT_THREADS, ++j) {
-    float4 d[ATT_RPW];
+    float4 d[RPW];
 #pragma unroll
-    for (int s = 0; s < ATT_RPW; ++s) {
+    for (int s = 0; s < RPW; ++s) {
       d[s] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (s < nr) {
         const uint2 raw = j < ATT_GPF ? dgp[j < ATT_GPF ? j : 0][s]
@@ -334,12 +137,12 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
       if (c < C) {
         const float4 v = G[(int64_t)c * G44 + cg];
 #pragma unroll
-        for (int s = 0; s < ATT_RPW; ++s)
+        for (int s = 0; s < RPW; ++s)
           part[s][c] += d[s].x * v.x + d[s].y * v.y + d[s].z * v.z + d[s].w * v.w;
       }
     }
   }
-  block_sum_partials<MAXC>(part, s_red, s_da);
+  block_sum_partials<MAXC, RPW>(part, s_red, s_da);
   // 2. softmax backward: de_c = alpha_c (dalpha_c - sum_k alpha_k dalpha_k), in place
   if (tid < nr) {
     const float* al = alpha + (int64_t)(r0 + tid) * C;
@@ -347,7 +150,10 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     float av[MAXC], sa = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      av[c] = c < C ? al[c] : 0.f;
+      if (MAXC <= 8)
+        av[c] = avp[MAXC <= 8 ? c : 0];
+      else
+        av[c] = c < C ? al[c] : 0.f;
       sa += c < C ? av[c] * da[c] : 0.f;
     }
 #pragma unroll
@@ -371,15 +177,15 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   // 3. scorer backward, thread per attention unit a:
   //    dz = de_c w_a (1 - u^2), u = tanh(P_c + q_s); dq_s = sum_c dz; dP_c = sum_s dz
   auto unit = [&](int a, const float* pa, const float* qa, float (&dp)[MAXC], float (&dwa)[NW]) {
-    float dq[ATT_RPW];
+    float dq[RPW];
 #pragma unroll
-    for (int s = 0; s < ATT_RPW; ++s) dq[s] = 0.f;
+    for (int s = 0; s < RPW; ++s) dq[s] = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       if (c < C) {
         const float wa_a = wa[PERC ? c * A + a : a];
 #pragma unroll
-        for (int s = 0; s < ATT_RPW; ++s) {
+        for (int s = 0; s < RPW; ++s) {
           if (s < nr) {
             const float u = tanhf_(pa[c] + qa[s]);
             const float de = s_de[s * MAXC + c];
@@ -393,7 +199,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     }
     if (write_dq) {
 #pragma unroll
-      for (int s = 0; s < ATT_RPW; ++s)
+      for (int s = 0; s < RPW; ++s)
         if (s < nr) dG[(int64_t)(r0 + s) * ldg + G4 + a] = f2bf(dq[s]);
     }
   };
@@ -413,7 +219,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     }
   } else {
     for (int a = tid; a < A; a += ATT_THREADS) {
-      float dp[MAXC], pa[MAXC], qa[ATT_RPW], dw[NW];
+      float dp[MAXC], pa[MAXC], qa[RPW], dw[NW];
 #pragma unroll
       for (int w = 0; w < NW; ++w) dw[w] = 0.f;
 #pragma unroll
@@ -422,7 +228,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
         pa[c] = c < C ? P[c * A + a] : 0.f;
       }
 #pragma unroll
-      for (int s = 0; s < ATT_RPW; ++s)
+      for (int s = 0; s < RPW; ++s)
         qa[s] = (q != nullptr && s < nr) ? q[(int64_t)(r0 + s) * A + a] : 0.f;
       unit(a, pa, qa, dp, dw);
 #pragma unroll
@@ -435,18 +241,19 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   }
 }
 
-int att_groups(int vdiv) { return (vdiv + ATT_RPW - 1) / ATT_RPW; }
+int att_groups(int vdiv, int rpw) { return (vdiv + rpw - 1) / rpw; }
 
-void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
-                    const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
-                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate,
-                    int per_frame) {
-  const int ng = att_groups(vdiv);
+template <int RPW>
+static void launch_att_fwd_t(const float* gv, const float* pre, const float* q,
+                             const int* q_rowmap, const float* wa, const float* ba, int Bv,
+                             int vdiv, int C, int A, int G4, float* vg_out, float* alpha_out,
+                             hipStream_t stream, int accumulate, int per_frame) {
+  const int ng = (vdiv + RPW - 1) / RPW;
   const int wa_ld = per_frame ? A : 0, ba_ld = per_frame ? 1 : 0;
-#define ATT_FWD(M)                                                                          \
-  hipLaunchKernelGGL(att_fwd_kernel<M>, dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, gv, pre, \
-                     q, q_rowmap, wa, ba, wa_ld, ba_ld, vdiv, ng, C, A, G4, vg_out, alpha_out,  \
-                     accumulate)
+#define ATT_FWD(M)                                                                              \
+  hipLaunchKernelGGL((att_fwd_kernel<M, RPW>), dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, args)
+  const AttFwdArgs args{gv, pre, q, q_rowmap, wa, ba, wa_ld, ba_ld, vdiv, ng, C, A, G4, vg_out,
+                        alpha_out, accumulate};
   if (C <= 8)
     ATT_FWD(8);
   else if (C <= 16)
@@ -457,13 +264,25 @@ void launch_att_fwd(const float* gv, const float* pre, const float* q, const int
   post_launch("att_fwd_kernel", stream);
 }
 
-template <int MAXC, bool PERC>
+void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
+                    const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
+                    float* vg_out, float* alpha_out, hipStream_t stream, int accumulate,
+                    int per_frame, int rpw) {
+  if (rpw == 0) rpw = vdiv >= 4 ? 4 : vdiv >= 2 ? 2 : 1;
+  switch (rpw) {
+    case 1: launch_att_fwd_t<1>(gv, pre, q, q_rowmap, wa, ba, Bv, vdiv, C, A, G4, vg_out, alpha_out, stream, accumulate, per_frame); break;
+    case 2: launch_att_fwd_t<2>(gv, pre, q, q_rowmap, wa, ba, Bv, vdiv, C, A, G4, vg_out, alpha_out, stream, accumulate, per_frame); break;
+    default: launch_att_fwd_t<4>(gv, pre, q, q_rowmap, wa, ba, Bv, vdiv, C, A, G4, vg_out, alpha_out, stream, accumulate, per_frame); break;
+  }
+}
+
+template <int MAXC, bool PERC, int RPW>
 static void launch_att_bwd_t(uint16_t* dG, int ldg, const float* gv, const float* pre,
                              const float* q, const float* alpha, const float* wa, int Bv, int vdiv,
                              int C, int A, int G4, int write_dq, float* dpre_part, float* dwa_part,
                              float* dba_part, hipStream_t stream) {
-  const int ng = att_groups(vdiv);
-  hipLaunchKernelGGL((att_bwd_kernel<MAXC, PERC>), dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, dG, ldg,
+  const int ng = att_groups(vdiv, RPW);
+  hipLaunchKernelGGL((att_bwd_kernel<MAXC, PERC, RPW>), dim3(Bv * ng), dim3(ATT_THREADS), 0, stream, dG, ldg,
                      gv, pre, q, alpha, wa, vdiv, ng, C, A, G4, write_dq, dpre_part, dwa_part,
                      dba_part);
   post_launch("att_bwd_kernel", stream);
@@ -472,19 +291,19 @@ static void launch_att_bwd_t(uint16_t* dG, int ldg, const float* gv, const float
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,
                     const float* alpha, const float* wa, int Bv, int vdiv, int C, int A, int G4,
                     int write_dq, float* dpre_part, float* dwa_part, float* dba_part,
-                    hipStream_t stream, int per_frame) {
-#define ATT_BWD(M, PF)                                                                        \
-  launch_att_bwd_t<M, PF>(dG, ldg, gv, pre, q, alpha, wa, Bv, vdiv, C, A, G4, write_dq, dpre_part, \
-                          dwa_part, dba_part, stream)
+                    hipStream_t stream, int per_frame, int rpw) {
+#define ATT_BWD(M, PF, RP)                                                                   \
+  launch_att_bwd_t<M, PF, RP>(dG, ldg, gv, pre, q, alpha, wa, Bv, vdiv, C, A, G4, write_dq,   \
+                              dpre_part, dwa_part, dba_part, stream)
   if (per_frame) {  // MANet: C = number of modalities
     if (C > 8) throw std::runtime_error("per-frame attention weights: at most 8 frames");
-    ATT_BWD(8, true);
+    if (rpw == 2) ATT_BWD(8, true, 2); else ATT_BWD(8, true, 4);
   } else if (C <= 8) {
-    ATT_BWD(8, false);
+    if (rpw == 2) ATT_BWD(8, false, 2); else ATT_BWD(8, false, 4);
   } else if (C <= 16) {
-    ATT_BWD(16, false);
+    ATT_BWD(16, false, 4);
   } else {
-    ATT_BWD(32, false);
+    ATT_BWD(32, false, 4);
   }
 #undef ATT_BWD
 }

@@ -151,37 +151,45 @@ __global__ __launch_bounds__(256) void featpool_bwd_kernel(FeatPoolArgs a, const
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float dbias = 0.f;  // kt == 0 blocks, thread tid < 64: unit u0 + tid
-  for (int rs = 0; rs < a.rows; rs += FP_KS) {
-    // 32 rows x 64 columns of dz and of x: 2 float4 of each per thread,
-    // written transposed (column-major = K-contiguous per unit / k)
+  // 32 rows x 64 columns of dz and of x per K step: 2 float4 of each per
+  // thread.  The next step's rows are requested before this step's MFMAs, so
+  // their latency hides under the math (a K loop of 16 steps at 512 rows).
+  float4 dy[2], yv[2], xv[2];
+  auto load = [&](int rs) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int rr = (tid >> 4) + 16 * i, c4 = 4 * (tid & 15), r = rs + rr;
-      float4 dz = make_float4(0.f, 0.f, 0.f, 0.f), xv = make_float4(0.f, 0.f, 0.f, 0.f);
+      dy[i] = yv[i] = xv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (r < a.rows) {
         const int64_t o = (int64_t)r * FH + f * a.H + u0 + c4;
-        const float4 dy = *reinterpret_cast<const float4*>(dout + o);
-        const float4 y = *reinterpret_cast<const float4*>(outp + o);
-        dz = make_float4(y.x > 0.f ? dy.x * inv_keep : 0.f, y.y > 0.f ? dy.y * inv_keep : 0.f,
-                         y.z > 0.f ? dy.z * inv_keep : 0.f, y.w > 0.f ? dy.w * inv_keep : 0.f);
-        if (k0 + c4 < g.d) xv = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.d + k0 + c4);
+        dy[i] = *reinterpret_cast<const float4*>(dout + o);
+        yv[i] = *reinterpret_cast<const float4*>(outp + o);
+        if (k0 + c4 < g.d) xv[i] = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.d + k0 + c4);
       }
-      As[(c4 + 0) * FP_LDA + rr] = dz.x;
-      As[(c4 + 1) * FP_LDA + rr] = dz.y;
-      As[(c4 + 2) * FP_LDA + rr] = dz.z;
-      As[(c4 + 3) * FP_LDA + rr] = dz.w;
-      Bs[(c4 + 0) * FP_LDA + rr] = xv.x;
-      Bs[(c4 + 1) * FP_LDA + rr] = xv.y;
-      Bs[(c4 + 2) * FP_LDA + rr] = xv.z;
-      Bs[(c4 + 3) * FP_LDA + rr] = xv.w;
+    }
+  };
+  load(0);
+  for (int rs = 0; rs < a.rows; rs += FP_KS) {
+    // written transposed (column-major = K-contiguous per unit / k)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = (tid >> 4) + 16 * i, c4 = 4 * (tid & 15);
+      const float4 d = dy[i], y = yv[i], x = xv[i];
+      As[(c4 + 0) * FP_LDA + rr] = y.x > 0.f ? d.x * inv_keep : 0.f;
+      As[(c4 + 1) * FP_LDA + rr] = y.y > 0.f ? d.y * inv_keep : 0.f;
+      As[(c4 + 2) * FP_LDA + rr] = y.z > 0.f ? d.z * inv_keep : 0.f;
+      As[(c4 + 3) * FP_LDA + rr] = y.w > 0.f ? d.w * inv_keep : 0.f;
+      Bs[(c4 + 0) * FP_LDA + rr] = x.x;
+      Bs[(c4 + 1) * FP_LDA + rr] = x.y;
+      Bs[(c4 + 2) * FP_LDA + rr] = x.z;
+      Bs[(c4 + 3) * FP_LDA + rr] = x.w;
     }
     __syncthreads();
+    if (rs + FP_KS < a.rows) load(rs + FP_KS);
     fp_mfma_step(As, Bs, acc);
-    if (kt == 0 && tid < FP_T) {  // bias gradient in fp32 (L2-resident re-read)
-      for (int rr = 0; rr < FP_KS && rs + rr < a.rows; ++rr) {
-        const int64_t o = (int64_t)(rs + rr) * FH + f * a.H + u0 + tid;
-        dbias += outp[o] > 0.f ? dout[o] * inv_keep : 0.f;
-      }
+    if (kt == 0 && tid < FP_T) {  // bias gradient: this step's dz column of the unit (LDS)
+#pragma unroll 8
+      for (int rr = 0; rr < FP_KS; ++rr) dbias += As[tid * FP_LDA + rr];
     }
     __syncthreads();
   }

@@ -71,6 +71,19 @@ struct CellLaunch {
   int step;
   int cell;  // CellType (common.h)
 };
+// temporal-attention forward operands (kernels/att_fwd.h)
+struct AttFwdArgs {
+  const float* gv;       // (Bv, C, G4) per-frame gate tables
+  const float* pre;      // (Bv, C, A) projected frames P
+  const float* q;        // (rows, A) queries (nullptr: q = 0)
+  const int* q_rowmap;   // nullable: query row of each row
+  const float* wa;       // scorer weights (A) or (C, A) per frame
+  const float* ba;       // scorer bias (1) or (C)
+  int wa_ld, ba_ld, vdiv, ngroups, C, A, G4;
+  float* vg_out;         // (rows, G4): per-row video gate term
+  float* alpha_out;      // nullable (rows, C)
+  int accumulate;        // 1: vg_out += (else =)
+};
 // size of the end-of-sequence flag area per decode step (ints) of `counts`
 int combine_count_ints_per_step();
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
@@ -137,17 +150,24 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal
 // attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
-int att_groups(int vdiv);
+// rows of one video per attention-backward workgroup (2 or 4; C > 8: 4)
+constexpr int ATT_BWD_RPW = 4;
+int att_groups(int vdiv, int rpw = ATT_BWD_RPW);  // backward workgroups per video
 // vg_out[r] = sum_c alpha_rc Gv[b, c]  (+= when accumulate: adds into pre)
+// rows of one video per attention-forward workgroup: 0 = by the rows per
+// video (4 at >= 4, e.g. the rollout's 20; 1 for the one-row greedy baseline:
+// 16.6 vs 22.7 us at 1,280 rows, 9.2 vs 7.2 us at 64,
+// profiles/r2/microbench_kernels_v11.json)
+constexpr int ATT_FWD_RPW = 0;
 void launch_att_fwd(const float* gv, const float* pre, const float* q, const int* q_rowmap,
                     const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
                     float* vg_out, float* alpha_out, hipStream_t stream, int accumulate,
-                    int per_frame);
+                    int per_frame, int rpw = ATT_FWD_RPW);
 // dwa_part / dba_part: per-workgroup slots of (A) / (1), or (C, A) / (C) per_frame
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,
                     const float* alpha, const float* wa, int Bv, int vdiv, int C, int A, int G4,
                     int write_dq, float* dpre_part, float* dwa_part, float* dba_part,
-                    hipStream_t stream, int per_frame);
+                    hipStream_t stream, int per_frame, int rpw = ATT_BWD_RPW);
 
 // featpool.hip: FeatPool (per modality Linear -> ReLU -> Dropout, concat)
 constexpr int FEATPOOL_MAX_F = 8;

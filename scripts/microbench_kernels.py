@@ -53,5 +53,8 @@ if os.environ.get('ATT', '1') == '1':  # temporal attention kernels, 8 frames
     for R in (1280, 64):
         q = torch.randn(R, A, device=dev) * 0.5
         res['att_fwd_R%d_us' % R] = round(C.att_bench(gv, P, q, wa, ba, R, 0, 50), 2)
+        res['att_fwd_rpw2_R%d_us' % R] = round(C.att_bench(gv, P, q, wa, ba, R, 2, 50), 2)
+        res['att_fwd_rpw1_R%d_us' % R] = round(C.att_bench(gv, P, q, wa, ba, R, 3, 50), 2)
         res['att_bwd_R%d_us' % R] = round(C.att_bench(gv, P, q, wa, ba, R, 1, 50), 2)
+        res['att_bwd_rpw2_R%d_us' % R] = round(C.att_bench(gv, P, q, wa, ba, R, 4, 50), 2)
 print(json.dumps(res))
