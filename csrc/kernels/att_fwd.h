@@ -144,17 +144,44 @@ __device__ __forceinline__ void att_fwd_block(int bid, const AttFwdArgs& args) {
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) part[s][c] = 0.f;
   const float* P = pre + (int64_t)b * C * A;
-  for (int a = tid; a < A; a += ATT_THREADS) {
-    float qv[RPW];
+  // A <= 512 (C <= 8): every unit's query / frame / scorer operand is
+  // requested in ONE batch (a single memory round trip instead of one per
+  // unit group); the latency-bound kernel has registers to spare
+  constexpr int AJ = 2;
+  if (MAXC <= 8 && A <= AJ * ATT_THREADS) {
+    float qv[AJ][RPW], pcv[AJ][MAXC], wav[AJ][MAXC];
 #pragma unroll
-    for (int s = 0; s < RPW; ++s) qv[s] = q != nullptr ? q[(int64_t)qrow[s] * A + a] : 0.f;
+    for (int j = 0; j < AJ; ++j) {
+      const int a = tid + j * ATT_THREADS;
+      const bool ok = a < A;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c < C) {
-        const float wa_a = wa[c * wa_ld + a];
-        const float pc = P[(int64_t)c * A + a];
+      for (int s = 0; s < RPW; ++s)
+        qv[j][s] = (ok && q != nullptr) ? q[(int64_t)qrow[s] * A + a] : 0.f;
 #pragma unroll
-        for (int s = 0; s < RPW; ++s) part[s][c] += wa_a * tanhf_(pc + qv[s]);
+      for (int c = 0; c < MAXC; ++c) {
+        wav[j][c] = (ok && c < C) ? wa[c * wa_ld + a] : 0.f;  // 0: no contribution
+        pcv[j][c] = (ok && c < C) ? P[(int64_t)c * A + a] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < AJ; ++j)
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int s = 0; s < RPW; ++s) part[s][c] += wav[j][c] * tanhf_(pcv[j][c] + qv[j][s]);
+  } else {
+    for (int a = tid; a < A; a += ATT_THREADS) {
+      float qv[RPW];
+#pragma unroll
+      for (int s = 0; s < RPW; ++s) qv[s] = q != nullptr ? q[(int64_t)qrow[s] * A + a] : 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        if (c < C) {
+          const float wa_a = wa[c * wa_ld + a];
+          const float pc = P[(int64_t)c * A + a];
+#pragma unroll
+          for (int s = 0; s < RPW; ++s) part[s][c] += wa_a * tanhf_(pc + qv[s]);
+        }
       }
     }
   }

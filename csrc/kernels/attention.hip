@@ -73,7 +73,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   constexpr int AJ = 2;  // attention units per thread held in registers (A <= 512)
   constexpr int NW = PERC ? MAXC : 1;  // scorer-weight rows
   const bool apf = MAXC <= 8 && A <= AJ * ATT_THREADS;  // (register budget)
-  float acc_dp[AJ][MAXC], acc_dw[AJ][NW], pv[AJ][MAXC], qv[AJ][RPW];
+  float acc_dp[AJ][MAXC], acc_dw[AJ][NW], pv[AJ][MAXC], qv[AJ][RPW], wap[AJ][NW];
   float* dpp = dpre_part + (int64_t)blockIdx.x * C * A;
   float* dwp = dwa_part + (int64_t)blockIdx.x * (PERC ? C : 1) * A;
   const float* P = pre + (int64_t)b * C * A;
@@ -82,7 +82,10 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     for (int j = 0; j < AJ; ++j) {
       const int a = tid + j * ATT_THREADS;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) acc_dw[j][w] = (a < A && w < C) ? dwp[w * A + a] : 0.f;
+      for (int w = 0; w < NW; ++w) {
+        acc_dw[j][w] = (a < A && w < C) ? dwp[w * A + a] : 0.f;
+        wap[j][w] = (a < A && w < C) ? wa[PERC ? w * A + a : a] : 0.f;
+      }
 #pragma unroll
       for (int c = 0; c < MAXC; ++c) {
         acc_dp[j][c] = (a < A && c < C) ? dpp[c * A + a] : 0.f;
@@ -120,7 +123,34 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     for (int c = 0; c < MAXC; ++c) part[s][c] = 0.f;
   const float4* G = reinterpret_cast<const float4*>(gv + (int64_t)b * C * G4);
   const int G44 = G4 >> 2;
-  for (int cg = tid, j = 0; cg < G44; cg += ATT_THREADS, ++j) {
+  // C <= 8, 4H <= 2048: the video's frame gate rows are requested with the dG
+  // rows (one memory round trip for the whole dalpha phase)
+  const bool gpf = MAXC <= 8 && G44 <= ATT_GPF * ATT_THREADS;
+  if (gpf) {
+    float4 gvp[ATT_GPF][MAXC <= 8 ? MAXC : 1];
+#pragma unroll
+    for (int j = 0; j < ATT_GPF; ++j)
+#pragma unroll
+      for (int c = 0; c < (MAXC <= 8 ? MAXC : 1); ++c) {
+        const int cg = tid + j * ATT_THREADS;
+        gvp[j][c] = (c < C && cg < G44) ? G[(int64_t)c * G44 + cg] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+    for (int j = 0; j < ATT_GPF; ++j) {
+#pragma unroll
+      for (int s = 0; s < RPW; ++s) {
+        const uint2 raw = dgp[j][s];  // zero for rows / columns outside
+        const float4 d = make_float4(bf2f(raw.x & 0xffff), bf2f(raw.x >> 16),
+                                     bf2f(raw.y & 0xffff), bf2f(raw.y >> 16));
+#pragma unroll
+        for (int c = 0; c < (MAXC <= 8 ? MAXC : 1); ++c) {
+          const float4 v = gvp[j][c];
+          part[s][c] += d.x * v.x + d.y * v.y + d.z * v.z + d.w * v.w;
+        }
+      }
+    }
+  }
+  for (int cg = tid, j = 0; !gpf && cg < G44; cg += ATT_THREADS, ++j) {
     float4 d[RPW];
 #pragma unroll
     for (int s = 0; s < RPW; ++s) {
@@ -176,14 +206,15 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
   }
   // 3. scorer backward, thread per attention unit a:
   //    dz = de_c w_a (1 - u^2), u = tanh(P_c + q_s); dq_s = sum_c dz; dP_c = sum_s dz
-  auto unit = [&](int a, const float* pa, const float* qa, float (&dp)[MAXC], float (&dwa)[NW]) {
+  auto unit = [&](int a, const float* pa, const float* qa, float (&dp)[MAXC], float (&dwa)[NW],
+                  const float* wv) {  // wv: the unit's scorer weights (prefetched) or nullptr
     float dq[RPW];
 #pragma unroll
     for (int s = 0; s < RPW; ++s) dq[s] = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       if (c < C) {
-        const float wa_a = wa[PERC ? c * A + a : a];
+        const float wa_a = wv != nullptr ? wv[PERC ? c : 0] : wa[PERC ? c * A + a : a];
 #pragma unroll
         for (int s = 0; s < RPW; ++s) {
           if (s < nr) {
@@ -208,7 +239,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
     for (int j = 0; j < AJ; ++j) {
       const int a = tid + j * ATT_THREADS;
       if (a < A) {
-        unit(a, pv[j], qv[j], acc_dp[j], acc_dw[j]);
+        unit(a, pv[j], qv[j], acc_dp[j], acc_dw[j], wap[j]);
 #pragma unroll
         for (int w = 0; w < NW; ++w)
           if (w < C) dwp[w * A + a] = acc_dw[j][w];
@@ -230,7 +261,7 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
 #pragma unroll
       for (int s = 0; s < RPW; ++s)
         qa[s] = (q != nullptr && s < nr) ? q[(int64_t)(r0 + s) * A + a] : 0.f;
-      unit(a, pa, qa, dp, dw);
+      unit(a, pa, qa, dp, dw, nullptr);
 #pragma unroll
       for (int w = 0; w < NW; ++w)
         if (w < C) dwp[w * A + a] += dw[w];

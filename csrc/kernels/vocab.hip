@@ -75,6 +75,13 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // tiles in vocab_combine_kernel, and the union of independent races is the
 // race over all of V.
 constexpr int VT_V = 128;  // vocab entries per block
+// exp-store staging tile in LDS: BN rows x (VT_V + 8) bf16 (16-byte aligned
+// row starts), placed behind the GroupStat area (4 groups x BN rows x 32 B)
+constexpr int EXP_STAGE_LD = VT_V + 8;
+__host__ __device__ constexpr int exp_stage_off(int BN) { return 4 * BN * 32; }
+__host__ __device__ constexpr int epilogue_lds_bytes(int BN) {
+  return exp_stage_off(BN) + BN * EXP_STAGE_LD * 2;
+}
 // VF_EXP: the saved copy is E = exp(x - eoff[r]) in bf16 instead of fp16 x
 // (eoff = the row's LSE of the previous decode step), see vocab_grad.hip
 enum VocabFlags : int {
@@ -85,7 +92,7 @@ enum VocabFlags : int {
   VF_EXP = 16
 };
 
-struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS
+struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS (exp_stage_off)
   float m, s, zkey, zlogit;
   int zidx, xidx;
   float xt, pad;
@@ -242,22 +249,19 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       // ~88; that would surface as a non-finite gradient, which the optimizer's
       // NaN guard skips)
       const float f = __builtin_amdgcn_exp2f((msafe - ec[j]) * L2E);
-      uint16_t* dst = logits16 + (int64_t)r * ldl;
+      // staged through LDS (behind the row statistics' GroupStat area): the
+      // MFMA layout gives each lane 8-byte pieces of 32 different rows; the
+      // block then writes whole 256-byte row segments (see below)
+      uint16_t* et = reinterpret_cast<uint16_t*>(lds + exp_stage_off(BN)) + row_l * EXP_STAGE_LD;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int v = vb + 32 * i + 8 * q;
-          if (v + 4 <= V) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(ew[i][4 * q] * f) | ((uint32_t)f2bf(ew[i][4 * q + 1] * f) << 16);
-            pk.y = (uint32_t)f2bf(ew[i][4 * q + 2] * f) | ((uint32_t)f2bf(ew[i][4 * q + 3] * f) << 16);
-            *reinterpret_cast<uint2*>(dst + v) = pk;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (v + e < V) dst[v + e] = f2bf(ew[i][4 * q + e] * f);
-          }
+          const int vl = vb - v0 + 32 * i + 8 * q;  // entries past V: weight 0
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(ew[i][4 * q] * f) | ((uint32_t)f2bf(ew[i][4 * q + 1] * f) << 16);
+          pk.y = (uint32_t)f2bf(ew[i][4 * q + 2] * f) | ((uint32_t)f2bf(ew[i][4 * q + 3] * f) << 16);
+          *reinterpret_cast<uint2*>(et + vl) = pk;
         }
     }
 
@@ -362,6 +366,20 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       p.xtgt = a.xt;
       p.pad = 0.f;
       part[(int64_t)vt * R + r] = p;
+    }
+  }
+  if ((flags & VF_EXP) && logits16 != nullptr) {
+    // the staged exp-store tile (written before the barrier above): 16 bytes
+    // per thread and pass, 16 threads per 256-byte row segment; columns past
+    // V hold 0 (bias -inf) and are written up to the row stride ldl
+    const uint16_t* et = reinterpret_cast<const uint16_t*>(lds + exp_stage_off(BN));
+#pragma unroll
+    for (int idx = threadIdx.x; idx < BN * (VT_V / 8); idx += 256) {
+      const int row = idx / (VT_V / 8), ch = idx % (VT_V / 8);
+      const int r = r0 + row, v = v0 + 8 * ch;
+      if (r < R && v + 8 <= ldl)
+        *reinterpret_cast<uint4*>(logits16 + (int64_t)r * ldl + v) =
+            *reinterpret_cast<const uint4*>(et + row * EXP_STAGE_LD + 8 * ch);
     }
   }
 }
@@ -649,9 +667,9 @@ static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const
                                 float inv_temp, const uint32_t* rng, int step,
                                 hipStream_t stream, const float* eoff = nullptr) {
   using TL = Tile<VT_V, BN, STAGES>;
-  constexpr int LDS = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
+  constexpr int LDS = TL::STAGES * TL::STAGE_BYTES > epilogue_lds_bytes(BN)
                           ? TL::STAGES * TL::STAGE_BYTES
-                          : 4 * BN * (int)sizeof(GroupStat);
+                          : epilogue_lds_bytes(BN);
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
   static bool attr_set = false;
   if (!attr_set) {
@@ -726,9 +744,9 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
                                 const uint16_t* whh, const float* vgate, int vdiv, float* pre,
                                 int NQ, float* q_out, hipStream_t stream, const float* eoff) {
   using TL = Tile<VT_V, BN, STAGES>;
-  constexpr int LV = TL::STAGES * TL::STAGE_BYTES > 4 * BN * (int)sizeof(GroupStat)
+  constexpr int LV = TL::STAGES * TL::STAGE_BYTES > epilogue_lds_bytes(BN)
                          ? TL::STAGES * TL::STAGE_BYTES
-                         : 4 * BN * (int)sizeof(GroupStat);
+                         : epilogue_lds_bytes(BN);
   constexpr int LDS = LV > LT::LDS_BYTES ? LV : LT::LDS_BYTES;
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
   const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H, NQ) + 7) / 8 * 8 : 0;
