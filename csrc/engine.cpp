@@ -419,6 +419,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 //            the loop on one GPU, concurrently with the loop under data
 //            parallelism so the vocab head's all-reduce (comm_stream waits
 //            on it) hides under the loop.
+static bool ds_ready_pre(const at::Tensor& ds_bias) {
+  return ds_bias.defined() && ds_bias.numel() > 0;
+}
+
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -499,7 +503,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor buf = logits16.scalar_type() == at::kBFloat16 ? logits16 : logits16.view(at::kBFloat16);
   at::Tensor Ev = buf.view({NR, ldl}).narrow(1, 0, V);  // E (or dense dS), K = V columns
   at::Tensor hd2 = hdrop_all.view({NR, H});
-  at::Tensor dHd = at::empty({NR, H}, f32);
+  // DHD16 (A/B): the vocab head's X = E' W as bf16 GEMM output
+  static const bool dhd16_env = [] {
+    const char* e = getenv("CSTCAP_EXP_DHD16");
+    return e != nullptr && e[0] == '1';
+  }();
+  const bool dhd16 = dhd16_env && !ds_ready_pre(ds_bias);
+  at::Tensor dHd = at::empty({NR, H}, dhd16 ? wx.options() : f32);
   const bool early = out_wlog.defined() && out_wlog.numel() > 0;
   if (early) {
     TORCH_CHECK(out_wlog.scalar_type() == at::kFloat && out_wlog.is_contiguous() &&
@@ -559,7 +569,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // X = E' W; the reverse loop reads alpha X (row scales at load), so the
     // loop starts right after the GEMM and the scaled Hd rows of the dW GEMM
     // are formed under it
-    at::mm_out(dHd, Ev, wlog, at::kFloat);
+    if (dhd16)
+      at::mm_out(dHd, Ev, wlog);
+    else
+      at::mm_out(dHd, Ev, wlog, at::kFloat);
     (void)hipEventRecord(ev_dhd, side.stream());
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
@@ -621,12 +634,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // top layer first: its h gradient comes from the vocab head (dHd, with the
     // vocab dropout mask); layer l < top gets dG_{l+1, t} W_ih_{l+1} through
     // the inter-layer dropout mask of layer l's output
+    auto dhd_f = [&](int64_t tt) -> const float* {
+      return dhd16 ? nullptr : dHd.data_ptr<float>() + tt * R * H;
+    };
+    auto dhd_h = [&](int64_t tt) -> const uint16_t* {
+      return dhd16 ? reinterpret_cast<const uint16_t*>(dHd.data_ptr()) + tt * R * H : nullptr;
+    };
     for (int64_t l = NL - 1; l >= 1; --l) {
-      const float* dh_in = dHd.data_ptr<float>() + t * R * H;
+      const float* dh_in = dhd_f(t);
+      const uint16_t* dh_in16 = dhd_h(t);
       const float* dh_sc = dh_scale_t(t);
       if (l < NL - 1) {
         at::mm_out(dX_up, dG_up[l + 1][t], upw(l + 1, 0).narrow(1, 0, H), at::kFloat);
         dh_in = dX_up.data_ptr<float>();
+        dh_in16 = nullptr;
         dh_sc = nullptr;
       }
       launch_lstm_step_bwd(
@@ -635,13 +656,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
           dc_up[l].data_ptr<float>(), reinterpret_cast<const uint16_t*>(upw(l, 3)[t].data_ptr()),
           upw(l, 2)[t].data_ptr<float>(), t > 0 ? upw(l, 2)[t - 1].data_ptr<float>() : nullptr,
           (int)R, (int)H, (float)drop_p, RNG, key(l, t),
-          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell, dh_sc);
+          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell, dh_sc,
+          dh_in16);
     }
-    const float* dh0_in = dHd.data_ptr<float>() + t * R * H;
+    const float* dh0_in = dhd_f(t);
+    const uint16_t* dh0_in16 = dhd_h(t);
     const float* dh0_sc = dh_scale_t(t);
     if (NL > 1) {
       at::mm_out(dX_up, dG_up[1][t], upw(1, 0).narrow(1, 0, H), at::kFloat);
       dh0_in = dX_up.data_ptr<float>();
+      dh0_in16 = nullptr;
       dh0_sc = nullptr;
     }
     launch_lstm_step_bwd(
@@ -651,7 +675,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         c_all[t].data_ptr<float>(),
         t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
         (int)R, (int)H, (float)drop_p, RNG, key(0, t),
-        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc);
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc,
+        dh0_in16);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
@@ -716,11 +741,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   if (!has_att) {
     dvg = dG_all.sum(0, false, at::kFloat);  // (R, 4H), sum over time
   } else {
-    // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r]: one batched GEMM
-    // per (step, video), K = rows per video, summed over steps
-    at::Tensor al = a_alpha.to(at::kBFloat16).view({n_steps * Bv, vdiv, C}).transpose(1, 2);
-    at::Tensor dgv = dG_all.view({n_steps * Bv, vdiv, KD}).narrow(2, 0, H4);
-    at::Tensor dGv = at::bmm(al, dgv, at::kFloat).view({n_steps, Bv, C, H4}).sum(0);
+    // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r] (kernels/attention.hip:
+    // one pass over the bf16 dG rows, partials per step chunk)
+    at::Tensor dGv;
+    if (C <= 8) {
+      at::Tensor part = at::empty({att_dgv_chunks((int)n_steps), Bv, C, H4}, f32);
+      launch_att_dgv(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)KD,
+                     a_alpha.data_ptr<float>(), (int)n_steps, (int)R, (int)Bv, (int)vdiv, (int)C,
+                     (int)H4, part.data_ptr<float>(), st);
+      dGv = part.sum(0);
+    } else {  // one batched GEMM per (step, video), K = rows per video
+      at::Tensor al = a_alpha.to(at::kBFloat16).view({n_steps * Bv, vdiv, C}).transpose(1, 2);
+      at::Tensor dgv = dG_all.view({n_steps * Bv, vdiv, KD}).narrow(2, 0, H4);
+      dGv = at::bmm(al, dgv, at::kFloat).view({n_steps, Bv, C, H4}).sum(0);
+    }
     const int64_t ng = att_groups((int)vdiv);
     res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0).view_as(a_wa),
            dba_part.sum(0).view({NWA}), dWq};

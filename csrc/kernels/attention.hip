@@ -274,6 +274,71 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
 
 int att_groups(int vdiv, int rpw) { return (vdiv + rpw - 1) / rpw; }
 
+// Video-gate gradient of the per-frame gate tables (after the reverse loop):
+//     dGv[b, c, :] = sum over steps t and rows r of video b of alpha[t, r, c] dG_t[r, 0:G4].
+// A batched GEMM over (step, video) pairs has K = 20 rows and 1,792 batch
+// entries (3 TFLOP/s, plus a 117 MB fp32 intermediate summed over steps);
+// here block (b, step chunk) streams its rows' bf16 dG once (16 bytes per
+// thread and row, coalesced), the row's C attention weights are uniform
+// across the block, and each thread keeps C x 8 fp32 sums; one partial per
+// step chunk (summed by the caller: deterministic, no atomics).
+constexpr int DGV_TCHUNK = 4;
+template <int MAXC>
+__global__ __launch_bounds__(256) void att_dgv_kernel(const uint16_t* __restrict__ dG, int ldg,
+                                                      const float* __restrict__ alpha, int n_steps,
+                                                      int R, int Bv, int vdiv, int C, int G4,
+                                                      float* __restrict__ part) {
+  const int b = blockIdx.x, tc = blockIdx.y;
+  const int t0 = tc * DGV_TCHUNK, t1 = min(n_steps, t0 + DGV_TCHUNK);
+  for (int cg = threadIdx.x; 8 * cg < G4; cg += 256) {
+    float acc[MAXC][8];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[c][k] = 0.f;
+    for (int t = t0; t < t1; ++t) {
+#pragma unroll 4
+      for (int rr = 0; rr < vdiv; ++rr) {
+        const int64_t row = (int64_t)t * R + (int64_t)b * vdiv + rr;
+        const uint4 g = *reinterpret_cast<const uint4*>(dG + row * ldg + 8 * cg);
+        const uint32_t w[4] = {g.x, g.y, g.z, g.w};
+        float d[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[2 * k] = bf2f(w[k] & 0xffff);
+          d[2 * k + 1] = bf2f(w[k] >> 16);
+        }
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+          const float al = c < C ? alpha[row * C + c] : 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[c][k] += al * d[k];
+        }
+      }
+    }
+    float* out = part + ((int64_t)tc * Bv + b) * C * G4 + 8 * cg;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < C) {
+        reinterpret_cast<float4*>(out + (int64_t)c * G4)[0] =
+            make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+        reinterpret_cast<float4*>(out + (int64_t)c * G4)[1] =
+            make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+      }
+  }
+}
+
+int att_dgv_chunks(int n_steps) { return (n_steps + DGV_TCHUNK - 1) / DGV_TCHUNK; }
+
+void launch_att_dgv(const uint16_t* dG, int ldg, const float* alpha, int n_steps, int R, int Bv,
+                    int vdiv, int C, int G4, float* part, hipStream_t stream) {
+  if (C > 8 || G4 % 8 != 0 || ldg % 8 != 0 || Bv * vdiv != R)
+    throw std::runtime_error("att_dgv: C <= 8, G4 and ldg multiples of 8, R = Bv * vdiv");
+  hipLaunchKernelGGL(att_dgv_kernel<8>, dim3(Bv, att_dgv_chunks(n_steps)), dim3(256), 0, stream,
+                     dG, ldg, alpha, n_steps, R, Bv, vdiv, C, G4, part);
+  post_launch("att_dgv_kernel", stream);
+}
+
 template <int RPW>
 static void launch_att_fwd_t(const float* gv, const float* pre, const float* q,
                              const int* q_rowmap, const float* wa, const float* ba, int Bv,

@@ -205,22 +205,18 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
           }
         }
     } else if (logits16 != nullptr && r < R && !(flags & VF_EXP)) {
-      uint16_t* dst = logits16 + (int64_t)r * ldl;
+      // fp16 logits: staged through LDS like the exp store (written below);
+      // entries past V hold -inf and stay inside the row stride ldl
+      uint16_t* et = reinterpret_cast<uint16_t*>(lds + exp_stage_off(BN)) + row_l * EXP_STAGE_LD;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int v = vb + 32 * i + 8 * q;
-          if (v + 4 <= V) {
-            uint2 pk;
-            pk.x = (uint32_t)f2h(x[i][4 * q]) | ((uint32_t)f2h(x[i][4 * q + 1]) << 16);
-            pk.y = (uint32_t)f2h(x[i][4 * q + 2]) | ((uint32_t)f2h(x[i][4 * q + 3]) << 16);
-            *reinterpret_cast<uint2*>(dst + v) = pk;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (v + e < V) dst[v + e] = f2h(x[i][4 * q + e]);
-          }
+          const int vl = vb - v0 + 32 * i + 8 * q;
+          uint2 pk;
+          pk.x = (uint32_t)f2h(x[i][4 * q]) | ((uint32_t)f2h(x[i][4 * q + 1]) << 16);
+          pk.y = (uint32_t)f2h(x[i][4 * q + 2]) | ((uint32_t)f2h(x[i][4 * q + 3]) << 16);
+          *reinterpret_cast<uint2*>(et + vl) = pk;
         }
     }
 
@@ -368,8 +364,9 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       part[(int64_t)vt * R + r] = p;
     }
   }
-  if ((flags & VF_EXP) && logits16 != nullptr) {
-    // the staged exp-store tile (written before the barrier above): 16 bytes
+  if (logits16 != nullptr && !(flags & VF_SAVE_F32)) {
+    // the staged 16-bit tile (exp store or fp16 logits, written before the
+    // barrier above): 16 bytes
     // per thread and pass, 16 threads per 256-byte row segment; columns past
     // V hold 0 (bias -inf) and are written up to the row stride ldl
     const uint16_t* et = reinterpret_cast<const uint16_t*>(lds + exp_stage_off(BN));

@@ -146,13 +146,19 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                          const float* dh_scale = nullptr);  // dh_logit row scales (nullable)
+                          const float* dh_scale = nullptr,   // dh_logit row scales (nullable)
+                          const uint16_t* dh16 = nullptr);   // bf16 dh_logit instead (nullable)
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal
 // attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
 // rows of one video per attention-backward workgroup (2 or 4; C > 8: 4)
 constexpr int ATT_BWD_RPW = 4;
 int att_groups(int vdiv, int rpw = ATT_BWD_RPW);  // backward workgroups per video
+// dGv partials (att_dgv_chunks(n_steps), Bv, C, G4) fp32 of sum_{t, r in b}
+// alpha[t, r, c] dG[t, r, 0:G4] (dG rows bf16, stride ldg; alpha (n, R, C))
+int att_dgv_chunks(int n_steps);
+void launch_att_dgv(const uint16_t* dG, int ldg, const float* alpha, int n_steps, int R, int Bv,
+                    int vdiv, int C, int G4, float* part, hipStream_t stream);
 // vg_out[r] = sum_c alpha_rc Gv[b, c]  (+= when accumulate: adds into pre)
 // rows of one video per attention-forward workgroup: 0 = by the rows per
 // video (4 at >= 4, e.g. the rollout's 20; 1 for the one-row greedy baseline:
