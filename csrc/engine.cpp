@@ -419,10 +419,6 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 //            the loop on one GPU, concurrently with the loop under data
 //            parallelism so the vocab head's all-reduce (comm_stream waits
 //            on it) hides under the loop.
-static bool ds_ready_pre(const at::Tensor& ds_bias) {
-  return ds_bias.defined() && ds_bias.numel() > 0;
-}
-
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -503,13 +499,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor buf = logits16.scalar_type() == at::kBFloat16 ? logits16 : logits16.view(at::kBFloat16);
   at::Tensor Ev = buf.view({NR, ldl}).narrow(1, 0, V);  // E (or dense dS), K = V columns
   at::Tensor hd2 = hdrop_all.view({NR, H});
-  // DHD16 (A/B): the vocab head's X = E' W as bf16 GEMM output
-  static const bool dhd16_env = [] {
-    const char* e = getenv("CSTCAP_EXP_DHD16");
-    return e != nullptr && e[0] == '1';
-  }();
-  const bool dhd16 = dhd16_env && !ds_ready_pre(ds_bias);
-  at::Tensor dHd = at::empty({NR, H}, dhd16 ? wx.options() : f32);
+  at::Tensor dHd = at::empty({NR, H}, f32);
   const bool early = out_wlog.defined() && out_wlog.numel() > 0;
   if (early) {
     TORCH_CHECK(out_wlog.scalar_type() == at::kFloat && out_wlog.is_contiguous() &&
@@ -569,10 +559,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // X = E' W; the reverse loop reads alpha X (row scales at load), so the
     // loop starts right after the GEMM and the scaled Hd rows of the dW GEMM
     // are formed under it
-    if (dhd16)
-      at::mm_out(dHd, Ev, wlog);
-    else
-      at::mm_out(dHd, Ev, wlog, at::kFloat);
+    at::mm_out(dHd, Ev, wlog, at::kFloat);
     (void)hipEventRecord(ev_dhd, side.stream());
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
@@ -634,20 +621,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // top layer first: its h gradient comes from the vocab head (dHd, with the
     // vocab dropout mask); layer l < top gets dG_{l+1, t} W_ih_{l+1} through
     // the inter-layer dropout mask of layer l's output
-    auto dhd_f = [&](int64_t tt) -> const float* {
-      return dhd16 ? nullptr : dHd.data_ptr<float>() + tt * R * H;
-    };
-    auto dhd_h = [&](int64_t tt) -> const uint16_t* {
-      return dhd16 ? reinterpret_cast<const uint16_t*>(dHd.data_ptr()) + tt * R * H : nullptr;
-    };
     for (int64_t l = NL - 1; l >= 1; --l) {
-      const float* dh_in = dhd_f(t);
-      const uint16_t* dh_in16 = dhd_h(t);
+      const float* dh_in = dHd.data_ptr<float>() + t * R * H;
       const float* dh_sc = dh_scale_t(t);
       if (l < NL - 1) {
         at::mm_out(dX_up, dG_up[l + 1][t], upw(l + 1, 0).narrow(1, 0, H), at::kFloat);
         dh_in = dX_up.data_ptr<float>();
-        dh_in16 = nullptr;
         dh_sc = nullptr;
       }
       launch_lstm_step_bwd(
@@ -656,16 +635,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
           dc_up[l].data_ptr<float>(), reinterpret_cast<const uint16_t*>(upw(l, 3)[t].data_ptr()),
           upw(l, 2)[t].data_ptr<float>(), t > 0 ? upw(l, 2)[t - 1].data_ptr<float>() : nullptr,
           (int)R, (int)H, (float)drop_p, RNG, key(l, t),
-          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell, dh_sc,
-          dh_in16);
+          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell, dh_sc);
     }
-    const float* dh0_in = dhd_f(t);
-    const uint16_t* dh0_in16 = dhd_h(t);
+    const float* dh0_in = dHd.data_ptr<float>() + t * R * H;
     const float* dh0_sc = dh_scale_t(t);
     if (NL > 1) {
       at::mm_out(dX_up, dG_up[1][t], upw(1, 0).narrow(1, 0, H), at::kFloat);
       dh0_in = dX_up.data_ptr<float>();
-      dh0_in16 = nullptr;
       dh0_sc = nullptr;
     }
     launch_lstm_step_bwd(
@@ -675,8 +651,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         c_all[t].data_ptr<float>(),
         t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
         (int)R, (int)H, (float)drop_p, RNG, key(0, t),
-        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc,
-        dh0_in16);
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc);
     if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),

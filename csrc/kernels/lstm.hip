@@ -153,7 +153,6 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
                                                   const float* __restrict__ c_prev,
                                                   const float* __restrict__ dc_carry,
                                                   const float* __restrict__ dh_logit,
-                                                  const uint16_t* __restrict__ dh16,
                                                   const float* __restrict__ dh_scale,
                                                   uint2* pg, float* pc, float* pcp, float* pdc,
                                                   float* pdl) {
@@ -166,7 +165,7 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
     pc[i] = c_t[o];
     pcp[i] = c_prev ? c_prev[o] : 0.f;
     pdc[i] = dc_carry[o];
-    pdl[i] = (dh16 != nullptr ? bf2f(dh16[o]) : dh_logit[o]) * (dh_scale ? dh_scale[r] : 1.f);
+    pdl[i] = dh_logit[o] * (dh_scale ? dh_scale[r] : 1.f);
   }
 }
 
@@ -177,7 +176,7 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p,
     const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int cell,
-    const float* __restrict__ dh_scale, const uint16_t* __restrict__ dh16) {
+    const float* __restrict__ dh_scale) {
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
@@ -194,7 +193,7 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
   uint2 pg[RPT];
   float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
   // the epilogue operands' latency hides under the GEMM
-  lstm_bwd_load_epi<BM, GROUPS>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, dh16,
+  lstm_bwd_load_epi<BM, GROUPS>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit,
                                 dh_scale, pg, pc, pcp, pdc, pdl);
 
   f32x16 acc[TL::TM][TL::TN];
@@ -262,8 +261,7 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
                                    const float* dh_logit, float* dc_carry, const uint16_t* gates,
                                    const float* c_t, const float* c_prev, int R, int H,
                                    float drop_p, const uint32_t* rng, int step, uint16_t* dG,
-                                   int KD, hipStream_t stream, int cell, const float* dh_scale,
-                                   const uint16_t* dh16) {
+                                   int KD, hipStream_t stream, int cell, const float* dh_scale) {
   constexpr int BM = 64;
   using TL = Tile<BM, 64, STAGES>;
   constexpr int LDS = GROUPS * TL::STAGES * TL::STAGE_BYTES > GROUPS * BM * TL::CSTRIDE * 4
@@ -278,7 +276,7 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
   const int n = (H / 64) * ((R + BM - 1) / BM);
   hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS>), dim3(n),
                      dim3(256 * GROUPS), LDS, stream, dg_next, whhT, dh_logit, dc_carry, gates,
-                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale, dh16);
+                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale);
   post_launch("lstm_step_bwd_kernel", stream);
 }
 
@@ -286,16 +284,16 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                          const float* dh_scale, const uint16_t* dh16) {
+                          const float* dh_scale) {
   // two K groups per block when the K-tiles split evenly
   // (measured per step: 1 group 4.66 ms, 2 groups 4.54 ms, 4 groups with 2
   // LDS stages each 4.51 vs 4.47 ms for 2 groups on another box)
   if ((KD / 64) % 2 == 0)
     launch_lstm_step_bwd_g<2>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, dh16);
+                              drop_p, rng, step, dG, KD, stream, cell, dh_scale);
   else
     launch_lstm_step_bwd_g<1>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, dh16);
+                              drop_p, rng, step, dG, KD, stream, cell, dh_scale);
 }
 
 // 128-row tiles x 64 packed gate columns, 3 LDS stages (72 KB, 2 blocks per CU)

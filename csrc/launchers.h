@@ -146,8 +146,7 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                          const float* dh_scale = nullptr,   // dh_logit row scales (nullable)
-                          const uint16_t* dh16 = nullptr);   // bf16 dh_logit instead (nullable)
+                          const float* dh_scale = nullptr);  // dh_logit row scales (nullable)
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal
 // attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
