@@ -57,8 +57,11 @@ __global__ __launch_bounds__(256) void token_group_sum_kernel(
   const int n = hi - lo;
   if (n <= 0) return;  // the chunk lies inside a short group begun earlier
   CST_DCHECK(n <= GS_SPAN);
+  // s_tok carries the long-group flag in bit 31 (so the flush branch reads no
+  // global count: a vector load there would wait for every row load before it)
   for (int i = tid; i < n; i += 256) {
-    s_tok[i] = stok[lo + i];
+    const int t = stok[lo + i];
+    s_tok[i] = t | (count[t] > GS_LONG ? (int)0x80000000u : 0);
     s_row[i] = srow[lo + i];
   }
   __syncthreads();
@@ -68,8 +71,9 @@ __global__ __launch_bounds__(256) void token_group_sum_kernel(
   for (int j = 0; j < MAXJ; ++j)
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
-  auto flush = [&](int v) {
-    if (count[v] <= GS_LONG) {  // whole group in this block: final value
+  auto flush = [&](int tf) {
+    const int v = tf & 0x7fffffff;
+    if (tf >= 0) {  // whole group in this block: final value
 #pragma unroll
       for (int j = 0; j < MAXJ; ++j) {
         const int c = tid + 256 * j;
@@ -96,20 +100,29 @@ __global__ __launch_bounds__(256) void token_group_sum_kernel(
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
   };
+  // Double-buffered batches of GS_PF rows: the next batch's loads are issued
+  // before the current batch is summed, every load unconditional (row index
+  // clamped to the last owned entry, column chunk clamped to the last one,
+  // surplus values masked at the add), and compiler barriers keep the loads
+  // where they are.  (With conditional refills the compiler could not count
+  // the loads issued after a buffer's and waited vmcnt(0) at every row, and it
+  // sank the prefetches next to their uses: the loop was serialised on memory
+  // latency, 365 us per step for a 147 MB pass.)
   auto load = [&](int i, uint4 (&r)[MAXJ]) {
-    const uint16_t* row = x + (int64_t)s_row[i] * ld;
+    const uint16_t* row = x + (int64_t)s_row[min(i, n - 1)] * ld;
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
-      const int c = tid + 256 * j;
-      r[j] = c < nch ? *reinterpret_cast<const uint4*>(row + 8 * c) : make_uint4(0, 0, 0, 0);
-    }
+    for (int j = 0; j < MAXJ; ++j)
+      r[j] = *reinterpret_cast<const uint4*>(row + 8 * min(tid + 256 * j, nch - 1));
   };
-  uint4 buf[GS_PF][MAXJ];
+  uint4 cb[GS_PF][MAXJ], nb[GS_PF][MAXJ];
 #pragma unroll
-  for (int p = 0; p < GS_PF; ++p)
-    if (p < n) load(p, buf[p]);
+  for (int p = 0; p < GS_PF; ++p) load(p, cb[p]);
   int cur = s_tok[0];
   for (int i0 = 0; i0 < n; i0 += GS_PF) {
+    const bool more = i0 + GS_PF < n;
+#pragma unroll
+    for (int p = 0; p < GS_PF; ++p) load(i0 + GS_PF + p, nb[p]);  // clamped past n
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int p = 0; p < GS_PF; ++p) {
       const int i = i0 + p;
@@ -121,16 +134,22 @@ __global__ __launch_bounds__(256) void token_group_sum_kernel(
         }
 #pragma unroll
         for (int j = 0; j < MAXJ; ++j) {
-          const uint32_t w[4] = {buf[p][j].x, buf[p][j].y, buf[p][j].z, buf[p][j].w};
+          const bool live = tid + 256 * j < nch;
+          const uint32_t w[4] = {cb[p][j].x, cb[p][j].y, cb[p][j].z, cb[p][j].w};
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            acc[j][2 * k] += bf2f(w[k] & 0xffff);
-            acc[j][2 * k + 1] += bf2f(w[k] >> 16);
+            acc[j][2 * k] += live ? bf2f(w[k] & 0xffff) : 0.f;
+            acc[j][2 * k + 1] += live ? bf2f(w[k] >> 16) : 0.f;
           }
         }
-        if (i + GS_PF < n) load(i + GS_PF, buf[p]);
       }
     }
+    asm volatile("" ::: "memory");
+    if (!more) break;
+#pragma unroll
+    for (int p = 0; p < GS_PF; ++p)
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) cb[p][j] = nb[p][j];
   }
   flush(cur);
 }
