@@ -515,10 +515,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     hs = at::empty({NR, H}, wx.options());
     cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
   }
-  auto launch_colsum = [&]() {
+  auto launch_colsum = [&](hipStream_t s) {
     launch_vgrad_colsum(reinterpret_cast<const uint16_t*>(buf.data_ptr()), ldl, (int)V, NR,
                         alpha.data_ptr<float>(), cs_part.data_ptr<float>(),
-                        dblog.data_ptr<float>(), side.stream());
+                        dblog.data_ptr<float>(), s);
   };
   // 3. dW_logit and the bias gradient: exp store: dW = E'^T (alpha Hd), db =
   // sum_r alpha_r E'_r; dense dS: dW = dS^T Hd, db = ds_bias.  Neither needs
@@ -532,11 +532,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   auto dw_gemm = [&]() {  // (current stream: side)
     at::mm_out(dWlog, Ev.t(), ds_ready ? hd2 : hs, at::kFloat);
   };
-  auto db_sums = [&]() {
+  auto db_sums = [&](hipStream_t s) {  // (current stream: s)
     if (ds_ready)
       dblog.copy_(ds_bias);
     else
-      launch_colsum();
+      launch_colsum(s);
   };
   auto dw_done = [&]() {
     (void)hipEventRecord(ev_done, side.stream());
@@ -567,7 +567,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                         reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
     if (vh_sched == 2) {
       dw_gemm();
-      db_sums();
+      db_sums(side.stream());
       dw_done();
     }
   }
@@ -661,28 +661,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      dba_part.data_ptr<float>(), st, per_frame);
   }
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
-  if (vh_sched == 0) {
-    (void)hipEventRecord(ev_ready, st);  // reverse loop done
-    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
-    c10::hip::HIPStreamGuard guard(side);
-    dw_gemm();
-    db_sums();
-    dw_done();
-  }
-
-  // 5. input-token gradients through the per-token sums S[v] = sum of the dG
-  //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
-  //    input-weight gradient S^T emb -- GEMMs over V rows instead of n*R
   at::Tensor dG2 = dGx.narrow(1, 0, H4);
-  launch_token_group_sum(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)H4, KD,
-                         stok.data_ptr<int>(), srow.data_ptr<int>(), (int)NR,
-                         sort_ws.data_ptr<int>(), (int)V,
-                         reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
-  at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   // 6. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
   //    reductions run as batched GEMMs over groups of steps (many more output
   //    tiles in flight than one K = 35k GEMM), summed afterwards.
   at::Tensor dWx = at::empty({H4, E + H}, f32);
+  at::Tensor dWq = has_att ? at::empty({A, H}, f32) : at::Tensor();
   auto grouped_wgrad = [&](at::Tensor a_rows, at::Tensor b_rows, int64_t nsteps) {
     int64_t G = 1;  // steps per group: largest divisor <= 7
     for (int64_t g = 7; g >= 1; --g)
@@ -692,25 +676,49 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     at::Tensor b = b_rows.reshape({nc, G * R, b_rows.size(1)});
     return at::bmm(a, b, at::kFloat).sum(0);
   };
-  at::Tensor dWq;
+  // recurrent columns dW_hh = sum_t dG_t^T h_{t-1} (+ dG_0^T h0 with an
+  // initial state); with attention the extra rows of [dG | dq]^T h_prev are dW_q
+  auto whh_grad = [&]() {
+    if (n_steps > 1) {
+      at::Tensor wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
+                                    h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
+                                    n_steps - 1);
+      dWx.narrow(1, E, H).copy_(wh.narrow(0, 0, H4));
+      if (has_att) dWq.copy_(wh.narrow(0, H4, A));
+    } else {
+      dWx.narrow(1, E, H).zero_();
+      if (has_att) dWq.zero_();
+    }
+    if (has_s0) dWx.narrow(1, E, H).add_(at::mm(dG2.narrow(0, 0, R).t(), state0[0], at::kFloat));
+  };
+  // One GPU: after the loop the main stream's chain (per-token sums, the
+  // input-token GEMMs) outlasts the side stream's dW_logit GEMM + bias column
+  // sums, so the recurrent-weight GEMMs join the side stream.  (Outputs
+  // written there were allocated on the main stream, which joins the side
+  // stream before returning.)
+  if (vh_sched == 0) {
+    (void)hipEventRecord(ev_ready, st);  // reverse loop done
+    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
+    c10::hip::HIPStreamGuard guard(side);
+    dw_gemm();
+    db_sums(side.stream());
+    whh_grad();
+    dw_done();
+  }
+
+  // 5. input-token gradients through the per-token sums S[v] = sum of the dG
+  //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
+  //    input-weight gradient S^T emb -- GEMMs over V rows instead of n*R
+  launch_token_group_sum(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)H4, KD,
+                         stok.data_ptr<int>(), srow.data_ptr<int>(), (int)NR,
+                         sort_ws.data_ptr<int>(), (int)V,
+                         reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
+  at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   dWx.narrow(1, 0, E).copy_(at::mm(S_tok.t(), emb, at::kFloat));
-  if (n_steps > 1) {
-    // with attention the extra rows of [dG | dq]^T h_prev are dW_q
-    at::Tensor wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
-                                  h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
-                                  n_steps - 1);
-    dWx.narrow(1, E, H).copy_(wh.narrow(0, 0, H4));
-    if (has_att) dWq = wh.narrow(0, H4, A).contiguous();
-  } else {
-    dWx.narrow(1, E, H).zero_();
-    if (has_att) dWq = at::zeros({A, H}, f32);
-  }
+  if (vh_sched != 0) whh_grad();
   at::Tensor dh0;
-  if (has_s0) {  // step 0's recurrent input h0: dW_hh += dG_0^T h0, dh0 = dG_0 W_hh
-    at::Tensor dG0 = dG2.narrow(0, 0, R);
-    dWx.narrow(1, E, H).add_(at::mm(dG0.t(), state0[0], at::kFloat));
-    dh0 = at::mm(dG0, wx.narrow(1, E, H), at::kFloat);
-  }
+  if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
+    dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);
   at::Tensor dvg;
   std::vector<at::Tensor> res;
   if (!has_att) {
