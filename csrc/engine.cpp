@@ -693,7 +693,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   };
   // One GPU: after the loop the main stream's chain (per-token sums, the
   // input-token GEMMs) outlasts the side stream's dW_logit GEMM + bias column
-  // sums, so the recurrent-weight GEMMs join the side stream.  (Outputs
+  // sums, so the recurrent-weight GEMMs join the side stream (with the
+  // split-K S^T emb below: 3.775-3.799 vs 3.832-3.846 ms per step,
+  // interleaved on one box, profiles/r2/ab_whh_side_splitk.txt).  (Outputs
   // written there were allocated on the main stream, which joins the side
   // stream before returning.)
   if (vh_sched == 0) {
@@ -714,7 +716,24 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
-  dWx.narrow(1, 0, E).copy_(at::mm(S_tok.t(), emb, at::kFloat));
+  // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
+  // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134
+  // TFLOP/s at V = 10,509); a split-K batch over the largest divisor of V up to
+  // 8 multiplies the tiles in flight, the partial products summed afterwards
+  // (49 us + a ~20 us sum, profiles/r2/kernel_summary_r2_v19.txt).
+  {
+    int64_t nk = 1;
+    for (int64_t g = 8; g >= 2; --g)
+      if (V % g == 0 && V / g >= 512) { nk = g; break; }
+    at::Tensor dWie = dWx.narrow(1, 0, E);
+    if (nk > 1 && emb.is_contiguous())
+      at::sum_out(dWie,
+                  at::bmm(S_tok.view({nk, V / nk, H4}).transpose(1, 2), emb.view({nk, V / nk, E}),
+                          at::kFloat),
+                  0);
+    else
+      dWie.copy_(at::mm(S_tok.t(), emb, at::kFloat));
+  }
   if (vh_sched != 0) whh_grad();
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh

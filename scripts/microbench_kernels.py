@@ -3,7 +3,8 @@
 vocab_fwd at the rollout shape (R = 1280 rows) and the greedy shape (R = 64),
 with the epilogue pieces switched on one at a time:
   mainloop = GEMM only; stats = max/LSE (+target); sample; sample+save
-  (fp16 logits for the backward); argmax.
+  (fp16 logits for the backward); argmax.  Also: token sort, per-token
+gate-gradient sums (TGS=1), bias column sums (CS=1), attention (ATT=1).
 VARIANTS="0 1 2 ..." times other <BN, STAGES, OCC> shapes of the vocab kernel
 (launch_vocab_fwd_variant in csrc/kernels/vocab.hip).
 """
@@ -36,6 +37,21 @@ for R in (1280, 64):
             res['v%d_R%d_%s' % (var, R, name)] = round(us, 2)
 toks = torch.randint(0, V, (28 * 1280,), device=dev)
 res['token_sort_us'] = round(C.token_sort_bench(toks, V, 50), 2)
+if os.environ.get('TGS', '1') == '1':  # per-token gate-gradient sums, alone on the GPU
+    x = torch.randn(28 * 1280, 4 * H, device=dev).bfloat16()
+    tk = toks.clone()
+    tk[:1280] = 0  # step 0: every row's input is BOS (one long group)
+    for _ in range(3):
+        C.token_group_sum(x, tk, V)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(20):
+        C.token_group_sum(x, tk, V)
+    ev1.record()
+    torch.cuda.synchronize()
+    us = ev0.elapsed_time(ev1) * 1e3 / 20
+    res['token_group_sum_op_us'] = round(us, 1)  # sort + sums + finalize
+    res['token_group_sum_read_TBps'] = round(x.numel() * 2 / us / 1e6, 2)
 if os.environ.get('CS', '1') == '1':  # bias-gradient column sums over the exp store
     n, R = 28, 1280
     ldl = (V + 63) // 64 * 64
