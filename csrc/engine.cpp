@@ -761,6 +761,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0).view_as(a_wa),
            dba_part.sum(0).view({NWA}), dWq};
   }
+  // (The bias column sums at the end of the main chain, which ends ~0.3 ms
+  // before the side stream's in step_timeline_r2_v20.txt, measured slower:
+  // 3.86-3.88 vs 3.76-3.86 ms, they contend with the dW_logit GEMM;
+  // profiles/r2/ab_colsum_main.txt.)
   // join the side stream (dW_logit): every tensor it touched was allocated
   // on the main stream and is released after this point
   (void)hipStreamWaitEvent(st, ev_done, 0);
