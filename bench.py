@@ -231,6 +231,11 @@ def main():
                    'grad_wire': a.grad_wire,
                    'temporal_attention_frames': a.num_chunks if a.num_chunks > 1 else None},
         'final_loss': loss, 'datagen_s': round(t_gen, 1),
+        # optimizer updates the NaN guard skipped (non-finite loss or gradient
+        # norm) over warmup + timed steps, all ranks agree (adam.hip)
+        'skipped_steps': int(trainer.optimizer.skipped().item()),
+        # exp-store rows the backward recomputed (LSE jump > 60 between steps)
+        'exp_fix_rows': int(engine.exp_fix_rows.item()) if engine is not None else None,
         'world_size_seen': ctx.world_size, 'backend': ctx.backend or 'none',
     }
     if phases:

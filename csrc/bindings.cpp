@@ -25,7 +25,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          int64_t comm_stream, std::vector<at::Tensor> att,
                                          at::Tensor out_emb, at::Tensor ds_bias, int64_t cell,
                                          std::vector<at::Tensor> state0,
-                                         std::vector<at::Tensor> up);
+                                         std::vector<at::Tensor> up, at::Tensor blog,
+                                         at::Tensor fix_total);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,
@@ -56,7 +57,8 @@ at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::stri
                        double log_ref_len, int64_t use_eos);
 at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
                           at::Tensor partials, at::Tensor scal, at::Tensor skip, at::Tensor hyper,
-                          double b1, double b2, double eps, double clip, at::Tensor shadow_meta,
+                          double b1, double b2, double eps, double clip, double gscale,
+                          int64_t phase, at::Tensor shadow_meta,
                           std::vector<at::Tensor> shadow_dst);
 void refresh_shadows(at::Tensor p, at::Tensor shadow_meta, std::vector<at::Tensor> shadow_dst);
 

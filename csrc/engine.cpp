@@ -429,7 +429,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          int64_t comm_stream, std::vector<at::Tensor> att,
                                          at::Tensor out_emb, at::Tensor ds_bias, int64_t cell,
                                          std::vector<at::Tensor> state0,
-                                         std::vector<at::Tensor> up) {
+                                         std::vector<at::Tensor> up, at::Tensor blog,
+                                         at::Tensor fix_total) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -547,14 +548,29 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   {
     c10::hip::HIPStreamGuard guard(side);
     if (!ds_ready) {  // alpha, one-hot terms folded into E (dS = diag(alpha) E')
+      // exp-store range guard: rows whose LSE jumped by > 60 since the previous
+      // step are listed and recomputed exactly (vocab_grad.hip vgrad_fix)
+      const bool guard = blog.defined() && blog.numel() == V;
+      at::Tensor fix = guard ? at::zeros({1 + NR}, i32) : at::Tensor();
       VGradRows va{(int)R, (int)n_steps, (int)T_sel, (int)H, (int)V, lse.data_ptr<float>(),
                    has_sel ? seq.data_ptr<int64_t>() : nullptr,
                    has_sel ? dg_sel.data_ptr<float>() : nullptr,
                    has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
                    has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                   has_xe ? dg_xe.size(1) : 0};
+                   has_xe ? dg_xe.size(1) : 0, guard ? fix.data_ptr<int>() : nullptr};
       launch_vgrad_onehot(va, reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl,
                           alpha.data_ptr<float>(), side.stream());
+      if (guard) {
+        TORCH_CHECK(blog.is_cuda() && blog.scalar_type() == at::kFloat && blog.is_contiguous(),
+                    "blog must be a contiguous fp32 GPU tensor");
+        TORCH_CHECK(!fix_total.defined() || fix_total.numel() == 0 ||
+                        (fix_total.is_cuda() && fix_total.scalar_type() == at::kInt),
+                    "fix_total must be an int32 GPU tensor");
+        launch_vgrad_fix(va, reinterpret_cast<const uint16_t*>(hd2.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
+                         reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl, alpha.data_ptr<float>(),
+                         ptr_or_null<int>(fix_total), side.stream());
+      }
     }
     // X = E' W; the reverse loop reads alpha X (row scales at load), so the
     // loop starts right after the GEMM and the scaled Hd rows of the dW GEMM
@@ -969,22 +985,31 @@ static ShadowSegs make_shadow_segs(const at::Tensor& meta, const std::vector<at:
   return ss;
 }
 
-// hyper (device fp32): [lr, step]; the caller increments step before the call
+// hyper (device fp32): [lr, step before, skipped, step after] (kernels/adam.hip).
+// phase: 0 = both passes; 1 = sum of squares only (the caller all-reduces the
+// partials of a sharded update before phase 2); 2 = update only.
 at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v,
                           at::Tensor partials, at::Tensor scal, at::Tensor skip, at::Tensor hyper,
-                          double b1, double b2, double eps, double clip, at::Tensor shadow_meta,
+                          double b1, double b2, double eps, double clip, double gscale,
+                          int64_t phase, at::Tensor shadow_meta,
                           std::vector<at::Tensor> shadow_dst) {
   check_cuda(p, "p");
+  for (auto* t : {&g, &m, &v}) {
+    check_cuda(*t, "adam operand");
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == p.numel(), "adam operand shape");
+  }
   TORCH_CHECK(partials.numel() >= 1024 && scal.numel() >= 2, "workspace too small");
-  TORCH_CHECK(hyper.is_cuda() && hyper.scalar_type() == at::kFloat && hyper.numel() >= 2,
-              "hyper must be fp32 [lr, step] on the GPU");
+  TORCH_CHECK(hyper.is_cuda() && hyper.scalar_type() == at::kFloat && hyper.numel() >= 4,
+              "hyper must be fp32 [lr, step, skipped, step after] on the GPU");
+  TORCH_CHECK(phase >= 0 && phase <= 2, "phase: 0 both, 1 sumsq, 2 update");
   const ShadowSegs ss = make_shadow_segs(shadow_meta, shadow_dst);
   for (int k = 0; k < ss.n; ++k)
     TORCH_CHECK(ss.s[k].off >= 0 && ss.s[k].off + ss.s[k].n <= p.numel(), "shadow range");
   launch_flat_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                    v.data_ptr<float>(), p.numel(), partials.data_ptr<float>(),
                    skip.data_ptr<bool>(), scal.data_ptr<float>(), hyper.data_ptr<float>(),
-                   (float)b1, (float)b2, (float)eps, (float)clip, ss, cur_stream());
+                   (float)b1, (float)b2, (float)eps, (float)clip, (float)gscale, (int)phase, ss,
+                   cur_stream());
   return scal.narrow(0, 0, 1).squeeze(0);
 }
 

@@ -12,10 +12,24 @@
 //           PyTorch's Adam update with the clipped gradient; an optional
 //           device-side skip flag (non-finite loss) turns the step into a
 //           no-op without a host round trip.
-// Learning rate and step count are read from device memory (hyper[0] = lr,
-// hyper[1] = step, already incremented), so the bias corrections of a
-// replayed HIP graph follow the live step count and an LR decay between
-// replays needs no re-capture.
+// Learning rate and step count live in device memory, so the bias
+// corrections of a replayed HIP graph follow the live step count and an LR
+// decay between replays needs no re-capture.  hyper = [lr, step at the start
+// of the update, skipped updates, step after the update]: the update pass
+// reads hyper[1] (every block) and block 0 writes hyper[3] (the step advances
+// only when the update is applied, as torch.optim.Adam's step does); the
+// next sum-of-squares pass commits hyper[3] -> hyper[1].
+//
+// NaN guard: the update is skipped when the caller's flag is set (non-finite
+// loss, possibly on another DP rank) OR when the global gradient norm is not
+// finite (an overflowing gradient with a finite loss, e.g. an exp-store
+// entry out of bf16 range: clip / inf = 0 and inf * 0 = NaN would otherwise
+// poison p, m, v for good).  Every DP rank reduces the same gradient, so they
+// skip together.  Skips are counted in hyper[2] (reported in the log line).
+//
+// gscale: the gradient buffer holds gscale^-1 times the gradient (the DP
+// all-reduce SUMS over N ranks; gscale = 1/N folds the average in here
+// instead of a separate pass over the buffer).
 //
 // The update pass also refreshes the bf16 shadow copies of the decoder
 // weights that the MFMA kernels read (ShadowSegs: vocab head, embedding, and
@@ -45,8 +59,11 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 
 __global__ __launch_bounds__(ADAM_THREADS) void adam_sumsq_kernel(const float* __restrict__ g,
                                                                    int64_t n,
-                                                                   float* __restrict__ partials) {
+                                                                   float* __restrict__ partials,
+                                                                   float* __restrict__ hyper) {
   __shared__ float sh[ADAM_THREADS / 64];
+  // commit the previous update's step count (no block of this pass reads it)
+  if (blockIdx.x == 0 && threadIdx.x == 0) hyper[1] = hyper[3];
   float acc = 0.f;
   const int64_t n4 = n >> 2;
   const float4* g4 = reinterpret_cast<const float4*>(g);
@@ -113,26 +130,31 @@ __device__ __forceinline__ void adam_one(float& p, float& m, float& v, float g, 
 __global__ __launch_bounds__(ADAM_THREADS) void adam_update_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, int64_t n, const float* __restrict__ partials, int nparts,
-    const bool* __restrict__ skip, float* __restrict__ scal, const float* __restrict__ hyper,
-    float b1, float b2, float eps, float clip, ShadowSegs ss) {
+    const bool* __restrict__ skip, float* __restrict__ scal, float* __restrict__ hyper,
+    float b1, float b2, float eps, float clip, float gscale, ShadowSegs ss) {
   __shared__ float sh[ADAM_THREADS / 64];
   __shared__ float s_coef;
-  const float t = hyper[1];
+  __shared__ int s_skip;
+  const float t0 = hyper[1], t = t0 + 1.f;
   const float lr_bc1 = hyper[0] / (1.f - powf(b1, t));
   const float inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(b2, t));
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += ADAM_THREADS) acc += partials[i];
   const float tot = block_sum(acc, sh);
   if (threadIdx.x == 0) {
-    const float norm = sqrtf(tot);
-    s_coef = fminf(1.f, clip / (norm + 1e-6f));
+    const float norm = sqrtf(tot) * gscale;
+    const bool bad = *skip || !isfinite(norm);
+    s_skip = bad;
+    s_coef = fminf(1.f, clip / (norm + 1e-6f)) * gscale;
     if (blockIdx.x == 0) {
       scal[0] = norm;
-      scal[1] = s_coef;
+      scal[1] = bad ? 0.f : s_coef / gscale;
+      hyper[3] = bad ? t0 : t;
+      if (bad) hyper[2] += 1.f;
     }
   }
   __syncthreads();
-  if (*skip) return;
+  if (s_skip) return;
   const float coef = s_coef;
   const int64_t n4 = n >> 2;
   float4* p4 = reinterpret_cast<float4*>(p);
@@ -166,15 +188,21 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_update_kernel(
 }
 
 void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float* partials,
-                      const bool* skip, float* scal, const float* hyper, float b1, float b2,
-                      float eps, float clip, const ShadowSegs& ss, hipStream_t stream) {
+                      const bool* skip, float* scal, float* hyper, float b1, float b2,
+                      float eps, float clip, float gscale, int phase, const ShadowSegs& ss,
+                      hipStream_t stream) {
+  // (a sharded update: every rank's shard has the same n, so the same
+  // number of partials, which the caller all-reduces between phases 1 and 2)
   int blocks = (int)std::min<int64_t>(ADAM_MAX_PARTIALS, std::max<int64_t>(1, (n / 4 + 255) / 256));
-  hipLaunchKernelGGL(adam_sumsq_kernel, dim3(blocks), dim3(ADAM_THREADS), 0, stream, g, n,
-                     partials);
-  post_launch("adam_sumsq_kernel", stream);
+  if (phase != 2) {
+    hipLaunchKernelGGL(adam_sumsq_kernel, dim3(blocks), dim3(ADAM_THREADS), 0, stream, g, n,
+                       partials, hyper);
+    post_launch("adam_sumsq_kernel", stream);
+  }
+  if (phase == 1) return;
   int ublocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n / 4 + 255) / 256));
   hipLaunchKernelGGL(adam_update_kernel, dim3(ublocks), dim3(ADAM_THREADS), 0, stream, p, g, m,
-                     v, n, partials, blocks, skip, scal, hyper, b1, b2, eps, clip, ss);
+                     v, n, partials, blocks, skip, scal, hyper, b1, b2, eps, clip, gscale, ss);
   post_launch("adam_update_kernel", stream);
 }
 

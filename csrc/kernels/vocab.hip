@@ -240,10 +240,9 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       }
     if ((flags & VF_EXP) && logits16 != nullptr && r < R) {
       // E = exp(x - c) = exp(x - m) * exp(m - c): one multiply per entry on
-      // the weights already in registers (bf16: fp32's exponent range, so no
-      // overflow unless the row's max logit exceeds the previous step's LSE by
-      // ~88; that would surface as a non-finite gradient, which the optimizer's
-      // NaN guard skips)
+      // the weights already in registers (bf16: fp32's exponent range, so in
+      // range unless the row's LSE moves by ~80 from the previous step's; the
+      // backward recomputes such rows exactly, vocab_grad.hip vgrad_fix)
       const float f = __builtin_amdgcn_exp2f((msafe - ec[j]) * L2E);
       // staged through LDS (behind the row statistics' GroupStat area): the
       // MFMA layout gives each lane 8-byte pieces of 32 different rows; the

@@ -20,6 +20,15 @@
 // tokens (a + b = 0 with ys != yx, so dS_r = a (e_ys - e_yx)) keeps |alpha| >=
 // 2^-10 (|a| + |b|) s: its softmax part is then off by at most 2^-10 (|a| +
 // |b|) in total.
+//
+// Range of the exp store: E = exp(x - c) with c = the previous step's LSE
+// stays inside bf16 (fp32's exponent range) while the row's LSE moves by
+// less than ~80 between steps (overflow above, loss of the row's mass to
+// underflow below).  vgrad_onehot lists every row whose LSE moved by more
+// than EXP_SAFE_LSE_JUMP (60) and vgrad_fix recomputes those rows exactly
+// from the saved vocab input (offset = the row's own LSE, so s = 1) before
+// the GEMMs read them: no silent NaN / zero gradient, no skipped step, and a
+// running count of recomputed rows for the log.
 #include "../common.h"
 #include "../launchers.h"
 
@@ -30,7 +39,8 @@ struct RowW {
   int ys, yx;
 };
 
-__device__ __forceinline__ RowW row_weights(const VGradRows& g, int64_t row) {
+// unit_s: the row's E was written with its own LSE as offset (vgrad_fix)
+__device__ __forceinline__ RowW row_weights(const VGradRows& g, int64_t row, bool unit_s = false) {
   RowW w;
   const int t = (int)(row / g.R), r = (int)(row % g.R);
   const bool sel = g.dg_sel != nullptr && t < g.T_sel;
@@ -38,7 +48,7 @@ __device__ __forceinline__ RowW row_weights(const VGradRows& g, int64_t row) {
   w.ys = sel ? (int)g.y_sel[(int64_t)r * g.T_sel + t] : -1;
   w.b = g.dg_xe != nullptr ? g.dg_xe[(int64_t)r * g.dgxe_rs + t] : 0.f;
   w.yx = g.dg_xe != nullptr ? (int)g.y_xe[(int64_t)r * g.yxe_rs + t] : -1;
-  w.s = t > 0 ? __expf(g.lse[(int64_t)(t - 1) * g.R + r] - g.lse[row]) : 1.f;
+  w.s = (t > 0 && !unit_s) ? __expf(g.lse[(int64_t)(t - 1) * g.R + r] - g.lse[row]) : 1.f;
   w.al = -(w.a + w.b) * w.s;
   // weights that (nearly) cancel on two different tokens: keep alpha away from
   // 0 so the one-hot terms stay representable (ys == yx cancels exactly)
@@ -49,17 +59,9 @@ __device__ __forceinline__ RowW row_weights(const VGradRows& g, int64_t row) {
   return w;
 }
 
-// one thread per row: alpha, and the one-hot terms folded into E
-__global__ __launch_bounds__(256) void vgrad_onehot_kernel(VGradRows g, uint16_t* __restrict__ E,
-                                                           int64_t ldl,
-                                                           float* __restrict__ alpha) {
-  const int64_t NR = (int64_t)g.n_steps * g.R;
-  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (row >= NR) return;
-  const RowW w = row_weights(g, row);
-  alpha[row] = w.al;
+// the one-hot terms of row weights w folded into the row's E
+__device__ __forceinline__ void fold_onehot(const VGradRows& g, const RowW& w, uint16_t* e) {
   if (w.al == 0.f) return;  // no gradient through this row
-  uint16_t* e = E + row * ldl;
   const float inv = 1.f / w.al;
   const bool us = w.a != 0.f && w.ys >= 0, ux = w.b != 0.f && w.yx >= 0;
   CST_DCHECK(!us || w.ys < g.V);
@@ -72,12 +74,88 @@ __global__ __launch_bounds__(256) void vgrad_onehot_kernel(VGradRows g, uint16_t
   }
 }
 
+// one thread per row: alpha, and the one-hot terms folded into E
+__global__ __launch_bounds__(256) void vgrad_onehot_kernel(VGradRows g, uint16_t* __restrict__ E,
+                                                           int64_t ldl,
+                                                           float* __restrict__ alpha) {
+  const int64_t NR = (int64_t)g.n_steps * g.R;
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= NR) return;
+  const int t = (int)(row / g.R);
+  if (g.fix != nullptr && t > 0) {
+    const float d = g.lse[row] - g.lse[row - g.R];
+    if (fabsf(d) > EXP_SAFE_LSE_JUMP) {  // E may be out of range: recomputed by vgrad_fix
+      const int k = atomicAdd(g.fix, 1);
+      g.fix[1 + k] = (int)row;
+      return;
+    }
+  }
+  const RowW w = row_weights(g, row);
+  alpha[row] = w.al;
+  fold_onehot(g, w, E + row * ldl);
+}
+
 void launch_vgrad_onehot(const VGradRows& g, uint16_t* E, int64_t ldl, float* alpha,
                          hipStream_t stream) {
   const int64_t NR = (int64_t)g.n_steps * g.R;
   hipLaunchKernelGGL(vgrad_onehot_kernel, dim3((unsigned)((NR + 255) / 256)), dim3(256), 0, stream,
                      g, E, ldl, alpha);
   post_launch("vgrad_onehot_kernel", stream);
+}
+
+// Exact recompute of the rows vgrad_onehot listed (rare: an LSE jump of more
+// than 60 between consecutive steps).  One block per listed row at a time:
+// the row's vocab input (H bf16) in LDS, x_v = hd . W_v + b_v by 16-byte W
+// loads, E_v = exp(x_v - lse_row) (s = 1), then alpha and the one-hot fold.
+constexpr int VFIX_BLOCKS = 256, VFIX_MAXH = 2048;
+__global__ __launch_bounds__(256) void vgrad_fix_kernel(VGradRows g, const uint16_t* __restrict__ hd,
+                                                        const uint16_t* __restrict__ W,
+                                                        const float* __restrict__ bias,
+                                                        uint16_t* __restrict__ E, int64_t ldl,
+                                                        float* __restrict__ alpha,
+                                                        int* __restrict__ fix_total) {
+  __shared__ float s_h[VFIX_MAXH];
+  const int n = g.fix[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && fix_total != nullptr && n > 0) fix_total[0] += n;
+  const int H = g.H;
+  for (int k = blockIdx.x; k < n; k += gridDim.x) {
+    const int64_t row = g.fix[1 + k];
+    __syncthreads();  // s_h of the previous row consumed
+    for (int i = threadIdx.x; i < H; i += 256) s_h[i] = bf2f(hd[row * H + i]);
+    __syncthreads();
+    const float L = g.lse[row];
+    uint16_t* e = E + row * ldl;
+    for (int v = threadIdx.x; v < g.V; v += 256) {
+      const uint4* wr = reinterpret_cast<const uint4*>(W + (int64_t)v * H);
+      float x = 0.f;
+      for (int c = 0; c < H / 8; ++c) {
+        const uint4 q = wr[c];
+        const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x = fmaf(s_h[8 * c + 2 * j], bf2f(wv[j] & 0xffff), x);
+          x = fmaf(s_h[8 * c + 2 * j + 1], bf2f(wv[j] >> 16), x);
+        }
+      }
+      e[v] = f2bf(__expf(x + bias[v] - L));
+    }
+    __syncthreads();  // the row's E is complete before the one-hot fold
+    if (threadIdx.x == 0) {
+      const RowW w = row_weights(g, row, /*unit_s=*/true);
+      alpha[row] = w.al;
+      fold_onehot(g, w, e);
+    }
+  }
+}
+
+void launch_vgrad_fix(const VGradRows& g, const uint16_t* hd, const uint16_t* W, const float* bias,
+                      uint16_t* E, int64_t ldl, float* alpha, int* fix_total, hipStream_t stream) {
+  if (g.fix == nullptr) return;
+  if (g.H % 8 != 0 || g.H > VFIX_MAXH)
+    throw std::runtime_error("vgrad_fix: H must be a multiple of 8 and <= 2048");
+  hipLaunchKernelGGL(vgrad_fix_kernel, dim3(VFIX_BLOCKS), dim3(256), 0, stream, g, hd, W, bias, E,
+                     ldl, alpha, fix_total);
+  post_launch("vgrad_fix_kernel", stream);
 }
 
 constexpr int VG_THREADS = 256, VG_ROWS = VG_THREADS / WAVE;

@@ -34,10 +34,11 @@ struct ShadowSegs {
   ShadowSeg s[SHADOW_MAX_SEGS];
   int n;
 };
-// hyper (device): [lr, step]; the step must already count this update
+// hyper (device): [lr, step before, skipped count, step after] (adam.hip)
 void launch_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float* partials,
-                      const bool* skip, float* scal, const float* hyper, float b1, float b2,
-                      float eps, float clip, const ShadowSegs& ss, hipStream_t stream);
+                      const bool* skip, float* scal, float* hyper, float b1, float b2,
+                      float eps, float clip, float gscale, int phase, const ShadowSegs& ss,
+                      hipStream_t stream);
 void launch_shadow_refresh(const float* p, const ShadowSegs& ss, hipStream_t stream);
 
 // vocab.hip
@@ -117,10 +118,22 @@ struct VGradRows {
   int64_t yxe_rs;
   const float* dg_xe;     // row stride dgxe_rs, nullable
   int64_t dgxe_rs;
+  // exp-store range guard (nullable): rows whose LSE moved by more than
+  // EXP_SAFE_LSE_JUMP from the previous step are listed here by
+  // vgrad_onehot ([0] = count, then flat row ids) and recomputed by vgrad_fix
+  int* fix;
 };
+constexpr float EXP_SAFE_LSE_JUMP = 60.f;
 // alpha (NR) and the one-hot terms folded into E (NR rows, stride ldl), in place
 void launch_vgrad_onehot(const VGradRows& g, uint16_t* E, int64_t ldl, float* alpha,
                          hipStream_t stream);
+// Exact recompute of the listed rows (fix[0] of them, flat ids fix[1..]):
+// logits from the saved vocab input hd (NR x H bf16) and W / bias, the row's
+// E rewritten with its own LSE as offset (scale 1), alpha and the one-hot
+// terms set accordingly; fix_total[0] += fix[0] (a running count, nullable)
+void launch_vgrad_fix(const VGradRows& g, const uint16_t* hd, const uint16_t* W,
+                      const float* bias, uint16_t* E, int64_t ldl, float* alpha, int* fix_total,
+                      hipStream_t stream);
 // dhd = alpha . dhd in place (X = E' W -> dHd; dhd nullable: the consumer
 // scales the rows itself), hs = bf16(alpha . hd)
 void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd, float* dhd,

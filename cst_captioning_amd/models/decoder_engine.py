@@ -163,6 +163,9 @@ class _DecoderFn(torch.autograd.Function):
             full = (outs[4][:, :, :V].float() - lse.unsqueeze(2)).permute(1, 0, 2).contiguous()
         ctx.eng = eng
         ctx.drop_p, ctx.rng = drop_p, rng
+        # the backward recomputes exp-store rows out of bf16 range from the
+        # vocab input and the logit weights / bias (vocab_grad.hip vgrad_fix)
+        ctx.logit_b = logit_b.detach().float().contiguous() if save else None
         ctx.shapes = (w_ih.shape, emb_w.shape)
         ctx.has_att = has_att
         ctx.state0 = state0 if save else []
@@ -250,7 +253,8 @@ class _DecoderFn(torch.autograd.Function):
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
             ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell,
-            ctx.state0, eng.upper_operands(ctx.up_saved))
+            ctx.state0, eng.upper_operands(ctx.up_saved), ctx.logit_b, eng.exp_fix_rows)
+        ctx.logit_b = None
         ctx.up_saved = None
         d_up = []
         if eng.layers > 1:  # packed [W_ih | W_hh] of each upper layer
@@ -339,6 +343,9 @@ class DecoderEngine:
         self.wup = [torch.empty(4 * H, 2 * H, **bf) for _ in range(self.layers - 1)]
         self.whh_up = [torch.empty(4 * H, H, **bf) for _ in range(self.layers - 1)]
         self.fused_refresh = False  # True once an optimizer writes the shadows
+        # running count of exp-store rows the backward recomputed because the
+        # row's LSE jumped by > 60 between steps (csrc/kernels/vocab_grad.hip)
+        self.exp_fix_rows = torch.zeros(1, dtype=torch.int32, device=dev)
         self.direct_grad_slots = None
         self.direct_params = None
         self.direct_armed = False

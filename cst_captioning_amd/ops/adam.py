@@ -12,9 +12,12 @@ buffers of :class:`..parallel.FlatGradBucket`:
     (:meth:`set_shadows`).
 
 No host synchronisation.  Learning rate and step count live in a device
-tensor (``[lr, step]``): the bias corrections follow the device step, so a
-captured HIP graph replays correct updates, and :meth:`sync_lr` (outside
-any capture) publishes an LR change made through ``param_groups``.  The math is PyTorch's Adam:
+tensor (``[lr, step, skipped, step after]``): the bias corrections follow
+the device step, so a captured HIP graph replays correct updates, and
+:meth:`sync_lr` (outside any capture) publishes an LR change made through
+``param_groups``.  NaN guard: a device flag (non-finite loss on any rank) or
+a non-finite gradient norm turns the update into a no-op that does not
+advance the step; skips are counted on the device.  The math is PyTorch's Adam:
 ``denom = sqrt(v) / sqrt(1 - b2^t) + eps``,
 ``p -= lr / (1 - b1^t) * m / denom``.
 
@@ -34,7 +37,9 @@ class FlatAdam:
         self.betas = betas
         self.eps = eps
         self.grad_clip = grad_clip
-        self.step_count = 0
+        # the gradient buffer holds grad / grad_scale: a data-parallel SUM
+        # all-reduce sets 1 / world_size here instead of dividing the buffer
+        self.grad_scale = 1.0
         self.exp_avg = torch.zeros_like(bucket.data)
         self.exp_avg_sq = torch.zeros_like(bucket.data)
         self.param_groups = [{'lr': lr}]  # for adjust_learning_rate()
@@ -42,11 +47,13 @@ class FlatAdam:
         self._use_hip = _ext.available() and bucket.data.is_cuda
         self.supports_shadows = self._use_hip
         self._shadow = (torch.empty(0, dtype=torch.int64), [])
+        dev = bucket.data.device
+        # [lr, step before the update, skipped updates, step after the update]
+        # (csrc/kernels/adam.hip); the torch path uses the same layout
+        self._hyper = torch.tensor([float(lr), 0.0, 0.0, 0.0], dtype=torch.float32, device=dev)
         if self._use_hip:
-            dev = bucket.data.device
             self._partials = torch.empty(1024, dtype=torch.float32, device=dev)
             self._scal = torch.empty(2, dtype=torch.float32, device=dev)
-            self._hyper = torch.tensor([float(lr), 0.0], dtype=torch.float32, device=dev)
             self._no_skip = torch.zeros((), dtype=torch.bool, device=dev)
             self._lr_synced = float(lr)
 
@@ -67,56 +74,72 @@ class FlatAdam:
 
     def step(self, skip=None):
         """``skip``: optional 0-dim bool device tensor; when true the update
-        is a no-op (NaN guard without a host sync)."""
+        is a no-op (NaN guard without a host sync).  A non-finite gradient
+        norm skips the update too.  Skipped updates do not advance the step
+        count (as in torch.optim.Adam) and are counted (:meth:`skipped`)."""
         self.lr = self.param_groups[0]['lr']
-        self.step_count += 1
         b1, b2 = self.betas
         g, p = self.bucket.grad, self.bucket.data
         if self._use_hip:
             if not torch.cuda.is_current_stream_capturing():
                 self.sync_lr()
-            self._hyper[1:].add_(1.0)
             self.last_norm = _ext.ops().flat_adam_step(
                 p, g, self.exp_avg, self.exp_avg_sq, self._partials, self._scal,
                 skip if skip is not None else self._no_skip, self._hyper,
-                float(b1), float(b2), float(self.eps), float(self.grad_clip), *self._shadow)
+                float(b1), float(b2), float(self.eps), float(self.grad_clip),
+                float(self.grad_scale), 0, *self._shadow)
             return self.last_norm
-        bc1 = 1 - b1 ** self.step_count
-        bc2 = 1 - b2 ** self.step_count
-        norm = torch.linalg.vector_norm(g)
+        h = self._hyper
+        h[1].copy_(h[3])
+        t = h[1].double() + 1
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        norm = torch.linalg.vector_norm(g) * self.grad_scale
         self.last_norm = norm
-        coef = torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0)
-        keep = None if skip is None else ~skip
+        bad = ~torch.isfinite(norm)
+        if skip is not None:
+            bad = bad | skip.reshape(())
+        keep = ~bad
+        coef = torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0) * self.grad_scale
         gc = g * coef
         m_new = self.exp_avg * b1 + gc * (1 - b1)
         v_new = self.exp_avg_sq * b2 + gc * gc * (1 - b2)
-        denom = v_new.sqrt() / math.sqrt(bc2) + self.eps
-        upd = m_new / denom * (self.lr / bc1)
-        if keep is None:
-            self.exp_avg.copy_(m_new)
-            self.exp_avg_sq.copy_(v_new)
-            p.sub_(upd)
-        else:
-            # torch.where, not a 0/1 multiply: NaN * 0 is NaN
-            self.exp_avg.copy_(torch.where(keep, m_new, self.exp_avg))
-            self.exp_avg_sq.copy_(torch.where(keep, v_new, self.exp_avg_sq))
-            p.copy_(torch.where(keep, p - upd, p))
+        denom = v_new.sqrt() / bc2.sqrt().float() + self.eps
+        upd = m_new / denom * (self.lr / bc1).float()
+        # torch.where, not a 0/1 multiply: NaN * 0 is NaN
+        self.exp_avg.copy_(torch.where(keep, m_new, self.exp_avg))
+        self.exp_avg_sq.copy_(torch.where(keep, v_new, self.exp_avg_sq))
+        p.copy_(torch.where(keep, p - upd, p))
+        h[3].copy_(torch.where(keep, t.float(), h[1]))
+        h[2].add_(bad.float())
         return norm
+
+    @property
+    def step_count(self):
+        return self._steps()
+
+    def skipped(self):
+        """Updates the NaN guard skipped so far (0-dim device tensor: reading
+        it synchronises, so the trainer converts it at log time only)."""
+        return self._hyper[2]
 
     def _steps(self):
         # graph replays advance only the device counter
-        return int(self._hyper[1].item()) if self._use_hip else self.step_count
+        return int(self._hyper[3].item())
 
     def state_dict(self):
         return {'step': self._steps(), 'exp_avg': self.exp_avg,
                 'exp_avg_sq': self.exp_avg_sq, 'lr': self.param_groups[0]['lr'],
-                'betas': self.betas, 'eps': self.eps}
+                'betas': self.betas, 'eps': self.eps,
+                'skipped': int(self._hyper[2].item())}
 
     def load_state_dict(self, s):
-        self.step_count = s['step']
         self.exp_avg.copy_(s['exp_avg'])
         self.exp_avg_sq.copy_(s['exp_avg_sq'])
         self.param_groups[0]['lr'] = s['lr']
+        self._hyper[1].fill_(float(s['step']))
+        self._hyper[3].fill_(float(s['step']))
+        self._hyper[2].fill_(float(s.get('skipped', 0)))
+        self._hyper[0].fill_(float(s['lr']))
         if self._use_hip:
-            self._hyper[1].fill_(float(s['step']))
-            self.sync_lr()
+            self._lr_synced = float(s['lr'])

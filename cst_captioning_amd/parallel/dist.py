@@ -256,8 +256,15 @@ class FlatGradBucket:
             n += p.numel()
         return n
 
+    def grad_scale(self, ctx):
+        """Factor between the reduced buffer and the mean gradient: the fp32
+        path SUMS over ranks and leaves the 1/N to the optimizer (FlatAdam's
+        ``grad_scale``), so no separate pass over the buffer divides it."""
+        return 1.0 / ctx.world_size if (ctx.enabled and self.wire == 'fp32') else 1.0
+
     def all_reduce(self, ctx):
-        """Sum the gradient over ranks and divide by the world size.
+        """Reduce the gradient over ranks: fp32 wire -> the SUM (the mean is
+        ``grad * grad_scale(ctx)``); bf16 wire -> the mean.
 
         wire 'fp32': one RCCL ring all-reduce of the fp32 buffer (plus the
         early vocab-head slice, if one was launched).  wire 'bf16': half the
@@ -285,4 +292,3 @@ class FlatGradBucket:
             dist.all_reduce(rest, op=dist.ReduceOp.SUM)
             if early:
                 self.early.wait()
-            self.grad.div_(ctx.world_size)

@@ -44,7 +44,8 @@ def _encode(obj):
         return {'__ndarray__': torch.from_numpy(np.ascontiguousarray(obj))}
     if isinstance(obj, np.generic):
         return obj.item()
-    if isinstance(obj, tuple) and len(obj) == 5 and obj[0] == 'MT19937':
+    if (isinstance(obj, tuple) and len(obj) == 5 and isinstance(obj[0], str)
+            and obj[0] == 'MT19937'):
         return {'__np_rng__': [obj[0], torch.from_numpy(obj[1].astype(np.int64)), int(obj[2]),
                                int(obj[3]), float(obj[4])]}
     if isinstance(obj, argparse.Namespace):
@@ -57,6 +58,8 @@ def _encode(obj):
 
 
 def _decode(obj):
+    if isinstance(obj, np.generic):  # numpy scalars of a reference checkpoint
+        return obj.item()
     if isinstance(obj, argparse.Namespace):
         return argparse.Namespace(**_decode(vars(obj)))
     if isinstance(obj, dict):
@@ -71,13 +74,33 @@ def _decode(obj):
     return obj
 
 
+def _safe_globals():
+    """Classes a reference checkpoint needs beyond tensors and containers:
+    ``opt`` is a pickled ``argparse.Namespace`` (``/root/reference/train.py:87-91``)
+    and the best-model ``infos`` carry numpy float64 scores from coco-caption
+    (``train.py:403-407`` after ``infos.update(scores)``).  numpy scalars
+    unpickle through ``multiarray.scalar(dtype, bytes)`` and the dtype
+    classes: reconstructors that only rebuild a value, they run no code from
+    the file."""
+    out = [argparse.Namespace, np.dtype]
+    try:
+        from numpy._core.multiarray import scalar  # numpy >= 2
+    except ImportError:  # pragma: no cover - numpy 1.x
+        from numpy.core.multiarray import scalar
+    out.append(scalar)
+    dtypes = getattr(np, 'dtypes', None)
+    if dtypes is not None:
+        out += [getattr(dtypes, n) for n in dir(dtypes) if n.endswith('DType')]
+    return out
+
+
 def load_checkpoint(path, map_location='cpu'):
     """Load a checkpoint with ``torch.load(weights_only=True)`` -- nothing in
-    the file is executed.  The reference pickles an ``argparse.Namespace`` as
-    ``opt`` (``/root/reference/train.py:87-91``), so that one class is on the
-    allow-list; files this framework writes hold only tensors, containers and
-    numbers (numpy state is tagged by :func:`_encode`)."""
-    with torch.serialization.safe_globals([argparse.Namespace]):
+    the file is executed.  Allow-listed: ``argparse.Namespace`` and the numpy
+    scalar reconstructors (:func:`_safe_globals`); numpy scalars come back as
+    Python numbers.  Files this framework writes hold only tensors, containers
+    and numbers (numpy state is tagged by :func:`_encode`)."""
+    with torch.serialization.safe_globals(_safe_globals()):
         s = torch.load(path, map_location=map_location, weights_only=True)
     return _decode(s)
 

@@ -120,6 +120,7 @@ class Trainer:
         else:
             betas, eps = (0.9, 0.999), 1e-8  # train.py:492 ignores --optim_*
         self.optimizer = FlatAdam(self.bucket, opt.learning_rate, betas, eps, opt.grad_clip)
+        self.optimizer.grad_scale = self.bucket.grad_scale(self.ctx)
         if engine is not None:
             engine.attach_optimizer(self)
         self.scorer = None
@@ -510,6 +511,11 @@ class Trainer:
         if opt.use_cst == 1:
             items.append(('scb_captions', out['scb_captions']))
         items.append(('Time', elapsed))
+        # updates the NaN guard skipped so far (non-finite loss on any rank or
+        # non-finite gradient norm; csrc/kernels/adam.hip)
+        items.append(('Skipped', int(self.optimizer.skipped().item())))
+        if self.engine is not None:  # exp-store rows recomputed (LSE jump > 60)
+            items.append(('ExpFix', int(self.engine.exp_fix_rows.item())))
         # throughput since the previous log line (the scalar reduction above
         # synchronised the device, so the wall clock covers finished work)
         now = time.perf_counter()

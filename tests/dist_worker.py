@@ -50,7 +50,8 @@ def main(out):
     # of the next train_step pins AccumulateGrad nodes to the default stream
     del loss
     tr.bucket.all_reduce(ctx)
-    grad = tr.bucket.grad.detach().cpu().clone()
+    # (the fp32 path sums; the optimizer applies the 1/N)
+    grad = (tr.bucket.grad * tr.optimizer.grad_scale).detach().cpu().clone()
     # two full steps: parameters must stay identical on every rank
     for _ in range(2):
         tr.train_step(loader.get_batch(), 0)

@@ -109,6 +109,39 @@ def test_flat_adam_skip_flag():
     p.grad.fill_(1.0)
     opt.step(skip=torch.ones((), dtype=torch.bool, device=DEV))
     torch.testing.assert_close(p.detach(), before)
+    assert opt.step_count == 0 and int(opt.skipped()) == 1
+
+
+def test_flat_adam_skips_nonfinite_grad_norm_and_folds_grad_scale():
+    """A finite loss with an overflowing gradient (inf in one slot) must not
+    write NaN into p / m / v: the kernel skips on a non-finite norm, keeps
+    the step count and counts the skip.  grad_scale = 1/N (DP sum) equals a
+    pre-divided buffer."""
+    from cst_captioning_amd.ops.adam import FlatAdam
+    from cst_captioning_amd.parallel import FlatGradBucket
+    torch.manual_seed(1)
+    p = torch.randn(1000, device=DEV, requires_grad=True)
+    q = p.detach().clone().requires_grad_(True)
+    bp, bq = FlatGradBucket([p]), FlatGradBucket([q])
+    op, oq = FlatAdam(bp, lr=1e-2, grad_clip=0.25), FlatAdam(bq, lr=1e-2, grad_clip=0.25)
+    op.grad_scale = 0.125
+    for _ in range(2):
+        g = torch.randn(1000, device=DEV)
+        p.grad.copy_(g * 8)
+        q.grad.copy_(g)
+        op.step()
+        oq.step()
+    torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
+    before = (p.detach().clone(), op.exp_avg.clone(), op.exp_avg_sq.clone())
+    p.grad[17] = float('inf')
+    op.step()
+    torch.cuda.synchronize()
+    for a, b in zip((p.detach(), op.exp_avg, op.exp_avg_sq), before):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    assert op.step_count == 2 and int(op.skipped()) == 1
+    p.grad[17] = 0.0
+    op.step()
+    assert op.step_count == 3 and torch.isfinite(p).all()
 
 
 # V = 1299 is not a multiple of the 128-wide vocab tile, 330 rows not of the
@@ -509,3 +542,69 @@ def test_exp_store_backward_matches_dense_path():
     for n in ref:
         err = (got[n] - ref[n]).norm() / (ref[n].norm() + 1e-12)
         assert err < 2e-2, (n, float(err))
+
+
+def test_exp_store_lse_jump_rows_recomputed():
+    """Exp-store range guard (csrc/kernels/vocab_grad.hip vgrad_fix).  The
+    decode kernel saves E = bf16(exp(x - lse_{t-1})); rows whose LSE jumps by
+    about +-100 between steps overflow (inf) or underflow (0) there.  Saved
+    tensors are built here exactly as the decode kernel writes them, with the
+    vocab input of chosen rows scaled x60 on alternate steps (LSE ~7 <-> ~120);
+    the backward must list and recompute those rows and give the fp32
+    softmax gradient of the vocab head (no NaN, no lost rows)."""
+    ops = _ext()
+    torch.manual_seed(7)
+    n, R, H, E, V = 4, 64, 128, 128, 1299
+    ldl = (V + 63) // 64 * 64
+    bf = torch.bfloat16
+    wlog = (torch.rand(V, H, device=DEV) * 0.2 - 0.1).to(bf)
+    blog = torch.randn(V, device=DEV) * 0.1
+    scale = torch.ones(n, R, 1, device=DEV)
+    jump = torch.arange(R, device=DEV) % 3 == 0  # every third row jumps
+    scale[1::2, jump] = 60.0  # steps 1, 3: peaked (overflow); steps 2: back (underflow)
+    hd = (torch.randn(n, R, H, device=DEV) * scale).to(bf)
+    x = hd.float() @ wlog.float().t() + blog  # (n, R, V) fp32 logits
+    lse = torch.logsumexp(x, 2)
+    off = torch.cat([lse[:1], lse[:-1]], 0)  # step 0: its own LSE (exp_convert)
+    Es = torch.zeros(n, R, ldl, device=DEV, dtype=bf)
+    Es[:, :, :V] = torch.exp(x - off.unsqueeze(2)).to(bf)
+    d = (lse[1:] - lse[:-1]).abs()
+    n_jump = int((d > 60).sum())
+    assert n_jump >= 2 * int(jump.sum()) and not torch.isfinite(Es.float()).all()
+    T_sel = n
+    seq = torch.multinomial(torch.softmax(x.view(-1, V), 1), 1).view(n, R).t().contiguous()
+    dg_sel = torch.randn(R, T_sel, device=DEV)
+    toks = torch.cat([torch.ones(1, R, dtype=torch.long, device=DEV), seq.t()[:-1]], 0).reshape(-1)
+    wx = (torch.randn(4 * H, E + H, device=DEV) * 0.05).to(bf)
+    emb = (torch.randn(V, E, device=DEV) * 0.1).to(bf)
+    gates = (torch.rand(n, R, 4 * H, device=DEV)).to(bf)
+    c_all = torch.randn(n, R, H, device=DEV) * 0.1
+    h_all = (torch.randn(n, R, H, device=DEV) * 0.1).to(bf)
+    empty = torch.empty(0, device=DEV)
+    fix_total = torch.zeros(1, dtype=torch.int32, device=DEV)
+    res = ops.decoder_backward(wx, wlog, emb, lse.contiguous(), Es, hd.contiguous(), gates, c_all,
+                               h_all, seq, torch.empty(0, dtype=torch.long, device=DEV), toks,
+                               dg_sel, empty, 0.0, torch.empty(0, dtype=torch.int32, device=DEV),
+                               empty, empty, 0, [], empty, empty, 0, [], [], blog, fix_total)
+    torch.cuda.synchronize()
+    assert int(fix_total) == n_jump
+    dWlog, dblog = res[1], res[2]
+    # fp32 reference: dS = a (onehot(ys) - p)
+    p = torch.softmax(x, 2)
+    a = dg_sel.t()  # (n, R)
+    dS = -a.unsqueeze(2) * p
+    dS.scatter_add_(2, seq.t().unsqueeze(2), a.unsqueeze(2))
+    ref_w = dS.reshape(-1, V).t() @ hd.float().reshape(-1, H)
+    ref_b = dS.reshape(-1, V).sum(0)
+    assert torch.isfinite(dWlog).all() and torch.isfinite(dblog).all()
+    for got, ref in ((dWlog, ref_w), (dblog, ref_b)):
+        err = (got - ref).norm() / ref.norm()
+        assert err < 2e-2, float(err)
+    # without the guard (no bias given) the same inputs are not usable
+    res0 = ops.decoder_backward(wx, wlog, emb, lse.contiguous(), Es, hd.contiguous(), gates,
+                                c_all, h_all, seq, torch.empty(0, dtype=torch.long, device=DEV),
+                                toks, dg_sel, empty, 0.0,
+                                torch.empty(0, dtype=torch.int32, device=DEV), empty, empty, 0,
+                                [], empty, empty, 0, [], [], empty, empty)
+    bad = res0[1]
+    assert (not torch.isfinite(bad).all()) or (bad - ref_w).norm() / ref_w.norm() > 0.1
