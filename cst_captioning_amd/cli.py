@@ -67,10 +67,12 @@ def build_model(opt, device, impl=None):
         logger.warning('--precision fp32: using the PyTorch decoder path (the HIP engine is bf16)')
         return model, None
     if impl == 'hip':
-        from .models.decoder_engine import DecoderEngine, engine_supports
-        if not engine_supports(opt):
-            logger.warning('fused HIP decoder supports lstm/1-layer/concat (num_chunks <= 32); '
-                           'using the PyTorch decoder path for this configuration')
+        from .models.decoder_engine import DecoderEngine, engine_unsupported_reason
+        why = engine_unsupported_reason(opt)
+        if why is not None:
+            # (the engine covers lstm / gru / rnn cells, concat / standard /
+            # manet models, up to 5 stacked layers and temporal attention)
+            logger.warning('fused HIP decoder: %s; using the PyTorch decoder path', why)
             return model, None
         engine = DecoderEngine(model, opt)
         model.impl = 'hip'

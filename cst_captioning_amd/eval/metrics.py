@@ -11,8 +11,9 @@ image, so this module re-implements the metrics from their definitions:
   * ROUGE-L-- LCS F-measure, beta = 1.2, max precision/recall over refs;
   * CIDEr  -- coco CIDEr (corpus df, no clipping/penalty), via
               :mod:`..reward.cider_d_cpu`;
-  * METEOR -- exact + Porter-stem matching with the METEOR 1.5 English
-              parameters (alpha .85, beta .2, gamma .6; stem weight .6).
+  * METEOR -- exact + stem matching (the Snowball English / Porter2
+              stemmer METEOR 1.5 uses, :mod:`.stem`) with the METEOR 1.5
+              English parameters (alpha .85, beta .2, gamma .6; stem weight .6).
               WordNet synonyms/paraphrases are not available, so this is an
               approximation (parity unpinned); if ``java`` and a METEOR jar
               are found (``METEOR_JAR`` env var) the real scorer is used.
@@ -30,6 +31,7 @@ from collections import Counter
 import numpy as np
 
 from ..reward.cider_d_cpu import Cider
+from .stem import stem
 
 _PUNCT = {"''", "'", "``", "`", "-lrb-", "-rrb-", "-lcb-", "-rcb-", ".", "?", "!", ",",
           ":", "-", "--", "...", ";"}
@@ -130,12 +132,6 @@ class Rouge:
         return float(np.mean(scores)), scores
 
 
-def _porter_light(w):
-    """A small suffix stripper standing in for the Porter stemmer."""
-    for suf in ('ingly', 'edly', 'ing', 'ed', 'ies', 'es', 's', 'ly'):
-        if w.endswith(suf) and len(w) - len(suf) >= 3:
-            return w[:-len(suf)] + ('y' if suf == 'ies' else '')
-    return w
 
 
 _METEOR_WARNED = False
@@ -159,7 +155,7 @@ class Meteor:
     def _align(self, h, r):
         used = [False] * len(r)
         pairs = []
-        for stage, key in ((self.w_exact, lambda w: w), (self.w_stem, _porter_light)):
+        for stage, key in ((self.w_exact, lambda w: w), (self.w_stem, stem)):
             for i, w in enumerate(h):
                 if any(p[0] == i for p in pairs):
                     continue

@@ -90,20 +90,30 @@ MANET_MAX_FEATS = 8  # modalities with per-frame scorer weights (attention.hip)
 MAX_LAYERS = 5  # bf16 shadow segments of the fused Adam pass (SHADOW_MAX_SEGS)
 
 
-def engine_supports(opt):
+def engine_unsupported_reason(opt):
+    """None when the fused engine runs this configuration, else why not."""
     layers = getattr(opt, 'num_layers', 1)
-    ok = (getattr(opt, 'rnn_type', 'lstm') in CELLS and 1 <= layers <= MAX_LAYERS
-          and getattr(opt, 'model_type', 'concat') in ('concat', 'standard', 'manet')
-          and opt.input_encoding_size % 64 == 0
-          and opt.rnn_size % 64 == 0)
+    mt = getattr(opt, 'model_type', 'concat')
     C = getattr(opt, 'num_chunks', 1)
-    if ok and layers > 1:
-        ok = getattr(opt, 'model_type', 'concat') == 'concat' and C == 1
-    if ok and getattr(opt, 'model_type', 'concat') == 'manet':
-        ok = C == 1 and len(getattr(opt, 'feat_dims', [])) <= MANET_MAX_FEATS
-    if ok and C > 1:  # attention size == rnn_size (TemporalAttention)
-        ok = C <= ATT_MAX_CHUNKS and getattr(opt, 'model_type', 'concat') == 'concat'
-    return ok
+    if getattr(opt, 'rnn_type', 'lstm') not in CELLS:
+        return 'rnn_type %r (supported: lstm, gru, rnn)' % getattr(opt, 'rnn_type', None)
+    if not 1 <= layers <= MAX_LAYERS:
+        return 'num_layers %d (supported: 1..%d)' % (layers, MAX_LAYERS)
+    if mt not in ('concat', 'standard', 'manet'):
+        return 'model_type %r' % mt
+    if opt.input_encoding_size % 64 or opt.rnn_size % 64:
+        return 'input_encoding_size / rnn_size must be multiples of 64'
+    if layers > 1 and (mt != 'concat' or C != 1):
+        return 'stacked layers need model_type concat without temporal attention'
+    if mt == 'manet' and (C != 1 or len(getattr(opt, 'feat_dims', [])) > MANET_MAX_FEATS):
+        return 'manet needs num_chunks 1 and at most %d modalities' % MANET_MAX_FEATS
+    if C > 1 and (C > ATT_MAX_CHUNKS or mt != 'concat'):
+        return 'temporal attention needs model_type concat and num_chunks <= %d' % ATT_MAX_CHUNKS
+    return None
+
+
+def engine_supports(opt):
+    return engine_unsupported_reason(opt) is None
 
 
 def gate_maps(rnn_type, H):
@@ -301,9 +311,9 @@ class _DecoderFn(torch.autograd.Function):
 
 class DecoderEngine:
     def __init__(self, model, opt):
-        if not engine_supports(opt):
-            raise ValueError('fused engine supports lstm, gru, rnn / 1 layer / concat '
-                             '(num_chunks <= %d with attention)' % ATT_MAX_CHUNKS)
+        why = engine_unsupported_reason(opt)
+        if why is not None:
+            raise ValueError('fused engine: unsupported configuration: ' + why)
         if not _ext.available():
             raise RuntimeError('HIP extension not available')
         self.H = model.rnn_size

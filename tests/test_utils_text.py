@@ -41,3 +41,29 @@ def test_schedules():
     o = default_opts(scb_captions=-1, use_cst_after=0, cst_increase_every=5)
     assert scb_captions(o, 0, 20) == 1 and scb_captions(o, 5, 20) == 2
     assert scb_captions(o, 1000, 20) == 19
+
+
+def test_snowball_english_stemmer():
+    """METEOR's stem stage (eval/stem.py): Snowball English (Porter2) stems of
+    the algorithm's published examples and caption-style words."""
+    from cst_captioning_amd.eval.stem import stem
+    pairs = dict(consign='consign', consigned='consign', consigning='consign',
+                 consignment='consign', consisted='consist', consistency='consist',
+                 knackeries='knackeri', generously='generous', generation='generat',
+                 running='run', happily='happili', caresses='caress', ponies='poni',
+                 ties='tie', cried='cri', hoped='hope', hopping='hop', agreed='agre',
+                 feed='feed', skies='sky', dying='die', gaps='gap', gas='gas', kiwis='kiwi',
+                 luxuriated='luxuri', dancing='danc', riding='ride', people='peopl',
+                 beautiful='beauti', relational='relat', conditional='condit',
+                 sensibility='sensibl', fruitlessly='fruitless', hopefulness='hope',
+                 communication='communic', arsenal='arsenal', news='news', controlled='control')
+    assert {w: stem(w) for w in pairs} == pairs
+
+
+def test_meteor_matches_stems():
+    from cst_captioning_amd.eval.metrics import Meteor
+    m = Meteor()
+    exact = m._segment('a man is riding a horse'.split(), 'a man is riding a horse'.split())
+    stemmed = m._segment('a man rides horses'.split(), 'a man riding a horse'.split())
+    none = m._segment('a man rides horses'.split(), 'a woman cooks food'.split())
+    assert exact > stemmed > none > 0
