@@ -48,6 +48,8 @@ std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
                                           std::vector<at::Tensor> xs,
                                           std::vector<at::Tensor> ws, double drop_p,
                                           std::vector<at::Tensor> outs);
+std::vector<at::Tensor> att_mfma_fwd(at::Tensor h, at::Tensor wq, at::Tensor P, at::Tensor wa,
+                                     at::Tensor ba, at::Tensor gv);
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);
@@ -128,6 +130,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("token_sort", &cst::token_sort);
   m.def("token_group_sum", &cst::token_group_sum);
   m.def("vocab_select", &cst::vocab_select);
+  m.def("att_mfma_fwd", &cst::att_mfma_fwd);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);
   m.def("scst_loss_forward", &cst::scst_loss_forward);

@@ -311,6 +311,21 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   };
   const float* VG = has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>();
   const int VDIV = has_att ? 1 : (int)vgate_div;
+  // MFMA attention path (kernels/att_mfma.h): from step 1 on, the attention of
+  // step t+1 runs as extra workgroups of step t's decode launch (it needs only
+  // h_t) and writes bf16 per-row video gates that the combine's cell epilogue
+  // adds; no attention launch between the decode launch and the combine.
+  // Step 0 (q = 0) and other shapes use the attention kernels of attention.hip.
+  const int CPAD = C <= 8 ? 8 : 16;
+  const bool att_mfma = has_att && att_mfma_ok((int)vgate_div, (int)C, (int)A, (int)H, per_frame);
+  at::Tensor gv16, vg16, att_ep, att_cnt;
+  if (att_mfma) {
+    gv16 = at::zeros({Bv, H4, CPAD}, bf);  // frame-minor, frames zero-padded
+    gv16.narrow(2, 0, C).copy_(a_gv.transpose(1, 2));
+    vg16 = at::empty({R, H4}, bf);
+    att_ep = at::empty({Bv, A / 64, 32, CPAD}, f32);
+    att_cnt = at::zeros({Bv}, at::TensorOptions().dtype(at::kInt).device(dev));
+  }
 
   // step 0: fused cell step from (h_{-1}, c_{-1}) = (h0, c0)
   if (has_att) run_att(0);
@@ -339,14 +354,25 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     // adds each row's video term into pre before the combine's cell epilogue
     at::Tensor q_next;
     if (has_att && next) q_next = save ? q_all[t + 1] : q_tmp;
+    AttMfmaArgs am{};
+    if (att_mfma && next)
+      am = AttMfmaArgs{h_buf(0, t), WHH + H4 * H, a_pre.data_ptr<float>(), a_wa.data_ptr<float>(),
+                       a_ba.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gv16.data_ptr()),
+                       (int)H, (int)A, (int)C, CPAD, (int)H4, (int)vgate_div, (int)Bv,
+                       reinterpret_cast<uint16_t*>(vg16.data_ptr()),
+                       save ? alpha_all[t + 1].data_ptr<float>() : nullptr,
+                       save ? q_next.data_ptr<float>() : nullptr, att_ep.data_ptr<float>(),
+                       att_cnt.data_ptr<int>()};
+    const bool q_tiles = has_att && !att_mfma;  // W_q tiles in the recurrent GEMM
     launch_vocab_lstm_fwd(vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
                           save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
                           part.data_ptr(), tgt, L, vflags, inv_temp, RNG, (int)t,
                           h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
-                          next ? pre.data_ptr<float>() : nullptr, st, has_att ? (int)A : 0,
-                          has_att && next ? q_next.data_ptr<float>() : nullptr,
-                          exp_t ? lse[t - 1].data_ptr<float>() : nullptr);
-    if (has_att && next)
+                          next ? pre.data_ptr<float>() : nullptr, st, q_tiles ? (int)A : 0,
+                          q_tiles && next ? q_next.data_ptr<float>() : nullptr,
+                          exp_t ? lse[t - 1].data_ptr<float>() : nullptr,
+                          att_mfma && next ? &am : nullptr);
+    if (q_tiles && next)
       launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), q_next.data_ptr<float>(),
                      nullptr, a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv,
                      (int)vgate_div, (int)C, (int)A, (int)H4, pre.data_ptr<float>(),
@@ -357,7 +383,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       TORCH_CHECK(choose, "internal: a next step needs a chosen token");
       cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_buf(0, t), c_buf(0, t + 1),
                       h_buf(0, t + 1), hd_buf(0, t + 1), (int)H, gates_buf(0, t + 1), (int)H,
-                      (float)drop_p, key(0, t + 1), (int)cell};
+                      (float)drop_p, key(0, t + 1), (int)cell,
+                      att_mfma ? reinterpret_cast<const uint16_t*>(vg16.data_ptr()) : nullptr};
     }
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                          choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
@@ -613,7 +640,25 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor whhT = has_att ? at::cat({wx.narrow(1, E, H).t(), a_wq.t()}, 1).contiguous()
                             : wx.narrow(1, E, H).t().contiguous();
   at::Tensor dpre_part, dwa_part, dba_part;
-  if (has_att) {
+  // MFMA attention path backward: dalpha partials from the step kernel's
+  // epilogue (lstm.hip) + att_bwd_mfma (attention.hip); else att_bwd
+  const int CPAD = C <= 8 ? 8 : 16;
+  const bool att_mfma = has_att &&
+                        att_mfma_ok((int)vdiv, (int)C, (int)A, (int)H, per_frame) &&
+                        att_bwd_epi_ok((int)vdiv, (int)C, (int)H) && (KD / 64) % 2 == 0;
+  at::Tensor gvb16, dal_part;
+  AttBwdEpi abe{};
+  if (att_mfma) {
+    // gate tables with the 4 packed gates of a unit innermost: (Bv, H, CP, 4)
+    gvb16 = at::zeros({Bv, H, CPAD, 4}, wx.options());
+    gvb16.narrow(2, 0, C).copy_(a_gv.view({Bv, C, H, 4}).permute({0, 2, 1, 3}));
+    dal_part = at::empty({H / 64, R, CPAD}, f32);
+    abe = AttBwdEpi{reinterpret_cast<const uint16_t*>(gvb16.data_ptr()), (int)vdiv, (int)C, CPAD,
+                    dal_part.data_ptr<float>()};
+    dpre_part = at::zeros({Bv, C, A}, f32);
+    dwa_part = at::zeros({Bv, A}, f32);
+    dba_part = at::zeros({Bv, 1}, f32);
+  } else if (has_att) {
     const int64_t nwg = Bv * att_groups((int)vdiv);
     dpre_part = at::zeros({nwg, C, A}, f32);
     dwa_part = at::zeros({nwg, NWA * A}, f32);
@@ -667,8 +712,17 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         c_all[t].data_ptr<float>(),
         t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
         (int)R, (int)H, (float)drop_p, RNG, key(0, t),
-        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc);
-    if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc,
+        att_mfma ? &abe : nullptr);
+    if (att_mfma)
+      launch_att_bwd_mfma(dal_part.data_ptr<float>(), (int)(H / 64), (int)R,
+                          a_alpha[t].data_ptr<float>(), t > 0 ? a_q[t].data_ptr<float>() : nullptr,
+                          a_pre.data_ptr<float>(), a_wa.data_ptr<float>(), (int)Bv, (int)vdiv,
+                          (int)C, CPAD, (int)A, (int)H4,
+                          reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, t > 0 ? 1 : 0,
+                          dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
+                          dba_part.data_ptr<float>(), st);
+    else if (has_att)  // dq_t (bf16, columns [4H, 4H+A) of dG_t) + dP / dw_a / db_a partials
       launch_att_bwd(reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
                      a_gv.data_ptr<float>(), a_pre.data_ptr<float>(),
                      t > 0 ? a_q[t].data_ptr<float>() : nullptr, a_alpha[t].data_ptr<float>(),
@@ -773,9 +827,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       at::Tensor dgv = dG_all.view({n_steps * Bv, vdiv, KD}).narrow(2, 0, H4);
       dGv = at::bmm(al, dgv, at::kFloat).view({n_steps, Bv, C, H4}).sum(0);
     }
-    const int64_t ng = att_groups((int)vdiv);
-    res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0).view_as(a_wa),
-           dba_part.sum(0).view({NWA}), dWq};
+    if (att_mfma) {
+      res = {dGv, dpre_part, dwa_part.sum(0).view_as(a_wa), dba_part.sum(0).view({1}), dWq};
+    } else {
+      const int64_t ng = att_groups((int)vdiv);
+      res = {dGv, dpre_part.view({Bv, ng, C, A}).sum(1), dwa_part.sum(0).view_as(a_wa),
+             dba_part.sum(0).view({NWA}), dWq};
+    }
   }
   // (The bias column sums at the end of the main chain, which ends ~0.3 ms
   // before the side stream's in step_timeline_r2_v20.txt, measured slower:
@@ -1226,6 +1284,40 @@ double att_bench(at::Tensor gv, at::Tensor P, at::Tensor q, at::Tensor wa, at::T
   at::Tensor dpp = at::zeros({nwg, C, A}, f32), dwp = at::zeros({nwg, A}, f32),
              dbp = at::zeros({nwg, 1}, f32);
   hipStream_t st = cur_stream();
+  const int64_t H = H4 / 4;
+  if (which == 5 || which == 6) {  // MFMA path: att_mfma forward workgroups / att_bwd_mfma
+    auto bf = gv.options().dtype(at::kBFloat16);
+    const int CP = C <= 8 ? 8 : 16;
+    at::Tensor h = (at::rand({R, H}, f32) * 2 - 1).to(at::kBFloat16);
+    at::Tensor wq = (at::randn({A, H}, f32) * 0.05).to(at::kBFloat16);
+    at::Tensor gv16 = at::zeros({Bv, H4, CP}, bf), vg = at::empty({R, H4}, bf);
+    gv16.narrow(2, 0, C).copy_(gv.transpose(1, 2));
+    at::Tensor qo = at::empty({R, A}, f32), dal = at::randn({H / 64, R, CP}, f32);
+    at::Tensor dP = at::zeros({Bv, C, A}, f32), dwa = at::zeros({Bv, A}, f32),
+               dba = at::zeros({Bv, 1}, f32);
+    at::Tensor ep = at::empty({Bv, A / 64, 32, CP}, f32);
+    at::Tensor cnt = at::zeros({Bv}, f32.dtype(at::kInt));
+    AttMfmaArgs am{reinterpret_cast<const uint16_t*>(h.data_ptr()),
+                   reinterpret_cast<const uint16_t*>(wq.data_ptr()), P.data_ptr<float>(),
+                   wa.data_ptr<float>(), ba.data_ptr<float>(),
+                   reinterpret_cast<const uint16_t*>(gv16.data_ptr()), (int)H, (int)A, (int)C, CP,
+                   (int)H4, vdiv, (int)Bv, reinterpret_cast<uint16_t*>(vg.data_ptr()),
+                   alpha.data_ptr<float>(), qo.data_ptr<float>(), ep.data_ptr<float>(),
+                   cnt.data_ptr<int>()};
+    return time_launches(
+        [&](int) {
+          if (which == 5)
+            launch_att_mfma_fwd(am, st);
+          else
+            launch_att_bwd_mfma(dal.data_ptr<float>(), (int)(H / 64), (int)R,
+                                alpha.data_ptr<float>(), q.data_ptr<float>(), P.data_ptr<float>(),
+                                wa.data_ptr<float>(), (int)Bv, vdiv, (int)C, CP, (int)A, (int)H4,
+                                reinterpret_cast<uint16_t*>(dG.data_ptr()), (int)(H4 + A), 1,
+                                dP.data_ptr<float>(), dwa.data_ptr<float>(),
+                                dba.data_ptr<float>(), st);
+        },
+        iters, st);
+  }
   return time_launches(
       [&](int) {
         if (which != 1 && which != 4)  // forward at 4 (0), 2 (2) or 1 (3) rows per workgroup
@@ -1261,6 +1353,40 @@ double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters) {
 // the vocab projection + sampler/argmax + combine alone (tests of the exact
 // two-level sampler): rows hd (R, H) bf16 -> {token (R) int64, lse (R)}.
 // mode: SEL_SAMPLE_H (1) or SEL_GREEDY_H (2).
+// MFMA temporal-attention workgroups as a launch of their own (tests /
+// microbenchmarks of kernels/att_mfma.h): h (R, H) bf16, wq (A, H) bf16,
+// P (Bv, C, A), wa (A), ba (1) fp32, gv (Bv, C, 4H) fp32 ->
+// {vg (R, 4H) bf16, alpha (R, C), q (R, A)}
+std::vector<at::Tensor> att_mfma_fwd(at::Tensor h, at::Tensor wq, at::Tensor P, at::Tensor wa,
+                                     at::Tensor ba, at::Tensor gv) {
+  for (auto* t : {&h, &wq, &P, &wa, &ba, &gv}) check_cuda(*t, "att_mfma operand");
+  TORCH_CHECK(h.scalar_type() == at::kBFloat16 && wq.scalar_type() == at::kBFloat16 &&
+                  P.scalar_type() == at::kFloat && wa.scalar_type() == at::kFloat &&
+                  ba.scalar_type() == at::kFloat && gv.scalar_type() == at::kFloat,
+              "att_mfma: h / wq bf16, P / wa / ba / gv fp32");
+  const int64_t R = h.size(0), H = h.size(1), A = wq.size(0), Bv = P.size(0), C = P.size(1);
+  TORCH_CHECK(wq.size(1) == H && P.size(2) == A && wa.numel() == A && ba.numel() == 1 &&
+                  gv.size(0) == Bv && gv.size(1) == C && gv.size(2) == 4 * H && R % Bv == 0,
+              "att_mfma: operand shapes");
+  const int vdiv = (int)(R / Bv), CP = C <= 8 ? 8 : 16;
+  TORCH_CHECK(att_mfma_ok(vdiv, (int)C, (int)A, (int)H, 0), "att_mfma: unsupported shape");
+  at::Tensor gv16 = at::zeros({Bv, 4 * H, CP}, h.options());
+  gv16.narrow(2, 0, C).copy_(gv.transpose(1, 2));
+  at::Tensor vg = at::empty({R, 4 * H}, h.options());
+  at::Tensor alpha = at::empty({R, C}, P.options()), q = at::empty({R, A}, P.options());
+  at::Tensor ep = at::empty({Bv, A / 64, 32, CP}, P.options());
+  at::Tensor cnt = at::zeros({Bv}, P.options().dtype(at::kInt));
+  AttMfmaArgs a{reinterpret_cast<const uint16_t*>(h.data_ptr()),
+                reinterpret_cast<const uint16_t*>(wq.data_ptr()), P.data_ptr<float>(),
+                wa.data_ptr<float>(), ba.data_ptr<float>(),
+                reinterpret_cast<const uint16_t*>(gv16.data_ptr()), (int)H, (int)A, (int)C, CP,
+                (int)(4 * H), vdiv, (int)Bv, reinterpret_cast<uint16_t*>(vg.data_ptr()),
+                alpha.data_ptr<float>(), q.data_ptr<float>(), ep.data_ptr<float>(),
+                cnt.data_ptr<int>()};
+  launch_att_mfma_fwd(a, cur_stream());
+  return {vg, alpha, q};
+}
+
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step) {

@@ -1,0 +1,261 @@
+// Temporal attention, forward of one decode step, on MFMA (K11-ext; the
+// model and its reference anchors are described in attention.hip).  Used as
+// extra workgroups of the merged decode launch (vocab.hip
+// vocab_lstm_fwd_kernel): the attention of step t+1 depends only on h_t, like
+// the recurrent GEMM of that launch, so it runs concurrently with the
+// vocabulary tiles of step t instead of as a launch of its own between the
+// decode launch and the combine.
+//
+// A video's attention is split over NS = A / 64 workgroups of 256 threads
+// (4 waves): workgroup (b, s) owns the 64 query units [64 s, 64 s + 64) and
+// all rows of video b (rows_per_video <= 32: two 16-row MFMA column tiles).
+//   1. q^T = W_q[units] h_t^T     (64 x 32, K = H)  v_mfma_f32_16x16x32_bf16.
+//      The video's h_t rows (32 x H bf16) are staged ONCE per workgroup in LDS
+//      by LDS-DMA (16-byte chunks XOR-swizzled by row on the source address,
+//      so the B-fragment ds_read_b128 of 16 rows is bank-conflict free); wave
+//      w streams its 16 W_q rows straight into registers, every k-step's
+//      fragment requested up front (one memory round trip for the GEMM).
+//      In the output layout a lane holds 4 consecutive units of one row per
+//      column tile, so the tanh scorer's sum over units is register-local;
+//   2. partial scores sum_{a in slice} w_a tanh(P[b, c, a] + q_r[a]) (P / w_a
+//      of the slice in LDS, 16-byte broadcast reads), combined over the 4 lane
+//      groups and the 4 waves, stored to the workgroup's slot with
+//      write-through (sc1) stores; one agent-scope ticket add per workgroup;
+//   3. the video's LAST workgroup (ticket NS - 1; MI355X_MICROARCH.md
+//      "Valid forms", row 1: sc1 stores drained by vmcnt(0) before the add,
+//      sc1 loads after it) sums the NS slots, adds b_a, takes the softmax over
+//      frames and forms vgate^T = Gv[b]^T alpha^T (4H x 32, K = 16 frames) on
+//      MFMA (v_mfma_f32_32x32x16_bf16): A operand = the per-frame gate table
+//      in frame-minor bf16 layout gv16[b][n][CP], requested before the slot
+//      loads; B operand = alpha (bf16, LDS).  A lane's output registers
+//      4g..4g+3 are the 4 packed gates of one hidden unit of its row: one
+//      8-byte store each into the bf16 per-row video-gate buffer that the
+//      combine's cell epilogue adds.  It re-arms the ticket.
+// No load is conditional (the compiler branches around, and waits for, each
+// conditional load): indices are clamped and values masked instead.
+// Training also stores alpha (R x C) and q (R x A, fp32) for the backward.
+#pragma once
+#include "gemm_tile.h"
+#include "../launchers.h"
+
+namespace cst {
+
+constexpr int ATT_SLICE = 64;  // query units per workgroup
+
+// LDS bytes of one attention workgroup: h rows (32 x H bf16), P slice
+// (C x 64 fp32), w_a slice, wave partial scores (4 x 32 x CP), alpha bf16
+// (32 x 16), ticket flag
+__host__ __device__ constexpr int att_mfma_lds_bytes(int C, int CP, int H) {
+  return 32 * H * 2 + (C * ATT_SLICE + ATT_SLICE + 4 * 32 * CP) * 4 + 32 * 16 * 2 + 16;
+}
+
+__device__ __forceinline__ bf16x8 ld_bf16x8(const uint16_t* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+// tanh(x) = 1 - 2 / (exp(2x) + 1): one exp, one reciprocal, three plain ops
+// (saturates to +-1 through exp -> inf / 0)
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// CP: frames padded to 8 / 16.  blk = b * NS + s.
+template <int CP>
+__device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g, char* lds) {
+  const int A = g.A, H = g.H, C = g.C, G4 = g.G4, vdiv = g.vdiv, NS = A / ATT_SLICE;
+  const int b = blk / NS, s = blk - b * NS;
+  uint16_t* s_h = reinterpret_cast<uint16_t*>(lds);  // [32][H], chunks swizzled
+  float* s_P = reinterpret_cast<float*>(lds + 32 * H * 2);  // [C][64]
+  float* s_wa = s_P + C * ATT_SLICE;
+  float* s_e = s_wa + ATT_SLICE;
+  uint16_t* s_alb = reinterpret_cast<uint16_t*>(s_e + 4 * 32 * CP);
+  int* s_flag = reinterpret_cast<int*>(s_alb + 32 * 16);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row0 = b * vdiv, a0 = s * ATT_SLICE;
+  // h rows of the video -> LDS by LDS-DMA (rows >= vdiv repeat the last row)
+  const int cpr = H / 8;  // 16-byte chunks per row
+  const int swm = (cpr < 16 ? cpr : 16) - 1;
+  {
+    const rsrc_t rh = make_rsrc(g.h + (int64_t)row0 * H, (int64_t)vdiv * H * 2);
+    const int nins = 32 * H * 2 / 1024;  // 1 KiB wave-instructions
+    for (int i = w; i < nins; i += 4) {
+      const int e = i * 64 + lane;  // chunk of the LDS image
+      const int row = e / cpr, ch = e % cpr;
+      const int src = min(row, vdiv - 1) * cpr + (ch ^ (row & swm));
+      glds16(rh, src * 16, 0, reinterpret_cast<char*>(s_h) + 1024 * i);
+    }
+  }
+  // W_q fragments of this wave (16 units), all k-steps requested at once
+  const int ku = lane >> 4, ru = lane & 15;  // k group / row within a 16-row tile
+  constexpr int MAXK = 16;                   // H <= 512: K / 32 k-steps
+  const int nks = H / 32;
+  const uint16_t* wrow = g.wq + (int64_t)(a0 + 16 * w + ru) * H + 8 * ku;
+  bf16x8 af[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) af[k] = ld_bf16x8(wrow + 32 * min(k, nks - 1));
+  // P slice and w_a
+  for (int i = tid; i < C * (ATT_SLICE / 4); i += 256) {
+    const int c = i / (ATT_SLICE / 4), k = i % (ATT_SLICE / 4);
+    reinterpret_cast<float4*>(s_P)[i] =
+        reinterpret_cast<const float4*>(g.P + ((int64_t)b * C + c) * A + a0)[k];
+  }
+  if (tid < ATT_SLICE / 4)
+    reinterpret_cast<float4*>(s_wa)[tid] = reinterpret_cast<const float4*>(g.wa + a0)[tid];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // h rows, P, w_a in LDS
+  // 1. q^T tiles (16 units x 16 rows) x 2 row tiles
+  f32x4v acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < nks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = 16 * j + ru, ch = 4 * k + ku;
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(
+            reinterpret_cast<const char*>(s_h) + row * H * 2 + ((ch ^ (row & swm)) << 4));
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], bfr, acc[j], 0, 0, 0);
+      }
+    }
+  }
+  // lane: units u0 .. u0 + 3 (registers 0..3) of rows 16 j + ru
+  const int u0 = 16 * w + 4 * ku;
+  if (g.q_out != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 16 * j + ru;
+      if (row < vdiv)
+        *reinterpret_cast<float4*>(g.q_out + (int64_t)(row0 + row) * A + a0 + u0) =
+            make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    }
+  }
+  // 2. partial scores of the slice, one frame per iteration
+  const float4 wv = *reinterpret_cast<const float4*>(s_wa + u0);
+  for (int c = 0; c < C; ++c) {
+    const float4 p = *reinterpret_cast<const float4*>(s_P + c * ATT_SLICE + u0);
+    float ec[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      ec[j] = wv.x * tanh_fast(p.x + acc[j][0]);
+      ec[j] = fmaf(wv.y, tanh_fast(p.y + acc[j][1]), ec[j]);
+      ec[j] = fmaf(wv.z, tanh_fast(p.z + acc[j][2]), ec[j]);
+      ec[j] = fmaf(wv.w, tanh_fast(p.w + acc[j][3]), ec[j]);
+      ec[j] += __shfl_xor(ec[j], 16, 64);
+      ec[j] += __shfl_xor(ec[j], 32, 64);
+    }
+    if (ku == 0) {
+      s_e[(w * 32 + ru) * CP + c] = ec[0];
+      s_e[(w * 32 + 16 + ru) * CP + c] = ec[1];
+    }
+  }
+  __syncthreads();
+  // the slice's partial (rows x frames) -> its slot, write-through (sc1)
+  float* slot = g.e_part + ((int64_t)b * NS + s) * 32 * CP;
+  for (int i = tid; i < 32 * CP; i += 256) {
+    const int rr = i / CP, c = i % CP;
+    const float v = s_e[rr * CP + c] + s_e[(32 + rr) * CP + c] + s_e[(64 + rr) * CP + c] +
+                    s_e[(96 + rr) * CP + c];
+    __hip_atomic_store(slot + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int ticket = __hip_atomic_fetch_add(g.cnt + b, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = ticket == NS - 1;
+  }
+  __syncthreads();
+  if (!*s_flag) return;
+  // 3. last workgroup of the video: scores, softmax, vgate.  The gate-table
+  // tiles do not depend on alpha: all of this wave's are requested first, so
+  // their latency overlaps the slot loads and the softmax.
+  const int hh = lane >> 5, r = lane & 31;
+  const int ntw = G4 / 128;  // vgate tiles per wave
+  constexpr int MAXT = 16;   // 4H <= 2048
+  const uint16_t* gvb = g.gv16 + (int64_t)b * G4 * CP;
+  const bool ghalf = CP == 16 || hh == 0;  // CP = 8: frames 8..15 are zero
+  bf16x8 ga[MAXT];
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    const int n0 = (w * ntw + min(i, ntw - 1)) * 32;
+    ga[i] = ld_bf16x8(gvb + (int64_t)(n0 + r) * CP + (CP == 16 ? 8 * hh : 0));
+  }
+  if (tid == 0) g.cnt[b] = 0;  // re-arm for the next step (stream-ordered)
+  // the NS slots summed per (row, frame): one pair per thread, all slot loads
+  // of a thread out together (sc1, the hand-off's loads)
+  {
+    constexpr int MAXS = 16;  // A <= 1024
+    for (int i = tid; i < 32 * CP; i += 256) {
+      const float* sl = g.e_part + (int64_t)b * NS * 32 * CP + i;
+      float v[MAXS];
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k)
+        v[k] = __hip_atomic_load(sl + (int64_t)min(k, NS - 1) * 32 * CP, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k) t += k < NS ? v[k] : 0.f;
+      s_e[i] = t;  // (the wave partials are consumed: reused)
+    }
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float x[CP], mx = -INFINITY;
+    const float ba = g.ba[0];
+#pragma unroll
+    for (int c = 0; c < CP; ++c) x[c] = s_e[tid * CP + c] + ba;
+#pragma unroll
+    for (int c = 0; c < CP; ++c)
+      if (c < C) mx = fmaxf(mx, x[c]);
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < CP; ++c) {
+      x[c] = c < C ? __expf(x[c] - mx) : 0.f;
+      sum += x[c];
+    }
+    const float inv = 1.f / sum;
+    const bool ok = tid < vdiv;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float al = (c < CP && c < C && ok) ? x[c < CP ? c : 0] * inv : 0.f;
+      s_alb[tid * 16 + c] = f2bf(al);
+      if (c < C && ok && g.alpha_out != nullptr) g.alpha_out[(int64_t)(row0 + tid) * C + c] = al;
+    }
+  }
+  __syncthreads();
+  // vgate^T tiles: 4H / 32 gate-column tiles over the 4 waves
+  const bf16x8 bal = ld_bf16x8(s_alb + r * 16 + 8 * hh);
+  const bf16x8 zero8 = {};
+  const bool rv = r < vdiv;
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    const int n0 = (w * ntw + i) * 32;
+    f32x16 o;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0.f;
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ghalf ? ga[i] : zero8, bal, o, 0, 0, 0);
+    if (rv && i < ntw) {
+      uint16_t* dst = g.vg_out + (int64_t)(row0 + r) * G4 + n0 + 4 * hh;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(o[4 * j]) | ((uint32_t)f2bf(o[4 * j + 1]) << 16);
+        pk.y = (uint32_t)f2bf(o[4 * j + 2]) | ((uint32_t)f2bf(o[4 * j + 3]) << 16);
+        *reinterpret_cast<uint2*>(dst + 8 * j) = pk;
+      }
+    }
+  }
+}
+
+// attention variant of a kernel template: 0 = none, else the padded frame
+// count CP (8 or 16)
+constexpr int att_variant(int C) { return C <= 8 ? 8 : 16; }
+// workgroups of one step's attention
+__host__ __device__ constexpr int att_mfma_blocks(int Bv, int A) { return Bv * (A / ATT_SLICE); }
+
+}  // namespace cst

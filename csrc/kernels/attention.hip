@@ -44,6 +44,7 @@
 //     free.  dP / dw_a / db_a accumulate in per-workgroup slots (the grid
 //     shape is the same every step, so no atomics and a deterministic sum).
 #include "att_fwd.h"
+#include "att_mfma.h"
 #include "../launchers.h"
 
 namespace cst {
@@ -273,6 +274,146 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
 }
 
 int att_groups(int vdiv, int rpw) { return (vdiv + rpw - 1) / rpw; }
+
+// MFMA attention path, backward of one reverse step (see launchers.h): block
+// (video b, 128-unit slice of A).  dalpha[r][c] = the sum of the backward step
+// kernel's H/64 partials (lstm.hip attention epilogue: the dG . Gv^T
+// contraction happened there, on the dG tile already in registers), so this
+// kernel never reads the 4H-wide dG rows or the gate tables.  Softmax backward
+// per row, then thread (unit a, row parity) runs the tanh-scorer backward over
+// its rows: dq_t[r][a] as bf16 into the dG row's tail (the next reverse step's
+// recurrent GEMM folds dq_t W_q into dh_{t-1}), dP[b][c][a] accumulated in
+// place (this block owns it), dw_a / db_a into per-video slots.
+constexpr int ATTB_UNITS = 128, ATTB_MAXR = 16;  // rows per parity (vdiv <= 32)
+template <int CP>
+__global__ __launch_bounds__(256) void att_bwd_mfma_kernel(
+    const float* __restrict__ dal_part, int n_ut, int R, const float* __restrict__ alpha,
+    const float* __restrict__ q, const float* __restrict__ P, const float* __restrict__ wa,
+    int vdiv, int C, int A, int G4, uint16_t* __restrict__ dG, int ldg, int write_dq,
+    float* __restrict__ dP_acc, float* __restrict__ dwa_part, float* __restrict__ dba_part) {
+  __shared__ float s_da[32 * CP];
+  __shared__ float s_de[32 * CP];
+  __shared__ float s_red[ATTB_UNITS * (CP + 1)];
+  const int b = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
+  const int row0 = b * vdiv;
+  const int a = sl * ATTB_UNITS + (tid & (ATTB_UNITS - 1)), par = tid >> 7;
+  // 1. dalpha[r][c] = sum of the step kernel's H/64 partials, one (r, c) per
+  // thread: its loads go out first (they gate the softmax backward)
+  const int nrc = vdiv * CP;
+  constexpr int MAXUT = 16;  // H <= 1024: every partial load goes out at once
+  float dsum[2] = {0.f, 0.f};
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    // (no conditional loads: indices clamped, values masked)
+    const int rc = min(tid + 256 * h2, nrc - 1);
+    const float* pp = dal_part + (int64_t)row0 * CP + rc;
+    float x[MAXUT];
+#pragma unroll
+    for (int ut = 0; ut < MAXUT; ++ut) x[ut] = pp[(int64_t)min(ut, n_ut - 1) * R * CP];
+#pragma unroll
+    for (int ut = 0; ut < MAXUT; ++ut) dsum[h2] += ut < n_ut ? x[ut] : 0.f;
+  }
+  // this thread's scorer operands and accumulators, requested meanwhile
+  float pv[CP], qv[ATTB_MAXR];
+#pragma unroll
+  for (int c = 0; c < CP; ++c) pv[c] = P[((int64_t)b * C + min(c, C - 1)) * A + a];
+  const float wav = wa[a];
+  const float* qb = q != nullptr ? q : P;  // step 0: q = 0 (masked below)
+#pragma unroll
+  for (int k = 0; k < ATTB_MAXR; ++k) {
+    const int rr = min(par + 2 * k, vdiv - 1);
+    qv[k] = qb[(int64_t)(q != nullptr ? row0 + rr : 0) * A + a];
+  }
+  if (q == nullptr) {
+#pragma unroll
+    for (int k = 0; k < ATTB_MAXR; ++k) qv[k] = 0.f;
+  }
+  float dp_old[CP], dw_old;
+#pragma unroll
+  for (int c = 0; c < CP; ++c) dp_old[c] = dP_acc[((int64_t)b * C + min(c, C - 1)) * A + a];
+  dw_old = dwa_part[(int64_t)b * A + a];
+  float alr[CP];
+  {
+    const int rr = min(tid, vdiv - 1);
+#pragma unroll
+    for (int c = 0; c < CP; ++c) alr[c] = alpha[(int64_t)(row0 + rr) * C + min(c, C - 1)];
+#pragma unroll
+    for (int c = 0; c < CP; ++c) alr[c] = c < C ? alr[c] : 0.f;
+  }
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2)
+    if (tid + 256 * h2 < nrc) s_da[tid + 256 * h2] = dsum[h2];
+  __syncthreads();
+  // 2. softmax backward: de_c = alpha_c (dalpha_c - sum_k alpha_k dalpha_k)
+  if (tid < vdiv) {
+    float sa = 0.f;
+#pragma unroll
+    for (int c = 0; c < CP; ++c) sa += alr[c] * s_da[tid * CP + c];
+#pragma unroll
+    for (int c = 0; c < CP; ++c) s_de[tid * CP + c] = alr[c] * (s_da[tid * CP + c] - sa);
+  }
+  __syncthreads();
+  if (sl == 0 && tid == 0) {
+    float sb = 0.f;
+    for (int r = 0; r < vdiv; ++r)
+      for (int c = 0; c < C; ++c) sb += s_de[r * CP + c];
+    dba_part[b] += sb;
+  }
+  // 3. tanh-scorer backward over this thread's rows
+  float dp[CP], dw = 0.f;
+#pragma unroll
+  for (int c = 0; c < CP; ++c) dp[c] = 0.f;
+#pragma unroll
+  for (int k = 0; k < ATTB_MAXR; ++k) {
+    const int rr = par + 2 * k;
+    if (rr < vdiv) {
+      float dq = 0.f;
+#pragma unroll
+      for (int c = 0; c < CP; ++c) {
+        if (c < C) {
+          const float u = tanh_fast(pv[c] + qv[k]);
+          const float de = s_de[rr * CP + c];
+          dw = fmaf(de, u, dw);
+          const float dz = de * wav * fmaf(-u, u, 1.f);
+          dq += dz;
+          dp[c] += dz;
+        }
+      }
+      if (write_dq) dG[(int64_t)(row0 + rr) * ldg + G4 + a] = f2bf(dq);
+    }
+  }
+  const int ul = tid & (ATTB_UNITS - 1);
+  if (par == 1) {
+#pragma unroll
+    for (int c = 0; c < CP; ++c) s_red[ul * (CP + 1) + c] = dp[c];
+    s_red[ul * (CP + 1) + CP] = dw;
+  }
+  __syncthreads();
+  if (par == 0) {
+#pragma unroll
+    for (int c = 0; c < CP; ++c)
+      if (c < C) dP_acc[((int64_t)b * C + c) * A + a] = dp_old[c] + dp[c] + s_red[ul * (CP + 1) + c];
+    dwa_part[(int64_t)b * A + a] = dw_old + dw + s_red[ul * (CP + 1) + CP];
+  }
+}
+
+void launch_att_bwd_mfma(const float* dal_part, int n_ut, int R, const float* alpha,
+                         const float* q, const float* P, const float* wa, int Bv, int vdiv, int C,
+                         int CP, int A, int G4, uint16_t* dG, int ldg, int write_dq, float* dP_acc,
+                         float* dwa_part, float* dba_part, hipStream_t stream) {
+  if (vdiv > 2 * ATTB_MAXR || A % ATTB_UNITS != 0 || C > CP || (CP != 8 && CP != 16) ||
+      Bv * vdiv != R || n_ut > 16)
+    throw std::runtime_error("att_bwd_mfma: unsupported shape");
+  const dim3 grid(Bv, A / ATTB_UNITS);
+  if (CP == 8)
+    hipLaunchKernelGGL(att_bwd_mfma_kernel<8>, grid, dim3(256), 0, stream, dal_part, n_ut, R, alpha,
+                       q, P, wa, vdiv, C, A, G4, dG, ldg, write_dq, dP_acc, dwa_part, dba_part);
+  else
+    hipLaunchKernelGGL(att_bwd_mfma_kernel<16>, grid, dim3(256), 0, stream, dal_part, n_ut, R,
+                       alpha, q, P, wa, vdiv, C, A, G4, dG, ldg, write_dq, dP_acc, dwa_part,
+                       dba_part);
+  post_launch("att_bwd_mfma_kernel", stream);
+}
 
 // Video-gate gradient of the per-frame gate tables (after the reverse loop):
 //     dGv[b, c, :] = sum over steps t and rows r of video b of alpha[t, r, c] dG_t[r, 0:G4].

@@ -21,6 +21,7 @@
 //     h_t, and h after dropout (the input of the vocabulary projection; mask
 //     from the mix32 counter hash dropout_keep(), regenerated in backward).
 #include "gemm_tile.h"
+#include "../launchers.h"
 
 namespace cst {
 
@@ -146,6 +147,29 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
 // tiles in LDS, and all 8 waves run the cell epilogue on the sum.  No global
 // workspace, no atomics, and every epilogue operand is prefetched before the
 // main loop.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// butterfly all-reduce of N per-lane values over 64 lanes: N - 1 shuffles,
+// afterwards lane l holds the total of value index l (N = 64) in v[0]
+template <int N, int M>
+struct Bfly2 {
+  static __device__ __forceinline__ void run(float* v, int lane) {
+    constexpr int Hh = N / 2;
+    const bool up = (lane & M) != 0;
+#pragma unroll
+    for (int i = 0; i < Hh; ++i) {
+      const float send = up ? v[i] : v[i + Hh];
+      const float keep = up ? v[i + Hh] : v[i];
+      v[i] = keep + __shfl_xor(send, M, WAVE);
+    }
+    Bfly2<Hh, M / 2>::run(v, lane);
+  }
+};
+template <>
+struct Bfly2<1, 0> {
+  static __device__ __forceinline__ void run(float*, int) {}
+};
+
 template <int BM, int GROUPS>
 __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, int hu,
                                                   const uint16_t* __restrict__ gates,
@@ -169,14 +193,33 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
   }
 }
 
-template <int BM, int STAGES, int GROUPS>
+// Attention epilogue (ATT): the tile's rows span the videos
+// [r0 / vdiv, (r0 + BM - 1) / vdiv]; their gate-table slices for the tile's
+// 64 hidden units (64 units x CP frames x 4 gates, bf16, 4 KB per video at
+// CP = 8, layout gvb16[v][u][c][g]) are requested before the main loop and
+// parked in LDS behind the C tiles; each thread forms
+// sum_g dG[r][4u + g] Gv[v][u][c][g] for its rows with two v_dot2c_f32_bf16
+// per frame on the bf16 gate-gradient pairs it has just packed, and a
+// butterfly over the 64 units of the wave finishes the tile's partial.
+constexpr int ATT_EPI_PF = 5;  // 16-byte slice chunks per thread
+__host__ __device__ constexpr int att_epi_videos(int vdiv) { return (62 + vdiv) / vdiv + 1; }
+
+bool att_bwd_epi_ok(int vdiv, int C, int H) {
+  const int CP = C <= 8 ? 8 : 16;
+  const int nv = att_epi_videos(vdiv);
+  // slice chunks (16 B) of the block: nv x 64 units x 4 gates x CP x 2 B
+  return C <= 16 && vdiv >= 2 && H % 64 == 0 && nv * 64 * 4 * CP * 2 <= ATT_EPI_PF * 512 * 16 &&
+         2 * 64 * 72 * 4 + nv * 64 * 4 * CP * 2 <= 2 * LSTM_BWD_STAGES * 16384;
+}
+
+template <int BM, int STAGES, int GROUPS, bool ATT, int CP>
 __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
     const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
     const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p,
     const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int cell,
-    const float* __restrict__ dh_scale) {
+    const float* __restrict__ dh_scale, AttBwdEpi att) {
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
@@ -195,6 +238,21 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
   // the epilogue operands' latency hides under the GEMM
   lstm_bwd_load_epi<BM, GROUPS>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit,
                                 dh_scale, pg, pc, pcp, pdc, pdl);
+  static_assert(!ATT || (GROUPS == 2 && BM == 64), "attention epilogue: 2 groups of 64 rows");
+  constexpr int SLICE = 64 * 4 * CP;  // bf16 per video slice
+  int v0 = 0, nvs = 0;
+  uint4 gpf[ATT ? ATT_EPI_PF : 1];
+  if (ATT) {
+    v0 = r0 / att.vdiv;
+    nvs = min(r0 + BM, R) - 1 >= r0 ? (min(r0 + BM, R) - 1) / att.vdiv - v0 + 1 : 0;
+#pragma unroll
+    for (int k = 0; k < ATT_EPI_PF; ++k) {  // (unconditional loads, clamped)
+      const int ch = tid + k * 256 * GROUPS, vj = min(ch / (SLICE / 8), nvs - 1),
+                o = ch % (SLICE / 8);
+      gpf[k] = reinterpret_cast<const uint4*>(
+          att.gvb16 + ((int64_t)(v0 + vj) * H + u0) * CP * 4)[o];
+    }
+  }
 
   f32x16 acc[TL::TM][TL::TN];
   if (nkg > 0) {
@@ -228,7 +286,23 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
   }
   float* C = reinterpret_cast<float*>(lds);  // GROUPS partial tiles of BM x CSTRIDE
   store_acc_to_lds<TL>(acc, C + grp * BM * TL::CSTRIDE, [](int) { return 0.f; }, gtid);
+  uint16_t* s_gv = reinterpret_cast<uint16_t*>(C + GROUPS * BM * TL::CSTRIDE);
+  // 16-byte chunks of a unit's slice (frame pairs) are XOR-swizzled by the unit
+  // index, so the 16-lane groups of the epilogue's ds_read_b128 (lanes =
+  // consecutive units, CP * 8 bytes apart) hit distinct bank slots
+  constexpr int NCH = CP / 2, SWD = 16 / NCH;
+  if (ATT) {
+#pragma unroll
+    for (int k = 0; k < ATT_EPI_PF; ++k) {
+      const int ch = tid + k * 256 * GROUPS;
+      if (ch < nvs * (SLICE / 8)) {
+        const int uu = (ch % (SLICE / 8)) / NCH, c2 = ch % NCH;
+        reinterpret_cast<uint4*>(s_gv)[ch - c2 + (c2 ^ ((uu / SWD) & (NCH - 1)))] = gpf[k];
+      }
+    }
+  }
   __syncthreads();
+  float pd[ATT ? RPT : 1][ATT ? CP : 1];
 
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
@@ -250,18 +324,53 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
       pk.x = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
       pk.y = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
       *reinterpret_cast<uint2*>(dG + (int64_t)r * KD + 4 * hu) = pk;
+      if (ATT) {  // the row's dalpha over this thread's 4 gate columns (bf16 dG, as stored)
+        const uint4* gs =
+            reinterpret_cast<const uint4*>(s_gv + (r / att.vdiv - v0) * SLICE + u * CP * 4);
+        const bf16x2_t d01 = __builtin_bit_cast(bf16x2_t, pk.x);
+        const bf16x2_t d23 = __builtin_bit_cast(bf16x2_t, pk.y);
+#pragma unroll
+        for (int c2 = 0; c2 < CP / 2; ++c2) {  // frames 2 c2, 2 c2 + 1
+          const uint4 q = gs[c2 ^ ((u / SWD) & (NCH - 1))];
+          pd[i][2 * c2] = __builtin_amdgcn_fdot2_f32_bf16(
+              d01, __builtin_bit_cast(bf16x2_t, q.x),
+              __builtin_amdgcn_fdot2_f32_bf16(d23, __builtin_bit_cast(bf16x2_t, q.y), 0.f, false),
+              false);
+          pd[i][2 * c2 + 1] = __builtin_amdgcn_fdot2_f32_bf16(
+              d01, __builtin_bit_cast(bf16x2_t, q.z),
+              __builtin_amdgcn_fdot2_f32_bf16(d23, __builtin_bit_cast(bf16x2_t, q.w), 0.f, false),
+              false);
+        }
+      }
+    } else if (ATT) {
+#pragma unroll
+      for (int c = 0; c < CP; ++c) pd[i][c] = 0.f;
+    }
+  }
+  if (ATT) {
+    // sum over the wave's 64 hidden units: after the butterfly lane l holds
+    // value l of each 64-value chunk (row i = idx / CP, frame c = idx % CP)
+    float* flat = &pd[0][0];
+    const int lane = tid & 63;
+#pragma unroll
+    for (int c0 = 0; c0 < RPT * CP; c0 += 64) {
+      Bfly2<64, 32>::run(flat + c0, lane);
+      const int idx = c0 + lane, i = idx / CP, c = idx % CP;
+      const int r = r0 + rg + RG * i;
+      if (r < R) att.dal_part[((int64_t)ut * R + r) * CP + c] = flat[c0];
     }
   }
 }
 
 int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
-template <int GROUPS, int STAGES = LSTM_BWD_STAGES>
+template <int GROUPS, bool ATT = false, int CP = 8, int STAGES = LSTM_BWD_STAGES>
 static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT,
                                    const float* dh_logit, float* dc_carry, const uint16_t* gates,
                                    const float* c_t, const float* c_prev, int R, int H,
                                    float drop_p, const uint32_t* rng, int step, uint16_t* dG,
-                                   int KD, hipStream_t stream, int cell, const float* dh_scale) {
+                                   int KD, hipStream_t stream, int cell, const float* dh_scale,
+                                   const AttBwdEpi& att) {
   constexpr int BM = 64;
   using TL = Tile<BM, 64, STAGES>;
   constexpr int LDS = GROUPS * TL::STAGES * TL::STAGE_BYTES > GROUPS * BM * TL::CSTRIDE * 4
@@ -269,14 +378,14 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
                           : GROUPS * BM * TL::CSTRIDE * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, STAGES, GROUPS>,
+    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
   const int n = (H / 64) * ((R + BM - 1) / BM);
-  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS>), dim3(n),
+  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP>), dim3(n),
                      dim3(256 * GROUPS), LDS, stream, dg_next, whhT, dh_logit, dc_carry, gates,
-                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale);
+                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale, att);
   post_launch("lstm_step_bwd_kernel", stream);
 }
 
@@ -284,16 +393,31 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                          const float* dh_scale) {
+                          const float* dh_scale, const AttBwdEpi* att) {
   // two K groups per block when the K-tiles split evenly
   // (measured per step: 1 group 4.66 ms, 2 groups 4.54 ms, 4 groups with 2
   // LDS stages each 4.51 vs 4.47 ms for 2 groups on another box)
+  if (att != nullptr) {
+    if ((KD / 64) % 2 != 0 || !att_bwd_epi_ok(att->vdiv, att->C, H) ||
+        att->CP != (att->C <= 8 ? 8 : 16))
+      throw std::runtime_error("lstm_step_bwd: unsupported attention epilogue shape");
+    if (att->CP == 8)
+      launch_lstm_step_bwd_g<2, true, 8>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev,
+                                         R, H, drop_p, rng, step, dG, KD, stream, cell, dh_scale,
+                                         *att);
+    else
+      launch_lstm_step_bwd_g<2, true, 16>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev,
+                                          R, H, drop_p, rng, step, dG, KD, stream, cell, dh_scale,
+                                          *att);
+    return;
+  }
+  const AttBwdEpi none{};
   if ((KD / 64) % 2 == 0)
     launch_lstm_step_bwd_g<2>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream, cell, dh_scale);
+                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, none);
   else
     launch_lstm_step_bwd_g<1>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream, cell, dh_scale);
+                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, none);
 }
 
 // 128-row tiles x 64 packed gate columns, 3 LDS stages (72 KB, 2 blocks per CU)

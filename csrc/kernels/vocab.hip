@@ -34,6 +34,7 @@
 //     exp(x - lse) in place; the backward (vocab_grad.hip) never forms dS.
 #include "gemm_tile.h"
 #include "lstm_gemm.h"
+#include "att_mfma.h"
 #include "../launchers.h"
 
 namespace cst {
@@ -392,18 +393,76 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(VOCAB_TR_PARAMS)
 // tiles leave idle instead of running before it.  The first n_lstm_pad
 // blocks (a multiple of 8, so both halves keep their XCD-aware mapping) are
 // LSTM tiles.
-template <int BN, int STAGES, int OCC, class LT>
+// ATT: the first n_att workgroups (a multiple of 8, like the LSTM tiles) are
+// the MFMA temporal attention of step t+1, one per video (att_mfma.h): they
+// depend only on h_t too, and are dispatched first, so they finish under the
+// vocabulary tiles.
+template <int BN, int STAGES, int OCC, class LT, int AV>
 __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
     VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
     const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad, int NQ,
-    float* __restrict__ q_out) {
+    float* __restrict__ q_out, AttMfmaArgs att, int n_att) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  if ((int)blockIdx.x < n_lstm_pad) {
-    if ((int)blockIdx.x < lstm_gemm_blocks(R, H, NQ))
-      lstm_gemm_block<LT>(blockIdx.x, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
+  int bid = blockIdx.x;
+  if constexpr (AV != 0) {
+    if (bid < n_att) {
+      if (bid < att_mfma_blocks(att.Bv, att.A)) att_mfma_fwd_block<AV>(bid, att, lds);
+      return;
+    }
+    bid -= n_att;
+  }
+  if (bid < n_lstm_pad) {
+    if (bid < lstm_gemm_blocks(R, H, NQ))
+      lstm_gemm_block<LT>(bid, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
     return;
   }
-  vocab_tr_block<BN, STAGES>(blockIdx.x - n_lstm_pad, lds, VOCAB_TR_ARGS);
+  vocab_tr_block<BN, STAGES>(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
+}
+
+// the same attention workgroups as a launch of their own
+template <int AV>
+__global__ __launch_bounds__(256) void att_mfma_fwd_kernel(AttMfmaArgs att) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  att_mfma_fwd_block<AV>(blockIdx.x, att, lds);
+}
+
+// host dispatch over the attention variants (frames padded to 8 / 16)
+#define ATT_VARIANTS(X) X(8) X(16)
+
+bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame) {
+  return !per_frame && vdiv >= 2 && vdiv <= 32 && C >= 1 && C <= 16 && A % ATT_SLICE == 0 &&
+         A <= 16 * ATT_SLICE && H % 32 == 0 && H >= 64 && H <= 512 &&
+         att_mfma_lds_bytes(C, C <= 8 ? 8 : 16, H) <= 48 * 1024;
+}
+
+static void check_att_mfma(const AttMfmaArgs& a) {
+  if (!att_mfma_ok(a.vdiv, a.C, a.A, a.H, 0) || a.G4 != 4 * a.H || a.CP != (a.C <= 8 ? 8 : 16) ||
+      a.e_part == nullptr || a.cnt == nullptr)
+    throw std::runtime_error("att_mfma: unsupported attention shape");
+}
+
+template <int AV>
+static void launch_att_mfma_fwd_t(const AttMfmaArgs& a, hipStream_t stream) {
+  const int lds = att_mfma_lds_bytes(a.C, a.CP, a.H);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)att_mfma_fwd_kernel<AV>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 48 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(att_mfma_fwd_kernel<AV>, dim3(att_mfma_blocks(a.Bv, a.A)), dim3(256), lds,
+                     stream, a);
+  post_launch("att_mfma_fwd_kernel", stream);
+}
+
+void launch_att_mfma_fwd(const AttMfmaArgs& a, hipStream_t stream) {
+  check_att_mfma(a);
+  switch (att_variant(a.C)) {
+#define X(V) case V: launch_att_mfma_fwd_t<V>(a, stream); break;
+    ATT_VARIANTS(X)
+#undef X
+    default: throw std::runtime_error("att_mfma: no kernel variant");
+  }
 }
 
 // token-selection modes of one decode step
@@ -423,6 +482,7 @@ int combine_count_ints_per_step() { return CMB_CNT_SLOTS * CMB_CNT_STRIDE; }
 // is chosen (see lstm_gemm.h): gates = pre + P[tok] -> i, f, g, o -> c, h.
 struct CellArgs {
   const float* pre;    // (R, 4H) h_t W_hh^T + vgate, packed gates; nullptr = no cell
+  const uint16_t* vg16;  // nullable (R, 4H) bf16 per-row video gates (MFMA attention)
   const float* ptab;   // (V, 4H) projected embedding table
   const float* c_prev;
   float* c_out;
@@ -584,6 +644,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
       for (int u0 = sub; u0 < H; u0 += CMB_LANES * CELL_U) {
         float4 p[CELL_U], x[CELL_U];
         float cp[CELL_U];
+        uint2 vq[CELL_U];
 #pragma unroll
         for (int k = 0; k < CELL_U; ++k) {
           const int u = u0 + k * CMB_LANES;
@@ -591,6 +652,17 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
             p[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
             x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
             cp[k] = cell.c_prev[(int64_t)r * H + u];
+            if (cell.vg16 != nullptr)
+              vq[k] = *reinterpret_cast<const uint2*>(cell.vg16 + (int64_t)r * 4 * H + 4 * u);
+          }
+        }
+        if (cell.vg16 != nullptr) {  // attention: the row's video gates (bf16)
+#pragma unroll
+          for (int k = 0; k < CELL_U; ++k) {
+            p[k].x += bf2f(vq[k].x & 0xffff);
+            p[k].y += bf2f(vq[k].x >> 16);
+            p[k].z += bf2f(vq[k].y & 0xffff);
+            p[k].w += bf2f(vq[k].y >> 16);
           }
         }
 #pragma unroll
@@ -721,8 +793,8 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           const CellLaunch* cl) {
   CellArgs cell{};
   if (cl != nullptr) {
-    cell = CellArgs{cl->pre, cl->ptab, cl->c_prev, cl->c_out, cl->h_out, cl->hdrop_out,
-                    cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step, cl->cell};
+    cell = CellArgs{cl->pre, cl->vg16, cl->ptab, cl->c_prev, cl->c_out, cl->h_out,
+                    cl->hdrop_out, cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step, cl->cell};
   }
   hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + CMB_ROWS - 1) / CMB_ROWS), dim3(CMB_THREADS), 0,
                      stream,
@@ -732,30 +804,38 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   post_launch("vocab_combine_kernel", stream);
 }
 
-template <int BN, int STAGES, int OCC, class LT = LGTile>
+template <int BN, int STAGES, int OCC, class LT, int AV>
 static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
                                 float inv_temp, const uint32_t* rng, int step, const uint16_t* h_t,
                                 const uint16_t* whh, const float* vgate, int vdiv, float* pre,
-                                int NQ, float* q_out, hipStream_t stream, const float* eoff) {
+                                int NQ, float* q_out, hipStream_t stream, const float* eoff,
+                                const AttMfmaArgs* att) {
   using TL = Tile<VT_V, BN, STAGES>;
   constexpr int LV = TL::STAGES * TL::STAGE_BYTES > epilogue_lds_bytes(BN)
                          ? TL::STAGES * TL::STAGE_BYTES
                          : epilogue_lds_bytes(BN);
   constexpr int LDS = LV > LT::LDS_BYTES ? LV : LT::LDS_BYTES;
+  static_assert(AV == 0 || LDS >= 48 * 1024, "attention workgroups assume 48 KB of LDS");
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
   const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H, NQ) + 7) / 8 * 8 : 0;
+  AttMfmaArgs a{};
+  int n_att = 0;
+  if (AV != 0) {
+    a = *att;
+    n_att = (att_mfma_blocks(a.Bv, a.A) + 7) / 8 * 8;
+  }
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT>,
+    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT>), dim3(n_l + n_vt * n_rt), dim3(256),
-                     LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
-                     tgt, tgt_stride, flags, inv_temp, rng, step, eoff, h_t, whh, vgate, vdiv, pre, n_l,
-                     NQ, q_out);
+  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV>),
+                     dim3(n_att + n_l + n_vt * n_rt), dim3(256), LDS, stream, hd, ldh, R, H, W,
+                     bias, V, logits16, ldl, (VocabPartial*)part, tgt, tgt_stride, flags, inv_temp,
+                     rng, step, eoff, h_t, whh, vgate, vdiv, pre, n_l, NQ, q_out, a, n_att);
   post_launch("vocab_lstm_fwd_kernel", stream);
 }
 
@@ -764,14 +844,27 @@ void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
-                           float* q_out, const float* eoff) {
+                           float* q_out, const float* eoff, const AttMfmaArgs* att) {
   // 64-row tiles, 3 blocks per CU (48 KB of LDS each; the recurrent tiles use
   // 2 stages to fit): one block's epilogue overlaps the others' main loops.
   // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
   // CU (3 interleaved rounds; profiles/r2/ab_vocab_tiles.txt)
-  launch_vocab_lstm_t<64, 2, 3, LGTile2>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
-                                         tgt_stride, flags, inv_temp, rng, step, h_t, whh, vgate,
-                                         vdiv, pre, NQ, q_out, stream, eoff);
+#define VL(AVX)                                                                              \
+  launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, \
+                                            tgt_stride, flags, inv_temp, rng, step, h_t, whh,    \
+                                            vgate, vdiv, pre, NQ, q_out, stream, eoff, att)
+  if (att == nullptr) {
+    VL(0);
+    return;
+  }
+  check_att_mfma(*att);
+  switch (att_variant(att->C)) {
+#define X(AVX) case AVX: VL(AVX); break;
+    ATT_VARIANTS(X)
+#undef X
+    default: throw std::runtime_error("vocab_lstm_fwd: no attention variant");
+  }
+#undef VL
 }
 
 void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,

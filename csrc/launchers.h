@@ -71,6 +71,7 @@ struct CellLaunch {
   float drop_p;
   int step;
   int cell;  // CellType (common.h)
+  const uint16_t* vg16;  // nullable (R, 4H) bf16 per-row video gates (attention)
 };
 // temporal-attention forward operands (kernels/att_fwd.h)
 struct AttFwdArgs {
@@ -85,6 +86,27 @@ struct AttFwdArgs {
   float* alpha_out;      // nullable (rows, C)
   int accumulate;        // 1: vg_out += (else =)
 };
+// MFMA temporal attention of one decode step, one workgroup per video
+// (kernels/att_mfma.h), run as extra workgroups of the merged decode launch
+struct AttMfmaArgs {
+  const uint16_t* h;     // (R, H) bf16 query input h_t
+  const uint16_t* wq;    // (A, H) bf16
+  const float* P;        // (Bv, C, A) projected frames
+  const float* wa;       // (A) scorer weights
+  const float* ba;       // (1) scorer bias
+  const uint16_t* gv16;  // (Bv, 4H, CP) bf16 per-frame gate tables, frame-minor
+  int H, A, C, CP, G4, vdiv, Bv;
+  uint16_t* vg_out;      // (R, 4H) bf16 per-row video gates
+  float* alpha_out;      // nullable (R, C)
+  float* q_out;          // nullable (R, A) fp32
+  float* e_part;         // (Bv, A / 64, 32, CP) partial-score slots
+  int* cnt;              // (Bv) tickets, zero at the first launch (re-armed by the kernel)
+};
+// the MFMA attention path applies: rows per video 2..32, C <= 16, A % 64 == 0,
+// A <= 1024, H % 32 == 0, 64 <= H <= 512, the shared scorer (not per frame)
+bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame);
+// standalone launch of the same workgroups (tests / microbenchmarks)
+void launch_att_mfma_fwd(const AttMfmaArgs& a, hipStream_t stream);
 // size of the end-of-sequence flag area per decode step (ints) of `counts`
 int combine_count_ints_per_step();
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
@@ -101,7 +123,8 @@ void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream,
-                           int NQ = 0, float* q_out = nullptr, const float* eoff = nullptr);
+                           int NQ = 0, float* q_out = nullptr, const float* eoff = nullptr,
+                           const AttMfmaArgs* att = nullptr);
 // exp store of step 0: fp16 logits rows -> bf16 exp(x - lse_r), in place
 void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,
                               hipStream_t stream);
@@ -155,11 +178,22 @@ void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* p
 // dg_next / dG rows have stride KD: 4H gate columns (+ A attention-query
 // columns, matched by extra whhT columns [W_hh^T | W_q^T] of width KD)
 int lstm_bwd_tiles(int R, int H);
+// Temporal-attention term of the backward step's epilogue (MFMA attention
+// path): per 64-unit column tile, the partial dalpha[r][c] = sum over the
+// tile's 256 packed gate columns of dG[r][n] Gv[video(r)][n][c] (kernels
+// lstm.hip); kernels/attention.hip att_bwd_mfma sums the H/64 partials.
+struct AttBwdEpi {
+  const uint16_t* gvb16;  // (Bv, H, CP, 4) bf16 gate tables, the 4 gates of a unit innermost
+  int vdiv, C, CP;
+  float* dal_part;       // (H / 64, R, CP) fp32
+};
+bool att_bwd_epi_ok(int vdiv, int C, int H);
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                          const float* dh_scale = nullptr);  // dh_logit row scales (nullable)
+                          const float* dh_scale = nullptr,  // dh_logit row scales (nullable)
+                          const AttBwdEpi* att = nullptr);
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal
 // attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
@@ -181,6 +215,15 @@ void launch_att_fwd(const float* gv, const float* pre, const float* q, const int
                     const float* wa, const float* ba, int Bv, int vdiv, int C, int A, int G4,
                     float* vg_out, float* alpha_out, hipStream_t stream, int accumulate,
                     int per_frame, int rpw = ATT_FWD_RPW);
+// MFMA attention path backward of one step, grid (Bv, A / 128): dalpha from
+// the step kernel's partials, softmax backward, tanh-scorer backward; dq_t
+// written as bf16 into columns [4H, 4H + A) of the dG rows (write_dq), dP
+// accumulated in place (dP_acc (Bv, C, A)), dw_a / db_a into per-video slots
+// (Bv, A) / (Bv).  q nullable (step 0: q = 0).
+void launch_att_bwd_mfma(const float* dal_part, int n_ut, int R, const float* alpha,
+                         const float* q, const float* P, const float* wa, int Bv, int vdiv, int C,
+                         int CP, int A, int G4, uint16_t* dG, int ldg, int write_dq, float* dP_acc,
+                         float* dwa_part, float* dba_part, hipStream_t stream);
 // dwa_part / dba_part: per-workgroup slots of (A) / (1), or (C, A) / (C) per_frame
 void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, const float* q,
                     const float* alpha, const float* wa, int Bv, int vdiv, int C, int A, int G4,

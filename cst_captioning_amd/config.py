@@ -125,6 +125,10 @@ def build_parser():
     add('--grad_wire', type=str, default='fp32', choices=['fp32', 'bf16'],
         help='data-parallel gradient reduction: fp32 all-reduce, or bf16 on the wire with '
              'fp32 accumulation (all-to-all + all-gather, half the bytes)')
+    add('--dp_update', type=str, default='allreduce', choices=['allreduce', 'sharded'],
+        help='data-parallel update: all-reduce the fp32 gradient and run Adam on the whole '
+             'buffer on every rank (default), or reduce-scatter -> Adam on this rank\'s '
+             '1/N shard (fp32 moments kept for the shard only) -> all-gather the parameters')
     add('--profile_phases', type=int, default=0, help='log per-phase HIP-event timings')
     return p
 

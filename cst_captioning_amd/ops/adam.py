@@ -52,7 +52,8 @@ class FlatAdam:
         # (csrc/kernels/adam.hip); the torch path uses the same layout
         self._hyper = torch.tensor([float(lr), 0.0, 0.0, 0.0], dtype=torch.float32, device=dev)
         if self._use_hip:
-            self._partials = torch.empty(1024, dtype=torch.float32, device=dev)
+            # 1024 sum-of-squares partials + the sharded update's skip-flag slot
+            self._partials = torch.zeros(1025, dtype=torch.float32, device=dev)
             self._scal = torch.empty(2, dtype=torch.float32, device=dev)
             self._no_skip = torch.zeros((), dtype=torch.bool, device=dev)
             self._lr_synced = float(lr)
@@ -113,6 +114,73 @@ class FlatAdam:
         h[3].copy_(torch.where(keep, t.float(), h[1]))
         h[2].add_(bad.float())
         return norm
+
+    def step_sharded(self, ctx, gshard, skip=None):
+        """Data-parallel sharded update (``--dp_update sharded``): ``gshard``
+        is this rank's shard of the gradient SUM (FlatGradBucket.reduce_scatter).
+        The clip norm is global: the shard's sum-of-squares partials (and the
+        rank's skip flag) are all-reduced before the update; Adam then runs on
+        the shard only (moments of other shards stay untouched here) and the
+        caller all-gathers the parameters.  Same arithmetic as :meth:`step` on
+        the all-reduced buffer with ``grad_scale = 1 / N``."""
+        import torch.distributed as dist
+        b1, b2 = self.betas
+        lo, hi = self.bucket.shard_range(ctx.rank)
+        p, m, v = self.bucket.data[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
+        gscale = 1.0 / ctx.world_size
+        flag = skip.reshape(1).float() if skip is not None else None
+        if self._use_hip:
+            if not torch.cuda.is_current_stream_capturing():
+                self.sync_lr()
+            ops = _ext.ops()
+            args = (float(b1), float(b2), float(self.eps), float(self.grad_clip), gscale)
+            ops.flat_adam_step(p, gshard, m, v, self._partials, self._scal, self._no_skip,
+                               self._hyper, *args, 1, torch.empty(0, dtype=torch.int64), [])
+            if flag is not None:
+                self._partials[1024:1025].copy_(flag)
+            else:
+                self._partials[1024:1025].zero_()
+            dist.all_reduce(self._partials, op=dist.ReduceOp.SUM)
+            any_skip = self._partials[1024] > 0
+            self.last_norm = ops.flat_adam_step(
+                p, gshard, m, v, self._partials, self._scal, any_skip, self._hyper, *args, 2,
+                torch.empty(0, dtype=torch.int64), [])
+            return self.last_norm
+        h = self._hyper
+        h[1].copy_(h[3])
+        t = h[1].double() + 1
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        red = torch.stack([gshard.double().pow(2).sum(),
+                           flag.double().sum() if flag is not None else torch.zeros((), dtype=torch.float64)])
+        dist.all_reduce(red, op=dist.ReduceOp.SUM)
+        norm = red[0].sqrt().float() * gscale
+        self.last_norm = norm
+        bad = ~torch.isfinite(norm) | (red[1] > 0)
+        keep = ~bad
+        coef = torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0) * gscale
+        gc = gshard * coef
+        m_new = m * b1 + gc * (1 - b1)
+        v_new = v * b2 + gc * gc * (1 - b2)
+        denom = v_new.sqrt() / bc2.sqrt().float() + self.eps
+        upd = m_new / denom * (self.lr / bc1).float()
+        m.copy_(torch.where(keep, m_new, m))
+        v.copy_(torch.where(keep, v_new, v))
+        p.copy_(torch.where(keep, p - upd, p))
+        h[3].copy_(torch.where(keep, t.float(), h[1]))
+        h[2].add_(bad.float())
+        return norm
+
+    def consolidate(self, ctx):
+        """Sharded update: gather every rank's moment shards, so the full
+        Adam state is on every rank (checkpoints).  Collective."""
+        import torch.distributed as dist
+        if not (self.bucket.sharded and ctx.enabled):
+            return
+        lo, hi = self.bucket.shard_range(ctx.rank)
+        for buf in (self.exp_avg, self.exp_avg_sq):
+            mine = buf[lo:hi].clone()
+            dist.all_gather_into_tensor(buf, mine)
 
     @property
     def step_count(self):

@@ -5,7 +5,8 @@ layer adds DP for one node of MI355X GPUs, one process per GPU:
 
   C1  broadcast of parameters/buffers from rank 0 at start;
   C2  ONE all-reduce per step of the whole gradient as a single flat
-      bucket.  The decoder is trained by BPTT, so every gradient is only
+      bucket (or, --dp_update sharded: reduce-scatter -> Adam on the rank's
+      1/N shard -> all-gather of the updated parameters).  The decoder is trained by BPTT, so every gradient is only
       final after the full reverse time loop: bucketed overlap with backward
       would buy nothing, while one large message is what a point-to-point
       xGMI ring moves at full per-link bandwidth (~20 M params = 81 MB fp32,
@@ -189,14 +190,20 @@ class FlatGradBucket:
     clip + Adam kernel cover every parameter.
     """
 
-    def __init__(self, params, first=(), world_size=1, wire='fp32'):
+    def __init__(self, params, first=(), world_size=1, wire='fp32', update='allreduce'):
         """``first``: parameters placed at the start of the buffer (the ones
         an :class:`EarlyAllReduce` reduces ahead of the rest).  ``wire``:
         'fp32' (one all-reduce) or 'bf16' (see :meth:`all_reduce`); the buffer
         is padded so it splits into ``world_size`` equal chunks."""
         if wire not in ('fp32', 'bf16'):
             raise ValueError('wire must be fp32 or bf16')
+        if update not in ('allreduce', 'sharded'):
+            raise ValueError('update must be allreduce or sharded')
+        if update == 'sharded' and wire != 'fp32':
+            raise ValueError('the sharded update reduce-scatters an fp32 gradient')
         self.wire = wire
+        self.update = update
+        self.world_size = world_size
         params = [p for p in params if p.requires_grad]
         first_ids = {id(p) for p in first}
         self.params = [p for p in params if id(p) in first_ids] + \
@@ -255,6 +262,31 @@ class FlatGradBucket:
                 raise ValueError('parameters are not the leading slots of the bucket')
             n += p.numel()
         return n
+
+    # -- sharded update (ZeRO-1 style, --dp_update sharded) ----------------------
+    @property
+    def sharded(self):
+        return self.update == 'sharded' and self.world_size > 1
+
+    def shard_range(self, rank):
+        n = self.grad.numel() // self.world_size
+        return rank * n, (rank + 1) * n
+
+    def reduce_scatter(self, ctx):
+        """Sum of every rank's gradient over this rank's 1/N shard (returned,
+        a buffer of its own); the rest of the local buffer is left as is.
+        Every rank's skip flag is carried separately (FlatAdam.step_sharded)."""
+        lo, hi = self.shard_range(ctx.rank)
+        if not hasattr(self, '_gshard') or self._gshard.numel() != hi - lo:
+            self._gshard = torch.empty(hi - lo, dtype=self.grad.dtype, device=self.grad.device)
+        dist.reduce_scatter_tensor(self._gshard, self.grad, op=dist.ReduceOp.SUM)
+        return self._gshard
+
+    def all_gather_params(self, ctx):
+        """Every rank's updated shard into the full parameter buffer."""
+        lo, hi = self.shard_range(ctx.rank)
+        mine = self.data[lo:hi].clone()  # (input and output must not alias)
+        dist.all_gather_into_tensor(self.data, mine)
 
     def grad_scale(self, ctx):
         """Factor between the reduced buffer and the mean gradient: the fp32

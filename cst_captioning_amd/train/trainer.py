@@ -90,13 +90,15 @@ class Trainer:
         early = [model.logit.weight, model.logit.bias]
         self.bucket = FlatGradBucket(model.parameters(), first=early,
                                      world_size=self.ctx.world_size,
-                                     wire=getattr(opt, 'grad_wire', 'fp32'))
+                                     wire=getattr(opt, 'grad_wire', 'fp32'),
+                                     update=getattr(opt, 'dp_update', 'allreduce'))
         # Early all-reduce of the vocab-head gradients under the reverse loop:
         # eager steps only.  With HIP graphs every step (eager warm-up or
         # replay) issues the same single bucket all-reduce, so ranks can never
         # disagree on the collective sequence.
         if (engine is not None and self.ctx.enabled and not getattr(opt, 'no_early_allreduce', 0)
-                and not getattr(opt, 'cuda_graph', 1) and self.bucket.wire == 'fp32'):
+                and not getattr(opt, 'cuda_graph', 1) and self.bucket.wire == 'fp32'
+                and not self.bucket.sharded):
             from ..parallel.dist import EarlyAllReduce
             self.bucket.early = EarlyAllReduce(self.ctx, self.bucket, early)
             engine.early_grad_hook = self.bucket.early
@@ -273,8 +275,8 @@ class Trainer:
         skip = None
         if getattr(opt, 'nan_guard', 1):
             skip = ~torch.isfinite(loss.detach())
-            if self.ctx.enabled:  # every rank must skip together: the flag
-                self.bucket.set_flag(skip)  # rides the gradient all-reduce
+            if self.ctx.enabled and not self.bucket.sharded:  # every rank must skip
+                self.bucket.set_flag(skip)  # together: the flag rides the all-reduce
         extra.update(loss=loss.detach(), mixer_from=mixer_from, scb_captions=scb)
         return extra, skip
 
@@ -287,6 +289,23 @@ class Trainer:
             self.engine.after_step()
         self.timer.mark('optimizer')
 
+    def _sharded_update(self, skip):
+        """--dp_update sharded (eager, between graph replays): reduce-scatter
+        of the gradient sum, clip + Adam on this rank's 1/N shard (the global
+        norm and every rank's skip flag through one 4 KB all-reduce), all-gather
+        of the updated parameters, bf16 shadows refreshed from them."""
+        gshard = self.bucket.reduce_scatter(self.ctx)
+        self.timer.mark('allreduce')
+        self.optimizer.step_sharded(self.ctx, gshard, skip)
+        self.bucket.all_gather_params(self.ctx)
+        if self.engine is not None:
+            meta, dsts = self.optimizer._shadow
+            if len(dsts):
+                from .. import _ext
+                _ext.ops().refresh_shadows(self.bucket.data, meta, dsts)
+            self.engine.after_step()
+        self.timer.mark('optimizer')
+
     def train_step(self, data, epoch):
         self.timer.reset()
         self.timer.mark('start')
@@ -296,6 +315,9 @@ class Trainer:
             if out is not None:
                 return out
         extra, skip = self._forward_backward(data, mixer_from, scb)
+        if self.bucket.sharded:
+            self._sharded_update(skip)
+            return extra
         self.bucket.all_reduce(self.ctx)
         self.timer.mark('allreduce')
         self._apply_update(skip)
@@ -342,7 +364,9 @@ class Trainer:
         self.optimizer.sync_lr()
         g_a, g_b = self._graph
         g_a.replay()
-        if g_b is not None:  # data parallel: eager all-reduce between the graphs
+        if self.bucket.sharded:  # data parallel, sharded update: eager after the graph
+            self._sharded_update(self._graph_skip)
+        elif g_b is not None:  # data parallel: eager all-reduce between the graphs
             self.bucket.all_reduce(self.ctx)
             g_b.replay()
         return self._graph_out
@@ -365,11 +389,12 @@ class Trainer:
             if not self.ctx.enabled:
                 self._apply_update(skip)
         g_b = None
-        if self.ctx.enabled:
+        if self.ctx.enabled and not self.bucket.sharded:
             g_b = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_b, pool=pool):
                 self._apply_update(skip)
         self._graph, self._graph_key, self._graph_out = (g_a, g_b), key, extra
+        self._graph_skip = skip
         logger.info('captured the training step as a HIP graph (%s)',
                     'two graphs around the all-reduce' if g_b is not None else 'one graph')
 
@@ -415,6 +440,7 @@ class Trainer:
         opt = self.opt
         if not (opt.model_file and getattr(opt, 'save_last', 1)):
             return
+        self.optimizer.consolidate(self.ctx)  # sharded update: full moments on every rank
         mine = {'loader': self.train_loader.state_dict(), 'rng': ckpt.rng_state()}
         if self.val_loader is not None:  # its caption draws continue too
             mine['val_loader'] = self.val_loader.state_dict()

@@ -19,7 +19,8 @@ ARGS = ['--synthetic', 'msvd', '--synthetic_videos', '24', '--synthetic_vocab', 
         '--impl', os.environ.get('CSTCAP_TEST_IMPL', 'torch'), '--loglevel', 'WARNING',
         '--drop_prob_lm', '0', '--cuda_graph', os.environ.get('CSTCAP_TEST_GRAPH', '1'),
         '--learning_rate', '1e-3', '--language_eval', '0',
-        '--grad_wire', os.environ.get('CSTCAP_TEST_WIRE', 'fp32')]
+        '--grad_wire', os.environ.get('CSTCAP_TEST_WIRE', 'fp32'),
+        '--dp_update', os.environ.get('CSTCAP_TEST_DPUPDATE', 'allreduce')]
 
 
 def build(rank, world, device):
@@ -58,6 +59,10 @@ def main(out):
     flat = tr.bucket.data.detach().cpu().clone()
     allp = ctx.all_gather_object(flat)
     same = all(torch.equal(allp[0], p) for p in allp)
+    tr.optimizer.consolidate(ctx)  # (sharded update: gather the moment shards)
+    moments = (tr.optimizer.exp_avg.detach().cpu().clone(),
+               tr.optimizer.exp_avg_sq.detach().cpu().clone())
+    steps_done = tr.optimizer.step_count
     # NaN guard: only the last rank's loss is NaN; its skip flag rides the
     # gradient all-reduce, so every rank must skip the update
     data = loader.get_batch()
@@ -80,7 +85,8 @@ def main(out):
         torch.save({'init': init, 'grad': grad, 'same_after_steps': same, 'nan_skip_all': nan_skip,
                     'predictions': res['predictions'], 'loss': res['scores']['Loss'],
                     'world': ctx.world_size, 'logged': logged, 'xe_logged': xe_logged,
-                    'xe_losses': xe_losses}, out)
+                    'xe_losses': xe_losses, 'params_after': flat, 'moments': moments,
+                    'steps_done': steps_done, 'skipped': int(tr.optimizer.skipped())}, out)
     ctx.destroy()
 
 

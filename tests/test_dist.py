@@ -29,9 +29,10 @@ def _free_port():
     return p
 
 
-def _run(world, out, wire='fp32'):
+def _run(world, out, wire='fp32', update='allreduce'):
     env = dict(os.environ)
     env['CSTCAP_TEST_WIRE'] = wire
+    env['CSTCAP_TEST_DPUPDATE'] = update
     env['PYTHONPATH'] = ROOT + os.pathsep + env.get('PYTHONPATH', '')
     env['CUDA_VISIBLE_DEVICES'] = ''  # CPU ranks (gloo)
     env['OMP_NUM_THREADS'] = '1'
@@ -53,6 +54,12 @@ def runs(tmp_path_factory):
 def runs_bf16(tmp_path_factory):
     d = tmp_path_factory.mktemp('dist_bf16')
     return {w: _run(w, str(d / ('w%d.pt' % w)), 'bf16') for w in (2, 4)}
+
+
+@pytest.fixture(scope='module')
+def runs_sharded(tmp_path_factory):
+    d = tmp_path_factory.mktemp('dist_sharded')
+    return {w: _run(w, str(d / ('w%d.pt' % w)), update='sharded') for w in (2, 4)}
 
 
 def _reference_grad(world, with_abs=False):
@@ -139,3 +146,21 @@ def test_bf16_wire_reduction(runs_bf16, world):
     assert err.max() > 0  # the wire really is bf16
     assert r['same_after_steps'] and r['nan_skip_all']
     assert r['xe_logged'] == pytest.approx([sum(r['xe_losses']) / world], rel=1e-6)
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_sharded_update_matches_allreduce(runs, runs_sharded, world):
+    """--dp_update sharded (reduce-scatter -> Adam on the rank's 1/N shard with
+    the global clip norm -> all-gather) gives the parameters and the Adam
+    moments of the all-reduce path, keeps the ranks identical, and skips
+    everywhere when one rank's loss is NaN.  (Not bit-equal: the norm and the
+    gradient sums are accumulated in another order.)"""
+    a, b = runs[world], runs_sharded[world]
+    # (Adam's m / sqrt(v) magnifies last-bit differences of near-zero gradients:
+    # atol 1e-6 = 0.1 % of one lr = 1e-3 step)
+    torch.testing.assert_close(b['params_after'], a['params_after'], rtol=1e-5, atol=1e-6)
+    for x, y in zip(b['moments'], a['moments']):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-10)
+    assert b['same_after_steps'] and b['nan_skip_all']
+    assert b['steps_done'] == a['steps_done'] and b['skipped'] == a['skipped'] == 1
+    assert b['xe_logged'] == pytest.approx([sum(b['xe_losses']) / world], rel=1e-6)

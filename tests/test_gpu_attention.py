@@ -3,7 +3,9 @@ CaptionModel path (fp32 reference of the same model): teacher-forced
 log-probs and every parameter gradient (attention scorer, frame projection,
 LSTM, vocab head, FeatPool), REINFORCE gradients through a rollout, greedy
 decoding and beam search.  Kernels: csrc/kernels/attention.hip
-(att_fwd_kernel / att_bwd_kernel) plus the K = 4H + A recurrent backward GEMM.
+(att_fwd_kernel / att_bwd_kernel) plus the K = 4H + A recurrent backward GEMM
+at H = A = 64; at H = A = 128 the MFMA path (att_mfma.h workgroups inside the
+decode launch, the lstm.hip dalpha epilogue and att_bwd_mfma).
 """
 import copy
 
@@ -16,6 +18,7 @@ DEV = 'cuda'
 
 
 def _tiny(C=4, V=300, H=64, feat_dims=(48, 32), S=5, B=6, L=12, seed=0):
+    # (feat_dims: FeatPool output F * H; the attention size equals H)
     from cst_captioning_amd.config import default_opts
     from cst_captioning_amd.data import make_synthetic, CaptionLoader
     from cst_captioning_amd.models import CaptionModel
@@ -54,9 +57,10 @@ def _grad_errors(model, ref):
     return out
 
 
-@pytest.mark.parametrize('C', [4, 8, 12])
-def test_attention_teacher_forced_matches_torch(C):
-    ds, opt, model, loader = _tiny(C=C)
+@pytest.mark.parametrize('C,H,S', [(4, 64, 5), (8, 64, 5), (12, 64, 5), (8, 128, 10),
+                                   (12, 128, 16), (3, 128, 4)])
+def test_attention_teacher_forced_matches_torch(C, H, S):
+    ds, opt, model, loader = _tiny(C=C, H=H, S=S)
     eng = _engine(model, opt)
     model.train()
     data = loader.get_batch()
@@ -83,8 +87,9 @@ def test_attention_teacher_forced_matches_torch(C):
     assert not bad, bad
 
 
-def test_attention_rollout_gradient_matches_torch():
-    ds, opt, model, loader = _tiny(C=6, seed=2)
+@pytest.mark.parametrize('H,S', [(64, 5), (128, 10)])
+def test_attention_rollout_gradient_matches_torch(H, S):
+    ds, opt, model, loader = _tiny(C=6, seed=2, H=H, S=S)
     eng = _engine(model, opt)
     model.train()
     model.set_mixer_from(1)
@@ -107,8 +112,9 @@ def test_attention_rollout_gradient_matches_torch():
     assert not bad, bad
 
 
-def test_attention_greedy_and_beam_match_torch():
-    ds, opt, model, loader = _tiny(C=5, seed=3)
+@pytest.mark.parametrize('H,S', [(64, 5), (128, 10)])
+def test_attention_greedy_and_beam_match_torch(H, S):
+    ds, opt, model, loader = _tiny(C=5, seed=3, H=H, S=S)
     with torch.no_grad():
         model.logit.weight.mul_(3.0)  # peaked distributions: few near-ties
     eng = _engine(model, opt)
