@@ -56,6 +56,7 @@ static const uint32_t* rng_ptr(const at::Tensor& rng) {
 
 // Events and side streams are created once per device and reused: nothing
 // is created or destroyed while a HIP graph is being captured.
+constexpr int MAX_DHD_CHUNKS = 32;  // per-chunk events of the vocab-head dHd GEMM
 struct DeviceAux {
   std::vector<hipEvent_t> ev;
   c10::hip::HIPStream side[2];
@@ -66,7 +67,7 @@ static DeviceAux& device_aux(int dev_index) {
   if (it == aux.end()) {
     auto* a = new DeviceAux{{}, {c10::hip::getStreamFromPool(false, dev_index),
                                  c10::hip::getStreamFromPool(false, dev_index)}};
-    a->ev.resize(6);
+    a->ev.resize(6 + MAX_DHD_CHUNKS);
     for (auto& e : a->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     it = aux.emplace(dev_index, a).first;
   }
@@ -507,8 +508,24 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   TORCH_CHECK(V < 65536, "vocab: token sort supports V < 65536");
   const int64_t NR = n_steps * R;
   DeviceAux& aux = device_aux((int)dev.index());
-  hipEvent_t ev_ready = aux.ev[0], ev_dhd = aux.ev[1], ev_done = aux.ev[2];
-  c10::hip::HIPStream side = aux.side[0];
+  hipEvent_t ev_ready = aux.ev[0], ev_done = aux.ev[2], ev_tok = aux.ev[3];
+  c10::hip::HIPStream side = aux.side[0], side2 = aux.side[1];
+  // dHd = alpha X, X = E' W, is computed in chunks of steps in reverse time
+  // order on the side stream, one event per chunk: reverse step t waits only
+  // for the chunk that holds its rows, so the loop starts after the first
+  // (smallest) chunk instead of after the whole 35,840-row GEMM, and the rest
+  // of the GEMM runs under the loop
+  std::vector<std::array<int64_t, 2>> dhd_chunks;  // [t0, t1)
+  {
+    int64_t t1 = n_steps;
+    while (t1 > 0) {
+      const int64_t k = dhd_chunks.empty() ? 2 : 4;
+      const int64_t t0 = std::max<int64_t>(0, t1 - k);
+      dhd_chunks.push_back({t0, t1});
+      t1 = t0;
+    }
+    TORCH_CHECK((int)dhd_chunks.size() <= MAX_DHD_CHUNKS, "too many decode steps for the dHd chunks");
+  }
 
   // 1-2. vocab head on the side stream.  Exp store (training): alpha and the
   // one-hot terms folded into E, X = E' W (dHd = alpha X, scaled by the
@@ -556,7 +573,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // profiles/r2/ab_vh_sched.txt).  Data parallelism runs them concurrently
   // with the loop, so the vocab head's all-reduce hides under it.
   const bool early_comm = early && comm_stream != 0;
-  const int vh_sched = early_comm ? 2 : 0;
+  int vh_sched = early_comm ? 2 : 0;
+  if (const char* e = getenv("CSTCAP_VH_SCHED")) vh_sched = atoi(e);  // A/B experiments
   auto dw_gemm = [&]() {  // (current stream: side)
     at::mm_out(dWlog, Ev.t(), ds_ready ? hd2 : hs, at::kFloat);
   };
@@ -599,11 +617,14 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          ptr_or_null<int>(fix_total), side.stream());
       }
     }
-    // X = E' W; the reverse loop reads alpha X (row scales at load), so the
-    // loop starts right after the GEMM and the scaled Hd rows of the dW GEMM
-    // are formed under it
-    at::mm_out(dHd, Ev, wlog, at::kFloat);
-    (void)hipEventRecord(ev_dhd, side.stream());
+    // X = E' W, chunk by chunk; the reverse loop reads alpha X (row scales at
+    // load), and the scaled Hd rows of the dW GEMM are formed under it
+    for (size_t ci = 0; ci < dhd_chunks.size(); ++ci) {
+      const int64_t r0 = dhd_chunks[ci][0] * R, nr = (dhd_chunks[ci][1] - dhd_chunks[ci][0]) * R;
+      at::Tensor dst = dHd.narrow(0, r0, nr);
+      at::mm_out(dst, Ev.narrow(0, r0, nr), wlog, at::kFloat);
+      (void)hipEventRecord(aux.ev[6 + ci], side.stream());
+    }
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
                         reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
@@ -626,10 +647,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor stok = at::empty({NR}, i32), srow = at::empty({NR}, i32);
   at::Tensor S_tok = at::empty({V, H4}, wx.options());  // per-token gate-gradient sums
   at::Tensor S32 = at::empty({V, H4}, f32);  // rows of long groups only (token_long_zero)
-  // on the main stream, under the side stream's vocab-head GEMM
+  // on the second side stream, off the critical path (needed after the loop)
+  (void)hipStreamWaitEvent(side2.stream(), ev_ready, 0);
   launch_token_sort(toks.data_ptr<int64_t>(), (int)NR, (int)V, sort_ws.data_ptr<int>(),
-                    stok.data_ptr<int>(), srow.data_ptr<int>(), st);
-  launch_token_long_zero(sort_ws.data_ptr<int>(), (int)V, (int)H4, S32.data_ptr<float>(), st);
+                    stok.data_ptr<int>(), srow.data_ptr<int>(), side2.stream());
+  launch_token_long_zero(sort_ws.data_ptr<int>(), (int)V, (int)H4, S32.data_ptr<float>(),
+                         side2.stream());
+  (void)hipEventRecord(ev_tok, side2.stream());
 
   // 4. reverse LSTM loop on the main stream
   at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
@@ -677,8 +701,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   auto dh_scale_t = [&](int64_t t) -> const float* {
     return ds_ready ? nullptr : alpha.data_ptr<float>() + t * R;
   };
-  (void)hipStreamWaitEvent(st, ev_dhd, 0);
+  size_t next_chunk = 0;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
+    if (next_chunk < dhd_chunks.size() && t == dhd_chunks[next_chunk][1] - 1)
+      (void)hipStreamWaitEvent(st, aux.ev[6 + next_chunk++], 0);  // dHd rows of this chunk
     // top layer first: its h gradient comes from the vocab head (dHd, with the
     // vocab dropout mask); layer l < top gets dG_{l+1, t} W_ih_{l+1} through
     // the inter-layer dropout mask of layer l's output
@@ -781,6 +807,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // 5. input-token gradients through the per-token sums S[v] = sum of the dG
   //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
   //    input-weight gradient S^T emb -- GEMMs over V rows instead of n*R
+  (void)hipStreamWaitEvent(st, ev_tok, 0);  // the token sort (second side stream)
   launch_token_group_sum(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)H4, KD,
                          stok.data_ptr<int>(), srow.data_ptr<int>(), (int)NR,
                          sort_ws.data_ptr<int>(), (int)V,

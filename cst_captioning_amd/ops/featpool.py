@@ -85,6 +85,20 @@ class _FeatPoolVgateFn(torch.autograd.Function):
         return (None,) * (4 + nf) + tuple(g[:nf]) + tuple(g[nf:]) + (d_wih,)
 
 
+# Tests may pin the dropout seeds: a callable dev -> int32[2] device tensor
+# (graph-vs-eager equivalence, tests/test_gpu_graph.py).  None = a fresh
+# on-device draw per pass (graph-safe).
+SEED_SOURCE = None
+
+
+def _seeds(p, dev):
+    if p <= 0:
+        return torch.zeros(2, dtype=torch.int32, device=dev)
+    if SEED_SOURCE is not None:
+        return SEED_SOURCE(dev)
+    return torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev)
+
+
 def featpool_vgate(eng, model, feats):
     """Packed video gate term (B, 4H) of the concat model through the fused
     FeatPool (train-mode dropout as the module's)."""
@@ -92,8 +106,7 @@ def featpool_vgate(eng, model, feats):
     lins = [m[0] for m in pool.feat_list]
     p = float(pool.feat_list[0][2].p) if pool.training else 0.0
     dev = feats[0].device
-    rng = (torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev) if p > 0
-           else torch.zeros(2, dtype=torch.int32, device=dev))
+    rng = _seeds(p, dev)
     xs = [f.reshape(-1, f.size(-1)).contiguous() for f in feats]
     return _FeatPoolVgateFn.apply(eng, p, rng, len(xs), *xs, *[l.weight for l in lins],
                                   *[l.bias for l in lins], model.core.rnn.weight_ih_l0)
@@ -105,8 +118,7 @@ def featpool(pool, feats):
     lins = [m[0] for m in pool.feat_list]
     p = float(pool.feat_list[0][2].p) if pool.training else 0.0
     dev = feats[0].device
-    rng = (torch.randint(0, 2 ** 31 - 1, (2,), dtype=torch.int32, device=dev) if p > 0
-           else torch.zeros(2, dtype=torch.int32, device=dev))
+    rng = _seeds(p, dev)
     xs = [f.reshape(-1, f.size(-1)).contiguous() for f in feats]
     out = _FeatPoolFn.apply(p, rng, len(xs), *xs, *[l.weight for l in lins],
                             *[l.bias for l in lins])

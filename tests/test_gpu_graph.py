@@ -56,6 +56,43 @@ def test_graph_xe_steps_match_eager():
     assert b.optimizer.state_dict()['step'] == 6
 
 
+@pytest.mark.parametrize('H', [128, 512])
+def test_graph_scst_step_matches_eager_with_fixed_seeds(H):
+    """The step that ships -- one captured HIP graph: FeatPool + video gate,
+    MIXER rollout, the greedy baseline decoded concurrently on a side stream,
+    on-GPU CIDEr-D of both, the fused SCST reward / mask / REINFORCE loss,
+    the backward, clip + Adam + bf16 weight shadows -- against the same step
+    enqueued eagerly (reference step: /root/reference/train.py:167-218), with
+    dropout 0.5 and the dropout / sampling seeds pinned on the device: the
+    same sampled tokens, rewards and loss every step, and the same weights
+    after 5 updates."""
+    from cst_captioning_amd.ops import featpool as fp
+    fixed = torch.tensor([12345, 67890], dtype=torch.int32, device=DEV)
+    a, la = _setup(rl=True, drop=0.5, graph=0, H=H)
+    b, lb = _setup(rl=True, drop=0.5, graph=1, H=H)
+    torch.testing.assert_close(_flat(a.model), _flat(b.model), rtol=0, atol=0)
+    for tr in (a, b):
+        tr.engine._rng = lambda dev: fixed
+    old = fp.SEED_SOURCE
+    fp.SEED_SOURCE = lambda dev: fixed
+    try:
+        for _ in range(5):
+            oa = a.train_step(la.get_batch(), 0)
+            ob = b.train_step(lb.get_batch(), 0)
+            torch.cuda.synchronize()
+            assert torch.equal(oa['seq'], ob['seq'])
+            torch.testing.assert_close(oa['reward'], ob['reward'], rtol=1e-5, atol=1e-6)
+            for k in ('loss', 'm', 'b'):
+                torch.testing.assert_close(torch.as_tensor(oa[k]).float(),
+                                           torch.as_tensor(ob[k]).float(), rtol=1e-5, atol=1e-6)
+    finally:
+        fp.SEED_SOURCE = old
+    assert b._graph is not None and a._graph is None
+    pa, pb = _flat(a.model), _flat(b.model)
+    assert ((pa - pb).norm() / pa.norm()).item() < 1e-4
+    assert a.optimizer.step_count == b.optimizer.step_count == 5
+
+
 def test_graph_replays_draw_fresh_samples():
     """The same batch replayed twice gives different rollouts (seeds are
     drawn on the device inside the graph), and the weights keep training."""

@@ -201,3 +201,30 @@ def test_two_level_sampler_chi_square_full_vocab(temperature):
     assert (tok2.cpu().numpy() != tok).mean() > 0.5
     tg, _ = C.vocab_select(hd[:4], W, b, rng, 2, 1.0, 0)
     assert (tg.cpu().numpy() == int(torch.argmax(x))).all()
+
+
+def test_headline_beam5_matches_torch_batched_beam():
+    """Beam search K = 5 over 64 videos at the headline shape (H = E = 512,
+    V = 10,509, L = 30): the GPU beam step (csrc/kernels/beam.hip) against the
+    PyTorch batched beam search (itself pinned to a per-video spec of the
+    reference's sample_beam, /root/reference/model.py:369-512, in
+    tests/test_model.py) on the same bf16-rounded weights."""
+    model, eng, loader = _headline_model(seed=3, drop=0.0)
+    with torch.no_grad():
+        model.logit.weight.mul_(3.0)  # peaked distributions: few near-ties
+    eng.refresh_weights()
+    model.eval()
+    data = loader.get_batch()
+    import copy
+    ref = copy.deepcopy(model)
+    ref.impl = 'torch'
+    ref._engine = None
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(p.bfloat16().float())
+        seq_ref, lp_ref = ref.sample(data['feats'], {'beam_size': 5})
+        seq, lp = eng.sample_beam(model, data['feats'], {'beam_size': 5})
+    assert seq.shape == seq_ref.shape == (64, 30)
+    same = (seq == seq_ref).all(1)
+    assert same.float().mean().item() >= 0.8, same.float().mean().item()
+    assert ((lp - lp_ref).abs()[same] < 0.05).all()
