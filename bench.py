@@ -16,6 +16,12 @@ Every step inside the timed region does ALL of the above (nothing cached,
 no layers skipped).  Timed region: barrier + synchronize, K steps, barrier +
 synchronize; the MAX over ranks is reported.
 
+BASELINE.json's metric names the LSTM-attn decoder while the headline config
+(the reference default ``--num_chunks 1``) mean-pools the features, so an SCST
+run also times the 8-frame temporal-attention config of the same job (same K
+and W, after the headline run's buffers are freed) and reports it as the
+``att8`` field ({value, ms_per_step, ...}); ``--att8 0`` skips it.
+
 Modes:
   --impl hip   (default) fused HIP engine + on-GPU CIDEr-D, bf16 MFMA
   --impl torch --reward cpu --precision fp32 --dedupe_greedy 0
@@ -73,6 +79,9 @@ def parse():
     p.add_argument('--num_layers', type=int, default=1)
     p.add_argument('--grad_wire', default='fp32', choices=['fp32', 'bf16'],
                    help='DP gradient reduction: fp32 all-reduce or bf16 wire / fp32 accumulation')
+    p.add_argument('--att8', type=int, default=1,
+                   help='scst with --num_chunks 1: also time the 8-frame temporal-attention '
+                        'config in the same invocation and report it as the "att8" field')
     p.add_argument('--json_out', default='')
     p.add_argument('--profile_phases', type=int, default=0,
                    help='print the mean per-phase GPU time (HIP events) of the timed steps')
@@ -104,35 +113,29 @@ def relaunch_if_needed(a):
     sys.exit(subprocess.call(cmd))
 
 
-def main():
-    a = parse()
-    relaunch_if_needed(a)
+def run_config(a, ctx, num_chunks, sync, sync_debug=0):
+    """Build the dataset, model, engine and trainer for ``num_chunks`` frames
+    per video, run ``a.warmup`` untimed and ``a.steps`` timed steps (barrier +
+    synchronize on both sides, MAX over ranks) and free the GPU buffers."""
+    import gc
     import torch
     from cst_captioning_amd.config import default_opts
     from cst_captioning_amd.data import CaptionLoader, make_synthetic
-    from cst_captioning_amd.parallel import init_distributed
     from cst_captioning_amd.cli import build_model, seed_everything
     from cst_captioning_amd.train.trainer import Trainer
 
-    ctx = init_distributed()
-    if ctx.world_size != a.gpus:
-        print('bench.py: --gpus %d but the job has %d rank(s) (WORLD_SIZE=%s)'
-              % (a.gpus, ctx.world_size, os.environ.get('WORLD_SIZE')), file=sys.stderr)
-        ctx.destroy()
-        sys.exit(3)
-    if a.impl == 'torch':
-        os.environ['CSTCAP_ALLOW_TORCH_FALLBACK'] = '1'
     seed_everything(a.seed, ctx.rank)
     t_gen = time.time()
     ds = make_synthetic('msrvtt', num_videos=a.videos, vocab_size=a.vocab, seed=a.seed,
-                        num_chunks=a.num_chunks)
+                        num_chunks=num_chunks)
     t_gen = time.time() - t_gen
     S = 20
     opt = default_opts(
         batch_size=a.batch_size, train_seq_per_img=S, test_seq_per_img=S, rnn_size=512,
         input_encoding_size=512 * len(ds.feat_dims) if a.model_type == 'standard' else 512,
-        drop_prob_lm=0.5, rnn_type=a.rnn_type, num_layers=a.num_layers, learning_rate=1e-4, grad_clip=0.25,
-        model_type=a.model_type, num_chunks=a.num_chunks, eval_metric='CIDEr', max_epochs=10 ** 9, print_log_interval=0,
+        drop_prob_lm=0.5, rnn_type=a.rnn_type, num_layers=a.num_layers, learning_rate=1e-4,
+        grad_clip=0.25, model_type=a.model_type, num_chunks=num_chunks, eval_metric='CIDEr',
+        max_epochs=10 ** 9, print_log_interval=0,
         use_rl=1 if a.mode != 'xe' else 0, use_rl_after=0, use_cst=1 if a.mode == 'cst' else 0,
         use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=2, scb_captions=S,
         impl=a.impl, precision=a.precision, reward_device=a.reward,
@@ -158,11 +161,10 @@ def main():
             return {'loss': seq.float().mean()}
         return trainer.train_step(data, 0)
 
-    sync = torch.cuda.synchronize if dev.type == 'cuda' else (lambda: None)
     for _ in range(a.warmup):
         out = step()
     sync()
-    if a.sync_debug and dev.type == 'cuda':
+    if sync_debug and dev.type == 'cuda':
         import warnings
         warnings.simplefilter('always')
         torch.cuda.set_sync_debug_mode('warn')
@@ -191,10 +193,48 @@ def main():
     sync()
     dt = time.perf_counter() - t0
     dt = ctx.max_scalar(dt)
-    loss = float(out['loss'])
-    ms = dt / a.steps * 1e3
-    caps = a.batch_size * S * ctx.world_size * a.steps / dt
-    vids = a.batch_size * ctx.world_size * a.steps / dt
+    res = {'dt': dt, 'ms': dt / a.steps * 1e3, 'loss': float(out['loss']),
+           'caps': a.batch_size * S * ctx.world_size * a.steps / dt,
+           'vids': a.batch_size * ctx.world_size * a.steps / dt, 'phases': phases,
+           'skipped': int(trainer.optimizer.skipped().item()),
+           'exp_fix': int(engine.exp_fix_rows.item()) if engine is not None else None,
+           'graph': int(trainer._graph is not None), 'n_params': n_params, 't_gen': t_gen,
+           'bf16': engine is not None or trainer.autocast_bf16}
+    del trainer, model, engine, loader, ds, step, out
+    gc.collect()
+    if dev.type == 'cuda':
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    a = parse()
+    relaunch_if_needed(a)
+    import torch
+    from cst_captioning_amd.parallel import init_distributed
+
+    ctx = init_distributed()
+    if ctx.world_size != a.gpus:
+        print('bench.py: --gpus %d but the job has %d rank(s) (WORLD_SIZE=%s)'
+              % (a.gpus, ctx.world_size, os.environ.get('WORLD_SIZE')), file=sys.stderr)
+        ctx.destroy()
+        sys.exit(3)
+    if a.impl == 'torch':
+        os.environ['CSTCAP_ALLOW_TORCH_FALLBACK'] = '1'
+    sync = torch.cuda.synchronize if ctx.device.type == 'cuda' else (lambda: None)
+    main_run = run_config(a, ctx, a.num_chunks, sync, sync_debug=a.sync_debug)
+    att8 = None
+    if a.att8 and a.mode == 'scst' and a.num_chunks == 1:
+        # the temporal-attention variant of the same job (8 frames per video),
+        # same steps / warmup, measured after the headline run's buffers are freed
+        r = run_config(a, ctx, 8, sync)
+        att8 = {'value': round(r['caps'], 2), 'ms_per_step': round(r['ms'], 3),
+                'temporal_attention_frames': 8, 'final_loss': r['loss'],
+                'skipped_steps': r['skipped']}
+    dt, ms, caps, vids = main_run['dt'], main_run['ms'], main_run['caps'], main_run['vids']
+    loss, n_params, t_gen = main_run['loss'], main_run['n_params'], main_run['t_gen']
+    S = 20
     baseline = None
     if os.path.exists(BASELINE_FILE):
         with open(BASELINE_FILE) as f:
@@ -216,7 +256,7 @@ def main():
         'vs_baseline': round(caps / baseline, 3) if (baseline and a.mode == 'scst') else None,
         # effective compute dtype: the fused engine is bf16; the PyTorch path is
         # bf16 under autocast with --precision bf16 on a GPU, else fp32
-        'dtype': 'bf16' if (engine is not None or trainer.autocast_bf16) else 'fp32',
+        'dtype': 'bf16' if main_run['bf16'] else 'fp32',
         'data': 'synthetic (MSR-VTT-shaped, random-init weights)',
         'config': {'model': 'CaptionModel %s %s%s-512 (resnet+c3d+mfcc+category, '
                             'V=%d, L=30)' % (a.model_type, a.rnn_type.upper(),
@@ -227,19 +267,23 @@ def main():
                    'parallelism': 'dp%d' % ctx.world_size, 'impl': a.impl,
                    'reward': a.reward, 'mode': a.mode, 'params': n_params,
                    'dedupe_greedy': a.dedupe_greedy,
-                   'cuda_graph': int(trainer._graph is not None),
+                   'cuda_graph': main_run['graph'],
                    'grad_wire': a.grad_wire,
                    'temporal_attention_frames': a.num_chunks if a.num_chunks > 1 else None},
         'final_loss': loss, 'datagen_s': round(t_gen, 1),
         # optimizer updates the NaN guard skipped (non-finite loss or gradient
         # norm) over warmup + timed steps, all ranks agree (adam.hip)
-        'skipped_steps': int(trainer.optimizer.skipped().item()),
+        'skipped_steps': main_run['skipped'],
         # exp-store rows the backward recomputed (LSE jump > 60 between steps)
-        'exp_fix_rows': int(engine.exp_fix_rows.item()) if engine is not None else None,
+        'exp_fix_rows': main_run['exp_fix'],
         'world_size_seen': ctx.world_size, 'backend': ctx.backend or 'none',
     }
-    if phases:
-        rec['phases_ms'] = {k: round(v, 3) for k, v in phases.items()}
+    if att8 is not None:
+        # BASELINE.json's metric names the LSTM-attn decoder: its temporal-
+        # attention config (C = 8 frames, MFMA attention) on the same job
+        rec['att8'] = att8
+    if main_run['phases']:
+        rec['phases_ms'] = {k: round(v, 3) for k, v in main_run['phases'].items()}
     if ctx.is_main:
         line = json.dumps(rec)
         print(line, flush=True)

@@ -52,6 +52,10 @@ def test_bench_json_line(world, launcher):
     assert rec['backend'] == ('gloo' if world > 1 else 'none')
     # whole-job value = global captions / step time
     assert abs(rec['value'] - 4 * 20 * world / (rec['ms_per_step'] / 1e3)) < 0.02 * rec['value']
+    # the 8-frame temporal-attention config, timed in the same invocation
+    att = rec['att8']
+    assert att['temporal_attention_frames'] == 8 and att['value'] > 0
+    assert abs(att['value'] - 4 * 20 * world / (att['ms_per_step'] / 1e3)) < 0.02 * att['value']
 
 
 def test_bench_world_size_mismatch_fails():
