@@ -279,7 +279,13 @@ class FlatGradBucket:
         lo, hi = self.shard_range(ctx.rank)
         if not hasattr(self, '_gshard') or self._gshard.numel() != hi - lo:
             self._gshard = torch.empty(hi - lo, dtype=self.grad.dtype, device=self.grad.device)
-        dist.reduce_scatter_tensor(self._gshard, self.grad, op=dist.ReduceOp.SUM)
+        if ctx.backend == 'gloo' and self.grad.is_cuda:
+            # gloo has no reduce-scatter of device tensors (the shared-GPU
+            # tests): the same sums through an all-reduce, then this shard
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+            self._gshard.copy_(self.grad[lo:hi])
+        else:
+            dist.reduce_scatter_tensor(self._gshard, self.grad, op=dist.ReduceOp.SUM)
         return self._gshard
 
     def all_gather_params(self, ctx):

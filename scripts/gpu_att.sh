@@ -1,5 +1,6 @@
 #!/bin/bash
-# attention + graph + headline GPU tests, attention microbenchmarks, benches
+# attention + graph + headline GPU tests, attention microbenchmarks, benches,
+# kernel-trace profiles of the concat and att8 steps
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -8,7 +9,8 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_attention_headline.py tests
 rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 200 python scripts/microbench_att.py > gpurun_out/mb_att.json 2> gpurun_out/mb_att.err || exit $?
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --num_chunks 8 > gpurun_out/bench_att8.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_hip.log 2>&1 || exit $?
-CSTCAP_VH_SCHED=2 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_hip_vh2.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_hip.log 2>&1 || exit $?
+CSTCAP_VH_SCHED=2 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --att8 0 > gpurun_out/bench_hip_vh2.log 2>&1 || exit $?
+TAG=rc bash scripts/gpu_prof.sh || exit $?
+TAG=att8 BENCH_ARGS="--num_chunks 8" bash scripts/gpu_prof.sh || exit $?
 exit $rc

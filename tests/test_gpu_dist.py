@@ -26,8 +26,9 @@ def _free_port():
     return p
 
 
-def _run(world, out, graph, wire='fp32'):
-    env = dict(os.environ, CSTCAP_TEST_GRAPH=str(graph), CSTCAP_TEST_WIRE=wire)
+def _run(world, out, graph, wire='fp32', update='allreduce'):
+    env = dict(os.environ, CSTCAP_TEST_GRAPH=str(graph), CSTCAP_TEST_WIRE=wire,
+               CSTCAP_TEST_DPUPDATE=update)
     env.update(PYTHONPATH=ROOT + os.pathsep + env.get('PYTHONPATH', ''), CSTCAP_SHARE_GPU='1',
                CSTCAP_DIST_BACKEND='gloo', CSTCAP_TEST_IMPL='hip', OMP_NUM_THREADS='4',
                PYTHONFAULTHANDLER='1')
@@ -75,3 +76,19 @@ def test_engine_dp_allreduce_matches_single_process(tmp_path, graph, wire):
         assert ((got - ref).abs() <= bound).all()
     assert r2['same_after_steps']
     assert r1['predictions'] == r2['predictions']
+
+
+def test_engine_dp_sharded_update_matches_allreduce(tmp_path):
+    """--dp_update sharded on the GPU (HIP-graph steps, fused engine): the
+    reduce-scattered gradient, the Adam update of each rank's 1/N shard with
+    the global clip norm and the all-gather give the parameters and moments of
+    the all-reduce path, keep the ranks identical and skip everywhere on one
+    rank's NaN loss."""
+    os.environ['CSTCAP_TEST_IMPL'] = 'hip'
+    a = _run(2, str(tmp_path / 'ar.pt'), 1)
+    b = _run(2, str(tmp_path / 'sh.pt'), 1, update='sharded')
+    torch.testing.assert_close(b['params_after'], a['params_after'], rtol=1e-5, atol=1e-6)
+    for x, y in zip(b['moments'], a['moments']):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-10)
+    assert b['same_after_steps'] and b['nan_skip_all']
+    assert b['steps_done'] == a['steps_done'] and b['skipped'] == a['skipped'] == 1
