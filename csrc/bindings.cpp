@@ -50,6 +50,11 @@ std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
                                           std::vector<at::Tensor> outs);
 std::vector<at::Tensor> att_mfma_fwd(at::Tensor h, at::Tensor wq, at::Tensor P, at::Tensor wa,
                                      at::Tensor ba, at::Tensor gv);
+std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor wlog,
+                                         at::Tensor blog, at::Tensor whh, at::Tensor vgate,
+                                         int64_t vdiv, at::Tensor tgt, at::Tensor eoff,
+                                         int64_t save, int64_t mode, int64_t step, at::Tensor rng,
+                                         int64_t rr);
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);
@@ -130,6 +135,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("token_sort", &cst::token_sort);
   m.def("token_group_sum", &cst::token_group_sum);
   m.def("vocab_select", &cst::vocab_select);
+  m.def("decode_step_test", &cst::decode_step_test);
   m.def("att_mfma_fwd", &cst::att_mfma_fwd);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);

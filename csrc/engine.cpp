@@ -175,8 +175,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor g_sel = at::empty({R, T - 1}, f32);
   at::Tensor g_xe = want_xe ? at::empty({R, T}, f32) : at::Tensor();
   at::Tensor lse = at::empty({n_steps, R}, f32);
-  const int n_vt = vocab_num_tiles((int)V);
-  at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4}, f32);
+  at::Tensor part =
+      at::empty({(int64_t)vocab_part_slots((int)V) * R * vocab_partial_bytes() / 4}, f32);
   at::Tensor counts = at::zeros({(T + 1) * combine_count_ints_per_step()},
                                 at::TensorOptions().dtype(at::kInt).device(dev));
   at::Tensor unfinished =
@@ -365,14 +365,13 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                        save ? q_next.data_ptr<float>() : nullptr, att_ep.data_ptr<float>(),
                        att_cnt.data_ptr<int>()};
     const bool q_tiles = has_att && !att_mfma;  // W_q tiles in the recurrent GEMM
-    launch_vocab_lstm_fwd(vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
-                          save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl,
-                          part.data_ptr(), tgt, L, vflags, inv_temp, RNG, (int)t,
-                          h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
-                          next ? pre.data_ptr<float>() : nullptr, st, q_tiles ? (int)A : 0,
-                          q_tiles && next ? q_next.data_ptr<float>() : nullptr,
-                          exp_t ? lse[t - 1].data_ptr<float>() : nullptr,
-                          att_mfma && next ? &am : nullptr);
+    const int n_vt = launch_vocab_lstm_fwd(
+        vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
+        save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl, part.data_ptr(),
+        tgt, L, vflags, inv_temp, RNG, (int)t, h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
+        next ? pre.data_ptr<float>() : nullptr, st, q_tiles ? (int)A : 0,
+        q_tiles && next ? q_next.data_ptr<float>() : nullptr,
+        exp_t ? lse[t - 1].data_ptr<float>() : nullptr, att_mfma && next ? &am : nullptr);
     if (q_tiles && next)
       launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), q_next.data_ptr<float>(),
                      nullptr, a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv,
@@ -1439,6 +1438,71 @@ std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor 
                        tok.data_ptr<int64_t>(), 1, nullptr, 0, nullptr, 0, nullptr, 0, (int)mode,
                        0.f, rng_ptr(rng), (int)step, nullptr, 0, nullptr, st);
   return {tok.view({R}), lse};
+}
+
+// One decode step (vocab projection + recurrent GEMM + combine without the
+// cell), for tests of the two launch forms: rr = 1 row-resident (vocab_rr.h),
+// 0 tiled, -1 default.  save: 0 none, 1 fp16 logits, 2 exp store (eoff given).
+// Returns {lse, tok, g_sel, g_xe, saved rows (R, ldl), pre (R, 4H), n_parts}.
+std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor wlog,
+                                         at::Tensor blog, at::Tensor whh, at::Tensor vgate,
+                                         int64_t vdiv, at::Tensor tgt, at::Tensor eoff,
+                                         int64_t save, int64_t mode, int64_t step, at::Tensor rng,
+                                         int64_t rr) {
+  check_cuda(hd, "hd");
+  check_cuda(wlog, "wlog");
+  const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
+  TORCH_CHECK(hd.scalar_type() == at::kBFloat16 && wlog.scalar_type() == at::kBFloat16 &&
+                  hd.is_contiguous() && wlog.is_contiguous() && wlog.size(1) == H &&
+                  blog.scalar_type() == at::kFloat && blog.numel() == V, "hd / wlog / blog");
+  const bool lstm = whh.defined() && whh.numel() > 0;
+  if (lstm)
+    TORCH_CHECK(h.scalar_type() == at::kBFloat16 && h.is_contiguous() && h.sizes() == hd.sizes() &&
+                    whh.scalar_type() == at::kBFloat16 && whh.is_contiguous() &&
+                    whh.size(0) == 4 * H && whh.size(1) == H, "h / whh");
+  const bool has_vg = vgate.defined() && vgate.numel() > 0;
+  if (has_vg)
+    TORCH_CHECK(vgate.scalar_type() == at::kFloat && vgate.is_contiguous() &&
+                    vgate.size(0) * vdiv == R && vgate.size(1) == 4 * H, "vgate (R / vdiv, 4H)");
+  const bool has_tgt = tgt.defined() && tgt.numel() > 0;
+  if (has_tgt) TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.numel() == R, "tgt (R) int64");
+  if (save == 2)
+    TORCH_CHECK(eoff.defined() && eoff.scalar_type() == at::kFloat && eoff.numel() == R, "eoff (R)");
+  auto dev = hd.device();
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+  const int64_t ldl = (V + 63) / 64 * 64;
+  at::Tensor part = at::empty({(int64_t)vocab_part_slots((int)V) * R * vocab_partial_bytes() / 4}, f32);
+  at::Tensor saved = save ? at::zeros({R, ldl}, at::TensorOptions()
+                                                    .dtype(save == 2 ? at::kBFloat16 : at::kHalf)
+                                                    .device(dev))
+                          : at::Tensor();
+  at::Tensor pre = lstm ? at::zeros({R, 4 * H}, f32) : at::Tensor();
+  at::Tensor lse = at::empty({R}, f32), gsel = at::zeros({R}, f32), gxe = at::zeros({R}, f32);
+  at::Tensor tok = at::zeros({R}, at::TensorOptions().dtype(at::kLong).device(dev));
+  hipStream_t st = cur_stream();
+  const int flags = (mode == SEL_SAMPLE_H ? 1 : 0) | (mode == SEL_GREEDY_H ? 2 : 0) | (save == 2 ? 16 : 0);
+  set_decode_rr((int)rr);
+  int n = 0;
+  try {
+    n = launch_vocab_lstm_fwd(
+        reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R, (int)H,
+        reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(), (int)V,
+        save ? reinterpret_cast<uint16_t*>(saved.data_ptr()) : nullptr, ldl, part.data_ptr(),
+        has_tgt ? tgt.data_ptr<int64_t>() : nullptr, 1, flags, 1.f, rng_ptr(rng), (int)step,
+        lstm ? reinterpret_cast<const uint16_t*>(h.data_ptr()) : nullptr,
+        lstm ? reinterpret_cast<const uint16_t*>(whh.data_ptr()) : nullptr,
+        has_vg ? vgate.data_ptr<float>() : nullptr, (int)vdiv, lstm ? pre.data_ptr<float>() : nullptr,
+        st, 0, nullptr, save == 2 ? eoff.data_ptr<float>() : nullptr, nullptr);
+  } catch (...) {
+    set_decode_rr(-1);
+    throw;
+  }
+  set_decode_rr(-1);
+  launch_vocab_combine(part.data_ptr(), n, (int)R, lse.data_ptr<float>(), tok.data_ptr<int64_t>(), 1,
+                       gsel.data_ptr<float>(), 1, has_tgt ? gxe.data_ptr<float>() : nullptr, 1,
+                       has_tgt ? tgt.data_ptr<int64_t>() : nullptr, 1, (int)mode, 0.f, rng_ptr(rng),
+                       (int)step, nullptr, 0, nullptr, st);
+  return {lse, tok, gsel, gxe, saved, pre, at::full({1}, n, at::TensorOptions().dtype(at::kLong))};
 }
 
 // the counting sort itself, for tests: returns {stok, srow} (int32)

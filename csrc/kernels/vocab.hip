@@ -35,30 +35,11 @@
 #include "gemm_tile.h"
 #include "lstm_gemm.h"
 #include "att_mfma.h"
+#include "vocab_common.h"
+#include "vocab_rr.h"
 #include "../launchers.h"
 
 namespace cst {
-
-struct VocabPartial {  // 32 bytes per (tile, row)
-  float m;       // max logit in tile
-  float s;       // sum exp(x - m)
-  float zval;    // max of x/temp + gumbel
-  float zlogit;  // logit at zidx
-  int zidx;      // sampled token candidate
-  int xidx;      // argmax token (first on ties)
-  float xtgt;    // logit of the target token (-inf if not in tile)
-  float pad;
-};
-
-// XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch),
-// so consecutive ids of the remapped index land on the same XCD's L2.  Vocab
-// tiles are the outer index: the 8 XCDs each stream a contiguous 1/8 of W
-// (~1.3 MB at V=10.5k, H=512) and every row tile re-reads it from their L2.
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (bid >> 3);
-}
 
 // -------------------------------------------------------------------------------
 // Transposed epilogue: the MFMA computes C^T = W . h_drop^T (vocab rows
@@ -83,16 +64,6 @@ __host__ __device__ constexpr int exp_stage_off(int BN) { return 4 * BN * 32; }
 __host__ __device__ constexpr int epilogue_lds_bytes(int BN) {
   return exp_stage_off(BN) + BN * EXP_STAGE_LD * 2;
 }
-// VF_EXP: the saved copy is E = exp(x - eoff[r]) in bf16 instead of fp16 x
-// (eoff = the row's LSE of the previous decode step), see vocab_grad.hip
-enum VocabFlags : int {
-  VF_SAMPLE = 1,
-  VF_ARGMAX = 2,
-  VF_BENCH_MAINLOOP = 4,
-  VF_SAVE_F32 = 8,
-  VF_EXP = 16
-};
-
 struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS (exp_stage_off)
   float m, s, zkey, zlogit;
   int zidx, xidx;
@@ -621,7 +592,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
         unfinished[r] = u;
         if (!u) tok = 0;
       }
-      CST_DCHECK(tok >= 0 && tok < (int64_t)n_vt * VT_V);
+      CST_DCHECK(tok >= 0);
       tok_out[(int64_t)r * tok_stride] = tok;
       if (g_sel) g_sel[(int64_t)r * gsel_stride] = tl - lse;
       if (counts != nullptr && tok != 0) atomicAdd(&s_nonzero, 1);
@@ -839,12 +810,127 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   post_launch("vocab_lstm_fwd_kernel", stream);
 }
 
-void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
-                           const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
-                           const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
-                           const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
-                           const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
-                           float* q_out, const float* eoff, const AttMfmaArgs* att) {
+// ---- row-resident launch (vocab_rr.h) -------------------------------------------
+static int device_cu_count() {
+  static int n[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int c = 0;
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    n[dev] = c > 0 ? c : 256;
+  }
+  return n[dev];
+}
+
+// CSTCAP_DECODE_RR=0 selects the tiled launch everywhere (A/B runs); tests
+// force either launch with set_decode_rr
+static int g_rr_override = -1;
+void set_decode_rr(int on) { g_rr_override = on; }
+static bool rr_enabled() {
+  if (g_rr_override >= 0) return g_rr_override == 1;
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CSTCAP_DECODE_RR");
+    on = (e != nullptr && e[0] == '1') ? 1 : 0;  // (off until measured on the GPU)
+  }
+  return on == 1;
+}
+
+int vocab_part_slots(int V) {
+  const int a = (V + VT_V - 1) / VT_V, b = (V + RR_UNIT - 1) / RR_UNIT;
+  return a > b ? a : b;
+}
+
+template <int SAMPLE, int STORE, int ARGMAX>
+static void launch_rr_t(const RRArgs& a, int grid, int lds, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)vocab_rr_kernel<SAMPLE, STORE, ARGMAX>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RR_MAX_LDS);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((vocab_rr_kernel<SAMPLE, STORE, ARGMAX>), dim3(grid), dim3(RR_THREADS), lds,
+                     stream, a);
+  post_launch("vocab_rr_kernel", stream);
+}
+
+// Geometry of the row-resident launch; false when the shape is not covered
+// (the tiled launch runs instead).  Row groups of 256 rows; per row group
+// about (CUs / row groups) workgroups, split between the vocabulary units
+// (64 weight rows, with the softmax epilogue) and the recurrent units by
+// their measured relative cost.
+static bool rr_plan(int R, int H, int V, int G4, bool lstm, const float* vgate, int vdiv,
+                    RRArgs& a, int& grid, int& lds) {
+  if (H != RR_K || R < 2 * RR_BROWS || !rr_enabled()) return false;
+  if (lstm && G4 % RR_UNIT != 0) return false;
+  const int n_rg = (R + RR_BROWS - 1) / RR_BROWS;
+  const int per = std::max(2, device_cu_count() / n_rg);
+  const int nuv = (V + RR_UNIT - 1) / RR_UNIT, nul = lstm ? G4 / RR_UNIT : 0;
+  constexpr float COST_V = 2.7f, COST_L = 2.0f;  // per unit
+  int nbl = 0;
+  if (lstm) {
+    const float per_wg = (nuv * COST_V + nul * COST_L) / per;
+    nbl = std::max(1, std::min(nul, (int)(nul * COST_L / per_wg + 0.5f)));
+  }
+  const int nbv = std::max(1, std::min(nuv, per - nbl));
+  a.n_rg = n_rg, a.nbv = nbv, a.nbl = nbl, a.nuv = nuv, a.nul = nul;
+  const int bias_bytes = (nuv + nbv - 1) / nbv * RR_UNIT * 4;
+  int vg_bytes = 0;
+  a.vg_cols = lstm ? (nul + nbl - 1) / nbl * RR_UNIT : 0;
+  a.vg_vids = 1;
+  if (lstm && vgate != nullptr) {
+    if (vdiv < 1) return false;
+    a.vg_vids = (RR_BROWS - 1) / vdiv + 2;
+    vg_bytes = a.vg_vids * a.vg_cols * 4;
+  } else if (lstm) {
+    vg_bytes = a.vg_cols * 4;
+  }
+  lds = RR_FIXED_LDS + std::max(bias_bytes, vg_bytes);
+  if (lds > RR_MAX_LDS) return false;
+  grid = n_rg * (nbv + nbl);
+  return true;
+}
+
+int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+                          const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
+                          const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
+                          const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
+                          const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
+                          float* q_out, const float* eoff, const AttMfmaArgs* att) {
+  // Row-resident launch (vocab_rr.h) where it applies: H = 512, >= 512 rows,
+  // no attention workgroups or query tiles, temperature 1 when sampling.
+  const bool sample = (flags & VF_SAMPLE) != 0, argmax = (flags & VF_ARGMAX) != 0;
+  if (att == nullptr && NQ == 0 && !(flags & (VF_SAVE_F32 | VF_BENCH_MAINLOOP)) &&
+      (!sample || inv_temp == 1.f) && !(sample && argmax) && (ldl % RR_UNIT == 0 || !logits16)) {
+    RRArgs a{};
+    int grid = 0, lds = 0;
+    if (rr_plan(R, H, V, 4 * H, pre != nullptr, vgate, vdiv, a, grid, lds)) {
+      a.hd = hd, a.ldh = ldh, a.R = R, a.V = V, a.W = W, a.bias = bias;
+      a.out16 = logits16, a.ldl = ldl, a.part = (VocabPartial*)part;
+      a.tgt = tgt, a.tgt_stride = tgt_stride, a.rng = rng, a.step = step, a.eoff = eoff;
+      a.h = h_t, a.whh = whh, a.vgate = vgate, a.vdiv = vdiv, a.pre = pre, a.G4 = 4 * H;
+      const int store = logits16 == nullptr ? RR_ST_NONE : (flags & VF_EXP) ? RR_ST_EXP : RR_ST_F16;
+      if ((flags & VF_EXP) && eoff == nullptr) throw std::runtime_error("vocab_rr: exp store needs eoff");
+#define RRV(S, ST, A) launch_rr_t<S, ST, A>(a, grid, lds, stream)
+      if (sample) {
+        if (store == RR_ST_EXP) RRV(1, RR_ST_EXP, 0);
+        else if (store == RR_ST_F16) RRV(1, RR_ST_F16, 0);
+        else RRV(1, RR_ST_NONE, 0);
+      } else if (argmax) {
+        if (store == RR_ST_EXP) RRV(0, RR_ST_EXP, 1);
+        else if (store == RR_ST_F16) RRV(0, RR_ST_F16, 1);
+        else RRV(0, RR_ST_NONE, 1);
+      } else {
+        if (store == RR_ST_EXP) RRV(0, RR_ST_EXP, 0);
+        else if (store == RR_ST_F16) RRV(0, RR_ST_F16, 0);
+        else RRV(0, RR_ST_NONE, 0);
+      }
+#undef RRV
+      return a.nbv;
+    }
+  }
   // 64-row tiles, 3 blocks per CU (48 KB of LDS each; the recurrent tiles use
   // 2 stages to fit): one block's epilogue overlaps the others' main loops.
   // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
@@ -855,7 +941,7 @@ void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint
                                             vgate, vdiv, pre, NQ, q_out, stream, eoff, att)
   if (att == nullptr) {
     VL(0);
-    return;
+    return vocab_num_tiles(V);
   }
   check_att_mfma(*att);
   switch (att_variant(att->C)) {
@@ -865,6 +951,7 @@ void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint
     default: throw std::runtime_error("vocab_lstm_fwd: no attention variant");
   }
 #undef VL
+  return vocab_num_tiles(V);
 }
 
 void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,

@@ -1,0 +1,449 @@
+// Row-resident decode launch (gfx950): the vocabulary projection of step t and
+// the recurrent GEMM of step t+1 with their operand ROWS kept in registers.
+//
+// Why: the tiled launch (vocab_tr_block, 128 vocab x 64 caption-row tiles,
+// K = H = 512 staged through LDS per tile) re-streams both operands for every
+// tile: 13.8 GB x (1/64 + 1/128) = 320 MB of L2 -> CU traffic per decode step
+// at R = 1,280, V = 10,509, against the ~70 GB/s an MI355X CU draws from L2.
+// That, not the MFMAs, set its ~17 us main loop.
+//
+// Here each 512-thread workgroup (one per CU, the grid is one wave of the
+// chip) owns 256 caption rows -- each of its 8 waves (two per SIMD) holds 32
+// rows x 512 as bf16 MFMA B-fragments in 128 of its 256 registers -- and
+// streams a contiguous
+// slice of the weight rows through a 3-stage LDS ring, 32 rows (one MFMA M
+// tile, 32 KB) per chunk.  Every weight row is read once per row group, every
+// caption row once per workgroup: 5 row groups x 51 workgroups at R = 1,280
+// move ~130 MB, and the MFMA work (16.5 GFLOP) bounds the launch instead.
+//
+// Roles (per workgroup, uniform):
+//   vocab: B = hd_t (dropout applied), weights W_logit; per chunk the
+//     epilogue folds the chunk's logits into per-row running statistics held
+//     in registers (online max / sum of exp, argmax, target logit, an
+//     inverse-CDF draw inside the lane's 16 entries entered into an
+//     exponential race -- the same exact two-level sampler as vocab.hip) and
+//     writes the exp store E = exp(x - lse_{t-1}) (or fp16 logits at step 0)
+//     through a per-wave LDS staging tile as 64-byte row segments; one
+//     VocabPartial per (workgroup, row) at the end, merged by
+//     vocab_combine_kernel.
+//   lstm: B = h_t, weights W_hh (packed gates); pre_{t+1} = h_t W_hh^T +
+//     vgate[row / vdiv] (the workgroup's video-gate slice preloaded in LDS).
+//
+// The two waves of a SIMD run the chunk loop half a phase apart: between two
+// workgroup barriers an "early" wave (w < 4) issues chunk c's 32 MFMAs and
+// then chunk c's epilogue, a "late" wave (w >= 4, same SIMD) the epilogue of
+// chunk c-1 and then chunk c's MFMAs, so one wave's VALU epilogue runs beside
+// the other's MFMAs and each needs a single accumulator.  (64 rows per wave
+// at one wave per SIMD needed 256 registers of B fragments and spilled; so
+// did a second accumulator per wave.)  Weight chunks are loaded by LDS-DMA two chunks ahead; the counted
+// vmcnt waits assume the per-iteration vector-memory op order fixed by the
+// compiler barriers below (see rr_wait).
+#pragma once
+#include "gemm_tile.h"
+#include "vocab_common.h"
+
+namespace cst {
+
+constexpr int RR_WAVES = 8, RR_THREADS = 64 * RR_WAVES;
+constexpr int RR_WROWS = 32;                      // caption rows per wave (one MFMA N tile)
+constexpr int RR_BROWS = RR_WAVES * RR_WROWS;     // caption rows per workgroup
+constexpr int RR_CH = 32;                         // weight rows per chunk (one MFMA M tile)
+constexpr int RR_UNIT = 64;                       // weight rows per work unit (2 chunks)
+constexpr int RR_STAGES = 3;
+constexpr int RR_K = 512;                         // H
+constexpr int RR_NKS = RR_K / 16;                 // MFMA k-steps
+// LDS rows padded by 16 bytes (1040 B): the 16-lane groups of a ds_read_b128
+// (rows {0-3, 12-15, 20-27}, ... of the chunk) hit 16 distinct 4-bank slots, and
+// every fragment address is the lane's row base plus an immediate
+constexpr int RR_ROW_LD = RR_K * 2 + 16;
+constexpr int RR_CHUNK_BYTES = RR_CH * RR_ROW_LD;
+constexpr int RR_STG_LD = RR_CH + 8;              // staging row stride (16-bit entries, 80 B)
+constexpr int RR_STG_BYTES = RR_WROWS * RR_STG_LD * 2;
+constexpr int RR_FIXED_LDS = RR_STAGES * RR_CHUNK_BYTES + RR_WAVES * RR_STG_BYTES;
+constexpr int RR_MAX_LDS = 160 * 1024;
+
+enum RRStore : int { RR_ST_NONE = 0, RR_ST_EXP = 1, RR_ST_F16 = 2 };
+
+struct RRArgs {
+  // vocab role
+  const uint16_t* hd;
+  int ldh;
+  int R;
+  int V;
+  const uint16_t* W;
+  const float* bias;
+  uint16_t* out16;  // exp store / fp16 logits, row stride ldl (nullable)
+  int64_t ldl;
+  VocabPartial* part;  // (nbv, R)
+  const int64_t* tgt;
+  int64_t tgt_stride;
+  const uint32_t* rng;
+  int step;
+  const float* eoff;
+  // lstm role
+  const uint16_t* h;
+  const uint16_t* whh;
+  const float* vgate;  // (R / vdiv, G4) or nullptr
+  int vdiv;
+  float* pre;
+  int G4;
+  // geometry
+  int n_rg, nbv, nbl, nuv, nul;
+  int vg_vids, vg_cols;  // LDS video-gate slice: videos x columns (lstm role)
+};
+
+// LDS-DMA of one 32-row chunk: wave w moves rows 4w .. 4w+3, one 1 KiB row per
+// wave-instruction (lane l: bytes 16 l .. 16 l + 15 of the row).
+constexpr int RR_DMA_PER_WAVE = RR_CH / RR_WAVES;
+__device__ __forceinline__ void rr_issue(rsrc_t src, int row0, int nrows, char* dst, int w,
+                                         int lane) {
+#pragma unroll
+  for (int i = 0; i < RR_DMA_PER_WAVE; ++i) {
+    const int j = RR_DMA_PER_WAVE * w + i;
+    const int row = min(row0 + j, nrows - 1);
+    glds16(src, row * (RR_K * 2) + (lane << 4), 0, dst + j * RR_ROW_LD);
+  }
+}
+
+// 32 MFMAs of one chunk into acc (B fragments resident in hf)
+__device__ __forceinline__ void rr_mfma_chunk(const char* stage, int lane,
+                                              const bf16x8 (&hf)[RR_NKS], f32x16& acc) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const char* base = stage + (lane & 31) * RR_ROW_LD + (lane >> 5) * 16;
+#pragma unroll
+  for (int s = 0; s < RR_NKS; ++s) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + 32 * s);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hf[s], acc, 0, 0, 0);
+  }
+}
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void rr_store16(rsrc_t r, int off, uint4 v) {
+  const u32x4v x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
+}
+
+// Running statistics of one caption row over the lane's entries.
+struct RRRow {
+  float m, s;            // max, sum exp(x - m)
+  float zk, zl;          // race key, logit of the candidate
+  int zi;                // sampled candidate
+  float xm;              // argmax value
+  int xi;                // argmax index
+  float xt;              // target logit
+};
+
+__device__ __forceinline__ void rr_row_init(RRRow& a) {
+  a.m = -INFINITY;
+  a.s = 0.f;
+  a.zk = -INFINITY;
+  a.zl = 0.f;
+  a.zi = 0x7fffffff;
+  a.xm = -INFINITY;
+  a.xi = 0x7fffffff;
+  a.xt = -INFINITY;
+}
+
+__device__ __forceinline__ void rr_row_merge(RRRow& a, const RRRow& c) {
+  const float M = fmaxf(a.m, c.m);
+  a.s = (a.m == -INFINITY ? 0.f : a.s * __expf(a.m - M)) +
+        (c.m == -INFINITY ? 0.f : c.s * __expf(c.m - M));
+  a.m = M;
+  if (c.zk > a.zk || (c.zk == a.zk && c.zi < a.zi)) {
+    a.zk = c.zk;
+    a.zi = c.zi;
+    a.zl = c.zl;
+  }
+  if (c.xm > a.xm || (c.xm == a.xm && c.xi < a.xi)) {
+    a.xm = c.xm;
+    a.xi = c.xi;
+  }
+  a.xt = fmaxf(a.xt, c.xt);
+}
+
+// Epilogue of one (chunk, 32-row tile) for the lane's caption row: entries
+// v(k) = v0 + 8 (k >> 2) + 4 hi + (k & 3), k < 16.
+template <int SAMPLE, int STORE, int ARGMAX>
+__device__ __forceinline__ void rr_vocab_epi(const f32x16& acc, const float (&bb)[16], RRRow& st,
+                                             int v0, int hi, float eo, int tg, uint32_t rowkey,
+                                             uint16_t* stg) {
+  constexpr float L2E = 1.4426950408889634f;
+  float x[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) x[k] = acc[k] + bb[k];
+  float mc = x[0];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) mc = fmaxf(mc, x[k]);
+  const float mn = fmaxf(st.m, mc);
+  const float mns = mn == -INFINITY ? 0.f : mn;
+  const float ml = mns * L2E;
+  float e[16];
+  float sc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    e[k] = __builtin_amdgcn_exp2f(fmaf(x[k], L2E, -ml));
+    sc += e[k];
+  }
+  st.s = fmaf(st.s, __builtin_amdgcn_exp2f(fmaf(st.m, L2E, -ml)), sc);
+  st.m = mn;
+  if constexpr (STORE == RR_ST_EXP) {
+    // E = exp(x - eo) = exp(x - m) exp(m - eo) (bf16; rows whose LSE jumps
+    // by > 60 between steps are recomputed by the backward, vocab_grad.hip)
+    const float f = __builtin_amdgcn_exp2f((mns - eo) * L2E);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(e[4 * q] * f) | ((uint32_t)f2bf(e[4 * q + 1] * f) << 16);
+      pk.y = (uint32_t)f2bf(e[4 * q + 2] * f) | ((uint32_t)f2bf(e[4 * q + 3] * f) << 16);
+      *reinterpret_cast<uint2*>(stg + 8 * q + 4 * hi) = pk;
+    }
+  } else if constexpr (STORE == RR_ST_F16) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint2 pk;
+      pk.x = (uint32_t)f2h(x[4 * q]) | ((uint32_t)f2h(x[4 * q + 1]) << 16);
+      pk.y = (uint32_t)f2h(x[4 * q + 2]) | ((uint32_t)f2h(x[4 * q + 3]) << 16);
+      *reinterpret_cast<uint2*>(stg + 8 * q + 4 * hi) = pk;
+    }
+  }
+  const int vb = v0 + 4 * hi;
+  if constexpr (ARGMAX != 0) {
+    int ci = 0x7fffffff;
+#pragma unroll
+    for (int k = 15; k >= 0; --k) ci = x[k] == mc ? vb + 8 * (k >> 2) + (k & 3) : ci;
+    if (mc > st.xm) {
+      st.xm = mc;
+      st.xi = ci;
+    }
+  }
+  {  // target logit (tg = -1: no target)
+    const int d = tg - vb;
+    const bool mine = d >= 0 && d < 32 && (d & 4) == 0;
+    const int kk = mine ? (d >> 3) * 4 + (d & 3) : -1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st.xt = k == kk ? x[k] : st.xt;
+  }
+  if constexpr (SAMPLE != 0) {
+    // inverse CDF inside the lane's 16 weights, then the exponential race
+    // (key log(mass) - log(E), E ~ Exp(1)) across lanes, chunks and workgroups
+    const uint32_t key = mix32(rowkey ^ (uint32_t)(v0 >> 5) * 0xC2B2AE3Du ^ (uint32_t)hi * 0x27D4EB2Fu);
+    const float u = ((float)(key >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    const float tm = u * sc;
+    float cum = 0.f, cl = 0.f;
+    int cand = -1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      cum += e[k];
+      const bool hit = cand < 0 && cum >= tm && e[k] > 0.f;
+      cand = hit ? vb + 8 * (k >> 2) + (k & 3) : cand;
+      cl = hit ? x[k] : cl;
+    }
+    if (sc > 0.f && cand >= 0) {
+      const uint32_t key2 = mix32(key ^ 0x68E31DA4u);
+      const float u2 = ((float)(key2 >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      const float zk = mns + __logf(sc) - __logf(-__logf(u2));
+      if (zk > st.zk) {
+        st.zk = zk;
+        st.zi = cand;
+        st.zl = cl;
+      }
+    }
+  }
+}
+
+// Counted wait for this wave's LDS-DMA of the chunk about to be consumed.
+// Per iteration c the wave issues, in this order: DMA(c + 2) (4 ops, if any),
+// its epilogue stores (>= 0 ops).  DMA(c) was issued in iteration c - 2, so at
+// the top of iteration c at least 4 ops (DMA(c + 1)) follow it unless c is the
+// last chunk; the first and the last iterations drain everything.
+__device__ __forceinline__ void rr_wait(int c, int nc) {
+  if (c == 0 || c == nc - 1)
+    wait_vmcnt<0>();
+  else
+    wait_vmcnt<RR_DMA_PER_WAVE>();
+}
+
+// The chunk loop shared by both roles.  Iteration c: wait for chunk c's DMA,
+// barrier, refill the stage chunk c-1 used with chunk c+2, then (early wave)
+// MFMAs of chunk c + epilogue of chunk c, or (late wave) epilogue of chunk
+// c-1 + MFMAs of chunk c.
+template <class Epi>
+__device__ __forceinline__ void rr_chunk_loop(int nc, rsrc_t wsrc, int row0, int nrows, char* ring,
+                                              int w, int lane, const bf16x8 (&hf)[RR_NKS],
+                                              Epi&& epilogue) {
+  f32x16 acc;
+  const bool late = w >= RR_WAVES / 2;
+  for (int c = 0; c < nc; ++c) {
+    rr_wait(c, nc);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + 2 < nc)
+      rr_issue(wsrc, row0 + (c + 2) * RR_CH, nrows, ring + ((c + 2) % RR_STAGES) * RR_CHUNK_BYTES,
+               w, lane);
+    asm volatile("" ::: "memory");
+    const char* stage = ring + (c % RR_STAGES) * RR_CHUNK_BYTES;
+    if (late) {
+      if (c > 0) epilogue(c - 1, acc);
+      rr_mfma_chunk(stage, lane, hf, acc);
+    } else {
+      rr_mfma_chunk(stage, lane, hf, acc);
+      epilogue(c, acc);
+    }
+    asm volatile("" ::: "memory");
+  }
+  if (late) epilogue(nc - 1, acc);
+}
+
+template <int SAMPLE, int STORE, int ARGMAX>
+__device__ __forceinline__ void rr_vocab_block(const RRArgs& a, int rg, int slot, char* lds) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int hi = lane >> 5;
+  const int u0 = slot * a.nuv / a.nbv, u1 = (slot + 1) * a.nuv / a.nbv;
+  const int nc = (u1 - u0) * (RR_UNIT / RR_CH);
+  const int vbase = u0 * RR_UNIT;
+  char* ring = lds;
+  uint16_t* stg = reinterpret_cast<uint16_t*>(lds + RR_STAGES * RR_CHUNK_BYTES + w * RR_STG_BYTES);
+  float* sbias = reinterpret_cast<float*>(lds + RR_FIXED_LDS);
+  const rsrc_t wsrc = make_rsrc(a.W, (int64_t)a.V * RR_K * 2);
+  // weight chunks 0 and 1 in flight first
+  rr_issue(wsrc, vbase, a.V, ring, w, lane);
+  if (nc > 1) rr_issue(wsrc, vbase + RR_CH, a.V, ring + RR_CHUNK_BYTES, w, lane);
+  // the workgroup's bias slice (-inf past V) in LDS
+  for (int i = threadIdx.x; i < nc * RR_CH; i += RR_THREADS) {
+    const int v = vbase + i;
+    sbias[i] = v < a.V ? a.bias[v] : -INFINITY;
+  }
+  // resident B fragments: the wave's 32 caption rows of hd_t
+  const int rw = rg * RR_BROWS + w * RR_WROWS;
+  const int r = min(rw + (lane & 31), a.R - 1);
+  bf16x8 hf[RR_NKS];
+  {
+    const uint16_t* src = a.hd + (int64_t)r * a.ldh + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < RR_NKS; ++s) hf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+  }
+  // per-row constants
+  const float eo = (STORE == RR_ST_EXP) ? a.eoff[r] : 0.f;
+  const int tg = a.tgt != nullptr ? (int)a.tgt[(int64_t)r * a.tgt_stride] : -1;
+  const uint32_t rowkey = rng_seed(a.rng, RNG_SLOT_SAMPLE) ^
+                          mix32((uint32_t)r * 0x9E3779B1u + (uint32_t)a.step * 0x85EBCA77u);
+  RRRow st;
+  rr_row_init(st);
+  __syncthreads();  // bias slice
+  // stores through a buffer resource: rows >= R fall outside its range and
+  // are dropped by the hardware (no branch splits the pipelined loop body)
+  const rsrc_t osrc = make_rsrc(a.out16, STORE != RR_ST_NONE ? (int64_t)a.R * a.ldl * 2 : 0);
+  uint16_t* stg_row = stg + (lane & 31) * RR_STG_LD;
+  rr_chunk_loop(nc, wsrc, vbase, a.V, ring, w, lane, hf, [&](int c, const f32x16& acc) {
+    float bb[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b4 = *reinterpret_cast<const float4*>(sbias + c * RR_CH + 8 * q + 4 * hi);
+      bb[4 * q] = b4.x, bb[4 * q + 1] = b4.y, bb[4 * q + 2] = b4.z, bb[4 * q + 3] = b4.w;
+    }
+    const int v0 = vbase + c * RR_CH;
+    rr_vocab_epi<SAMPLE, STORE, ARGMAX>(acc, bb, st, v0, hi, eo, tg, rowkey, stg_row);
+    if constexpr (STORE != RR_ST_NONE) {
+      // the wave's 32 rows x 32 entries: 64-byte row segments, 16 B per lane
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int row = 16 * p + (lane >> 2), piece = lane & 3;
+        const uint4 val = *reinterpret_cast<const uint4*>(stg + row * RR_STG_LD + 8 * piece);
+        rr_store16(osrc, (rw + row) * (int)a.ldl * 2 + (v0 + 8 * piece) * 2, val);
+      }
+    }
+  });
+  // lanes l and l ^ 32 hold the two halves of a row's entries
+  RRRow o;
+  o.m = __shfl_xor(st.m, 32, 64);
+  o.s = __shfl_xor(st.s, 32, 64);
+  o.zk = __shfl_xor(st.zk, 32, 64);
+  o.zl = __shfl_xor(st.zl, 32, 64);
+  o.zi = __shfl_xor(st.zi, 32, 64);
+  o.xm = __shfl_xor(st.xm, 32, 64);
+  o.xi = __shfl_xor(st.xi, 32, 64);
+  o.xt = __shfl_xor(st.xt, 32, 64);
+  rr_row_merge(st, o);
+  if (hi == 0 && rw + (lane & 31) < a.R) {
+    VocabPartial p;
+    p.m = st.m;
+    p.s = st.s;
+    p.zval = st.zk;
+    p.zlogit = st.zl;
+    p.zidx = st.zi;
+    // argmax off: the max's index is not needed (greedy rows only)
+    p.xidx = ARGMAX ? st.xi : 0x7fffffff;
+    p.xtgt = st.xt;
+    p.pad = 0.f;
+    a.part[(int64_t)slot * a.R + rw + (lane & 31)] = p;
+  }
+}
+
+__device__ __forceinline__ void rr_lstm_block(const RRArgs& a, int rg, int slot, char* lds) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int hi = lane >> 5;
+  const int u0 = slot * a.nul / a.nbl, u1 = (slot + 1) * a.nul / a.nbl;
+  const int nc = (u1 - u0) * (RR_UNIT / RR_CH);
+  const int nbase = u0 * RR_UNIT;
+  char* ring = lds;
+  float* svg = reinterpret_cast<float*>(lds + RR_FIXED_LDS);
+  const rsrc_t wsrc = make_rsrc(a.whh, (int64_t)a.G4 * RR_K * 2);
+  rr_issue(wsrc, nbase, a.G4, ring, w, lane);
+  if (nc > 1) rr_issue(wsrc, nbase + RR_CH, a.G4, ring + RR_CHUNK_BYTES, w, lane);
+  const int r_first = rg * RR_BROWS;
+  const int vid0 = a.vgate != nullptr ? r_first / a.vdiv : 0;
+  const int ncols = nc * RR_CH;
+  {  // videos x the workgroup's columns (one zero row without video gates)
+    const int vmax = a.vgate != nullptr ? (a.R - 1) / a.vdiv : 0;
+    const int nv = a.vgate != nullptr ? a.vg_vids : 1;
+    for (int i = threadIdx.x; i < nv * ncols; i += RR_THREADS) {
+      const int vv = i / ncols, cc = i - vv * ncols;
+      svg[vv * a.vg_cols + cc] =
+          a.vgate != nullptr ? a.vgate[(int64_t)min(vid0 + vv, vmax) * a.G4 + nbase + cc] : 0.f;
+    }
+  }
+  const int rw = r_first + w * RR_WROWS;
+  const int r = min(rw + (lane & 31), a.R - 1);
+  bf16x8 hf[RR_NKS];
+  {
+    const uint16_t* src = a.h + (int64_t)r * RR_K + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < RR_NKS; ++s) hf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+  }
+  const int vrow = a.vgate != nullptr ? (r / a.vdiv - vid0) * a.vg_cols : 0;
+  __syncthreads();  // video-gate slice
+  const rsrc_t psrc = make_rsrc(a.pre, (int64_t)a.R * a.G4 * 4);
+  const int rst = rw + (lane & 31);  // (rows >= R: outside psrc, dropped)
+  rr_chunk_loop(nc, wsrc, nbase, a.G4, ring, w, lane, hf, [&](int c, const f32x16& acc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cl = c * RR_CH + 8 * q + 4 * hi;
+      const float4 g = *reinterpret_cast<const float4*>(svg + vrow + cl);
+      uint4 o;
+      o.x = __float_as_uint(acc[4 * q] + g.x);
+      o.y = __float_as_uint(acc[4 * q + 1] + g.y);
+      o.z = __float_as_uint(acc[4 * q + 2] + g.z);
+      o.w = __float_as_uint(acc[4 * q + 3] + g.w);
+      rr_store16(psrc, (rst * a.G4 + nbase + cl) * 4, o);
+    }
+  });
+}
+
+template <int SAMPLE, int STORE, int ARGMAX>
+__global__ __launch_bounds__(RR_THREADS, 1) void vocab_rr_kernel(RRArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int nwg = a.n_rg * (a.nbv + a.nbl);
+  const int L = xcd_remap((int)blockIdx.x, nwg);
+  // consecutive remapped ids share an XCD: the row groups of one weight slice
+  // read it from that XCD's L2
+  const int slot = L / a.n_rg, rg = L - slot * a.n_rg;
+  if (slot < a.nbv)
+    rr_vocab_block<SAMPLE, STORE, ARGMAX>(a, rg, slot, lds);
+  else
+    rr_lstm_block(a, rg, slot - a.nbv, lds);
+}
+
+}  // namespace cst

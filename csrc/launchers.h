@@ -115,10 +115,15 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           float ss_prob, const uint32_t* rng, int step, int* counts, int count_step,
                           uint8_t* unfinished, hipStream_t stream, const CellLaunch* cell = nullptr);
 // vocab projection of step t + recurrent GEMM of step t+1 in one launch
-// (transposed-epilogue vocab kernel; pre == nullptr: vocab only).  NQ > 0:
-// whh has 4H + NQ rows, the last NQ (W_q) produce the attention query q_out
-// (R x NQ) and vgate must be nullptr.
-void launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
+// (row-resident kernel vocab_rr.h where it applies, else the tiled
+// transposed-epilogue kernel; pre == nullptr: vocab only).  NQ > 0: whh has
+// 4H + NQ rows, the last NQ (W_q) produce the attention query q_out (R x NQ)
+// and vgate must be nullptr.  Returns the number of partial slots per row it
+// wrote into part (the combine's n_vt); part must hold vocab_part_slots(V) x R.
+int vocab_part_slots(int V);
+// -1: launch by CSTCAP_DECODE_RR (default row-resident); 0 / 1: force (tests)
+void set_decode_rr(int on);
+int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                            const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
