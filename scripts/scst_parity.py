@@ -6,6 +6,11 @@ reward on the GPU).  Prints one JSON line per log point:
  val_greedy_cider}.
 
 usage: python scripts/scst_parity.py IMPL [PRECISION] [XE_STEPS] [RL_STEPS]
+
+CSTCAP_PARITY_SHAPE=headline runs the headline model (concat LSTM-512, 4
+modalities, V = 10,509, 64 videos x 20 captions per step) instead of the
+small default (H = 256, V = 2,000, 32 videos).  Every log line also carries
+the optimizer's NaN-guard skip count and the exp-store rows recomputed.
 """
 import json
 import os
@@ -28,15 +33,20 @@ if impl == 'torch':
     os.environ['CSTCAP_ALLOW_TORCH_FALLBACK'] = '1'
 dev = torch.device('cuda', 0)
 torch.manual_seed(0)
-tr, va, _ = make_splits('msrvtt', vocab_size=2000, feat_dims=[256, 128], train_videos=1280,
-                        seed=0)
-opt = default_opts(batch_size=32, train_seq_per_img=20, rnn_size=256, input_encoding_size=256,
+HEADLINE = os.environ.get('CSTCAP_PARITY_SHAPE') == 'headline'
+if HEADLINE:
+    V_, FD_, NV_, B_, H_ = 10509, [2048, 4096, 1024, 300], 6513, 64, 512
+else:
+    V_, FD_, NV_, B_, H_ = 2000, [256, 128], 1280, 32, 256
+tr, va, _ = make_splits('msrvtt', vocab_size=V_, feat_dims=FD_, train_videos=NV_, seed=0,
+                        eval_videos=256 if HEADLINE else None)
+opt = default_opts(batch_size=B_, train_seq_per_img=20, rnn_size=H_, input_encoding_size=H_,
                    learning_rate=2e-3, max_epochs=10 ** 9, print_log_interval=0, impl=impl,
                    precision=precision, loglevel='WARNING', use_rl=1, use_rl_after=10 ** 6,
                    use_cst=0, use_mixer=1, mixer_from=1, use_eos=1, drop_prob_lm=0.5)
 opt.vocab = {i: w for i, w in enumerate(tr.vocab)}
 opt.vocab_size, opt.seq_length, opt.feat_dims = tr.vocab_size, tr.seq_length, tr.feat_dims
-loader = CaptionLoader(tr, 32, 20, 'train', dev, seed=0)
+loader = CaptionLoader(tr, B_, 20, 'train', dev, seed=0)
 val = CaptionLoader(va, 64, 20, 'test', dev)
 model, eng = build_model(opt, dev, impl)
 t = Trainer(opt, model, loader, None, DistContext(device=dev), eng)
@@ -80,6 +90,9 @@ def log(phase, step, out):
         rec.update(reward_mean=round(float(out['reward'].float().mean()), 5),
                    sample_cider=round(float(out['m']), 5), greedy_cider=round(float(out['b']), 5))
     rec['val_greedy_cider'] = round(val_cider(), 5)
+    rec['skipped'] = int(t.optimizer.skipped()) if hasattr(t.optimizer, 'skipped') else None
+    if eng is not None:
+        rec['exp_fix_rows'] = int(eng.exp_fix_rows.item())
     print(json.dumps(rec), flush=True)
 
 
