@@ -32,6 +32,8 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     int64_t K, int64_t T, int64_t bos_index,
                                     std::vector<at::Tensor> att, int64_t cell,
                                     std::vector<at::Tensor> state0, std::vector<at::Tensor> up);
+double vocab_rr_bench(at::Tensor hd, at::Tensor h, at::Tensor wlog, at::Tensor blog,
+                      at::Tensor whh, at::Tensor vgate, int64_t vdiv, int64_t iters, int64_t dbg);
 double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
 double att_bench(at::Tensor gv, at::Tensor P, at::Tensor q, at::Tensor wa, at::Tensor ba,
@@ -130,6 +132,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("refresh_shadows", &cst::refresh_shadows);
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
   m.def("vgrad_colsum_bench", &cst::vgrad_colsum_bench);
+  m.def("vocab_rr_bench", &cst::vocab_rr_bench);
   m.def("token_sort_bench", &cst::token_sort_bench);
   m.def("att_bench", &cst::att_bench);
   m.def("token_sort", &cst::token_sort);

@@ -1277,6 +1277,36 @@ double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tens
       iters, st);
 }
 
+// row-resident decode launch alone (SCST sampling step + exp store +
+// recurrent GEMM with video gates), dbg: see launch_vocab_rr_bench; us per launch
+double vocab_rr_bench(at::Tensor hd, at::Tensor h, at::Tensor wlog, at::Tensor blog,
+                      at::Tensor whh, at::Tensor vgate, int64_t vdiv, int64_t iters, int64_t dbg) {
+  const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
+  auto dev = hd.device();
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+  const int64_t ldl = (V + 63) / 64 * 64;
+  at::Tensor out = at::empty({R, ldl}, hd.options());
+  at::Tensor part = at::empty({(int64_t)vocab_part_slots((int)V) * R * vocab_partial_bytes() / 4}, f32);
+  at::Tensor pre = at::empty({R, 4 * H}, f32), eoff = at::full({R}, 8.f, f32);
+  at::Tensor rng = at::full({2}, 1234, at::TensorOptions().dtype(at::kInt).device(dev));
+  hipStream_t st = cur_stream();
+  bool ok = true;
+  const double us = time_launches(
+      [&](int i) {
+        ok = ok && launch_vocab_rr_bench(
+                       reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)R, (int)H,
+                       reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
+                       (int)V, reinterpret_cast<uint16_t*>(out.data_ptr()), ldl, part.data_ptr(),
+                       rng_ptr(rng), i, eoff.data_ptr<float>(),
+                       reinterpret_cast<const uint16_t*>(h.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(whh.data_ptr()), vgate.data_ptr<float>(),
+                       (int)vdiv, pre.data_ptr<float>(), (int)dbg, st);
+      },
+      iters, st);
+  TORCH_CHECK(ok, "vocab_rr_bench: shape not covered by the row-resident launch");
+  return us;
+}
+
 // bias-gradient column sums over the exp store: E (n, R, ldl) bf16, alpha (n*R)
 double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t iters) {
   check_cuda(E, "E");

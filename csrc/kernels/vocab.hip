@@ -843,16 +843,16 @@ int vocab_part_slots(int V) {
   return a > b ? a : b;
 }
 
-template <int SAMPLE, int STORE, int ARGMAX>
+template <int SAMPLE, int STORE, int ARGMAX, int DBG = 0>
 static void launch_rr_t(const RRArgs& a, int grid, int lds, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_rr_kernel<SAMPLE, STORE, ARGMAX>,
+    (void)hipFuncSetAttribute((const void*)vocab_rr_kernel<SAMPLE, STORE, ARGMAX, DBG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, RR_MAX_LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((vocab_rr_kernel<SAMPLE, STORE, ARGMAX>), dim3(grid), dim3(RR_THREADS), lds,
-                     stream, a);
+  hipLaunchKernelGGL((vocab_rr_kernel<SAMPLE, STORE, ARGMAX, DBG>), dim3(grid), dim3(RR_THREADS),
+                     lds, stream, a);
   post_launch("vocab_rr_kernel", stream);
 }
 
@@ -890,6 +890,36 @@ static bool rr_plan(int R, int H, int V, int G4, bool lstm, const float* vgate, 
   lds = RR_FIXED_LDS + std::max(bias_bytes, vg_bytes);
   if (lds > RR_MAX_LDS) return false;
   grid = n_rg * (nbv + nbl);
+  return true;
+}
+
+// microbenchmark of the row-resident launch (SCST sampling step with the exp
+// store): dbg bits 1 / 2 / 4 drop the epilogue / MFMAs / resident-row loads,
+// 8 drops the recurrent workgroups; returns false if the shape is not covered
+bool launch_vocab_rr_bench(const uint16_t* hd, int R, int H, const uint16_t* W, const float* bias,
+                           int V, uint16_t* out16, int64_t ldl, void* part, const uint32_t* rng,
+                           int step, const float* eoff, const uint16_t* h_t, const uint16_t* whh,
+                           const float* vgate, int vdiv, float* pre, int dbg, hipStream_t stream) {
+  RRArgs a{};
+  int grid = 0, lds = 0;
+  const int saved = g_rr_override;
+  g_rr_override = 1;
+  const bool ok = rr_plan(R, H, V, 4 * H, !(dbg & 8), vgate, vdiv, a, grid, lds);
+  g_rr_override = saved;
+  if (!ok) return false;
+  a.hd = hd, a.ldh = H, a.R = R, a.V = V, a.W = W, a.bias = bias;
+  a.out16 = out16, a.ldl = ldl, a.part = (VocabPartial*)part;
+  a.tgt = nullptr, a.tgt_stride = 0, a.rng = rng, a.step = step, a.eoff = eoff;
+  a.h = h_t, a.whh = whh, a.vgate = vgate, a.vdiv = vdiv, a.pre = pre, a.G4 = 4 * H;
+  switch (dbg & 7) {
+    case 1: launch_rr_t<1, RR_ST_EXP, 0, 1>(a, grid, lds, stream); break;
+    case 2: launch_rr_t<1, RR_ST_EXP, 0, 2>(a, grid, lds, stream); break;
+    case 3: launch_rr_t<1, RR_ST_EXP, 0, 3>(a, grid, lds, stream); break;
+    case 4: launch_rr_t<1, RR_ST_EXP, 0, 4>(a, grid, lds, stream); break;
+    case 5: launch_rr_t<1, RR_ST_EXP, 0, 5>(a, grid, lds, stream); break;
+    case 7: launch_rr_t<1, RR_ST_EXP, 0, 7>(a, grid, lds, stream); break;
+    default: launch_rr_t<1, RR_ST_EXP, 0, 0>(a, grid, lds, stream); break;
+  }
   return true;
 }
 

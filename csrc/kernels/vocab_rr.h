@@ -268,7 +268,7 @@ __device__ __forceinline__ void rr_wait(int c, int nc) {
 // barrier, refill the stage chunk c-1 used with chunk c+2, then (early wave)
 // MFMAs of chunk c + epilogue of chunk c, or (late wave) epilogue of chunk
 // c-1 + MFMAs of chunk c.
-template <class Epi>
+template <int DBG, class Epi>
 __device__ __forceinline__ void rr_chunk_loop(int nc, rsrc_t wsrc, int row0, int nrows, char* ring,
                                               int w, int lane, const bf16x8 (&hf)[RR_NKS],
                                               Epi&& epilogue) {
@@ -285,9 +285,11 @@ __device__ __forceinline__ void rr_chunk_loop(int nc, rsrc_t wsrc, int row0, int
     const char* stage = ring + (c % RR_STAGES) * RR_CHUNK_BYTES;
     if (late) {
       if (c > 0) epilogue(c - 1, acc);
-      rr_mfma_chunk(stage, lane, hf, acc);
+      if constexpr (!(DBG & 2)) rr_mfma_chunk(stage, lane, hf, acc);
+      else acc[0] = stage[lane];
     } else {
-      rr_mfma_chunk(stage, lane, hf, acc);
+      if constexpr (!(DBG & 2)) rr_mfma_chunk(stage, lane, hf, acc);
+      else acc[0] = stage[lane];
       epilogue(c, acc);
     }
     asm volatile("" ::: "memory");
@@ -295,7 +297,7 @@ __device__ __forceinline__ void rr_chunk_loop(int nc, rsrc_t wsrc, int row0, int
   if (late) epilogue(nc - 1, acc);
 }
 
-template <int SAMPLE, int STORE, int ARGMAX>
+template <int SAMPLE, int STORE, int ARGMAX, int DBG>
 __device__ __forceinline__ void rr_vocab_block(const RRArgs& a, int rg, int slot, char* lds) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -319,10 +321,13 @@ __device__ __forceinline__ void rr_vocab_block(const RRArgs& a, int rg, int slot
   const int rw = rg * RR_BROWS + w * RR_WROWS;
   const int r = min(rw + (lane & 31), a.R - 1);
   bf16x8 hf[RR_NKS];
-  {
+  if constexpr (!(DBG & 4)) {
     const uint16_t* src = a.hd + (int64_t)r * a.ldh + 8 * hi;
 #pragma unroll
     for (int s = 0; s < RR_NKS; ++s) hf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+  } else {
+#pragma unroll
+    for (int s = 0; s < RR_NKS; ++s) hf[s] = bf16x8{};
   }
   // per-row constants
   const float eo = (STORE == RR_ST_EXP) ? a.eoff[r] : 0.f;
@@ -336,7 +341,11 @@ __device__ __forceinline__ void rr_vocab_block(const RRArgs& a, int rg, int slot
   // are dropped by the hardware (no branch splits the pipelined loop body)
   const rsrc_t osrc = make_rsrc(a.out16, STORE != RR_ST_NONE ? (int64_t)a.R * a.ldl * 2 : 0);
   uint16_t* stg_row = stg + (lane & 31) * RR_STG_LD;
-  rr_chunk_loop(nc, wsrc, vbase, a.V, ring, w, lane, hf, [&](int c, const f32x16& acc) {
+  rr_chunk_loop<DBG>(nc, wsrc, vbase, a.V, ring, w, lane, hf, [&](int c, const f32x16& acc) {
+    if constexpr (DBG & 1) {
+      st.m = fmaxf(st.m, acc[0]);
+      return;
+    }
     float bb[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -381,6 +390,7 @@ __device__ __forceinline__ void rr_vocab_block(const RRArgs& a, int rg, int slot
   }
 }
 
+template <int DBG>
 __device__ __forceinline__ void rr_lstm_block(const RRArgs& a, int rg, int slot, char* lds) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -408,16 +418,24 @@ __device__ __forceinline__ void rr_lstm_block(const RRArgs& a, int rg, int slot,
   const int rw = r_first + w * RR_WROWS;
   const int r = min(rw + (lane & 31), a.R - 1);
   bf16x8 hf[RR_NKS];
-  {
+  if constexpr (!(DBG & 4)) {
     const uint16_t* src = a.h + (int64_t)r * RR_K + 8 * hi;
 #pragma unroll
     for (int s = 0; s < RR_NKS; ++s) hf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+  } else {
+#pragma unroll
+    for (int s = 0; s < RR_NKS; ++s) hf[s] = bf16x8{};
   }
   const int vrow = a.vgate != nullptr ? (r / a.vdiv - vid0) * a.vg_cols : 0;
   __syncthreads();  // video-gate slice
   const rsrc_t psrc = make_rsrc(a.pre, (int64_t)a.R * a.G4 * 4);
   const int rst = rw + (lane & 31);  // (rows >= R: outside psrc, dropped)
-  rr_chunk_loop(nc, wsrc, nbase, a.G4, ring, w, lane, hf, [&](int c, const f32x16& acc) {
+  float sink = 0.f;
+  rr_chunk_loop<DBG>(nc, wsrc, nbase, a.G4, ring, w, lane, hf, [&](int c, const f32x16& acc) {
+    if constexpr (DBG & 1) {
+      sink += acc[0];
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int cl = c * RR_CH + 8 * q + 4 * hi;
@@ -430,9 +448,14 @@ __device__ __forceinline__ void rr_lstm_block(const RRArgs& a, int rg, int slot,
       rr_store16(psrc, (rst * a.G4 + nbase + cl) * 4, o);
     }
   });
+  if constexpr (DBG & 1) {
+    if (sink == 1234.5f) a.pre[0] = sink;
+  }
 }
 
-template <int SAMPLE, int STORE, int ARGMAX>
+// DBG (microbenchmark only, vocab_rr_bench): 1 no epilogue work, 2 no MFMAs,
+// 4 no resident-row loads
+template <int SAMPLE, int STORE, int ARGMAX, int DBG = 0>
 __global__ __launch_bounds__(RR_THREADS, 1) void vocab_rr_kernel(RRArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int nwg = a.n_rg * (a.nbv + a.nbl);
@@ -441,9 +464,9 @@ __global__ __launch_bounds__(RR_THREADS, 1) void vocab_rr_kernel(RRArgs a) {
   // read it from that XCD's L2
   const int slot = L / a.n_rg, rg = L - slot * a.n_rg;
   if (slot < a.nbv)
-    rr_vocab_block<SAMPLE, STORE, ARGMAX>(a, rg, slot, lds);
+    rr_vocab_block<SAMPLE, STORE, ARGMAX, DBG>(a, rg, slot, lds);
   else
-    rr_lstm_block(a, rg, slot - a.nbv, lds);
+    rr_lstm_block<DBG>(a, rg, slot - a.nbv, lds);
 }
 
 }  // namespace cst

@@ -123,6 +123,10 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
 int vocab_part_slots(int V);
 // -1: launch by CSTCAP_DECODE_RR (default row-resident); 0 / 1: force (tests)
 void set_decode_rr(int on);
+bool launch_vocab_rr_bench(const uint16_t* hd, int R, int H, const uint16_t* W, const float* bias,
+                           int V, uint16_t* out16, int64_t ldl, void* part, const uint32_t* rng,
+                           int step, const float* eoff, const uint16_t* h_t, const uint16_t* whh,
+                           const float* vgate, int vdiv, float* pre, int dbg, hipStream_t stream);
 int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                            const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                            const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,

@@ -226,5 +226,17 @@ def test_headline_beam5_matches_torch_batched_beam():
         seq, lp = eng.sample_beam(model, data['feats'], {'beam_size': 5})
     assert seq.shape == seq_ref.shape == (64, 30)
     same = (seq == seq_ref).all(1)
-    assert same.float().mean().item() >= 0.8, same.float().mean().item()
+    # bf16 hidden states against fp32 ones: where two hypotheses score within
+    # rounding of each other the searches may keep different beams, so
+    # videos whose captions differ must end on a beam of the same score
+    assert same.float().mean().item() >= 0.6, same.float().mean().item()
     assert ((lp - lp_ref).abs()[same] < 0.05).all()
+
+    def score(s, l):  # caption log-prob up to and including its EOS
+        alive = torch.cumprod((s > 0).long(), 1)
+        keep = torch.cat([torch.ones_like(alive[:, :1]), alive[:, :-1]], 1).float()
+        return (l.float() * keep).sum(1)
+
+    s_eng, s_ref = score(seq, lp), score(seq_ref, lp_ref)
+    gap = (s_eng - s_ref).abs()
+    assert (gap[~same] <= 0.02 * s_ref.abs()[~same] + 0.1).all(), (gap[~same], s_ref[~same])
