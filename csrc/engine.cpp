@@ -22,6 +22,7 @@
 #include <torch/extension.h>
 #include <array>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPGuard.h>
@@ -517,8 +518,15 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   std::vector<std::array<int64_t, 2>> dhd_chunks;  // [t0, t1)
   {
     int64_t t1 = n_steps;
+    // (A/B runs: CSTCAP_DHD_CHUNKS="first,rest" steps per chunk)
+    int64_t k_first = 2, k_rest = 4;
+    if (const char* env = getenv("CSTCAP_DHD_CHUNKS")) {
+      k_first = std::max<int64_t>(1, atoll(env));
+      const char* comma = strchr(env, ',');
+      k_rest = comma ? std::max<int64_t>(1, atoll(comma + 1)) : k_first;
+    }
     while (t1 > 0) {
-      const int64_t k = dhd_chunks.empty() ? 2 : 4;
+      const int64_t k = dhd_chunks.empty() ? k_first : k_rest;
       const int64_t t0 = std::max<int64_t>(0, t1 - k);
       dhd_chunks.push_back({t0, t1});
       t1 = t0;
