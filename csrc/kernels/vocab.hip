@@ -857,13 +857,13 @@ static void launch_rr_t(const RRArgs& a, int grid, int lds, hipStream_t stream) 
 }
 
 // Geometry of the row-resident launch; false when the shape is not covered
-// (the tiled launch runs instead).  Row groups of 256 rows; per row group
+// (the tiled launch runs instead).  Row groups of 128 rows; per row group
 // about (CUs / row groups) workgroups, split between the vocabulary units
 // (64 weight rows, with the softmax epilogue) and the recurrent units by
 // their measured relative cost.
 static bool rr_plan(int R, int H, int V, int G4, bool lstm, const float* vgate, int vdiv,
                     RRArgs& a, int& grid, int& lds) {
-  if (H != RR_K || R < 2 * RR_BROWS || !rr_enabled()) return false;
+  if (H != RR_K || R < 4 * RR_BROWS || !rr_enabled()) return false;
   if (lstm && G4 % RR_UNIT != 0) return false;
   const int n_rg = (R + RR_BROWS - 1) / RR_BROWS;
   const int per = std::max(2, device_cu_count() / n_rg);
@@ -887,7 +887,7 @@ static bool rr_plan(int R, int H, int V, int G4, bool lstm, const float* vgate, 
   } else if (lstm) {
     vg_bytes = a.vg_cols * 4;
   }
-  lds = RR_FIXED_LDS + std::max(bias_bytes, vg_bytes);
+  lds = std::max(RR_FIXED_LDS + bias_bytes, RR_STG_OFF + vg_bytes);
   if (lds > RR_MAX_LDS) return false;
   grid = n_rg * (nbv + nbl);
   return true;

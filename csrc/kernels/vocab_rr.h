@@ -8,13 +8,25 @@
 // That, not the MFMAs, set its ~17 us main loop.
 //
 // Here each 512-thread workgroup (one per CU, the grid is one wave of the
-// chip) owns 256 caption rows -- each of its 8 waves (two per SIMD) holds 32
-// rows x 512 as bf16 MFMA B-fragments in 128 of its 256 registers -- and
-// streams a contiguous
-// slice of the weight rows through a 3-stage LDS ring, 32 rows (one MFMA M
-// tile, 32 KB) per chunk.  Every weight row is read once per row group, every
-// caption row once per workgroup: 5 row groups x 51 workgroups at R = 1,280
-// move ~130 MB, and the MFMA work (16.5 GFLOP) bounds the launch instead.
+// chip) owns 128 caption rows and streams a contiguous slice of the weight
+// rows through a 3-stage LDS ring, 32 rows (one MFMA M tile, 32 KB) per
+// chunk.  Every weight row is read once per row group, every caption row once
+// per workgroup: 10 row groups x 25 workgroups at R = 1,280 move ~160 MB
+// (the tiled launch: ~320 MB).
+//
+// Waves are specialised, one pair per SIMD:
+//   compute wave w (0-3): holds its 32 caption rows x 512 as bf16 MFMA
+//     B-fragments in 128 registers; per chunk, 32 MFMAs onto an accumulator
+//     initialised with the chunk's bias / video-gate term, then the 32 x 32
+//     fp32 tile to an LDS mailbox (double-buffered by chunk parity);
+//   epilogue wave 4 + w (same SIMD): in the next chunk period, reads that
+//     tile and runs the epilogue while its partner's MFMAs of the next chunk
+//     run -- the matrix pipe and the VALU of the SIMD work concurrently, and
+//     neither wave needs the other's registers.
+// (Holding the rows in the waves that also run the epilogue -- 64 rows per
+// wave at one wave per SIMD, or 32 rows per wave with two waves per SIMD --
+// ran out of registers: spills, or every LDS fragment read right before its
+// MFMA.)
 //
 // Roles (per workgroup, uniform):
 //   vocab: B = hd_t (dropout applied), weights W_logit; per chunk the
@@ -29,15 +41,9 @@
 //   lstm: B = h_t, weights W_hh (packed gates); pre_{t+1} = h_t W_hh^T +
 //     vgate[row / vdiv] (the workgroup's video-gate slice preloaded in LDS).
 //
-// The two waves of a SIMD run the chunk loop half a phase apart: between two
-// workgroup barriers an "early" wave (w < 4) issues chunk c's 32 MFMAs and
-// then chunk c's epilogue, a "late" wave (w >= 4, same SIMD) the epilogue of
-// chunk c-1 and then chunk c's MFMAs, so one wave's VALU epilogue runs beside
-// the other's MFMAs and each needs a single accumulator.  (64 rows per wave
-// at one wave per SIMD needed 256 registers of B fragments and spilled; so
-// did a second accumulator per wave.)  Weight chunks are loaded by LDS-DMA two chunks ahead; the counted
-// vmcnt waits assume the per-iteration vector-memory op order fixed by the
-// compiler barriers below (see rr_wait).
+// One workgroup barrier per chunk period orders the LDS ring (weight chunks
+// loaded by LDS-DMA two chunks ahead, counted vmcnt waits, see rr_wait) and
+// the mailboxes.
 #pragma once
 #include "gemm_tile.h"
 #include "vocab_common.h"
@@ -45,8 +51,9 @@
 namespace cst {
 
 constexpr int RR_WAVES = 8, RR_THREADS = 64 * RR_WAVES;
-constexpr int RR_WROWS = 32;                      // caption rows per wave (one MFMA N tile)
-constexpr int RR_BROWS = RR_WAVES * RR_WROWS;     // caption rows per workgroup
+constexpr int RR_CWAVES = 4;                      // compute waves (one per SIMD)
+constexpr int RR_WROWS = 32;                      // caption rows per compute wave
+constexpr int RR_BROWS = RR_CWAVES * RR_WROWS;    // caption rows per workgroup
 constexpr int RR_CH = 32;                         // weight rows per chunk (one MFMA M tile)
 constexpr int RR_UNIT = 64;                       // weight rows per work unit (2 chunks)
 constexpr int RR_STAGES = 3;
@@ -59,8 +66,13 @@ constexpr int RR_ROW_LD = RR_K * 2 + 16;
 constexpr int RR_CHUNK_BYTES = RR_CH * RR_ROW_LD;
 constexpr int RR_STG_LD = RR_CH + 8;              // staging row stride (16-bit entries, 80 B)
 constexpr int RR_STG_BYTES = RR_WROWS * RR_STG_LD * 2;
-constexpr int RR_FIXED_LDS = RR_STAGES * RR_CHUNK_BYTES + RR_WAVES * RR_STG_BYTES;
+// mailboxes: 2 parities x 4 compute waves x (16 x 64 floats)
+constexpr int RR_MBOX_BYTES = 16 * 64 * 4;
+constexpr int RR_MBOX_OFF = RR_STAGES * RR_CHUNK_BYTES;
+constexpr int RR_STG_OFF = RR_MBOX_OFF + 2 * RR_CWAVES * RR_MBOX_BYTES;
+constexpr int RR_FIXED_LDS = RR_STG_OFF + RR_CWAVES * RR_STG_BYTES;
 constexpr int RR_MAX_LDS = 160 * 1024;
+constexpr int RR_PF = 4;  // LDS fragment prefetch distance (k-steps)
 
 enum RRStore : int { RR_ST_NONE = 0, RR_ST_EXP = 1, RR_ST_F16 = 2 };
 
@@ -92,7 +104,7 @@ struct RRArgs {
   int vg_vids, vg_cols;  // LDS video-gate slice: videos x columns (lstm role)
 };
 
-// LDS-DMA of one 32-row chunk: wave w moves rows 4w .. 4w+3, one 1 KiB row per
+// LDS-DMA of one 32-row chunk: wave w (all 8) moves rows 4w .. 4w+3, one 1 KiB row per
 // wave-instruction (lane l: bytes 16 l .. 16 l + 15 of the row).
 constexpr int RR_DMA_PER_WAVE = RR_CH / RR_WAVES;
 __device__ __forceinline__ void rr_issue(rsrc_t src, int row0, int nrows, char* dst, int w,
@@ -105,16 +117,19 @@ __device__ __forceinline__ void rr_issue(rsrc_t src, int row0, int nrows, char* 
   }
 }
 
-// 32 MFMAs of one chunk into acc (B fragments resident in hf)
+// 32 MFMAs of one chunk accumulated onto acc (B fragments resident in hf);
+// A fragments read RR_PF k-steps ahead
 __device__ __forceinline__ void rr_mfma_chunk(const char* stage, int lane,
                                               const bf16x8 (&hf)[RR_NKS], f32x16& acc) {
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const char* base = stage + (lane & 31) * RR_ROW_LD + (lane >> 5) * 16;
+  bf16x8 a[RR_PF];
+#pragma unroll
+  for (int p = 0; p < RR_PF; ++p) a[p] = *reinterpret_cast<const bf16x8*>(base + 32 * p);
 #pragma unroll
   for (int s = 0; s < RR_NKS; ++s) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + 32 * s);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hf[s], acc, 0, 0, 0);
+    const bf16x8 cur = a[s % RR_PF];
+    if (s + RR_PF < RR_NKS) a[s % RR_PF] = *reinterpret_cast<const bf16x8*>(base + 32 * (s + RR_PF));
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, hf[s], acc, 0, 0, 0);
   }
 }
 
@@ -162,16 +177,12 @@ __device__ __forceinline__ void rr_row_merge(RRRow& a, const RRRow& c) {
   a.xt = fmaxf(a.xt, c.xt);
 }
 
-// Epilogue of one (chunk, 32-row tile) for the lane's caption row: entries
-// v(k) = v0 + 8 (k >> 2) + 4 hi + (k & 3), k < 16.
+// Epilogue of one (chunk, 32-row tile) for the lane's caption row: logits x
+// (bias included) of entries v(k) = v0 + 8 (k >> 2) + 4 hi + (k & 3), k < 16.
 template <int SAMPLE, int STORE, int ARGMAX>
-__device__ __forceinline__ void rr_vocab_epi(const f32x16& acc, const float (&bb)[16], RRRow& st,
-                                             int v0, int hi, float eo, int tg, uint32_t rowkey,
-                                             uint16_t* stg) {
+__device__ __forceinline__ void rr_vocab_epi(const f32x16& x, RRRow& st, int v0, int hi, float eo,
+                                             int tg, uint32_t rowkey, uint16_t* stg) {
   constexpr float L2E = 1.4426950408889634f;
-  float x[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) x[k] = acc[k] + bb[k];
   float mc = x[0];
 #pragma unroll
   for (int k = 1; k < 16; ++k) mc = fmaxf(mc, x[k]);
@@ -252,49 +263,99 @@ __device__ __forceinline__ void rr_vocab_epi(const f32x16& acc, const float (&bb
   }
 }
 
-// Counted wait for this wave's LDS-DMA of the chunk about to be consumed.
-// Per iteration c the wave issues, in this order: DMA(c + 2) (4 ops, if any),
-// its epilogue stores (>= 0 ops).  DMA(c) was issued in iteration c - 2, so at
-// the top of iteration c at least 4 ops (DMA(c + 1)) follow it unless c is the
-// last chunk; the first and the last iterations drain everything.
+// Counted wait for this wave's LDS-DMA of the chunk about to be consumed,
+// and (lgkmcnt 0) for its LDS writes of the previous period: per period c
+// every wave issues, in this order, DMA(c + 2) (4 ops, if any) and then its
+// global stores (>= 0 ops).  DMA(c) was issued in period c - 2, so at the top
+// of period c at least 4 ops (DMA(c + 1)) follow it unless c >= nc - 1;
+// the first and the last periods drain everything.
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0x0 << 8));
+}
 __device__ __forceinline__ void rr_wait(int c, int nc) {
-  if (c == 0 || c == nc - 1)
-    wait_vmcnt<0>();
+  if (c == 0 || c >= nc - 1)
+    wait_vm_lgkm0<0>();
   else
-    wait_vmcnt<RR_DMA_PER_WAVE>();
+    wait_vm_lgkm0<RR_DMA_PER_WAVE>();
 }
 
-// The chunk loop shared by both roles.  Iteration c: wait for chunk c's DMA,
-// barrier, refill the stage chunk c-1 used with chunk c+2, then (early wave)
-// MFMAs of chunk c + epilogue of chunk c, or (late wave) epilogue of chunk
-// c-1 + MFMAs of chunk c.
-template <int DBG, class Epi>
-__device__ __forceinline__ void rr_chunk_loop(int nc, rsrc_t wsrc, int row0, int nrows, char* ring,
+// mailbox of compute wave cw, parity p: element k of lane l at float index
+// (k / 4) * 256 + l * 4 + (k & 3) (16-byte pieces lane-contiguous: no LDS
+// bank conflicts for either side)
+__device__ __forceinline__ float* rr_mbox(char* lds, int p, int cw) {
+  return reinterpret_cast<float*>(lds + RR_MBOX_OFF + (p * RR_CWAVES + cw) * RR_MBOX_BYTES);
+}
+__device__ __forceinline__ void rr_mbox_put(float* mb, int lane, const f32x16& acc) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<float4*>(mb + q * 256 + lane * 4) =
+        make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+}
+__device__ __forceinline__ void rr_mbox_get(const float* mb, int lane, f32x16& x) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(mb + q * 256 + lane * 4);
+    x[4 * q] = v.x, x[4 * q + 1] = v.y, x[4 * q + 2] = v.z, x[4 * q + 3] = v.w;
+  }
+}
+
+// The chunk loop of both roles: nc + 1 periods.  Period c: wait for chunk
+// c's DMA, barrier, refill the stage chunk c-1 used with chunk c+2; compute
+// waves: accumulator = init(c) (bias / video gates, from LDS), chunk c's 32
+// MFMAs, tile -> mailbox c & 1; epilogue waves: epilogue of chunk c-1 from
+// mailbox (c-1) & 1.
+template <int DBG, class Init, class Epi>
+__device__ __forceinline__ void rr_chunk_loop(int nc, rsrc_t wsrc, int row0, int nrows, char* lds,
                                               int w, int lane, const bf16x8 (&hf)[RR_NKS],
-                                              Epi&& epilogue) {
-  f32x16 acc;
-  const bool late = w >= RR_WAVES / 2;
-  for (int c = 0; c < nc; ++c) {
+                                              Init&& init, Epi&& epilogue) {
+  const bool compute = w < RR_CWAVES;
+  const int cw = compute ? w : w - RR_CWAVES;
+  for (int c = 0; c <= nc; ++c) {
     rr_wait(c, nc);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (c + 2 < nc)
-      rr_issue(wsrc, row0 + (c + 2) * RR_CH, nrows, ring + ((c + 2) % RR_STAGES) * RR_CHUNK_BYTES,
+      rr_issue(wsrc, row0 + (c + 2) * RR_CH, nrows, lds + ((c + 2) % RR_STAGES) * RR_CHUNK_BYTES,
                w, lane);
     asm volatile("" ::: "memory");
-    const char* stage = ring + (c % RR_STAGES) * RR_CHUNK_BYTES;
-    if (late) {
-      if (c > 0) epilogue(c - 1, acc);
-      if constexpr (!(DBG & 2)) rr_mfma_chunk(stage, lane, hf, acc);
-      else acc[0] = stage[lane];
-    } else {
-      if constexpr (!(DBG & 2)) rr_mfma_chunk(stage, lane, hf, acc);
-      else acc[0] = stage[lane];
-      epilogue(c, acc);
+    if (compute) {
+      if (c < nc) {
+        f32x16 acc;
+        init(c, acc);
+        if constexpr (!(DBG & 2)) {
+          rr_mfma_chunk(lds + (c % RR_STAGES) * RR_CHUNK_BYTES, lane, hf, acc);
+          // keep the fragment reads RR_PF MFMAs ahead (the scheduler otherwise
+          // pairs each read with the next MFMA and the LDS latency shows)
+          __builtin_amdgcn_sched_group_barrier(0x100, 4 + RR_PF, 0);  // init + first reads
+#pragma unroll
+          for (int s = 0; s < RR_NKS - RR_PF; ++s) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, RR_PF, 0);
+        }
+        rr_mbox_put(rr_mbox(lds, c & 1, cw), lane, acc);
+      }
+    } else if (c > 0) {
+      f32x16 x;
+      rr_mbox_get(rr_mbox(lds, (c - 1) & 1, cw), lane, x);
+      epilogue(c - 1, x);
     }
     asm volatile("" ::: "memory");
   }
-  if (late) epilogue(nc - 1, acc);
+}
+
+// resident B fragments of a compute wave: rows r (clamped), k = 16 s + 8 hi
+template <int DBG>
+__device__ __forceinline__ void rr_load_rows(const uint16_t* src, bf16x8 (&hf)[RR_NKS]) {
+  if constexpr (!(DBG & 4)) {
+#pragma unroll
+    for (int s = 0; s < RR_NKS; ++s) hf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+  } else {
+#pragma unroll
+    for (int s = 0; s < RR_NKS; ++s) hf[s] = bf16x8{};
+  }
 }
 
 template <int SAMPLE, int STORE, int ARGMAX, int DBG>
@@ -302,58 +363,56 @@ __device__ __forceinline__ void rr_vocab_block(const RRArgs& a, int rg, int slot
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int hi = lane >> 5;
+  const int cw = w & (RR_CWAVES - 1);
   const int u0 = slot * a.nuv / a.nbv, u1 = (slot + 1) * a.nuv / a.nbv;
   const int nc = (u1 - u0) * (RR_UNIT / RR_CH);
   const int vbase = u0 * RR_UNIT;
-  char* ring = lds;
-  uint16_t* stg = reinterpret_cast<uint16_t*>(lds + RR_STAGES * RR_CHUNK_BYTES + w * RR_STG_BYTES);
+  uint16_t* stg = reinterpret_cast<uint16_t*>(lds + RR_STG_OFF + cw * RR_STG_BYTES);
   float* sbias = reinterpret_cast<float*>(lds + RR_FIXED_LDS);
   const rsrc_t wsrc = make_rsrc(a.W, (int64_t)a.V * RR_K * 2);
   // weight chunks 0 and 1 in flight first
-  rr_issue(wsrc, vbase, a.V, ring, w, lane);
-  if (nc > 1) rr_issue(wsrc, vbase + RR_CH, a.V, ring + RR_CHUNK_BYTES, w, lane);
+  rr_issue(wsrc, vbase, a.V, lds, w, lane);
+  if (nc > 1) rr_issue(wsrc, vbase + RR_CH, a.V, lds + RR_CHUNK_BYTES, w, lane);
   // the workgroup's bias slice (-inf past V) in LDS
   for (int i = threadIdx.x; i < nc * RR_CH; i += RR_THREADS) {
     const int v = vbase + i;
     sbias[i] = v < a.V ? a.bias[v] : -INFINITY;
   }
-  // resident B fragments: the wave's 32 caption rows of hd_t
-  const int rw = rg * RR_BROWS + w * RR_WROWS;
+  const int rw = rg * RR_BROWS + cw * RR_WROWS;
   const int r = min(rw + (lane & 31), a.R - 1);
   bf16x8 hf[RR_NKS];
-  if constexpr (!(DBG & 4)) {
-    const uint16_t* src = a.hd + (int64_t)r * a.ldh + 8 * hi;
-#pragma unroll
-    for (int s = 0; s < RR_NKS; ++s) hf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
-  } else {
-#pragma unroll
-    for (int s = 0; s < RR_NKS; ++s) hf[s] = bf16x8{};
+  if (w < RR_CWAVES) rr_load_rows<DBG>(a.hd + (int64_t)r * a.ldh + 8 * hi, hf);
+  // per-row constants (epilogue waves)
+  float eo = 0.f;
+  int tg = -1;
+  uint32_t rowkey = 0;
+  if (w >= RR_CWAVES) {
+    eo = (STORE == RR_ST_EXP) ? a.eoff[r] : 0.f;
+    tg = a.tgt != nullptr ? (int)a.tgt[(int64_t)r * a.tgt_stride] : -1;
+    rowkey = rng_seed(a.rng, RNG_SLOT_SAMPLE) ^
+             mix32((uint32_t)r * 0x9E3779B1u + (uint32_t)a.step * 0x85EBCA77u);
   }
-  // per-row constants
-  const float eo = (STORE == RR_ST_EXP) ? a.eoff[r] : 0.f;
-  const int tg = a.tgt != nullptr ? (int)a.tgt[(int64_t)r * a.tgt_stride] : -1;
-  const uint32_t rowkey = rng_seed(a.rng, RNG_SLOT_SAMPLE) ^
-                          mix32((uint32_t)r * 0x9E3779B1u + (uint32_t)a.step * 0x85EBCA77u);
   RRRow st;
   rr_row_init(st);
   __syncthreads();  // bias slice
   // stores through a buffer resource: rows >= R fall outside its range and
-  // are dropped by the hardware (no branch splits the pipelined loop body)
+  // are dropped by the hardware (no branch in the loop body)
   const rsrc_t osrc = make_rsrc(a.out16, STORE != RR_ST_NONE ? (int64_t)a.R * a.ldl * 2 : 0);
   uint16_t* stg_row = stg + (lane & 31) * RR_STG_LD;
-  rr_chunk_loop<DBG>(nc, wsrc, vbase, a.V, ring, w, lane, hf, [&](int c, const f32x16& acc) {
-    if constexpr (DBG & 1) {
-      st.m = fmaxf(st.m, acc[0]);
-      return;
-    }
-    float bb[16];
+  auto init = [&](int c, f32x16& acc) {  // the chunk's bias (-inf past V)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float4 b4 = *reinterpret_cast<const float4*>(sbias + c * RR_CH + 8 * q + 4 * hi);
-      bb[4 * q] = b4.x, bb[4 * q + 1] = b4.y, bb[4 * q + 2] = b4.z, bb[4 * q + 3] = b4.w;
+      acc[4 * q] = b4.x, acc[4 * q + 1] = b4.y, acc[4 * q + 2] = b4.z, acc[4 * q + 3] = b4.w;
+    }
+  };
+  rr_chunk_loop<DBG>(nc, wsrc, vbase, a.V, lds, w, lane, hf, init, [&](int c, const f32x16& x) {
+    if constexpr (DBG & 1) {
+      st.m = fmaxf(st.m, x[0]);
+      return;
     }
     const int v0 = vbase + c * RR_CH;
-    rr_vocab_epi<SAMPLE, STORE, ARGMAX>(acc, bb, st, v0, hi, eo, tg, rowkey, stg_row);
+    rr_vocab_epi<SAMPLE, STORE, ARGMAX>(x, st, v0, hi, eo, tg, rowkey, stg_row);
     if constexpr (STORE != RR_ST_NONE) {
       // the wave's 32 rows x 32 entries: 64-byte row segments, 16 B per lane
 #pragma unroll
@@ -364,6 +423,7 @@ __device__ __forceinline__ void rr_vocab_block(const RRArgs& a, int rg, int slot
       }
     }
   });
+  if (w < RR_CWAVES) return;
   // lanes l and l ^ 32 hold the two halves of a row's entries
   RRRow o;
   o.m = __shfl_xor(st.m, 32, 64);
@@ -395,14 +455,15 @@ __device__ __forceinline__ void rr_lstm_block(const RRArgs& a, int rg, int slot,
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int hi = lane >> 5;
+  const int cw = w & (RR_CWAVES - 1);
   const int u0 = slot * a.nul / a.nbl, u1 = (slot + 1) * a.nul / a.nbl;
   const int nc = (u1 - u0) * (RR_UNIT / RR_CH);
   const int nbase = u0 * RR_UNIT;
-  char* ring = lds;
-  float* svg = reinterpret_cast<float*>(lds + RR_FIXED_LDS);
+  // (the recurrent role has no exp-store staging: its video gates start there)
+  float* svg = reinterpret_cast<float*>(lds + RR_STG_OFF);
   const rsrc_t wsrc = make_rsrc(a.whh, (int64_t)a.G4 * RR_K * 2);
-  rr_issue(wsrc, nbase, a.G4, ring, w, lane);
-  if (nc > 1) rr_issue(wsrc, nbase + RR_CH, a.G4, ring + RR_CHUNK_BYTES, w, lane);
+  rr_issue(wsrc, nbase, a.G4, lds, w, lane);
+  if (nc > 1) rr_issue(wsrc, nbase + RR_CH, a.G4, lds + RR_CHUNK_BYTES, w, lane);
   const int r_first = rg * RR_BROWS;
   const int vid0 = a.vgate != nullptr ? r_first / a.vdiv : 0;
   const int ncols = nc * RR_CH;
@@ -415,36 +476,35 @@ __device__ __forceinline__ void rr_lstm_block(const RRArgs& a, int rg, int slot,
           a.vgate != nullptr ? a.vgate[(int64_t)min(vid0 + vv, vmax) * a.G4 + nbase + cc] : 0.f;
     }
   }
-  const int rw = r_first + w * RR_WROWS;
+  const int rw = r_first + cw * RR_WROWS;
   const int r = min(rw + (lane & 31), a.R - 1);
   bf16x8 hf[RR_NKS];
-  if constexpr (!(DBG & 4)) {
-    const uint16_t* src = a.h + (int64_t)r * RR_K + 8 * hi;
-#pragma unroll
-    for (int s = 0; s < RR_NKS; ++s) hf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
-  } else {
-#pragma unroll
-    for (int s = 0; s < RR_NKS; ++s) hf[s] = bf16x8{};
-  }
+  if (w < RR_CWAVES) rr_load_rows<DBG>(a.h + (int64_t)r * RR_K + 8 * hi, hf);
   const int vrow = a.vgate != nullptr ? (r / a.vdiv - vid0) * a.vg_cols : 0;
   __syncthreads();  // video-gate slice
   const rsrc_t psrc = make_rsrc(a.pre, (int64_t)a.R * a.G4 * 4);
   const int rst = rw + (lane & 31);  // (rows >= R: outside psrc, dropped)
   float sink = 0.f;
-  rr_chunk_loop<DBG>(nc, wsrc, nbase, a.G4, ring, w, lane, hf, [&](int c, const f32x16& acc) {
+  auto init = [&](int c, f32x16& acc) {  // the row's video-gate term (0 without)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 g = *reinterpret_cast<const float4*>(svg + vrow + c * RR_CH + 8 * q + 4 * hi);
+      acc[4 * q] = g.x, acc[4 * q + 1] = g.y, acc[4 * q + 2] = g.z, acc[4 * q + 3] = g.w;
+    }
+  };
+  rr_chunk_loop<DBG>(nc, wsrc, nbase, a.G4, lds, w, lane, hf, init, [&](int c, const f32x16& x) {
     if constexpr (DBG & 1) {
-      sink += acc[0];
+      sink += x[0];
       return;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int cl = c * RR_CH + 8 * q + 4 * hi;
-      const float4 g = *reinterpret_cast<const float4*>(svg + vrow + cl);
       uint4 o;
-      o.x = __float_as_uint(acc[4 * q] + g.x);
-      o.y = __float_as_uint(acc[4 * q + 1] + g.y);
-      o.z = __float_as_uint(acc[4 * q + 2] + g.z);
-      o.w = __float_as_uint(acc[4 * q + 3] + g.w);
+      o.x = __float_as_uint(x[4 * q]);
+      o.y = __float_as_uint(x[4 * q + 1]);
+      o.z = __float_as_uint(x[4 * q + 2]);
+      o.w = __float_as_uint(x[4 * q + 3]);
       rr_store16(psrc, (rst * a.G4 + nbase + cl) * 4, o);
     }
   });

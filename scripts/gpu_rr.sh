@@ -5,6 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc_rr
+timeout -k 10 300 python -u -m pytest tests/test_gpu_decode_rr.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_rr.log 2>&1 || exit $?
 timeout -k 10 200 python scripts/microbench_rr.py > gpurun_out/mb_rr.json 2> gpurun_out/mb_rr.err || exit $?
 run() {
   local tag=$1; shift
