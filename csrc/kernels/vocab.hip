@@ -505,10 +505,13 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   if (threadIdx.x == 0) s_nonzero = 0;
   // The row's tile partials are loaded unconditionally (clamped index,
   // neutralised in the merge) so they issue back to back: one memory round
-  // trip instead of one per merge step.  The cell epilogue's operands are
-  // loaded afterwards in one batch (pre-activations, c_t and the token's
-  // table row together): the vector-memory counter retires loads in order,
-  // so prefetching them before the partials made the merge wait for them.
+  // trip instead of one per merge step.  The cell epilogue's token-independent
+  // operands (pre-activations, c_t, video gates) are requested right AFTER
+  // them: the vector-memory counter retires loads in order, so the merge
+  // waits for the partials only while those are in flight (requested before
+  // the partials, they delayed the merge; requested after the merge, their
+  // latency added to the chain).  Only the token's table row waits for the
+  // merge.
   constexpr int CMB_MAXP = 4;  // n_vt <= 128: V <= 16384 at 128-wide tiles
   const bool fastp = n_vt <= CMB_MAXP * CMB_LANES;
   VocabPartial pp[CMB_MAXP];
@@ -518,6 +521,25 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
       pp[k] = part[(int64_t)min(sub + k * CMB_LANES, n_vt - 1) * R + r];
   }
   const bool do_cell = cell.pre != nullptr && tok_out != nullptr;
+  // one batch of CELL_U units per lane covers H <= 512 (every lane of the row
+  // owns units sub, sub + 32, ...); larger H loads per batch after the merge
+  constexpr int CELL_U = 16;
+  const bool pre_early = do_cell && valid && cell.H <= CMB_LANES * CELL_U;
+  float4 pe[CELL_U];
+  float ce[CELL_U];
+  uint2 ve[CELL_U];
+  if (pre_early) {
+    const int H = cell.H;
+    const float* prow = cell.pre + (int64_t)r * 4 * H;
+#pragma unroll
+    for (int k = 0; k < CELL_U; ++k) {
+      const int u = min(sub + k * CMB_LANES, H - 1);  // (clamped: no branch)
+      pe[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
+      ce[k] = cell.c_prev[(int64_t)r * H + u];
+      if (cell.vg16 != nullptr)
+        ve[k] = *reinterpret_cast<const uint2*>(cell.vg16 + (int64_t)r * 4 * H + 4 * u);
+    }
+  }
   // the selecting lane's other inputs, requested now (they do not depend on
   // the merge): ground-truth token, previous step's non-EOS count, row mask
   int64_t gt_pre = 0;
@@ -611,20 +633,29 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
       // batches of CELL_U units (all of H = 512 in one): every load of a
       // batch is issued before the first store (the stores could alias the
       // inputs as far as the compiler knows, which would serialise the loads)
-      constexpr int CELL_U = 16;
       for (int u0 = sub; u0 < H; u0 += CMB_LANES * CELL_U) {
         float4 p[CELL_U], x[CELL_U];
         float cp[CELL_U];
         uint2 vq[CELL_U];
+        if (pre_early) {
 #pragma unroll
-        for (int k = 0; k < CELL_U; ++k) {
-          const int u = u0 + k * CMB_LANES;
-          if (u < H) {
-            p[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
-            x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
-            cp[k] = cell.c_prev[(int64_t)r * H + u];
-            if (cell.vg16 != nullptr)
-              vq[k] = *reinterpret_cast<const uint2*>(cell.vg16 + (int64_t)r * 4 * H + 4 * u);
+          for (int k = 0; k < CELL_U; ++k) {
+            p[k] = pe[k];
+            cp[k] = ce[k];
+            vq[k] = ve[k];
+            x[k] = *reinterpret_cast<const float4*>(trow + 4 * min(u0 + k * CMB_LANES, H - 1));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < CELL_U; ++k) {
+            const int u = u0 + k * CMB_LANES;
+            if (u < H) {
+              p[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
+              x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
+              cp[k] = cell.c_prev[(int64_t)r * H + u];
+              if (cell.vg16 != nullptr)
+                vq[k] = *reinterpret_cast<const uint2*>(cell.vg16 + (int64_t)r * 4 * H + 4 * u);
+            }
           }
         }
         if (cell.vg16 != nullptr) {  // attention: the row's video gates (bf16)
