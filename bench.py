@@ -85,6 +85,11 @@ def parse():
     p.add_argument('--json_out', default='')
     p.add_argument('--profile_phases', type=int, default=0,
                    help='print the mean per-phase GPU time (HIP events) of the timed steps')
+    p.add_argument('--stamps', type=int, default=0,
+                   help='N > 0: device timeline stamps (utils/stamps.py) captured into the '
+                        'graph; after the timed steps, N more steps are stamped and the mean '
+                        'phase times (us after the step start) are printed to stderr and '
+                        'stored as "stamps_us" (diagnostic: stamps add ~2 us per phase)')
     p.add_argument('--sync_debug', type=int, default=0,
                    help='after warmup: report host-synchronising calls and host enqueue time of one step')
     return p.parse_args()
@@ -161,6 +166,9 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
             return {'loss': seq.float().mean()}
         return trainer.train_step(data, 0)
 
+    if a.stamps and dev.type == 'cuda':
+        from cst_captioning_amd.utils import stamps as stamps_mod
+        stamps_mod.enable(dev)  # before the first step: the captured graph carries them
     for _ in range(a.warmup):
         out = step()
     sync()
@@ -193,13 +201,26 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
     sync()
     dt = time.perf_counter() - t0
     dt = ctx.max_scalar(dt)
+    stamp_mean = {}
+    if a.stamps and dev.type == 'cuda':
+        for _ in range(a.stamps):
+            step()
+            for k, v in stamps_mod.read().items():
+                stamp_mean[k] = stamp_mean.get(k, 0.0) + v / a.stamps
+        stamps_mod.disable()
+        stamp_mean = {k: round(v, 1) for k, v in sorted(stamp_mean.items(), key=lambda kv: kv[1])}
+        print('stamps (us after the step stamp, mean of %d steps, %d frames):' % (a.stamps, num_chunks),
+              file=sys.stderr)
+        for k, v in stamp_mean.items():
+            print('  %9.1f  %s' % (v, k), file=sys.stderr)
+        sys.stderr.flush()
     res = {'dt': dt, 'ms': dt / a.steps * 1e3, 'loss': float(out['loss']),
            'caps': a.batch_size * S * ctx.world_size * a.steps / dt,
            'vids': a.batch_size * ctx.world_size * a.steps / dt, 'phases': phases,
            'skipped': int(trainer.optimizer.skipped().item()),
            'exp_fix': int(engine.exp_fix_rows.item()) if engine is not None else None,
            'graph': int(trainer._graph is not None), 'n_params': n_params, 't_gen': t_gen,
-           'bf16': engine is not None or trainer.autocast_bf16}
+           'bf16': engine is not None or trainer.autocast_bf16, 'stamps': stamp_mean}
     del trainer, model, engine, loader, ds, step, out
     gc.collect()
     if dev.type == 'cuda':
@@ -232,6 +253,8 @@ def main():
         att8 = {'value': round(r['caps'], 2), 'ms_per_step': round(r['ms'], 3),
                 'temporal_attention_frames': 8, 'final_loss': r['loss'],
                 'skipped_steps': r['skipped']}
+        if r['stamps']:
+            att8['stamps_us'] = r['stamps']
     dt, ms, caps, vids = main_run['dt'], main_run['ms'], main_run['caps'], main_run['vids']
     loss, n_params, t_gen = main_run['loss'], main_run['n_params'], main_run['t_gen']
     S = 20
@@ -282,6 +305,8 @@ def main():
         # BASELINE.json's metric names the LSTM-attn decoder: its temporal-
         # attention config (C = 8 frames, MFMA attention) on the same job
         rec['att8'] = att8
+    if main_run['stamps']:
+        rec['stamps_us'] = main_run['stamps']
     if main_run['phases']:
         rec['phases_ms'] = {k: round(v, 3) for k, v in main_run['phases'].items()}
     if ctx.is_main:

@@ -70,6 +70,10 @@ at::Tensor flat_adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v
                           int64_t phase, at::Tensor shadow_meta,
                           std::vector<at::Tensor> shadow_dst);
 void refresh_shadows(at::Tensor p, at::Tensor shadow_meta, std::vector<at::Tensor> shadow_dst);
+void set_stamp_base(int64_t base);
+void stamp_buffer(at::Tensor buf);
+void stamp_now(int64_t slot);
+int64_t wall_clock_khz();
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -145,4 +149,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scst_loss_forward", &cst::scst_loss_forward);
   m.def("scst_loss_backward", &cst::scst_loss_backward);
   m.def("featpool_backward", &cst::featpool_backward);
+  m.def("set_stamp_base", &cst::set_stamp_base);
+  m.def("stamp_buffer", &cst::stamp_buffer);
+  m.def("stamp_now", &cst::stamp_now);
+  m.def("wall_clock_khz", &cst::wall_clock_khz);
 }

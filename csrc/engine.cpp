@@ -34,6 +34,31 @@ namespace cst {
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// Device timeline stamps (kernels/stamp.hip): the caller picks the base slot
+// of the next decoder_forward / decoder_backward call (sample and greedy
+// decodes of one step use different bases); -1 = no stamps from the executor.
+static int g_stamp_base = -1;
+void set_stamp_base(int64_t base) { g_stamp_base = (int)base; }
+static void stamp(int rel, hipStream_t s) {
+  if (g_stamp_base >= 0) launch_stamp(g_stamp_base + rel, s);
+}
+void stamp_buffer(at::Tensor buf) {
+  if (!buf.defined() || buf.numel() == 0) {
+    set_stamp_buffer(nullptr, 0);
+    return;
+  }
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kLong && buf.is_contiguous(),
+              "stamp buffer must be a contiguous int64 GPU tensor");
+  set_stamp_buffer(buf.data_ptr<int64_t>(), (int)buf.numel());
+}
+void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
+int64_t wall_clock_khz() {
+  int dev = 0, khz = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  return khz;
+}
+
 template <class T>
 static T* ptr_or_null(const at::Tensor& t) {
   return t.defined() && t.numel() > 0 ? reinterpret_cast<T*>(t.data_ptr()) : nullptr;
@@ -330,6 +355,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   }
 
   // step 0: fused cell step from (h_{-1}, c_{-1}) = (h0, c0)
+  stamp(STAMP_FWD_BEGIN, st);
   if (has_att) run_att(0);
   launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
                        ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(h0.data_ptr()),
@@ -400,7 +426,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                (int)R, lse[0].data_ptr<float>(), st);
     if (next)
       for (int64_t l = 1; l < NL; ++l) upper_step(l, t + 1);
+    if (t == 0) stamp(STAMP_FWD_STEP0, st);
   }
+  stamp(STAMP_FWD_END, st);
   // saved: {logits16, hd of the top layer (vocab input), layer 0's gates, c, h}
   // (+ {alpha_all, q_all}) (+ {h, c, gates of layer l, hd of layer l-1} per l >= 1)
   std::vector<at::Tensor> out = {seq, g_sel, want_xe ? g_xe : at::Tensor(), lse};
@@ -595,6 +623,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     (void)hipEventRecord(ev_done, side.stream());
     if (early_comm) (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
   };
+  stamp(STAMP_BWD_BEGIN, st);
   (void)hipEventRecord(ev_ready, st);
   (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
   {
@@ -623,6 +652,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl, alpha.data_ptr<float>(),
                          ptr_or_null<int>(fix_total), side.stream());
       }
+      stamp(STAMP_BWD_ONEHOT, side.stream());
     }
     // X = E' W, chunk by chunk; the reverse loop reads alpha X (row scales at
     // load), and the scaled Hd rows of the dW GEMM are formed under it
@@ -631,13 +661,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       at::Tensor dst = dHd.narrow(0, r0, nr);
       at::mm_out(dst, Ev.narrow(0, r0, nr), wlog, at::kFloat);
       (void)hipEventRecord(aux.ev[6 + ci], side.stream());
+      if (ci == 0) stamp(STAMP_BWD_DHD0, side.stream());
     }
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
                         reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
                         reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
+    stamp(STAMP_BWD_DHD, side.stream());
     if (vh_sched == 2) {
       dw_gemm();
+      stamp(STAMP_BWD_DW, side.stream());
       db_sums(side.stream());
       dw_done();
     }
@@ -762,7 +795,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      a_wa.data_ptr<float>(), (int)Bv, (int)vdiv, (int)C, (int)A, (int)H4,
                      t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
                      dba_part.data_ptr<float>(), st, per_frame);
+    if (t == n_steps - 1) stamp(STAMP_BWD_LOOP0, st);
   }
+  stamp(STAMP_BWD_LOOP, st);
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
   at::Tensor dG2 = dGx.narrow(1, 0, H4);
   // 6. weight gradients dWx = dG^T [x ; h_prev].  The K = steps*rows
@@ -806,8 +841,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
     dw_gemm();
+    stamp(STAMP_BWD_DW, side.stream());
     db_sums(side.stream());
     whh_grad();
+    stamp(STAMP_BWD_SIDE, side.stream());
     dw_done();
   }
 
@@ -819,6 +856,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          stok.data_ptr<int>(), srow.data_ptr<int>(), (int)NR,
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
+  stamp(STAMP_BWD_TOKSUM, st);
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134
@@ -838,6 +876,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     else
       dWie.copy_(at::mm(S_tok.t(), emb, at::kFloat));
   }
+  stamp(STAMP_BWD_TOKGEMM, st);
   if (vh_sched != 0) whh_grad();
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
@@ -869,6 +908,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
              dba_part.sum(0).view({NWA}), dWq};
     }
   }
+  stamp(STAMP_BWD_END, st);
   // (The bias column sums at the end of the main chain, which ends ~0.3 ms
   // before the side stream's in step_timeline_r2_v20.txt, measured slower:
   // 3.86-3.88 vs 3.76-3.86 ms, they contend with the dW_logit GEMM;

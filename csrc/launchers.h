@@ -285,6 +285,30 @@ void launch_token_group_sum(const uint16_t* x, int C, int64_t ld, const int* sto
 void launch_token_sort(const int64_t* toks, int N, int V, int* ws, int* stok, int* srow,
                        hipStream_t stream);
 
+// stamp.hip: device timeline stamps (wall clock, 100 MHz) into a registered
+// int64 buffer; no buffer registered = nothing is enqueued
+void set_stamp_buffer(int64_t* buf, int slots);
+bool stamps_enabled();
+void launch_stamp(int slot, hipStream_t stream);
+// slots written by the C++ executor, relative to the base the caller set
+// (engine.cpp set_stamp_base): forward and backward phases
+enum StampSlot : int {
+  STAMP_FWD_BEGIN = 0,    // decoder_forward: before the first cell step
+  STAMP_FWD_STEP0 = 1,    // after step 0's decode launch + combine
+  STAMP_FWD_END = 2,      // after the last combine
+  STAMP_BWD_BEGIN = 0,    // decoder_backward, main stream: entry
+  STAMP_BWD_ONEHOT = 1,   // side: alpha / one-hot terms folded into E
+  STAMP_BWD_DHD0 = 2,     // side: first dHd chunk
+  STAMP_BWD_DHD = 3,      // side: all dHd chunks (+ scaled Hd rows)
+  STAMP_BWD_LOOP0 = 4,    // main: first reverse step done
+  STAMP_BWD_LOOP = 5,     // main: reverse loop done
+  STAMP_BWD_DW = 6,       // side: dW_logit GEMM done
+  STAMP_BWD_SIDE = 7,     // side: bias column sums + recurrent weight GEMMs done
+  STAMP_BWD_TOKSUM = 8,   // main: per-token gate-gradient sums done
+  STAMP_BWD_TOKGEMM = 9,  // main: embedding / input-weight GEMMs done
+  STAMP_BWD_END = 10,     // main: video / attention gradients done (return)
+};
+
 // beam.hip
 void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,
                       float* top_v, int* top_i, hipStream_t stream);

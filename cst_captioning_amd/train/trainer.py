@@ -35,7 +35,7 @@ from ..ops.adam import FlatAdam
 from ..ops.cider_d import CiderDScorer, GenericScorer
 from ..parallel import FlatGradBucket
 from ..reward.rewards import cst_from_scores, scst_from_scores
-from ..utils import schedules
+from ..utils import schedules, stamps
 from ..utils.text import decode_sequence, compute_avglogp
 from ..data.dataset import LazyGather
 from ..utils.timers import PhaseTimer
@@ -195,14 +195,21 @@ class Trainer:
         # fused engine: reward, mask and REINFORCE loss in one launch
         # (ops/scst_loss.py), the greedy scores per video
         fused = self.engine is not None and opt.use_cst == 0 and self.device.type == 'cuda'
+        stamps.base('fwd_sample')
         model_res, logprobs, _ = self._decode_rollout(data)
+        stamps.mark('rollout_enq')
         if side is not None:
             side.wait_event(inputs_ready)
             with torch.cuda.stream(side):
+                stamps.mark('greedy_begin')
+                stamps.base('fwd_greedy')
                 greedy_scores = self._greedy_scores(data, scorer, S, per_video=fused)
+                stamps.mark('greedy_end')
+        stamps.base(None)
         self.timer.mark('rollout')
         if opt.use_cst == 0:
             sample_scores = scorer.score(model_res, vid_rows)
+            stamps.mark('sample_scores')
             if side is not None:
                 main.wait_stream(side)
                 greedy_scores.record_stream(main)
@@ -212,6 +219,7 @@ class Trainer:
                 from ..ops.scst_loss import scst_loss
                 loss, reward, m_score, b_score = scst_loss(model_res, logprobs, sample_scores,
                                                            greedy_scores)
+                stamps.mark('loss')
                 self.timer.mark('reward')
                 return loss, {'reward': reward, 'm': m_score, 'b': b_score, 'seq': model_res}
             reward, m_score, b_score = scst_from_scores(sample_scores.float(),
@@ -265,12 +273,16 @@ class Trainer:
         m.train()
         self.optimizer.zero_grad()
         m.set_seq_per_img(self.train_loader.get_seq_per_img())
+        stamps.mark('step')
         with torch.autocast('cuda', dtype=torch.bfloat16, enabled=self.autocast_bf16):
             if self.rl_training:
                 loss, extra = self.rl_loss(data, scb)
             else:
                 loss, extra = self.xe_loss(data)
+        stamps.base('bwd')
         loss.backward()
+        stamps.base(None)
+        stamps.mark('bwd_end')
         self.timer.mark('backward')
         skip = None
         if getattr(opt, 'nan_guard', 1):
@@ -284,9 +296,12 @@ class Trainer:
         """(after the gradient all-reduce) clip + Adam + weight shadows."""
         if getattr(self.opt, 'nan_guard', 1) and self.ctx.enabled:
             skip = self.bucket.flag_any()
+        stamps.mark('adam_begin')
         self.optimizer.step(skip)
+        stamps.mark('adam_end')
         if self.engine is not None:
             self.engine.after_step()
+        stamps.mark('ptab_end')
         self.timer.mark('optimizer')
 
     def _sharded_update(self, skip):
