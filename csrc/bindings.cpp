@@ -26,7 +26,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor out_emb, at::Tensor ds_bias, int64_t cell,
                                          std::vector<at::Tensor> state0,
                                          std::vector<at::Tensor> up, at::Tensor blog,
-                                         at::Tensor fix_total);
+                                         at::Tensor fix_total, int64_t vgate_div,
+                                         at::Tensor xw);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,

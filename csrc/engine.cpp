@@ -299,6 +299,38 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
   at::Tensor xin = NL > 1 ? at::empty({R, H4}, f32) : at::Tensor();
 
+  // X in the rollout: the vocab head's backward GEMM X = E W (dHd = alpha X +
+  // one-hot rows, kernels/vocab_grad.hip) reads only the exp store and the
+  // logit weights, so it runs here, chunk by chunk on a side stream, in the
+  // CUs the latency-bound decode chain leaves idle, instead of in front of
+  // the reverse loop.  Chunks of CSTCAP_FWD_X steps (0 = off) and a last
+  // one-step chunk, so the join at the end of the forward waits for one
+  // 1,280-row GEMM at most.  Measured (device stamps, gpurun_out ->
+  // profiles/r3/ab_fwdx.txt): the reverse loop alone drops from 830 to 524 us,
+  // but the GEMM's long-K workgroups hold CUs the 28 decode launches need
+  // (rollout 1.50 -> 2.22 ms) and the greedy branch starts late: 4.57 ms per
+  // step at 4-step chunks, 4.04 at 7, vs 3.82-3.92 off.  Kept as an option,
+  // default off.
+  int64_t x_chunk = 0;  // off: see the comment above
+  if (const char* e = getenv("CSTCAP_FWD_X")) x_chunk = atoll(e);
+  const bool fwd_x = save && store_exp && x_chunk > 0;
+  at::Tensor xw = fwd_x ? at::empty({n_steps, R, H}, f32) : at::empty({0}, f32);
+  DeviceAux& faux = device_aux((int)dev.index());
+  int64_t x_next = 0;  // first step not yet in a chunk
+  auto x_chunk_after = [&](int64_t t) {  // step t's exp rows are enqueued on st
+    if (!fwd_x) return;
+    const bool end = (t + 1) % x_chunk == 0 || t + 1 >= n_steps - 1;
+    if (!end) return;
+    (void)hipEventRecord(faux.ev[4], st);
+    (void)hipStreamWaitEvent(faux.side[0].stream(), faux.ev[4], 0);
+    c10::hip::HIPStreamGuard guard(faux.side[0]);
+    const int64_t r0 = x_next * R, nr = (t + 1 - x_next) * R;
+    at::Tensor dst = xw.view({n_steps * R, H}).narrow(0, r0, nr);
+    at::mm_out(dst, logits16.view({n_steps * R, ldl}).narrow(0, r0, nr).narrow(1, 0, V), wlog,
+               at::kFloat);
+    x_next = t + 1;
+  };
+
   // layer l >= 1 at step t (its zero initial state is h0 / c0's zeros)
   auto upper_step = [&](int64_t l, int64_t t) {
     const at::Tensor& wu = up[2 * (l - 1)];
@@ -424,9 +456,14 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     if (save && store_exp && t == 0)
       launch_vocab_exp_convert(reinterpret_cast<uint16_t*>(logits16[0].data_ptr()), ldl, (int)V,
                                (int)R, lse[0].data_ptr<float>(), st);
+    x_chunk_after(t);
     if (next)
       for (int64_t l = 1; l < NL; ++l) upper_step(l, t + 1);
     if (t == 0) stamp(STAMP_FWD_STEP0, st);
+  }
+  if (fwd_x) {  // join the X chunks (the last one covers a single step)
+    (void)hipEventRecord(faux.ev[5], faux.side[0].stream());
+    (void)hipStreamWaitEvent(st, faux.ev[5], 0);
   }
   stamp(STAMP_FWD_END, st);
   // saved: {logits16, hd of the top layer (vocab input), layer 0's gates, c, h}
@@ -449,10 +486,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       out.push_back(HDs[l - 1]);
     }
   }
+  out.push_back(xw);  // last: X = E W from the rollout (empty unless computed)
   return out;
 }
 
-// Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), d_emb (V, E), dvg_rows (R, 4H)}
+// Returns {dWx_packed (4H, E+H), dWlog (V, H), dblog (V), d_emb (V, E), d_vgate (R / vgate_div, 4H)}
 // (+ {dGv (Bv, C, 4H), dP (Bv, C, A), dw_a (A), db_a (1), dW_q (A, H)} with attention,
 // att = {Gv, P, W_q bf16, w_a, alpha_all (n, R, C), q_all (n, R, A)}; dvg_rows empty)
 // (+ {dh0 (R, H) through W_hh, dc0 (R, H) the state carry} with an initial
@@ -486,7 +524,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          at::Tensor out_emb, at::Tensor ds_bias, int64_t cell,
                                          std::vector<at::Tensor> state0,
                                          std::vector<at::Tensor> up, at::Tensor blog,
-                                         at::Tensor fix_total) {
+                                         at::Tensor fix_total, int64_t vgate_div,
+                                         at::Tensor xw) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -544,7 +583,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // (smallest) chunk instead of after the whole 35,840-row GEMM, and the rest
   // of the GEMM runs under the loop
   std::vector<std::array<int64_t, 2>> dhd_chunks;  // [t0, t1)
-  {
+  // X = E W computed during the rollout (decoder_forward "X in the rollout"):
+  // no GEMM here, the loop waits only for the row weights
+  const bool have_x = xw.defined() && xw.numel() > 0;
+  if (have_x)
+    TORCH_CHECK(xw.is_cuda() && xw.scalar_type() == at::kFloat && xw.is_contiguous() &&
+                    xw.numel() == NR * H && !(ds_bias.defined() && ds_bias.numel() > 0),
+                "xw must be the forward's fp32 (n_steps, R, H) X = E W (exp store only)");
+  if (have_x) {
+    dhd_chunks.push_back({0, n_steps});
+  } else {
     int64_t t1 = n_steps;
     // (A/B runs: CSTCAP_DHD_CHUNKS="first,rest" steps per chunk)
     int64_t k_first = 2, k_rest = 4;
@@ -579,7 +627,17 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor buf = logits16.scalar_type() == at::kBFloat16 ? logits16 : logits16.view(at::kBFloat16);
   at::Tensor Ev = buf.view({NR, ldl}).narrow(1, 0, V);  // E (or dense dS), K = V columns
   at::Tensor hd2 = hdrop_all.view({NR, H});
-  at::Tensor dHd = at::empty({NR, H}, f32);
+  at::Tensor dHd = have_x ? xw.view({NR, H}) : at::empty({NR, H}, f32);
+  // the row's one-hot weights / tokens for the loop (forward X only)
+  at::Tensor oh_a, oh_ys, oh_b, oh_yx;
+  if (have_x) {
+    oh_a = at::empty({NR}, f32);
+    oh_ys = at::empty({NR}, i32);
+    if (has_xe) {
+      oh_b = at::empty({NR}, f32);
+      oh_yx = at::empty({NR}, i32);
+    }
+  }
   const bool early = out_wlog.defined() && out_wlog.numel() > 0;
   if (early) {
     TORCH_CHECK(out_wlog.scalar_type() == at::kFloat && out_wlog.is_contiguous() &&
@@ -610,8 +668,23 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const bool early_comm = early && comm_stream != 0;
   int vh_sched = early_comm ? 2 : 0;
   if (const char* e = getenv("CSTCAP_VH_SCHED")) vh_sched = atoi(e);  // A/B experiments
+  // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
+  // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
+  // split-K batch over groups of decode steps multiplies the tiles in flight,
+  // the partial products summed afterwards (CSTCAP_DW_SPLITK; must divide the
+  // step count)
+  int64_t dw_split = 1;
+  if (const char* e = getenv("CSTCAP_DW_SPLITK")) dw_split = std::max<int64_t>(1, atoll(e));
+  if (n_steps % dw_split != 0) dw_split = 1;
   auto dw_gemm = [&]() {  // (current stream: side)
-    at::mm_out(dWlog, Ev.t(), ds_ready ? hd2 : hs, at::kFloat);
+    const at::Tensor& rhs = ds_ready ? hd2 : hs;
+    if (dw_split == 1) {
+      at::mm_out(dWlog, Ev.t(), rhs, at::kFloat);
+      return;
+    }
+    const int64_t kr = NR / dw_split;
+    at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
+    at::sum_out(dWlog, at::bmm(a, rhs.view({dw_split, kr, H}), at::kFloat), 0);
   };
   auto db_sums = [&](hipStream_t s) {  // (current stream: s)
     if (ds_ready)
@@ -638,7 +711,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                    has_sel ? dg_sel.data_ptr<float>() : nullptr,
                    has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
                    has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                   has_xe ? dg_xe.size(1) : 0, guard ? fix.data_ptr<int>() : nullptr};
+                   has_xe ? dg_xe.size(1) : 0, guard ? fix.data_ptr<int>() : nullptr,
+                   ptr_or_null<float>(oh_a), ptr_or_null<int>(oh_ys), ptr_or_null<float>(oh_b),
+                   ptr_or_null<int>(oh_yx), have_x ? dHd.data_ptr<float>() : nullptr};
       launch_vgrad_onehot(va, reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl,
                           alpha.data_ptr<float>(), side.stream());
       if (guard) {
@@ -659,7 +734,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     for (size_t ci = 0; ci < dhd_chunks.size(); ++ci) {
       const int64_t r0 = dhd_chunks[ci][0] * R, nr = (dhd_chunks[ci][1] - dhd_chunks[ci][0]) * R;
       at::Tensor dst = dHd.narrow(0, r0, nr);
-      at::mm_out(dst, Ev.narrow(0, r0, nr), wlog, at::kFloat);
+      if (!have_x) at::mm_out(dst, Ev.narrow(0, r0, nr), wlog, at::kFloat);
       (void)hipEventRecord(aux.ev[6 + ci], side.stream());
       if (ci == 0) stamp(STAMP_BWD_DHD0, side.stream());
     }
@@ -673,6 +748,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       stamp(STAMP_BWD_DW, side.stream());
       db_sums(side.stream());
       dw_done();
+    } else if (vh_sched == 3) {  // bias column sums (HBM-bound) under the loop
+      db_sums(side.stream());
     }
   }
   // token-only operands of the embedding / input-weight gradients: rows
@@ -741,20 +818,31 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   auto dh_scale_t = [&](int64_t t) -> const float* {
     return ds_ready ? nullptr : alpha.data_ptr<float>() + t * R;
   };
+  // forward X: the one-hot rows of the top layer's h gradient (see DhOneHot)
+  auto dh_onehot_t = [&](int64_t t) -> DhOneHot {
+    if (!have_x) return DhOneHot{};
+    return DhOneHot{reinterpret_cast<const uint16_t*>(wlog.data_ptr()),
+                    oh_a.data_ptr<float>() + t * R, oh_ys.data_ptr<int>() + t * R,
+                    has_xe ? oh_b.data_ptr<float>() + t * R : nullptr,
+                    has_xe ? oh_yx.data_ptr<int>() + t * R : nullptr};
+  };
   size_t next_chunk = 0;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     if (next_chunk < dhd_chunks.size() && t == dhd_chunks[next_chunk][1] - 1)
       (void)hipStreamWaitEvent(st, aux.ev[6 + next_chunk++], 0);  // dHd rows of this chunk
+    const DhOneHot oh_t = dh_onehot_t(t);
     // top layer first: its h gradient comes from the vocab head (dHd, with the
     // vocab dropout mask); layer l < top gets dG_{l+1, t} W_ih_{l+1} through
     // the inter-layer dropout mask of layer l's output
     for (int64_t l = NL - 1; l >= 1; --l) {
       const float* dh_in = dHd.data_ptr<float>() + t * R * H;
       const float* dh_sc = dh_scale_t(t);
+      const DhOneHot* ohp = &oh_t;
       if (l < NL - 1) {
         at::mm_out(dX_up, dG_up[l + 1][t], upw(l + 1, 0).narrow(1, 0, H), at::kFloat);
         dh_in = dX_up.data_ptr<float>();
         dh_sc = nullptr;
+        ohp = nullptr;
       }
       launch_lstm_step_bwd(
           t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_up[l][t + 1].data_ptr()) : nullptr,
@@ -762,7 +850,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
           dc_up[l].data_ptr<float>(), reinterpret_cast<const uint16_t*>(upw(l, 3)[t].data_ptr()),
           upw(l, 2)[t].data_ptr<float>(), t > 0 ? upw(l, 2)[t - 1].data_ptr<float>() : nullptr,
           (int)R, (int)H, (float)drop_p, RNG, key(l, t),
-          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell, dh_sc);
+          reinterpret_cast<uint16_t*>(dG_up[l][t].data_ptr()), (int)H4, st, (int)cell, dh_sc,
+          nullptr, ohp);
     }
     const float* dh0_in = dHd.data_ptr<float>() + t * R * H;
     const float* dh0_sc = dh_scale_t(t);
@@ -779,7 +868,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
         (int)R, (int)H, (float)drop_p, RNG, key(0, t),
         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc,
-        att_mfma ? &abe : nullptr);
+        att_mfma ? &abe : nullptr, NL == 1 ? &oh_t : nullptr);
     if (att_mfma)
       launch_att_bwd_mfma(dal_part.data_ptr<float>(), (int)(H / 64), (int)R,
                           a_alpha[t].data_ptr<float>(), t > 0 ? a_q[t].data_ptr<float>() : nullptr,
@@ -836,13 +925,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // interleaved on one box, profiles/r2/ab_whh_side_splitk.txt).  (Outputs
   // written there were allocated on the main stream, which joins the side
   // stream before returning.)
-  if (vh_sched == 0) {
+  if (vh_sched == 0 || vh_sched == 3) {
     (void)hipEventRecord(ev_ready, st);  // reverse loop done
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
     dw_gemm();
     stamp(STAMP_BWD_DW, side.stream());
-    db_sums(side.stream());
+    if (vh_sched == 0) db_sums(side.stream());
     whh_grad();
     stamp(STAMP_BWD_SIDE, side.stream());
     dw_done();
@@ -877,14 +966,21 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       dWie.copy_(at::mm(S_tok.t(), emb, at::kFloat));
   }
   stamp(STAMP_BWD_TOKGEMM, st);
-  if (vh_sched != 0) whh_grad();
+  if (vh_sched == 2) whh_grad();
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
     dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);
   at::Tensor dvg;
   std::vector<at::Tensor> res;
   if (!has_att) {
-    dvg = dG_all.sum(0, false, at::kFloat);  // (R, 4H), sum over time
+    // (Bv, 4H): sum over time and over the rows of each video in one pass
+    // (kernels/embed_grad.hip; was a (R, 4H) sum over time, 78 us, plus a
+    // per-video sum in Python)
+    TORCH_CHECK(vgate_div >= 1 && R % vgate_div == 0, "vgate_div must divide the rows");
+    dvg = at::empty({R / vgate_div, H4}, f32);
+    launch_video_gate_grad(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), KD,
+                           (int)n_steps, (int)R, (int)vgate_div, (int)H4, dvg.data_ptr<float>(),
+                           st);
   } else {
     // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r] (kernels/attention.hip:
     // one pass over the bf16 dG rows, partials per step chunk)

@@ -295,4 +295,71 @@ void launch_token_sort(const int64_t* toks, int N, int V, int* ws, int* stok, in
   post_launch("token_scatter_kernel", stream);
 }
 
+// ---- video-gate gradient (mean-pooled features) -----------------------------
+// d_vgate[b] = sum over steps t and the vdiv rows of video b of dG_t[row, 0:G4]
+// (the per-video gate term W_iv . v enters every step's cell of every caption
+// row of the video, lstm.hip).  One pass over the bf16 gate-gradient rows
+// (n_steps x R x ld) straight into the (Bv, G4) fp32 result: the former
+// dG.sum over time (fp32 R x G4 intermediate, 147 MB read) plus a second
+// reduction over the rows of each video are one launch.  Block (video b,
+// 256-column chunk): thread = 8 consecutive columns (one 16-byte load) of
+// every 8th row of the video's n_steps * vdiv rows, RG_PF loads in flight;
+// the 8 row partials are summed through LDS.
+constexpr int RG_PF = 4;
+__global__ __launch_bounds__(256) void video_gate_grad_kernel(const uint16_t* __restrict__ dG,
+                                                              int64_t ld, int n_steps, int R,
+                                                              int vdiv, int G4,
+                                                              float* __restrict__ out) {
+  __shared__ float s_part[8][256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int cg = tid & 31, rs = tid >> 5;
+  const int col = blockIdx.y * 256 + 8 * cg;
+  const int colc = min(col, G4 - 8);  // (clamped: loads stay unconditional)
+  const int nrows = n_steps * vdiv;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  auto row_ptr = [&](int i) {
+    const int t = i / vdiv, j = i - t * vdiv;
+    return reinterpret_cast<const uint4*>(dG + ((int64_t)t * R + (int64_t)b * vdiv + j) * ld + colc);
+  };
+  for (int i0 = rs; i0 < nrows; i0 += 8 * RG_PF) {
+    uint4 q[RG_PF];
+#pragma unroll
+    for (int k = 0; k < RG_PF; ++k) q[k] = *row_ptr(min(i0 + 8 * k, nrows - 1));
+#pragma unroll
+    for (int k = 0; k < RG_PF; ++k) {
+      if (i0 + 8 * k < nrows) {
+        const uint32_t w[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += bf2f(w[e] & 0xffff);
+          acc[2 * e + 1] += bf2f(w[e] >> 16);
+        }
+      }
+    }
+  }
+  // column chunk of 8 -> LDS row rs, then column tid sums the 8 row partials
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s_part[rs][8 * cg + k] = acc[k];
+  __syncthreads();
+  const int c = blockIdx.y * 256 + tid;
+  if (c < G4 && col <= G4) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v += s_part[r][tid];
+    out[(int64_t)b * G4 + c] = v;
+  }
+}
+
+void launch_video_gate_grad(const uint16_t* dG, int64_t ld, int n_steps, int R, int vdiv, int G4,
+                            float* out, hipStream_t stream) {
+  if (G4 % 8 != 0 || G4 < 8 || R % vdiv != 0 || ld % 8 != 0)
+    throw std::runtime_error("video_gate_grad: unsupported shape");
+  const dim3 grid(R / vdiv, (G4 + 255) / 256);
+  hipLaunchKernelGGL(video_gate_grad_kernel, grid, dim3(256), 0, stream, dG, ld, n_steps, R, vdiv,
+                     G4, out);
+  post_launch("video_gate_grad_kernel", stream);
+}
+
 }  // namespace cst

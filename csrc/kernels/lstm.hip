@@ -178,8 +178,8 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
                                                   const float* __restrict__ dc_carry,
                                                   const float* __restrict__ dh_logit,
                                                   const float* __restrict__ dh_scale,
-                                                  uint2* pg, float* pc, float* pcp, float* pdc,
-                                                  float* pdl) {
+                                                  const DhOneHot& oh, uint2* pg, float* pc,
+                                                  float* pcp, float* pdc, float* pdl) {
   constexpr int RG = 4 * GROUPS, RPT = BM / RG;
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
@@ -190,6 +190,24 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
     pcp[i] = c_prev ? c_prev[o] : 0.f;
     pdc[i] = dc_carry[o];
     pdl[i] = dh_logit[o] * (dh_scale ? dh_scale[r] : 1.f);
+  }
+  // forward-computed X = E W: the one-hot terms a W[ys] + b W[yx] of the row
+  // (uniform branches; the token rows are gathered with the other operands)
+  if (oh.a != nullptr) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = min(r0 + rg + RG * i, R - 1);
+      const int y = oh.ys[r];
+      pdl[i] = fmaf(oh.a[r], bf2f(oh.W[(int64_t)max(y, 0) * H + hu]), pdl[i]);
+    }
+  }
+  if (oh.b != nullptr) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = min(r0 + rg + RG * i, R - 1);
+      const int y = oh.yx[r];
+      pdl[i] = fmaf(oh.b[r], bf2f(oh.W[(int64_t)max(y, 0) * H + hu]), pdl[i]);
+    }
   }
 }
 
@@ -219,7 +237,7 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p,
     const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int cell,
-    const float* __restrict__ dh_scale, AttBwdEpi att) {
+    const float* __restrict__ dh_scale, AttBwdEpi att, DhOneHot oh) {
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
@@ -237,7 +255,7 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
   float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
   // the epilogue operands' latency hides under the GEMM
   lstm_bwd_load_epi<BM, GROUPS>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit,
-                                dh_scale, pg, pc, pcp, pdc, pdl);
+                                dh_scale, oh, pg, pc, pcp, pdc, pdl);
   static_assert(!ATT || (GROUPS == 2 && BM == 64), "attention epilogue: 2 groups of 64 rows");
   constexpr int SLICE = 64 * 4 * CP;  // bf16 per video slice
   int v0 = 0, nvs = 0;
@@ -370,7 +388,7 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
                                    const float* c_t, const float* c_prev, int R, int H,
                                    float drop_p, const uint32_t* rng, int step, uint16_t* dG,
                                    int KD, hipStream_t stream, int cell, const float* dh_scale,
-                                   const AttBwdEpi& att) {
+                                   const AttBwdEpi& att, const DhOneHot& oh) {
   constexpr int BM = 64;
   using TL = Tile<BM, 64, STAGES>;
   constexpr int LDS = GROUPS * TL::STAGES * TL::STAGE_BYTES > GROUPS * BM * TL::CSTRIDE * 4
@@ -385,7 +403,7 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
   const int n = (H / 64) * ((R + BM - 1) / BM);
   hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP>), dim3(n),
                      dim3(256 * GROUPS), LDS, stream, dg_next, whhT, dh_logit, dc_carry, gates,
-                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale, att);
+                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale, att, oh);
   post_launch("lstm_step_bwd_kernel", stream);
 }
 
@@ -393,7 +411,8 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                          const float* dh_scale, const AttBwdEpi* att) {
+                          const float* dh_scale, const AttBwdEpi* att, const DhOneHot* ohp) {
+  const DhOneHot oh = ohp != nullptr ? *ohp : DhOneHot{};
   // two K groups per block when the K-tiles split evenly
   // (measured per step: 1 group 4.66 ms, 2 groups 4.54 ms, 4 groups with 2
   // LDS stages each 4.51 vs 4.47 ms for 2 groups on another box)
@@ -404,20 +423,20 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
     if (att->CP == 8)
       launch_lstm_step_bwd_g<2, true, 8>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev,
                                          R, H, drop_p, rng, step, dG, KD, stream, cell, dh_scale,
-                                         *att);
+                                         *att, oh);
     else
       launch_lstm_step_bwd_g<2, true, 16>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev,
                                           R, H, drop_p, rng, step, dG, KD, stream, cell, dh_scale,
-                                          *att);
+                                          *att, oh);
     return;
   }
   const AttBwdEpi none{};
   if ((KD / 64) % 2 == 0)
     launch_lstm_step_bwd_g<2>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, none);
+                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, none, oh);
   else
     launch_lstm_step_bwd_g<1>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H,
-                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, none);
+                              drop_p, rng, step, dG, KD, stream, cell, dh_scale, none, oh);
 }
 
 // 128-row tiles x 64 packed gate columns, 3 LDS stages (72 KB, 2 blocks per CU)

@@ -82,6 +82,15 @@ __global__ __launch_bounds__(256) void vgrad_onehot_kernel(VGradRows g, uint16_t
   const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (row >= NR) return;
   const int t = (int)(row / g.R);
+  if (g.oh_a != nullptr) {  // forward-computed X: the loop adds the one-hot terms itself
+    const RowW w = row_weights(g, row);
+    g.oh_a[row] = w.a;
+    g.oh_ys[row] = w.ys;
+    if (g.oh_b != nullptr) {
+      g.oh_b[row] = w.b;
+      g.oh_yx[row] = w.yx;
+    }
+  }
   if (g.fix != nullptr && t > 0) {
     const float d = g.lse[row] - g.lse[row - g.R];
     if (fabsf(d) > EXP_SAFE_LSE_JUMP) {  // E may be out of range: recomputed by vgrad_fix
@@ -140,6 +149,14 @@ __global__ __launch_bounds__(256) void vgrad_fix_kernel(VGradRows g, const uint1
       e[v] = f2bf(__expf(x + bias[v] - L));
     }
     __syncthreads();  // the row's E is complete before the one-hot fold
+    if (g.X != nullptr) {  // forward-computed X = E W: this row's, from the exact E
+      for (int hc = threadIdx.x; hc < H; hc += 256) {
+        float x = 0.f;
+        for (int v = 0; v < g.V; ++v) x = fmaf(bf2f(e[v]), bf2f(W[(int64_t)v * H + hc]), x);
+        g.X[row * H + hc] = x;
+      }
+      __syncthreads();  // every thread read the unfolded row
+    }
     if (threadIdx.x == 0) {
       const RowW w = row_weights(g, row, /*unit_s=*/true);
       alpha[row] = w.al;

@@ -154,6 +154,15 @@ struct VGradRows {
   // EXP_SAFE_LSE_JUMP from the previous step are listed here by
   // vgrad_onehot ([0] = count, then flat row ids) and recomputed by vgrad_fix
   int* fix;
+  // forward-computed X = E W (engine.cpp "X in the rollout"): vgrad_onehot also
+  // writes each row's one-hot weights / tokens (nullable outputs, NR each;
+  // token -1 = none), so the loop forms dHd = alpha X + a W[ys] + b W[yx]
+  // without the folded E', and vgrad_fix recomputes the listed rows of X
+  float* oh_a;
+  int* oh_ys;
+  float* oh_b;
+  int* oh_yx;
+  float* X;  // (NR, H) fp32, nullable
 };
 constexpr float EXP_SAFE_LSE_JUMP = 60.f;
 // alpha (NR) and the one-hot terms folded into E (NR rows, stride ldl), in place
@@ -191,6 +200,17 @@ int lstm_bwd_tiles(int R, int H);
 // path): per 64-unit column tile, the partial dalpha[r][c] = sum over the
 // tile's 256 packed gate columns of dG[r][n] Gv[video(r)][n][c] (kernels
 // lstm.hip); kernels/attention.hip att_bwd_mfma sums the H/64 partials.
+// One-hot part of the vocab head's h gradient when the loop reads the
+// forward-computed X = E W instead of E' W: dh_logit row r gets
+// + a[r] W[ys[r]] + b[r] W[yx[r]] (W: logit weights (V, H) bf16; a / ys, b /
+// yx nullable, this step's R rows; token < 0: no term)
+struct DhOneHot {
+  const uint16_t* W;
+  const float* a;
+  const int* ys;
+  const float* b;
+  const int* yx;
+};
 struct AttBwdEpi {
   const uint16_t* gvb16;  // (Bv, H, CP, 4) bf16 gate tables, the 4 gates of a unit innermost
   int vdiv, C, CP;
@@ -202,7 +222,8 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
                           int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
                           const float* dh_scale = nullptr,  // dh_logit row scales (nullable)
-                          const AttBwdEpi* att = nullptr);
+                          const AttBwdEpi* att = nullptr,
+                          const struct DhOneHot* oh = nullptr);
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal
 // attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
@@ -280,6 +301,10 @@ void launch_token_long_zero(const int* ws, int V, int C, float* S32, hipStream_t
 void launch_token_group_sum(const uint16_t* x, int C, int64_t ld, const int* stok,
                             const int* srow, int N, const int* ws, int V, uint16_t* S, float* S32,
                             hipStream_t stream);
+// d_vgate (Bv = R / vdiv, G4) fp32 = sum over the n_steps steps and the vdiv
+// rows of each video of the bf16 rows dG (row stride ld, first G4 columns)
+void launch_video_gate_grad(const uint16_t* dG, int64_t ld, int n_steps, int R, int vdiv, int G4,
+                            float* out, hipStream_t stream);
 // counting sort of N token ids (< V <= 65536) into (stok, srow); ws: 2V + 1 ints,
 // ws[2V] = number of sorted entries (ids outside [0, V) are left out)
 void launch_token_sort(const int64_t* toks, int N, int V, int* ws, int* stok, int* srow,

@@ -160,6 +160,8 @@ class _DecoderFn(torch.autograd.Function):
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
             drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell,
             state0, eng.upper_operands(), bool(save and not want_full))
+        # last output: X = E W computed during the rollout (empty if not)
+        xw, outs = outs[-1], outs[:-1]
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
         # training rollouts save E = exp(logit - previous step's LSE) (bf16) for
@@ -181,7 +183,7 @@ class _DecoderFn(torch.autograd.Function):
         ctx.state0 = state0 if save else []
         ctx.att_saved = None
         if save:
-            ctx.saved = (lse, *outs[4:9], seq, labels, bos)
+            ctx.saved = (lse, *outs[4:9], seq, labels, bos, xw)
             if has_att:  # Gv, P, W_q, w_a, alpha_all, q_all
                 ctx.att_saved = (att[0], att[1], att[2], att[3], outs[9], outs[10])
             ctx.up_saved = outs[11 if has_att else 9:]  # (h, c, gates, hd_in) per upper layer
@@ -201,7 +203,7 @@ class _DecoderFn(torch.autograd.Function):
             raise RuntimeError('decoder forward ran without saving activations')
         R, T, vdiv, want_xe = ctx.save_dims
         eng = ctx.eng
-        lse, logits16, hdrop, gates, c_all, h_all, seq, labels, bos = ctx.saved
+        lse, logits16, hdrop, gates, c_all, h_all, seq, labels, bos, xw = ctx.saved
         ctx.saved = None  # (the fp16-logits buffer is overwritten in place by dS)
         att = list(ctx.att_saved) if ctx.has_att else []
         ctx.att_saved = None
@@ -263,7 +265,8 @@ class _DecoderFn(torch.autograd.Function):
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
             ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell,
-            ctx.state0, eng.upper_operands(ctx.up_saved), ctx.logit_b, eng.exp_fix_rows)
+            ctx.state0, eng.upper_operands(ctx.up_saved), ctx.logit_b, eng.exp_fix_rows,
+            vdiv, xw if ctx.store_exp else empty)
         ctx.logit_b = None
         ctx.up_saved = None
         d_up = []
@@ -303,8 +306,7 @@ class _DecoderFn(torch.autograd.Function):
             d_wa, d_ba = d_wa.view(ctx.att_shapes[0]), d_ba.view(ctx.att_shapes[1])
             return (None, d_wih, d_whh, d_emb, dWlog, dblog, d_gv, d_pre, d_wq, d_wa,
                     d_ba) + (None,) * 18
-        nv = R // vdiv
-        d_vgate = dvg.view(nv, vdiv, -1).sum(1)
+        d_vgate = dvg  # (R // vdiv, 4H): summed over steps and each video's rows
         return (d_vgate, d_wih, d_whh, d_emb, dWlog, dblog) + (None,) * 5 + d_state + \
             (None,) * 16 + tuple(d_up)
 
@@ -353,6 +355,18 @@ class DecoderEngine:
         self.wup = [torch.empty(4 * H, 2 * H, **bf) for _ in range(self.layers - 1)]
         self.whh_up = [torch.empty(4 * H, H, **bf) for _ in range(self.layers - 1)]
         self.fused_refresh = False  # True once an optimizer writes the shadows
+        # the input-token gate table is refreshed lazily: after_step() only
+        # bumps weights_version; the next training step computes the table on
+        # a side stream under its prologue (prefetch_ptab), every other user
+        # recomputes a stale table first (ensure_ptab)
+        self.weights_version = 0
+        self._ptab_version = -1
+        self._ptab_pending = None  # event of this step's prefetch
+        self._ptab_stream = None
+        if dev.type == 'cuda':  # (created here: never during a graph capture)
+            self._ptab_stream = torch.cuda.Stream(device=dev)
+            self._ptab_ev0 = torch.cuda.Event()
+            self._ptab_ev1 = torch.cuda.Event()
         # running count of exp-store rows the backward recomputed because the
         # row's LSE jumped by > 60 between steps (csrc/kernels/vocab_grad.hip)
         self.exp_fix_rows = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -428,6 +442,34 @@ class DecoderEngine:
         # input-token gate table P = emb . W_ie^T (V x 4H, packed gate order):
         # one GEMM per optimizer step instead of K=E of work in every decode step
         torch.mm(self.emb, self.wx[:, :self.E].t(), out_dtype=torch.float32, out=self.ptab)
+        self._ptab_version = self.weights_version
+
+    def prefetch_ptab(self):
+        """Start of a training step: a stale table is recomputed on a side
+        stream, concurrently with the step's batch gather / FeatPool prologue
+        (the decode waits for it in ensure_ptab).  Graph-capturable: the fork
+        and the join are both inside the captured step."""
+        if self._ptab_version == self.weights_version or self._ptab_stream is None:
+            return
+        main = torch.cuda.current_stream(self.ptab.device)
+        self._ptab_ev0.record(main)
+        self._ptab_stream.wait_event(self._ptab_ev0)
+        with torch.cuda.stream(self._ptab_stream):
+            self.update_ptab()
+            self._ptab_ev1.record(self._ptab_stream)
+        self._ptab_pending = self._ptab_ev1
+
+    def ensure_ptab(self):
+        """Before a decode reads the table: join this step's prefetch, or
+        recompute a stale table on the current stream."""
+        if self._ptab_version != self.weights_version:
+            self.update_ptab()
+        elif self._ptab_pending is not None:
+            torch.cuda.current_stream(self.ptab.device).wait_event(self._ptab_pending)
+
+    def current_ptab(self):
+        self.ensure_ptab()
+        return self.ptab
 
     def attach_optimizer(self, trainer):
         """The trainer's flat Adam writes the bf16 shadows in its update pass."""
@@ -438,9 +480,9 @@ class DecoderEngine:
         self.refresh_weights()  # params were re-homed into the flat buffer
 
     def after_step(self):
-        if self.fused_refresh:
-            self.update_ptab()
-        else:
+        self.weights_version += 1
+        self._ptab_pending = None
+        if not self.fused_refresh:
             self.refresh_weights()
 
     # -- gradient slots written by the fused backward -------------------------------
@@ -599,6 +641,7 @@ class DecoderEngine:
         # (inside Function.forward grad mode is off, so decide here)
         diff_in = [t for t in (vg, h0, c0) + tuple(att) if t is not None] + list(ws) + ups
         save = want_full or (torch.is_grad_enabled() and any(t.requires_grad for t in diff_in))
+        self.ensure_ptab()
         return _DecoderFn.apply(vg, *ws, *att, h0, c0, self,
                                 labels.contiguous() if labels is not None else None, bos, R, T,
                                 modes, float(ss_prob), float(drop_p), float(temperature),
@@ -690,6 +733,7 @@ class DecoderEngine:
         if self.standard:
             h0, c0 = self._initial_state(model, feats)
             state0 = [h0.bfloat16().contiguous(), c0.float().contiguous()]
+        self.ensure_ptab()
         seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog,
                                          model.logit.bias.detach().float().contiguous(),
                                          vg.detach().float().contiguous(), K, model.seq_length,

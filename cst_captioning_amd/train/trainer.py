@@ -270,6 +270,9 @@ class Trainer:
         """zero_grad -> forward -> loss -> backward (+ the NaN-guard flag).
         Device work only: no host synchronisation (graph-capturable)."""
         opt, m = self.opt, self.model
+        if (self.engine is not None and self.device.type == 'cuda'
+                and os.environ.get('CSTCAP_PTAB_PREFETCH', '1') != '0'):
+            self.engine.prefetch_ptab()  # under the prologue, on a side stream
         m.train()
         self.optimizer.zero_grad()
         m.set_seq_per_img(self.train_loader.get_seq_per_img())

@@ -215,7 +215,7 @@ def test_cell_graph_training_keeps_packed_shadows(variant):
         assert torch.isfinite(out['loss']).item()
     assert tr._graph is not None
     assert not torch.equal(w0, model.core.rnn.weight_hh_l0.detach())
-    got = [t.clone() for t in (eng.wx, eng.whh_q, eng.emb, eng.wlog, eng.ptab)]
+    got = [t.clone() for t in (eng.wx, eng.whh_q, eng.emb, eng.wlog, eng.current_ptab())]
     got_up = [t.clone() for t in eng.wup + eng.whh_up]
     eng.refresh_weights()
     for g, r in zip(got, (eng.wx, eng.whh_q, eng.emb, eng.wlog)):

@@ -117,7 +117,7 @@ def test_adam_pass_writes_the_bf16_shadows():
     for _ in range(4):
         tr.train_step(loader.get_batch(), 0)
     eng = tr.engine
-    got = [t.clone() for t in (eng.wx, eng.whh_q, eng.emb, eng.wlog, eng.ptab)]
+    got = [t.clone() for t in (eng.wx, eng.whh_q, eng.emb, eng.wlog, eng.current_ptab())]
     eng.refresh_weights()
     for g, r in zip(got, (eng.wx, eng.whh_q, eng.emb, eng.wlog)):
         assert torch.equal(g, r)

@@ -582,10 +582,11 @@ def test_exp_store_lse_jump_rows_recomputed():
     h_all = (torch.randn(n, R, H, device=DEV) * 0.1).to(bf)
     empty = torch.empty(0, device=DEV)
     fix_total = torch.zeros(1, dtype=torch.int32, device=DEV)
+    Es_fresh = Es.clone()  # the backward folds / rewrites rows of E in place
     res = ops.decoder_backward(wx, wlog, emb, lse.contiguous(), Es, hd.contiguous(), gates, c_all,
                                h_all, seq, torch.empty(0, dtype=torch.long, device=DEV), toks,
                                dg_sel, empty, 0.0, torch.empty(0, dtype=torch.int32, device=DEV),
-                               empty, empty, 0, [], empty, empty, 0, [], [], blog, fix_total)
+                               empty, empty, 0, [], empty, empty, 0, [], [], blog, fix_total, 1, empty)
     torch.cuda.synchronize()
     assert int(fix_total) == n_jump
     dWlog, dblog = res[1], res[2]
@@ -605,6 +606,23 @@ def test_exp_store_lse_jump_rows_recomputed():
                                 c_all, h_all, seq, torch.empty(0, dtype=torch.long, device=DEV),
                                 toks, dg_sel, empty, 0.0,
                                 torch.empty(0, dtype=torch.int32, device=DEV), empty, empty, 0,
-                                [], empty, empty, 0, [], [], empty, empty)
+                                [], empty, empty, 0, [], [], empty, empty, 1, empty)
     bad = res0[1]
     assert (not torch.isfinite(bad).all()) or (bad - ref_w).norm() / ref_w.norm() > 0.1
+    # X = E W from the rollout (engine.cpp "X in the rollout"): the listed rows'
+    # X is recomputed from their exact E, the loop adds the one-hot rows, and
+    # every gradient equals the X-less path's
+    xw = (Es_fresh[:, :, :V].float() @ wlog.float()).contiguous()  # inf / nan rows included
+    fix2 = torch.zeros(1, dtype=torch.int32, device=DEV)
+    res2 = ops.decoder_backward(wx, wlog, emb, lse.contiguous(), Es_fresh, hd.contiguous(), gates,
+                                c_all, h_all, seq, torch.empty(0, dtype=torch.long, device=DEV),
+                                toks, dg_sel, empty, 0.0,
+                                torch.empty(0, dtype=torch.int32, device=DEV), empty, empty, 0,
+                                [], empty, empty, 0, [], [], blog, fix2, 1, xw)
+    torch.cuda.synchronize()
+    assert int(fix2) == n_jump
+    for k in (0, 1, 2, 3, 4):  # dWx (the loop's dG), dWlog, dblog, d_emb, d_vgate
+        a, b = res2[k], res[k]
+        assert torch.isfinite(a).all(), k
+        err = (a - b).norm() / (b.norm() + 1e-12)
+        assert err < 2e-2, (k, float(err))
