@@ -666,14 +666,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // profiles/r2/ab_vh_sched.txt).  Data parallelism runs them concurrently
   // with the loop, so the vocab head's all-reduce hides under it.
   const bool early_comm = early && comm_stream != 0;
-  int vh_sched = early_comm ? 2 : 0;
+  // One GPU: the bias column sums (HBM-bound) under the latency-bound
+  // reverse loop, dW_logit after it (vh_sched 3; interleaved A/B 3.745-3.792
+  // vs 3.774-3.831 ms per step with the loop-after schedule 0,
+  // profiles/r3/ab_sched.txt)
+  int vh_sched = early_comm ? 2 : 3;
   if (const char* e = getenv("CSTCAP_VH_SCHED")) vh_sched = atoi(e);  // A/B experiments
   // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
   // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
   // split-K batch over groups of decode steps multiplies the tiles in flight,
   // the partial products summed afterwards (CSTCAP_DW_SPLITK; must divide the
   // step count)
-  int64_t dw_split = 1;
+  // (4 groups: 3.745-3.774 vs 3.792-3.831 ms per step for one GEMM, 7 groups
+  // 3.862-3.873, profiles/r3/ab_sched.txt)
+  int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
   if (const char* e = getenv("CSTCAP_DW_SPLITK")) dw_split = std::max<int64_t>(1, atoll(e));
   if (n_steps % dw_split != 0) dw_split = 1;
   auto dw_gemm = [&]() {  // (current stream: side)
