@@ -75,6 +75,7 @@ void set_stamp_base(int64_t base);
 void stamp_buffer(at::Tensor buf);
 void stamp_now(int64_t slot);
 int64_t wall_clock_khz();
+void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -154,4 +155,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stamp_buffer", &cst::stamp_buffer);
   m.def("stamp_now", &cst::stamp_now);
   m.def("wall_clock_khz", &cst::wall_clock_khz);
+  m.def("vocab_x", &cst::vocab_x);
 }

@@ -52,6 +52,20 @@ void stamp_buffer(at::Tensor buf) {
   set_stamp_buffer(buf.data_ptr<int64_t>(), (int)buf.numel());
 }
 void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
+// X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
+// fp32, on the current stream (engine.launch_x; the same GEMM as the
+// backward's dHd chunks)
+void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
+  TORCH_CHECK(logits16.is_cuda() && logits16.scalar_type() == at::kBFloat16 &&
+                  logits16.dim() == 3 && logits16.is_contiguous(),
+              "vocab_x: exp store must be a contiguous bf16 (n, R, ldl) GPU tensor");
+  const int64_t NR = logits16.size(0) * logits16.size(1), V = wlog.size(0), H = wlog.size(1);
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kFloat && out.numel() == NR * H &&
+                  logits16.size(2) >= V,
+              "vocab_x: out must be a contiguous fp32 (n, R, H) tensor");
+  at::Tensor dst = out.view({NR, H});
+  at::mm_out(dst, logits16.view({NR, logits16.size(2)}).narrow(1, 0, V), wlog, at::kFloat);
+}
 int64_t wall_clock_khz() {
   int dev = 0, khz = 0;
   (void)hipGetDevice(&dev);

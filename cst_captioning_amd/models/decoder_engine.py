@@ -182,8 +182,11 @@ class _DecoderFn(torch.autograd.Function):
         ctx.has_att = has_att
         ctx.state0 = state0 if save else []
         ctx.att_saved = None
+        ctx.xw_late = None
         if save:
             ctx.saved = (lse, *outs[4:9], seq, labels, bos, xw)
+            if ctx.store_exp and eng.x_after_rollout and xw.numel() == 0:
+                eng._x_pending = ctx  # launch_x computes X = E W for this forward
             if has_att:  # Gv, P, W_q, w_a, alpha_all, q_all
                 ctx.att_saved = (att[0], att[1], att[2], att[3], outs[9], outs[10])
             ctx.up_saved = outs[11 if has_att else 9:]  # (h, c, gates, hd_in) per upper layer
@@ -204,6 +207,10 @@ class _DecoderFn(torch.autograd.Function):
         R, T, vdiv, want_xe = ctx.save_dims
         eng = ctx.eng
         lse, logits16, hdrop, gates, c_all, h_all, seq, labels, bos, xw = ctx.saved
+        if ctx.xw_late is not None:  # X = E W launched after the rollout (launch_x)
+            xw, ev = ctx.xw_late
+            ctx.xw_late = None
+            torch.cuda.current_stream(xw.device).wait_event(ev)
         ctx.saved = None  # (the fp16-logits buffer is overwritten in place by dS)
         att = list(ctx.att_saved) if ctx.has_att else []
         ctx.att_saved = None
@@ -370,6 +377,14 @@ class DecoderEngine:
         # running count of exp-store rows the backward recomputed because the
         # row's LSE jumped by > 60 between steps (csrc/kernels/vocab_grad.hip)
         self.exp_fix_rows = torch.zeros(1, dtype=torch.int32, device=dev)
+        # X = E W after the rollout (launch_x): the trainer enables it and calls
+        # launch_x on its greedy side stream once the greedy decode is enqueued
+        self.x_after_rollout = False
+        self._x_pending = None
+        if dev.type == 'cuda':
+            self._x_stream = torch.cuda.Stream(device=dev)
+            self._x_ev0 = torch.cuda.Event()
+            self._x_ev1 = torch.cuda.Event()
         self.direct_grad_slots = None
         self.direct_params = None
         self.direct_armed = False
@@ -484,6 +499,35 @@ class DecoderEngine:
         self._ptab_pending = None
         if not self.fused_refresh:
             self.refresh_weights()
+
+    def launch_x(self, stream=None):
+        """X = E W of the last training forward (the vocab head's backward GEMM
+        without the one-hot terms; see csrc/engine.cpp "X in the rollout") on
+        ``stream``, after the rollout: the GEMM then runs while the rewards
+        and the loss are computed, and the backward's reverse loop reads
+        alpha X + the one-hot rows instead of waiting for the GEMM.  No-op
+        unless a forward left one pending."""
+        ctx, self._x_pending = self._x_pending, None
+        if ctx is None or ctx.saved is None:
+            return
+        if stream is None:
+            import os
+            stream = self._ptab_stream if os.environ.get('CSTCAP_X_STREAM') == 'ptab' \
+                else self._x_stream
+        logits16 = ctx.saved[1]
+        n, R, ldl = logits16.shape
+        main = torch.cuda.current_stream(logits16.device)
+        # allocated on the main stream, which waits for the GEMM (backward)
+        # before anything else touches it or frees it, like the exp store
+        xw = torch.empty(n, R, self.H, dtype=torch.float32, device=logits16.device)
+        self._x_ev0.record(main)  # the rollout (enqueued before this call) is done
+        stream.wait_event(self._x_ev0)
+        with torch.cuda.stream(stream):
+            _ext.ops().vocab_x(logits16, self.wlog, xw)
+            from ..utils import stamps
+            stamps.mark('x_end')
+            self._x_ev1.record(stream)
+        ctx.xw_late = (xw, self._x_ev1)
 
     # -- gradient slots written by the fused backward -------------------------------
     def set_direct_slots(self, slots, params):

@@ -125,6 +125,9 @@ class Trainer:
         self.optimizer.grad_scale = self.bucket.grad_scale(self.ctx)
         if engine is not None:
             engine.attach_optimizer(self)
+            # SCST: the vocab head's X = E W runs behind the greedy decode on the
+            # side stream (rl_loss -> engine.launch_x)
+            engine.x_after_rollout = os.environ.get('CSTCAP_X_AFTER_ROLLOUT', '0') == '1'
         self.scorer = None
         # PyTorch decoder path at --precision bf16: torch autocast (bf16 GEMMs /
         # LSTM, fp32 softmax), the same-precision baseline of the fused engine
@@ -188,6 +191,7 @@ class Trainer:
                 # 8.7 ms per step: the queue priority throttles the rollout)
                 self._side_stream = torch.cuda.Stream(device=self.device)
                 self._ev_inputs = torch.cuda.Event()
+                self._ev_greedy = torch.cuda.Event()
             side = self._side_stream
             main = torch.cuda.current_stream(self.device)
             inputs_ready = self._ev_inputs
@@ -205,13 +209,20 @@ class Trainer:
                 stamps.base('fwd_greedy')
                 greedy_scores = self._greedy_scores(data, scorer, S, per_video=fused)
                 stamps.mark('greedy_end')
+                self._ev_greedy.record(side)
+        if self.engine is not None:
+            # the vocab head's X = E W on the engine's own stream once the
+            # rollout is done, under the reward / loss computation
+            # (engine.launch_x; on the greedy stream behind its decode, the
+            # backward's deferred join crashed hipStreamEndCapture)
+            self.engine.launch_x()
         stamps.base(None)
         self.timer.mark('rollout')
         if opt.use_cst == 0:
             sample_scores = scorer.score(model_res, vid_rows)
             stamps.mark('sample_scores')
             if side is not None:
-                main.wait_stream(side)
+                main.wait_event(self._ev_greedy)  # (not the X GEMM queued behind it)
                 greedy_scores.record_stream(main)
             else:
                 greedy_scores = self._greedy_scores(data, scorer, S, per_video=fused)
