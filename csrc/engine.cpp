@@ -662,10 +662,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor dWlog = early ? out_wlog : at::empty({V, H}, f32);
   at::Tensor dblog = early ? out_blog.view({V}) : at::empty({V}, f32);
   at::Tensor alpha, hs, cs_part;
+  // bias gradient inside the dW GEMM: hs rows carry alpha (bf16 hi + lo) as
+  // extra columns, padded to a multiple of 16 (CSTCAP_DB_IN_DW=0: the
+  // column-sum pass over E' instead)
+  bool db_in_dw = !ds_ready;
+  if (const char* e = getenv("CSTCAP_DB_IN_DW")) db_in_dw = db_in_dw && atoi(e) != 0;
+  const int64_t ldhs = db_in_dw ? H + 16 : H;
   if (!ds_ready) {
     alpha = at::empty({NR}, f32);
-    hs = at::empty({NR, H}, wx.options());
-    cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
+    hs = at::empty({NR, ldhs}, wx.options());
+    if (!db_in_dw) cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
   }
   auto launch_colsum = [&](hipStream_t s) {
     launch_vgrad_colsum(reinterpret_cast<const uint16_t*>(buf.data_ptr()), ldl, (int)V, NR,
@@ -698,18 +704,24 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   if (n_steps % dw_split != 0) dw_split = 1;
   auto dw_gemm = [&]() {  // (current stream: side)
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
+    const int64_t N = rhs.size(1);
+    at::Tensor out = N == H ? dWlog : at::empty({V, N}, f32);
     if (dw_split == 1) {
-      at::mm_out(dWlog, Ev.t(), rhs, at::kFloat);
-      return;
+      at::mm_out(out, Ev.t(), rhs, at::kFloat);
+    } else {
+      const int64_t kr = NR / dw_split;
+      at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
+      at::sum_out(out, at::bmm(a, rhs.view({dw_split, kr, N}), at::kFloat), 0);
     }
-    const int64_t kr = NR / dw_split;
-    at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
-    at::sum_out(dWlog, at::bmm(a, rhs.view({dw_split, kr, H}), at::kFloat), 0);
+    if (N != H) {  // the extra columns: sum_r alpha_r E'_r (hi + lo)
+      dWlog.copy_(out.narrow(1, 0, H));
+      at::add_out(dblog, out.select(1, H), out.select(1, H + 1));
+    }
   };
   auto db_sums = [&](hipStream_t s) {  // (current stream: s)
     if (ds_ready)
       dblog.copy_(ds_bias);
-    else
+    else if (!db_in_dw)
       launch_colsum(s);
   };
   auto dw_done = [&]() {
@@ -761,7 +773,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
                         reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
-                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
+                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream(), (int)ldhs);
     stamp(STAMP_BWD_DHD, side.stream());
     if (vh_sched == 2) {
       dw_gemm();

@@ -276,7 +276,9 @@ __global__ __launch_bounds__(ATT_THREADS) void att_bwd_kernel(
 int att_groups(int vdiv, int rpw) { return (vdiv + rpw - 1) / rpw; }
 
 // MFMA attention path, backward of one reverse step (see launchers.h): block
-// (video b, 128-unit slice of A).  dalpha[r][c] = the sum of the backward step
+// (video b, 64-unit slice of A; 4 row groups of the video's rows, so the
+// tanh-scorer loop of a thread covers 8 rows, not 16: 512 blocks at A = 512
+// spread it over every CU).  dalpha[r][c] = the sum of the backward step
 // kernel's H/64 partials (lstm.hip attention epilogue: the dG . Gv^T
 // contraction happened there, on the dG tile already in registers), so this
 // kernel never reads the 4H-wide dG rows or the gate tables.  Softmax backward
@@ -284,7 +286,7 @@ int att_groups(int vdiv, int rpw) { return (vdiv + rpw - 1) / rpw; }
 // its rows: dq_t[r][a] as bf16 into the dG row's tail (the next reverse step's
 // recurrent GEMM folds dq_t W_q into dh_{t-1}), dP[b][c][a] accumulated in
 // place (this block owns it), dw_a / db_a into per-video slots.
-constexpr int ATTB_UNITS = 128, ATTB_MAXR = 16;  // rows per parity (vdiv <= 32)
+constexpr int ATTB_UNITS = 64, ATTB_RG = 4, ATTB_MAXR = 8;  // rows per group (vdiv <= 32)
 template <int CP>
 __global__ __launch_bounds__(256) void att_bwd_mfma_kernel(
     const float* __restrict__ dal_part, int n_ut, int R, const float* __restrict__ alpha,
@@ -293,10 +295,10 @@ __global__ __launch_bounds__(256) void att_bwd_mfma_kernel(
     float* __restrict__ dP_acc, float* __restrict__ dwa_part, float* __restrict__ dba_part) {
   __shared__ float s_da[32 * CP];
   __shared__ float s_de[32 * CP];
-  __shared__ float s_red[ATTB_UNITS * (CP + 1)];
+  __shared__ float s_red[(ATTB_RG - 1) * ATTB_UNITS * (CP + 1)];
   const int b = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x;
   const int row0 = b * vdiv;
-  const int a = sl * ATTB_UNITS + (tid & (ATTB_UNITS - 1)), par = tid >> 7;
+  const int a = sl * ATTB_UNITS + (tid & (ATTB_UNITS - 1)), par = tid / ATTB_UNITS;
   // 1. dalpha[r][c] = sum of the step kernel's H/64 partials, one (r, c) per
   // thread: its loads go out first (they gate the softmax backward)
   const int nrc = vdiv * CP;
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(256) void att_bwd_mfma_kernel(
   const float* qb = q != nullptr ? q : P;  // step 0: q = 0 (masked below)
 #pragma unroll
   for (int k = 0; k < ATTB_MAXR; ++k) {
-    const int rr = min(par + 2 * k, vdiv - 1);
+    const int rr = min(par + ATTB_RG * k, vdiv - 1);
     qv[k] = qb[(int64_t)(q != nullptr ? row0 + rr : 0) * A + a];
   }
   if (q == nullptr) {
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(256) void att_bwd_mfma_kernel(
   for (int c = 0; c < CP; ++c) dp[c] = 0.f;
 #pragma unroll
   for (int k = 0; k < ATTB_MAXR; ++k) {
-    const int rr = par + 2 * k;
+    const int rr = par + ATTB_RG * k;
     if (rr < vdiv) {
       float dq = 0.f;
 #pragma unroll
@@ -383,17 +385,25 @@ __global__ __launch_bounds__(256) void att_bwd_mfma_kernel(
     }
   }
   const int ul = tid & (ATTB_UNITS - 1);
-  if (par == 1) {
+  if (par > 0) {
+    float* sr = s_red + ((par - 1) * ATTB_UNITS + ul) * (CP + 1);
 #pragma unroll
-    for (int c = 0; c < CP; ++c) s_red[ul * (CP + 1) + c] = dp[c];
-    s_red[ul * (CP + 1) + CP] = dw;
+    for (int c = 0; c < CP; ++c) sr[c] = dp[c];
+    sr[CP] = dw;
   }
   __syncthreads();
   if (par == 0) {
 #pragma unroll
+    for (int g = 0; g < ATTB_RG - 1; ++g) {
+      const float* sr = s_red + (g * ATTB_UNITS + ul) * (CP + 1);
+#pragma unroll
+      for (int c = 0; c < CP; ++c) dp[c] += sr[c];
+      dw += sr[CP];
+    }
+#pragma unroll
     for (int c = 0; c < CP; ++c)
-      if (c < C) dP_acc[((int64_t)b * C + c) * A + a] = dp_old[c] + dp[c] + s_red[ul * (CP + 1) + c];
-    dwa_part[(int64_t)b * A + a] = dw_old + dw + s_red[ul * (CP + 1) + CP];
+      if (c < C) dP_acc[((int64_t)b * C + c) * A + a] = dp_old[c] + dp[c];
+    dwa_part[(int64_t)b * A + a] = dw_old + dw;
   }
 }
 
@@ -401,7 +411,7 @@ void launch_att_bwd_mfma(const float* dal_part, int n_ut, int R, const float* al
                          const float* q, const float* P, const float* wa, int Bv, int vdiv, int C,
                          int CP, int A, int G4, uint16_t* dG, int ldg, int write_dq, float* dP_acc,
                          float* dwa_part, float* dba_part, hipStream_t stream) {
-  if (vdiv > 2 * ATTB_MAXR || A % ATTB_UNITS != 0 || C > CP || (CP != 8 && CP != 16) ||
+  if (vdiv > ATTB_RG * ATTB_MAXR || A % ATTB_UNITS != 0 || C > CP || (CP != 8 && CP != 16) ||
       Bv * vdiv != R || n_ut > 16)
     throw std::runtime_error("att_bwd_mfma: unsupported shape");
   const dim3 grid(Bv, A / ATTB_UNITS);

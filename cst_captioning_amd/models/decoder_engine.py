@@ -649,9 +649,16 @@ class DecoderEngine:
         frames = self._encode(model, feats)  # (B, C, F*H), FeatPool dropout in train mode
         ta = model.temporal_att
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
-        gv = self.pack_rows(F.linear(frames, w_iv), self.src_ie, 2)
-        pre = ta.precompute(frames)
-        return (gv, pre, ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), frames.size(0)
+        # the per-frame gate table (kept as bf16 by the kernels) and the
+        # projected frames as bf16 GEMMs with fp32 accumulation, like every
+        # other decoder GEMM (fp32 GEMMs: ~50 + 21 us forward and again in the
+        # backward at 8 frames)
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=frames.is_cuda):
+            gv = F.linear(frames, w_iv)
+            pre = ta.precompute(frames)
+        gv = self.pack_rows(gv.float(), self.src_ie, 2)
+        return (gv, pre.float(), ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), \
+            frames.size(0)
 
     def _run(self, model, feats, labels, modes, want_xe, use_counts, use_unfinished,
              expand=True, ss_prob=0.0, drop=True, temperature=1.0, bos_rows=None,

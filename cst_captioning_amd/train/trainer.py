@@ -127,7 +127,7 @@ class Trainer:
             engine.attach_optimizer(self)
             # SCST: the vocab head's X = E W runs behind the greedy decode on the
             # side stream (rl_loss -> engine.launch_x)
-            engine.x_after_rollout = os.environ.get('CSTCAP_X_AFTER_ROLLOUT', '0') == '1'
+            engine.x_after_rollout = os.environ.get('CSTCAP_X_AFTER_ROLLOUT', '1') != '0'
         self.scorer = None
         # PyTorch decoder path at --precision bf16: torch autocast (bf16 GEMMs /
         # LSTM, fp32 softmax), the same-precision baseline of the fused engine
@@ -199,17 +199,24 @@ class Trainer:
         # fused engine: reward, mask and REINFORCE loss in one launch
         # (ops/scst_loss.py), the greedy scores per video
         fused = self.engine is not None and opt.use_cst == 0 and self.device.type == 'cuda'
-        stamps.base('fwd_sample')
-        model_res, logprobs, _ = self._decode_rollout(data)
-        stamps.mark('rollout_enq')
-        if side is not None:
+
+        def enqueue_greedy():
             side.wait_event(inputs_ready)
             with torch.cuda.stream(side):
                 stamps.mark('greedy_begin')
                 stamps.base('fwd_greedy')
-                greedy_scores = self._greedy_scores(data, scorer, S, per_video=fused)
+                g = self._greedy_scores(data, scorer, S, per_video=fused)
                 stamps.mark('greedy_end')
                 self._ev_greedy.record(side)
+            return g
+        greedy_first = side is not None and os.environ.get('CSTCAP_GREEDY_FIRST', '1') != '0'
+        if greedy_first:
+            greedy_scores = enqueue_greedy()
+        stamps.base('fwd_sample')
+        model_res, logprobs, _ = self._decode_rollout(data)
+        stamps.mark('rollout_enq')
+        if side is not None and not greedy_first:
+            greedy_scores = enqueue_greedy()
         if self.engine is not None:
             # the vocab head's X = E W on the engine's own stream once the
             # rollout is done, under the reward / loss computation
