@@ -662,11 +662,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor dWlog = early ? out_wlog : at::empty({V, H}, f32);
   at::Tensor dblog = early ? out_blog.view({V}) : at::empty({V}, f32);
   at::Tensor alpha, hs, cs_part;
-  // bias gradient inside the dW GEMM: hs rows carry alpha (bf16 hi + lo) as
-  // extra columns, padded to a multiple of 16 (CSTCAP_DB_IN_DW=0: the
-  // column-sum pass over E' instead)
-  bool db_in_dw = !ds_ready;
-  if (const char* e = getenv("CSTCAP_DB_IN_DW")) db_in_dw = db_in_dw && atoi(e) != 0;
+  // CSTCAP_DB_IN_DW=1: the bias gradient inside the dW GEMM (hs rows carry
+  // alpha as bf16 hi + lo extra columns, padded to a multiple of 16) instead
+  // of the column-sum pass over E' (which runs under the reverse loop).  Off:
+  // the N = 528 GEMM took ~100 us longer than the N = 512 one (A/B 3.63-3.65
+  // vs 3.52-3.65 ms, profiles/r3/ab_dbdw.txt)
+  bool db_in_dw = false;
+  if (const char* e = getenv("CSTCAP_DB_IN_DW")) db_in_dw = !ds_ready && atoi(e) != 0;
   const int64_t ldhs = db_in_dw ? H + 16 : H;
   if (!ds_ready) {
     alpha = at::empty({NR}, f32);

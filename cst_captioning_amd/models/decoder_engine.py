@@ -318,7 +318,36 @@ class _DecoderFn(torch.autograd.Function):
             (None,) * 16 + tuple(d_up)
 
 
+_AUX = {}
+
+
+def _device_aux(dev):
+    """Per-device side streams and events of the engine (token-table prefetch,
+    X = E W after the rollout), created once."""
+    import types
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _AUX:
+        _AUX[key] = types.SimpleNamespace(
+            ptab_stream=torch.cuda.Stream(device=dev), ptab_ev0=torch.cuda.Event(),
+            ptab_ev1=torch.cuda.Event(), x_stream=torch.cuda.Stream(device=dev),
+            x_ev0=torch.cuda.Event(), x_ev1=torch.cuda.Event(), x_pending={})
+    return key
+
+
 class DecoderEngine:
+    @property
+    def _aux(self):
+        return _AUX[self._aux_key] if self._aux_key is not None else None
+
+    @property
+    def _x_pending(self):
+        return self._aux.x_pending.get(id(self)) if self._aux is not None else None
+
+    @_x_pending.setter
+    def _x_pending(self, ctx):
+        if self._aux is not None:
+            self._aux.x_pending[id(self)] = ctx
+
     def __init__(self, model, opt):
         why = engine_unsupported_reason(opt)
         if why is not None:
@@ -368,23 +397,16 @@ class DecoderEngine:
         # recomputes a stale table first (ensure_ptab)
         self.weights_version = 0
         self._ptab_version = -1
-        self._ptab_pending = None  # event of this step's prefetch
-        self._ptab_stream = None
-        if dev.type == 'cuda':  # (created here: never during a graph capture)
-            self._ptab_stream = torch.cuda.Stream(device=dev)
-            self._ptab_ev0 = torch.cuda.Event()
-            self._ptab_ev1 = torch.cuda.Event()
+        self._ptab_pending = False  # this step's prefetch is in flight (aux.ptab_ev1)
+        # side streams / events (created here, never during a graph capture;
+        # kept outside the instance so a deepcopy of the model stays possible)
+        self._aux_key = _device_aux(dev) if dev.type == 'cuda' else None
         # running count of exp-store rows the backward recomputed because the
         # row's LSE jumped by > 60 between steps (csrc/kernels/vocab_grad.hip)
         self.exp_fix_rows = torch.zeros(1, dtype=torch.int32, device=dev)
         # X = E W after the rollout (launch_x): the trainer enables it and calls
         # launch_x on its greedy side stream once the greedy decode is enqueued
         self.x_after_rollout = False
-        self._x_pending = None
-        if dev.type == 'cuda':
-            self._x_stream = torch.cuda.Stream(device=dev)
-            self._x_ev0 = torch.cuda.Event()
-            self._x_ev1 = torch.cuda.Event()
         self.direct_grad_slots = None
         self.direct_params = None
         self.direct_armed = False
@@ -464,23 +486,23 @@ class DecoderEngine:
         stream, concurrently with the step's batch gather / FeatPool prologue
         (the decode waits for it in ensure_ptab).  Graph-capturable: the fork
         and the join are both inside the captured step."""
-        if self._ptab_version == self.weights_version or self._ptab_stream is None:
+        if self._ptab_version == self.weights_version or self._aux is None:
             return
         main = torch.cuda.current_stream(self.ptab.device)
-        self._ptab_ev0.record(main)
-        self._ptab_stream.wait_event(self._ptab_ev0)
-        with torch.cuda.stream(self._ptab_stream):
+        self._aux.ptab_ev0.record(main)
+        self._aux.ptab_stream.wait_event(self._aux.ptab_ev0)
+        with torch.cuda.stream(self._aux.ptab_stream):
             self.update_ptab()
-            self._ptab_ev1.record(self._ptab_stream)
-        self._ptab_pending = self._ptab_ev1
+            self._aux.ptab_ev1.record(self._aux.ptab_stream)
+        self._ptab_pending = True
 
     def ensure_ptab(self):
         """Before a decode reads the table: join this step's prefetch, or
         recompute a stale table on the current stream."""
         if self._ptab_version != self.weights_version:
             self.update_ptab()
-        elif self._ptab_pending is not None:
-            torch.cuda.current_stream(self.ptab.device).wait_event(self._ptab_pending)
+        elif self._ptab_pending:
+            torch.cuda.current_stream(self.ptab.device).wait_event(self._aux.ptab_ev1)
 
     def current_ptab(self):
         self.ensure_ptab()
@@ -496,7 +518,7 @@ class DecoderEngine:
 
     def after_step(self):
         self.weights_version += 1
-        self._ptab_pending = None
+        self._ptab_pending = False
         if not self.fused_refresh:
             self.refresh_weights()
 
@@ -512,22 +534,22 @@ class DecoderEngine:
             return
         if stream is None:
             import os
-            stream = self._ptab_stream if os.environ.get('CSTCAP_X_STREAM') == 'ptab' \
-                else self._x_stream
+            stream = self._aux.ptab_stream if os.environ.get('CSTCAP_X_STREAM') == 'ptab' \
+                else self._aux.x_stream
         logits16 = ctx.saved[1]
         n, R, ldl = logits16.shape
         main = torch.cuda.current_stream(logits16.device)
         # allocated on the main stream, which waits for the GEMM (backward)
         # before anything else touches it or frees it, like the exp store
         xw = torch.empty(n, R, self.H, dtype=torch.float32, device=logits16.device)
-        self._x_ev0.record(main)  # the rollout (enqueued before this call) is done
-        stream.wait_event(self._x_ev0)
+        self._aux.x_ev0.record(main)  # the rollout (enqueued before this call) is done
+        stream.wait_event(self._aux.x_ev0)
         with torch.cuda.stream(stream):
             _ext.ops().vocab_x(logits16, self.wlog, xw)
             from ..utils import stamps
             stamps.mark('x_end')
-            self._x_ev1.record(stream)
-        ctx.xw_late = (xw, self._x_ev1)
+            self._aux.x_ev1.record(stream)
+        ctx.xw_late = (xw, self._aux.x_ev1)
 
     # -- gradient slots written by the fused backward -------------------------------
     def set_direct_slots(self, slots, params):
@@ -649,16 +671,12 @@ class DecoderEngine:
         frames = self._encode(model, feats)  # (B, C, F*H), FeatPool dropout in train mode
         ta = model.temporal_att
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
-        # the per-frame gate table (kept as bf16 by the kernels) and the
-        # projected frames as bf16 GEMMs with fp32 accumulation, like every
-        # other decoder GEMM (fp32 GEMMs: ~50 + 21 us forward and again in the
-        # backward at 8 frames)
-        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=frames.is_cuda):
-            gv = F.linear(frames, w_iv)
-            pre = ta.precompute(frames)
-        gv = self.pack_rows(gv.float(), self.src_ie, 2)
-        return (gv, pre.float(), ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), \
-            frames.size(0)
+        # (fp32 GEMMs: under bf16 autocast the projected frames' bias gradient
+        # drifted to 8.8 % of the fp32 reference at H = 64,
+        # tests/test_gpu_attention.py)
+        gv = self.pack_rows(F.linear(frames, w_iv), self.src_ie, 2)
+        pre = ta.precompute(frames)
+        return (gv, pre, ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), frames.size(0)
 
     def _run(self, model, feats, labels, modes, want_xe, use_counts, use_unfinished,
              expand=True, ss_prob=0.0, drop=True, temperature=1.0, bos_rows=None,
