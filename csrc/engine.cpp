@@ -52,6 +52,30 @@ void stamp_buffer(at::Tensor buf) {
   set_stamp_buffer(buf.data_ptr<int64_t>(), (int)buf.numel());
 }
 void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
+
+// Step hook of the next training decode (one-shot): decoder_forward calls the
+// Python callable once it has enqueued step `g_hook_step`, so the caller can
+// enqueue other work (the SCST greedy decode on its stream) at that point.
+// In a replayed HIP graph the runtime submits nodes in capture order, ~2.7 us
+// each: the greedy branch enqueued before the rollout delayed the rollout's
+// first launch by its ~100 nodes, enqueued after it, the greedy branch waited
+// for the rollout's; enqueued a few steps into the rollout, both start early.
+static int64_t g_hook_step = -1;
+static py::object* g_hook = nullptr;  // never destroyed (no Py_DECREF after finalize)
+void set_step_hook(int64_t step, py::object fn) {
+  if (g_hook == nullptr) g_hook = new py::object();
+  g_hook_step = fn.is_none() ? -1 : step;
+  *g_hook = fn;
+}
+static void run_step_hook(int64_t t) {
+  if (g_hook_step < 0 || t != g_hook_step || g_hook == nullptr) return;
+  py::object fn = *g_hook;
+  g_hook_step = -1;  // one-shot, and not inside the decodes the hook enqueues
+  *g_hook = py::none();
+  const int base = g_stamp_base;
+  fn();
+  g_stamp_base = base;
+}
 // X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
 // fp32, on the current stream (engine.launch_x; the same GEMM as the
 // backward's dHd chunks)
@@ -474,6 +498,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     if (next)
       for (int64_t l = 1; l < NL; ++l) upper_step(l, t + 1);
     if (t == 0) stamp(STAMP_FWD_STEP0, st);
+    if (save) run_step_hook(t);
   }
   if (fwd_x) {  // join the X chunks (the last one covers a single step)
     (void)hipEventRecord(faux.ev[5], faux.side[0].stream());
@@ -959,8 +984,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // interleaved on one box, profiles/r2/ab_whh_side_splitk.txt).  (Outputs
   // written there were allocated on the main stream, which joins the side
   // stream before returning.)
-  if (vh_sched == 0 || vh_sched == 3) {
-    (void)hipEventRecord(ev_ready, st);  // reverse loop done
+  // (CSTCAP_TOKSUM_FIRST=1: the side stream's GEMMs start only after the
+  // main stream's per-token sums, which then run without the dW GEMM beside
+  // them)
+  const bool toksum_first = getenv("CSTCAP_TOKSUM_FIRST") && atoi(getenv("CSTCAP_TOKSUM_FIRST"));
+  auto post_loop_side = [&]() {
+    (void)hipEventRecord(ev_ready, st);  // reverse loop (+ token sums) done
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
     dw_gemm();
@@ -969,7 +998,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     whh_grad();
     stamp(STAMP_BWD_SIDE, side.stream());
     dw_done();
-  }
+  };
+  if ((vh_sched == 0 || vh_sched == 3) && !toksum_first) post_loop_side();
 
   // 5. input-token gradients through the per-token sums S[v] = sum of the dG
   //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
@@ -980,6 +1010,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
+  if ((vh_sched == 0 || vh_sched == 3) && toksum_first) post_loop_side();
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134

@@ -209,14 +209,27 @@ class Trainer:
                 stamps.mark('greedy_end')
                 self._ev_greedy.record(side)
             return g
-        greedy_first = side is not None and os.environ.get('CSTCAP_GREEDY_FIRST', '1') != '0'
-        if greedy_first:
-            greedy_scores = enqueue_greedy()
+        # where the greedy branch goes in the captured step's node order (the
+        # graph runtime submits nodes in capture order, ~2.7 us each):
+        # CSTCAP_GREEDY_AT = k > 0: from the rollout's step-k hook (both
+        # decodes start early), 0: before the rollout, -1: after it
+        greedy_at = int(os.environ.get('CSTCAP_GREEDY_AT', '6')) if side is not None else -1
+        holder = []
+        if side is not None and greedy_at == 0:
+            holder.append(enqueue_greedy())
+        hook = side is not None and greedy_at > 0 and self.engine is not None
+        if hook:
+            from .. import _ext
+            _ext.ops().set_step_hook(greedy_at, lambda: holder.append(enqueue_greedy()))
         stamps.base('fwd_sample')
-        model_res, logprobs, _ = self._decode_rollout(data)
+        try:
+            model_res, logprobs, _ = self._decode_rollout(data)
+        finally:
+            if hook:
+                _ext.ops().set_step_hook(-1, None)
         stamps.mark('rollout_enq')
-        if side is not None and not greedy_first:
-            greedy_scores = enqueue_greedy()
+        if side is not None:
+            greedy_scores = holder[0] if holder else enqueue_greedy()
         if self.engine is not None:
             # the vocab head's X = E W on the engine's own stream once the
             # rollout is done, under the reward / loss computation
