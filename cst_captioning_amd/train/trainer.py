@@ -194,6 +194,12 @@ class Trainer:
                 self._ev_greedy = torch.cuda.Event()
             side = self._side_stream
             main = torch.cuda.current_stream(self.device)
+            # the batch's device part (a LazyGather inside a captured step) is
+            # gathered HERE, on the main stream, before the event both decodes
+            # order behind: gathered lazily by whichever decode touched it
+            # first, the other stream would read it unordered
+            data['feats']
+            data['labels']
             inputs_ready = self._ev_inputs
             inputs_ready.record(main)
         # fused engine: reward, mask and REINFORCE loss in one launch
@@ -201,6 +207,7 @@ class Trainer:
         fused = self.engine is not None and opt.use_cst == 0 and self.device.type == 'cuda'
 
         def enqueue_greedy():
+            inputs_ready.record(main)  # (everything main enqueued so far)
             side.wait_event(inputs_ready)
             with torch.cuda.stream(side):
                 stamps.mark('greedy_begin')
@@ -213,7 +220,7 @@ class Trainer:
         # graph runtime submits nodes in capture order, ~2.7 us each):
         # CSTCAP_GREEDY_AT = k > 0: from the rollout's step-k hook (both
         # decodes start early), 0: before the rollout, -1: after it
-        greedy_at = int(os.environ.get('CSTCAP_GREEDY_AT', '6')) if side is not None else -1
+        greedy_at = int(os.environ.get('CSTCAP_GREEDY_AT', '0')) if side is not None else -1
         holder = []
         if side is not None and greedy_at == 0:
             holder.append(enqueue_greedy())
