@@ -237,7 +237,8 @@ class Trainer:
         stamps.mark('rollout_enq')
         if side is not None:
             greedy_scores = holder[0] if holder else enqueue_greedy()
-        if self.engine is not None:
+        x_at_loss = os.environ.get('CSTCAP_X_AT', 'rollout') == 'loss'
+        if self.engine is not None and not x_at_loss:
             # the vocab head's X = E W on the engine's own stream once the
             # rollout is done, under the reward / loss computation
             # (engine.launch_x; on the greedy stream behind its decode, the
@@ -258,6 +259,8 @@ class Trainer:
                 loss, reward, m_score, b_score = scst_loss(model_res, logprobs, sample_scores,
                                                            greedy_scores)
                 stamps.mark('loss')
+                if self.engine is not None and x_at_loss:  # (A/B: X after the loss)
+                    self.engine.launch_x()
                 self.timer.mark('reward')
                 return loss, {'reward': reward, 'm': m_score, 'b': b_score, 'seq': model_res}
             reward, m_score, b_score = scst_from_scores(sample_scores.float(),
