@@ -88,6 +88,16 @@ void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
                   logits16.size(2) >= V,
               "vocab_x: out must be a contiguous fp32 (n, R, H) tensor");
   at::Tensor dst = out.view({NR, H});
+  // CSTCAP_X_SPLITK=s > 1 (dividing V): a split-K batch over column blocks of
+  // E, partial products summed (more workgroups in flight for N = H = 512)
+  int64_t s = 1;
+  if (const char* e = getenv("CSTCAP_X_SPLITK")) s = std::max<int64_t>(1, atoll(e));
+  if (s > 1 && V % s == 0) {
+    const int64_t kc = V / s, ldl = logits16.size(2);
+    at::Tensor a = logits16.view({NR, ldl}).as_strided({s, NR, kc}, {kc, ldl, 1});
+    at::sum_out(dst, at::bmm(a, wlog.view({s, kc, H}), at::kFloat), 0);
+    return;
+  }
   at::mm_out(dst, logits16.view({NR, logits16.size(2)}).narrow(1, 0, V), wlog, at::kFloat);
 }
 int64_t wall_clock_khz() {
