@@ -76,7 +76,6 @@ void stamp_buffer(at::Tensor buf);
 void stamp_now(int64_t slot);
 int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
-void set_step_hook(int64_t step, py::object fn);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -157,5 +156,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stamp_now", &cst::stamp_now);
   m.def("wall_clock_khz", &cst::wall_clock_khz);
   m.def("vocab_x", &cst::vocab_x);
-  m.def("set_step_hook", &cst::set_step_hook);
 }

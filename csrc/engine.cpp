@@ -53,29 +53,6 @@ void stamp_buffer(at::Tensor buf) {
 }
 void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
 
-// Step hook of the next training decode (one-shot): decoder_forward calls the
-// Python callable once it has enqueued step `g_hook_step`, so the caller can
-// enqueue other work (the SCST greedy decode on its stream) at that point.
-// In a replayed HIP graph the runtime submits nodes in capture order, ~2.7 us
-// each: the greedy branch enqueued before the rollout delayed the rollout's
-// first launch by its ~100 nodes, enqueued after it, the greedy branch waited
-// for the rollout's; enqueued a few steps into the rollout, both start early.
-static int64_t g_hook_step = -1;
-static py::object* g_hook = nullptr;  // never destroyed (no Py_DECREF after finalize)
-void set_step_hook(int64_t step, py::object fn) {
-  if (g_hook == nullptr) g_hook = new py::object();
-  g_hook_step = fn.is_none() ? -1 : step;
-  *g_hook = fn;
-}
-static void run_step_hook(int64_t t) {
-  if (g_hook_step < 0 || t != g_hook_step || g_hook == nullptr) return;
-  py::object fn = *g_hook;
-  g_hook_step = -1;  // one-shot, and not inside the decodes the hook enqueues
-  *g_hook = py::none();
-  const int base = g_stamp_base;
-  fn();
-  g_stamp_base = base;
-}
 // X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
 // fp32, on the current stream (engine.launch_x; the same GEMM as the
 // backward's dHd chunks)
@@ -88,16 +65,8 @@ void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
                   logits16.size(2) >= V,
               "vocab_x: out must be a contiguous fp32 (n, R, H) tensor");
   at::Tensor dst = out.view({NR, H});
-  // CSTCAP_X_SPLITK=s > 1 (dividing V): a split-K batch over column blocks of
-  // E, partial products summed (more workgroups in flight for N = H = 512)
-  int64_t s = 1;
-  if (const char* e = getenv("CSTCAP_X_SPLITK")) s = std::max<int64_t>(1, atoll(e));
-  if (s > 1 && V % s == 0) {
-    const int64_t kc = V / s, ldl = logits16.size(2);
-    at::Tensor a = logits16.view({NR, ldl}).as_strided({s, NR, kc}, {kc, ldl, 1});
-    at::sum_out(dst, at::bmm(a, wlog.view({s, kc, H}), at::kFloat), 0);
-    return;
-  }
+  // (a 3-way split-K batch measured slower: 3.74 vs 3.67-3.73 ms per step,
+  // profiles/r3/ab_xsplitk.txt)
   at::mm_out(dst, logits16.view({NR, logits16.size(2)}).narrow(1, 0, V), wlog, at::kFloat);
 }
 int64_t wall_clock_khz() {
@@ -347,38 +316,6 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
   at::Tensor xin = NL > 1 ? at::empty({R, H4}, f32) : at::Tensor();
 
-  // X in the rollout: the vocab head's backward GEMM X = E W (dHd = alpha X +
-  // one-hot rows, kernels/vocab_grad.hip) reads only the exp store and the
-  // logit weights, so it runs here, chunk by chunk on a side stream, in the
-  // CUs the latency-bound decode chain leaves idle, instead of in front of
-  // the reverse loop.  Chunks of CSTCAP_FWD_X steps (0 = off) and a last
-  // one-step chunk, so the join at the end of the forward waits for one
-  // 1,280-row GEMM at most.  Measured (device stamps, gpurun_out ->
-  // profiles/r3/ab_fwdx.txt): the reverse loop alone drops from 830 to 524 us,
-  // but the GEMM's long-K workgroups hold CUs the 28 decode launches need
-  // (rollout 1.50 -> 2.22 ms) and the greedy branch starts late: 4.57 ms per
-  // step at 4-step chunks, 4.04 at 7, vs 3.82-3.92 off.  Kept as an option,
-  // default off.
-  int64_t x_chunk = 0;  // off: see the comment above
-  if (const char* e = getenv("CSTCAP_FWD_X")) x_chunk = atoll(e);
-  const bool fwd_x = save && store_exp && x_chunk > 0;
-  at::Tensor xw = fwd_x ? at::empty({n_steps, R, H}, f32) : at::empty({0}, f32);
-  DeviceAux& faux = device_aux((int)dev.index());
-  int64_t x_next = 0;  // first step not yet in a chunk
-  auto x_chunk_after = [&](int64_t t) {  // step t's exp rows are enqueued on st
-    if (!fwd_x) return;
-    const bool end = (t + 1) % x_chunk == 0 || t + 1 >= n_steps - 1;
-    if (!end) return;
-    (void)hipEventRecord(faux.ev[4], st);
-    (void)hipStreamWaitEvent(faux.side[0].stream(), faux.ev[4], 0);
-    c10::hip::HIPStreamGuard guard(faux.side[0]);
-    const int64_t r0 = x_next * R, nr = (t + 1 - x_next) * R;
-    at::Tensor dst = xw.view({n_steps * R, H}).narrow(0, r0, nr);
-    at::mm_out(dst, logits16.view({n_steps * R, ldl}).narrow(0, r0, nr).narrow(1, 0, V), wlog,
-               at::kFloat);
-    x_next = t + 1;
-  };
-
   // layer l >= 1 at step t (its zero initial state is h0 / c0's zeros)
   auto upper_step = [&](int64_t l, int64_t t) {
     const at::Tensor& wu = up[2 * (l - 1)];
@@ -504,15 +441,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     if (save && store_exp && t == 0)
       launch_vocab_exp_convert(reinterpret_cast<uint16_t*>(logits16[0].data_ptr()), ldl, (int)V,
                                (int)R, lse[0].data_ptr<float>(), st);
-    x_chunk_after(t);
     if (next)
       for (int64_t l = 1; l < NL; ++l) upper_step(l, t + 1);
     if (t == 0) stamp(STAMP_FWD_STEP0, st);
-    if (save) run_step_hook(t);
-  }
-  if (fwd_x) {  // join the X chunks (the last one covers a single step)
-    (void)hipEventRecord(faux.ev[5], faux.side[0].stream());
-    (void)hipStreamWaitEvent(st, faux.ev[5], 0);
   }
   stamp(STAMP_FWD_END, st);
   // saved: {logits16, hd of the top layer (vocab input), layer 0's gates, c, h}
@@ -535,7 +466,6 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
       out.push_back(HDs[l - 1]);
     }
   }
-  out.push_back(xw);  // last: X = E W from the rollout (empty unless computed)
   return out;
 }
 
@@ -632,8 +562,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // (smallest) chunk instead of after the whole 35,840-row GEMM, and the rest
   // of the GEMM runs under the loop
   std::vector<std::array<int64_t, 2>> dhd_chunks;  // [t0, t1)
-  // X = E W computed during the rollout (decoder_forward "X in the rollout"):
-  // no GEMM here, the loop waits only for the row weights
+  // X = E W computed right after the rollout (engine.launch_x, vocab_x): no
+  // GEMM here, the loop waits only for the row weights
   const bool have_x = xw.defined() && xw.numel() > 0;
   if (have_x)
     TORCH_CHECK(xw.is_cuda() && xw.scalar_type() == at::kFloat && xw.is_contiguous() &&
@@ -643,13 +573,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dhd_chunks.push_back({0, n_steps});
   } else {
     int64_t t1 = n_steps;
-    // (A/B runs: CSTCAP_DHD_CHUNKS="first,rest" steps per chunk)
-    int64_t k_first = 2, k_rest = 4;
-    if (const char* env = getenv("CSTCAP_DHD_CHUNKS")) {
-      k_first = std::max<int64_t>(1, atoll(env));
-      const char* comma = strchr(env, ',');
-      k_rest = comma ? std::max<int64_t>(1, atoll(comma + 1)) : k_first;
-    }
+    const int64_t k_first = 2, k_rest = 4;  // steps per chunk
     while (t1 > 0) {
       const int64_t k = dhd_chunks.empty() ? k_first : k_rest;
       const int64_t t0 = std::max<int64_t>(0, t1 - k);
@@ -697,18 +621,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   at::Tensor dWlog = early ? out_wlog : at::empty({V, H}, f32);
   at::Tensor dblog = early ? out_blog.view({V}) : at::empty({V}, f32);
   at::Tensor alpha, hs, cs_part;
-  // CSTCAP_DB_IN_DW=1: the bias gradient inside the dW GEMM (hs rows carry
-  // alpha as bf16 hi + lo extra columns, padded to a multiple of 16) instead
-  // of the column-sum pass over E' (which runs under the reverse loop).  Off:
-  // the N = 528 GEMM took ~100 us longer than the N = 512 one (A/B 3.63-3.65
-  // vs 3.52-3.65 ms, profiles/r3/ab_dbdw.txt)
-  bool db_in_dw = false;
-  if (const char* e = getenv("CSTCAP_DB_IN_DW")) db_in_dw = !ds_ready && atoi(e) != 0;
-  const int64_t ldhs = db_in_dw ? H + 16 : H;
+  // (the bias gradient as two extra bf16 columns (alpha hi / lo) of the dW
+  // GEMM instead of the column sums measured slower: the N = 528 GEMM took
+  // ~100 us longer, profiles/r3/ab_dbdw.txt)
   if (!ds_ready) {
     alpha = at::empty({NR}, f32);
-    hs = at::empty({NR, ldhs}, wx.options());
-    if (!db_in_dw) cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
+    hs = at::empty({NR, H}, wx.options());
+    cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
   }
   auto launch_colsum = [&](hipStream_t s) {
     launch_vgrad_colsum(reinterpret_cast<const uint16_t*>(buf.data_ptr()), ldl, (int)V, NR,
@@ -727,8 +646,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // reverse loop, dW_logit after it (vh_sched 3; interleaved A/B 3.745-3.792
   // vs 3.774-3.831 ms per step with the loop-after schedule 0,
   // profiles/r3/ab_sched.txt)
-  int vh_sched = early_comm ? 2 : 3;
-  if (const char* e = getenv("CSTCAP_VH_SCHED")) vh_sched = atoi(e);  // A/B experiments
+  const int vh_sched = early_comm ? 2 : 3;
   // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
   // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
   // split-K batch over groups of decode steps multiplies the tiles in flight,
@@ -736,29 +654,21 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // step count)
   // (4 groups: 3.745-3.774 vs 3.792-3.831 ms per step for one GEMM, 7 groups
   // 3.862-3.873, profiles/r3/ab_sched.txt)
-  int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
-  if (const char* e = getenv("CSTCAP_DW_SPLITK")) dw_split = std::max<int64_t>(1, atoll(e));
-  if (n_steps % dw_split != 0) dw_split = 1;
+  const int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
   auto dw_gemm = [&]() {  // (current stream: side)
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
-    const int64_t N = rhs.size(1);
-    at::Tensor out = N == H ? dWlog : at::empty({V, N}, f32);
     if (dw_split == 1) {
-      at::mm_out(out, Ev.t(), rhs, at::kFloat);
-    } else {
-      const int64_t kr = NR / dw_split;
-      at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
-      at::sum_out(out, at::bmm(a, rhs.view({dw_split, kr, N}), at::kFloat), 0);
+      at::mm_out(dWlog, Ev.t(), rhs, at::kFloat);
+      return;
     }
-    if (N != H) {  // the extra columns: sum_r alpha_r E'_r (hi + lo)
-      dWlog.copy_(out.narrow(1, 0, H));
-      at::add_out(dblog, out.select(1, H), out.select(1, H + 1));
-    }
+    const int64_t kr = NR / dw_split;
+    at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
+    at::sum_out(dWlog, at::bmm(a, rhs.view({dw_split, kr, H}), at::kFloat), 0);
   };
   auto db_sums = [&](hipStream_t s) {  // (current stream: s)
     if (ds_ready)
       dblog.copy_(ds_bias);
-    else if (!db_in_dw)
+    else
       launch_colsum(s);
   };
   auto dw_done = [&]() {
@@ -810,7 +720,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
                         reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
-                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream(), (int)ldhs);
+                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
     stamp(STAMP_BWD_DHD, side.stream());
     if (vh_sched == 2) {
       dw_gemm();
@@ -994,12 +904,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // interleaved on one box, profiles/r2/ab_whh_side_splitk.txt).  (Outputs
   // written there were allocated on the main stream, which joins the side
   // stream before returning.)
-  // (CSTCAP_TOKSUM_FIRST=1: the side stream's GEMMs start only after the
-  // main stream's per-token sums, which then run without the dW GEMM beside
-  // them)
-  const bool toksum_first = getenv("CSTCAP_TOKSUM_FIRST") && atoi(getenv("CSTCAP_TOKSUM_FIRST"));
-  auto post_loop_side = [&]() {
-    (void)hipEventRecord(ev_ready, st);  // reverse loop (+ token sums) done
+  // (starting them only after the main stream's per-token sums measured
+  // slower: 3.76-3.81 vs 3.71-3.72 ms, profiles/r3/ab_toksum_first.txt)
+  if (vh_sched == 0 || vh_sched == 3) {
+    (void)hipEventRecord(ev_ready, st);  // reverse loop done
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
     c10::hip::HIPStreamGuard guard(side);
     dw_gemm();
@@ -1008,8 +916,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     whh_grad();
     stamp(STAMP_BWD_SIDE, side.stream());
     dw_done();
-  };
-  if ((vh_sched == 0 || vh_sched == 3) && !toksum_first) post_loop_side();
+  }
 
   // 5. input-token gradients through the per-token sums S[v] = sum of the dG
   //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
@@ -1020,7 +927,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
-  if ((vh_sched == 0 || vh_sched == 3) && toksum_first) post_loop_side();
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134

@@ -376,20 +376,13 @@ __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int bid = blockIdx.x;
   if constexpr (AV != 0) {
-    if (n_att > 0) {  // attention workgroups dispatched first
-      if (bid < n_att) {
-        if (bid < att_mfma_blocks(att.Bv, att.A)) att_mfma_fwd_block<AV>(bid, att, lds);
-        return;
-      }
-      bid -= n_att;
-    } else if (n_att < 0) {  // ... or last (n_att = -count): into the vocab tiles' drain
-      const int first = (int)gridDim.x + n_att;
-      if (bid >= first) {
-        if (bid - first < att_mfma_blocks(att.Bv, att.A))
-          att_mfma_fwd_block<AV>(bid - first, att, lds);
-        return;
-      }
+    // (dispatched after the vocabulary tiles instead, into their drain:
+    // att8 5.48-5.51 vs 5.19-5.22 ms per step, profiles/r3/ab_att_last.txt)
+    if (bid < n_att) {
+      if (bid < att_mfma_blocks(att.Bv, att.A)) att_mfma_fwd_block<AV>(bid, att, lds);
+      return;
     }
+    bid -= n_att;
   }
   if (bid < n_lstm_pad) {
     if (bid < lstm_gemm_blocks(R, H, NQ))
@@ -843,13 +836,10 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  // CSTCAP_ATT_LAST=1: the attention workgroups after the vocabulary tiles
-  static const bool att_last = getenv("CSTCAP_ATT_LAST") && atoi(getenv("CSTCAP_ATT_LAST")) != 0;
   hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV>),
                      dim3(n_att + n_l + n_vt * n_rt), dim3(256), LDS, stream, hd, ldh, R, H, W,
                      bias, V, logits16, ldl, (VocabPartial*)part, tgt, tgt_stride, flags, inv_temp,
-                     rng, step, eoff, h_t, whh, vgate, vdiv, pre, n_l, NQ, q_out, a,
-                     att_last ? -n_att : n_att);
+                     rng, step, eoff, h_t, whh, vgate, vdiv, pre, n_l, NQ, q_out, a, n_att);
   post_launch("vocab_lstm_fwd_kernel", stream);
 }
 

@@ -181,20 +181,13 @@ constexpr int VG_THREADS = 256, VG_ROWS = VG_THREADS / WAVE;
 // Hd) (and dHd = alpha X in place when dhd is given; the engine instead lets
 // the reverse loop scale the rows it reads, so this pass leaves the critical
 // path).
-// ldhs > H: the row also carries alpha itself as two bf16 columns (hi, lo =
-// alpha - hi) and zeros up to ldhs, so dW = E'^T hs yields the bias gradient
-// sum_r alpha_r E'_r as two extra output columns (no column-sum pass over E').
 __global__ __launch_bounds__(VG_THREADS) void vgrad_rows_kernel(
     const float* __restrict__ alpha, int64_t NR, int H, const uint16_t* __restrict__ hd,
-    float* __restrict__ dhd, uint16_t* __restrict__ hs, int ldhs) {
+    float* __restrict__ dhd, uint16_t* __restrict__ hs) {
   const int64_t row = (int64_t)blockIdx.x * VG_ROWS + (threadIdx.x >> 6);
   if (row >= NR) return;
   const int lane = threadIdx.x & 63;
   const float al = alpha[row];
-  if (ldhs > H && lane < ldhs - H) {
-    const uint16_t hi = f2bf(al);
-    hs[row * ldhs + H + lane] = lane == 0 ? hi : lane == 1 ? f2bf(al - bf2f(hi)) : (uint16_t)0;
-  }
   for (int c = lane; 8 * c < H; c += WAVE) {
     if (dhd != nullptr) {
       float4* xp = reinterpret_cast<float4*>(dhd + row * H + 8 * c);
@@ -211,17 +204,15 @@ __global__ __launch_bounds__(VG_THREADS) void vgrad_rows_kernel(
     for (int k = 0; k < 4; ++k)
       ho[k] = (uint32_t)f2bf(al * bf2f(hw[k] & 0xffff)) |
               ((uint32_t)f2bf(al * bf2f(hw[k] >> 16)) << 16);
-    *reinterpret_cast<uint4*>(hs + row * ldhs + 8 * c) = make_uint4(ho[0], ho[1], ho[2], ho[3]);
+    *reinterpret_cast<uint4*>(hs + row * H + 8 * c) = make_uint4(ho[0], ho[1], ho[2], ho[3]);
   }
 }
 
 void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd, float* dhd,
-                       uint16_t* hs, hipStream_t stream, int ldhs) {
-  if (ldhs <= 0) ldhs = H;
-  if (H % 8 != 0 || ldhs % 8 != 0 || ldhs < H || ldhs - H > 64)
-    throw std::runtime_error("vgrad_rows: H and the hs row stride must be multiples of 8");
+                       uint16_t* hs, hipStream_t stream) {
+  if (H % 8 != 0) throw std::runtime_error("vgrad_rows: H must be a multiple of 8");
   hipLaunchKernelGGL(vgrad_rows_kernel, dim3((unsigned)((NR + VG_ROWS - 1) / VG_ROWS)),
-                     dim3(VG_THREADS), 0, stream, alpha, NR, H, hd, dhd, hs, ldhs);
+                     dim3(VG_THREADS), 0, stream, alpha, NR, H, hd, dhd, hs);
   post_launch("vgrad_rows_kernel", stream);
 }
 

@@ -177,10 +177,8 @@ void launch_vgrad_fix(const VGradRows& g, const uint16_t* hd, const uint16_t* W,
                       hipStream_t stream);
 // dhd = alpha . dhd in place (X = E' W -> dHd; dhd nullable: the consumer
 // scales the rows itself), hs = bf16(alpha . hd)
-// (ldhs > H: row stride of hs, with alpha as two bf16 columns (hi, lo) at H,
-// H + 1 and zeros after them, for the bias gradient inside the dW GEMM)
 void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd, float* dhd,
-                       uint16_t* hs, hipStream_t stream, int ldhs = 0);
+                       uint16_t* hs, hipStream_t stream);
 // dblog = sum_r alpha_r E_rv (two launches: per-row-block partials, reduce);
 // part: vgrad_colsum_blocks(NR) * V floats
 int vgrad_colsum_blocks(int64_t NR);

@@ -160,8 +160,7 @@ class _DecoderFn(torch.autograd.Function):
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
             drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell,
             state0, eng.upper_operands(), bool(save and not want_full))
-        # last output: X = E W computed during the rollout (empty if not)
-        xw, outs = outs[-1], outs[:-1]
+        xw = torch.empty(0, device=dev)  # X = E W: engine.launch_x after the rollout
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
         # training rollouts save E = exp(logit - previous step's LSE) (bf16) for
@@ -533,9 +532,7 @@ class DecoderEngine:
         if ctx is None or ctx.saved is None:
             return
         if stream is None:
-            import os
-            stream = self._aux.ptab_stream if os.environ.get('CSTCAP_X_STREAM') == 'ptab' \
-                else self._aux.x_stream
+            stream = self._aux.x_stream
         logits16 = ctx.saved[1]
         n, R, ldl = logits16.shape
         main = torch.cuda.current_stream(logits16.device)

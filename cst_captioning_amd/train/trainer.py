@@ -127,7 +127,7 @@ class Trainer:
             engine.attach_optimizer(self)
             # SCST: the vocab head's X = E W runs behind the greedy decode on the
             # side stream (rl_loss -> engine.launch_x)
-            engine.x_after_rollout = os.environ.get('CSTCAP_X_AFTER_ROLLOUT', '1') != '0'
+            engine.x_after_rollout = True
         self.scorer = None
         # PyTorch decoder path at --precision bf16: torch autocast (bf16 GEMMs /
         # LSTM, fp32 softmax), the same-precision baseline of the fused engine
@@ -182,10 +182,7 @@ class Trainer:
         if opt.use_cst == 0 and self.device.type == 'cuda':
             # The greedy baseline only depends on the inputs and the current
             # weights: decode + score it on a second HIP stream, concurrently
-            # with the rollout on the main stream.  The rollout is enqueued
-            # first, so its launches keep the GPU busy while the host enqueues
-            # the small greedy decode (measured equal to greedy-first, 4.87 ms
-            # per step: the step is GPU-bound).
+            # with the rollout on the main stream.
             if getattr(self, '_side_stream', None) is None:
                 # (a high-priority stream for the greedy decode measured 4.5 ->
                 # 8.7 ms per step: the queue priority throttles the rollout)
@@ -216,33 +213,23 @@ class Trainer:
                 stamps.mark('greedy_end')
                 self._ev_greedy.record(side)
             return g
-        # where the greedy branch goes in the captured step's node order (the
-        # graph runtime submits nodes in capture order, ~2.7 us each):
-        # CSTCAP_GREEDY_AT = k > 0: from the rollout's step-k hook (both
-        # decodes start early), 0: before the rollout, -1: after it
-        greedy_at = int(os.environ.get('CSTCAP_GREEDY_AT', '0')) if side is not None else -1
-        holder = []
-        if side is not None and greedy_at == 0:
-            holder.append(enqueue_greedy())
-        hook = side is not None and greedy_at > 0 and self.engine is not None
-        if hook:
-            from .. import _ext
-            _ext.ops().set_step_hook(greedy_at, lambda: holder.append(enqueue_greedy()))
-        stamps.base('fwd_sample')
-        try:
-            model_res, logprobs, _ = self._decode_rollout(data)
-        finally:
-            if hook:
-                _ext.ops().set_step_hook(-1, None)
-        stamps.mark('rollout_enq')
+        # The greedy branch is captured BEFORE the rollout.  A replayed graph's
+        # nodes are submitted in capture order (~2.7 us each): captured after
+        # the rollout, the greedy branch started only after the rollout's ~85
+        # nodes, and with the X node below in the graph the runtime ran it
+        # behind the rollout altogether (device stamps,
+        # profiles/r3/README_r3.md "Node order of the replayed graph").
         if side is not None:
-            greedy_scores = holder[0] if holder else enqueue_greedy()
-        x_at_loss = os.environ.get('CSTCAP_X_AT', 'rollout') == 'loss'
-        if self.engine is not None and not x_at_loss:
+            greedy_scores = enqueue_greedy()
+        stamps.base('fwd_sample')
+        model_res, logprobs, _ = self._decode_rollout(data)
+        stamps.mark('rollout_enq')
+        if self.engine is not None:
             # the vocab head's X = E W on the engine's own stream once the
             # rollout is done, under the reward / loss computation
             # (engine.launch_x; on the greedy stream behind its decode, the
-            # backward's deferred join crashed hipStreamEndCapture)
+            # backward's deferred join crashed hipStreamEndCapture; launched
+            # after the loss instead: same step time, profiles/r3/ab_xat_vhsched.txt)
             self.engine.launch_x()
         stamps.base(None)
         self.timer.mark('rollout')
@@ -250,7 +237,7 @@ class Trainer:
             sample_scores = scorer.score(model_res, vid_rows)
             stamps.mark('sample_scores')
             if side is not None:
-                main.wait_event(self._ev_greedy)  # (not the X GEMM queued behind it)
+                main.wait_event(self._ev_greedy)
                 greedy_scores.record_stream(main)
             else:
                 greedy_scores = self._greedy_scores(data, scorer, S, per_video=fused)
@@ -259,8 +246,6 @@ class Trainer:
                 loss, reward, m_score, b_score = scst_loss(model_res, logprobs, sample_scores,
                                                            greedy_scores)
                 stamps.mark('loss')
-                if self.engine is not None and x_at_loss:  # (A/B: X after the loss)
-                    self.engine.launch_x()
                 self.timer.mark('reward')
                 return loss, {'reward': reward, 'm': m_score, 'b': b_score, 'seq': model_res}
             reward, m_score, b_score = scst_from_scores(sample_scores.float(),
@@ -311,8 +296,7 @@ class Trainer:
         """zero_grad -> forward -> loss -> backward (+ the NaN-guard flag).
         Device work only: no host synchronisation (graph-capturable)."""
         opt, m = self.opt, self.model
-        if (self.engine is not None and self.device.type == 'cuda'
-                and os.environ.get('CSTCAP_PTAB_PREFETCH', '1') != '0'):
+        if self.engine is not None and self.device.type == 'cuda':
             self.engine.prefetch_ptab()  # under the prologue, on a side stream
         m.train()
         self.optimizer.zero_grad()
