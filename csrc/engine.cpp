@@ -650,10 +650,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
   // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
   // split-K batch over groups of decode steps multiplies the tiles in flight,
-  // the partial products summed afterwards (CSTCAP_DW_SPLITK; must divide the
-  // step count)
-  // (4 groups: 3.745-3.774 vs 3.792-3.831 ms per step for one GEMM, 7 groups
-  // 3.862-3.873, profiles/r3/ab_sched.txt)
+  // the partial products summed afterwards (the group count divides the
+  // step count; 4 groups: 3.745-3.774 vs 3.792-3.831 ms per step for one
+  // GEMM, 7 groups 3.862-3.873, profiles/r3/ab_sched.txt)
   const int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
   auto dw_gemm = [&]() {  // (current stream: side)
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
