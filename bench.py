@@ -47,7 +47,11 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# BASELINE.md publishes no number for the metric (BASELINE.json "published":
+# {}), so vs_baseline is null; the self-measured reference-semantics and
+# same-precision PyTorch runs are reported as separate ratios
 BASELINE_FILE = os.path.join(REPO, 'profiles', 'reference_semantics_baseline.json')
+SAME_PRECISION_FILE = os.path.join(REPO, 'profiles', 'r2', 'bench_r2_torch_bf16_autocast.json')
 
 
 def parse():
@@ -258,10 +262,12 @@ def main():
     dt, ms, caps, vids = main_run['dt'], main_run['ms'], main_run['caps'], main_run['vids']
     loss, n_params, t_gen = main_run['loss'], main_run['n_params'], main_run['t_gen']
     S = 20
-    baseline = None
-    if os.path.exists(BASELINE_FILE):
-        with open(BASELINE_FILE) as f:
-            baseline = json.load(f).get('value')
+    def _value(path):
+        if not os.path.exists(path):
+            return None
+        with open(path) as f:
+            return json.load(f).get('value')
+    ref_sem, same_prec = _value(BASELINE_FILE), _value(SAME_PRECISION_FILE)
     if a.mode == 'beam':
         metric, value, unit = 'beam-%d evaluation decode videos/sec (whole job)' % a.beam_size, \
             vids, 'videos/s'
@@ -276,7 +282,14 @@ def main():
         'value': round(value, 2), 'unit': unit, 'n_gpus': ctx.world_size,
         'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': round(ms, 3),
         'higher_is_better': True, 'scaling': 'weak',
-        'vs_baseline': round(caps / baseline, 3) if (baseline and a.mode == 'scst') else None,
+        'vs_baseline': None,  # no published number
+        # self-measured, same job on one MI355X: reference semantics (PyTorch
+        # ops, fp32, CPU CIDEr-D; profiles/reference_semantics_baseline.json)
+        # and the same-precision PyTorch path (bf16 autocast, GPU CIDEr-D)
+        'vs_reference_semantics_1gpu': (round(caps / ctx.world_size / ref_sem, 2)
+                                        if (ref_sem and a.mode == 'scst') else None),
+        'vs_pytorch_bf16_1gpu': (round(caps / ctx.world_size / same_prec, 2)
+                                 if (same_prec and a.mode == 'scst') else None),
         # effective compute dtype: the fused engine is bf16; the PyTorch path is
         # bf16 under autocast with --precision bf16 on a GPU, else fp32
         'dtype': 'bf16' if main_run['bf16'] else 'fp32',
