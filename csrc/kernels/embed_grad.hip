@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void video_gate_grad_kernel(const uint16_t* __
   for (int k = 0; k < 8; ++k) s_part[rs][8 * cg + k] = acc[k];
   __syncthreads();
   const int c = blockIdx.y * 256 + tid;
-  if (c < G4 && col <= G4) {
+  if (c < G4) {  // (chunks past G4 loaded clamped columns into LDS slots >= G4: unused)
     float v = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) v += s_part[r][tid];
