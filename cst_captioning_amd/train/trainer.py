@@ -195,8 +195,8 @@ class Trainer:
             # gathered HERE, on the main stream, before the event both decodes
             # order behind: gathered lazily by whichever decode touched it
             # first, the other stream would read it unordered
-            data['feats']
-            data['labels']
+            gathered = (data['feats'], data['labels'])  # (LazyGather: gathers now)
+            del gathered
             inputs_ready = self._ev_inputs
             inputs_ready.record(main)
         # fused engine: reward, mask and REINFORCE loss in one launch
