@@ -33,8 +33,6 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                                     int64_t K, int64_t T, int64_t bos_index,
                                     std::vector<at::Tensor> att, int64_t cell,
                                     std::vector<at::Tensor> state0, std::vector<at::Tensor> up);
-double vocab_rr_bench(at::Tensor hd, at::Tensor h, at::Tensor wlog, at::Tensor blog,
-                      at::Tensor whh, at::Tensor vgate, int64_t vdiv, int64_t iters, int64_t dbg);
 double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t iters);
 double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters);
 double att_bench(at::Tensor gv, at::Tensor P, at::Tensor q, at::Tensor wa, at::Tensor ba,
@@ -57,7 +55,11 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
                                          at::Tensor blog, at::Tensor whh, at::Tensor vgate,
                                          int64_t vdiv, at::Tensor tgt, at::Tensor eoff,
                                          int64_t save, int64_t mode, int64_t step, at::Tensor rng,
-                                         int64_t rr);
+                                         int64_t fused, at::Tensor ptab, at::Tensor c_prev,
+                                         double drop_p, int64_t cell, int64_t eos,
+                                         at::Tensor unfinished, double ss_prob);
+int64_t decode_sync_errors(bool reset);
+void set_fused_decode_mode(int64_t on);
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);
@@ -138,13 +140,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("refresh_shadows", &cst::refresh_shadows);
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
   m.def("vgrad_colsum_bench", &cst::vgrad_colsum_bench);
-  m.def("vocab_rr_bench", &cst::vocab_rr_bench);
   m.def("token_sort_bench", &cst::token_sort_bench);
   m.def("att_bench", &cst::att_bench);
   m.def("token_sort", &cst::token_sort);
   m.def("token_group_sum", &cst::token_group_sum);
   m.def("vocab_select", &cst::vocab_select);
   m.def("decode_step_test", &cst::decode_step_test);
+  m.def("decode_sync_errors", &cst::decode_sync_errors, py::arg("reset") = false);
+  m.def("set_fused_decode", &cst::set_fused_decode_mode);
   m.def("att_mfma_fwd", &cst::att_mfma_fwd);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);

@@ -117,6 +117,33 @@ static DeviceAux& device_aux(int dev_index) {
   return *it->second;
 }
 
+// Timeout counter of the fused decode step's in-launch waits (vocab.hip): one
+// persistent int per device, allocated outside graph capture (the first
+// decoder_forward of a device runs eagerly before any capture).  A non-zero
+// value means a wait gave up: decode_sync_errors() reports it.
+static std::map<int, at::Tensor>& decode_err_bufs() {
+  static std::map<int, at::Tensor> m;
+  return m;
+}
+static int* decode_err_ptr(const at::Device& dev) {
+  auto& m = decode_err_bufs();
+  auto it = m.find((int)dev.index());
+  if (it == m.end())
+    it = m.emplace((int)dev.index(),
+                   at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev)))
+             .first;
+  return it->second.data_ptr<int>();
+}
+int64_t decode_sync_errors(bool reset) {
+  int64_t n = 0;
+  for (auto& kv : decode_err_bufs()) {
+    n += kv.second.item<int>();
+    if (reset) kv.second.zero_();
+  }
+  return n;
+}
+void set_fused_decode_mode(int64_t on) { set_fused_decode((int)on); }
+
 // Read-only zeros of at least n elements (initial decoder states): one
 // persistent buffer per (device, dtype), so a decode does not launch a fill
 // kernel per call.  Grown only outside graph capture; replaced buffers stay
@@ -220,8 +247,16 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor lse = at::empty({n_steps, R}, f32);
   at::Tensor part =
       at::empty({(int64_t)vocab_part_slots((int)V) * R * vocab_partial_bytes() / 4}, f32);
-  at::Tensor counts = at::zeros({(T + 1) * combine_count_ints_per_step()},
-                                at::TensorOptions().dtype(at::kInt).device(dev));
+  // one zero-filled int area: the end-of-sequence flags of every step, then
+  // (fused decode step) each step's arrival counters / ready flags
+  const int64_t n_cnt = (T + 1) * combine_count_ints_per_step();
+  const int64_t n_sync = fused_sync_ints((int)R);
+  const bool fused_ok = fused_decode_enabled();
+  at::Tensor flags_area = at::zeros({n_cnt + (fused_ok ? n_steps * n_sync : 0)},
+                                    at::TensorOptions().dtype(at::kInt).device(dev));
+  at::Tensor counts = flags_area.narrow(0, 0, n_cnt);
+  at::Tensor tok32 = fused_ok ? at::empty({R}, at::TensorOptions().dtype(at::kInt).device(dev))
+                              : at::Tensor();
   at::Tensor unfinished =
       use_unfinished ? at::ones({R}, at::TensorOptions().dtype(at::kByte).device(dev))
                      : at::Tensor();
@@ -409,13 +444,31 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                        save ? q_next.data_ptr<float>() : nullptr, att_ep.data_ptr<float>(),
                        att_cnt.data_ptr<int>()};
     const bool q_tiles = has_att && !att_mfma;  // W_q tiles in the recurrent GEMM
+    // fused decode step (vocab.hip): the combine and the next step's cell run
+    // inside this launch; the last step (no recurrent part) keeps the combine
+    const bool fuse = fused_ok && next && !q_tiles;
+    FuseArgs fz{};
+    if (fuse) {
+      fz = FuseArgs{flags_area.data_ptr<int>() + n_cnt + t * n_sync, tok32.data_ptr<int>(),
+                    decode_err_ptr(dev),
+                    lse[t].data_ptr<float>(), seq.data_ptr<int64_t>() + t, T - 1,
+                    g_sel.data_ptr<float>() + t, T - 1,
+                    want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
+                    (float)ss_prob, use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
+                    use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr,
+                    ptab.data_ptr<float>(), c_buf(0, t), c_buf(0, t + 1), h_buf(0, t + 1),
+                    hd_buf(0, t + 1), (int)H, gates_buf(0, t + 1), (float)drop_p, key(0, t + 1),
+                    (int)cell,
+                    att_mfma ? reinterpret_cast<const uint16_t*>(vg16.data_ptr()) : nullptr};
+    }
     const int n_vt = launch_vocab_lstm_fwd(
         vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
         save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl, part.data_ptr(),
         tgt, L, vflags, inv_temp, RNG, (int)t, h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
         next ? pre.data_ptr<float>() : nullptr, st, q_tiles ? (int)A : 0,
         q_tiles && next ? q_next.data_ptr<float>() : nullptr,
-        exp_t ? lse[t - 1].data_ptr<float>() : nullptr, att_mfma && next ? &am : nullptr);
+        exp_t ? lse[t - 1].data_ptr<float>() : nullptr, att_mfma && next ? &am : nullptr,
+        fuse ? &fz : nullptr);
     if (q_tiles && next)
       launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), q_next.data_ptr<float>(),
                      nullptr, a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv,
@@ -430,14 +483,15 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                       (float)drop_p, key(0, t + 1), (int)cell,
                       att_mfma ? reinterpret_cast<const uint16_t*>(vg16.data_ptr()) : nullptr};
     }
-    launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
-                         choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
-                         choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,
-                         want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
-                         (float)ss_prob, RNG, (int)t,
-                         use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
-                         use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st,
-                         next ? &cl : nullptr);
+    if (!fuse)
+      launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
+                           choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
+                           choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,
+                           want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
+                           (float)ss_prob, RNG, (int)t,
+                           use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
+                           use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st,
+                           next ? &cl : nullptr);
     if (save && store_exp && t == 0)
       launch_vocab_exp_convert(reinterpret_cast<uint16_t*>(logits16[0].data_ptr()), ldl, (int)V,
                                (int)R, lse[0].data_ptr<float>(), st);
@@ -1401,36 +1455,6 @@ double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tens
       iters, st);
 }
 
-// row-resident decode launch alone (SCST sampling step + exp store +
-// recurrent GEMM with video gates), dbg: see launch_vocab_rr_bench; us per launch
-double vocab_rr_bench(at::Tensor hd, at::Tensor h, at::Tensor wlog, at::Tensor blog,
-                      at::Tensor whh, at::Tensor vgate, int64_t vdiv, int64_t iters, int64_t dbg) {
-  const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
-  auto dev = hd.device();
-  auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
-  const int64_t ldl = (V + 63) / 64 * 64;
-  at::Tensor out = at::empty({R, ldl}, hd.options());
-  at::Tensor part = at::empty({(int64_t)vocab_part_slots((int)V) * R * vocab_partial_bytes() / 4}, f32);
-  at::Tensor pre = at::empty({R, 4 * H}, f32), eoff = at::full({R}, 8.f, f32);
-  at::Tensor rng = at::full({2}, 1234, at::TensorOptions().dtype(at::kInt).device(dev));
-  hipStream_t st = cur_stream();
-  bool ok = true;
-  const double us = time_launches(
-      [&](int i) {
-        ok = ok && launch_vocab_rr_bench(
-                       reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)R, (int)H,
-                       reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
-                       (int)V, reinterpret_cast<uint16_t*>(out.data_ptr()), ldl, part.data_ptr(),
-                       rng_ptr(rng), i, eoff.data_ptr<float>(),
-                       reinterpret_cast<const uint16_t*>(h.data_ptr()),
-                       reinterpret_cast<const uint16_t*>(whh.data_ptr()), vgate.data_ptr<float>(),
-                       (int)vdiv, pre.data_ptr<float>(), (int)dbg, st);
-      },
-      iters, st);
-  TORCH_CHECK(ok, "vocab_rr_bench: shape not covered by the row-resident launch");
-  return us;
-}
-
 // bias-gradient column sums over the exp store: E (n, R, ldl) bf16, alpha (n*R)
 double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t iters) {
   check_cuda(E, "E");
@@ -1594,15 +1618,22 @@ std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor 
   return {tok.view({R}), lse};
 }
 
-// One decode step (vocab projection + recurrent GEMM + combine without the
-// cell), for tests of the two launch forms: rr = 1 row-resident (vocab_rr.h),
-// 0 tiled, -1 default.  save: 0 none, 1 fp16 logits, 2 exp store (eoff given).
-// Returns {lse, tok, g_sel, g_xe, saved rows (R, ldl), pre (R, 4H), n_parts}.
+// One decode step for tests of the two launch forms: the decode launch +
+// vocab_combine_kernel (fused = 0) or the fused decode step (fused = 1, needs
+// the recurrent part and the cell).  save: 0 none, 1 fp16 logits, 2 exp store
+// (eoff given).  Cell (ptab defined): the next step's cell from c_prev and
+// the chosen tokens (dropout drop_p, step key `step + 1`).  eos: 0 no
+// end-of-sequence rules; 1 / 2 the all-rows-ended counter with a live / dead
+// previous step; unfinished (R) uint8 nullable: the per-row mask, updated in
+// place.  Returns {lse, tok, g_sel, g_xe, saved rows (R, ldl), pre (R, 4H),
+// n_parts, h, c, h_drop, gates, counts}.
 std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor wlog,
                                          at::Tensor blog, at::Tensor whh, at::Tensor vgate,
                                          int64_t vdiv, at::Tensor tgt, at::Tensor eoff,
                                          int64_t save, int64_t mode, int64_t step, at::Tensor rng,
-                                         int64_t rr) {
+                                         int64_t fused, at::Tensor ptab, at::Tensor c_prev,
+                                         double drop_p, int64_t cell, int64_t eos,
+                                         at::Tensor unfinished, double ss_prob) {
   check_cuda(hd, "hd");
   check_cuda(wlog, "wlog");
   const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
@@ -1622,8 +1653,23 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
   if (has_tgt) TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.numel() == R, "tgt (R) int64");
   if (save == 2)
     TORCH_CHECK(eoff.defined() && eoff.scalar_type() == at::kFloat && eoff.numel() == R, "eoff (R)");
+  const bool do_cell = ptab.defined() && ptab.numel() > 0;
+  if (do_cell) {
+    TORCH_CHECK(lstm, "the cell needs the recurrent part");
+    check_cuda(ptab, "ptab");
+    check_cuda(c_prev, "c_prev");
+    TORCH_CHECK(ptab.scalar_type() == at::kFloat && ptab.size(0) == V && ptab.size(1) == 4 * H &&
+                    c_prev.scalar_type() == at::kFloat && c_prev.numel() == R * H,
+                "ptab (V, 4H) / c_prev (R, H) fp32");
+  }
+  TORCH_CHECK(!fused || do_cell, "the fused decode step needs the cell");
+  const bool has_unf = unfinished.defined() && unfinished.numel() > 0;
+  if (has_unf)
+    TORCH_CHECK(unfinished.is_cuda() && unfinished.scalar_type() == at::kByte &&
+                    unfinished.numel() == R, "unfinished (R) uint8");
   auto dev = hd.device();
   auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+  auto bf = at::TensorOptions().dtype(at::kBFloat16).device(dev);
   const int64_t ldl = (V + 63) / 64 * 64;
   at::Tensor part = at::empty({(int64_t)vocab_part_slots((int)V) * R * vocab_partial_bytes() / 4}, f32);
   at::Tensor saved = save ? at::zeros({R, ldl}, at::TensorOptions()
@@ -1633,30 +1679,61 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
   at::Tensor pre = lstm ? at::zeros({R, 4 * H}, f32) : at::Tensor();
   at::Tensor lse = at::empty({R}, f32), gsel = at::zeros({R}, f32), gxe = at::zeros({R}, f32);
   at::Tensor tok = at::zeros({R}, at::TensorOptions().dtype(at::kLong).device(dev));
-  hipStream_t st = cur_stream();
-  const int flags = (mode == SEL_SAMPLE_H ? 1 : 0) | (mode == SEL_GREEDY_H ? 2 : 0) | (save == 2 ? 16 : 0);
-  set_decode_rr((int)rr);
-  int n = 0;
-  try {
-    n = launch_vocab_lstm_fwd(
-        reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R, (int)H,
-        reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(), (int)V,
-        save ? reinterpret_cast<uint16_t*>(saved.data_ptr()) : nullptr, ldl, part.data_ptr(),
-        has_tgt ? tgt.data_ptr<int64_t>() : nullptr, 1, flags, 1.f, rng_ptr(rng), (int)step,
-        lstm ? reinterpret_cast<const uint16_t*>(h.data_ptr()) : nullptr,
-        lstm ? reinterpret_cast<const uint16_t*>(whh.data_ptr()) : nullptr,
-        has_vg ? vgate.data_ptr<float>() : nullptr, (int)vdiv, lstm ? pre.data_ptr<float>() : nullptr,
-        st, 0, nullptr, save == 2 ? eoff.data_ptr<float>() : nullptr, nullptr);
-  } catch (...) {
-    set_decode_rr(-1);
-    throw;
+  at::Tensor h_out, c_out, hdrop, gates;
+  if (do_cell) {
+    h_out = at::zeros({R, H}, bf);
+    c_out = at::zeros({R, H}, f32);
+    hdrop = at::zeros({R, H}, bf);
+    gates = at::zeros({R, 4 * H}, bf);
   }
-  set_decode_rr(-1);
-  launch_vocab_combine(part.data_ptr(), n, (int)R, lse.data_ptr<float>(), tok.data_ptr<int64_t>(), 1,
-                       gsel.data_ptr<float>(), 1, has_tgt ? gxe.data_ptr<float>() : nullptr, 1,
-                       has_tgt ? tgt.data_ptr<int64_t>() : nullptr, 1, (int)mode, 0.f, rng_ptr(rng),
-                       (int)step, nullptr, 0, nullptr, st);
-  return {lse, tok, gsel, gxe, saved, pre, at::full({1}, n, at::TensorOptions().dtype(at::kLong))};
+  // counts: steps 0..2 of the end-of-sequence flags; this step is count step 2
+  const int cps = combine_count_ints_per_step();
+  at::Tensor flags_area = at::zeros({3 * cps + fused_sync_ints((int)R)},
+                                    at::TensorOptions().dtype(at::kInt).device(dev));
+  if (eos == 1) flags_area.narrow(0, cps, 1).fill_(1);  // a live row at the previous step
+  at::Tensor counts = flags_area.narrow(0, 0, 3 * cps);
+  int* CNT = eos ? counts.data_ptr<int>() : nullptr;
+  at::Tensor tok32 = at::empty({R}, at::TensorOptions().dtype(at::kInt).device(dev));
+  hipStream_t st = cur_stream();
+  const int flags = (mode == SEL_SAMPLE_H || mode == SEL_SS_H ? 1 : 0) |
+                    (mode == SEL_GREEDY_H ? 2 : 0) | (save == 2 ? 16 : 0);
+  const int64_t* TG = has_tgt ? tgt.data_ptr<int64_t>() : nullptr;
+  uint8_t* UNF = has_unf ? unfinished.data_ptr<uint8_t>() : nullptr;
+  FuseArgs fz{};
+  if (fused)
+    fz = FuseArgs{flags_area.data_ptr<int>() + 3 * cps, tok32.data_ptr<int>(), decode_err_ptr(dev),
+                  lse.data_ptr<float>(), tok.data_ptr<int64_t>(), 1, gsel.data_ptr<float>(), 1,
+                  has_tgt ? gxe.data_ptr<float>() : nullptr, 1, TG, 1, (int)mode, (float)ss_prob,
+                  CNT, 2, UNF, ptab.data_ptr<float>(), c_prev.data_ptr<float>(),
+                  c_out.data_ptr<float>(), reinterpret_cast<uint16_t*>(h_out.data_ptr()),
+                  reinterpret_cast<uint16_t*>(hdrop.data_ptr()), (int)H,
+                  reinterpret_cast<uint16_t*>(gates.data_ptr()), (float)drop_p, (int)step + 1,
+                  (int)cell, nullptr};
+  const int n = launch_vocab_lstm_fwd(
+      reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R, (int)H,
+      reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(), (int)V,
+      save ? reinterpret_cast<uint16_t*>(saved.data_ptr()) : nullptr, ldl, part.data_ptr(), TG, 1,
+      flags, 1.f, rng_ptr(rng), (int)step,
+      lstm ? reinterpret_cast<const uint16_t*>(h.data_ptr()) : nullptr,
+      lstm ? reinterpret_cast<const uint16_t*>(whh.data_ptr()) : nullptr,
+      has_vg ? vgate.data_ptr<float>() : nullptr, (int)vdiv, lstm ? pre.data_ptr<float>() : nullptr,
+      st, 0, nullptr, save == 2 ? eoff.data_ptr<float>() : nullptr, nullptr,
+      fused ? &fz : nullptr);
+  if (!fused) {
+    CellLaunch cl{};
+    if (do_cell)
+      cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_prev.data_ptr<float>(),
+                      c_out.data_ptr<float>(), reinterpret_cast<uint16_t*>(h_out.data_ptr()),
+                      reinterpret_cast<uint16_t*>(hdrop.data_ptr()), (int)H,
+                      reinterpret_cast<uint16_t*>(gates.data_ptr()), (int)H, (float)drop_p,
+                      (int)step + 1, (int)cell, nullptr};
+    launch_vocab_combine(part.data_ptr(), n, (int)R, lse.data_ptr<float>(), tok.data_ptr<int64_t>(),
+                         1, gsel.data_ptr<float>(), 1, has_tgt ? gxe.data_ptr<float>() : nullptr, 1,
+                         TG, 1, (int)mode, (float)ss_prob, rng_ptr(rng), (int)step, CNT, 2, UNF, st,
+                         do_cell ? &cl : nullptr);
+  }
+  return {lse, tok, gsel, gxe, saved, pre, at::full({1}, n, at::TensorOptions().dtype(at::kLong)),
+          h_out, c_out, hdrop, gates, counts};
 }
 
 // the counting sort itself, for tests: returns {stok, srow} (int32)

@@ -21,9 +21,12 @@
 //      of the slice in LDS, 16-byte broadcast reads), combined over the 4 lane
 //      groups and the 4 waves, stored to the workgroup's slot with
 //      write-through (sc1) stores; one agent-scope ticket add per workgroup;
-//   3. the video's LAST workgroup (ticket NS - 1; MI355X_MICROARCH.md
-//      "Valid forms", row 1: sc1 stores drained by vmcnt(0) before the add,
-//      sc1 loads after it) sums the NS slots, adds b_a, takes the softmax over
+//   3. the video's LAST workgroup (ticket NS - 1; the hand-off is write-through
+//      (sc1) slot stores, drained by every storing wave's s_waitcnt vmcnt(0)
+//      and a workgroup barrier before ONE lane's agent-scope ticket add, and
+//      sc1 loads of the slots by the workgroup that drew the last ticket: no
+//      L1 line of another CU and no unflushed L2 line of another XCD is ever
+//      read) sums the NS slots, adds b_a, takes the softmax over
 //      frames and forms vgate^T = Gv[b]^T alpha^T (4H x 32, K = 16 frames) on
 //      MFMA (v_mfma_f32_32x32x16_bf16): A operand = the per-frame gate table
 //      in frame-minor bf16 layout gv16[b][n][CP], requested before the slot
@@ -243,12 +246,22 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
       uint16_t* dst = g.vg_out + (int64_t)(row0 + r) * G4 + n0 + 4 * hh;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(o[4 * j]) | ((uint32_t)f2bf(o[4 * j + 1]) << 16);
-        pk.y = (uint32_t)f2bf(o[4 * j + 2]) | ((uint32_t)f2bf(o[4 * j + 3]) << 16);
-        *reinterpret_cast<uint2*>(dst + 8 * j) = pk;
+        const uint64_t pk =
+            (uint64_t)((uint32_t)f2bf(o[4 * j]) | ((uint32_t)f2bf(o[4 * j + 1]) << 16)) |
+            ((uint64_t)((uint32_t)f2bf(o[4 * j + 2]) | ((uint32_t)f2bf(o[4 * j + 3]) << 16))
+             << 32);
+        // write-through (sc1): in the fused decode step the recurrent tiles of
+        // this same launch read these rows (sc1 loads) once `done` counts
+        // the video
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(dst + 8 * j), pk, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+  }
+  if (g.done != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(g.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
