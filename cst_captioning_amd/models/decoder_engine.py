@@ -205,6 +205,8 @@ class _DecoderFn(torch.autograd.Function):
             raise RuntimeError('decoder forward ran without saving activations')
         R, T, vdiv, want_xe = ctx.save_dims
         eng = ctx.eng
+        if eng._x_pending is ctx:  # never handed to launch_x: do not keep ctx alive
+            eng._x_pending = None
         lse, logits16, hdrop, gates, c_all, h_all, seq, labels, bos, xw = ctx.saved
         if ctx.xw_late is not None:  # X = E W launched after the rollout (launch_x)
             xw, ev = ctx.xw_late
@@ -403,8 +405,9 @@ class DecoderEngine:
         # running count of exp-store rows the backward recomputed because the
         # row's LSE jumped by > 60 between steps (csrc/kernels/vocab_grad.hip)
         self.exp_fix_rows = torch.zeros(1, dtype=torch.int32, device=dev)
-        # X = E W after the rollout (launch_x): the trainer enables it and calls
-        # launch_x on its greedy side stream once the greedy decode is enqueued
+        # X = E W after the rollout (launch_x): the trainer enables it for RL
+        # steps and calls launch_x right after the rollout is enqueued; the
+        # GEMM runs on the engine's own x_stream
         self.x_after_rollout = False
         self.direct_grad_slots = None
         self.direct_params = None
@@ -516,10 +519,18 @@ class DecoderEngine:
         self.refresh_weights()  # params were re-homed into the flat buffer
 
     def after_step(self):
+        """The weights changed (an optimizer step ran, eagerly or inside a
+        replayed graph): the gate table is stale from here on."""
         self.weights_version += 1
         self._ptab_pending = False
         if not self.fused_refresh:
             self.refresh_weights()
+
+    def invalidate_ptab(self):
+        """Mark the gate table stale: a graph captured next then always holds
+        its refresh (prefetch_ptab), whatever an eval just computed."""
+        self._ptab_version = -1
+        self._ptab_pending = False
 
     def launch_x(self, stream=None):
         """X = E W of the last training forward (the vocab head's backward GEMM

@@ -125,10 +125,10 @@ class Trainer:
         self.optimizer.grad_scale = self.bucket.grad_scale(self.ctx)
         if engine is not None:
             engine.attach_optimizer(self)
-            # SCST: the vocab head's X = E W runs behind the greedy decode on the
-            # side stream (rl_loss -> engine.launch_x)
-            engine.x_after_rollout = True
         self.scorer = None
+        # SCST with the fused engine: X = E W launched right after the rollout
+        # (engine.launch_x); False keeps the backward's own E' W GEMM (tests)
+        self.use_x_after_rollout = True
         # PyTorch decoder path at --precision bf16: torch autocast (bf16 GEMMs /
         # LSTM, fp32 softmax), the same-precision baseline of the fused engine
         self.autocast_bf16 = (engine is None and self.device.type == 'cuda'
@@ -298,6 +298,11 @@ class Trainer:
         opt, m = self.opt, self.model
         if self.engine is not None and self.device.type == 'cuda':
             self.engine.prefetch_ptab()  # under the prologue, on a side stream
+        if self.engine is not None:
+            # RL steps: the vocab head's X = E W right after the rollout, on the
+            # engine's stream (rl_loss -> engine.launch_x); nothing consumes it
+            # in an XE step
+            self.engine.x_after_rollout = bool(self.rl_training and self.use_x_after_rollout)
         m.train()
         self.optimizer.zero_grad()
         m.set_seq_per_img(self.train_loader.get_seq_per_img())
@@ -408,10 +413,14 @@ class Trainer:
         g_a, g_b = self._graph
         g_a.replay()
         if self.bucket.sharded:  # data parallel, sharded update: eager after the graph
-            self._sharded_update(self._graph_skip)
-        elif g_b is not None:  # data parallel: eager all-reduce between the graphs
-            self.bucket.all_reduce(self.ctx)
-            g_b.replay()
+            self._sharded_update(self._graph_skip)  # (calls engine.after_step)
+        else:
+            if g_b is not None:  # data parallel: eager all-reduce between the graphs
+                self.bucket.all_reduce(self.ctx)
+                g_b.replay()
+            # the replayed update changed the weights on the device: the gate
+            # table an eval may have refreshed since is stale again
+            self.engine.after_step()
         return self._graph_out
 
     def _capture(self, loader, idx, key, mixer_from, scb):
@@ -421,6 +430,8 @@ class Trainer:
         default stream, and the cross-stream wait they add breaks the capture."""
         self._graph = self._graph_out = None
         torch.cuda.synchronize(self.device)
+        # the captured step must refresh the gate table itself on every replay
+        self.engine.invalidate_ptab()
         self._static_idx = [t.clone() for t in idx]
         pool = torch.cuda.graph_pool_handle()
         g_a = torch.cuda.CUDAGraph()

@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from test_gpu_graph import _setup  # noqa: E402
 
 tr, loader = _setup(rl=True, drop=0.5, graph=1, H=int(sys.argv[2]) if len(sys.argv) > 2 else 128)
-tr.engine.x_after_rollout = sys.argv[1] == '1'
+tr.use_x_after_rollout = sys.argv[1] == '1'
 for i in range(4):
     out = tr.train_step(loader.get_batch(), 0)
     torch.cuda.synchronize()

@@ -113,9 +113,9 @@ def test_x_after_rollout_matches_folded_path(H):
                 tr, ld = _setup(rl=True, drop=0.5, graph=graph, H=H)
                 tr.engine._rng = lambda dev: fixed
                 if graph:  # eager warm-up step of the key (same path), then the capture
-                    tr.engine.x_after_rollout = False
+                    tr.use_x_after_rollout = False
                     tr.train_step(ld.get_batch(), 0)
-                tr.engine.x_after_rollout = x_after
+                tr.use_x_after_rollout = x_after
                 p0 = _flat(tr.model)
                 out = tr.train_step(ld.get_batch(), 0)
                 torch.cuda.synchronize()
@@ -161,6 +161,37 @@ def test_adam_pass_writes_the_bf16_shadows():
     for g, r in zip(got, (eng.wx, eng.whh_q, eng.emb, eng.wlog)):
         assert torch.equal(g, r)
     torch.testing.assert_close(got[4], eng.ptab, rtol=1e-5, atol=1e-5)
+
+
+def test_gate_table_tracks_replayed_updates():
+    """The gate table P = emb W_ie^T is refreshed lazily (decoder_engine.py
+    prefetch_ptab / ensure_ptab).  An eval between replays refreshes it; the
+    replays after it change the weights on the device only, so the next
+    user must see P stale again (a replay did not bump the
+    version).  And a graph captured while P is marked fresh must still hold
+    its refresh: every replay then trains with the current P."""
+    tr, loader = _setup(rl=True, drop=0.5)
+    eng = tr.engine
+    for _ in range(3):  # eager warm-up, capture + replay
+        tr.train_step(loader.get_batch(), 0)
+    eng.current_ptab()  # an eval: P marked fresh
+    for _ in range(2):
+        tr.train_step(loader.get_batch(), 0)
+    got = eng.current_ptab().clone()
+    eng.refresh_weights()
+    torch.testing.assert_close(got, eng.ptab, rtol=1e-5, atol=1e-5)
+    # recapture while P is fresh (a new schedule key after an eval)
+    tr._graph_key = None
+    tr._graph_warm = {k: 1 for k in tr._graph_warm}
+    eng.current_ptab()
+    before = eng.ptab.clone()
+    tr.train_step(loader.get_batch(), 0)  # capture + replay
+    tr.train_step(loader.get_batch(), 0)  # replay: trains with the refreshed P
+    torch.cuda.synchronize()
+    assert not torch.equal(before, eng.ptab), 'the captured step never refreshed P'
+    got = eng.current_ptab().clone()
+    eng.refresh_weights()
+    torch.testing.assert_close(got, eng.ptab, rtol=1e-5, atol=1e-5)
 
 
 def test_token_counting_sort():
