@@ -1166,10 +1166,11 @@ std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Ten
               "scst_loss: seq / lp (R, T), sample (R), greedy (R or R / rows per video)");
   auto f32 = lp.options();
   at::Tensor out = at::empty({4}, f32), reward = at::empty({R}, f32), loss = at::empty({}, f32);
+  at::Tensor ws = at::zeros({scst_loss_ws_ints((int)R)}, f32.dtype(at::kInt));
   launch_scst_loss_fwd(seq.data_ptr<int64_t>(), lp.data_ptr<float>(), (int)R, (int)T,
                        sample.data_ptr<float>(), greedy.data_ptr<float>(),
                        (int)(R / greedy.numel()), reward.data_ptr<float>(), out.data_ptr<float>(),
-                       loss.data_ptr<float>(), cur_stream());
+                       loss.data_ptr<float>(), ws.data_ptr<int>(), cur_stream());
   return {loss, out, reward};
 }
 

@@ -11,51 +11,94 @@
 
 namespace cst {
 
-constexpr int SL_THREADS = 1024;
+// Forward: 16 rows per 256-thread workgroup (4 rows per wave, the row's
+// T tokens across the lanes: no per-element division), per-workgroup partials
+// {num, den, sum sample, sum greedy} stored write-through, then one lane's
+// agent-scope ticket; the workgroup that draws the last ticket sums the
+// partials in workgroup order (deterministic) and writes out / loss.  One
+// launch of ~R / 16 workgroups instead of a single 1,024-thread block that
+// walked all R x T elements (178 us at 1,280 x 28, profiles/r3).
+constexpr int SL_ROWS = 16;  // rows per workgroup
+int scst_loss_ws_ints(int R) { return 4 * ((R + SL_ROWS - 1) / SL_ROWS) + 64; }
 
-__device__ __forceinline__ float block_sum_1024(float v, float* sh) {
+__device__ __forceinline__ float block_sum_256(float v, float* sh) {
   v = wave_sum(v);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  __syncthreads();
   if (lane == 0) sh[w] = v;
   __syncthreads();
-  float t = 0.f;
-  if (threadIdx.x < SL_THREADS / WAVE) t = sh[threadIdx.x];
-  if (w == 0) t = wave_sum(t);
-  return t;  // valid in thread 0
+  const float t = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return t;
 }
 
-// one block: out = {loss, mean(sample), mean(greedy per row), sum(mask)},
-// reward[r] = sample[r] - greedy[r / gdiv]
-__global__ __launch_bounds__(SL_THREADS) void scst_loss_fwd_kernel(
+// out = {loss, mean(sample), mean(greedy per row), sum(mask)},
+// reward[r] = sample[r] - greedy[r / gdiv]; ws: scst_loss_ws_ints(R) ints,
+// the ticket word (ws[0]) zero at the first launch (re-armed by the kernel)
+__global__ __launch_bounds__(256) void scst_loss_fwd_kernel(
     const int64_t* __restrict__ seq, const float* __restrict__ lp, int R, int T,
     const float* __restrict__ sample, const float* __restrict__ greedy, int gdiv,
-    float* __restrict__ reward, float* __restrict__ out, float* __restrict__ loss) {
-  __shared__ float sh[SL_THREADS / WAVE];
+    float* __restrict__ reward, float* __restrict__ out, float* __restrict__ loss,
+    int* __restrict__ ws) {
+  __shared__ float sh[4];
+  __shared__ int s_last;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float num = 0.f, den = 0.f, ssum = 0.f, gsum = 0.f;
-  for (int r = threadIdx.x; r < R; r += SL_THREADS) {
-    const float s = sample[r], g = greedy[r / gdiv];
-    reward[r] = s - g;
-    ssum += s;
-    gsum += g;
+#pragma unroll
+  for (int j = 0; j < SL_ROWS / 4; ++j) {
+    const int r = blockIdx.x * SL_ROWS + w * (SL_ROWS / 4) + j;
+    if (r >= R) break;
+    const float sv = sample[r], gv = greedy[r / gdiv], rw = sv - gv;
+    if (lane == 0) {
+      reward[r] = rw;
+      ssum += sv;
+      gsum += gv;
+    }
+    const int64_t* srow = seq + (int64_t)r * T;
+    const float* lrow = lp + (int64_t)r * T;
+    for (int t = lane; t < T; t += 64) {
+      const float m = (t == 0 || srow[t - 1] > 0) ? 1.f : 0.f;
+      num += lrow[t] * rw * m;
+      den += m;
+    }
   }
-  for (int64_t i = threadIdx.x; i < (int64_t)R * T; i += SL_THREADS) {
-    const int r = (int)(i / T), t = (int)(i % T);
-    const float m = (t == 0 || seq[i - 1] > 0) ? 1.f : 0.f;
-    const float rw = sample[r] - greedy[r / gdiv];
-    num += lp[i] * rw * m;
-    den += m;
-  }
-  num = block_sum_1024(num, sh);
-  den = block_sum_1024(den, sh);
-  ssum = block_sum_1024(ssum, sh);
-  gsum = block_sum_1024(gsum, sh);
+  num = block_sum_256(num, sh);
+  den = block_sum_256(den, sh);
+  ssum = block_sum_256(ssum, sh);
+  gsum = block_sum_256(gsum, sh);
+  float* part = reinterpret_cast<float*>(ws + 64);
   if (threadIdx.x == 0) {
-    out[0] = -num / den;
-    loss[0] = out[0];
-    out[1] = ssum / (float)R;
-    out[2] = gsum / (float)R;
-    out[3] = den;
+    float4 v = make_float4(num, den, ssum, gsum);
+    __hip_atomic_store(part + 4 * blockIdx.x, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 4 * blockIdx.x + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 4 * blockIdx.x + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 4 * blockIdx.x + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ticket = __hip_atomic_fetch_add(ws, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = ticket == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // last workgroup: the partials in workgroup order, 4 per thread pass
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 64) {
+    for (int b = 0; b < (int)gridDim.x; b += 64) {
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (b + lane < (int)gridDim.x)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] = __hip_atomic_load(part + 4 * (b + lane) + k, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += wave_sum(v[k]);
+    }
+    if (lane == 0) {
+      out[0] = -a[0] / a[1];
+      loss[0] = out[0];
+      out[1] = a[2] / (float)R;
+      out[2] = a[3] / (float)R;
+      out[3] = a[1];
+      ws[0] = 0;  // re-arm for the next launch (stream-ordered)
+    }
   }
 }
 
@@ -74,9 +117,9 @@ __global__ __launch_bounds__(256) void scst_loss_bwd_kernel(const int64_t* __res
 
 void launch_scst_loss_fwd(const int64_t* seq, const float* lp, int R, int T, const float* sample,
                           const float* greedy, int gdiv, float* reward, float* out, float* loss,
-                          hipStream_t stream) {
-  hipLaunchKernelGGL(scst_loss_fwd_kernel, dim3(1), dim3(SL_THREADS), 0, stream, seq, lp, R, T,
-                     sample, greedy, gdiv, reward, out, loss);
+                          int* ws, hipStream_t stream) {
+  hipLaunchKernelGGL(scst_loss_fwd_kernel, dim3((R + SL_ROWS - 1) / SL_ROWS), dim3(256), 0, stream,
+                     seq, lp, R, T, sample, greedy, gdiv, reward, out, loss, ws);
   post_launch("scst_loss_fwd_kernel", stream);
 }
 

@@ -331,9 +331,12 @@ void launch_featpool_bwd(const FeatPoolArgs& a, const float* dout, const float* 
 
 // loss.hip: SCST reward + reward mask + REINFORCE loss (out = {loss, mean
 // sample, mean greedy, sum mask}), and its backward
+// ws: scst_loss_ws_ints(R) ints, zero before the first launch (the kernel
+// re-arms its ticket)
+int scst_loss_ws_ints(int R);
 void launch_scst_loss_fwd(const int64_t* seq, const float* lp, int R, int T, const float* sample,
                           const float* greedy, int gdiv, float* reward, float* out, float* loss,
-                          hipStream_t stream);
+                          int* ws, hipStream_t stream);
 void launch_scst_loss_bwd(const int64_t* seq, const float* reward, const float* out,
                           const float* dloss, int R, int T, float* dlp, hipStream_t stream);
 
