@@ -170,29 +170,48 @@ class Meteor:
                 pairs.append((i, j, stage))
         return sorted(pairs)
 
-    def _segment(self, h, r):
-        if not h or not r:
-            return 0.0
-        pairs = self._align(h, r)
-        if not pairs:
-            return 0.0
+    def _stats(self, h, r):
+        """Sufficient statistics of one (hypothesis, reference) alignment:
+        (weighted matches, hypothesis words, reference words, chunks, matched
+        pairs) -- what the jar's SCORE line hands to its EVAL aggregate."""
+        pairs = self._align(h, r) if h and r else []
         m = sum(p[2] for p in pairs)
-        P, R = m / len(h), m / len(r)
+        chunks = 0
+        if pairs:
+            chunks = 1
+            for a, b in zip(pairs[:-1], pairs[1:]):
+                if not (b[0] == a[0] + 1 and b[1] == a[1] + 1):
+                    chunks += 1
+        return (m, len(h), len(r), chunks, len(pairs))
+
+    def _score(self, st):
+        m, lh, lr, chunks, npairs = st
+        if m <= 0 or lh <= 0 or lr <= 0:
+            return 0.0
+        P, R = m / lh, m / lr
         fmean = P * R / (self.alpha * P + (1 - self.alpha) * R)
-        chunks = 1
-        for a, b in zip(pairs[:-1], pairs[1:]):
-            if not (b[0] == a[0] + 1 and b[1] == a[1] + 1):
-                chunks += 1
-        frag = chunks / float(len(pairs))
+        frag = chunks / float(npairs)
         pen = self.gamma * frag ** self.beta
         return (1 - pen) * fmean
 
+    def _segment(self, h, r):
+        return self._score(self._stats(h, r))
+
     def compute_score(self, gts, res):
+        """(corpus score, per-segment scores).  Per segment the best reference
+        is kept; the corpus score is computed from the summed statistics of
+        those alignments, as Meteor 1.5's EVAL command aggregates them
+        (coco-caption reports that number, /root/reference/utils.py:114-132),
+        not the mean of the segment scores."""
         if self.java:
             return self._java_score(gts, res)
-        scores = np.array([max(self._segment(res[k][0].split(), r.split()) for r in gts[k])
-                           for k in res])
-        return float(np.mean(scores)), scores
+        seg, tot = [], [0, 0, 0, 0, 0]
+        for k in res:
+            h = res[k][0].split()
+            best = max((self._stats(h, r.split()) for r in gts[k]), key=self._score)
+            seg.append(self._score(best))
+            tot = [a + b for a, b in zip(tot, best)]
+        return self._score(tuple(tot)), np.array(seg)
 
     def _java_score(self, gts, res):  # pragma: no cover - needs java + jar
         proc = subprocess.Popen(['java', '-jar', '-Xmx2G', self.jar, '-', '-', '-stdio', '-l',

@@ -67,3 +67,24 @@ def test_meteor_matches_stems():
     stemmed = m._segment('a man rides horses'.split(), 'a man riding a horse'.split())
     none = m._segment('a man rides horses'.split(), 'a woman cooks food'.split())
     assert exact > stemmed > none > 0
+
+
+def test_meteor_corpus_score_aggregates_statistics():
+    """The corpus METEOR is computed from the summed alignment statistics of
+    each segment's best reference (Meteor 1.5 EVAL), so a long segment weighs
+    more than a short one; it is not the mean of the segment scores.  (Parity
+    with the jar itself is unpinned: no java here.)"""
+    from cst_captioning_amd.eval.metrics import Meteor
+    m = Meteor()
+    gts = {0: ['a man is riding a horse on the beach near the sea'],
+           1: ['a cat', 'a dog sleeps']}
+    res = {0: ['a man is riding a horse on the beach near the sea'], 1: ['the bird']}
+    corpus, seg = m.compute_score(gts, res)
+    assert seg[0] > 0.5 and seg[1] == 0.0
+    # mean of the segments would be ~0.5; the aggregate follows the matched words
+    mean = float(seg.mean())
+    assert corpus > mean + 0.1, (corpus, mean)
+    st = [max((m._stats(res[k][0].split(), r.split()) for r in gts[k]), key=m._score)
+          for k in res]
+    tot = tuple(sum(x) for x in zip(*st))
+    assert abs(corpus - m._score(tot)) < 1e-12
