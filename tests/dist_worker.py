@@ -36,7 +36,51 @@ def build(rank, world, device):
     return opt, model, engine, loader, val
 
 
+def fix_seeds(tr, rank, dev):
+    """Rank-dependent but reproducible sampling: the fused engine reads its
+    (dropout, sampling) seeds and FeatPool's from fixed device tensors; the
+    PyTorch path draws from the global generator, seeded per step by the
+    caller."""
+    from cst_captioning_amd.ops import featpool as fp
+    fixed = torch.tensor([4242 + 17 * rank, 777 + 31 * rank], dtype=torch.int32, device=dev)
+    if tr.engine is not None:
+        tr.engine._rng = lambda d: fixed
+    fp.SEED_SOURCE = lambda d: fixed
+    return fixed
+
+
+def main_scst(out):
+    """SCST data parallelism (CSTCAP_TEST_MODE=scst): rank-local rollouts,
+    greedy baselines and CIDEr-D rewards.  Step 1 (eager: the warm-up of the
+    schedule key), then step 2 (with --cuda_graph 1 on the GPU: captured and
+    replayed).  Saves the parameters before step 2 and the all-reduced mean
+    gradient of step 2, which tests/test_dist.py compares with the mean of
+    the per-shard SCST gradients computed in one process."""
+    ctx = init_distributed()
+    opt, model, engine, loader, val = build(ctx.rank, ctx.world_size, ctx.device)
+    tr = Trainer(opt, model, loader, val, ctx, engine)
+    tr.rl_training = True
+    fix_seeds(tr, ctx.rank, ctx.device)
+    torch.manual_seed(555 + ctx.rank)
+    tr.train_step(loader.get_batch(), 0)
+    p1 = tr.bucket.data.detach().cpu().clone()
+    torch.manual_seed(999 + ctx.rank)
+    out_step = tr.train_step(loader.get_batch(), 0)
+    grad = (tr.bucket.grad * tr.optimizer.grad_scale).detach().cpu().clone()
+    flat = tr.bucket.data.detach().cpu().clone()
+    allp = ctx.all_gather_object(flat)
+    same = all(torch.equal(allp[0], q) for q in allp)
+    rewards = ctx.all_gather_object(out_step['reward'].detach().cpu().clone())
+    graphed = tr._graph is not None
+    if ctx.is_main:
+        torch.save({'p1': p1, 'grad': grad, 'same_after_steps': same, 'rewards': rewards,
+                    'graphed': graphed, 'world': ctx.world_size}, out)
+    ctx.destroy()
+
+
 def main(out):
+    if os.environ.get('CSTCAP_TEST_MODE') == 'scst':
+        return main_scst(out)
     ctx = init_distributed()
     opt, model, engine, loader, val = build(ctx.rank, ctx.world_size, ctx.device)
     tr = Trainer(opt, model, loader, val, ctx, engine)  # C1 broadcast happens here

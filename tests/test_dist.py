@@ -29,8 +29,9 @@ def _free_port():
     return p
 
 
-def _run(world, out, wire='fp32', update='allreduce'):
+def _run(world, out, wire='fp32', update='allreduce', mode='xe'):
     env = dict(os.environ)
+    env['CSTCAP_TEST_MODE'] = mode
     env['CSTCAP_TEST_WIRE'] = wire
     env['CSTCAP_TEST_DPUPDATE'] = update
     env['PYTHONPATH'] = ROOT + os.pathsep + env.get('PYTHONPATH', '')
@@ -84,6 +85,52 @@ def _reference_grad(world, with_abs=False):
     if with_abs:
         return model, grads, mags
     return model, grads
+
+
+def reference_scst_grad(world, p1, dev):
+    """Mean over shards k of the SCST gradient of rank k's second batch at
+    the parameters p1, one process, with rank k's sampling seeds
+    (dist_worker.fix_seeds) -- what the all-reduce must reproduce."""
+    sys.path.insert(0, HERE)
+    import dist_worker as W
+    from cst_captioning_amd.parallel import DistContext
+    from cst_captioning_amd.train.trainer import Trainer
+    grads = None
+    for k in range(world):
+        opt, model, engine, loader, _ = W.build(k, world, dev)
+        tr = Trainer(opt, model, loader, None, DistContext(device=dev), engine)
+        n = min(tr.bucket.data.numel(), p1.numel())
+        with torch.no_grad():
+            tr.bucket.data[:n].copy_(p1[:n].to(dev))
+        if engine is not None:
+            engine.refresh_weights()
+        W.fix_seeds(tr, k, dev)
+        tr.rl_training = True
+        loader.get_batch()  # the worker's first (warm-up) batch
+        data = loader.get_batch()
+        mixer_from, scb = tr._schedules(0)
+        torch.manual_seed(999 + k)
+        tr._forward_backward(data, mixer_from, scb)
+        g = tr.bucket.grad.detach().clone()[:n] / world
+        grads = g if grads is None else grads + g
+    return grads
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_scst_step_allreduce_matches_per_shard_mean(tmp_path, world):
+    """The headline recipe under data parallelism: every rank samples its own
+    rollout, decodes its greedy baseline and scores both with CIDEr-D on its
+    own shard; the all-reduced gradient equals the mean of the per-shard SCST
+    gradients (reference train.py:167-218 / utils.py:169-226 per shard), and
+    the ranks stay identical after the update."""
+    r = _run(world, str(tmp_path / ('scst%d.pt' % world)), mode='scst')
+    ref = reference_scst_grad(world, r['p1'], torch.device('cpu'))
+    n = ref.numel()
+    torch.testing.assert_close(r['grad'][:n], ref, rtol=1e-4, atol=1e-7)
+    assert r['same_after_steps']
+    assert ref.abs().sum() > 0
+    rw = r['rewards']
+    assert len(rw) == world and not all(torch.equal(rw[0], x) for x in rw[1:])
 
 
 def test_broadcast_and_allreduce(runs):

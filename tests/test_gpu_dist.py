@@ -26,9 +26,9 @@ def _free_port():
     return p
 
 
-def _run(world, out, graph, wire='fp32', update='allreduce'):
+def _run(world, out, graph, wire='fp32', update='allreduce', mode='xe'):
     env = dict(os.environ, CSTCAP_TEST_GRAPH=str(graph), CSTCAP_TEST_WIRE=wire,
-               CSTCAP_TEST_DPUPDATE=update)
+               CSTCAP_TEST_DPUPDATE=update, CSTCAP_TEST_MODE=mode)
     env.update(PYTHONPATH=ROOT + os.pathsep + env.get('PYTHONPATH', ''), CSTCAP_SHARE_GPU='1',
                CSTCAP_DIST_BACKEND='gloo', CSTCAP_TEST_IMPL='hip', OMP_NUM_THREADS='4',
                PYTHONFAULTHANDLER='1')
@@ -92,3 +92,24 @@ def test_engine_dp_sharded_update_matches_allreduce(tmp_path):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-10)
     assert b['same_after_steps'] and b['nan_skip_all']
     assert b['steps_done'] == a['steps_done'] and b['skipped'] == a['skipped'] == 1
+
+
+def test_engine_dp_scst_step_matches_per_shard_mean(tmp_path):
+    """The shipped headline step under data parallelism, on the GPU: fused
+    engine, SCST with rank-local rollouts, greedy baselines (side stream) and
+    on-GPU CIDEr-D rewards, the step captured and replayed as HIP graphs
+    around the eager bucket all-reduce.  The reduced gradient of the replayed
+    step equals the mean of the per-shard SCST gradients computed eagerly in
+    one process with each rank's sampling seeds (1e-4 relative), and the
+    ranks stay identical."""
+    os.environ['CSTCAP_TEST_IMPL'] = 'hip'
+    r = _run(2, str(tmp_path / 'scst.pt'), 1, mode='scst')
+    assert r['graphed'], 'the second step must be a replayed graph'
+    sys.path.insert(0, HERE)
+    from test_dist import reference_scst_grad
+    ref = reference_scst_grad(2, r['p1'], torch.device('cuda', 0)).cpu()
+    n = ref.numel()
+    err = ((r['grad'][:n] - ref).norm() / ref.norm()).item()
+    assert err < 1e-4, err
+    assert r['same_after_steps']
+    assert not torch.equal(r['rewards'][0], r['rewards'][1])
