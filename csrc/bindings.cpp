@@ -55,11 +55,9 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
                                          at::Tensor blog, at::Tensor whh, at::Tensor vgate,
                                          int64_t vdiv, at::Tensor tgt, at::Tensor eoff,
                                          int64_t save, int64_t mode, int64_t step, at::Tensor rng,
-                                         int64_t fused, at::Tensor ptab, at::Tensor c_prev,
-                                         double drop_p, int64_t cell, int64_t eos,
-                                         at::Tensor unfinished, double ss_prob);
-int64_t decode_sync_errors(bool reset);
-void set_fused_decode_mode(int64_t on);
+                                         at::Tensor ptab, at::Tensor c_prev, double drop_p,
+                                         int64_t cell, int64_t eos, at::Tensor unfinished,
+                                         double ss_prob);
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);
@@ -146,8 +144,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("token_group_sum", &cst::token_group_sum);
   m.def("vocab_select", &cst::vocab_select);
   m.def("decode_step_test", &cst::decode_step_test);
-  m.def("decode_sync_errors", &cst::decode_sync_errors, py::arg("reset") = false);
-  m.def("set_fused_decode", &cst::set_fused_decode_mode);
   m.def("att_mfma_fwd", &cst::att_mfma_fwd);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);

@@ -117,33 +117,6 @@ static DeviceAux& device_aux(int dev_index) {
   return *it->second;
 }
 
-// Timeout counter of the fused decode step's in-launch waits (vocab.hip): one
-// persistent int per device, allocated outside graph capture (the first
-// decoder_forward of a device runs eagerly before any capture).  A non-zero
-// value means a wait gave up: decode_sync_errors() reports it.
-static std::map<int, at::Tensor>& decode_err_bufs() {
-  static std::map<int, at::Tensor> m;
-  return m;
-}
-static int* decode_err_ptr(const at::Device& dev) {
-  auto& m = decode_err_bufs();
-  auto it = m.find((int)dev.index());
-  if (it == m.end())
-    it = m.emplace((int)dev.index(),
-                   at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev)))
-             .first;
-  return it->second.data_ptr<int>();
-}
-int64_t decode_sync_errors(bool reset) {
-  int64_t n = 0;
-  for (auto& kv : decode_err_bufs()) {
-    n += kv.second.item<int>();
-    if (reset) kv.second.zero_();
-  }
-  return n;
-}
-void set_fused_decode_mode(int64_t on) { set_fused_decode((int)on); }
-
 // Read-only zeros of at least n elements (initial decoder states): one
 // persistent buffer per (device, dtype), so a decode does not launch a fill
 // kernel per call.  Grown only outside graph capture; replaced buffers stay
@@ -247,16 +220,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   at::Tensor lse = at::empty({n_steps, R}, f32);
   at::Tensor part =
       at::empty({(int64_t)vocab_part_slots((int)V) * R * vocab_partial_bytes() / 4}, f32);
-  // one zero-filled int area: the end-of-sequence flags of every step, then
-  // (fused decode step) each step's arrival counters / ready flags
+  // the end-of-sequence flags of every step (zero-filled)
   const int64_t n_cnt = (T + 1) * combine_count_ints_per_step();
-  const int64_t n_sync = fused_sync_ints((int)R);
-  const bool fused_ok = fused_decode_enabled();
-  at::Tensor flags_area = at::zeros({n_cnt + (fused_ok ? n_steps * n_sync : 0)},
-                                    at::TensorOptions().dtype(at::kInt).device(dev));
-  at::Tensor counts = flags_area.narrow(0, 0, n_cnt);
-  at::Tensor tok32 = fused_ok ? at::empty({R}, at::TensorOptions().dtype(at::kInt).device(dev))
-                              : at::Tensor();
+  at::Tensor counts = at::zeros({n_cnt}, at::TensorOptions().dtype(at::kInt).device(dev));
   at::Tensor unfinished =
       use_unfinished ? at::ones({R}, at::TensorOptions().dtype(at::kByte).device(dev))
                      : at::Tensor();
@@ -444,31 +410,13 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                        save ? q_next.data_ptr<float>() : nullptr, att_ep.data_ptr<float>(),
                        att_cnt.data_ptr<int>()};
     const bool q_tiles = has_att && !att_mfma;  // W_q tiles in the recurrent GEMM
-    // fused decode step (vocab.hip): the combine and the next step's cell run
-    // inside this launch; the last step (no recurrent part) keeps the combine
-    const bool fuse = fused_ok && next && !q_tiles;
-    FuseArgs fz{};
-    if (fuse) {
-      fz = FuseArgs{flags_area.data_ptr<int>() + n_cnt + t * n_sync, tok32.data_ptr<int>(),
-                    decode_err_ptr(dev),
-                    lse[t].data_ptr<float>(), seq.data_ptr<int64_t>() + t, T - 1,
-                    g_sel.data_ptr<float>() + t, T - 1,
-                    want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
-                    (float)ss_prob, use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
-                    use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr,
-                    ptab.data_ptr<float>(), c_buf(0, t), c_buf(0, t + 1), h_buf(0, t + 1),
-                    hd_buf(0, t + 1), (int)H, gates_buf(0, t + 1), (float)drop_p, key(0, t + 1),
-                    (int)cell,
-                    att_mfma ? reinterpret_cast<const uint16_t*>(vg16.data_ptr()) : nullptr};
-    }
     const int n_vt = launch_vocab_lstm_fwd(
         vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
         save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl, part.data_ptr(),
         tgt, L, vflags, inv_temp, RNG, (int)t, h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
         next ? pre.data_ptr<float>() : nullptr, st, q_tiles ? (int)A : 0,
         q_tiles && next ? q_next.data_ptr<float>() : nullptr,
-        exp_t ? lse[t - 1].data_ptr<float>() : nullptr, att_mfma && next ? &am : nullptr,
-        fuse ? &fz : nullptr);
+        exp_t ? lse[t - 1].data_ptr<float>() : nullptr, att_mfma && next ? &am : nullptr);
     if (q_tiles && next)
       launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), q_next.data_ptr<float>(),
                      nullptr, a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv,
@@ -483,8 +431,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                       (float)drop_p, key(0, t + 1), (int)cell,
                       att_mfma ? reinterpret_cast<const uint16_t*>(vg16.data_ptr()) : nullptr};
     }
-    if (!fuse)
-      launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
+    launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                            choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
                            choose ? g_sel.data_ptr<float>() + t : nullptr, T - 1,
                            want_xe ? g_xe.data_ptr<float>() + t : nullptr, T, tgt, L, mode,
@@ -1619,9 +1566,7 @@ std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor 
   return {tok.view({R}), lse};
 }
 
-// One decode step for tests of the two launch forms: the decode launch +
-// vocab_combine_kernel (fused = 0) or the fused decode step (fused = 1, needs
-// the recurrent part and the cell).  save: 0 none, 1 fp16 logits, 2 exp store
+// One decode step for tests: the decode launch + vocab_combine_kernel.  save: 0 none, 1 fp16 logits, 2 exp store
 // (eoff given).  Cell (ptab defined): the next step's cell from c_prev and
 // the chosen tokens (dropout drop_p, step key `step + 1`).  eos: 0 no
 // end-of-sequence rules; 1 / 2 the all-rows-ended counter with a live / dead
@@ -1632,9 +1577,9 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
                                          at::Tensor blog, at::Tensor whh, at::Tensor vgate,
                                          int64_t vdiv, at::Tensor tgt, at::Tensor eoff,
                                          int64_t save, int64_t mode, int64_t step, at::Tensor rng,
-                                         int64_t fused, at::Tensor ptab, at::Tensor c_prev,
-                                         double drop_p, int64_t cell, int64_t eos,
-                                         at::Tensor unfinished, double ss_prob) {
+                                         at::Tensor ptab, at::Tensor c_prev, double drop_p,
+                                         int64_t cell, int64_t eos, at::Tensor unfinished,
+                                         double ss_prob) {
   check_cuda(hd, "hd");
   check_cuda(wlog, "wlog");
   const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);
@@ -1663,7 +1608,6 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
                     c_prev.scalar_type() == at::kFloat && c_prev.numel() == R * H,
                 "ptab (V, 4H) / c_prev (R, H) fp32");
   }
-  TORCH_CHECK(!fused || do_cell, "the fused decode step needs the cell");
   const bool has_unf = unfinished.defined() && unfinished.numel() > 0;
   if (has_unf)
     TORCH_CHECK(unfinished.is_cuda() && unfinished.scalar_type() == at::kByte &&
@@ -1689,27 +1633,14 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
   }
   // counts: steps 0..2 of the end-of-sequence flags; this step is count step 2
   const int cps = combine_count_ints_per_step();
-  at::Tensor flags_area = at::zeros({3 * cps + fused_sync_ints((int)R)},
-                                    at::TensorOptions().dtype(at::kInt).device(dev));
-  if (eos == 1) flags_area.narrow(0, cps, 1).fill_(1);  // a live row at the previous step
-  at::Tensor counts = flags_area.narrow(0, 0, 3 * cps);
+  at::Tensor counts = at::zeros({3 * cps}, at::TensorOptions().dtype(at::kInt).device(dev));
+  if (eos == 1) counts.narrow(0, cps, 1).fill_(1);  // a live row at the previous step
   int* CNT = eos ? counts.data_ptr<int>() : nullptr;
-  at::Tensor tok32 = at::empty({R}, at::TensorOptions().dtype(at::kInt).device(dev));
   hipStream_t st = cur_stream();
   const int flags = (mode == SEL_SAMPLE_H || mode == SEL_SS_H ? 1 : 0) |
                     (mode == SEL_GREEDY_H ? 2 : 0) | (save == 2 ? 16 : 0);
   const int64_t* TG = has_tgt ? tgt.data_ptr<int64_t>() : nullptr;
   uint8_t* UNF = has_unf ? unfinished.data_ptr<uint8_t>() : nullptr;
-  FuseArgs fz{};
-  if (fused)
-    fz = FuseArgs{flags_area.data_ptr<int>() + 3 * cps, tok32.data_ptr<int>(), decode_err_ptr(dev),
-                  lse.data_ptr<float>(), tok.data_ptr<int64_t>(), 1, gsel.data_ptr<float>(), 1,
-                  has_tgt ? gxe.data_ptr<float>() : nullptr, 1, TG, 1, (int)mode, (float)ss_prob,
-                  CNT, 2, UNF, ptab.data_ptr<float>(), c_prev.data_ptr<float>(),
-                  c_out.data_ptr<float>(), reinterpret_cast<uint16_t*>(h_out.data_ptr()),
-                  reinterpret_cast<uint16_t*>(hdrop.data_ptr()), (int)H,
-                  reinterpret_cast<uint16_t*>(gates.data_ptr()), (float)drop_p, (int)step + 1,
-                  (int)cell, nullptr};
   const int n = launch_vocab_lstm_fwd(
       reinterpret_cast<const uint16_t*>(hd.data_ptr()), (int)H, (int)R, (int)H,
       reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(), (int)V,
@@ -1718,21 +1649,18 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
       lstm ? reinterpret_cast<const uint16_t*>(h.data_ptr()) : nullptr,
       lstm ? reinterpret_cast<const uint16_t*>(whh.data_ptr()) : nullptr,
       has_vg ? vgate.data_ptr<float>() : nullptr, (int)vdiv, lstm ? pre.data_ptr<float>() : nullptr,
-      st, 0, nullptr, save == 2 ? eoff.data_ptr<float>() : nullptr, nullptr,
-      fused ? &fz : nullptr);
-  if (!fused) {
-    CellLaunch cl{};
-    if (do_cell)
-      cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_prev.data_ptr<float>(),
-                      c_out.data_ptr<float>(), reinterpret_cast<uint16_t*>(h_out.data_ptr()),
-                      reinterpret_cast<uint16_t*>(hdrop.data_ptr()), (int)H,
-                      reinterpret_cast<uint16_t*>(gates.data_ptr()), (int)H, (float)drop_p,
-                      (int)step + 1, (int)cell, nullptr};
-    launch_vocab_combine(part.data_ptr(), n, (int)R, lse.data_ptr<float>(), tok.data_ptr<int64_t>(),
-                         1, gsel.data_ptr<float>(), 1, has_tgt ? gxe.data_ptr<float>() : nullptr, 1,
-                         TG, 1, (int)mode, (float)ss_prob, rng_ptr(rng), (int)step, CNT, 2, UNF, st,
-                         do_cell ? &cl : nullptr);
-  }
+      st, 0, nullptr, save == 2 ? eoff.data_ptr<float>() : nullptr, nullptr);
+  CellLaunch cl{};
+  if (do_cell)
+    cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_prev.data_ptr<float>(),
+                    c_out.data_ptr<float>(), reinterpret_cast<uint16_t*>(h_out.data_ptr()),
+                    reinterpret_cast<uint16_t*>(hdrop.data_ptr()), (int)H,
+                    reinterpret_cast<uint16_t*>(gates.data_ptr()), (int)H, (float)drop_p,
+                    (int)step + 1, (int)cell, nullptr};
+  launch_vocab_combine(part.data_ptr(), n, (int)R, lse.data_ptr<float>(), tok.data_ptr<int64_t>(),
+                       1, gsel.data_ptr<float>(), 1, has_tgt ? gxe.data_ptr<float>() : nullptr, 1,
+                       TG, 1, (int)mode, (float)ss_prob, rng_ptr(rng), (int)step, CNT, 2, UNF, st,
+                       do_cell ? &cl : nullptr);
   return {lse, tok, gsel, gxe, saved, pre, at::full({1}, n, at::TensorOptions().dtype(at::kLong)),
           h_out, c_out, hdrop, gates, counts};
 }

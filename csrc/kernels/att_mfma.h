@@ -246,22 +246,12 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
       uint16_t* dst = g.vg_out + (int64_t)(row0 + r) * G4 + n0 + 4 * hh;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint64_t pk =
-            (uint64_t)((uint32_t)f2bf(o[4 * j]) | ((uint32_t)f2bf(o[4 * j + 1]) << 16)) |
-            ((uint64_t)((uint32_t)f2bf(o[4 * j + 2]) | ((uint32_t)f2bf(o[4 * j + 3]) << 16))
-             << 32);
-        // write-through (sc1): in the fused decode step the recurrent tiles of
-        // this same launch read these rows (sc1 loads) once `done` counts
-        // the video
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(dst + 8 * j), pk, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(o[4 * j]) | ((uint32_t)f2bf(o[4 * j + 1]) << 16);
+        pk.y = (uint32_t)f2bf(o[4 * j + 2]) | ((uint32_t)f2bf(o[4 * j + 3]) << 16);
+        *reinterpret_cast<uint2*>(dst + 8 * j) = pk;
       }
     }
-  }
-  if (g.done != nullptr) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(g.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

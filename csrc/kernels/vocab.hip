@@ -78,13 +78,8 @@ struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS (exp_stage_off
 #define VOCAB_TR_ARGS \
   hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, rng, step, eoff
 
-// FZ (fused decode step): the partials are stored write-through and wave 0
-// then arrives on the row tile's counter (arrive, one line per 64-row tile);
-// the merge happens in a recurrent tile of the same launch (fz_merge_rows).
-template <int BN, int STAGES, bool FZ = false>
-__device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARAMS,
-                                               int* arrive = nullptr) {
-  static_assert(!FZ || BN == 64, "fused arrival: the partials are stored by wave 0");
+template <int BN, int STAGES>
+__device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARAMS) {
   using TL = Tile<VT_V, BN, STAGES>;  // M = vocab, N = caption rows
   constexpr int TM = TL::TM, TN = TL::TN;
   static_assert(TM == 2, "lane owns 32 vocab entries per row");
@@ -336,25 +331,7 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       p.xidx = a.xidx;
       p.xtgt = a.xt;
       p.pad = 0.f;
-      if constexpr (FZ) {
-        const rsrc_t rp = make_rsrc(part, (int64_t)n_vt * R * (int)sizeof(VocabPartial));
-        const int off = (vt * R + r) * (int)sizeof(VocabPartial);
-        st16_sc1(rp, off, u32x4v{__float_as_uint(p.m), __float_as_uint(p.s),
-                                 __float_as_uint(p.zval), __float_as_uint(p.zlogit)});
-        st16_sc1(rp, off + 16, u32x4v{(uint32_t)p.zidx, (uint32_t)p.xidx,
-                                      __float_as_uint(p.xtgt), 0u});
-      } else {
-        part[(int64_t)vt * R + r] = p;
-      }
-    }
-  }
-  if constexpr (FZ) {
-    // wave 0 stored every partial of the tile: drain them, then one lane arrives
-    if (threadIdx.x < 64) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(arrive + rt * FZ_LINE, 1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+      part[(int64_t)vt * R + r] = p;
     }
   }
   if (logits16 != nullptr && !(flags & VF_SAVE_F32)) {
@@ -718,245 +695,6 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   }
 }
 
-// -------------------------------------------------------------------------------
-// Fused decode step (FuseArgs, launchers.h): the combine folded into the decode
-// launch.  Block order: [attention workgroups] [vocabulary tiles, padded to a
-// multiple of 8] [recurrent tiles].  Roles:
-//   vocabulary tile (vocab_tr_block<FZ>): partials stored write-through; wave
-//     0 drains them and arrives on its 64-row tile's counter;
-//   merging recurrent tile: the recurrent tiles of column tiles 0 / 1 of the
-//     128-row group g (the first 2 x groups recurrent block ids) merge 64-row
-//     tile 2g / 2g + 1 once its n_vt arrivals are in, after their own GEMM:
-//     per row the n_vt partials (write-through loads, 4 lanes per row), the
-//     token selection (finish_row, the combine's code), the int32 token copy
-//     (write-through), then the row tile's ready flag;
-//   every recurrent tile: its 128 x 64 accumulator tile (16 hidden units x 4
-//     packed gates) stays in LDS; once the ready flags of its rows are set it
-//     gathers the chosen tokens' rows of the gate table P and applies the
-//     cell -- what vocab_combine_kernel's cell epilogue did, from
-//     pre-activations that never leave the CU (no R x 4H fp32 round trip, no
-//     combine launch, one graph node per decode step).
-// Hand-offs (all inside the launch): write-through (sc1) stores drained by the
-// storing wave's s_waitcnt vmcnt(0) (plus a workgroup barrier where several
-// waves stored) before ONE lane's agent-scope counter add / flag store;
-// write-through loads after the poll by the polling lane, and by the other
-// waves after a barrier.  Everything else a recurrent tile reads was written by
-// earlier launches.
-// Forward progress: a wait only ever waits on workgroups with LOWER block ids
-// (vocabulary tiles for a merge; the merging tiles -- the first recurrent
-// tiles -- and the attention workgroups for a cell), and those wait on nothing
-// dispatched after them; the waiting workgroups (the recurrent tiles, 320 at
-// the headline shape) are far fewer than the chip's resident slots (3 per
-// CU), so the ones they wait on always find a slot.  Waits are bounded anyway
-// (FZ_SPIN_MAX polls, ~0.3 s): a timeout is counted in FuseArgs::err and the
-// kernel continues on clamped indices instead of hanging the GPU.
-constexpr int FZ_SPIN_MAX = 1 << 18;
-int fused_sync_ints(int R) { return (2 * ((R + 63) / 64) + 2) * FZ_LINE; }
-
-__device__ __forceinline__ void fz_wait_geq(const int* p, int target, int* err) {
-  for (int i = 0; i < FZ_SPIN_MAX; ++i) {
-    if (ld_sc1(p) >= target) return;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (err != nullptr) atomicAdd(err, 1);
-}
-
-// merge of 64-row tile v (256 threads, 4 lanes per row; lane q merges vocab
-// tiles q, q + 4, ...).  s_nz: one int of LDS scratch.
-__device__ __forceinline__ void fz_merge_rows(int v, const FuseArgs& fz,
-                                           const VocabPartial* __restrict__ part, int n_vt, int R,
-                                           int V, const uint32_t* __restrict__ rng, int step,
-                                           int n_vrt, int* s_nz) {
-  int* sync = fz.sync;
-  if (threadIdx.x == 0) {
-    *s_nz = 0;
-    fz_wait_geq(sync + v * FZ_LINE, n_vt, fz.err);
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, row_l = threadIdx.x >> 2, q = threadIdx.x & 3;
-  const int r = v * 64 + row_l;
-  const bool valid = r < R;
-  const int rr = min(r, R - 1);
-  // the selecting lane's other inputs, requested with the partials
-  int64_t gt_tok = 0;
-  bool unf_pre = true;
-  if (valid && q == 0) {
-    gt_tok = fz.gt ? fz.gt[(int64_t)r * fz.gt_stride] : 0;
-    unf_pre = fz.unfinished == nullptr || fz.unfinished[r] != 0;
-  }
-  // "some row emitted a non-EOS token at the previous step" (flags written by
-  // the previous launch): lanes 0..31 of every wave read the 32 slots
-  int nzp = 0;
-  if (fz.counts != nullptr && fz.count_step > 1 && lane < CMB_CNT_SLOTS)
-    nzp = fz.counts[((fz.count_step - 1) * CMB_CNT_SLOTS + lane) * CMB_CNT_STRIDE];
-  const bool dead_pre = fz.counts != nullptr && fz.count_step > 1 && __ballot(nzp != 0) == 0;
-  const rsrc_t rp = make_rsrc(part, (int64_t)n_vt * R * (int)sizeof(VocabPartial));
-  RowStat a = {-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff};
-  constexpr int NB = 8;  // partials per lane in flight
-  for (int t0 = q; t0 < n_vt; t0 += 4 * NB) {
-    u32x4v lo[NB], hi[NB];
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      const int off = (min(t0 + 4 * k, n_vt - 1) * R + rr) * (int)sizeof(VocabPartial);
-      lo[k] = ld16_sc1(rp, off);
-      hi[k] = ld16_sc1(rp, off + 16);
-    }
-#pragma unroll
-    for (int k = 0; k < NB; ++k)
-      if (t0 + 4 * k < n_vt)
-        merge_stat(a, __uint_as_float(lo[k].x), __uint_as_float(lo[k].y),
-                   __uint_as_float(lo[k].z), __uint_as_float(lo[k].w), (int)hi[k].x,
-                   __uint_as_float(lo[k].x), (int)hi[k].y, __uint_as_float(hi[k].z));
-  }
-#pragma unroll
-  for (int o = 1; o < 4; o <<= 1)
-    merge_stat(a, __shfl_xor(a.m, o, 64), __shfl_xor(a.s, o, 64), __shfl_xor(a.zv, o, 64),
-               __shfl_xor(a.zl, o, 64), __shfl_xor(a.zi, o, 64), __shfl_xor(a.xm, o, 64),
-               __shfl_xor(a.xi, o, 64), __shfl_xor(a.xt, o, 64));
-  if (valid && q == 0) {
-    const RowSel o{fz.lse_out, fz.g_xe,    fz.gxe_stride, fz.tok_out, fz.tok_stride, fz.g_sel,
-                   fz.gsel_stride, fz.mode, fz.ss_prob, rng, step, fz.unfinished, V};
-    const int tok = finish_row(a, r, o, gt_tok, dead_pre, unf_pre);
-    if (fz.counts != nullptr && tok != 0) atomicAdd(s_nz, 1);
-    __hip_atomic_store(fz.tok32 + r, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(sync + (n_vrt + v) * FZ_LINE, 1, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    // end-of-sequence flag for the next step (read by the next launch)
-    if (fz.counts != nullptr && *s_nz > 0)
-      fz.counts[(fz.count_step * CMB_CNT_SLOTS + v % CMB_CNT_SLOTS) * CMB_CNT_STRIDE] = 1;
-  }
-}
-
-// Recurrent tile j of the fused launch (see above): pre_{t+1} = h_t W_hh^T
-// (+ vgate) on MFMA, [merge of one 64-row tile], then the cell of step t+1.
-// n_att_videos: attention videos whose completion the cell waits for (0: no
-// attention; their bf16 per-row video gates fz.vg16 are added).
-template <class LT>
-__device__ __forceinline__ void fz_lstm_block(int j, const uint16_t* __restrict__ h, int R, int H,
-                                              const uint16_t* __restrict__ whh,
-                                              const float* __restrict__ vgate, int vdiv, char* lds,
-                                              const FuseArgs& fz,
-                                              const VocabPartial* __restrict__ part, int n_vt,
-                                              int V, const uint32_t* __restrict__ rng, int step,
-                                              int n_att_videos) {
-  static_assert(LT::BM == 128 && LT::BN == 64, "recurrent tile: 128 rows x 16 units");
-  const int n_nt = 4 * H / LT::BN, n_rt = (R + LT::BM - 1) / LT::BM, n_vrt = (R + 63) / 64;
-  int nt, rtl;
-  if (j < 2 * n_rt) {  // the merging tiles first, spread over the XCDs
-    nt = j & 1;
-    rtl = j >> 1;
-  } else {
-    const int b = xcd_remap_g(j - 2 * n_rt, (n_nt - 2) * n_rt);
-    nt = 2 + b / n_rt;
-    rtl = b % n_rt;
-  }
-  const int r0 = rtl * LT::BM, n0 = nt * LT::BN;
-  const int nk = H / 64;
-  f32x16 acc[LT::TM][LT::TN];
-  {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    DmaSrc<LT::BM / 32> a;
-    DmaSrc<LT::BN / 32> bsrc;
-    a.r0 = a.r1 = make_rsrc(h, (int64_t)R * H * 2);
-    a.ksplit = nk;
-#pragma unroll
-    for (int i = 0; i < LT::BM / 32; ++i) {
-      const int row = dma_row(w, i, lane);
-      a.voff0[i] = min(r0 + row, R - 1) * H * 2 + dma_chunk(row, lane) * 16;
-      a.voff1[i] = a.voff0[i];
-    }
-    bsrc.r0 = bsrc.r1 = make_rsrc(whh, (int64_t)4 * H * H * 2);
-    bsrc.ksplit = nk;
-#pragma unroll
-    for (int i = 0; i < LT::BN / 32; ++i) {
-      const int row = dma_row(w, i, lane);
-      bsrc.voff0[i] = (n0 + row) * H * 2 + dma_chunk(row, lane) * 16;
-      bsrc.voff1[i] = bsrc.voff0[i];
-    }
-    gemm_nt_mainloop<LT>(nk, a, bsrc, lds, acc);
-  }
-  float* C = reinterpret_cast<float*>(lds);
-  store_acc_to_lds<LT>(acc, C, [](int) { return 0.f; });
-  int* s_nz = reinterpret_cast<int*>(lds + LT::C_BYTES);
-  __syncthreads();
-  const int vm = 2 * rtl + nt;
-  if (nt < 2 && vm < n_vrt) fz_merge_rows(vm, fz, part, n_vt, R, V, rng, step, n_vrt, s_nz);
-
-  // cell: thread (rg, u) owns hidden unit n0 / 4 + u of rows r0 + rg + 16 i
-  const int u = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const int unit = n0 / 4 + u;
-  constexpr int NR = LT::BM / 16;
-  // token-independent operands first
-  float cp[NR];
-  float4 vg[NR];
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int r = min(r0 + rg + 16 * i, R - 1);
-    cp[i] = fz.c_prev[(int64_t)r * H + unit];
-    vg[i] = vgate != nullptr
-                ? *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * (4 * H) + n0 + 4 * u)
-                : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  if (threadIdx.x == 0) {
-    int* rdy = fz.sync + n_vrt * FZ_LINE;
-    fz_wait_geq(rdy + (2 * rtl) * FZ_LINE, 1, fz.err);
-    if (2 * rtl + 1 < n_vrt) fz_wait_geq(rdy + (2 * rtl + 1) * FZ_LINE, 1, fz.err);
-    if (n_att_videos > 0) fz_wait_geq(fz.sync + 2 * n_vrt * FZ_LINE, n_att_videos, fz.err);
-  }
-  __syncthreads();
-  int tk[NR];
-#pragma unroll
-  for (int i = 0; i < NR; ++i)
-    tk[i] = min(max(ld_sc1(fz.tok32 + min(r0 + rg + 16 * i, R - 1)), 0), V - 1);
-  float4 pt[NR];
-  uint64_t vq[NR];
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    pt[i] = *reinterpret_cast<const float4*>(fz.ptab + (int64_t)tk[i] * (4 * H) + n0 + 4 * u);
-    vq[i] = 0;
-    if (n_att_videos > 0)
-      vq[i] = __hip_atomic_load(
-          reinterpret_cast<const uint64_t*>(fz.vg16 + (int64_t)min(r0 + rg + 16 * i, R - 1) * (4 * H) +
-                                            n0 + 4 * u),
-          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const float inv_keep = fz.drop_p > 0.f ? 1.f / (1.f - fz.drop_p) : 1.f;
-  const uint32_t dseed = rng_seed(rng, RNG_SLOT_DROPOUT);
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int row = rg + 16 * i, r = r0 + row;
-    if (r >= R) continue;
-    const float4 x = *reinterpret_cast<const float4*>(C + row * LT::CSTRIDE + 4 * u);
-    // the combine's order: (x + vgate) [+ video gates] + P[token]
-    float4 p = make_float4(x.x + vg[i].x, x.y + vg[i].y, x.z + vg[i].z, x.w + vg[i].w);
-    if (n_att_videos > 0) {
-      p.x += bf2f((uint16_t)(vq[i] & 0xffff));
-      p.y += bf2f((uint16_t)((vq[i] >> 16) & 0xffff));
-      p.z += bf2f((uint16_t)((vq[i] >> 32) & 0xffff));
-      p.w += bf2f((uint16_t)(vq[i] >> 48));
-    }
-    const CellFwd cf = cell_fwd(fz.cell, p.x + pt[i].x, p.y + pt[i].y, p.z + pt[i].z,
-                                p.w + pt[i].w, cp[i]);
-    const int64_t o = (int64_t)r * H + unit;
-    fz.c_out[o] = cf.c;
-    fz.h_out[o] = f2bf(cf.h);
-    if (fz.hdrop_out) {
-      const bool keep = fz.drop_p <= 0.f || dropout_keep(dseed, fz.cstep, r, unit, fz.drop_p);
-      fz.hdrop_out[(int64_t)r * fz.ldh + unit] = f2bf(keep ? cf.h * inv_keep : 0.f);
-    }
-    if (fz.gates_out) {
-      uint2 pk;
-      pk.x = (uint32_t)f2bf(cf.s0) | ((uint32_t)f2bf(cf.s1) << 16);
-      pk.y = (uint32_t)f2bf(cf.s2) | ((uint32_t)f2bf(cf.s3) << 16);
-      *reinterpret_cast<uint2*>(fz.gates_out + (int64_t)r * 4 * H + n0 + 4 * u) = pk;
-    }
-  }
-}
-
 // One launch = vocab projection of step t (rows hd_t) + the recurrent GEMM of
 // step t+1 (pre_{t+1} = h_t W_hh^T + vgate, lstm_gemm.h).  The two are
 // independent, so the LSTM's latency-bound GEMM fills the CUs the vocab
@@ -967,11 +705,11 @@ __device__ __forceinline__ void fz_lstm_block(int j, const uint16_t* __restrict_
 // the MFMA temporal attention of step t+1, one per video (att_mfma.h): they
 // depend only on h_t too, and are dispatched first, so they finish under the
 // vocabulary tiles.
-template <int BN, int STAGES, int OCC, class LT, int AV, bool FZ>
+template <int BN, int STAGES, int OCC, class LT, int AV>
 __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
     VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
     const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad, int NQ,
-    float* __restrict__ q_out, AttMfmaArgs att, int n_att, FuseArgs fz) {
+    float* __restrict__ q_out, AttMfmaArgs att, int n_att) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int bid = blockIdx.x;
   if constexpr (AV != 0) {
@@ -982,19 +720,6 @@ __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
       return;
     }
     bid -= n_att;
-  }
-  if constexpr (FZ) {
-    // fused decode step: vocabulary tiles (padded to a multiple of 8), then
-    // the recurrent tiles, which merge and apply the cell
-    const int n_voc = ((V + VT_V - 1) / VT_V) * ((R + BN - 1) / BN);
-    const int nv_pad = (n_voc + 7) / 8 * 8;
-    if (bid < nv_pad) {
-      if (bid < n_voc) vocab_tr_block<BN, STAGES, true>(bid, lds, VOCAB_TR_ARGS, fz.sync);
-      return;
-    }
-    fz_lstm_block<LT>(bid - nv_pad, h_t, R, H, whh, vgate, vdiv, lds, fz, part,
-                      (V + VT_V - 1) / VT_V, V, rng, step, AV != 0 ? att.Bv : 0);
-    return;
   }
   if (bid < n_lstm_pad) {
     if (bid < lstm_gemm_blocks(R, H, NQ))
@@ -1108,107 +833,68 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   post_launch("vocab_combine_kernel", stream);
 }
 
-template <int BN, int STAGES, int OCC, class LT, int AV, bool FZ>
+template <int BN, int STAGES, int OCC, class LT, int AV>
 static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
                                 float inv_temp, const uint32_t* rng, int step, const uint16_t* h_t,
                                 const uint16_t* whh, const float* vgate, int vdiv, float* pre,
                                 int NQ, float* q_out, hipStream_t stream, const float* eoff,
-                                const AttMfmaArgs* att, const FuseArgs* fz) {
+                                const AttMfmaArgs* att) {
   using TL = Tile<VT_V, BN, STAGES>;
   constexpr int LV = TL::STAGES * TL::STAGE_BYTES > epilogue_lds_bytes(BN)
                          ? TL::STAGES * TL::STAGE_BYTES
                          : epilogue_lds_bytes(BN);
   constexpr int LDS = LV > LT::LDS_BYTES ? LV : LT::LDS_BYTES;
   static_assert(AV == 0 || LDS >= 48 * 1024, "attention workgroups assume 48 KB of LDS");
-  static_assert(!FZ || LDS >= LT::C_BYTES + 16, "fused merge scratch behind the C tile");
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
   AttMfmaArgs a{};
   int n_att = 0;
-  FuseArgs f{};
   if (AV != 0) {
     a = *att;
     n_att = (att_mfma_blocks(a.Bv, a.A) + 7) / 8 * 8;
   }
-  int n_l, grid;
-  if (FZ) {
-    f = *fz;
-    if (AV != 0) a.done = f.sync + 2 * ((R + 63) / 64) * FZ_LINE;
-    n_l = lstm_gemm_blocks(R, H, 0);
-    grid = n_att + (n_vt * n_rt + 7) / 8 * 8 + n_l;
-  } else {
-    n_l = pre != nullptr ? (lstm_gemm_blocks(R, H, NQ) + 7) / 8 * 8 : 0;
-    grid = n_att + n_l + n_vt * n_rt;
-  }
+  const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H, NQ) + 7) / 8 * 8 : 0;
+  const int grid = n_att + n_l + n_vt * n_rt;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, FZ>,
+    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, FZ>), dim3(grid), dim3(256),
+  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV>), dim3(grid), dim3(256),
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
                      tgt, tgt_stride, flags, inv_temp, rng, step, eoff, h_t, whh, vgate, vdiv, pre,
-                     n_l, NQ, q_out, a, n_att, f);
+                     n_l, NQ, q_out, a, n_att);
   post_launch("vocab_lstm_fwd_kernel", stream);
 }
 
 int vocab_part_slots(int V) { return (V + VT_V - 1) / VT_V; }
-
-// CSTCAP_FUSED_DECODE=0 keeps the separate combine launch (A/B runs); tests
-// force either form with set_fused_decode
-static int g_fz_override = -1;
-void set_fused_decode(int on) { g_fz_override = on; }
-bool fused_decode_enabled() {
-  if (g_fz_override >= 0) return g_fz_override == 1;
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("CSTCAP_FUSED_DECODE");
-    on = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  return on == 1;
-}
 
 int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                           const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
                           const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                           const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                           const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
-                          float* q_out, const float* eoff, const AttMfmaArgs* att,
-                          const FuseArgs* fz) {
-  if (fz != nullptr) {
-    if (pre == nullptr || NQ != 0 || (flags & (VF_SAVE_F32 | VF_BENCH_MAINLOOP)) ||
-        fz->sync == nullptr || fz->tok32 == nullptr || fz->tok_out == nullptr ||
-        fz->ptab == nullptr || fz->c_prev == nullptr || fz->c_out == nullptr ||
-        fz->h_out == nullptr || (att != nullptr && fz->vg16 == nullptr) || H % 16 != 0 ||
-        V > 65535)
-      throw std::runtime_error("vocab_lstm_fwd: fused decode step not applicable");
-  }
+                          float* q_out, const float* eoff, const AttMfmaArgs* att) {
   // 64-row tiles, 3 blocks per CU (48 KB of LDS each; the recurrent tiles use
   // 2 stages to fit): one block's epilogue overlaps the others' main loops.
   // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
   // CU (3 interleaved rounds; profiles/r2/ab_vocab_tiles.txt)
-#define VL(AVX, FZX)                                                                          \
-  launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX, FZX>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, \
-                                                   tgt, tgt_stride, flags, inv_temp, rng, step,  \
-                                                   h_t, whh, vgate, vdiv, pre, NQ, q_out, stream, \
-                                                   eoff, att, fz)
+#define VL(AVX)                                                                            \
+  launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, \
+                                              tgt, tgt_stride, flags, inv_temp, rng, step,  \
+                                              h_t, whh, vgate, vdiv, pre, NQ, q_out, stream, \
+                                              eoff, att)
   if (att == nullptr) {
-    if (fz != nullptr)
-      VL(0, true);
-    else
-      VL(0, false);
+    VL(0);
     return vocab_num_tiles(V);
   }
   check_att_mfma(*att);
   switch (att_variant(att->C)) {
-#define X(AVX)         \
-  case AVX:            \
-    if (fz != nullptr) \
-      VL(AVX, true);   \
-    else               \
-      VL(AVX, false);  \
+#define X(AVX)  \
+  case AVX:     \
+    VL(AVX);    \
     break;
     ATT_VARIANTS(X)
 #undef X

@@ -26,24 +26,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
-// 16-byte write-through stores / loads (buffer instructions with the sc1
-// cache policy, bit 4 of the builtins' aux operand on gfx950): the hand-off
-// form of data produced and consumed by different workgroups of ONE launch --
-// the bytes bypass the consumer CU's L1 and are written through the producer
-// XCD's L2, so no fence is needed on either side (the producer still drains
-// its stores with s_waitcnt vmcnt(0) before it signals).
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-constexpr int CPOL_SC1 = 16;
-__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int off, u32x4v v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, CPOL_SC1);
-}
-__device__ __forceinline__ u32x4v ld16_sc1(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CPOL_SC1);
-}
-__device__ __forceinline__ int ld_sc1(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // VF_EXP: the saved copy is E = exp(x - eoff[r]) in bf16 instead of fp16 x
 // (eoff = the row's LSE of the previous decode step), see vocab_grad.hip
 enum VocabFlags : int {

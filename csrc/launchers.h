@@ -101,7 +101,6 @@ struct AttMfmaArgs {
   float* q_out;          // nullable (R, A) fp32
   float* e_part;         // (Bv, A / 64, 32, CP) partial-score slots
   int* cnt;              // (Bv) tickets, zero at the first launch (re-armed by the kernel)
-  int* done;             // nullable: videos completed in this launch (fused decode step)
 };
 // the MFMA attention path applies: rows per video 2..32, C <= 16, A % 64 == 0,
 // A <= 1024, H % 32 == 0, 64 <= H <= 512, the shared scorer (not per frame)
@@ -110,53 +109,6 @@ bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame);
 void launch_att_mfma_fwd(const AttMfmaArgs& a, hipStream_t stream);
 // size of the end-of-sequence flag area per decode step (ints) of `counts`
 int combine_count_ints_per_step();
-// Fused decode step (vocab.hip "fused decode step"): the combine folded into
-// the decode launch.  The vocabulary tiles publish their partials and arrive
-// on a per-row-tile counter; the recurrent (LSTM) tiles, dispatched after
-// them, merge the partials of one 64-row tile each (the first 2 column tiles
-// of every 128-row group), publish the chosen tokens, and every recurrent
-// tile then applies the next step's cell to its own (rows x units) straight
-// from its accumulators (no pre-activation round trip, no combine launch).
-constexpr int FZ_LINE = 16;  // ints per synchronisation word (one 64-byte line each)
-// ints of one decode step's synchronisation area: arrival counters and ready
-// flags of the n_vrt 64-row tiles, the attention completion counter, a pad line
-int fused_sync_ints(int R);
-struct FuseArgs {
-  int* sync;             // this step's area (fused_sync_ints), zero before the launch
-  int* tok32;            // (R) chosen tokens, int32 (written by the mergers)
-  int* err;              // nullable: incremented by a wait that timed out
-  // merge outputs, as launch_vocab_combine
-  float* lse_out;
-  int64_t* tok_out;
-  int64_t tok_stride;
-  float* g_sel;
-  int64_t gsel_stride;
-  float* g_xe;
-  int64_t gxe_stride;
-  const int64_t* gt;
-  int64_t gt_stride;
-  int mode;
-  float ss_prob;
-  int* counts;
-  int count_step;
-  uint8_t* unfinished;
-  // cell of the next step (see CellLaunch)
-  const float* ptab;
-  const float* c_prev;
-  float* c_out;
-  uint16_t* h_out;
-  uint16_t* hdrop_out;
-  int ldh;
-  uint16_t* gates_out;
-  float drop_p;
-  int cstep;
-  int cell;
-  const uint16_t* vg16;  // attention: per-row bf16 video gates of this launch's attention
-};
-// the fused form applies to the tiled launch with a recurrent part (pre !=
-// nullptr, no W_q tiles); CSTCAP_FUSED_DECODE=0 turns it off (A/B runs)
-bool fused_decode_enabled();
-void set_fused_decode(int on);  // -1: environment, 0 / 1: force (tests)
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
@@ -167,9 +119,7 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
 // whh has 4H + NQ rows, the last NQ (W_q) produce the attention query q_out
 // (R x NQ) and vgate must be nullptr.  Returns the number of partial slots
 // per row it wrote into part (the combine's n_vt); part must hold
-// vocab_part_slots(V) x R.  fz != nullptr: the fused form (FuseArgs; pre is
-// then not written, the cell outputs and the merge outputs are, and no
-// combine follows).
+// vocab_part_slots(V) x R.
 int vocab_part_slots(int V);
 int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                            const float* bias, int V, uint16_t* logits16, int64_t ldl, void* part,
@@ -177,7 +127,7 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream,
                            int NQ = 0, float* q_out = nullptr, const float* eoff = nullptr,
-                           const AttMfmaArgs* att = nullptr, const FuseArgs* fz = nullptr);
+                           const AttMfmaArgs* att = nullptr);
 // exp store of step 0: fp16 logits rows -> bf16 exp(x - lse_r), in place
 void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,
                               hipStream_t stream);
