@@ -94,6 +94,9 @@ def parse():
                         'graph; after the timed steps, N more steps are stamped and the mean '
                         'phase times (us after the step start) are printed to stderr and '
                         'stored as "stamps_us" (diagnostic: stamps add ~2 us per phase)')
+    p.add_argument('--sync_each', type=int, default=0,
+                   help='diagnostic: synchronise after every timed step (isolated steps; '
+                        'not the headline measurement)')
     p.add_argument('--sync_debug', type=int, default=0,
                    help='after warmup: report host-synchronising calls and host enqueue time of one step')
     return p.parse_args()
@@ -197,6 +200,8 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
     phases = {}
     for _ in range(a.steps):
         out = step()
+        if a.sync_each:
+            sync()
         if a.profile_phases:  # reads the events: synchronises, diagnostic only
             for k, v in trainer.timer.summary().items():
                 phases[k] = phases.get(k, 0.0) + v / a.steps
@@ -208,6 +213,9 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
     stamp_mean = {}
     if a.stamps and dev.type == 'cuda':
         for _ in range(a.stamps):
+            # two back-to-back steps per read: the second one's 'prev_end' is
+            # the first one's last stamp (> 0: the two steps overlapped)
+            step()
             step()
             for k, v in stamps_mod.read().items():
                 stamp_mean[k] = stamp_mean.get(k, 0.0) + v / a.stamps

@@ -695,6 +695,8 @@ class DecoderEngine:
         else:
             vg, B = self._vgate(model, feats, expand)
             att = (None,) * 5
+        from ..utils import stamps
+        stamps.mark_fwd('vgate')
         S = model.feat_expander.n if expand else 1
         h0 = c0 = None
         if self.standard:

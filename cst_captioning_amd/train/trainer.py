@@ -197,6 +197,7 @@ class Trainer:
             # first, the other stream would read it unordered
             gathered = (data['feats'], data['labels'])  # (LazyGather: gathers now)
             del gathered
+            stamps.mark('gathered')
             inputs_ready = self._ev_inputs
             inputs_ready.record(main)
         # fused engine: reward, mask and REINFORCE loss in one launch

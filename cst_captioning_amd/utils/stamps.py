@@ -19,14 +19,16 @@ import torch
 # trainer phases (slot), then the executor's slot bases (csrc/launchers.h
 # StampSlot: forward 0..2, backward 0..10)
 TRAINER = ['step', 'rollout_enq', 'greedy_begin', 'greedy_end', 'sample_scores', 'loss',
-           'bwd_end', 'adam_begin', 'adam_end', 'ptab_end', 'x_end']
-FWD = ['begin', 'step0', 'end']
+           'bwd_end', 'adam_begin', 'adam_end', 'ptab_end', 'x_end', 'gathered', 'prev_end']
+# executor slots 0..2 (csrc), 3: the decode's prologue (video gates) done (Python)
+FWD = ['begin', 'step0', 'end', 'vgate']
 BWD = ['begin', 'onehot', 'dhd0', 'dhd', 'loop0', 'loop', 'dw', 'side', 'toksum', 'tokgemm',
        'end']
 BASE = {'trainer': 0, 'fwd_sample': 16, 'fwd_greedy': 20, 'bwd': 32}
 NSLOTS = 64
 
 _buf = None
+_base = None
 
 
 def names():
@@ -69,16 +71,29 @@ def mark(name):
     if _buf is None:
         return
     from .. import _ext
+    if name == 'step':  # the previous step's last stamp, before this step's first
+        _buf[TRAINER.index('prev_end')].copy_(_buf[TRAINER.index('ptab_end')])
     _ext.ops().stamp_now(BASE['trainer'] + TRAINER.index(name))
 
 
 def base(which):
     """Slot base of the next executor call ('fwd_sample', 'fwd_greedy',
     'bwd'; None = no executor stamps)."""
+    global _base
     if _buf is None:
         return
     from .. import _ext
+    _base = which
     _ext.ops().set_stamp_base(-1 if which is None else BASE[which])
+
+
+def mark_fwd(name):
+    """Stamp decode phase ``name`` (FWD) of the current executor base on the
+    current stream (no-op if disabled or no forward base is set)."""
+    if _buf is None or _base not in ('fwd_sample', 'fwd_greedy'):
+        return
+    from .. import _ext
+    _ext.ops().stamp_now(BASE[_base] + FWD.index(name))
 
 
 def read(clear=True):
