@@ -15,13 +15,20 @@ def test_slots_are_disjoint_and_fit():
     bw = [stamps.BASE['bwd'] + i for i in range(len(stamps.BWD))]
     allslots = tr + fs + fg + bw
     assert len(allslots) == len(set(allslots))
-    # the executor's backward uses 11 slots (STAMP_BWD_BEGIN .. STAMP_BWD_END)
-    assert len(stamps.BWD) == 11 and len(stamps.FWD) == 3
+    # the executor's backward uses 11 slots (STAMP_BWD_BEGIN .. STAMP_BWD_END),
+    # its forward 3 (STAMP_FWD_*) plus the decode prologue's Python stamp
+    assert len(stamps.BWD) == 11 and len(stamps.FWD) == 4
+    assert stamps.FWD[:3] == ['begin', 'step0', 'end']
+    # each forward base has room for its 4 slots before the next base
+    assert stamps.BASE['fwd_greedy'] - stamps.BASE['fwd_sample'] >= len(stamps.FWD)
+    assert stamps.BASE['bwd'] - stamps.BASE['fwd_greedy'] >= len(stamps.FWD)
+    assert stamps.BASE['fwd_sample'] >= len(stamps.TRAINER)
 
 
 def test_disabled_helpers_are_no_ops():
     assert not stamps.enabled()
     stamps.mark('step')
+    stamps.mark_fwd('vgate')
     stamps.base('bwd')
     stamps.base(None)
     assert stamps.read() == {}
