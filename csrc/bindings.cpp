@@ -15,6 +15,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         bool use_unfinished, std::vector<at::Tensor> att,
                                         int64_t cell, std::vector<at::Tensor> state0,
                                         std::vector<at::Tensor> up, bool store_exp);
+void set_grad_events(bool on);
+void grad_event_wait(int64_t k, int64_t stream);
+void grad_event_record(int64_t k, int64_t stream);
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -144,6 +147,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("token_group_sum", &cst::token_group_sum);
   m.def("vocab_select", &cst::vocab_select);
   m.def("decode_step_test", &cst::decode_step_test);
+  m.def("set_grad_events", &cst::set_grad_events);
+  m.def("grad_event_wait", &cst::grad_event_wait);
+  m.def("grad_event_record", &cst::grad_event_record);
   m.def("att_mfma_fwd", &cst::att_mfma_fwd);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);

@@ -103,6 +103,7 @@ constexpr int MAX_DHD_CHUNKS = 32;  // per-chunk events of the vocab-head dHd GE
 struct DeviceAux {
   std::vector<hipEvent_t> ev;
   c10::hip::HIPStream side[2];
+  hipEvent_t grad_ev[2];  // data parallelism: gradient groups final (set_grad_events)
 };
 static DeviceAux& device_aux(int dev_index) {
   static std::map<int, DeviceAux*> aux;
@@ -112,9 +113,57 @@ static DeviceAux& device_aux(int dev_index) {
                                  c10::hip::getStreamFromPool(false, dev_index)}};
     a->ev.resize(6 + MAX_DHD_CHUNKS);
     for (auto& e : a->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    for (auto& e : a->grad_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     it = aux.emplace(dev_index, a).first;
   }
   return *it->second;
+}
+
+// Data parallelism, communication overlapped with the backward: with
+// set_grad_events(true) decoder_backward records grad_ev[0] once the vocab
+// head's gradients (logit W, b) are final (side stream, after dW_logit, which
+// then runs under the reverse loop) and grad_ev[1] once the embedding
+// gradient is (main stream, after its GEMM).  Inside a graph capture they are
+// event-record NODES of the captured graph (record_grad_event), so after each replay
+// the trainer's comm stream waits on them (grad_event_wait) and all-reduces
+// those bucket slices while the rest of the replayed backward still runs --
+// eager RCCL between replays, no collective inside the graph.
+static bool g_grad_events_on = false;
+void set_grad_events(bool on) { g_grad_events_on = on; }
+static void record_grad_event(hipEvent_t ev, hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  unsigned long long id = 0;
+  hipError_t e = hipStreamGetCaptureInfo_v2(s, &cs, &id, &graph, &deps, &nd);
+  TORCH_CHECK(e == hipSuccess, "grad event: capture info: ", hipGetErrorString(e));
+  if (cs != hipStreamCaptureStatusActive) {
+    e = hipEventRecord(ev, s);
+    TORCH_CHECK(e == hipSuccess, "grad event: record: ", hipGetErrorString(e));
+    return;
+  }
+  // an event-record node of the graph being captured, after the stream's
+  // current dependencies; the stream's later work then follows the node
+  // (hipEventRecordWithFlags(hipEventRecordExternal) failed with "invalid
+  // argument" inside a capture on this ROCm)
+  hipGraphNode_t node = nullptr;
+  e = hipGraphAddEventRecordNode(&node, graph, deps, nd, ev);
+  TORCH_CHECK(e == hipSuccess, "grad event: record node: ", hipGetErrorString(e));
+  e = hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+  TORCH_CHECK(e == hipSuccess, "grad event: capture dependencies: ", hipGetErrorString(e));
+}
+void grad_event_record(int64_t k, int64_t stream) {  // (tests)
+  TORCH_CHECK(k >= 0 && k < 2, "grad_event_record: group 0 or 1");
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  record_grad_event(device_aux(dev).grad_ev[k], reinterpret_cast<hipStream_t>(stream));
+}
+void grad_event_wait(int64_t k, int64_t stream) {
+  TORCH_CHECK(k >= 0 && k < 2, "grad_event_wait: group 0 or 1");
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), device_aux(dev).grad_ev[k], 0);
 }
 
 // Read-only zeros of at least n elements (initial decoder states): one
@@ -643,11 +692,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // profiles/r2/ab_vh_sched.txt).  Data parallelism runs them concurrently
   // with the loop, so the vocab head's all-reduce hides under it.
   const bool early_comm = early && comm_stream != 0;
+  // DP overlap (set_grad_events): vocab head / embedding gradients final events
+  const bool grad_ev = g_grad_events_on && early;
   // One GPU: the bias column sums (HBM-bound) under the latency-bound
   // reverse loop, dW_logit after it (vh_sched 3; interleaved A/B 3.745-3.792
   // vs 3.774-3.831 ms per step with the loop-after schedule 0,
   // profiles/r3/ab_sched.txt)
-  const int vh_sched = early_comm ? 2 : 3;
+  const int vh_sched = (early_comm || grad_ev) ? 2 : 3;
   // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
   // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
   // split-K batch over groups of decode steps multiplies the tiles in flight,
@@ -673,6 +724,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   };
   auto dw_done = [&]() {
     (void)hipEventRecord(ev_done, side.stream());
+    if (grad_ev) record_grad_event(aux.grad_ev[0], side.stream());
     if (early_comm) (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
   };
   stamp(STAMP_BWD_BEGIN, st);
@@ -928,6 +980,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
+  if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st);
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134
   // TFLOP/s at V = 10,509); a split-K batch over the largest divisor of V up to

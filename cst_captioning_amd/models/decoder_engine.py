@@ -247,18 +247,14 @@ class _DecoderFn(torch.autograd.Function):
         # input token of every step: it_0 = BOS / labels[:, 0], it_t = seq[:, t-1]
         first = labels[:, :1] if labels is not None else bos.view(-1, 1)
         toks = torch.cat([first, seq[:, :n_steps - 1]], 1).t().reshape(-1)
-        # DP overlap: the vocab-head weight gradients go straight into their
-        # flat-bucket slots and are all-reduced during the reverse LSTM loop
-        hook = getattr(eng, 'early_grad_hook', None)
-        early = hook is not None and hook.active
-        # without DP the same slots are written directly too (no autograd
-        # accumulate pass over the V x H gradient), on the late schedule
+        # the vocab-head weight gradients go straight into their flat-bucket
+        # slots (no autograd accumulate pass over the V x H gradient); under
+        # data parallelism the backward also marks them final with an event
+        # (engine set_grad_events), for the comm stream (parallel/dist.py)
         direct = getattr(eng, 'direct_grad_slots', None)
         if direct is not None:
             eng.check_direct_slots()
-        if early:
-            out_w, out_b, comm = hook.out_wlog, hook.out_blog, hook.comm_ptr
-        elif direct is not None:
+        if direct is not None:
             out_w, out_b, comm = direct['wlog'], direct['blog'], 0
         else:
             out_w, out_b, comm = empty, empty, 0
@@ -290,9 +286,7 @@ class _DecoderFn(torch.autograd.Function):
             res = res[:-2]
         ctx.state0 = []
         dWx, dWlog, dblog, d_emb, dvg = res[:5]
-        if early:
-            hook.launch()
-        if early or direct is not None:
+        if direct is not None:
             dWlog = dblog = None  # already in the gradient buffers
         if emb_direct:
             d_emb = None

@@ -4,13 +4,19 @@ The reference is single-GPU with no collectives.  This
 layer adds DP for one node of MI355X GPUs, one process per GPU:
 
   C1  broadcast of parameters/buffers from rank 0 at start;
-  C2  ONE all-reduce per step of the whole gradient as a single flat
-      bucket (or, --dp_update sharded: reduce-scatter -> Adam on the rank's
-      1/N shard -> all-gather of the updated parameters).  The decoder is trained by BPTT, so every gradient is only
-      final after the full reverse time loop: bucketed overlap with backward
-      would buy nothing, while one large message is what a point-to-point
-      xGMI ring moves at full per-link bandwidth (~20 M params = 81 MB fp32,
-      ~0.5 ms at 8 GPUs).  288 GB HBM makes the contiguous buffer free;
+  C2  the whole gradient as ONE flat bucket, all-reduced in at most three
+      large slices ordered by when the backward finalises them
+      (:meth:`FlatGradBucket.all_reduce`): the vocabulary head (logit W, b:
+      final after its dW GEMM, which runs under the reverse LSTM loop), the
+      embedding (final after its GEMM in the post-loop tail), then the rest.
+      The fused backward marks the first two with events (external
+      event-record nodes inside a captured HIP graph), the comm stream waits
+      on them after each replay, and their all-reduces run while the rest of
+      the backward does -- eager RCCL, nothing captured.  Large slices are
+      what a point-to-point xGMI ring moves at full per-link bandwidth
+      (~20 M params = 84 MB fp32).  --dp_update sharded: reduce-scatter ->
+      Adam on the rank's 1/N shard -> all-gather of the updated parameters.
+      288 GB HBM makes the contiguous buffer free;
   C3  all-reduce of a small vector of log scalars;
   C4  all-gather of per-rank evaluation results;
   C5  broadcast of rank-0 decisions (best model / early stop);
@@ -140,47 +146,6 @@ def init_distributed(device_type=None, timeout_s=600):
     return DistContext(rank, world, local, device, backend)
 
 
-class EarlyAllReduce:
-    """Overlap of the gradient all-reduce with the backward (C2).
-
-    The fused decoder's backward produces the vocabulary-head gradients
-    (logit weight + bias, ~26 % of the parameters) before its reverse LSTM
-    loop (~0.5-0.8 ms).  With this hook the engine writes them straight into
-    their slots of the flat bucket (which places them first), makes
-    ``comm_stream`` wait for them, and :meth:`launch` starts their
-    all-reduce there -- it runs under the LSTM loop.  The rest of the bucket
-    is reduced after ``backward()`` and :meth:`FlatGradBucket.all_reduce`
-    joins both.
-    """
-
-    def __init__(self, ctx, bucket, params):
-        self.ctx = ctx
-        self.bucket = bucket
-        self.n = bucket.prefix_numel(params)
-        self.out_wlog, self.out_blog = (p.grad for p in params)
-        self.stream = torch.cuda.Stream(device=ctx.device) if ctx.device.type == 'cuda' else None
-        self.comm_ptr = self.stream.cuda_stream if self.stream is not None else 0
-        self.active = ctx.enabled
-        self.work = None
-
-    def launch(self):
-        view = self.bucket.grad[:self.n]
-        if self.stream is not None:
-            with torch.cuda.stream(self.stream):  # waits on the engine's event
-                self.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True)
-        else:
-            self.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True)
-
-    def wait(self):
-        if self.work is not None:
-            self.work.wait()
-            if self.stream is not None:
-                torch.cuda.current_stream(self.ctx.device).wait_stream(self.stream)
-            self.work = None
-            return True
-        return False
-
-
 class FlatGradBucket:
     """All trainable parameters re-homed into one contiguous fp32 buffer,
     with their ``.grad`` tensors viewing one contiguous gradient buffer.
@@ -191,8 +156,8 @@ class FlatGradBucket:
     """
 
     def __init__(self, params, first=(), world_size=1, wire='fp32', update='allreduce'):
-        """``first``: parameters placed at the start of the buffer (the ones
-        an :class:`EarlyAllReduce` reduces ahead of the rest).  ``wire``:
+        """``first``: parameters placed at the start of the buffer, in this
+        order (the slices :meth:`set_groups` reduces ahead of the rest).  ``wire``:
         'fp32' (one all-reduce) or 'bf16' (see :meth:`all_reduce`); the buffer
         is padded so it splits into ``world_size`` equal chunks."""
         if wire not in ('fp32', 'bf16'):
@@ -205,10 +170,11 @@ class FlatGradBucket:
         self.update = update
         self.world_size = world_size
         params = [p for p in params if p.requires_grad]
+        first = [p for p in first if p.requires_grad]
         first_ids = {id(p) for p in first}
-        self.params = [p for p in params if id(p) in first_ids] + \
-            [p for p in params if id(p) not in first_ids]
-        self.early = None
+        self.params = list(first) + [p for p in params if id(p) not in first_ids]
+        self.groups = []  # streamed slices (set_groups)
+        self.comm = None
         self.on_zero = None
         if not self.params:
             raise ValueError('no trainable parameters')
@@ -300,19 +266,38 @@ class FlatGradBucket:
         ``grad_scale``), so no separate pass over the buffer divides it."""
         return 1.0 / ctx.world_size if (ctx.enabled and self.wire == 'fp32') else 1.0
 
+    def set_groups(self, groups, ctx):
+        """Leading slices reduced as soon as the backward marks them final:
+        ``groups`` = [params of slice 0, params of slice 1] (at most two; they
+        must be the buffer's leading parameters, in order).  The fused
+        backward records the matching events (engine ``set_grad_events``)."""
+        self.groups = []
+        off = 0
+        want = [p for g in groups for p in g]
+        self.prefix_numel(want)  # (checks the order)
+        for g in groups:
+            n = sum(p.numel() for p in g)
+            self.groups.append((off, off + n))
+            off += n
+        if self.grad.is_cuda and self.comm is None:
+            self.comm = torch.cuda.Stream(device=self.grad.device)
+
     def all_reduce(self, ctx):
         """Reduce the gradient over ranks: fp32 wire -> the SUM (the mean is
         ``grad * grad_scale(ctx)``); bf16 wire -> the mean.
 
-        wire 'fp32': one RCCL ring all-reduce of the fp32 buffer (plus the
-        early vocab-head slice, if one was launched).  wire 'bf16': half the
-        bytes on xGMI with fp32 accumulation -- every rank sends chunk j of its
-        gradient as bf16 to rank j (all-to-all), sums the N received chunks in
-        fp32, and the reduced chunks are all-gathered as bf16.  Per rank that
-        moves (N-1)/N of the buffer in bf16 twice, half of the fp32 ring's
-        2 (N-1)/N x 4 bytes; the applied gradient carries one bf16 rounding of
-        each input and of the sum (relative 2^-9), which Adam's normalised
-        update tolerates.  The skip flag (0 / 1) is exact in bf16."""
+        wire 'fp32': RCCL ring all-reduces of the fp32 buffer -- with groups,
+        each leading slice on the comm stream once its event fired (they run
+        while the enqueued backward still computes the rest), then the rest
+        on the current stream, which finally waits for the slices.  Every rank
+        issues the same collectives in the same order.  wire 'bf16': half the
+        bytes on xGMI with fp32 accumulation -- every rank sends chunk j of
+        its gradient as bf16 to rank j (all-to-all), sums the N received chunks
+        in fp32, and the reduced chunks are all-gathered as bf16.  Per rank
+        that moves (N-1)/N of the buffer in bf16 twice, half of the fp32
+        ring's 2 (N-1)/N x 4 bytes; the applied gradient carries one bf16
+        rounding of each input and of the sum (relative 2^-9), which Adam's
+        normalised update tolerates.  The skip flag (0 / 1) is exact in bf16."""
         if ctx.enabled and self.wire == 'bf16':
             N = ctx.world_size
             chunk = self.grad.numel() // N
@@ -324,9 +309,21 @@ class FlatGradBucket:
             dist.all_gather_into_tensor(out, mine)
             self.grad.copy_(out)
             return
-        if ctx.enabled:
-            early = self.early is not None and self.early.work is not None
-            rest = self.grad[self.early.n:] if early else self.grad
-            dist.all_reduce(rest, op=dist.ReduceOp.SUM)
-            if early:
-                self.early.wait()
+        if not ctx.enabled:
+            return
+        if not self.groups or self.comm is None:
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+            return
+        from .. import _ext
+        main = torch.cuda.current_stream(self.grad.device)
+        self.comm.wait_stream(main)  # (everything enqueued before this step's backward)
+        works = []
+        with torch.cuda.stream(self.comm):
+            for k, (lo, hi) in enumerate(self.groups):
+                _ext.ops().grad_event_wait(k, self.comm.cuda_stream)
+                works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM,
+                                             async_op=True))
+        dist.all_reduce(self.grad[self.groups[-1][1]:], op=dist.ReduceOp.SUM)
+        for w in works:
+            w.wait()
+        main.wait_stream(self.comm)

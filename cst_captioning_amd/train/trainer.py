@@ -87,21 +87,23 @@ class Trainer:
         self.xe_criterion = CrossEntropyCriterion()
         self.rl_criterion = RewardCriterion()
         self.ctx.broadcast_module(model)
+        # bucket order = the order the fused backward finalises gradients:
+        # vocab head (under the reverse loop), embedding (post-loop tail), rest
         early = [model.logit.weight, model.logit.bias]
-        self.bucket = FlatGradBucket(model.parameters(), first=early,
+        self.bucket = FlatGradBucket(model.parameters(), first=early + [model.embed.weight],
                                      world_size=self.ctx.world_size,
                                      wire=getattr(opt, 'grad_wire', 'fp32'),
                                      update=getattr(opt, 'dp_update', 'allreduce'))
-        # Early all-reduce of the vocab-head gradients under the reverse loop:
-        # eager steps only.  With HIP graphs every step (eager warm-up or
-        # replay) issues the same single bucket all-reduce, so ranks can never
-        # disagree on the collective sequence.
-        if (engine is not None and self.ctx.enabled and not getattr(opt, 'no_early_allreduce', 0)
-                and not getattr(opt, 'cuda_graph', 1) and self.bucket.wire == 'fp32'
+        # Data parallelism: those two slices are all-reduced on a comm stream
+        # as soon as the backward marks them final (events; external
+        # event-record nodes in the captured graph), under the rest of the
+        # backward, eager RCCL between replays (parallel/dist.py)
+        if (engine is not None and self.ctx.enabled and self.device.type == 'cuda'
+                and not getattr(opt, 'no_early_allreduce', 0) and self.bucket.wire == 'fp32'
                 and not self.bucket.sharded):
-            from ..parallel.dist import EarlyAllReduce
-            self.bucket.early = EarlyAllReduce(self.ctx, self.bucket, early)
-            engine.early_grad_hook = self.bucket.early
+            from .. import _ext
+            self.bucket.set_groups([early, [model.embed.weight]], self.ctx)
+            _ext.ops().set_grad_events(True)
         if engine is not None:
             # the fused backward writes the vocab-head, embedding and LSTM
             # weight gradients straight into their bucket slots (one backward

@@ -41,12 +41,13 @@ def _run(world, out, graph, wire='fp32', update='allreduce', mode='xe'):
 
 
 @pytest.mark.parametrize('graph,wire', [(1, 'fp32'), (0, 'fp32'), (1, 'bf16')],
-                         ids=['hip_graph', 'eager_early_allreduce', 'hip_graph_bf16_wire'])
+                         ids=['hip_graph_streamed', 'eager_streamed', 'hip_graph_bf16_wire'])
 def test_engine_dp_allreduce_matches_single_process(tmp_path, graph, wire):
-    """graph=1: steps replayed as HIP graphs around one bucket all-reduce;
-    graph=0: eager steps with the vocab-head all-reduce started under the
-    reverse LSTM loop (EarlyAllReduce); bf16 wire: all-to-all + fp32 sum +
-    all-gather of bf16 chunks."""
+    """graph=1: steps replayed as HIP graphs, the vocab-head and embedding
+    slices all-reduced on the comm stream once the replayed backward's
+    external events fire, the rest after the replay; graph=0: the same
+    streamed slices behind the eager backward's events; bf16 wire:
+    all-to-all + fp32 sum + all-gather of bf16 chunks."""
     os.environ['CSTCAP_TEST_IMPL'] = 'hip'
     r2 = _run(2, str(tmp_path / 'w2.pt'), graph, wire)
     r1 = _run(1, str(tmp_path / 'w1.pt'), graph, wire)
