@@ -20,7 +20,10 @@ BASELINE.json's metric names the LSTM-attn decoder while the headline config
 (the reference default ``--num_chunks 1``) mean-pools the features, so an SCST
 run also times the 8-frame temporal-attention config of the same job (same K
 and W, after the headline run's buffers are freed) and reports it as the
-``att8`` field ({value, ms_per_step, ...}); ``--att8 0`` skips it.
+``att8`` field ({value, ms_per_step, ...}); ``--att8 0`` skips it.  After the
+timed steps the headline run also times the beam-5 evaluation decode of one
+batch (BASELINE config 5) on the weights it trained: the ``beam5`` field
+({videos_per_s (whole job), ms_per_batch, ...}); ``--beam5 0`` skips it.
 
 Modes:
   --impl hip   (default) fused HIP engine + on-GPU CIDEr-D, bf16 MFMA
@@ -86,6 +89,10 @@ def parse():
     p.add_argument('--att8', type=int, default=1,
                    help='scst with --num_chunks 1: also time the 8-frame temporal-attention '
                         'config in the same invocation and report it as the "att8" field')
+    p.add_argument('--beam5', type=int, default=1,
+                   help='scst, headline config: also time the beam-5 evaluation decode of one '
+                        'batch (BASELINE config 5) on the trained weights and report it as the '
+                        '"beam5" field')
     p.add_argument('--json_out', default='')
     p.add_argument('--profile_phases', type=int, default=0,
                    help='print the mean per-phase GPU time (HIP events) of the timed steps')
@@ -226,13 +233,39 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
         for k, v in stamp_mean.items():
             print('  %9.1f  %s' % (v, k), file=sys.stderr)
         sys.stderr.flush()
+    beam = None
+    if (a.beam5 and a.mode == 'scst' and num_chunks == 1 and engine is not None
+            and dev.type == 'cuda'):
+        # BASELINE config 5: beam-5 evaluation decode of one batch (64 videos
+        # per rank) with the weights the timed steps trained
+        model.eval()
+        bdata = loader.get_batch()
+        nb = max(a.steps, 5)
+        with torch.no_grad():
+            for _ in range(3):
+                model.sample(bdata['feats'], {'beam_size': 5})
+            sync()
+            ctx.barrier()
+            sync()
+            tb = time.perf_counter()
+            for _ in range(nb):
+                model.sample(bdata['feats'], {'beam_size': 5})
+            sync()
+            ctx.barrier()
+            sync()
+        tb = ctx.max_scalar(time.perf_counter() - tb)
+        beam = {'videos_per_s': round(a.batch_size * ctx.world_size * nb / tb, 1),
+                'ms_per_batch': round(tb / nb * 1e3, 3), 'videos_per_batch_per_gpu': a.batch_size,
+                'beam_size': 5, 'decodes': nb}
+        model.train()
     res = {'dt': dt, 'ms': dt / a.steps * 1e3, 'loss': float(out['loss']),
            'caps': a.batch_size * S * ctx.world_size * a.steps / dt,
            'vids': a.batch_size * ctx.world_size * a.steps / dt, 'phases': phases,
            'skipped': int(trainer.optimizer.skipped().item()),
            'exp_fix': int(engine.exp_fix_rows.item()) if engine is not None else None,
            'graph': int(trainer._graph is not None), 'n_params': n_params, 't_gen': t_gen,
-           'bf16': engine is not None or trainer.autocast_bf16, 'stamps': stamp_mean}
+           'bf16': engine is not None or trainer.autocast_bf16, 'stamps': stamp_mean,
+           'beam5': beam}
     del trainer, model, engine, loader, ds, step, out
     gc.collect()
     if dev.type == 'cuda':
@@ -326,6 +359,9 @@ def main():
         # BASELINE.json's metric names the LSTM-attn decoder: its temporal-
         # attention config (C = 8 frames, MFMA attention) on the same job
         rec['att8'] = att8
+    if main_run.get('beam5'):
+        # BASELINE config 5: beam-5 evaluation decode (graph-replayed), whole job
+        rec['beam5'] = main_run['beam5']
     if main_run['stamps']:
         rec['stamps_us'] = main_run['stamps']
     if main_run['phases']:

@@ -26,15 +26,30 @@ namespace cst {
 
 constexpr int BEAM_MAXK = 16;
 
-// top-K (value, index) of logit - lse for each of R rows; ties -> smaller index
+// top-K (value, index) of logit - lse for each of R rows; ties -> smaller
+// index.  One 256-thread block per row: each thread keeps a sorted register
+// list of its strided entries (a value not above the list's K-th is rejected
+// with one compare, so after the first few entries almost nothing is
+// inserted), each wave takes K rounds of wave arg-max over its lanes' list
+// heads, and wave 0 merges the 4 waves' K candidates the same way.
+__device__ __forceinline__ void wave_argmax(float& best, int& besti) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(besti, o, 64);
+    if (ov > best || (ov == best && oi < besti)) best = ov, besti = oi;
+  }
+}
+
 __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict__ logits,
                                                         int64_t ldl, int V, int R, int K,
                                                         const float* __restrict__ lse,
                                                         float* __restrict__ top_v,
                                                         int* __restrict__ top_i) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= R) return;
+  __shared__ float s_v[4 * BEAM_MAXK];
+  __shared__ int s_i[4 * BEAM_MAXK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = blockIdx.x;
   const float* x = logits + (int64_t)r * ldl;
   // lane-local sorted top-K by an unrolled insertion pass (static register
   // indices only; strict > keeps the earlier, smaller index on ties)
@@ -42,37 +57,48 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict_
   int bi[BEAM_MAXK];
 #pragma unroll
   for (int k = 0; k < BEAM_MAXK; ++k) bv[k] = -INFINITY, bi[k] = 0x7fffffff;
-  for (int v = lane; v < V; v += 64) {
+  float thr = -INFINITY;  // the list's K-th value
+  for (int v = threadIdx.x; v < V; v += 256) {
     float cv = x[v];
+    if (!(cv > thr)) continue;
     int ci = v;
-    {
 #pragma unroll
-      for (int p = 0; p < BEAM_MAXK; ++p) {
-        if (p < K && cv > bv[p]) {
-          const float tv = bv[p];
-          const int ti = bi[p];
-          bv[p] = cv, bi[p] = ci;
-          cv = tv, ci = ti;
-        }
+    for (int p = 0; p < BEAM_MAXK; ++p) {
+      if (p < K && cv > bv[p]) {
+        const float tv = bv[p];
+        const int ti = bi[p];
+        bv[p] = cv, bi[p] = ci;
+        cv = tv, ci = ti;
       }
     }
+#pragma unroll
+    for (int p = 0; p < BEAM_MAXK; ++p) thr = p == K - 1 ? bv[p] : thr;
   }
   // K rounds of wave arg-max over the lanes' list heads; the winner shifts
-  const float L = lse[r];
   for (int k = 0; k < K; ++k) {
     float best = bv[0];
     int besti = bi[0];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const float ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(besti, o, 64);
-      if (ov > best || (ov == best && oi < besti)) best = ov, besti = oi;
-    }
+    wave_argmax(best, besti);
     if (bi[0] == besti) {
 #pragma unroll
       for (int p = 0; p + 1 < BEAM_MAXK; ++p) bv[p] = bv[p + 1], bi[p] = bi[p + 1];
       bv[BEAM_MAXK - 1] = -INFINITY, bi[BEAM_MAXK - 1] = 0x7fffffff;
     }
+    if (lane == 0) s_v[w * BEAM_MAXK + k] = best, s_i[w * BEAM_MAXK + k] = besti;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  // the 4 waves' sorted candidate lists: lane l < 4K holds candidate l
+  const int ww = lane / BEAM_MAXK, kk = lane % BEAM_MAXK;
+  const bool have = lane < 4 * BEAM_MAXK && kk < K;
+  float cv = have ? s_v[ww * BEAM_MAXK + kk] : -INFINITY;
+  int ci = have ? s_i[ww * BEAM_MAXK + kk] : 0x7fffffff;
+  const float L = lse[r];
+  for (int k = 0; k < K; ++k) {
+    float best = cv;
+    int besti = ci;
+    wave_argmax(best, besti);
+    if (ci == besti && cv == best) cv = -INFINITY, ci = 0x7fffffff;
     if (lane == 0) {
       top_v[(int64_t)r * K + k] = best - L;
       top_i[(int64_t)r * K + k] = besti;
@@ -171,8 +197,8 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
 
 void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,
                       float* top_v, int* top_i, hipStream_t stream) {
-  hipLaunchKernelGGL(beam_topk_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, logits, ldl, V,
-                     R, K, lse, top_v, top_i);
+  hipLaunchKernelGGL(beam_topk_kernel, dim3(R), dim3(256), 0, stream, logits, ldl, V, R, K, lse,
+                     top_v, top_i);
   post_launch("beam_topk_kernel", stream);
 }
 

@@ -71,6 +71,8 @@ Supported configuration: ``rnn_type lstm | gru | rnn``, ``model_type concat
 ``concat``, ``num_layers >= 1`` (> 1 with concat, no attention); other
 configurations use the PyTorch path (``build_model`` decides).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -807,8 +809,38 @@ class DecoderEngine:
             h0, c0 = self._initial_state(model, feats)
             state0 = [h0.bfloat16().contiguous(), c0.float().contiguous()]
         self.ensure_ptab()
-        seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog,
-                                         model.logit.bias.detach().float().contiguous(),
-                                         vg.detach().float().contiguous(), K, model.seq_length,
-                                         BOS, att, self.cell, state0, self.upper_operands())
+        blog = model.logit.bias.detach().float().contiguous()
+        vg = vg.detach().float().contiguous()
+        if (not att and not state0 and self.layers == 1 and vg.is_cuda
+                and os.environ.get('CSTCAP_BEAM_GRAPH', '1') != '0'
+                and not torch.cuda.is_current_stream_capturing()):
+            return self._beam_graphed(vg, blog, K, model.seq_length)
+        seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog, blog, vg, K,
+                                         model.seq_length, BOS, att, self.cell, state0,
+                                         self.upper_operands())
         return seq, lp
+
+    def _beam_graphed(self, vg, blog, K, T):
+        """The whole beam decode (T-1 steps x 5 launches) replayed as one
+        captured HIP graph per (videos, K, T): the weights are the engine's
+        persistent shadows (updated in place), the video gates are copied
+        into the graph's static input, the outputs cloned out."""
+        key = (tuple(vg.shape), int(K), int(T), blog.data_ptr())
+        cache = self.__dict__.setdefault('_beam_graphs', {})
+        ent = cache.get(key)
+        if ent is None:
+            if len(cache) >= 4:
+                cache.clear()
+            static_vg = vg.clone()
+            args = lambda: (self.wx, self.ptab, self.whh, self.wlog, blog, static_vg, K, T, BOS,
+                            [], self.cell, [], [])
+            _ext.ops().beam_search(*args())  # (kernel attributes, allocator, outside capture)
+            torch.cuda.synchronize(vg.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = _ext.ops().beam_search(*args())
+            ent = cache[key] = (g, static_vg, out)
+        g, static_vg, out = ent
+        static_vg.copy_(vg)
+        g.replay()
+        return out[0].clone(), out[1].clone()

@@ -240,3 +240,37 @@ def test_headline_beam5_matches_torch_batched_beam():
     s_eng, s_ref = score(seq, lp), score(seq_ref, lp_ref)
     gap = (s_eng - s_ref).abs()
     assert (gap[~same] <= 0.02 * s_ref.abs()[~same] + 0.1).all(), (gap[~same], s_ref[~same])
+
+
+def test_headline_beam5_graph_replay_equals_eager():
+    """The beam decode replayed as a captured HIP graph (engine._beam_graphed)
+    equals the eager launches bit for bit, on two different batches through
+    the same graph, and after a weight update (the graph reads the engine's
+    in-place shadows)."""
+    import os
+    model, eng, loader = _headline_model(seed=4, drop=0.0)
+    model.eval()
+    batches = [loader.get_batch()['feats'] for _ in range(2)]
+    outs = {}
+    for mode in ('1', '0'):
+        os.environ['CSTCAP_BEAM_GRAPH'] = mode
+        try:
+            res = []
+            for feats in batches:
+                with torch.no_grad():
+                    res.append(eng.sample_beam(model, feats, {'beam_size': 5}))
+            w0 = model.logit.weight.detach().clone()
+            with torch.no_grad():
+                model.logit.weight.mul_(1.5)
+            eng.refresh_weights()
+            with torch.no_grad():
+                res.append(eng.sample_beam(model, batches[1], {'beam_size': 5}))
+                model.logit.weight.copy_(w0)
+            eng.refresh_weights()
+            outs[mode] = res
+        finally:
+            os.environ.pop('CSTCAP_BEAM_GRAPH', None)
+    assert getattr(eng, '_beam_graphs', None), 'the graphed beam path never ran'
+    for (s1, l1), (s0, l0) in zip(outs['1'], outs['0']):
+        assert torch.equal(s1, s0)
+        assert torch.equal(l1, l0)
