@@ -14,6 +14,13 @@ Captions are not noise: every video has a latent topic, features are a
 topic embedding plus noise, and caption words are drawn from a Zipf law over
 a topic-specific word permutation.  A model can therefore learn the task
 (used by the "loss decreases / CIDEr improves" integration tests).
+``caption_mode='template'`` makes the captions (nearly) a deterministic
+function of the features: each topic has one template sentence of
+topic-specific words, and every caption is that template with each word
+replaced by a random topic word with probability 0.15 and the last word
+dropped with probability 0.2 -- a greedy decoder that recovers the topic
+from the features scores a high CIDEr-D, so learning curves separate from
+noise (the Zipf captions' CIDEr-D stays near zero at the headline scale).
 
 The generator goes through the real preprocessing code path
 (tokens -> vocab -> label store -> df table), so synthetic artefacts are
@@ -39,10 +46,23 @@ def _captions_for(rng, topic_perm, n_words, ncap, mean_len, max_words, zipf_a):
     return caps
 
 
+def _template_captions(rng, template, topic_perm, n_words, ncap):
+    caps = []
+    for _ in range(ncap):
+        t = list(template)
+        if len(t) > 4 and rng.rand() < 0.2:
+            t = t[:-1]
+        for k in range(len(t)):
+            if rng.rand() < 0.15:
+                t[k] = 'w%d' % topic_perm[min(rng.zipf(1.35) - 1, n_words - 1)]
+        caps.append(t)
+    return caps
+
+
 def make_synthetic(kind='msrvtt', num_videos=None, vocab_size=10509, seq_length=30,
                    feat_dims=None, num_chunks=1, n_topics=64, seed=0, mean_len=9.3,
                    with_consensus=False, split='train', start_video_id=0, consensus_cols=20,
-                   world_seed=None):
+                   world_seed=None, caption_mode='zipf'):
     """``world_seed``: seed of the generative "world" (topic word
     distributions, topic feature embeddings); splits that share it are
     different videos of the same world, so a model trained on one
@@ -67,14 +87,24 @@ def make_synthetic(kind='msrvtt', num_videos=None, vocab_size=10509, seq_length=
                                   wrng.permutation(np.arange(min(32, n_words), n_words))])
                   for _ in range(n_topics)]
     topics = rng.randint(n_topics, size=num_videos)
+    if caption_mode not in ('zipf', 'template'):
+        raise ValueError('caption_mode must be zipf or template')
+    templates = None
+    if caption_mode == 'template':  # one sentence of topic-specific words per topic
+        templates = [['w%d' % topic_perm[k][32 + wrng.randint(min(400, n_words - 32))]
+                      for _ in range(int(wrng.randint(6, 13)))] for k in range(n_topics)]
     # Every word appears in the vocab: word ids are w0..w{n_words-1}, and the
     # vocabulary is built in id order (threshold 0), so ids are stable.
     words = ['w%d' % i for i in range(n_words)]
     vocab = SPECIALS + words
     videos = []
     for i in range(num_videos):
-        toks = _captions_for(rng, topic_perm[topics[i]], n_words, caps_per_video(), mean_len,
-                             seq_length + 6, 1.35)
+        if templates is not None:
+            toks = _template_captions(rng, templates[topics[i]], topic_perm[topics[i]], n_words,
+                                      caps_per_video())
+        else:
+            toks = _captions_for(rng, topic_perm[topics[i]], n_words, caps_per_video(),
+                                 mean_len, seq_length + 6, 1.35)
         videos.append({'video_id': start_video_id + i, 'captions': [' '.join(t) for t in toks],
                        'processed_tokens': toks, 'category': int(topics[i])})
     store = build_label_store(vocab, videos, seq_length)
@@ -107,19 +137,21 @@ def make_synthetic(kind='msrvtt', num_videos=None, vocab_size=10509, seq_length=
 
 def make_splits(kind='msrvtt', vocab_size=10509, seq_length=30, feat_dims=None,
                 num_chunks=1, train_videos=None, eval_videos=None, seed=0,
-                with_consensus=False, seq_per_img=20):
+                with_consensus=False, seq_per_img=20, caption_mode='zipf'):
     """(train, val, test) synthetic splits sharing one vocabulary."""
     # one generative world (topic vocabularies / feature embeddings) for all
     # three splits, different videos in each
     world = 10007 + seed
     tr = make_synthetic(kind, train_videos, vocab_size, seq_length, feat_dims, num_chunks,
                         seed=seed, with_consensus=with_consensus, consensus_cols=seq_per_img,
-                        world_seed=world)
+                        world_seed=world, caption_mode=caption_mode)
     n_eval = eval_videos or max(8, (train_videos or 600) // 10)
     va = make_synthetic(kind, n_eval, vocab_size, seq_length, feat_dims, num_chunks,
-                        seed=seed + 1, start_video_id=10 ** 6, world_seed=world)
+                        seed=seed + 1, start_video_id=10 ** 6, world_seed=world,
+                        caption_mode=caption_mode)
     te = make_synthetic(kind, n_eval, vocab_size, seq_length, feat_dims, num_chunks,
-                        seed=seed + 2, start_video_id=2 * 10 ** 6, world_seed=world)
+                        seed=seed + 2, start_video_id=2 * 10 ** 6, world_seed=world,
+                        caption_mode=caption_mode)
     # train df is the one used for CIDEr-D rewards on every split
     va.df = te.df = tr.df
     return tr, va, te

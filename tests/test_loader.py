@@ -119,3 +119,33 @@ def test_h5_without_h5py_is_a_clear_error(tmp_path):
         pytest.skip('h5py installed')
     with pytest.raises(RuntimeError, match='h5py'):
         load_label_file(str(tmp_path / 'x.h5'))
+
+
+def test_template_captions_follow_the_video_topic():
+    """caption_mode='template' (the learnable task of the learning-parity
+    runs): the captions of a video are noisy copies of its topic's template,
+    and the validation split shares the training split's templates."""
+    from cst_captioning_amd.data import make_splits
+    tr, va, _ = make_splits('msrvtt', vocab_size=2000, feat_dims=[64, 32], train_videos=200,
+                            seed=3, caption_mode='template')
+
+    def words(ds, vid):
+        return [c.split() for c in ds.gt_refs[vid]]
+
+    def agree(a, b):
+        n = min(len(a), len(b))
+        return sum(x == y for x, y in zip(a[:n], b[:n])) / max(len(a), len(b))
+
+    # the 20 captions of one video agree with each other on most positions
+    caps = words(tr, 0)
+    assert len(caps) == 20
+    assert sum(agree(caps[0], c) for c in caps[1:]) / 19 > 0.6
+    # validation videos' captions match some training video's (same world;
+    # a topic may be missing from 200 training videos)
+    firsts = [words(tr, v)[0] for v in list(tr.gt_refs)[:200]]
+    best = sorted(max(agree(words(va, 10 ** 6 + i)[0], c) for c in firsts) for i in range(10))
+    assert best[5] > 0.6, best
+    # the Zipf mode stays the default
+    tz, _, _ = make_splits('msrvtt', vocab_size=2000, feat_dims=[64, 32], train_videos=50, seed=3)
+    zc = [c.split() for c in tz.gt_refs[0]]
+    assert sum(agree(zc[0], c) for c in zc[1:]) / 19 < 0.5
