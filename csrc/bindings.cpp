@@ -18,6 +18,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 void set_grad_events(bool on);
 void grad_event_wait(int64_t k, int64_t stream);
 void grad_event_record(int64_t k, int64_t stream);
+void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
+                     int64_t n_cand);
+std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at::Tensor b,
+                                       bool tb);
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -147,6 +151,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("token_group_sum", &cst::token_group_sum);
   m.def("vocab_select", &cst::vocab_select);
   m.def("decode_step_test", &cst::decode_step_test);
+  m.def("gemm_bf16_tuned", &cst::gemm_bf16_tuned, py::arg("out"), py::arg("a"), py::arg("ta"),
+        py::arg("b"), py::arg("tb"), py::arg("n_cand") = 24);
+  m.def("gemm_tuned_timings", &cst::gemm_tuned_timings);
   m.def("set_grad_events", &cst::set_grad_events);
   m.def("grad_event_wait", &cst::grad_event_wait);
   m.def("grad_event_record", &cst::grad_event_record);

@@ -1321,9 +1321,12 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
   hipStream_t st = cur_stream();
   const int64_t ldl = (V + 7) / 8 * 8;
-  at::Tensor logits = at::empty({R, ldl}, f32);
-  at::Tensor lse = at::empty({R}, f32);
   const int n_vt = vocab_num_tiles((int)V);
+  // K <= 8: the vocab launch keeps each tile's K best logits per row (VF_TOPK)
+  // and the top-K merges n_vt * K candidates -- no R x V fp32 logits
+  const bool tile_topk = K <= 8;
+  at::Tensor logits = tile_topk ? at::empty({(int64_t)n_vt * R * K * 2}, f32) : at::empty({R, ldl}, f32);
+  at::Tensor lse = at::empty({R}, f32);
   at::Tensor part = at::empty({(int64_t)n_vt * R * vocab_partial_bytes() / 4}, f32);
   at::Tensor top_v = at::empty({R, K}, f32);
   at::Tensor top_i = at::empty({R, K}, i32);
@@ -1362,8 +1365,13 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   }
   for (int64_t t = 0; t < T - 1; ++t) {
     if (t >= 1) {
-      launch_beam_topk(logits.data_ptr<float>(), ldl, (int)V, (int)R, (int)K,
-                       lse.data_ptr<float>(), top_v.data_ptr<float>(), top_i.data_ptr<int>(), st);
+      if (tile_topk)
+        launch_beam_topk_cand(logits.data_ptr(), n_vt, (int)R, (int)K, lse.data_ptr<float>(),
+                              top_v.data_ptr<float>(), top_i.data_ptr<int>(), st);
+      else
+        launch_beam_topk(logits.data_ptr<float>(), ldl, (int)V, (int)R, (int)K,
+                         lse.data_ptr<float>(), top_v.data_ptr<float>(), top_i.data_ptr<int>(),
+                         st);
       launch_beam_step(top_v.data_ptr<float>(), top_i.data_ptr<int>(), (int)B, (int)K, (int)T,
                        (int)t, beam_sum.data_ptr<float>(), seq_hist.data_ptr<int64_t>(),
                        lp_hist.data_ptr<float>(), best_ppl.data_ptr<float>(),
@@ -1404,7 +1412,8 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
     launch_vocab_fwd(reinterpret_cast<const uint16_t*>(htop.data_ptr()), (int)H, (int)R, (int)H, W,
                      blog.data_ptr<float>(), (int)V,
                      reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl, part.data_ptr(),
-                     nullptr, 0, /*flags=*/8, 1.f, nullptr, (int)t, st);
+                     nullptr, 0, tile_topk ? (VF_TOPK_H | ((int)K << 8)) : /*fp32 logits*/ 8, 1.f,
+                     nullptr, (int)t, st);
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse.data_ptr<float>(), nullptr, 0,
                          nullptr, 0, nullptr, 0, nullptr, 0, SEL_GT_H, 0.f, nullptr, (int)t, nullptr,
                          0, nullptr, st);

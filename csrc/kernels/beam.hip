@@ -58,21 +58,33 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict_
 #pragma unroll
   for (int k = 0; k < BEAM_MAXK; ++k) bv[k] = -INFINITY, bi[k] = 0x7fffffff;
   float thr = -INFINITY;  // the list's K-th value
-  for (int v = threadIdx.x; v < V; v += 256) {
-    float cv = x[v];
-    if (!(cv > thr)) continue;
-    int ci = v;
+  // TK_U independent loads in flight per chunk, then the (mostly rejecting)
+  // insertions: one load at a time left the scan latency-bound (~50 us)
+  constexpr int TK_U = 8;
+  for (int v0 = threadIdx.x; v0 < V; v0 += 256 * TK_U) {
+    float xs[TK_U];
 #pragma unroll
-    for (int p = 0; p < BEAM_MAXK; ++p) {
-      if (p < K && cv > bv[p]) {
-        const float tv = bv[p];
-        const int ti = bi[p];
-        bv[p] = cv, bi[p] = ci;
-        cv = tv, ci = ti;
-      }
+    for (int u = 0; u < TK_U; ++u) {
+      const int v = v0 + 256 * u;
+      xs[u] = v < V ? x[v] : -INFINITY;
     }
 #pragma unroll
-    for (int p = 0; p < BEAM_MAXK; ++p) thr = p == K - 1 ? bv[p] : thr;
+    for (int u = 0; u < TK_U; ++u) {
+      float cv = xs[u];
+      if (!(cv > thr)) continue;
+      int ci = v0 + 256 * u;
+#pragma unroll
+      for (int p = 0; p < BEAM_MAXK; ++p) {
+        if (p < K && cv > bv[p]) {
+          const float tv = bv[p];
+          const int ti = bi[p];
+          bv[p] = cv, bi[p] = ci;
+          cv = tv, ci = ti;
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < BEAM_MAXK; ++p) thr = p == K - 1 ? bv[p] : thr;
+    }
   }
   // K rounds of wave arg-max over the lanes' list heads; the winner shifts
   for (int k = 0; k < K; ++k) {
@@ -104,6 +116,76 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(const float* __restrict_
       top_i[(int64_t)r * K + k] = besti;
     }
   }
+}
+
+// The same top-K from the vocab launch's per-tile candidates (VF_TOPK:
+// n_vt x K (logit, index) per row, each tile's list sorted): one wavefront per
+// row merges n_vt * K candidates instead of scanning V fp32 logits.
+__global__ __launch_bounds__(256) void beam_topk_cand_kernel(const float2* __restrict__ cand,
+                                                             int n_vt, int R, int K,
+                                                             const float* __restrict__ lse,
+                                                             float* __restrict__ top_v,
+                                                             int* __restrict__ top_i) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  constexpr int MK = 8;  // (VF_TOPK_MAXK)
+  float bv[MK];
+  int bi[MK];
+#pragma unroll
+  for (int k = 0; k < MK; ++k) bv[k] = -INFINITY, bi[k] = 0x7fffffff;
+  const int n = n_vt * K;
+  float thr = -INFINITY;
+  for (int c0 = lane; c0 < n; c0 += 64 * 4) {
+    float2 xs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + 64 * u;
+      // candidate c = (tile c / K, rank c % K) of row r
+      xs[u] = c < n ? cand[((int64_t)(c / K) * R + r) * K + c % K]
+                    : make_float2(-INFINITY, __int_as_float(0x7fffffff));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float cv = xs[u].x;
+      int ci = __float_as_int(xs[u].y);
+      if (!(cv > thr || (cv == thr && ci < 0x7fffffff))) continue;
+#pragma unroll
+      for (int p = 0; p < MK; ++p) {
+        if (p < K && (cv > bv[p] || (cv == bv[p] && ci < bi[p]))) {
+          const float tv = bv[p];
+          const int tix = bi[p];
+          bv[p] = cv, bi[p] = ci;
+          cv = tv, ci = tix;
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < MK; ++p) thr = p == K - 1 ? bv[p] : thr;
+    }
+  }
+  const float L = lse[r];
+  for (int k = 0; k < K; ++k) {
+    float best = bv[0];
+    int besti = bi[0];
+    wave_argmax(best, besti);
+    if (bi[0] == besti) {
+#pragma unroll
+      for (int p = 0; p + 1 < MK; ++p) bv[p] = bv[p + 1], bi[p] = bi[p + 1];
+      bv[MK - 1] = -INFINITY, bi[MK - 1] = 0x7fffffff;
+    }
+    if (lane == 0) {
+      top_v[(int64_t)r * K + k] = best - L;
+      top_i[(int64_t)r * K + k] = besti;
+    }
+  }
+}
+
+void launch_beam_topk_cand(const void* cand, int n_vt, int R, int K, const float* lse,
+                           float* top_v, int* top_i, hipStream_t stream) {
+  if (K < 1 || K > 8) throw std::runtime_error("beam_topk_cand: K must be in [1, 8]");
+  hipLaunchKernelGGL(beam_topk_cand_kernel, dim3((R + 3) / 4), dim3(256), 0, stream,
+                     (const float2*)cand, n_vt, R, K, lse, top_v, top_i);
+  post_launch("beam_topk_cand_kernel", stream);
 }
 
 // One wavefront per video.  State (per video b, beam q):
@@ -176,23 +258,31 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
     tok_out[b * K + v] = top_i[(int64_t)(b * K + q) * K + c];
     parent_out[b * K + v] = b * K + q;
   }
-  // harvest, in beam order (earliest wins ties)
+  // harvest, in beam order (earliest wins ties): lane 0 picks the winning
+  // beam, then the lanes copy its history in parallel (this block wrote it
+  // above; the barrier orders the copy after those stores)
+  __shared__ int s_win;
   if (lane == 0) {
+    int win = -1;
+    float bp = best_ppl[b];
     for (int v = 0; v < K; ++v) {
       const int j = s_sel[v], c = j / rows, q = j % rows;
       const int w = top_i[(int64_t)(b * K + q) * K + c];
       if (w == 0 || t == T - 2) {
         const float ppl = t > 1 ? __expf(-s_p[j] / (float)(t - 1)) : 10000.f;
-        if (ppl < best_ppl[b]) {
-          best_ppl[b] = ppl;
-          for (int pos = 0; pos < T; ++pos) {
-            best_seq[(int64_t)b * T + pos] = sh_new[(int64_t)(b * K + v) * T + pos];
-            best_lp[(int64_t)b * T + pos] = lh_new[(int64_t)(b * K + v) * T + pos];
-          }
-        }
+        if (ppl < bp) bp = ppl, win = v;
       }
     }
+    if (win >= 0) best_ppl[b] = bp;
+    s_win = win;
   }
+  __syncthreads();
+  const int win = s_win;
+  if (win >= 0)
+    for (int pos = lane; pos < T; pos += 64) {
+      best_seq[(int64_t)b * T + pos] = sh_new[(int64_t)(b * K + win) * T + pos];
+      best_lp[(int64_t)b * T + pos] = lh_new[(int64_t)(b * K + win) * T + pos];
+    }
 }
 
 void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,

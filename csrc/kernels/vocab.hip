@@ -78,7 +78,8 @@ struct GroupStat {  // 32 bytes, one per (lane group, row) in LDS (exp_stage_off
 #define VOCAB_TR_ARGS \
   hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, rng, step, eoff
 
-template <int BN, int STAGES>
+// TOPK (flags VF_TOPK, beam search only): the per-tile top-K candidates
+template <int BN, int STAGES, bool TOPK = false>
 __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARAMS) {
   using TL = Tile<VT_V, BN, STAGES>;  // M = vocab, N = caption rows
   constexpr int TM = TL::TM, TN = TL::TN;
@@ -159,7 +160,35 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
 #pragma unroll
       for (int k = 0; k < 16; ++k) x[i][k] = acc[i][j][k] + pb[i][k];
 
-    if ((flags & VF_SAVE_F32) && logits16 != nullptr && r < R) {  // fp32 logits (beam search)
+    if (TOPK && (flags & VF_TOPK)) {
+      // beam search: the lane's K best of its 32 logits (sorted, ties -> the
+      // smaller index), then the 4 lane groups of the row merged below
+      const int K = vf_topk_k(flags);
+      float tv[VF_TOPK_MAXK];
+      int ti[VF_TOPK_MAXK];
+#pragma unroll
+      for (int p = 0; p < VF_TOPK_MAXK; ++p) tv[p] = -INFINITY, ti[p] = 0x7fffffff;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          float cv = x[i][k];
+          int ci = vb + 32 * i + 8 * (k >> 2) + (k & 3);  // ascending in (i, k): ties keep the first
+#pragma unroll
+          for (int p = 0; p < VF_TOPK_MAXK; ++p) {
+            if (p < K && cv > tv[p]) {
+              const float a = tv[p];
+              const int b = ti[p];
+              tv[p] = cv, ti[p] = ci;
+              cv = a, ci = b;
+            }
+          }
+        }
+      float2* tk = reinterpret_cast<float2*>(lds + exp_stage_off(BN));  // [4 groups][BN rows][MAXK]
+#pragma unroll
+      for (int p = 0; p < VF_TOPK_MAXK; ++p)
+        tk[(g * BN + row_l) * VF_TOPK_MAXK + p] = make_float2(tv[p], __int_as_float(ti[p]));
+    } else if ((flags & VF_SAVE_F32) && logits16 != nullptr && r < R) {  // fp32 logits (beam search)
       float* dst = reinterpret_cast<float*>(logits16) + (int64_t)r * ldl;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -332,9 +361,29 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
       p.xtgt = a.xt;
       p.pad = 0.f;
       part[(int64_t)vt * R + r] = p;
+      if (TOPK && (flags & VF_TOPK)) {  // merge the row's 4 sorted group lists -> K candidates
+        const int K = vf_topk_k(flags);
+        const float2* tk = reinterpret_cast<const float2*>(lds + exp_stage_off(BN));
+        int hd4[4] = {0, 0, 0, 0};
+        float2* dst = reinterpret_cast<float2*>(logits16) + ((int64_t)vt * R + r) * K;
+        for (int k = 0; k < K; ++k) {
+          float bvv = -INFINITY;
+          int bii = 0x7fffffff, bq = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float2 c = hd4[q] < K ? tk[(q * BN + row_l) * VF_TOPK_MAXK + hd4[q]]
+                                        : make_float2(-INFINITY, __int_as_float(0x7fffffff));
+            const int ci = __float_as_int(c.y);
+            if (c.x > bvv || (c.x == bvv && ci < bii)) bvv = c.x, bii = ci, bq = q;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) hd4[q] += q == bq ? 1 : 0;
+          dst[k] = make_float2(bvv, __int_as_float(bii));
+        }
+      }
     }
   }
-  if (logits16 != nullptr && !(flags & VF_SAVE_F32)) {
+  if (logits16 != nullptr && !(flags & (VF_SAVE_F32 | VF_TOPK))) {
     // the staged 16-bit tile (exp store or fp16 logits, written before the
     // barrier above): 16 bytes
     // per thread and pass, 16 threads per 256-byte row segment; columns past
@@ -351,10 +400,10 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
   }
 }
 
-template <int BN, int STAGES, int OCC>
+template <int BN, int STAGES, int OCC, bool TOPK = false>
 __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(VOCAB_TR_PARAMS) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  vocab_tr_block<BN, STAGES>(blockIdx.x, lds, VOCAB_TR_ARGS);
+  vocab_tr_block<BN, STAGES, TOPK>(blockIdx.x, lds, VOCAB_TR_ARGS);
 }
 
 // the same attention workgroups as a launch of their own
@@ -757,7 +806,7 @@ __global__ __launch_bounds__(256) void vocab_exp_convert_kernel(uint16_t* __rest
 // -------------------------------------------------------------------------------
 // Launchers.  Tiles: 128 vocab x 64 caption rows, 2 LDS stages (48 KB, 3
 // blocks per CU).
-template <int BN, int STAGES, int OCC>
+template <int BN, int STAGES, int OCC, bool TOPK = false>
 static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
@@ -770,11 +819,11 @@ static void launch_vocab_fwd_tr(const uint16_t* hd, int ldh, int R, int H, const
   const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_fwd_tr_kernel<BN, STAGES, OCC>,
+    (void)hipFuncSetAttribute((const void*)vocab_fwd_tr_kernel<BN, STAGES, OCC, TOPK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((vocab_fwd_tr_kernel<BN, STAGES, OCC>), dim3(n_vt * n_rt), dim3(256), LDS,
+  hipLaunchKernelGGL((vocab_fwd_tr_kernel<BN, STAGES, OCC, TOPK>), dim3(n_vt * n_rt), dim3(256), LDS,
                      stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt,
                      tgt_stride, flags, inv_temp, rng, step, eoff);
   post_launch("vocab_fwd_tr_kernel", stream);
@@ -786,6 +835,13 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
                       const uint32_t* rng, int step, hipStream_t stream, const float* eoff) {
   // (microbenchmark at V = 10,509: 31.0 vs 33.5 us at R = 1280, 8.7 vs 12.4
   // us at R = 64 against 128-row tiles, 2 blocks per CU)
+  if (flags & VF_TOPK) {
+    if (vf_topk_k(flags) < 1 || vf_topk_k(flags) > VF_TOPK_MAXK)
+      throw std::runtime_error("vocab_fwd: VF_TOPK needs 1 <= K <= 8");
+    launch_vocab_fwd_tr<64, 2, 3, true>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt,
+                                        tgt_stride, flags, inv_temp, rng, step, stream, eoff);
+    return;
+  }
   launch_vocab_fwd_tr<64, 2, 3>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
                                 flags, inv_temp, rng, step, stream, eoff);
 }

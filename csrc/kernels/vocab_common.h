@@ -28,12 +28,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // VF_EXP: the saved copy is E = exp(x - eoff[r]) in bf16 instead of fp16 x
 // (eoff = the row's LSE of the previous decode step), see vocab_grad.hip
+constexpr int VF_TOPK_MAXK = 8;
+__host__ __device__ constexpr int vf_topk_k(int flags) { return (flags >> 8) & 15; }
 enum VocabFlags : int {
   VF_SAMPLE = 1,
   VF_ARGMAX = 2,
   VF_BENCH_MAINLOOP = 4,
   VF_SAVE_F32 = 8,
-  VF_EXP = 16
+  VF_EXP = 16,
+  // beam search: each (vocab tile, row) writes its TOPK_K(flags) best logits
+  // (value, index) to logits16 as float2 [n_vt][R][K] instead of fp32 logits
+  VF_TOPK = 32
 };
 
 }  // namespace cst

@@ -43,6 +43,9 @@ void launch_shadow_refresh(const float* p, const ShadowSegs& ss, hipStream_t str
 
 // vocab.hip
 enum SelModeHost : int { SEL_GT_H = 0, SEL_SAMPLE_H = 1, SEL_GREEDY_H = 2, SEL_SS_H = 3 };
+// vocab flag of the beam search's per-tile top-K candidates (kernels/vocab_common.h
+// VF_TOPK; the beam size in bits 8..11)
+constexpr int VF_TOPK_H = 32;
 int vocab_num_tiles(int V);
 void launch_vocab_fwd_variant(int variant, const uint16_t* hd, int ldh, int R, int H,
                               const uint16_t* W, const float* bias, int V, uint16_t* logits16,
@@ -332,6 +335,9 @@ enum StampSlot : int {
 };
 
 // beam.hip
+// the same top-K from the vocab launch's per-tile candidates (flags VF_TOPK)
+void launch_beam_topk_cand(const void* cand, int n_vt, int R, int K, const float* lse,
+                           float* top_v, int* top_i, hipStream_t stream);
 void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,
                       float* top_v, int* top_i, hipStream_t stream);
 void launch_beam_step(const float* top_v, const int* top_i, int B, int K, int T, int t,

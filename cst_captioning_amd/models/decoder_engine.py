@@ -684,7 +684,7 @@ class DecoderEngine:
 
     def _run(self, model, feats, labels, modes, want_xe, use_counts, use_unfinished,
              expand=True, ss_prob=0.0, drop=True, temperature=1.0, bos_rows=None,
-             want_full=False):
+             want_full=False, rows_per_video=None):
         if self.attention:
             att, B = self._att_inputs(model, feats)
             vg = None
@@ -693,7 +693,7 @@ class DecoderEngine:
             att = (None,) * 5
         from ..utils import stamps
         stamps.mark_fwd('vgate')
-        S = model.feat_expander.n if expand else 1
+        S = rows_per_video or (model.feat_expander.n if expand else 1)
         h0 = c0 = None
         if self.standard:
             h0, c0 = self._initial_state(model, feats)
@@ -779,10 +779,28 @@ class DecoderEngine:
         expand = opt.get('expand_feat', 0) == 1
         T = model.seq_length - 1
         modes = [SEL_GREEDY if sample_max == 1 else SEL_SAMPLE] * (T - 1)
+        # temporal attention, one greedy row per video (the SCST baseline):
+        # decode each video on TWO identical rows, so the MFMA attention of
+        # the decode launch applies (it needs >= 2 rows per video, vocab.hip
+        # att_mfma_ok) instead of a VALU attention launch + a query GEMM per
+        # step; greedy rows are deterministic, row 0 of each pair is kept
+        dup = (self.attention and not self.manet and not expand and sample_max == 1
+               and self._att_mfma_shape_ok(model))
         seq, lp, _, _ = self._run(model, feats, None, modes, want_xe=False, use_counts=False,
                                   use_unfinished=True, expand=expand, drop=False,
-                                  temperature=temperature)
+                                  temperature=temperature, rows_per_video=2 if dup else None)
+        if dup:
+            seq, lp = seq[0::2].contiguous(), lp[0::2].contiguous()
         return seq, lp
+
+    def _att_mfma_shape_ok(self, model):
+        """The MFMA attention's shape limits (csrc/kernels/vocab.hip
+        att_mfma_ok, shared scorer): frames <= 16, A % 64 == 0 and <= 1024,
+        64 <= H <= 512 with H % 32 == 0."""
+        C = getattr(model, 'num_chunks', 1)
+        A, H = self.att_dim, self.H
+        return (1 <= C <= 16 and A % 64 == 0 and A <= 1024 and H % 32 == 0 and 64 <= H <= 512
+                and os.environ.get('CSTCAP_GREEDY_DUP', '1') != '0')
 
     @torch.no_grad()
     def sample_beam(self, model, feats, opt):

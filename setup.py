@@ -78,7 +78,8 @@ class BuildWithHip(BuildExtension):
 SANITIZE = os.environ.get('CSTCAP_HOST_SANITIZE') == '1'
 ext = CppExtension(
     'cst_captioning_amd._C_san' if SANITIZE else 'cst_captioning_amd._C',
-    ['csrc/engine.cpp', 'csrc/bindings.cpp', 'csrc/host/cider_host.cpp'],
+    ['csrc/engine.cpp', 'csrc/bindings.cpp', 'csrc/host/cider_host.cpp',
+     'csrc/host/blaslt_tuned.cpp'],
     include_dirs=[os.path.join(HERE, 'csrc')] + include_paths(device_type='cuda'),
     define_macros=[('__HIP_PLATFORM_AMD__', '1'), ('USE_ROCM', '1')]
     + ([('_GLIBCXX_ASSERTIONS', '1')] if SANITIZE else []),
@@ -88,7 +89,7 @@ ext = CppExtension(
     extra_link_args=['-fsanitize=undefined'] if SANITIZE else [],
     extra_objects=hip_objects(),
     library_dirs=[os.path.join(ROCM, 'lib')],
-    libraries=['amdhip64', 'c10_hip', 'torch_hip'],
+    libraries=['amdhip64', 'c10_hip', 'torch_hip', 'hipblaslt'],
 )
 
 setup(

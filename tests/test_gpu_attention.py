@@ -133,3 +133,34 @@ def test_attention_greedy_and_beam_match_torch(H, S):
         b, _ = eng.sample_beam(model, data['feats'], {'beam_size': K})
         assert b.shape == b_ref.shape
         assert (b == b_ref).all(1).float().mean().item() >= 0.8, (K, b, b_ref)
+
+
+@pytest.mark.parametrize('H', [64, 512])
+def test_attention_greedy_on_duplicated_rows_equals_one_row(H):
+    """The SCST greedy baseline under temporal attention decodes each video on
+    two identical rows (engine.sample: the MFMA attention of the decode
+    launch needs >= 2 rows per video): the kept rows equal the one-row decode
+    through the VALU attention launches, tokens exactly, log-probs to fp32
+    rounding."""
+    import os
+    ds, opt, model, loader = _tiny(C=8, seed=5, H=H, S=5)
+    with torch.no_grad():
+        model.logit.weight.mul_(3.0)
+    eng = _engine(model, opt)
+    model.eval()
+    data = loader.get_batch()
+    assert eng._att_mfma_shape_ok(model)
+    outs = {}
+    for dup in ('1', '0'):
+        os.environ['CSTCAP_GREEDY_DUP'] = dup
+        try:
+            with torch.no_grad():
+                outs[dup] = eng.sample(model, data['feats'], {'sample_max': 1})
+        finally:
+            os.environ.pop('CSTCAP_GREEDY_DUP', None)
+    (s1, l1), (s0, l0) = outs['1'], outs['0']
+    assert s1.shape == s0.shape
+    # bf16 video gates (MFMA path) vs fp32 (VALU path): rare near-ties may flip
+    assert (s1 == s0).all(1).float().mean().item() >= 0.9
+    same = (s1 == s0).all(1)
+    torch.testing.assert_close(l1[same], l0[same], rtol=2e-2, atol=2e-2)
