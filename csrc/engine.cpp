@@ -53,6 +53,20 @@ void stamp_buffer(at::Tensor buf) {
 }
 void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
 
+void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
+                     int64_t n_cand);
+// The vocab head's backward GEMMs through the measured hipBLASLt algorithm
+// choice (host/blaslt_tuned.cpp) instead of PyTorch's heuristic first choice
+// when CSTCAP_TUNED_GEMM=1 (A/B runs; off by default)
+static bool tuned_gemm_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CSTCAP_TUNED_GEMM");
+    on = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return on == 1;
+}
+
 // X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
 // fp32, on the current stream (engine.launch_x; the same GEMM as the
 // backward's dHd chunks)
@@ -67,7 +81,12 @@ void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
   at::Tensor dst = out.view({NR, H});
   // (a 3-way split-K batch measured slower: 3.74 vs 3.67-3.73 ms per step,
   // profiles/r3/ab_xsplitk.txt)
-  at::mm_out(dst, logits16.view({NR, logits16.size(2)}).narrow(1, 0, V), wlog, at::kFloat);
+  at::Tensor Ev = logits16.view({NR, logits16.size(2)}).narrow(1, 0, V);
+  if (tuned_gemm_enabled()) {
+    gemm_bf16_tuned(dst, Ev, false, wlog, false, 32);
+    return;
+  }
+  at::mm_out(dst, Ev, wlog, at::kFloat);
 }
 int64_t wall_clock_khz() {
   int dev = 0, khz = 0;
@@ -708,6 +727,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
   auto dw_gemm = [&]() {  // (current stream: side)
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
+    if (tuned_gemm_enabled()) {  // one GEMM, the measured algorithm (split-K inside it)
+      gemm_bf16_tuned(dWlog, Ev, true, rhs, false, 32);
+      return;
+    }
     if (dw_split == 1) {
       at::mm_out(dWlog, Ev.t(), rhs, at::kFloat);
       return;
