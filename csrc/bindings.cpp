@@ -83,6 +83,9 @@ void stamp_buffer(at::Tensor buf);
 void stamp_now(int64_t slot);
 int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
+void gemm_nt_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant);
+bool gemm_nt_sk_ok(int64_t M, int64_t N, int64_t K, int64_t variant);
+at::Tensor transpose_pad_bf16(at::Tensor w, int64_t ldo);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -168,4 +171,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stamp_now", &cst::stamp_now);
   m.def("wall_clock_khz", &cst::wall_clock_khz);
   m.def("vocab_x", &cst::vocab_x);
+  m.def("gemm_nt_sk", &cst::gemm_nt_sk, py::arg("out"), py::arg("a"), py::arg("b"),
+        py::arg("variant") = -1);
+  m.def("gemm_nt_sk_ok", &cst::gemm_nt_sk_ok);
+  m.def("transpose_pad_bf16", &cst::transpose_pad_bf16);
 }

@@ -67,6 +67,74 @@ static bool tuned_gemm_enabled() {
   return on == 1;
 }
 
+// Hand-written persistent GEMM (kernels/gemm_sk.hip): out (M x N fp32) =
+// a (M x K) b (N x K)^T, both bf16 with unit column stride and 16-byte-aligned
+// rows.  Shapes it does not tile (M % 256, N % BN, K % 64) are refused.
+// variant: 0 = 256 x 256 tiles, 2 LDS stages; 1 = 256 x 128 tiles, 3 stages.
+static int sk_default_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CSTCAP_SK_VARIANT");
+    v = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return v;
+}
+bool gemm_nt_sk_ok(int64_t M, int64_t N, int64_t K, int64_t variant) {
+  const int64_t BN = variant == 1 ? 128 : 256;
+  return M > 0 && M % 256 == 0 && N % BN == 0 && K % 64 == 0 && K > 0 && M < (1 << 30);
+}
+void gemm_nt_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant) {
+  if (variant < 0) variant = sk_default_variant();
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && a.scalar_type() == at::kBFloat16 &&
+                  b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kFloat &&
+                  a.dim() == 2 && b.dim() == 2 && out.dim() == 2 && a.stride(1) == 1 &&
+                  b.stride(1) == 1 && out.stride(1) == 1,
+              "gemm_nt_sk: bf16 a (M, K), b (N, K) with unit column stride, fp32 out (M, N)");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_nt_sk: shapes");
+  TORCH_CHECK(gemm_nt_sk_ok(M, N, K, variant), "gemm_nt_sk: M % 256, N % ",
+              variant == 1 ? 128 : 256, ", K % 64 must be 0 (got ", M, ", ", N, ", ", K, ")");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+              "gemm_nt_sk: 16-byte-aligned rows");
+  TORCH_CHECK(a.stride(0) * 2 * 256 < (int64_t(1) << 31) && b.stride(0) * 2 * 256 < (int64_t(1) << 31),
+              "gemm_nt_sk: tile byte offsets must fit 31 bits");
+  int dev = 0, G = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&G, hipDeviceAttributeMultiprocessorCount, dev);
+  TORCH_CHECK(G % 8 == 0, "gemm_nt_sk: CU count must be a multiple of the 8 XCDs");
+  int64_t n_cnt = 0, n_slab = 0;
+  gemm_sk_plan((int)M, (int)N, (int)K, G, (int)variant, &n_cnt, &n_slab);
+  auto opts = out.options();
+  at::Tensor cnt = at::zeros({std::max<int64_t>(n_cnt, 1)}, opts.dtype(at::kInt));
+  at::Tensor slab = at::empty({std::max<int64_t>(n_slab, 1)}, opts);
+  launch_gemm_nt_sk(reinterpret_cast<const uint16_t*>(a.data_ptr()), a.stride(0),
+                    reinterpret_cast<const uint16_t*>(b.data_ptr()), b.stride(0),
+                    out.data_ptr<float>(), out.stride(0), (int)M, (int)N, (int)K, G, (int)variant,
+                    slab.data_ptr<float>(), cnt.data_ptr<int>(), cur_stream());
+}
+// W (rows x cols bf16) -> W^T (cols x ldo), zero columns past rows
+at::Tensor transpose_pad_bf16(at::Tensor w, int64_t ldo) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 &&
+                  w.is_contiguous() && ldo >= w.size(0),
+              "transpose_pad_bf16: contiguous bf16 (rows, cols), ldo >= rows");
+  at::Tensor out = at::empty({w.size(1), ldo}, w.options());
+  launch_transpose_pad_bf16(reinterpret_cast<const uint16_t*>(w.data_ptr()), (int)w.size(0),
+                            (int)w.size(1), reinterpret_cast<uint16_t*>(out.data_ptr()), ldo,
+                            cur_stream());
+  return out;
+}
+// X = E W through the hand-written GEMM when CSTCAP_SK_GEMM=1 (A/B runs)
+static bool sk_gemm_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CSTCAP_SK_GEMM");
+    on = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return on == 1;
+}
+
 // X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
 // fp32, on the current stream (engine.launch_x; the same GEMM as the
 // backward's dHd chunks)
@@ -81,7 +149,14 @@ void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
   at::Tensor dst = out.view({NR, H});
   // (a 3-way split-K batch measured slower: 3.74 vs 3.67-3.73 ms per step,
   // profiles/r3/ab_xsplitk.txt)
-  at::Tensor Ev = logits16.view({NR, logits16.size(2)}).narrow(1, 0, V);
+  const int64_t ldl = logits16.size(2);
+  if (sk_gemm_enabled() && gemm_nt_sk_ok(NR, H, ldl, sk_default_variant())) {
+    // the exp store's columns past V hold 0 up to ldl (kernels/vocab.hip), and
+    // W^T's padded columns are 0: K = ldl, no tail
+    gemm_nt_sk(dst, logits16.view({NR, ldl}), transpose_pad_bf16(wlog, ldl), -1);
+    return;
+  }
+  at::Tensor Ev = logits16.view({NR, ldl}).narrow(1, 0, V);
   if (tuned_gemm_enabled()) {
     gemm_bf16_tuned(dst, Ev, false, wlog, false, 32);
     return;
