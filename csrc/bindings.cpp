@@ -84,6 +84,7 @@ void stamp_now(int64_t slot);
 int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
 void gemm_nt_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant);
+void gemm_tn_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant);
 bool gemm_nt_sk_ok(int64_t M, int64_t N, int64_t K, int64_t variant);
 at::Tensor transpose_pad_bf16(at::Tensor w, int64_t ldo);
 
@@ -172,6 +173,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wall_clock_khz", &cst::wall_clock_khz);
   m.def("vocab_x", &cst::vocab_x);
   m.def("gemm_nt_sk", &cst::gemm_nt_sk, py::arg("out"), py::arg("a"), py::arg("b"),
+        py::arg("variant") = -1);
+  m.def("gemm_tn_sk", &cst::gemm_tn_sk, py::arg("out"), py::arg("a"), py::arg("b"),
         py::arg("variant") = -1);
   m.def("gemm_nt_sk_ok", &cst::gemm_nt_sk_ok);
   m.def("transpose_pad_bf16", &cst::transpose_pad_bf16);

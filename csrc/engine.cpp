@@ -68,8 +68,9 @@ static bool tuned_gemm_enabled() {
 }
 
 // Hand-written persistent GEMM (kernels/gemm_sk.hip): out (M x N fp32) =
-// a (M x K) b (N x K)^T, both bf16 with unit column stride and 16-byte-aligned
-// rows.  Shapes it does not tile (M % 256, N % BN, K % 64) are refused.
+// a (M x K) b (N x K)^T or a (K x M)^T b (K x N), bf16 operands with unit
+// column stride and 16-byte-aligned rows.  Shapes it does not tile (N % BN,
+// K % 64) are refused; M is free (the edge tile's rows past M are dropped).
 // variant: 0 = 256 x 256 tiles, 2 LDS stages; 1 = 256 x 128 tiles, 3 stages.
 static int sk_default_variant() {
   static int v = -1;
@@ -81,38 +82,59 @@ static int sk_default_variant() {
 }
 bool gemm_nt_sk_ok(int64_t M, int64_t N, int64_t K, int64_t variant) {
   const int64_t BN = variant == 1 ? 128 : 256;
-  return M > 0 && M % 256 == 0 && N % BN == 0 && K % 64 == 0 && K > 0 && M < (1 << 30);
+  return M > 0 && N > 0 && N % BN == 0 && K % 64 == 0 && K > 0 && M < (1 << 30);
 }
-void gemm_nt_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant) {
+static int64_t readable_bytes(const at::Tensor& t) {
+  return (int64_t)t.storage().nbytes() - t.storage_offset() * (int64_t)t.element_size();
+}
+// trans = false: out = a b^T, a (M x K), b (N x K).  trans = true: out =
+// a^T b, a (K x M), b (K x N) (both operands M / N-contiguous).
+static void gemm_sk(at::Tensor out, at::Tensor a, at::Tensor b, bool trans, int64_t variant) {
   if (variant < 0) variant = sk_default_variant();
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && a.scalar_type() == at::kBFloat16 &&
                   b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kFloat &&
                   a.dim() == 2 && b.dim() == 2 && out.dim() == 2 && a.stride(1) == 1 &&
                   b.stride(1) == 1 && out.stride(1) == 1,
-              "gemm_nt_sk: bf16 a (M, K), b (N, K) with unit column stride, fp32 out (M, N)");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_nt_sk: shapes");
-  TORCH_CHECK(gemm_nt_sk_ok(M, N, K, variant), "gemm_nt_sk: M % 256, N % ",
-              variant == 1 ? 128 : 256, ", K % 64 must be 0 (got ", M, ", ", N, ", ", K, ")");
+              "gemm_sk: bf16 a, b with unit column stride, fp32 out with unit column stride");
+  const int64_t M = trans ? a.size(1) : a.size(0), K = trans ? a.size(0) : a.size(1);
+  const int64_t N = trans ? b.size(1) : b.size(0);
+  TORCH_CHECK((trans ? b.size(0) : b.size(1)) == K && out.size(0) == M && out.size(1) == N,
+              "gemm_sk: shapes");
+  TORCH_CHECK(gemm_nt_sk_ok(M, N, K, variant), "gemm_sk: N % ", variant == 1 ? 128 : 256,
+              " and K % 64 must be 0 (got M ", M, ", N ", N, ", K ", K, ")");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
-              "gemm_nt_sk: 16-byte-aligned rows");
-  TORCH_CHECK(a.stride(0) * 2 * 256 < (int64_t(1) << 31) && b.stride(0) * 2 * 256 < (int64_t(1) << 31),
-              "gemm_nt_sk: tile byte offsets must fit 31 bits");
+              "gemm_sk: 16-byte-aligned rows");
+  if (trans) {
+    TORCH_CHECK(a.stride(0) >= M && K * a.stride(0) * 2 < (int64_t(1) << 31) &&
+                    K * b.stride(0) * 2 < (int64_t(1) << 31) && out.stride(0) * M * 4 < (int64_t(1) << 31),
+                "gemm_sk (trans): operand / output byte offsets must fit 31 bits");
+  } else {
+    TORCH_CHECK(a.stride(0) * 2 * 256 < (int64_t(1) << 31) &&
+                    b.stride(0) * 2 * 256 < (int64_t(1) << 31) &&
+                    out.stride(0) * 4 * 256 < (int64_t(1) << 31),
+                "gemm_sk: tile byte offsets must fit 31 bits");
+  }
   int dev = 0, G = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&G, hipDeviceAttributeMultiprocessorCount, dev);
-  TORCH_CHECK(G % 8 == 0, "gemm_nt_sk: CU count must be a multiple of the 8 XCDs");
+  TORCH_CHECK(G % 8 == 0, "gemm_sk: CU count must be a multiple of the 8 XCDs");
   int64_t n_cnt = 0, n_slab = 0;
   gemm_sk_plan((int)M, (int)N, (int)K, G, (int)variant, &n_cnt, &n_slab);
   auto opts = out.options();
   at::Tensor cnt = at::zeros({std::max<int64_t>(n_cnt, 1)}, opts.dtype(at::kInt));
   at::Tensor slab = at::empty({std::max<int64_t>(n_slab, 1)}, opts);
-  launch_gemm_nt_sk(reinterpret_cast<const uint16_t*>(a.data_ptr()), a.stride(0),
-                    reinterpret_cast<const uint16_t*>(b.data_ptr()), b.stride(0),
-                    out.data_ptr<float>(), out.stride(0), (int)M, (int)N, (int)K, G, (int)variant,
-                    slab.data_ptr<float>(), cnt.data_ptr<int>(), cur_stream());
+  launch_gemm_sk(reinterpret_cast<const uint16_t*>(a.data_ptr()), a.stride(0), readable_bytes(a),
+                 reinterpret_cast<const uint16_t*>(b.data_ptr()), b.stride(0), readable_bytes(b),
+                 out.data_ptr<float>(), out.stride(0), (int)M, (int)N, (int)K, trans, G,
+                 (int)variant, slab.data_ptr<float>(), cnt.data_ptr<int>(), cur_stream());
+}
+void gemm_nt_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant) {
+  gemm_sk(out, a, b, false, variant);
+}
+void gemm_tn_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant) {
+  gemm_sk(out, a, b, true, variant);
 }
 // W (rows x cols bf16) -> W^T (cols x ldo), zero columns past rows
 at::Tensor transpose_pad_bf16(at::Tensor w, int64_t ldo) {
@@ -125,15 +147,21 @@ at::Tensor transpose_pad_bf16(at::Tensor w, int64_t ldo) {
                             cur_stream());
   return out;
 }
-// X = E W through the hand-written GEMM when CSTCAP_SK_GEMM=1 (A/B runs)
-static bool sk_gemm_enabled() {
-  static int on = -1;
-  if (on < 0) {
+// The vocab head's backward GEMMs through the hand-written GEMM (A/B runs):
+// CSTCAP_SK_GEMM=1 both, =x X = E W only, =d dW_logit only; default off
+// (interleaved full-step A/B: 3.80-3.81 vs 3.68-3.70 ms per step with both,
+// profiles/r4/README_r4.md)
+static int sk_gemm_mask() {
+  static int m = -1;
+  if (m < 0) {
     const char* e = getenv("CSTCAP_SK_GEMM");
-    on = (e != nullptr && e[0] == '1') ? 1 : 0;
+    m = 0;
+    if (e != nullptr) m = e[0] == '1' ? 3 : e[0] == 'x' ? 1 : e[0] == 'd' ? 2 : 0;
   }
-  return on == 1;
+  return m;
 }
+static bool sk_gemm_enabled() { return (sk_gemm_mask() & 1) != 0; }
+static bool sk_gemm_dw_enabled() { return (sk_gemm_mask() & 2) != 0; }
 
 // X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
 // fp32, on the current stream (engine.launch_x; the same GEMM as the
@@ -802,6 +830,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
   auto dw_gemm = [&]() {  // (current stream: side)
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
+    if (sk_gemm_dw_enabled() && gemm_nt_sk_ok(V, H, NR, sk_default_variant())) {
+      gemm_tn_sk(dWlog, Ev, rhs, -1);  // E'^T (K = NR rows) x rhs, hand-written
+      return;
+    }
     if (tuned_gemm_enabled()) {  // one GEMM, the measured algorithm (split-K inside it)
       gemm_bf16_tuned(dWlog, Ev, true, rhs, false, 32);
       return;

@@ -44,8 +44,15 @@ namespace cst {
 
 namespace {
 
-template <int BN_, int STAGES_>
+// TRANS_: operand layout.  false ("NT"): A (M x K) and B (N x K) K-contiguous,
+// LDS images [row][64 k] read by ds_read_b128.  true ("TN"): A stored (K x M)
+// and B (K x N), M / N contiguous (dW = E'^T Hs: both operands have the
+// reduction index as their row); LDS images [64 k][BM or BN] filled by the
+// same lane-linear LDS-DMA, 16-byte chunks XOR-swizzled by (k & 3) << 2, and
+// the MFMA fragments read with ds_read_b64_tr_b16 (two per fragment).
+template <int BN_, int STAGES_, bool TRANS_ = false>
 struct SkCfg {
+  static constexpr bool TRANS = TRANS_;
   static constexpr int BM = 256, BN = BN_, BK = 64, THREADS = 512, STAGES = STAGES_;
   static constexpr int WAVES_M = 2, WAVES_N = 4;
   static constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;  // per-wave sub-tile
@@ -55,19 +62,25 @@ struct SkCfg {
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int LDS_BYTES = STAGES * STAGE_BYTES + 16;  // + the last-arriver flag
   static constexpr int NI = A_INS + B_INS;
+  // TN images: 16-byte chunks per k-row, k-rows per DMA wave-instruction
+  static constexpr int A_CPR = BM / 8, B_CPR = BN / 8;
+  static constexpr int A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;
+  static_assert(!TRANS || (A_CPR >= 16 && B_CPR >= 16 && 64 % A_CPR == 0 && 64 % B_CPR == 0),
+                "TN images: >= 16 chunks per k-row");
   static_assert(TM >= 1 && TN >= 1 && WN % 32 == 0, "tile");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
 struct SkArgs {
-  const uint16_t* A;  // M x K, row stride lda (elements)
-  const uint16_t* B;  // N x K, row stride ldb
+  const uint16_t* A;  // NT: M x K, row stride lda (elements); TN: K x M
+  const uint16_t* B;  // NT: N x K, row stride ldb; TN: K x N
+  int64_t a_bytes, b_bytes;  // readable bytes from A / B (buffer-resource bounds)
   float* C;           // M x N, row stride ldc
   float* slab;        // phase-2 partials: [rem tile][piece][BM * BN]
   int* cnt;           // phase-2 tickets, one per remainder tile (zeroed by the caller)
   int64_t lda, ldb, ldc;
   int M, N, nk;       // nk = K / 64
-  int tiles_n;        // N / BN
+  int tiles_n;        // N / BN (tiles_m = ceil(M / BM))
   int full_rounds;    // phase 1: whole tiles per workgroup
   int rem;            // phase 2: tiles split over all workgroups
   int pmax;           // slab pieces reserved per remainder tile
@@ -79,10 +92,36 @@ __device__ __forceinline__ int sk_owner(int64_t x, int64_t I, int G) {
   return (int)(((x + 1) * G + I - 1) / I - 1);
 }
 
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+
+// TN image byte offset of (k-row, column): chunk XOR (row & 3) << 2
+template <int ROWB>
+__device__ __forceinline__ int tn_off(int row, int col) {
+  return row * ROWB + ((((col >> 3) ^ ((row & 3) << 2))) << 4) + ((col & 7) << 1);
+}
+
+// one 32x32x16 operand fragment from a TN image: lane l holds column
+// c0 + (l & 31), k = k0 + 8 (l >> 5) + j; ds_read_b64_tr_b16 per 16-lane
+// group g delivers 4 k-rows x 16 columns, lane 4q + p addressing row q,
+// columns 4p .. 4p + 3 (two reads: k-rows 0-3 and 4-7 of the lane's half)
+template <int ROWB>
+__device__ __forceinline__ bf16x8 tn_frag(const char* img, int c0, int k0, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int row = k0 + 8 * (g >> 1) + (li >> 2);
+  const int col = c0 + 16 * (g & 1) + 4 * (li & 3);
+  typedef __attribute__((address_space(3))) v4i16 lds_v4;
+  const char* p0 = img + tn_off<ROWB>(row, col);
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0 + 4 * ROWB));
+  const v8i16 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 template <class CF>
 __device__ __forceinline__ void sk_mainloop(int kt0, int kt1, rsrc_t ra, const int (&va)[CF::A_INS],
-                                            rsrc_t rb, const int (&vb)[CF::B_INS], char* lds,
-                                            f32x16 (&acc)[CF::TM][CF::TN]) {
+                                            rsrc_t rb, const int (&vb)[CF::B_INS], int sa, int sb,
+                                            char* lds, f32x16 (&acc)[CF::TM][CF::TN]) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int wr = w / CF::WAVES_N, wc = w % CF::WAVES_N;
@@ -97,9 +136,9 @@ __device__ __forceinline__ void sk_mainloop(int kt0, int kt1, rsrc_t ra, const i
     char* As = lds + buf * CF::STAGE_BYTES;
     char* Bs = As + CF::A_BYTES;
 #pragma unroll
-    for (int i = 0; i < CF::A_INS; ++i) glds16(ra, va[i], kt * 128, As + 1024 * (w + 8 * i));
+    for (int i = 0; i < CF::A_INS; ++i) glds16(ra, va[i], kt * sa, As + 1024 * (w + 8 * i));
 #pragma unroll
-    for (int i = 0; i < CF::B_INS; ++i) glds16(rb, vb[i], kt * 128, Bs + 1024 * (w + 8 * i));
+    for (int i = 0; i < CF::B_INS; ++i) glds16(rb, vb[i], kt * sb, Bs + 1024 * (w + 8 * i));
   };
   const int n = kt1 - kt0;
 #pragma unroll
@@ -118,12 +157,21 @@ __device__ __forceinline__ void sk_mainloop(int kt0, int kt1, rsrc_t ra, const i
     for (int s = 0; s < 4; ++s) {
       const int c = 2 * s + (lane >> 5);
       bf16x8 af[CF::TM], bfr[CF::TN];
+      if constexpr (CF::TRANS) {
 #pragma unroll
-      for (int i = 0; i < CF::TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + swz(wr * CF::WM + i * 32 + (lane & 31), c));
+        for (int i = 0; i < CF::TM; ++i)
+          af[i] = tn_frag<CF::BM * 2>(As, wr * CF::WM + i * 32, 16 * s, lane);
 #pragma unroll
-      for (int j = 0; j < CF::TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wc * CF::WN + j * 32 + (lane & 31), c));
+        for (int j = 0; j < CF::TN; ++j)
+          bfr[j] = tn_frag<CF::BN * 2>(Bs, wc * CF::WN + j * 32, 16 * s, lane);
+      } else {
+#pragma unroll
+        for (int i = 0; i < CF::TM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(As + swz(wr * CF::WM + i * 32 + (lane & 31), c));
+#pragma unroll
+        for (int j = 0; j < CF::TN; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wc * CF::WN + j * 32 + (lane & 31), c));
+      }
 #pragma unroll
       for (int i = 0; i < CF::TM; ++i)
 #pragma unroll
@@ -134,47 +182,77 @@ __device__ __forceinline__ void sk_mainloop(int kt0, int kt1, rsrc_t ra, const i
   __syncthreads();  // every wave done with the staging buffers before the next tile's DMA
 }
 
-// per-lane DMA source offsets (bytes from the tile's first row) and the
-// buffer resources of one tile
+// per-lane DMA source offsets (bytes from the tile's origin) and the buffer
+// resources of one tile (bounded by the operand's last byte: reads past it
+// return 0)
 template <class CF>
 __device__ __forceinline__ void sk_tile_src(const SkArgs& g, int m0, int n0, rsrc_t& ra,
                                             int (&va)[CF::A_INS], rsrc_t& rb,
                                             int (&vb)[CF::B_INS]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t la = g.lda * 2, lb = g.ldb * 2;
-  ra = make_rsrc(g.A + (int64_t)m0 * g.lda, (int64_t)CF::BM * la);
-  rb = make_rsrc(g.B + (int64_t)n0 * g.ldb, (int64_t)CF::BN * lb);
+  if constexpr (CF::TRANS) {
+    // origin = column m0 (n0) of k-row 0; DMA instruction i of wave w fills
+    // k-rows RPI (w + 8 i) .. +RPI-1, lane l physical chunk l % CPR
+    ra = make_rsrc(g.A + m0, g.a_bytes - 2 * (int64_t)m0);
+    rb = make_rsrc(g.B + n0, g.b_bytes - 2 * (int64_t)n0);
 #pragma unroll
-  for (int i = 0; i < CF::A_INS; ++i) {
-    const int row = 8 * (w + 8 * i) + (lane >> 3);
-    va[i] = (int)(row * la) + 16 * dma_chunk(row, lane);
-  }
+    for (int i = 0; i < CF::A_INS; ++i) {
+      const int row = CF::A_RPI * (w + 8 * i) + lane / CF::A_CPR;
+      va[i] = (int)(row * la) + 16 * ((lane % CF::A_CPR) ^ ((row & 3) << 2));
+    }
 #pragma unroll
-  for (int i = 0; i < CF::B_INS; ++i) {
-    const int row = 8 * (w + 8 * i) + (lane >> 3);
-    vb[i] = (int)(row * lb) + 16 * dma_chunk(row, lane);
+    for (int i = 0; i < CF::B_INS; ++i) {
+      const int row = CF::B_RPI * (w + 8 * i) + lane / CF::B_CPR;
+      vb[i] = (int)(row * lb) + 16 * ((lane % CF::B_CPR) ^ ((row & 3) << 2));
+    }
+  } else {
+    ra = make_rsrc(g.A + (int64_t)m0 * g.lda, g.a_bytes - (int64_t)m0 * la);
+    rb = make_rsrc(g.B + (int64_t)n0 * g.ldb, g.b_bytes - (int64_t)n0 * lb);
+#pragma unroll
+    for (int i = 0; i < CF::A_INS; ++i) {
+      const int row = 8 * (w + 8 * i) + (lane >> 3);
+      va[i] = (int)(row * la) + 16 * dma_chunk(row, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < CF::B_INS; ++i) {
+      const int row = 8 * (w + 8 * i) + (lane >> 3);
+      vb[i] = (int)(row * lb) + 16 * dma_chunk(row, lane);
+    }
   }
 }
 
+// accumulators -> C rows < M (fp32, 2 x 128-byte row segments per store):
+// buffer stores through a resource that ends at row M, so the rows of an
+// edge tile past M are dropped by the hardware (no per-element branches)
 template <class CF>
 __device__ __forceinline__ void sk_store(const SkArgs& g, int m0, int n0,
                                          const f32x16 (&acc)[CF::TM][CF::TN]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w / CF::WAVES_N, wc = w % CF::WAVES_N;
+  const rsrc_t rc = make_rsrc(g.C + (int64_t)m0 * g.ldc, (int64_t)(g.M - m0) * g.ldc * 4);
+  const int ldc4 = (int)g.ldc * 4;
 #pragma unroll
-  for (int i = 0; i < CF::TM; ++i)
+  for (int i = 0; i < CF::TM; ++i) {
+    const int rl = wr * CF::WM + i * 32 + 4 * (lane >> 5);
 #pragma unroll
     for (int j = 0; j < CF::TN; ++j) {
-      float* c = g.C + (int64_t)(m0 + wr * CF::WM + i * 32 + 4 * (lane >> 5)) * g.ldc + n0 +
-                 wc * CF::WN + j * 32 + (lane & 31);
+      const int off = rl * ldc4 + 4 * (n0 + wc * CF::WN + j * 32 + (lane & 31));
 #pragma unroll
-      for (int r = 0; r < 16; ++r) c[(int64_t)((r & 3) + 8 * (r >> 2)) * g.ldc] = acc[i][j][r];
+      for (int r = 0; r < 16; ++r)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rc, off,
+                                              ((r & 3) + 8 * (r >> 2)) * ldc4, 0);
     }
+  }
 }
 
-template <int BN, int STAGES>
-__global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(SkArgs g) {
-  using CF = SkCfg<BN, STAGES>;
+template <int BN, int STAGES, bool TRANS>
+__global__ __launch_bounds__(512, 1) void gemm_sk_kernel(SkArgs g) {
+  using CF = SkCfg<BN, STAGES, TRANS>;
+  // K-tile advance of the DMA source (scalar offset): 64 columns (NT) or 64
+  // k-rows (TN)
+  const int sa = CF::TRANS ? (int)(64 * g.lda * 2) : 128;
+  const int sb = CF::TRANS ? (int)(64 * g.ldb * 2) : 128;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int* s_flag = reinterpret_cast<int*>(lds + CF::STAGES * CF::STAGE_BYTES);
   const int G = gridDim.x, b = blockIdx.x;
@@ -191,14 +269,18 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(SkArgs g) {
     const int u = f * G + xslot;
     const int m0 = (u / g.tiles_n) * CF::BM, n0 = (u % g.tiles_n) * CF::BN;
     sk_tile_src<CF>(g, m0, n0, ra, va, rb, vb);
-    sk_mainloop<CF>(0, g.nk, ra, va, rb, vb, lds, acc);
+    sk_mainloop<CF>(0, g.nk, ra, va, rb, vb, sa, sb, lds, acc);
     sk_store<CF>(g, m0, n0, acc);
   }
   if (g.rem == 0) return;
 
-  // phase 2: remainder tiles, K-iterations split evenly over the G workgroups
+  // phase 2: remainder tiles, K-iterations split evenly over min(G, I)
+  // workgroups (every one of them gets >= 1 iteration, so every piece a tile
+  // counts arrives)
   const int64_t I = (int64_t)g.rem * g.nk;
-  const int64_t lo = (int64_t)b * I / G, hi = (int64_t)(b + 1) * I / G;
+  const int G2 = (int)min<int64_t>(G, I);
+  if (b >= G2) return;
+  const int64_t lo = (int64_t)b * I / G2, hi = (int64_t)(b + 1) * I / G2;
   int64_t it = lo;
   while (it < hi) {
     const int q = (int)(it / g.nk);
@@ -207,10 +289,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(SkArgs g) {
     const int u = g.full_rounds * G + q;
     const int m0 = (u / g.tiles_n) * CF::BM, n0 = (u % g.tiles_n) * CF::BN;
     sk_tile_src<CF>(g, m0, n0, ra, va, rb, vb);
-    sk_mainloop<CF>(k0, k1, ra, va, rb, vb, lds, acc);
+    sk_mainloop<CF>(k0, k1, ra, va, rb, vb, sa, sb, lds, acc);
     it += k1 - k0;
-    const int fb = sk_owner((int64_t)q * g.nk, I, G);
-    const int lb = sk_owner((int64_t)(q + 1) * g.nk - 1, I, G);
+    const int fb = sk_owner((int64_t)q * g.nk, I, G2);
+    const int lb = sk_owner((int64_t)(q + 1) * g.nk - 1, I, G2);
     const int P = lb - fb + 1, p = b - fb;
     if (P == 1) {
       sk_store<CF>(g, m0, n0, acc);
@@ -265,11 +347,11 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(SkArgs g) {
   }
 }
 
-template <int BN, int STAGES>
+template <int BN, int STAGES, bool TRANS>
 void launch_sk(const SkArgs& g, int G, hipStream_t stream) {
-  using CF = SkCfg<BN, STAGES>;
-  hipLaunchKernelGGL((gemm_nt_sk_kernel<BN, STAGES>), dim3(G), dim3(CF::THREADS), CF::LDS_BYTES,
-                     stream, g);
+  using CF = SkCfg<BN, STAGES, TRANS>;
+  hipLaunchKernelGGL((gemm_sk_kernel<BN, STAGES, TRANS>), dim3(G), dim3(CF::THREADS),
+                     CF::LDS_BYTES, stream, g);
 }
 
 }  // namespace
@@ -279,15 +361,16 @@ void launch_sk(const SkArgs& g, int G, hipStream_t stream) {
 // 1 = 256 x 128 tiles / 3 stages.
 void gemm_sk_plan(int M, int N, int K, int G, int variant, int64_t* n_cnt, int64_t* n_slab) {
   const int BN = variant == 1 ? 128 : 256;
-  const int tiles = (M / 256) * (N / BN);
+  const int tiles = ((M + 255) / 256) * (N / BN);
   const int full = tiles / G, rem = tiles - full * G;
   const int nk = K / 64;
   int pmax = 0;
   if (rem > 0) {
     const int64_t I = (int64_t)rem * nk;
+    const int64_t G2 = std::min<int64_t>(G, I);
     for (int q = 0; q < rem; ++q) {
       const int64_t a = (int64_t)q * nk, z = (int64_t)(q + 1) * nk - 1;
-      const int fb = (int)(((a + 1) * G + I - 1) / I - 1), lb = (int)(((z + 1) * G + I - 1) / I - 1);
+      const int fb = (int)(((a + 1) * G2 + I - 1) / I - 1), lb = (int)(((z + 1) * G2 + I - 1) / I - 1);
       pmax = std::max(pmax, lb - fb + 1);
     }
   }
@@ -295,25 +378,35 @@ void gemm_sk_plan(int M, int N, int K, int G, int variant, int64_t* n_cnt, int64
   *n_slab = (int64_t)rem * pmax * 256 * BN;
 }
 
-void launch_gemm_nt_sk(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, float* C,
-                       int64_t ldc, int M, int N, int K, int G, int variant, float* slab, int* cnt,
-                       hipStream_t stream) {
+// trans = false: C = A B^T, A (M x K), B (N x K); trans = true: C = A^T B,
+// A (K x M), B (K x N).  a_bytes / b_bytes: readable bytes from A / B.
+void launch_gemm_sk(const uint16_t* A, int64_t lda, int64_t a_bytes, const uint16_t* B,
+                    int64_t ldb, int64_t b_bytes, float* C, int64_t ldc, int M, int N, int K,
+                    bool trans, int G, int variant, float* slab, int* cnt, hipStream_t stream) {
   const int BN = variant == 1 ? 128 : 256;
   SkArgs g;
   g.A = A, g.B = B, g.C = C, g.slab = slab, g.cnt = cnt;
+  g.a_bytes = a_bytes, g.b_bytes = b_bytes;
   g.lda = lda, g.ldb = ldb, g.ldc = ldc;
   g.M = M, g.N = N, g.nk = K / 64;
   g.tiles_n = N / BN;
-  const int tiles = (M / 256) * g.tiles_n;
+  const int tiles = ((M + 255) / 256) * g.tiles_n;
   g.full_rounds = tiles / G;
   g.rem = tiles - g.full_rounds * G;
   int64_t nc, ns;
   gemm_sk_plan(M, N, K, G, variant, &nc, &ns);
   g.pmax = g.rem > 0 ? (int)(ns / ((int64_t)g.rem * 256 * BN)) : 0;
-  if (variant == 1)
-    launch_sk<128, 3>(g, G, stream);
-  else
-    launch_sk<256, 2>(g, G, stream);
+  if (trans) {
+    if (variant == 1)
+      launch_sk<128, 3, true>(g, G, stream);
+    else
+      launch_sk<256, 2, true>(g, G, stream);
+  } else {
+    if (variant == 1)
+      launch_sk<128, 3, false>(g, G, stream);
+    else
+      launch_sk<256, 2, false>(g, G, stream);
+  }
 }
 
 // W (rows x cols, bf16 row-major) -> W^T (cols x ldo), columns rows .. ldo-1

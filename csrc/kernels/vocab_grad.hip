@@ -221,44 +221,65 @@ void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd
 // its chunk's 8 sums in registers over the rows (CS_UNROLL row loads in
 // flight) and writes one partial row per block; a second launch sums the
 // partials per column (deterministic, no atomics).
+// The rows per block are a run-time choice (CSTCAP_COLSUM_ROWS, a multiple of
+// CS_ROWS): 128 fills the chip (1,680 workgroups at the headline shape,
+// ~160 us at HBM rate); larger values leave most CU slots to the kernels that
+// run concurrently with the sums (the reverse loop) at a lower sum rate.
 constexpr int CS_ROWS = 128, CS_UNROLL = 8;
 
-int vgrad_colsum_blocks(int64_t NR) { return (int)((NR + CS_ROWS - 1) / CS_ROWS); }
+static int colsum_rows() {
+  static int rows = -1;
+  if (rows < 0) {
+    const char* e = getenv("CSTCAP_COLSUM_ROWS");
+    const int v = e != nullptr ? atoi(e) : CS_ROWS;
+    rows = v >= CS_ROWS ? v / CS_ROWS * CS_ROWS : CS_ROWS;
+  }
+  return rows;
+}
+
+int vgrad_colsum_blocks(int64_t NR) {
+  const int rows = colsum_rows();
+  return (int)((NR + rows - 1) / rows);
+}
 
 __global__ __launch_bounds__(256) void vgrad_colsum_kernel(const uint16_t* __restrict__ E,
                                                            int64_t ldl, int V, int64_t NR,
                                                            const float* __restrict__ alpha,
-                                                           float* __restrict__ part) {
+                                                           float* __restrict__ part, int rows) {
   __shared__ float s_al[CS_ROWS];
-  const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
-  const int nr = (int)min((int64_t)CS_ROWS, NR - r0);
-  if ((int)threadIdx.x < nr) s_al[threadIdx.x] = alpha[r0 + threadIdx.x];
-  __syncthreads();
   const int ci = blockIdx.y * 256 + threadIdx.x;  // chunk
   const int v0 = 8 * ci;
-  if (v0 >= V) return;
   const int nv = min(8, V - v0);  // ragged last chunk: lanes >= nv are masked
   float acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  const uint16_t* base = E + r0 * ldl + v0;
-  for (int i = 0; i < nr; i += CS_UNROLL) {
-    uint4 x[CS_UNROLL];
+  const int64_t rb = (int64_t)blockIdx.x * rows;
+  for (int64_t r0 = rb; r0 < min(rb + rows, NR); r0 += CS_ROWS) {
+    const int nr = (int)min((int64_t)CS_ROWS, NR - r0);
+    __syncthreads();  // previous chunk's weights read
+    if ((int)threadIdx.x < nr) s_al[threadIdx.x] = alpha[r0 + threadIdx.x];
+    __syncthreads();
+    if (v0 >= V) continue;
+    const uint16_t* base = E + r0 * ldl + v0;
+    for (int i = 0; i < nr; i += CS_UNROLL) {
+      uint4 x[CS_UNROLL];
 #pragma unroll
-    for (int u = 0; u < CS_UNROLL; ++u)
-      x[u] = i + u < nr ? *reinterpret_cast<const uint4*>(base + (int64_t)(i + u) * ldl)
-                        : make_uint4(0, 0, 0, 0);
+      for (int u = 0; u < CS_UNROLL; ++u)
+        x[u] = i + u < nr ? *reinterpret_cast<const uint4*>(base + (int64_t)(i + u) * ldl)
+                          : make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < CS_UNROLL; ++u) {
-      const float al = i + u < nr ? s_al[i + u] : 0.f;
-      const uint32_t w[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+      for (int u = 0; u < CS_UNROLL; ++u) {
+        const float al = i + u < nr ? s_al[i + u] : 0.f;
+        const uint32_t w[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        acc[2 * k] += al * bf2f(w[k] & 0xffff);
-        acc[2 * k + 1] += al * bf2f(w[k] >> 16);
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] += al * bf2f(w[k] & 0xffff);
+          acc[2 * k + 1] += al * bf2f(w[k] >> 16);
+        }
       }
     }
   }
+  if (v0 >= V) return;
   float* out = part + (int64_t)blockIdx.x * V + v0;
 #pragma unroll
   for (int k = 0; k < 8; ++k)
@@ -298,7 +319,7 @@ void launch_vgrad_colsum(const uint16_t* E, int64_t ldl, int V, int64_t NR, cons
   const int nb = vgrad_colsum_blocks(NR);
   const int nch = (V + 7) / 8;
   hipLaunchKernelGGL(vgrad_colsum_kernel, dim3(nb, (nch + 255) / 256), dim3(256), 0, stream, E, ldl,
-                     V, NR, alpha, part);
+                     V, NR, alpha, part, colsum_rows());
   post_launch("vgrad_colsum_kernel", stream);
   hipLaunchKernelGGL(vgrad_colsum_reduce_kernel, dim3((V + 63) / 64), dim3(256), 0, stream, part,
                      nb, V, dblog);

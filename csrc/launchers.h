@@ -6,12 +6,12 @@
 
 namespace cst {
 
-// gemm_sk.hip: persistent NT GEMM (C fp32 = A B^T, bf16 operands) and its
+// gemm_sk.hip: persistent GEMM (C fp32 = A B^T or A^T B, bf16 operands) and its
 // workspace sizes (tickets, slab floats) for a grid of G workgroups
 void gemm_sk_plan(int M, int N, int K, int G, int variant, int64_t* n_cnt, int64_t* n_slab);
-void launch_gemm_nt_sk(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, float* C,
-                       int64_t ldc, int M, int N, int K, int G, int variant, float* slab, int* cnt,
-                       hipStream_t stream);
+void launch_gemm_sk(const uint16_t* A, int64_t lda, int64_t a_bytes, const uint16_t* B,
+                    int64_t ldb, int64_t b_bytes, float* C, int64_t ldc, int M, int N, int K,
+                    bool trans, int G, int variant, float* slab, int* cnt, hipStream_t stream);
 void launch_transpose_pad_bf16(const uint16_t* in, int rows, int cols, uint16_t* out, int64_t ldo,
                                hipStream_t stream);
 

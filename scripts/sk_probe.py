@@ -1,4 +1,4 @@
-"""X = E W at the headline shape (35,840 x 512, K = 10,560 padded): the
+"""X = E W (35,840 x 512, K = 10,560 padded) and dW = E^T Hs at the headline shape: the
 hand-written persistent GEMM (csrc/kernels/gemm_sk.hip, variants 0 / 1) vs
 PyTorch's hipBLASLt default and the measured-choice hipBLASLt plan
 (csrc/host/blaslt_tuned.cpp).  Prints one JSON line (us per call, TFLOP/s,
@@ -49,5 +49,25 @@ for v in (0, 1):
     out['x_sk%d_tflops' % v] = round(flop / us * 1e-6, 1)
     out['x_sk%d_rel_err' % v] = float((X2 - X0).norm() / X0.norm())
 out['x_default_tflops'] = round(flop / out['x_default_us'] * 1e-6, 1)
+# dW = E^T Hs (10,509 x 512, K = 35,840): the TN path
+Hs = (torch.randn(NR, H, device=dev) * 0.1).bfloat16()
+D0 = torch.empty(V, H, device=dev)
+
+
+def dw_split():
+    kr = NR // 4
+    a = E.as_strided((4, V, kr), (kr * LDL, 1, LDL))
+    torch.sum(torch.bmm(a, Hs.view(4, kr, H), out_dtype=torch.float32), 0, out=D0)
+
+
+out['dw_default_splitk4_us'] = bench(dw_split)
+D1 = torch.empty(V, H, device=dev)
+out['dw_tuned_us'] = bench(lambda: ops.gemm_bf16_tuned(D1, Ev, True, Hs, False, 32))
+for v in (0, 1):
+    D2 = torch.empty(V, H, device=dev)
+    us = bench(lambda: ops.gemm_tn_sk(D2, Ev, Hs, v))
+    out['dw_sk%d_us' % v] = us
+    out['dw_sk%d_tflops' % v] = round(flop / us * 1e-6, 1)
+    out['dw_sk%d_rel_err' % v] = float((D2 - D0).norm() / D0.norm())
 out['x_tuned_tflops'] = round(flop / out['x_tuned_us'] * 1e-6, 1)
 print(json.dumps(out))

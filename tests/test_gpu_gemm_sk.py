@@ -29,6 +29,7 @@ def _int_operands(M, N, K, ld_pad=0, seed=0):
     (256 * 140, 512, 64 * 24),     # headline rows: phase 1 + a 24-tile remainder
     (256 * 4, 256, 64 * 3),        # fewer K-iterations than workgroups: one-iteration pieces
     (256 * 300, 256, 64 * 5),      # > 1 phase-1 round
+    (256 * 9 + 13, 512, 64 * 7),   # edge M tile (rows past M dropped)
 ])
 def test_gemm_nt_sk_exact_on_integers(M, N, K, variant):
     ops = _ops()
@@ -46,10 +47,32 @@ def test_gemm_nt_sk_exact_on_integers(M, N, K, variant):
     assert torch.equal(out, out2)
 
 
-def test_gemm_nt_sk_refuses_untiled_shapes():
+@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('M,N,K,ldm', [
+    (10509, 512, 64 * 40, 10560),  # dW_logit's M (edge tile), short K: phase 2
+    (256 * 3, 256, 64 * 9, 256 * 3),
+    (1000, 512, 64 * 300, 1024),   # long K split over many workgroups
+])
+def test_gemm_tn_sk_exact_on_integers(M, N, K, ldm, variant):
+    """out = a^T b with a (K x M, row stride ldm) and b (K x N): the
+    transposed-read (ds_read_b64_tr_b16) operand path."""
     ops = _ops()
-    a = torch.zeros(100, 64, device='cuda', dtype=torch.bfloat16)
-    b = torch.zeros(256, 64, device='cuda', dtype=torch.bfloat16)
+    if not ops.gemm_nt_sk_ok(M, N, K, variant):
+        pytest.skip('shape not tiled by this variant')
+    g = torch.Generator(device='cuda').manual_seed(1)
+    a = torch.randint(-2, 3, (K, ldm), generator=g, device='cuda').bfloat16()[:, :M]
+    b = torch.randint(-2, 3, (K, N), generator=g, device='cuda').bfloat16()
+    out = torch.full((M, N), float('nan'), device='cuda')
+    ops.gemm_tn_sk(out, a, b, variant)
+    ref = (a.double().t() @ b.double()).float()
+    bad = (out != ref)
+    assert not bad.any(), (variant, bad.sum().item(), bad.nonzero()[:8].tolist())
+
+
+def test_gemm_sk_refuses_untiled_shapes():
+    ops = _ops()
+    a = torch.zeros(100, 60, device='cuda', dtype=torch.bfloat16)
+    b = torch.zeros(256, 60, device='cuda', dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         ops.gemm_nt_sk(torch.empty(100, 256, device='cuda'), a, b, 0)
 
@@ -81,4 +104,11 @@ def test_vocab_x_sk_matches_fp32_at_headline_shape(variant, monkeypatch):
     ops.gemm_nt_sk(out, a, ops.transpose_pad_bf16(W, ldl), variant)
     ref = a[:, :V].float() @ W.float()
     err = (out - ref).norm() / ref.norm()
+    assert err < 1e-5, err.item()
+    # dW_logit = E^T Hs at the same shape (TN path, M = V edge tile)
+    Hs = (torch.randn(n * R, H, device='cuda') * 0.1).bfloat16()
+    dW = torch.empty(V, H, device='cuda')
+    ops.gemm_tn_sk(dW, a[:, :V], Hs, variant)
+    ref = a[:, :V].float().t() @ Hs.float()
+    err = (dW - ref).norm() / ref.norm()
     assert err < 1e-5, err.item()
