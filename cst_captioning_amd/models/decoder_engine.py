@@ -780,11 +780,15 @@ class DecoderEngine:
         T = model.seq_length - 1
         modes = [SEL_GREEDY if sample_max == 1 else SEL_SAMPLE] * (T - 1)
         # temporal attention, one greedy row per video (the SCST baseline):
-        # decode each video on TWO identical rows, so the MFMA attention of
-        # the decode launch applies (it needs >= 2 rows per video, vocab.hip
-        # att_mfma_ok) instead of a VALU attention launch + a query GEMM per
-        # step; greedy rows are deterministic, row 0 of each pair is kept
+        # CSTCAP_GREEDY_DUP=1 decodes each video on TWO identical rows, so the
+        # MFMA attention of the decode launch applies (it needs >= 2 rows per
+        # video, vocab.hip att_mfma_ok) instead of a VALU attention launch + a
+        # query GEMM per step; row 0 of each pair is kept.  Off by default:
+        # the doubled greedy vocab work slows the concurrent sampled rollout
+        # more than the branch gains (att8 5.317 vs 5.197 ms per step,
+        # profiles/r4/README_r4.md)
         dup = (self.attention and not self.manet and not expand and sample_max == 1
+               and os.environ.get('CSTCAP_GREEDY_DUP', '0') == '1'
                and self._att_mfma_shape_ok(model))
         seq, lp, _, _ = self._run(model, feats, None, modes, want_xe=False, use_counts=False,
                                   use_unfinished=True, expand=expand, drop=False,
@@ -799,8 +803,7 @@ class DecoderEngine:
         64 <= H <= 512 with H % 32 == 0."""
         C = getattr(model, 'num_chunks', 1)
         A, H = self.att_dim, self.H
-        return (1 <= C <= 16 and A % 64 == 0 and A <= 1024 and H % 32 == 0 and 64 <= H <= 512
-                and os.environ.get('CSTCAP_GREEDY_DUP', '1') != '0')
+        return 1 <= C <= 16 and A % 64 == 0 and A <= 1024 and H % 32 == 0 and 64 <= H <= 512
 
     @torch.no_grad()
     def sample_beam(self, model, feats, opt):
