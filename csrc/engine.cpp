@@ -57,15 +57,18 @@ void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool t
                      int64_t n_cand);
 // The vocab head's backward GEMMs through the measured hipBLASLt algorithm
 // choice (host/blaslt_tuned.cpp) instead of PyTorch's heuristic first choice
-// when CSTCAP_TUNED_GEMM=1 (A/B runs; off by default)
-static bool tuned_gemm_enabled() {
-  static int on = -1;
-  if (on < 0) {
+// (A/B runs; off by default): CSTCAP_TUNED_GEMM=1 both, =x X only, =d dW only
+static int tuned_gemm_mask() {
+  static int m = -1;
+  if (m < 0) {
     const char* e = getenv("CSTCAP_TUNED_GEMM");
-    on = (e != nullptr && e[0] == '1') ? 1 : 0;
+    m = 0;
+    if (e != nullptr) m = e[0] == '1' ? 3 : e[0] == 'x' ? 1 : e[0] == 'd' ? 2 : 0;
   }
-  return on == 1;
+  return m;
 }
+static bool tuned_gemm_enabled() { return (tuned_gemm_mask() & 1) != 0; }
+static bool tuned_gemm_dw_enabled() { return (tuned_gemm_mask() & 2) != 0; }
 
 // Hand-written persistent GEMM (kernels/gemm_sk.hip): out (M x N fp32) =
 // a (M x K) b (N x K)^T or a (K x M)^T b (K x N), bf16 operands with unit
@@ -816,11 +819,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const bool early_comm = early && comm_stream != 0;
   // DP overlap (set_grad_events): vocab head / embedding gradients final events
   const bool grad_ev = g_grad_events_on && early;
-  // One GPU: the bias column sums (HBM-bound) under the latency-bound
-  // reverse loop, dW_logit after it (vh_sched 3; interleaved A/B 3.745-3.792
-  // vs 3.774-3.831 ms per step with the loop-after schedule 0,
-  // profiles/r3/ab_sched.txt)
-  const int vh_sched = (early_comm || grad_ev) ? 2 : 3;
+  // vh_sched 2: dW_logit and the bias column sums on the side stream under
+  // the latency-bound reverse loop (data parallelism: the vocab head's
+  // all-reduce starts there too).  vh_sched 3: the sums under the loop,
+  // dW_logit after it (the round-3 one-GPU choice: 3.745-3.792 vs 3.774-3.831
+  // ms per step against schedule 0, profiles/r3/ab_sched.txt)
+  // Round 4: with the bias column sums in fewer workgroups (vocab_grad.hip
+  // colsum_rows) the concurrent schedule wins on one GPU too: interleaved A/B
+  // 3.591-3.604 vs 3.628-3.682 ms per step (profiles/r4/README_r4.md);
+  // CSTCAP_VH_SCHED=3 restores the loop-after schedule
+  static const int vh_env = [] {
+    const char* e = getenv("CSTCAP_VH_SCHED");
+    return e != nullptr ? atoi(e) : 2;
+  }();
+  const int vh_sched = (early_comm || grad_ev) ? 2 : (vh_env == 3 ? 3 : 2);
   // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
   // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
   // split-K batch over groups of decode steps multiplies the tiles in flight,
@@ -834,7 +846,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       gemm_tn_sk(dWlog, Ev, rhs, -1);  // E'^T (K = NR rows) x rhs, hand-written
       return;
     }
-    if (tuned_gemm_enabled()) {  // one GEMM, the measured algorithm (split-K inside it)
+    if (tuned_gemm_dw_enabled()) {  // one GEMM, the measured algorithm (split-K inside it)
       gemm_bf16_tuned(dWlog, Ev, true, rhs, false, 32);
       return;
     }

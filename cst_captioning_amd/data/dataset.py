@@ -259,7 +259,15 @@ class CaptionLoader:
         for a, k in zip(arrays, sizes):
             host[off:off + k] = a
             off += k
-        dev = self._pin[:n].to(self.device, non_blocking=True)
+        tgt = getattr(self, '_index_target', None)
+        if tgt is not None and tgt.numel() == n:
+            # the captured step's static index buffer: one host->device copy
+            # straight into it, stream-ordered after the previous replay that
+            # read it (Trainer._graph_step then has nothing to copy)
+            dev = tgt
+            dev.copy_(self._pin[:n], non_blocking=True)
+        else:
+            dev = self._pin[:n].to(self.device, non_blocking=True)
         self._pin_event = torch.cuda.Event()
         self._pin_event.record()
         out, off = [], 0
@@ -267,6 +275,13 @@ class CaptionLoader:
             out.append(dev[off:off + k])
             off += k
         return out
+
+    def set_index_target(self, flat):
+        """Upload the index arrays of every later batch whose total length
+        equals ``flat.numel()`` into ``flat`` (a graph-captured step's static
+        index buffer) instead of a fresh device tensor.  Batches alias it: a
+        batch's indices are valid until the next batch is assembled."""
+        self._index_target = flat
 
     def get_batch(self):
         return self._assemble(self._next_videos())

@@ -411,7 +411,8 @@ class Trainer:
                 return None
             self._capture(data._loader, idx, key, mixer_from, scb)
         for dst, src in zip(self._static_idx, idx):
-            dst.copy_(src, non_blocking=True)
+            if src.data_ptr() != dst.data_ptr():  # (the loader uploads into them)
+                dst.copy_(src, non_blocking=True)
         self.optimizer.sync_lr()
         g_a, g_b = self._graph
         g_a.replay()
@@ -435,7 +436,16 @@ class Trainer:
         torch.cuda.synchronize(self.device)
         # the captured step must refresh the gate table itself on every replay
         self.engine.invalidate_ptab()
-        self._static_idx = [t.clone() for t in idx]
+        # one flat static buffer; the loader uploads later batches' indices
+        # straight into it (no device-to-device copies before each replay)
+        flat = torch.cat([t.reshape(-1) for t in idx])
+        self._static_idx, off = [], 0
+        for t in idx:
+            self._static_idx.append(flat[off:off + t.numel()].view(t.shape))
+            off += t.numel()
+        if (hasattr(loader, 'set_index_target') and all(t.dim() == 1 for t in idx)
+                and os.environ.get('CSTCAP_IDX_ALIAS', '1') != '0'):
+            loader.set_index_target(flat)
         pool = torch.cuda.graph_pool_handle()
         g_a = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_a, pool=pool):
