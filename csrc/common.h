@@ -53,7 +53,13 @@ inline void post_launch(const char* kernel, hipStream_t stream) {
   const int mode = launch_check_mode();
   if (mode == 0) return;
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess && mode > 1) e = hipStreamSynchronize(stream);
+  if (e == hipSuccess && mode > 1) {
+    // (a stream being captured into a graph cannot be synchronised: the
+    // launch is checked, the fault check happens when the graph runs)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(stream, &cs);
+    if (cs == hipStreamCaptureStatusNone) e = hipStreamSynchronize(stream);
+  }
   if (e != hipSuccess)
     throw std::runtime_error(std::string("HIP error after ") + kernel + ": " +
                              hipGetErrorString(e));
