@@ -1100,6 +1100,24 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // stream before returning.)
   // (starting them only after the main stream's per-token sums measured
   // slower: 3.76-3.81 vs 3.71-3.72 ms, profiles/r3/ab_toksum_first.txt)
+  // vh_sched 2: the side stream is idle again long before the loop ends
+  // (dW_logit + sums under the loop), so the recurrent-weight GEMMs run there
+  // after the loop, concurrently with the main stream's input-token chain
+  // (CSTCAP_WHH_SIDE=0: after that chain on the main stream)
+  static const bool whh_side_env = [] {
+    const char* e = getenv("CSTCAP_WHH_SIDE");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  const bool whh_side = vh_sched == 2 && whh_side_env;
+  hipEvent_t ev_whh = aux.ev[4];
+  if (whh_side) {
+    (void)hipEventRecord(ev_ready, st);  // reverse loop done
+    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
+    c10::hip::HIPStreamGuard guard(side);
+    whh_grad();
+    stamp(STAMP_BWD_SIDE, side.stream());
+    (void)hipEventRecord(ev_whh, side.stream());
+  }
   if (vh_sched == 0 || vh_sched == 3) {
     (void)hipEventRecord(ev_ready, st);  // reverse loop done
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
@@ -1142,7 +1160,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       dWie.copy_(at::mm(S_tok.t(), emb, at::kFloat));
   }
   stamp(STAMP_BWD_TOKGEMM, st);
-  if (vh_sched == 2) whh_grad();
+  if (vh_sched == 2 && !whh_side) whh_grad();
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
     dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);
@@ -1188,6 +1206,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // join the side stream (dW_logit): every tensor it touched was allocated
   // on the main stream and is released after this point
   (void)hipStreamWaitEvent(st, ev_done, 0);
+  if (whh_side) (void)hipStreamWaitEvent(st, ev_whh, 0);
   std::vector<at::Tensor> out = {dWx, dWlog, dblog, d_emb, dvg};
   out.insert(out.end(), res.begin(), res.end());
   if (has_s0) {
