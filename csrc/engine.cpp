@@ -122,6 +122,13 @@ static void gemm_sk(at::Tensor out, at::Tensor a, at::Tensor b, bool trans, int6
   int dev = 0, G = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&G, hipDeviceAttributeMultiprocessorCount, dev);
+  // CSTCAP_SK_GRID: fewer persistent workgroups than CUs (A/B: leave CUs to a
+  // concurrent stream, e.g. the reverse loop next to dW_logit)
+  static const int grid_env = [] {
+    const char* e = getenv("CSTCAP_SK_GRID");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  if (grid_env >= 8 && grid_env < G) G = grid_env / 8 * 8;
   TORCH_CHECK(G % 8 == 0, "gemm_sk: CU count must be a multiple of the 8 XCDs");
   int64_t n_cnt = 0, n_slab = 0;
   gemm_sk_plan((int)M, (int)N, (int)K, G, (int)variant, &n_cnt, &n_slab);
