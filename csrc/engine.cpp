@@ -1107,13 +1107,14 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // stream before returning.)
   // (starting them only after the main stream's per-token sums measured
   // slower: 3.76-3.81 vs 3.71-3.72 ms, profiles/r3/ab_toksum_first.txt)
-  // vh_sched 2: the side stream is idle again long before the loop ends
-  // (dW_logit + sums under the loop), so the recurrent-weight GEMMs run there
-  // after the loop, concurrently with the main stream's input-token chain
-  // (CSTCAP_WHH_SIDE=0: after that chain on the main stream)
+  // vh_sched 2: the recurrent-weight GEMMs after the input-token chain on the
+  // main stream.  CSTCAP_WHH_SIDE=1 runs them on the (idle) side stream after
+  // the loop, concurrently with that chain: measured slower, 3.618-3.639 vs
+  // 3.563-3.620 ms (att8 5.115-5.141 vs 4.970-5.057), the two contend
+  // (profiles/r4/README_r4.md)
   static const bool whh_side_env = [] {
     const char* e = getenv("CSTCAP_WHH_SIDE");
-    return !(e != nullptr && e[0] == '0');
+    return e != nullptr && e[0] == '1';
   }();
   const bool whh_side = vh_sched == 2 && whh_side_env;
   hipEvent_t ev_whh = aux.ev[4];
