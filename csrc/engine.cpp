@@ -56,13 +56,15 @@ void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand);
 // The vocab head's backward GEMMs through the measured hipBLASLt algorithm
-// choice (host/blaslt_tuned.cpp) instead of PyTorch's heuristic first choice
-// (A/B runs; off by default): CSTCAP_TUNED_GEMM=1 both, =x X only, =d dW only
+// choice (host/blaslt_tuned.cpp) instead of PyTorch's heuristic first choice.
+// Default: X = E W only (interleaved A/B 3.503-3.505 vs 3.562-3.574 ms per
+// step); dW_logit through it measured slower (3.683-3.731 vs 3.628-3.682)
+// and stays the split-K batch.  CSTCAP_TUNED_GEMM=1 both, =x X, =d dW, =0 none.
 static int tuned_gemm_mask() {
   static int m = -1;
   if (m < 0) {
     const char* e = getenv("CSTCAP_TUNED_GEMM");
-    m = 0;
+    m = 1;
     if (e != nullptr) m = e[0] == '1' ? 3 : e[0] == 'x' ? 1 : e[0] == 'd' ? 2 : 0;
   }
   return m;
