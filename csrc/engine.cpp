@@ -70,6 +70,16 @@ static int tuned_gemm_mask() {
   return m;
 }
 static bool tuned_gemm_enabled() { return (tuned_gemm_mask() & 1) != 0; }
+// the post-loop weight-gradient GEMMs (W_hh / W_q columns, embedding,
+// W_ie columns) through the measured choice: CSTCAP_TUNED_TAIL=1 (A/B)
+static bool tuned_tail_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CSTCAP_TUNED_TAIL");
+    on = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return on == 1;
+}
 static bool tuned_gemm_dw_enabled() { return (tuned_gemm_mask() & 2) != 0; }
 
 // Hand-written persistent GEMM (kernels/gemm_sk.hip): out (M x N fp32) =
@@ -1089,9 +1099,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // initial state); with attention the extra rows of [dG | dq]^T h_prev are dW_q
   auto whh_grad = [&]() {
     if (n_steps > 1) {
-      at::Tensor wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
-                                    h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
-                                    n_steps - 1);
+      at::Tensor wh;
+      if (tuned_tail_enabled()) {  // one GEMM, K = (n - 1) R, the measured algorithm
+        wh = at::empty({KD, H}, f32);
+        gemm_bf16_tuned(wh, dGx.narrow(0, R, (n_steps - 1) * R), true,
+                        h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}), false, 32);
+      } else {
+        wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
+                           h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
+                           n_steps - 1);
+      }
       dWx.narrow(1, E, H).copy_(wh.narrow(0, 0, H4));
       if (has_att) dWq.copy_(wh.narrow(0, H4, A));
     } else {
@@ -1149,7 +1166,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
-  at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
+  if (tuned_tail_enabled())
+    gemm_bf16_tuned(d_emb, S_tok, false, wx.narrow(1, 0, E), false, 32);
+  else
+    at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st);
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134
@@ -1161,7 +1181,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     for (int64_t g = 8; g >= 2; --g)
       if (V % g == 0 && V / g >= 512) { nk = g; break; }
     at::Tensor dWie = dWx.narrow(1, 0, E);
-    if (nk > 1 && emb.is_contiguous())
+    if (tuned_tail_enabled() && emb.is_contiguous()) {
+      at::Tensor t = at::empty({H4, E}, f32);
+      gemm_bf16_tuned(t, S_tok, true, emb, false, 32);
+      dWie.copy_(t);
+    } else if (nk > 1 && emb.is_contiguous())
       at::sum_out(dWie,
                   at::bmm(S_tok.view({nk, V / nk, H4}).transpose(1, 2), emb.view({nk, V / nk, E}),
                           at::kFloat),
