@@ -71,7 +71,8 @@ static int tuned_gemm_mask() {
 }
 static bool tuned_gemm_enabled() { return (tuned_gemm_mask() & 1) != 0; }
 // the post-loop weight-gradient GEMMs (W_hh / W_q columns, embedding,
-// W_ie columns) through the measured choice: CSTCAP_TUNED_TAIL=1 (A/B)
+// W_ie columns) through the measured choice: CSTCAP_TUNED_TAIL=1 (A/B;
+// measured slower, 3.493-3.512 vs 3.472-3.486 ms, profiles/r4/README_r4.md)
 static bool tuned_tail_enabled() {
   static int on = -1;
   if (on < 0) {
