@@ -410,9 +410,10 @@ class Trainer:
                 self._graph_warm[key] = self._graph_warm.get(key, 0) + 1
                 return None
             self._capture(data._loader, idx, key, mixer_from, scb)
-        for dst, src in zip(self._static_idx, idx):
-            if src.data_ptr() != dst.data_ptr():  # (the loader uploads into them)
-                dst.copy_(src, non_blocking=True)
+        if not self._copy_flat(idx):
+            for dst, src in zip(self._static_idx, idx):
+                if src.data_ptr() != dst.data_ptr():  # (the loader uploads into them)
+                    dst.copy_(src, non_blocking=True)
         self.optimizer.sync_lr()
         g_a, g_b = self._graph
         g_a.replay()
@@ -426,6 +427,27 @@ class Trainer:
             # table an eval may have refreshed since is stale again
             self.engine.after_step()
         return self._graph_out
+
+    def _copy_flat(self, idx):
+        """The loader's index tensors are consecutive pieces of one upload:
+        one device copy into the static buffer instead of one per tensor."""
+        flat = getattr(self, '_static_flat', None)
+        if flat is None or len(idx) != len(self._static_idx) or not idx:
+            return False
+        t0 = idx[0]
+        off = t0.data_ptr()
+        for t, d in zip(idx, self._static_idx):
+            if (t.dtype != d.dtype or t.shape != d.shape or not t.is_contiguous()
+                    or t.data_ptr() != off or t.device != d.device):
+                return False
+            off += t.numel() * t.element_size()
+        if t0.data_ptr() == flat.data_ptr():
+            return True  # the loader uploaded into the static buffer itself
+        n = flat.numel()
+        if t0.storage_offset() + n > t0.untyped_storage().nbytes() // t0.element_size():
+            return False
+        flat.copy_(torch.as_strided(t0, (n,), (1,)), non_blocking=True)
+        return True
 
     def _capture(self, loader, idx, key, mixer_from, scb):
         """Capture one step (batch gather + forward + backward [+ update]).
@@ -442,6 +464,7 @@ class Trainer:
         # so off by default: a batch's indices then stay valid after the next
         # batch is assembled)
         flat = torch.cat([t.reshape(-1) for t in idx])
+        self._static_flat = flat
         self._static_idx, off = [], 0
         for t in idx:
             self._static_idx.append(flat[off:off + t.numel()].view(t.shape))
