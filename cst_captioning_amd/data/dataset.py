@@ -20,7 +20,6 @@ global order; rank ``r`` takes videos ``[r*B, (r+1)*B)`` of each global batch
 of ``world_size * B`` videos (weak scaling; ``world_size=1`` is the reference).
 """
 import logging
-import os
 
 import numpy as np
 import torch
@@ -269,21 +268,6 @@ class CaptionLoader:
             dev.copy_(self._pin[:n], non_blocking=True)
             self._pin_event = torch.cuda.Event()
             self._pin_event.record()
-        elif os.environ.get('CSTCAP_IDX_COPY_STREAM', '1') != '0':
-            # the host->device copy on a copy stream: it runs while the
-            # previous step is still executing, and the compute stream only
-            # waits on its (long completed) event instead of a copy-engine
-            # round trip between two graph replays
-            main = torch.cuda.current_stream(self.device)
-            cs = getattr(self, '_copy_stream', None)
-            if cs is None:
-                cs = self._copy_stream = torch.cuda.Stream(device=self.device)
-            with torch.cuda.stream(cs):
-                dev = self._pin[:n].to(self.device, non_blocking=True)
-                self._pin_event = torch.cuda.Event()
-                self._pin_event.record(cs)
-            main.wait_event(self._pin_event)
-            dev.record_stream(main)
         else:
             dev = self._pin[:n].to(self.device, non_blocking=True)
             self._pin_event = torch.cuda.Event()
