@@ -1019,6 +1019,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                     has_xe ? oh_b.data_ptr<float>() + t * R : nullptr,
                     has_xe ? oh_yx.data_ptr<int>() + t * R : nullptr};
   };
+  // W_hh gradient in two parts (CSTCAP_WHH_SPLIT = s, A/B): the steps >= s
+  // are final once the reverse loop passed step s, so their share of
+  // dW_hh = sum_t dG_t^T h_{t-1} runs on the side stream (behind dW_logit)
+  // while the loop finishes; only the steps < s remain for the post-loop tail
+  static const int whh_split_env = [] {
+    const char* e = getenv("CSTCAP_WHH_SPLIT");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  const int64_t whh_s = (vh_sched == 2 && NL == 1 && whh_split_env >= 2 &&
+                         whh_split_env < n_steps - 1)
+                            ? whh_split_env
+                            : 0;
+  at::Tensor whA = whh_s > 0 ? at::empty({KD, H}, f32) : at::Tensor();
+  hipEvent_t ev_wa = aux.ev[5];
   size_t next_chunk = 0;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     if (next_chunk < dhd_chunks.size() && t == dhd_chunks[next_chunk][1] - 1)
@@ -1078,6 +1092,20 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
                      dba_part.data_ptr<float>(), st, per_frame);
     if (t == n_steps - 1) stamp(STAMP_BWD_LOOP0, st);
+    if (whh_s > 0 && t == whh_s) {  // dG_t final for t >= whh_s
+      (void)hipEventRecord(aux.ev[1], st);
+      (void)hipStreamWaitEvent(side.stream(), aux.ev[1], 0);
+      c10::hip::HIPStreamGuard guard(side);
+      const int64_t ns = n_steps - whh_s;
+      int64_t G = 1;
+      for (int64_t g = 7; g >= 1; --g)
+        if (ns % g == 0) { G = g; break; }
+      at::Tensor a = dG_all.view({NR, KD}).narrow(0, whh_s * R, ns * R)
+                         .view({ns / G, G * R, KD}).transpose(1, 2);
+      at::Tensor b = h_all.narrow(0, whh_s - 1, ns).reshape({ns / G, G * R, H});
+      at::sum_out(whA, at::bmm(a, b, at::kFloat), 0);
+      (void)hipEventRecord(ev_wa, side.stream());
+    }
   }
   stamp(STAMP_BWD_LOOP, st);
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
@@ -1105,6 +1133,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         wh = at::empty({KD, H}, f32);
         gemm_bf16_tuned(wh, dGx.narrow(0, R, (n_steps - 1) * R), true,
                         h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}), false, 32);
+      } else if (whh_s > 0) {  // steps [1, s) here + the side stream's steps [s, n)
+        wh = grouped_wgrad(dGx.narrow(0, R, (whh_s - 1) * R),
+                           h_all.narrow(0, 0, whh_s - 1).reshape({(whh_s - 1) * R, H}),
+                           whh_s - 1);
+        (void)hipStreamWaitEvent(cur_stream(), ev_wa, 0);
+        wh.add_(whA);
       } else {
         wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
                            h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
