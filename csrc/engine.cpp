@@ -70,17 +70,6 @@ static int tuned_gemm_mask() {
   return m;
 }
 static bool tuned_gemm_enabled() { return (tuned_gemm_mask() & 1) != 0; }
-// the post-loop weight-gradient GEMMs (W_hh / W_q columns, embedding,
-// W_ie columns) through the measured choice: CSTCAP_TUNED_TAIL=1 (A/B;
-// measured slower, 3.493-3.512 vs 3.472-3.486 ms, profiles/r4/README_r4.md)
-static bool tuned_tail_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("CSTCAP_TUNED_TAIL");
-    on = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
-  return on == 1;
-}
 static bool tuned_gemm_dw_enabled() { return (tuned_gemm_mask() & 2) != 0; }
 
 // Hand-written persistent GEMM (kernels/gemm_sk.hip): out (M x N fp32) =
@@ -1019,20 +1008,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                     has_xe ? oh_b.data_ptr<float>() + t * R : nullptr,
                     has_xe ? oh_yx.data_ptr<int>() + t * R : nullptr};
   };
-  // W_hh gradient in two parts (CSTCAP_WHH_SPLIT = s, A/B): the steps >= s
-  // are final once the reverse loop passed step s, so their share of
-  // dW_hh = sum_t dG_t^T h_{t-1} runs on the side stream (behind dW_logit)
-  // while the loop finishes; only the steps < s remain for the post-loop tail
-  static const int whh_split_env = [] {
-    const char* e = getenv("CSTCAP_WHH_SPLIT");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  const int64_t whh_s = (vh_sched == 2 && NL == 1 && whh_split_env >= 2 &&
-                         whh_split_env < n_steps - 1)
-                            ? whh_split_env
-                            : 0;
-  at::Tensor whA = whh_s > 0 ? at::empty({KD, H}, f32) : at::Tensor();
-  hipEvent_t ev_wa = aux.ev[5];
   size_t next_chunk = 0;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     if (next_chunk < dhd_chunks.size() && t == dhd_chunks[next_chunk][1] - 1)
@@ -1092,20 +1067,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      t > 0 ? 1 : 0, dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
                      dba_part.data_ptr<float>(), st, per_frame);
     if (t == n_steps - 1) stamp(STAMP_BWD_LOOP0, st);
-    if (whh_s > 0 && t == whh_s) {  // dG_t final for t >= whh_s
-      (void)hipEventRecord(aux.ev[1], st);
-      (void)hipStreamWaitEvent(side.stream(), aux.ev[1], 0);
-      c10::hip::HIPStreamGuard guard(side);
-      const int64_t ns = n_steps - whh_s;
-      int64_t G = 1;
-      for (int64_t g = 7; g >= 1; --g)
-        if (ns % g == 0) { G = g; break; }
-      at::Tensor a = dG_all.view({NR, KD}).narrow(0, whh_s * R, ns * R)
-                         .view({ns / G, G * R, KD}).transpose(1, 2);
-      at::Tensor b = h_all.narrow(0, whh_s - 1, ns).reshape({ns / G, G * R, H});
-      at::sum_out(whA, at::bmm(a, b, at::kFloat), 0);
-      (void)hipEventRecord(ev_wa, side.stream());
-    }
   }
   stamp(STAMP_BWD_LOOP, st);
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
@@ -1129,21 +1090,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   auto whh_grad = [&]() {
     if (n_steps > 1) {
       at::Tensor wh;
-      if (tuned_tail_enabled()) {  // one GEMM, K = (n - 1) R, the measured algorithm
-        wh = at::empty({KD, H}, f32);
-        gemm_bf16_tuned(wh, dGx.narrow(0, R, (n_steps - 1) * R), true,
-                        h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}), false, 32);
-      } else if (whh_s > 0) {  // steps [1, s) here + the side stream's steps [s, n)
-        wh = grouped_wgrad(dGx.narrow(0, R, (whh_s - 1) * R),
-                           h_all.narrow(0, 0, whh_s - 1).reshape({(whh_s - 1) * R, H}),
-                           whh_s - 1);
-        (void)hipStreamWaitEvent(cur_stream(), ev_wa, 0);
-        wh.add_(whA);
-      } else {
-        wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
-                           h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
-                           n_steps - 1);
-      }
+      wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
+                         h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
+                         n_steps - 1);
       dWx.narrow(1, E, H).copy_(wh.narrow(0, 0, H4));
       if (has_att) dWq.copy_(wh.narrow(0, H4, A));
     } else {
@@ -1162,24 +1111,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // (starting them only after the main stream's per-token sums measured
   // slower: 3.76-3.81 vs 3.71-3.72 ms, profiles/r3/ab_toksum_first.txt)
   // vh_sched 2: the recurrent-weight GEMMs after the input-token chain on the
-  // main stream.  CSTCAP_WHH_SIDE=1 runs them on the (idle) side stream after
-  // the loop, concurrently with that chain: measured slower, 3.618-3.639 vs
-  // 3.563-3.620 ms (att8 5.115-5.141 vs 4.970-5.057), the two contend
-  // (profiles/r4/README_r4.md)
-  static const bool whh_side_env = [] {
-    const char* e = getenv("CSTCAP_WHH_SIDE");
-    return e != nullptr && e[0] == '1';
-  }();
-  const bool whh_side = vh_sched == 2 && whh_side_env;
-  hipEvent_t ev_whh = aux.ev[4];
-  if (whh_side) {
-    (void)hipEventRecord(ev_ready, st);  // reverse loop done
-    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
-    c10::hip::HIPStreamGuard guard(side);
-    whh_grad();
-    stamp(STAMP_BWD_SIDE, side.stream());
-    (void)hipEventRecord(ev_whh, side.stream());
-  }
+  // main stream (on the idle side stream after the loop, or their late steps'
+  // share on it during the loop, measured slower: they contend with the
+  // input-token chain / the loop, profiles/r4/README_r4.md)
   if (vh_sched == 0 || vh_sched == 3) {
     (void)hipEventRecord(ev_ready, st);  // reverse loop done
     (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
@@ -1201,10 +1135,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
-  if (tuned_tail_enabled())
-    gemm_bf16_tuned(d_emb, S_tok, false, wx.narrow(1, 0, E), false, 32);
-  else
-    at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
+  at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st);
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134
@@ -1216,11 +1147,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     for (int64_t g = 8; g >= 2; --g)
       if (V % g == 0 && V / g >= 512) { nk = g; break; }
     at::Tensor dWie = dWx.narrow(1, 0, E);
-    if (tuned_tail_enabled() && emb.is_contiguous()) {
-      at::Tensor t = at::empty({H4, E}, f32);
-      gemm_bf16_tuned(t, S_tok, true, emb, false, 32);
-      dWie.copy_(t);
-    } else if (nk > 1 && emb.is_contiguous())
+    if (nk > 1 && emb.is_contiguous())
       at::sum_out(dWie,
                   at::bmm(S_tok.view({nk, V / nk, H4}).transpose(1, 2), emb.view({nk, V / nk, E}),
                           at::kFloat),
@@ -1229,7 +1156,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       dWie.copy_(at::mm(S_tok.t(), emb, at::kFloat));
   }
   stamp(STAMP_BWD_TOKGEMM, st);
-  if (vh_sched == 2 && !whh_side) whh_grad();
+  if (vh_sched == 2) whh_grad();
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
     dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);
@@ -1275,7 +1202,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // join the side stream (dW_logit): every tensor it touched was allocated
   // on the main stream and is released after this point
   (void)hipStreamWaitEvent(st, ev_done, 0);
-  if (whh_side) (void)hipStreamWaitEvent(st, ev_whh, 0);
   std::vector<at::Tensor> out = {dWx, dWlog, dblog, d_emb, dvg};
   out.insert(out.end(), res.begin(), res.end());
   if (has_s0) {
