@@ -1261,12 +1261,18 @@ static FeatPoolArgs featpool_args(const std::vector<at::Tensor>& xs,
   TORCH_CHECK(a.H % 64 == 0, "featpool: output size must be a multiple of 64");
   for (int f = 0; f < a.nf; ++f) {
     const at::Tensor &x = xs[f], &w = ws[f];
-    check_cuda(x, "featpool x");
+    // x may be a column slice of a wider row (the loader gathers every
+    // modality in one pass): unit column stride, 16-byte-aligned rows
+    TORCH_CHECK(x.is_cuda(), "featpool x must be a GPU tensor");
     check_cuda(w, "featpool w");
     TORCH_CHECK(x.scalar_type() == at::kFloat && w.scalar_type() == at::kFloat && x.dim() == 2 &&
                     w.dim() == 2 && x.size(0) == a.rows && w.size(0) == a.H &&
-                    x.size(1) == w.size(1) && x.size(1) % 4 == 0,
-                "featpool: fp32 x (rows, d) and w (H, d) with d % 4 == 0");
+                    x.size(1) == w.size(1) && x.size(1) % 4 == 0 &&
+                    (x.size(1) == 1 || x.stride(1) == 1) && x.stride(0) % 4 == 0 &&
+                    x.stride(0) >= x.size(1) &&
+                    reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+                "featpool: fp32 x (rows, d) with unit column stride and 16-byte-aligned rows, "
+                "w (H, d), d % 4 == 0");
     a.s[f].x = x.data_ptr<float>();
     a.s[f].w = w.data_ptr<float>();
     if (!bs.empty()) {
@@ -1275,6 +1281,7 @@ static FeatPoolArgs featpool_args(const std::vector<at::Tensor>& xs,
       a.s[f].b = bs[f].data_ptr<float>();
     }
     a.s[f].d = (int)x.size(1);
+    a.s[f].ld = (int)x.stride(0);
   }
   featpool_layout(a);
   return a;

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void featpool_fwd_partial_kernel(FeatPoolArgs 
       const int row = (tid >> 3) + 32 * i, kk = k + 4 * (tid & 7);
       const bool kin = kk < kend;  // d % 4 == 0 (host check): a float4 is in or out
       const int r = r0 + row;
-      ra[i] = (kin && r < a.rows) ? *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.d + kk)
+      ra[i] = (kin && r < a.rows) ? *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.ld + kk)
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
       rb[i] = kin ? *reinterpret_cast<const float4*>(g.w + (int64_t)(u0 + row) * g.d + kk)
                   : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void featpool_bwd_kernel(FeatPoolArgs a, const
         const int64_t o = (int64_t)r * FH + f * a.H + u0 + c4;
         dy[i] = *reinterpret_cast<const float4*>(dout + o);
         yv[i] = *reinterpret_cast<const float4*>(outp + o);
-        if (k0 + c4 < g.d) xv[i] = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.d + k0 + c4);
+        if (k0 + c4 < g.d) xv[i] = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.ld + k0 + c4);
       }
     }
   };

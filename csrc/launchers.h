@@ -269,10 +269,10 @@ void launch_att_bwd(uint16_t* dG, int ldg, const float* gv, const float* pre, co
 // featpool.hip: FeatPool (per modality Linear -> ReLU -> Dropout, concat)
 constexpr int FEATPOOL_MAX_F = 8;
 struct FeatPoolSeg {
-  const float* x;  // (rows, d) features of modality f
+  const float* x;  // (rows, d) features of modality f, row stride ld
   const float* w;  // (H, d) weight
   const float* b;  // (H) bias
-  int d;
+  int d, ld;
   int blk0, bblk0;  // first forward / backward workgroup of the modality
 };
 struct FeatPoolArgs {

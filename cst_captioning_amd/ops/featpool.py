@@ -25,6 +25,16 @@ def fused_ok(pool, feats):
             and all(l.bias is not None for l in lins))
 
 
+def _rows(f):
+    """(rows, d) view of a modality's features: a column slice of the
+    loader's one-pass gather is passed as is (unit column stride, 16-byte
+    aligned rows), anything else as a contiguous copy."""
+    x = f.reshape(-1, f.size(-1))
+    if x.stride(-1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+        x = x.contiguous()
+    return x
+
+
 class _FeatPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, p, rng, nf, *args):
@@ -107,7 +117,7 @@ def featpool_vgate(eng, model, feats):
     p = float(pool.feat_list[0][2].p) if pool.training else 0.0
     dev = feats[0].device
     rng = _seeds(p, dev)
-    xs = [f.reshape(-1, f.size(-1)).contiguous() for f in feats]
+    xs = [_rows(f) for f in feats]
     return _FeatPoolVgateFn.apply(eng, p, rng, len(xs), *xs, *[l.weight for l in lins],
                                   *[l.bias for l in lins], model.core.rnn.weight_ih_l0)
 
@@ -119,7 +129,7 @@ def featpool(pool, feats):
     p = float(pool.feat_list[0][2].p) if pool.training else 0.0
     dev = feats[0].device
     rng = _seeds(p, dev)
-    xs = [f.reshape(-1, f.size(-1)).contiguous() for f in feats]
+    xs = [_rows(f) for f in feats]
     out = _FeatPoolFn.apply(p, rng, len(xs), *xs, *[l.weight for l in lins],
                             *[l.bias for l in lins])
     N, C = feats[0].shape[0], feats[0].shape[1]
