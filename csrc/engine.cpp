@@ -1069,27 +1069,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     if (t == n_steps - 1) stamp(STAMP_BWD_LOOP0, st);
   }
   stamp(STAMP_BWD_LOOP, st);
-  // the video-gate gradient (a pass over the dG rows) on the side stream right
-  // after the loop, concurrently with the input-token chain
-  // (CSTCAP_VG_SIDE=1, A/B)
-  static const bool vg_side_env = [] {
-    const char* e = getenv("CSTCAP_VG_SIDE");
-    return e != nullptr && e[0] == '1';
-  }();
-  const bool vg_side = vg_side_env && !has_att;
   at::Tensor dvg;
-  hipEvent_t ev_vg = aux.ev[5];
   if (!has_att) {
     TORCH_CHECK(vgate_div >= 1 && R % vgate_div == 0, "vgate_div must divide the rows");
     dvg = at::empty({R / vgate_div, H4}, f32);
-  }
-  if (vg_side) {
-    (void)hipEventRecord(aux.ev[1], st);
-    (void)hipStreamWaitEvent(side.stream(), aux.ev[1], 0);
-    launch_video_gate_grad(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), KD,
-                           (int)n_steps, (int)R, (int)vgate_div, (int)H4, dvg.data_ptr<float>(),
-                           side.stream());
-    (void)hipEventRecord(ev_vg, side.stream());
   }
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
   at::Tensor dG2 = dGx.narrow(1, 0, H4);
@@ -1187,12 +1170,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // (Bv, 4H): sum over time and over the rows of each video in one pass
     // (kernels/embed_grad.hip; was a (R, 4H) sum over time, 78 us, plus a
     // per-video sum in Python)
-    if (vg_side)
-      (void)hipStreamWaitEvent(st, ev_vg, 0);
-    else
-      launch_video_gate_grad(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), KD,
-                             (int)n_steps, (int)R, (int)vgate_div, (int)H4, dvg.data_ptr<float>(),
-                             st);
+    launch_video_gate_grad(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), KD,
+                           (int)n_steps, (int)R, (int)vgate_div, (int)H4, dvg.data_ptr<float>(), st);
   } else {
     // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r] (kernels/attention.hip:
     // one pass over the bf16 dG rows, partials per step chunk)

@@ -20,7 +20,6 @@ global order; rank ``r`` takes videos ``[r*B, (r+1)*B)`` of each global batch
 of ``world_size * B`` videos (weak scaling; ``world_size=1`` is the reference).
 """
 import logging
-import os
 
 import numpy as np
 import torch
@@ -102,13 +101,6 @@ class VideoCaptionDataset:
                 d['labels'] = torch.from_numpy(self.labels).to(device)
             if self.bcmrscores is not None:
                 d['bcmrscores'] = torch.from_numpy(self.bcmrscores).float().to(device)
-            if (len(self.feats) > 1 and all(f.shape[2] % 4 == 0 for f in self.feats)
-                    and os.environ.get('CSTCAP_FEAT_CAT', '1') != '0'):
-                # every modality side by side: one gather per batch instead of
-                # one per modality (the per-modality tensors are column slices)
-                d['feats_cat'] = torch.cat(d['feats'], dim=2)
-                offs = np.cumsum([0] + [f.shape[2] for f in self.feats])
-                d['feat_cols'] = [(int(o), int(f.shape[2])) for o, f in zip(offs, self.feats)]
             self._device_cache[key] = d
         return self._device_cache[key]
 
@@ -319,11 +311,7 @@ class CaptionLoader:
         keys = set(keys) if keys is not None else {'feats', 'labels', 'masks', 'bcmrscores'}
         out = {}
         if 'feats' in keys:
-            if 'feats_cat' in dev:
-                cat = dev['feats_cat'].index_select(0, vid_t)
-                out['feats'] = [cat[:, :, o:o + d] for o, d in dev['feat_cols']]
-            else:
-                out['feats'] = [f.index_select(0, vid_t) for f in dev['feats']]
+            out['feats'] = [f.index_select(0, vid_t) for f in dev['feats']]
         if rows_t is not None:
             if keys & {'labels', 'masks'}:
                 labels = dev['labels'].index_select(0, rows_t)

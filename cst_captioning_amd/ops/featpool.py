@@ -26,9 +26,9 @@ def fused_ok(pool, feats):
 
 
 def _rows(f):
-    """(rows, d) view of a modality's features: a column slice of the
-    loader's one-pass gather is passed as is (unit column stride, 16-byte
-    aligned rows), anything else as a contiguous copy."""
+    """(rows, d) view of a modality's features: rows with a unit column
+    stride and 16-byte alignment are passed as they are (the kernels take a
+    row stride), anything else as a contiguous copy."""
     x = f.reshape(-1, f.size(-1))
     if x.stride(-1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         x = x.contiguous()
