@@ -1523,9 +1523,28 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   }
   const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
+  // MFMA attention (the decode launch's att_mfma workgroups, launched on
+  // their own): the K beam rows of a video are its rows; the query input is
+  // h of each row's parent beam, gathered first.  CSTCAP_BEAM_ATT_MFMA=0:
+  // the fp32 VALU scorer with a query GEMM.
+  const char* bame = getenv("CSTCAP_BEAM_ATT_MFMA");  // (read per call: tests switch it)
+  const bool beam_att_mfma_env = !(bame != nullptr && bame[0] == '0');
+  const bool att_mfma_beam = has_att && beam_att_mfma_env && H4 == 4 * H &&
+                             att_mfma_ok((int)K, (int)C, (int)A, (int)H, per_frame);
+  at::Tensor gv16, vg16, hq, ep, cnt;
+  const int CP = C <= 8 ? 8 : 16;
   if (has_att) {
     vg_rows = at::empty({R, H4}, f32);
     qb = at::empty({R, A}, f32);
+    if (att_mfma_beam) {
+      auto bf = wx.options().dtype(at::kBFloat16);
+      gv16 = at::zeros({B, H4, CP}, bf);  // (Bv, 4H, CP) frame-minor gate tables
+      gv16.narrow(2, 0, C).copy_(att[0].transpose(1, 2));
+      vg16 = at::empty({R, H4}, bf);
+      hq = at::empty({R, H}, bf);
+      ep = at::empty({B, A / 64, 32, CP}, f32);
+      cnt = at::zeros({B}, f32.dtype(at::kInt));
+    }
   }
   for (int64_t t = 0; t < T - 1; ++t) {
     if (t >= 1) {
@@ -1547,7 +1566,20 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
     const at::Tensor& cp = c[t & 1];
     at::Tensor& ho = h[(t + 1) & 1];
     at::Tensor& co = c[(t + 1) & 1];
-    if (has_att) {
+    if (att_mfma_beam) {
+      if (t >= 1)
+        at::index_select_out(hq, hp, 0, parent);
+      else
+        hq.copy_(hp);
+      AttMfmaArgs am{reinterpret_cast<const uint16_t*>(hq.data_ptr()),
+                     reinterpret_cast<const uint16_t*>(att[2].data_ptr()), att[1].data_ptr<float>(),
+                     att[3].data_ptr<float>(), att[4].data_ptr<float>(),
+                     reinterpret_cast<const uint16_t*>(gv16.data_ptr()), (int)H, (int)A, (int)C,
+                     CP, (int)H4, (int)K, (int)B, reinterpret_cast<uint16_t*>(vg16.data_ptr()),
+                     nullptr, nullptr, ep.data_ptr<float>(), cnt.data_ptr<int>()};
+      launch_att_mfma_fwd(am, st);
+      vg_rows.copy_(vg16);
+    } else if (has_att) {
       if (t >= 1) at::mm_out(qb, hp, att[2].t(), at::kFloat);
       launch_att_fwd(att[0].data_ptr<float>(), att[1].data_ptr<float>(),
                      t >= 1 ? qb.data_ptr<float>() : nullptr, t >= 1 ? parent.data_ptr<int>() : nullptr,

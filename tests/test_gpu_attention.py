@@ -166,3 +166,31 @@ def test_attention_greedy_on_duplicated_rows_equals_one_row(H):
     assert (s1 == s0).all(1).float().mean().item() >= 0.7
     same = (s1 == s0).all(1)
     torch.testing.assert_close(l1[same], l0[same], rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize('H,K', [(64, 3), (512, 5)])
+def test_beam_mfma_attention_equals_valu_scorer(H, K):
+    """Beam search under temporal attention: the decode launch's MFMA
+    attention workgroups (beam rows of a video = its rows, query from each
+    row's parent h) against the fp32 VALU scorer + query GEMM
+    (CSTCAP_BEAM_ATT_MFMA=0): bf16 gate tables, so a near-tie may flip a
+    beam; most videos agree and the kept log-probs match."""
+    import os
+    ds, opt, model, loader = _tiny(C=8, seed=7, H=H, S=5)
+    eng = _engine(model, opt)
+    model.eval()
+    data = loader.get_batch()
+    outs = {}
+    for flag in ('1', '0'):
+        os.environ['CSTCAP_BEAM_ATT_MFMA'] = flag
+        try:
+            with torch.no_grad():
+                outs[flag] = eng.sample_beam(model, data['feats'], {'beam_size': K})
+        finally:
+            os.environ.pop('CSTCAP_BEAM_ATT_MFMA', None)
+    (s1, l1), (s0, l0) = outs['1'], outs['0']
+    assert s1.shape == s0.shape
+    assert (s1[:, :2] == s0[:, :2]).float().mean().item() >= 0.9
+    same = (s1 == s0).all(1)
+    assert same.float().mean().item() >= 0.6
+    torch.testing.assert_close(l1[same], l0[same], rtol=2e-2, atol=2e-2)
