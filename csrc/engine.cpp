@@ -1523,12 +1523,14 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   }
   const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
-  // MFMA attention (the decode launch's att_mfma workgroups, launched on
-  // their own): the K beam rows of a video are its rows; the query input is
-  // h of each row's parent beam, gathered first.  CSTCAP_BEAM_ATT_MFMA=0:
-  // the fp32 VALU scorer with a query GEMM.
+  // CSTCAP_BEAM_ATT_MFMA=1: MFMA attention (the decode launch's att_mfma
+  // workgroups, launched on their own): the K beam rows of a video are its
+  // rows; the query input is h of each row's parent beam, gathered first.
+  // Off by default: with the gather and the bf16 -> fp32 gate copy it is
+  // three launches per step against the VALU scorer's two, 26.0k vs 29.6k
+  // videos/s at att8 beam 5 (profiles/r4/README_r4.md)
   const char* bame = getenv("CSTCAP_BEAM_ATT_MFMA");  // (read per call: tests switch it)
-  const bool beam_att_mfma_env = !(bame != nullptr && bame[0] == '0');
+  const bool beam_att_mfma_env = bame != nullptr && bame[0] == '1';
   const bool att_mfma_beam = has_att && beam_att_mfma_env && H4 == 4 * H &&
                              att_mfma_ok((int)K, (int)C, (int)A, (int)H, per_frame);
   at::Tensor gv16, vg16, hq, ep, cnt;
