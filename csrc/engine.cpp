@@ -198,7 +198,13 @@ void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
   }
   at::Tensor Ev = logits16.view({NR, ldl}).narrow(1, 0, V);
   if (tuned_gemm_enabled()) {
-    gemm_bf16_tuned(dst, Ev, false, wlog, false, 32);
+    // heuristic candidates timed (CSTCAP_TUNED_NCAND, default 32)
+    static const int ncand = [] {
+      const char* e = getenv("CSTCAP_TUNED_NCAND");
+      const int v = e != nullptr ? atoi(e) : 32;
+      return v >= 1 && v <= 256 ? v : 32;
+    }();
+    gemm_bf16_tuned(dst, Ev, false, wlog, false, ncand);
     return;
   }
   at::mm_out(dst, Ev, wlog, at::kFloat);
