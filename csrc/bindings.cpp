@@ -18,10 +18,12 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 void set_grad_events(bool on);
 void grad_event_wait(int64_t k, int64_t stream);
 void grad_event_record(int64_t k, int64_t stream);
+int64_t grad_event_count(int64_t k);
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand);
 std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at::Tensor b,
                                        bool tb);
+std::vector<std::vector<double>> gemm_tuned_choices();
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -46,6 +48,8 @@ double att_bench(at::Tensor gv, at::Tensor P, at::Tensor q, at::Tensor wa, at::T
                  int64_t R, int64_t which, int64_t iters);
 std::vector<at::Tensor> token_sort(at::Tensor toks, int64_t V);
 at::Tensor token_group_sum(at::Tensor x, at::Tensor toks, int64_t V);
+std::vector<at::Tensor> cst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor scores,
+                                         at::Tensor bref, int64_t S, int64_t k);
 std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor sample,
                                           at::Tensor greedy);
 at::Tensor scst_loss_backward(at::Tensor seq, at::Tensor reward, at::Tensor out,
@@ -159,13 +163,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_bf16_tuned", &cst::gemm_bf16_tuned, py::arg("out"), py::arg("a"), py::arg("ta"),
         py::arg("b"), py::arg("tb"), py::arg("n_cand") = 24);
   m.def("gemm_tuned_timings", &cst::gemm_tuned_timings);
+  m.def("gemm_tuned_choices", &cst::gemm_tuned_choices);
   m.def("set_grad_events", &cst::set_grad_events);
   m.def("grad_event_wait", &cst::grad_event_wait);
   m.def("grad_event_record", &cst::grad_event_record);
+  m.def("grad_event_count", &cst::grad_event_count);
   m.def("att_mfma_fwd", &cst::att_mfma_fwd);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);
   m.def("scst_loss_forward", &cst::scst_loss_forward);
+  m.def("cst_loss_forward", &cst::cst_loss_forward);
   m.def("scst_loss_backward", &cst::scst_loss_backward);
   m.def("featpool_backward", &cst::featpool_backward);
   m.def("set_stamp_base", &cst::set_stamp_base);

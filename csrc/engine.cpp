@@ -270,7 +270,17 @@ static DeviceAux& device_aux(int dev_index) {
 // eager RCCL between replays, no collective inside the graph.
 static bool g_grad_events_on = false;
 void set_grad_events(bool on) { g_grad_events_on = on; }
-static void record_grad_event(hipEvent_t ev, hipStream_t s) {
+// host-side count of record calls per group (inline records and captured
+// record nodes): the trainer checks that a step (or the capture of one)
+// recorded both events before its comm stream relies on them -- a wait on an
+// event this step never recorded would order nothing
+static int64_t g_grad_ev_count[2] = {0, 0};
+int64_t grad_event_count(int64_t k) {
+  TORCH_CHECK(k >= 0 && k < 2, "grad_event_count: group 0 or 1");
+  return g_grad_ev_count[k];
+}
+static void record_grad_event(hipEvent_t ev, hipStream_t s, int k) {
+  g_grad_ev_count[k]++;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   hipGraph_t graph = nullptr;
   const hipGraphNode_t* deps = nullptr;
@@ -297,7 +307,7 @@ void grad_event_record(int64_t k, int64_t stream) {  // (tests)
   TORCH_CHECK(k >= 0 && k < 2, "grad_event_record: group 0 or 1");
   int dev = 0;
   (void)hipGetDevice(&dev);
-  record_grad_event(device_aux(dev).grad_ev[k], reinterpret_cast<hipStream_t>(stream));
+  record_grad_event(device_aux(dev).grad_ev[k], reinterpret_cast<hipStream_t>(stream), (int)k);
 }
 void grad_event_wait(int64_t k, int64_t stream) {
   TORCH_CHECK(k >= 0 && k < 2, "grad_event_wait: group 0 or 1");
@@ -881,7 +891,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   };
   auto dw_done = [&]() {
     (void)hipEventRecord(ev_done, side.stream());
-    if (grad_ev) record_grad_event(aux.grad_ev[0], side.stream());
+    if (grad_ev) record_grad_event(aux.grad_ev[0], side.stream(), 0);
     if (early_comm) (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
   };
   stamp(STAMP_BWD_BEGIN, st);
@@ -1147,7 +1157,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
-  if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st);
+  if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st, 1);
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134
   // TFLOP/s at V = 10,509); a split-K batch over the largest divisor of V up to
@@ -1340,7 +1350,37 @@ std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Ten
   launch_scst_loss_fwd(seq.data_ptr<int64_t>(), lp.data_ptr<float>(), (int)R, (int)T,
                        sample.data_ptr<float>(), greedy.data_ptr<float>(),
                        (int)(R / greedy.numel()), reward.data_ptr<float>(), out.data_ptr<float>(),
-                       loss.data_ptr<float>(), ws.data_ptr<int>(), cur_stream());
+                       loss.data_ptr<float>(), ws.data_ptr<int>(), CstBase{nullptr, 0, 0},
+                       cur_stream());
+  return {loss, out, reward};
+}
+
+// CST loss (the same launch, consensus baseline): scores (R) fp32 of the
+// rewarded rows, S rows per video (R % S == 0, S <= 64); bref: (R) GT
+// consensus scores (scb_baseline 1) or empty (scb_baseline 2: the scores
+// themselves); k = scb_captions (0: reward = score) -> {loss, out, reward}
+std::vector<at::Tensor> cst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor scores,
+                                         at::Tensor bref, int64_t S, int64_t k) {
+  for (auto* t : {&seq, &lp, &scores}) check_cuda(*t, "cst_loss operand");
+  const int64_t R = seq.size(0), T = seq.size(1);
+  const bool has_ref = bref.defined() && bref.numel() > 0;
+  TORCH_CHECK(seq.scalar_type() == at::kLong && lp.scalar_type() == at::kFloat &&
+                  lp.size(0) == R && lp.size(1) == T && scores.scalar_type() == at::kFloat &&
+                  scores.numel() == R && S >= 1 && S <= 64 && R % S == 0 && k >= 0 && k <= S,
+              "cst_loss: seq / lp (R, T), scores (R), 1 <= S <= 64 dividing R, 0 <= k <= S");
+  if (has_ref) {
+    check_cuda(bref, "cst_loss bref");
+    TORCH_CHECK(bref.scalar_type() == at::kFloat && bref.numel() == R, "cst_loss: bref (R) fp32");
+  }
+  auto f32 = lp.options();
+  at::Tensor out = at::empty({4}, f32), reward = at::empty({R}, f32), loss = at::empty({}, f32);
+  at::Tensor ws = at::zeros({scst_loss_ws_ints((int)R)}, f32.dtype(at::kInt));
+  launch_scst_loss_fwd(seq.data_ptr<int64_t>(), lp.data_ptr<float>(), (int)R, (int)T,
+                       scores.data_ptr<float>(), scores.data_ptr<float>(), 1,
+                       reward.data_ptr<float>(), out.data_ptr<float>(), loss.data_ptr<float>(),
+                       ws.data_ptr<int>(),
+                       CstBase{has_ref ? bref.data_ptr<float>() : nullptr, (int)S, (int)k},
+                       cur_stream());
   return {loss, out, reward};
 }
 

@@ -5,6 +5,12 @@
 // for the shape are timed once (outside any graph capture) and the fastest is
 // cached per (shape, layout) and reused, also inside captured graphs.
 //
+// Reproducibility: the candidates are timed on an IDLE device (the device is
+// synchronised first, so the step's concurrent kernels do not skew the
+// choice), and CSTCAP_BLASLT_ALGO=<i> pins candidate i of the heuristic list
+// (0 = the heuristic's first choice, PyTorch's pick) with no timing at all.
+// gemm_tuned_choices() reports the chosen candidate per shape (bench JSON).
+//
 // Row-major tensors are passed to the column-major API as their transposes:
 // C (M x N, row-major) = op(A) op(B) is computed as C^T = op(B)^T op(A)^T.
 #include <torch/extension.h>
@@ -31,6 +37,7 @@ struct Plan {
   hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
   hipblasLtMatmulAlgo_t algo{};
   bool have_algo = false;
+  int chosen = -1;  // index in the heuristic's list
   size_t ws = 0;
   std::vector<std::pair<int, float>> timings;  // (candidate, us)
 };
@@ -90,12 +97,26 @@ Plan& get_plan(int dev, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ld
   auto& ws = S.workspace[dev];
   if (!ws.defined())
     ws = at::empty({(int64_t)kWorkspace}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
+  static const int pinned = [] {
+    const char* e = getenv("CSTCAP_BLASLT_ALGO");
+    return e != nullptr && e[0] != 0 ? atoi(e) : -1;
+  }();
+  if (pinned >= 0 && pinned < got && res[pinned].workspaceSize <= kWorkspace) {
+    p.algo = res[pinned].algo;
+    p.ws = res[pinned].workspaceSize;
+    p.chosen = pinned;
+    p.have_algo = true;
+    return p;
+  }
   if (capturing(st) || got == 1) {  // no timing inside a capture: the heuristic's first
     p.algo = res[0].algo;
     p.ws = res[0].workspaceSize;
+    p.chosen = 0;
     p.have_algo = !capturing(st);
     return p;
   }
+  // time on an idle device: whatever else the step has in flight finishes first
+  (void)hipDeviceSynchronize();
   const float one = 1.f, zero = 0.f;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
@@ -126,6 +147,7 @@ Plan& get_plan(int dev, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ld
   TORCH_CHECK(!p.timings.empty(), "hipBLASLt: no runnable algorithm");
   p.algo = res[bi].algo;
   p.ws = res[bi].workspaceSize;
+  p.chosen = bi;
   p.have_algo = true;
   return p;
 }
@@ -168,6 +190,21 @@ std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at
   auto it = state().plans.find(key);
   if (it == state().plans.end()) return v;
   for (auto& t : it->second.timings) v.push_back(t.second);
+  return v;
+}
+
+// every tuned plan: {m, n, k (column-major terms), chosen candidate, its us}
+std::vector<std::vector<double>> gemm_tuned_choices() {
+  std::vector<std::vector<double>> v;
+  for (auto& kv : state().plans) {
+    const Plan& p = kv.second;
+    if (!p.have_algo) continue;
+    double us = -1.0;
+    for (auto& t : p.timings)
+      if (t.first == p.chosen) us = t.second;
+    v.push_back({(double)std::get<1>(kv.first), (double)std::get<2>(kv.first),
+                 (double)std::get<3>(kv.first), (double)p.chosen, us});
+  }
   return v;
 }
 

@@ -1,4 +1,4 @@
-// P19 + P21 on the device in two launches: the self-critical reward
+// P19 + P21 (and P22, CST) on the device in two launches: the self-critical reward
 // (sample CIDEr-D - greedy CIDEr-D, /root/reference/utils.py:215-224), the
 // reference's reward mask (a row's first token always counts, later tokens
 // while the previous one was not EOS; model.py RewardCriterion) and the
@@ -31,14 +31,17 @@ __device__ __forceinline__ float block_sum_256(float v, float* sh) {
   return t;
 }
 
-// out = {loss, mean(sample), mean(greedy per row), sum(mask)},
-// reward[r] = sample[r] - greedy[r / gdiv]; ws: scst_loss_ws_ints(R) ints,
+// out = {loss, mean(sample), mean(baseline score per row), sum(mask)},
+// reward[r] = sample[r] - greedy[r / gdiv] (SCST, cb.S == 0), or
+// sample[r] - mean of the cb.k lowest of the video's cb.S reference scores
+// (CST; the logged b: mean(bref) with GT consensus scores, mean(baseline)
+// with the samples' own, 0 for k = 0); ws: scst_loss_ws_ints(R) ints,
 // the ticket word (ws[0]) zero at the first launch (re-armed by the kernel)
 __global__ __launch_bounds__(256) void scst_loss_fwd_kernel(
     const int64_t* __restrict__ seq, const float* __restrict__ lp, int R, int T,
     const float* __restrict__ sample, const float* __restrict__ greedy, int gdiv,
     float* __restrict__ reward, float* __restrict__ out, float* __restrict__ loss,
-    int* __restrict__ ws) {
+    int* __restrict__ ws, CstBase cb) {
   __shared__ float sh[4];
   __shared__ int s_last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -47,11 +50,36 @@ __global__ __launch_bounds__(256) void scst_loss_fwd_kernel(
   for (int j = 0; j < SL_ROWS / 4; ++j) {
     const int r = blockIdx.x * SL_ROWS + w * (SL_ROWS / 4) + j;
     if (r >= R) break;
-    const float sv = sample[r], gv = greedy[r / gdiv], rw = sv - gv;
+    const float sv = sample[r];
+    float gv, gl;  // baseline of the row, its logged value
+    if (cb.S > 0) {
+      // CST (utils.py:292-324): the mean of the video's scb_captions lowest
+      // reference scores (the GT consensus scores, or the samples' own).
+      // Lane j holds score j of the video; its rank (ties by index) says
+      // whether it is among the k lowest -- the selection of a stable sort
+      // without sorting.
+      float base = 0.f;
+      if (cb.k > 0) {
+        const int v0 = (r / cb.S) * cb.S;
+        const float* ref = cb.bref != nullptr ? cb.bref : sample;
+        const float x = lane < cb.S ? ref[v0 + lane] : 0.f;
+        int rank = 0;
+        for (int i = 0; i < cb.S; ++i) {
+          const float y = __shfl(x, i, 64);
+          rank += (y < x || (y == x && i < lane)) ? 1 : 0;
+        }
+        base = wave_sum(lane < cb.S && rank < cb.k ? x : 0.f) / (float)cb.k;
+      }
+      gv = base;
+      gl = cb.k == 0 ? 0.f : (cb.bref != nullptr ? cb.bref[r] : base);
+    } else {
+      gv = gl = greedy[r / gdiv];
+    }
+    const float rw = sv - gv;
     if (lane == 0) {
       reward[r] = rw;
       ssum += sv;
-      gsum += gv;
+      gsum += gl;
     }
     const int64_t* srow = seq + (int64_t)r * T;
     const float* lrow = lp + (int64_t)r * T;
@@ -73,11 +101,14 @@ __global__ __launch_bounds__(256) void scst_loss_fwd_kernel(
     __hip_atomic_store(part + 4 * blockIdx.x + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(part + 4 * blockIdx.x + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int ticket = __hip_atomic_fetch_add(ws, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release: the partial stores above happen-before the ticket; the last
+    // arriver acquires (below) before it reads the other workgroups' partials
+    const int ticket = __hip_atomic_fetch_add(ws, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     s_last = ticket == (int)gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // last workgroup: the partials in workgroup order, 4 per thread pass
   float a[4] = {0.f, 0.f, 0.f, 0.f};
   if (threadIdx.x < 64) {
@@ -117,9 +148,9 @@ __global__ __launch_bounds__(256) void scst_loss_bwd_kernel(const int64_t* __res
 
 void launch_scst_loss_fwd(const int64_t* seq, const float* lp, int R, int T, const float* sample,
                           const float* greedy, int gdiv, float* reward, float* out, float* loss,
-                          int* ws, hipStream_t stream) {
+                          int* ws, CstBase cb, hipStream_t stream) {
   hipLaunchKernelGGL(scst_loss_fwd_kernel, dim3((R + SL_ROWS - 1) / SL_ROWS), dim3(256), 0, stream,
-                     seq, lp, R, T, sample, greedy, gdiv, reward, out, loss, ws);
+                     seq, lp, R, T, sample, greedy, gdiv, reward, out, loss, ws, cb);
   post_launch("scst_loss_fwd_kernel", stream);
 }
 

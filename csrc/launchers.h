@@ -296,9 +296,15 @@ void launch_featpool_bwd(const FeatPoolArgs& a, const float* dout, const float* 
 // ws: scst_loss_ws_ints(R) ints, zero before the first launch (the kernel
 // re-arms its ticket)
 int scst_loss_ws_ints(int R);
+// CST baseline of the fused loss (S == 0: SCST, the greedy scores)
+struct CstBase {
+  const float* bref;  // nullable (R) GT consensus scores (scb_baseline 1); null: the samples'
+  int S;              // rows (scores) per video, <= 64
+  int k;              // scb_captions: lowest scores averaged (0: no baseline)
+};
 void launch_scst_loss_fwd(const int64_t* seq, const float* lp, int R, int T, const float* sample,
                           const float* greedy, int gdiv, float* reward, float* out, float* loss,
-                          int* ws, hipStream_t stream);
+                          int* ws, CstBase cb, hipStream_t stream);
 void launch_scst_loss_bwd(const int64_t* seq, const float* reward, const float* out,
                           const float* dloss, int R, int T, float* dlp, hipStream_t stream);
 

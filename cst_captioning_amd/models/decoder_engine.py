@@ -844,24 +844,27 @@ class DecoderEngine:
     def _beam_graphed(self, vg, blog, K, T):
         """The whole beam decode (T-1 steps x 5 launches) replayed as one
         captured HIP graph per (videos, K, T): the weights are the engine's
-        persistent shadows (updated in place), the video gates are copied
-        into the graph's static input, the outputs cloned out."""
-        key = (tuple(vg.shape), int(K), int(T), blog.data_ptr())
+        persistent shadows (updated in place); the video gates and the fp32
+        logit bias are copied into the graph's own static buffers before each
+        replay (``blog`` may be a fresh temporary per call, so the graph never
+        reads the caller's memory), the outputs cloned out."""
+        key = (tuple(vg.shape), tuple(blog.shape), int(K), int(T))
         cache = self.__dict__.setdefault('_beam_graphs', {})
         ent = cache.get(key)
         if ent is None:
             if len(cache) >= 4:
                 cache.clear()
-            static_vg = vg.clone()
-            args = lambda: (self.wx, self.ptab, self.whh, self.wlog, blog, static_vg, K, T, BOS,
-                            [], self.cell, [], [])
+            static_vg, static_b = vg.clone(), blog.clone()
+            args = lambda: (self.wx, self.ptab, self.whh, self.wlog, static_b, static_vg, K, T,
+                            BOS, [], self.cell, [], [])
             _ext.ops().beam_search(*args())  # (kernel attributes, allocator, outside capture)
             torch.cuda.synchronize(vg.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 out = _ext.ops().beam_search(*args())
-            ent = cache[key] = (g, static_vg, out)
-        g, static_vg, out = ent
+            ent = cache[key] = (g, static_vg, static_b, out)
+        g, static_vg, static_b, out = ent
         static_vg.copy_(vg)
+        static_b.copy_(blog)
         g.replay()
         return out[0].clone(), out[1].clone()

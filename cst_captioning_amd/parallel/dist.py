@@ -10,9 +10,10 @@ layer adds DP for one node of MI355X GPUs, one process per GPU:
       final after its dW GEMM, which runs under the reverse LSTM loop), the
       embedding (final after its GEMM in the post-loop tail), then the rest.
       The fused backward marks the first two with events (external
-      event-record nodes inside a captured HIP graph), the comm stream waits
-      on them after each replay, and their all-reduces run while the rest of
-      the backward does -- eager RCCL, nothing captured.  Large slices are
+      event-record nodes inside a captured HIP graph); the comm stream (high
+      priority: a hardware queue of its own) waits on the step-start event and
+      on them -- never on the whole replay -- and their all-reduces run while
+      the rest of the backward does -- eager RCCL, nothing captured.  Large slices are
       what a point-to-point xGMI ring moves at full per-link bandwidth
       (~20 M params = 84 MB fp32).  --dp_update sharded: reduce-scatter ->
       Adam on the rank's 1/N shard -> all-gather of the updated parameters.
@@ -175,6 +176,9 @@ class FlatGradBucket:
         self.params = list(first) + [p for p in params if id(p) not in first_ids]
         self.groups = []  # streamed slices (set_groups)
         self.comm = None
+        self._ev_start = None
+        self._counts = None
+        self.events_ok = False
         self.on_zero = None
         if not self.params:
             raise ValueError('no trainable parameters')
@@ -280,16 +284,64 @@ class FlatGradBucket:
             self.groups.append((off, off + n))
             off += n
         if self.grad.is_cuda and self.comm is None:
-            self.comm = torch.cuda.Stream(device=self.grad.device)
+            # A HIGH-priority stream: the HIP runtime keeps one pool of
+            # hardware queues per priority (GPU_MAX_HW_QUEUES each), so this
+            # stream gets a queue of its own instead of sharing one of the 4
+            # normal-priority queues with the replayed graph -- an in-order
+            # queue shared with the graph would hold the collective behind
+            # the whole replay whatever the event says.
+            self.comm = torch.cuda.Stream(device=self.grad.device, priority=-1)
+            self._ev_start = torch.cuda.Event()
+        self._counts = None
+        self.events_ok = False
+
+    # -- streamed slices: ordering bookkeeping -------------------------------------
+    @staticmethod
+    def _event_counts():
+        from .. import _ext
+        return tuple(_ext.ops().grad_event_count(k) for k in range(2))
+
+    def mark_start(self):
+        """Record the step-start event on the current stream before a step's
+        device work is enqueued (eager forward or graph replay): the lower
+        bound of the comm stream (:meth:`all_reduce`)."""
+        if self.groups and self.comm is not None:
+            self._ev_start.record(torch.cuda.current_stream(self.grad.device))
+
+    def begin_step(self, record_start=True):
+        """Before a step's forward/backward is enqueued (``record_start``) or
+        captured (False: no event inside a capture): :meth:`mark_start` and a
+        snapshot of the engine's grad-event record counts, which
+        :meth:`end_enqueue` compares."""
+        if not self.groups or self.comm is None:
+            return
+        if record_start:
+            self.mark_start()
+        self._counts = self._event_counts()
+
+    def end_enqueue(self):
+        """After the step's backward was enqueued eagerly, or captured: True
+        when the backward recorded (or captured a record node of) the event of
+        every streamed slice.  Only then does :meth:`all_reduce` let the comm
+        stream start a slice before the backward is done."""
+        if not self.groups or self._counts is None:
+            self.events_ok = False
+            return False
+        now = self._event_counts()
+        self.events_ok = all(now[k] > self._counts[k] for k in range(len(self.groups)))
+        self._counts = None
+        return self.events_ok
 
     def all_reduce(self, ctx):
         """Reduce the gradient over ranks: fp32 wire -> the SUM (the mean is
         ``grad * grad_scale(ctx)``); bf16 wire -> the mean.
 
         wire 'fp32': RCCL ring all-reduces of the fp32 buffer -- with groups,
-        each leading slice on the comm stream once its event fired (they run
+        each leading slice on the comm stream once ITS event fired (they run
         while the enqueued backward still computes the rest), then the rest
-        on the current stream, which finally waits for the slices.  Every rank
+        on the current stream, which finally waits for the slices.  The comm
+        stream is ordered only behind the step-start event (:meth:`begin_step`)
+        and the slice events, never behind the whole backward.  Every rank
         issues the same collectives in the same order.  wire 'bf16': half the
         bytes on xGMI with fp32 accumulation -- every rank sends chunk j of
         its gradient as bf16 to rank j (all-to-all), sums the N received chunks
@@ -315,14 +367,27 @@ class FlatGradBucket:
             dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
             return
         from .. import _ext
+        from ..utils import stamps
         main = torch.cuda.current_stream(self.grad.device)
-        self.comm.wait_stream(main)  # (everything enqueued before this step's backward)
+        events_ok, self.events_ok = self.events_ok, False  # (one step's verdict)
+        if events_ok:
+            self.comm.wait_event(self._ev_start)
+        else:  # this step recorded no slice events: order behind the whole step
+            self.comm.wait_stream(main)
+        # nccl (RCCL): a synchronous collective is enqueued on the CURRENT
+        # stream (the comm stream here) and returns without blocking the host;
+        # gloo (shared-GPU tests): asynchronous work joined below
+        sync_on_stream = ctx.backend == 'nccl'
         works = []
         with torch.cuda.stream(self.comm):
             for k, (lo, hi) in enumerate(self.groups):
-                _ext.ops().grad_event_wait(k, self.comm.cuda_stream)
-                works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM,
-                                             async_op=True))
+                if events_ok:
+                    _ext.ops().grad_event_wait(k, self.comm.cuda_stream)
+                stamps.mark('comm%d' % k)
+                w = dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM,
+                                    async_op=not sync_on_stream)
+                if w is not None:
+                    works.append(w)
         dist.all_reduce(self.grad[self.groups[-1][1]:], op=dist.ReduceOp.SUM)
         for w in works:
             w.wait()

@@ -259,6 +259,16 @@ class Trainer:
                 scores = scorer.score(model_res, vid_rows).float().view(-1, S)
             else:
                 scores = bcmr.float()
+            if self.engine is not None and self.device.type == 'cuda':
+                # fused: consensus baseline, reward, mask and REINFORCE loss in
+                # one launch (csrc/kernels/loss.hip, CST mode)
+                from ..ops.scst_loss import cst_loss
+                loss, reward, m_score, b_score = cst_loss(
+                    model_res, logprobs, scores, None if bcmr is None else bcmr.float(),
+                    scb_captions, opt.scb_baseline)
+                stamps.mark('loss')
+                self.timer.mark('reward')
+                return loss, {'reward': reward, 'm': m_score, 'b': b_score, 'seq': model_res}
             reward, m_score, b_score = cst_from_scores(scores, bcmr, scb_captions,
                                                        opt.scb_baseline)
         self.timer.mark('reward')
@@ -365,7 +375,9 @@ class Trainer:
             out = self._graph_step(data, mixer_from, scb)
             if out is not None:
                 return out
+        self.bucket.begin_step()
         extra, skip = self._forward_backward(data, mixer_from, scb)
+        self._check_grad_events()
         if self.bucket.sharded:
             self._sharded_update(skip)
             return extra
@@ -416,6 +428,9 @@ class Trainer:
                     dst.copy_(src, non_blocking=True)
         self.optimizer.sync_lr()
         g_a, g_b = self._graph
+        if g_b is not None:  # data parallel: the comm stream's lower bound
+            self.bucket.mark_start()
+            self.bucket.events_ok = self._graph_events_ok
         g_a.replay()
         if self.bucket.sharded:  # data parallel, sharded update: eager after the graph
             self._sharded_update(self._graph_skip)  # (calls engine.after_step)
@@ -427,6 +442,18 @@ class Trainer:
             # table an eval may have refreshed since is stale again
             self.engine.after_step()
         return self._graph_out
+
+    def _check_grad_events(self):
+        """After a step's backward was enqueued or captured: did it record
+        the event of every streamed DP slice?  If the streamed all-reduce is
+        configured but an event is missing, the comm stream falls back to
+        waiting for the whole step (correct, not overlapped) -- logged once."""
+        ok = self.bucket.end_enqueue()
+        if self.bucket.groups and not ok and not getattr(self, '_warned_events', False):
+            self._warned_events = True
+            logger.warning('the backward did not record every gradient-slice event: the DP '
+                           'all-reduce waits for the whole step (no overlap)')
+        return ok
 
     def _copy_flat(self, idx):
         """The loader's index tensors are consecutive pieces of one upload:
@@ -474,6 +501,7 @@ class Trainer:
             loader.set_index_target(flat)
         pool = torch.cuda.graph_pool_handle()
         g_a = torch.cuda.CUDAGraph()
+        self.bucket.begin_step(record_start=False)
         with torch.cuda.graph(g_a, pool=pool):
             # the batch gather is captured too, each part on first use
             batch = LazyGather(loader, self._static_idx)
@@ -481,6 +509,8 @@ class Trainer:
             extra, skip = self._forward_backward(batch, mixer_from, scb)
             if not self.ctx.enabled:
                 self._apply_update(skip)
+        # every replay runs the captured record nodes of the slice events
+        self._graph_events_ok = self._check_grad_events()
         g_b = None
         if self.ctx.enabled and not self.bucket.sharded:
             g_b = torch.cuda.CUDAGraph()

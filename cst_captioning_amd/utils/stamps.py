@@ -19,7 +19,8 @@ import torch
 # trainer phases (slot), then the executor's slot bases (csrc/launchers.h
 # StampSlot: forward 0..2, backward 0..10)
 TRAINER = ['step', 'rollout_enq', 'greedy_begin', 'greedy_end', 'sample_scores', 'loss',
-           'bwd_end', 'adam_begin', 'adam_end', 'ptab_end', 'x_end', 'gathered', 'prev_end']
+           'bwd_end', 'adam_begin', 'adam_end', 'ptab_end', 'x_end', 'gathered', 'prev_end',
+           'comm0', 'comm1']
 # executor slots 0..2 (csrc), 3: the decode's prologue (video gates) done (Python)
 FWD = ['begin', 'step0', 'end', 'vgate']
 BWD = ['begin', 'onehot', 'dhd0', 'dhd', 'loop0', 'loop', 'dw', 'side', 'toksum', 'tokgemm',

@@ -1,0 +1,60 @@
+"""Worker of tests/test_gpu_dist.py::test_dp_slice_allreduce_starts_inside_the_backward
+(torchrun, 2 ranks sharing the test box's GPU, gloo backend).
+
+The TRAINER's data-parallel path at a headline-like width (LSTM 512, 320
+caption rows, L = 30, V = 4,000): SCST steps captured and replayed as HIP
+graphs around the streamed bucket all-reduce (parallel/dist.py).  Device
+stamps (utils/stamps.py) are on: the comm stream stamps ``comm0`` right
+after it waited for the vocab-head slice's event and ``comm1`` after the
+embedding slice's; the replayed graph stamps ``bwd_end`` when the whole
+backward is done.  Rank 0 saves the stamps of a few replayed steps and
+whether every step's backward recorded its slice events."""
+import os
+import sys
+
+import torch
+
+from cst_captioning_amd.cli import build_model, load_splits
+from cst_captioning_amd.config import parse_opts
+from cst_captioning_amd.data import CaptionLoader
+from cst_captioning_amd.parallel import init_distributed
+from cst_captioning_amd.train.trainer import Trainer
+from cst_captioning_amd.utils import stamps
+
+ARGS = ['--synthetic', 'msrvtt', '--synthetic_videos', '64', '--synthetic_vocab', '4000',
+        '--seq_length', '30', '--rnn_size', '512', '--input_encoding_size', '512',
+        '--feat_dims', '512', '256', '--batch_size', '16', '--train_seq_per_img', '20',
+        '--test_batch_size', '4', '--test_seq_per_img', '20', '--impl', 'hip',
+        '--loglevel', 'WARNING', '--cuda_graph', '1', '--language_eval', '0',
+        '--use_rl', '1', '--use_mixer', '1', '--mixer_from', '1', '--use_eos', '1']
+
+
+def main(out):
+    ctx = init_distributed()
+    opt = parse_opts(ARGS)
+    tr_split, _, _ = load_splits(opt)
+    loader = CaptionLoader(tr_split, opt.batch_size, opt.train_seq_per_img, 'train', ctx.device,
+                           ctx.rank, ctx.world_size, opt.seed)
+    opt.vocab, opt.vocab_size = loader.get_vocab(), loader.get_vocab_size()
+    opt.seq_length, opt.feat_dims = loader.get_seq_length(), loader.get_feat_dims()
+    model, engine = build_model(opt, ctx.device)
+    assert engine is not None
+    tr = Trainer(opt, model, loader, None, ctx, engine)
+    tr.rl_training = True
+    stamps.enable(ctx.device)  # before the capture: the graph carries the stamp nodes
+    runs = []
+    oks = []
+    for i in range(6):
+        tr.train_step(loader.get_batch(), 0)
+        oks.append(bool(tr._graph is not None and tr._graph_events_ok))
+        if i >= 3:
+            runs.append(stamps.read())
+    stamps.disable()
+    if ctx.is_main:
+        torch.save({'stamps': runs, 'events_ok': oks, 'graphed': tr._graph is not None,
+                    'comm_priority': tr.bucket.comm.priority}, out)
+    ctx.destroy()
+
+
+if __name__ == '__main__':
+    main(sys.argv[1])

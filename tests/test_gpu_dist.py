@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _run(world, out, graph, wire='fp32', update='allreduce', mode='xe'):
+def _run(world, out, graph, wire='fp32', update='allreduce', mode='xe', worker='dist_worker.py'):
     env = dict(os.environ, CSTCAP_TEST_GRAPH=str(graph), CSTCAP_TEST_WIRE=wire,
                CSTCAP_TEST_DPUPDATE=update, CSTCAP_TEST_MODE=mode)
     env.update(PYTHONPATH=ROOT + os.pathsep + env.get('PYTHONPATH', ''), CSTCAP_SHARE_GPU='1',
@@ -34,7 +34,7 @@ def _run(world, out, graph, wire='fp32', update='allreduce', mode='xe'):
                PYTHONFAULTHANDLER='1')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node',
            str(world), '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-           os.path.join(HERE, 'dist_worker.py'), out]
+           os.path.join(HERE, worker), out]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return torch.load(out, weights_only=False)
@@ -114,3 +114,22 @@ def test_engine_dp_scst_step_matches_per_shard_mean(tmp_path):
     assert err < 1e-4, err
     assert r['same_after_steps']
     assert not torch.equal(r['rewards'][0], r['rewards'][1])
+
+
+def test_dp_slice_allreduce_starts_inside_the_backward(tmp_path):
+    """The shipped DP path overlaps communication with the backward: in the
+    trainer's replayed SCST step (two ranks, shared GPU), the comm stream
+    passes the vocab-head slice's event -- and would start that slice's
+    all-reduce -- while the replayed backward is still running: the
+    ``comm0`` stamp (enqueued eagerly on the comm stream after the event
+    wait) lands before the graph's own ``bwd_end`` stamp.  Before round 5 the
+    comm stream first waited for the whole replay, which this catches."""
+    r = _run(2, str(tmp_path / 'ov.pt'), 1, mode='overlap', worker='gpu_overlap_worker.py')
+    assert r['graphed'], 'the steps must be replayed graphs'
+    assert all(r['events_ok'][1:]), r['events_ok']  # captured record nodes of both slices
+    assert r['comm_priority'] < 0  # high priority: a hardware queue of its own
+    for st in r['stamps']:
+        assert 'comm0' in st and 'bwd_end' in st, st
+        # the vocab head is final under the reverse loop, long before the tail
+        assert st['comm0'] < st['bwd_end'] - 50.0, st
+        assert st['comm0'] > st.get('bwd.begin', 0.0), st
