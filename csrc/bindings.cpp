@@ -87,11 +87,6 @@ void stamp_buffer(at::Tensor buf);
 void stamp_now(int64_t slot);
 int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
-void gemm_nt_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant);
-void gemm_tn_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant);
-void gemm_sk_plan(int M, int N, int K, int G, int variant, int64_t* n_cnt, int64_t* n_slab);
-bool gemm_nt_sk_ok(int64_t M, int64_t N, int64_t K, int64_t variant);
-at::Tensor transpose_pad_bf16(at::Tensor w, int64_t ldo);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -180,15 +175,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stamp_now", &cst::stamp_now);
   m.def("wall_clock_khz", &cst::wall_clock_khz);
   m.def("vocab_x", &cst::vocab_x);
-  m.def("gemm_nt_sk", &cst::gemm_nt_sk, py::arg("out"), py::arg("a"), py::arg("b"),
-        py::arg("variant") = -1);
-  m.def("gemm_tn_sk", &cst::gemm_tn_sk, py::arg("out"), py::arg("a"), py::arg("b"),
-        py::arg("variant") = -1);
-  m.def("gemm_nt_sk_ok", &cst::gemm_nt_sk_ok);
-  m.def("gemm_sk_plan", [](int M, int N, int K, int G, int variant) {
-    int64_t c = 0, sl = 0;
-    cst::gemm_sk_plan(M, N, K, G, variant, &c, &sl);
-    return std::make_pair(c, sl);
-  });
-  m.def("transpose_pad_bf16", &cst::transpose_pad_bf16);
 }

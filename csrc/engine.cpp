@@ -55,129 +55,16 @@ void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
 
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand);
-// The vocab head's backward GEMMs through the measured hipBLASLt algorithm
-// choice (host/blaslt_tuned.cpp) instead of PyTorch's heuristic first choice.
-// Default: X = E W only (interleaved A/B 3.503-3.505 vs 3.562-3.574 ms per
-// step); dW_logit through it measured slower (3.683-3.731 vs 3.628-3.682)
-// and stays the split-K batch.  CSTCAP_TUNED_GEMM=1 both, =x X, =d dW, =0 none.
-static int tuned_gemm_mask() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("CSTCAP_TUNED_GEMM");
-    m = 1;
-    if (e != nullptr) m = e[0] == '1' ? 3 : e[0] == 'x' ? 1 : e[0] == 'd' ? 2 : 0;
-  }
-  return m;
-}
-static bool tuned_gemm_enabled() { return (tuned_gemm_mask() & 1) != 0; }
-static bool tuned_gemm_dw_enabled() { return (tuned_gemm_mask() & 2) != 0; }
-
-// Hand-written persistent GEMM (kernels/gemm_sk.hip): out (M x N fp32) =
-// a (M x K) b (N x K)^T or a (K x M)^T b (K x N), bf16 operands with unit
-// column stride and 16-byte-aligned rows.  Shapes it does not tile (N % BN,
-// K % 64) are refused; M is free (the edge tile's rows past M are dropped).
-// variant: 0 = 256 x 256 tiles, 2 LDS stages; 1 = 256 x 128 tiles, 3 stages.
-static int sk_default_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CSTCAP_SK_VARIANT");
-    v = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
-  return v;
-}
-bool gemm_nt_sk_ok(int64_t M, int64_t N, int64_t K, int64_t variant) {
-  const int64_t BN = variant == 1 ? 128 : 256;
-  return M > 0 && N > 0 && N % BN == 0 && K % 64 == 0 && K > 0 && M < (1 << 30);
-}
-static int64_t readable_bytes(const at::Tensor& t) {
-  return (int64_t)t.storage().nbytes() - t.storage_offset() * (int64_t)t.element_size();
-}
-// trans = false: out = a b^T, a (M x K), b (N x K).  trans = true: out =
-// a^T b, a (K x M), b (K x N) (both operands M / N-contiguous).
-static void gemm_sk(at::Tensor out, at::Tensor a, at::Tensor b, bool trans, int64_t variant) {
-  if (variant < 0) variant = sk_default_variant();
-  TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && a.scalar_type() == at::kBFloat16 &&
-                  b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kFloat &&
-                  a.dim() == 2 && b.dim() == 2 && out.dim() == 2 && a.stride(1) == 1 &&
-                  b.stride(1) == 1 && out.stride(1) == 1,
-              "gemm_sk: bf16 a, b with unit column stride, fp32 out with unit column stride");
-  const int64_t M = trans ? a.size(1) : a.size(0), K = trans ? a.size(0) : a.size(1);
-  const int64_t N = trans ? b.size(1) : b.size(0);
-  TORCH_CHECK((trans ? b.size(0) : b.size(1)) == K && out.size(0) == M && out.size(1) == N,
-              "gemm_sk: shapes");
-  TORCH_CHECK(gemm_nt_sk_ok(M, N, K, variant), "gemm_sk: N % ", variant == 1 ? 128 : 256,
-              " and K % 64 must be 0 (got M ", M, ", N ", N, ", K ", K, ")");
-  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
-                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
-              "gemm_sk: 16-byte-aligned rows");
-  if (trans) {
-    TORCH_CHECK(a.stride(0) >= M && K * a.stride(0) * 2 < (int64_t(1) << 31) &&
-                    K * b.stride(0) * 2 < (int64_t(1) << 31) && out.stride(0) * M * 4 < (int64_t(1) << 31),
-                "gemm_sk (trans): operand / output byte offsets must fit 31 bits");
-  } else {
-    TORCH_CHECK(a.stride(0) * 2 * 256 < (int64_t(1) << 31) &&
-                    b.stride(0) * 2 * 256 < (int64_t(1) << 31) &&
-                    out.stride(0) * 4 * 256 < (int64_t(1) << 31),
-                "gemm_sk: tile byte offsets must fit 31 bits");
-  }
-  int dev = 0, G = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&G, hipDeviceAttributeMultiprocessorCount, dev);
-  // CSTCAP_SK_GRID: fewer persistent workgroups than CUs (A/B: leave CUs to a
-  // concurrent stream, e.g. the reverse loop next to dW_logit)
-  static const int grid_env = [] {
-    const char* e = getenv("CSTCAP_SK_GRID");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  if (grid_env >= 8 && grid_env < G) G = grid_env / 8 * 8;
-  TORCH_CHECK(G % 8 == 0, "gemm_sk: CU count must be a multiple of the 8 XCDs");
-  int64_t n_cnt = 0, n_slab = 0;
-  gemm_sk_plan((int)M, (int)N, (int)K, G, (int)variant, &n_cnt, &n_slab);
-  auto opts = out.options();
-  at::Tensor cnt = at::zeros({std::max<int64_t>(n_cnt, 1)}, opts.dtype(at::kInt));
-  at::Tensor slab = at::empty({std::max<int64_t>(n_slab, 1)}, opts);
-  launch_gemm_sk(reinterpret_cast<const uint16_t*>(a.data_ptr()), a.stride(0), readable_bytes(a),
-                 reinterpret_cast<const uint16_t*>(b.data_ptr()), b.stride(0), readable_bytes(b),
-                 out.data_ptr<float>(), out.stride(0), (int)M, (int)N, (int)K, trans, G,
-                 (int)variant, slab.data_ptr<float>(), cnt.data_ptr<int>(), cur_stream());
-}
-void gemm_nt_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant) {
-  gemm_sk(out, a, b, false, variant);
-}
-void gemm_tn_sk(at::Tensor out, at::Tensor a, at::Tensor b, int64_t variant) {
-  gemm_sk(out, a, b, true, variant);
-}
-// W (rows x cols bf16) -> W^T (cols x ldo), zero columns past rows
-at::Tensor transpose_pad_bf16(at::Tensor w, int64_t ldo) {
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 &&
-                  w.is_contiguous() && ldo >= w.size(0),
-              "transpose_pad_bf16: contiguous bf16 (rows, cols), ldo >= rows");
-  at::Tensor out = at::empty({w.size(1), ldo}, w.options());
-  launch_transpose_pad_bf16(reinterpret_cast<const uint16_t*>(w.data_ptr()), (int)w.size(0),
-                            (int)w.size(1), reinterpret_cast<uint16_t*>(out.data_ptr()), ldo,
-                            cur_stream());
-  return out;
-}
-// The vocab head's backward GEMMs through the hand-written GEMM (A/B runs):
-// CSTCAP_SK_GEMM=1 both, =x X = E W only, =d dW_logit only; default off
-// (interleaved full-step A/B: 3.80-3.81 vs 3.68-3.70 ms per step with both,
-// profiles/r4/README_r4.md)
-static int sk_gemm_mask() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("CSTCAP_SK_GEMM");
-    m = 0;
-    if (e != nullptr) m = e[0] == '1' ? 3 : e[0] == 'x' ? 1 : e[0] == 'd' ? 2 : 0;
-  }
-  return m;
-}
-static bool sk_gemm_enabled() { return (sk_gemm_mask() & 1) != 0; }
-static bool sk_gemm_dw_enabled() { return (sk_gemm_mask() & 2) != 0; }
 
 // X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
 // fp32, on the current stream (engine.launch_x; the same GEMM as the
-// backward's dHd chunks)
+// backward's dHd chunks), through hipBLASLt's measured algorithm choice
+// (host/blaslt_tuned.cpp: the heuristic's 32 candidates timed once on an idle
+// device, or pinned by CSTCAP_BLASLT_ALGO): interleaved A/B 3.503-3.505 vs
+// 3.562-3.574 ms per step against PyTorch's first choice, profiles/r4.
+// (A 3-way split-K batch measured slower: 3.74 vs 3.67-3.73 ms per step,
+// profiles/r3/ab_xsplitk.txt; the round-4 hand-written persistent GEMM was
+// correct but slower in the step, 3.80 vs 3.68 ms, and was removed.)
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
   TORCH_CHECK(logits16.is_cuda() && logits16.scalar_type() == at::kBFloat16 &&
                   logits16.dim() == 3 && logits16.is_contiguous(),
@@ -186,28 +73,9 @@ void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out) {
   TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kFloat && out.numel() == NR * H &&
                   logits16.size(2) >= V,
               "vocab_x: out must be a contiguous fp32 (n, R, H) tensor");
-  at::Tensor dst = out.view({NR, H});
-  // (a 3-way split-K batch measured slower: 3.74 vs 3.67-3.73 ms per step,
-  // profiles/r3/ab_xsplitk.txt)
   const int64_t ldl = logits16.size(2);
-  if (sk_gemm_enabled() && gemm_nt_sk_ok(NR, H, ldl, sk_default_variant())) {
-    // the exp store's columns past V hold 0 up to ldl (kernels/vocab.hip), and
-    // W^T's padded columns are 0: K = ldl, no tail
-    gemm_nt_sk(dst, logits16.view({NR, ldl}), transpose_pad_bf16(wlog, ldl), -1);
-    return;
-  }
-  at::Tensor Ev = logits16.view({NR, ldl}).narrow(1, 0, V);
-  if (tuned_gemm_enabled()) {
-    // heuristic candidates timed (CSTCAP_TUNED_NCAND, default 32)
-    static const int ncand = [] {
-      const char* e = getenv("CSTCAP_TUNED_NCAND");
-      const int v = e != nullptr ? atoi(e) : 32;
-      return v >= 1 && v <= 256 ? v : 32;
-    }();
-    gemm_bf16_tuned(dst, Ev, false, wlog, false, ncand);
-    return;
-  }
-  at::mm_out(dst, Ev, wlog, at::kFloat);
+  gemm_bf16_tuned(out.view({NR, H}), logits16.view({NR, ldl}).narrow(1, 0, V), false, wlog, false,
+                  32);
 }
 int64_t wall_clock_khz() {
   int dev = 0, khz = 0;
@@ -844,20 +712,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const bool early_comm = early && comm_stream != 0;
   // DP overlap (set_grad_events): vocab head / embedding gradients final events
   const bool grad_ev = g_grad_events_on && early;
-  // vh_sched 2: dW_logit and the bias column sums on the side stream under
-  // the latency-bound reverse loop (data parallelism: the vocab head's
-  // all-reduce starts there too).  vh_sched 3: the sums under the loop,
-  // dW_logit after it (the round-3 one-GPU choice: 3.745-3.792 vs 3.774-3.831
-  // ms per step against schedule 0, profiles/r3/ab_sched.txt)
-  // Round 4: with the bias column sums in fewer workgroups (vocab_grad.hip
-  // colsum_rows) the concurrent schedule wins on one GPU too: interleaved A/B
-  // 3.591-3.604 vs 3.628-3.682 ms per step (profiles/r4/README_r4.md);
-  // CSTCAP_VH_SCHED=3 restores the loop-after schedule
-  static const int vh_env = [] {
-    const char* e = getenv("CSTCAP_VH_SCHED");
-    return e != nullptr ? atoi(e) : 2;
-  }();
-  const int vh_sched = (early_comm || grad_ev) ? 2 : (vh_env == 3 ? 3 : 2);
+  // dW_logit and the bias column sums run on the side stream under the
+  // latency-bound reverse loop (data parallelism: the vocab head's all-reduce
+  // starts there too).  Round 4: with the bias column sums in fewer
+  // workgroups (vocab_grad.hip) this beats the sums-under-the-loop /
+  // dW-after-it schedule on one GPU too: interleaved A/B 3.591-3.604 vs
+  // 3.628-3.682 ms per step (profiles/r4/README_r4.md).
   // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
   // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
   // split-K batch over groups of decode steps multiplies the tiles in flight,
@@ -867,14 +727,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
   auto dw_gemm = [&]() {  // (current stream: side)
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
-    if (sk_gemm_dw_enabled() && gemm_nt_sk_ok(V, H, NR, sk_default_variant())) {
-      gemm_tn_sk(dWlog, Ev, rhs, -1);  // E'^T (K = NR rows) x rhs, hand-written
-      return;
-    }
-    if (tuned_gemm_dw_enabled()) {  // one GEMM, the measured algorithm (split-K inside it)
-      gemm_bf16_tuned(dWlog, Ev, true, rhs, false, 32);
-      return;
-    }
+    // (hipBLASLt's measured choice as one GEMM: 3.683-3.731 vs 3.628-3.682 ms
+    // per step, the round-4 hand-written GEMM 3.746-3.795: the split-K batch)
     if (dw_split == 1) {
       at::mm_out(dWlog, Ev.t(), rhs, at::kFloat);
       return;
@@ -941,14 +795,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                         reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
                         reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
     stamp(STAMP_BWD_DHD, side.stream());
-    if (vh_sched == 2) {
-      dw_gemm();
-      stamp(STAMP_BWD_DW, side.stream());
-      db_sums(side.stream());
-      dw_done();
-    } else if (vh_sched == 3) {  // bias column sums (HBM-bound) under the loop
-      db_sums(side.stream());
-    }
+    dw_gemm();
+    stamp(STAMP_BWD_DW, side.stream());
+    db_sums(side.stream());
+    dw_done();
   }
   // token-only operands of the embedding / input-weight gradients: rows
   // grouped by input token (counting sort), per-token sum scratch
@@ -1131,21 +981,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // stream before returning.)
   // (starting them only after the main stream's per-token sums measured
   // slower: 3.76-3.81 vs 3.71-3.72 ms, profiles/r3/ab_toksum_first.txt)
-  // vh_sched 2: the recurrent-weight GEMMs after the input-token chain on the
-  // main stream (on the idle side stream after the loop, or their late steps'
+  // The recurrent-weight GEMMs run after the input-token chain on the main
+  // stream (on the idle side stream after the loop, or their late steps'
   // share on it during the loop, measured slower: they contend with the
-  // input-token chain / the loop, profiles/r4/README_r4.md)
-  if (vh_sched == 0 || vh_sched == 3) {
-    (void)hipEventRecord(ev_ready, st);  // reverse loop done
-    (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
-    c10::hip::HIPStreamGuard guard(side);
-    dw_gemm();
-    stamp(STAMP_BWD_DW, side.stream());
-    if (vh_sched == 0) db_sums(side.stream());
-    whh_grad();
-    stamp(STAMP_BWD_SIDE, side.stream());
-    dw_done();
-  }
+  // input-token chain / the loop, profiles/r4/README_r4.md).
 
   // 5. input-token gradients through the per-token sums S[v] = sum of the dG
   //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
@@ -1177,7 +1016,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       dWie.copy_(at::mm(S_tok.t(), emb, at::kFloat));
   }
   stamp(STAMP_BWD_TOKGEMM, st);
-  if (vh_sched == 2) whh_grad();
+  whh_grad();
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
     dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);
@@ -1569,30 +1408,12 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   }
   const uint16_t* W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
   const uint16_t* WHH = reinterpret_cast<const uint16_t*>(whh.data_ptr());
-  // CSTCAP_BEAM_ATT_MFMA=1: MFMA attention (the decode launch's att_mfma
-  // workgroups, launched on their own): the K beam rows of a video are its
-  // rows; the query input is h of each row's parent beam, gathered first.
-  // Off by default: with the gather and the bf16 -> fp32 gate copy it is
-  // three launches per step against the VALU scorer's two, 26.0k vs 29.6k
-  // videos/s at att8 beam 5 (profiles/r4/README_r4.md)
-  const char* bame = getenv("CSTCAP_BEAM_ATT_MFMA");  // (read per call: tests switch it)
-  const bool beam_att_mfma_env = bame != nullptr && bame[0] == '1';
-  const bool att_mfma_beam = has_att && beam_att_mfma_env && H4 == 4 * H &&
-                             att_mfma_ok((int)K, (int)C, (int)A, (int)H, per_frame);
-  at::Tensor gv16, vg16, hq, ep, cnt;
-  const int CP = C <= 8 ? 8 : 16;
+  // (MFMA attention for the beam rows -- parent-gathered query input, the
+  // decode launch's attention workgroups on their own -- measured slower,
+  // 26.0k vs 29.6k videos/s at att8 beam 5, profiles/r4/README_r4.md)
   if (has_att) {
     vg_rows = at::empty({R, H4}, f32);
     qb = at::empty({R, A}, f32);
-    if (att_mfma_beam) {
-      auto bf = wx.options().dtype(at::kBFloat16);
-      gv16 = at::zeros({B, H4, CP}, bf);  // (Bv, 4H, CP) frame-minor gate tables
-      gv16.narrow(2, 0, C).copy_(att[0].transpose(1, 2));
-      vg16 = at::empty({R, H4}, bf);
-      hq = at::empty({R, H}, bf);
-      ep = at::empty({B, A / 64, 32, CP}, f32);
-      cnt = at::zeros({B}, f32.dtype(at::kInt));
-    }
   }
   for (int64_t t = 0; t < T - 1; ++t) {
     if (t >= 1) {
@@ -1614,20 +1435,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
     const at::Tensor& cp = c[t & 1];
     at::Tensor& ho = h[(t + 1) & 1];
     at::Tensor& co = c[(t + 1) & 1];
-    if (att_mfma_beam) {
-      if (t >= 1)
-        at::index_select_out(hq, hp, 0, parent);
-      else
-        hq.copy_(hp);
-      AttMfmaArgs am{reinterpret_cast<const uint16_t*>(hq.data_ptr()),
-                     reinterpret_cast<const uint16_t*>(att[2].data_ptr()), att[1].data_ptr<float>(),
-                     att[3].data_ptr<float>(), att[4].data_ptr<float>(),
-                     reinterpret_cast<const uint16_t*>(gv16.data_ptr()), (int)H, (int)A, (int)C,
-                     CP, (int)H4, (int)K, (int)B, reinterpret_cast<uint16_t*>(vg16.data_ptr()),
-                     nullptr, nullptr, ep.data_ptr<float>(), cnt.data_ptr<int>()};
-      launch_att_mfma_fwd(am, st);
-      vg_rows.copy_(vg16);
-    } else if (has_att) {
+    if (has_att) {
       if (t >= 1) at::mm_out(qb, hp, att[2].t(), at::kFloat);
       launch_att_fwd(att[0].data_ptr<float>(), att[1].data_ptr<float>(),
                      t >= 1 ? qb.data_ptr<float>() : nullptr, t >= 1 ? parent.data_ptr<int>() : nullptr,

@@ -221,22 +221,14 @@ void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd
 // its chunk's 8 sums in registers over the rows (CS_UNROLL row loads in
 // flight) and writes one partial row per block; a second launch sums the
 // partials per column (deterministic, no atomics).
-// Rows per block (CSTCAP_COLSUM_ROWS, a multiple of CS_ROWS; default 1024):
-// 128 fills the chip (1,680 workgroups at the headline shape, ~160 us at HBM
-// rate) and delays the reverse loop the sums run under; 1024 (210 workgroups)
-// leaves most CU slots to the loop: interleaved A/B 3.559-3.579 vs
-// 3.602-3.611 ms per step, 4096 3.659-3.676 (profiles/r4/README_r4.md).
+// Rows per block: 128 fills the chip (1,680 workgroups at the headline shape,
+// ~160 us at HBM rate) and delays the reverse loop the sums run under; 1024
+// (210 workgroups) leaves most CU slots to the loop: interleaved A/B
+// 3.559-3.579 vs 3.602-3.611 ms per step, 4096 3.659-3.676, 768 3.465-3.486
+// vs 1024 3.477-3.479 (profiles/r4/README_r4.md).
 constexpr int CS_ROWS = 128, CS_UNROLL = 8;
 
-static int colsum_rows() {
-  static int rows = -1;
-  if (rows < 0) {
-    const char* e = getenv("CSTCAP_COLSUM_ROWS");
-    const int v = e != nullptr ? atoi(e) : 1024;
-    rows = v >= CS_ROWS ? v / CS_ROWS * CS_ROWS : CS_ROWS;
-  }
-  return rows;
-}
+static int colsum_rows() { return 1024; }
 
 int vgrad_colsum_blocks(int64_t NR) {
   const int rows = colsum_rows();

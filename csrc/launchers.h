@@ -6,15 +6,6 @@
 
 namespace cst {
 
-// gemm_sk.hip: persistent GEMM (C fp32 = A B^T or A^T B, bf16 operands) and its
-// workspace sizes (tickets, slab floats) for a grid of G workgroups
-void gemm_sk_plan(int M, int N, int K, int G, int variant, int64_t* n_cnt, int64_t* n_slab);
-void launch_gemm_sk(const uint16_t* A, int64_t lda, int64_t a_bytes, const uint16_t* B,
-                    int64_t ldb, int64_t b_bytes, float* C, int64_t ldc, int M, int N, int K,
-                    bool trans, int G, int variant, float* slab, int* cnt, hipStream_t stream);
-void launch_transpose_pad_bf16(const uint16_t* in, int rows, int cols, uint16_t* out, int64_t ldo,
-                               hipStream_t stream);
-
 // cider_d.hip
 void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
                     const int64_t* ht_keys, const float* ht_vals, uint32_t ht_cap,

@@ -779,22 +779,14 @@ class DecoderEngine:
         expand = opt.get('expand_feat', 0) == 1
         T = model.seq_length - 1
         modes = [SEL_GREEDY if sample_max == 1 else SEL_SAMPLE] * (T - 1)
-        # temporal attention, one greedy row per video (the SCST baseline):
-        # CSTCAP_GREEDY_DUP=1 decodes each video on TWO identical rows, so the
-        # MFMA attention of the decode launch applies (it needs >= 2 rows per
-        # video, vocab.hip att_mfma_ok) instead of a VALU attention launch + a
-        # query GEMM per step; row 0 of each pair is kept.  Off by default:
-        # the doubled greedy vocab work slows the concurrent sampled rollout
-        # more than the branch gains (att8 5.317 vs 5.197 ms per step,
+        # (temporal attention, one greedy row per video: decoding each video on
+        # two identical rows so the decode launch's MFMA attention applies
+        # measured slower, 5.317 vs 5.197 ms per att8 step -- the doubled
+        # greedy vocabulary work slows the concurrent sampled rollout,
         # profiles/r4/README_r4.md)
-        dup = (self.attention and not self.manet and not expand and sample_max == 1
-               and os.environ.get('CSTCAP_GREEDY_DUP', '0') == '1'
-               and self._att_mfma_shape_ok(model))
         seq, lp, _, _ = self._run(model, feats, None, modes, want_xe=False, use_counts=False,
                                   use_unfinished=True, expand=expand, drop=False,
-                                  temperature=temperature, rows_per_video=2 if dup else None)
-        if dup:
-            seq, lp = seq[0::2].contiguous(), lp[0::2].contiguous()
+                                  temperature=temperature)
         return seq, lp
 
     def _att_mfma_shape_ok(self, model):

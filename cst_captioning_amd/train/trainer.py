@@ -485,20 +485,15 @@ class Trainer:
         torch.cuda.synchronize(self.device)
         # the captured step must refresh the gate table itself on every replay
         self.engine.invalidate_ptab()
-        # one flat static buffer; with CSTCAP_IDX_ALIAS=1 the loader uploads
-        # later batches' indices straight into it (no device-to-device copies
-        # before each replay; measured neutral, 3.558-3.563 vs 3.553-3.579 ms,
-        # so off by default: a batch's indices then stay valid after the next
-        # batch is assembled)
+        # one flat static buffer, refreshed by one device copy per replay
+        # (uploading later batches straight into it measured neutral,
+        # 3.558-3.563 vs 3.553-3.579 ms, profiles/r4/README_r4.md)
         flat = torch.cat([t.reshape(-1) for t in idx])
         self._static_flat = flat
         self._static_idx, off = [], 0
         for t in idx:
             self._static_idx.append(flat[off:off + t.numel()].view(t.shape))
             off += t.numel()
-        if (hasattr(loader, 'set_index_target') and all(t.dim() == 1 for t in idx)
-                and os.environ.get('CSTCAP_IDX_ALIAS', '0') == '1'):
-            loader.set_index_target(flat)
         pool = torch.cuda.graph_pool_handle()
         g_a = torch.cuda.CUDAGraph()
         self.bucket.begin_step(record_start=False)

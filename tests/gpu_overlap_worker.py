@@ -1,14 +1,22 @@
 """Worker of tests/test_gpu_dist.py::test_dp_slice_allreduce_starts_inside_the_backward
-(torchrun, 2 ranks sharing the test box's GPU, gloo backend).
+(one process, fresh: a long-lived test process has created many streams).
 
-The TRAINER's data-parallel path at a headline-like width (LSTM 512, 320
-caption rows, L = 30, V = 4,000): SCST steps captured and replayed as HIP
-graphs around the streamed bucket all-reduce (parallel/dist.py).  Device
-stamps (utils/stamps.py) are on: the comm stream stamps ``comm0`` right
-after it waited for the vocab-head slice's event and ``comm1`` after the
-embedding slice's; the replayed graph stamps ``bwd_end`` when the whole
-backward is done.  Rank 0 saves the stamps of a few replayed steps and
-whether every step's backward recorded its slice events."""
+The data-parallel code path of the trainer with a 1-rank gloo process group
+standing in for the collectives: the trainer is told the job has 2 ranks
+(DistContext world_size 2), so it builds the streamed bucket, the slice
+events and the two graphs around the all-reduce exactly as under RCCL, while
+each "all-reduce" is a 1-rank no-op.  (Two processes sharing the one GPU of
+the test box time-slice the device at millisecond granularity, which says
+nothing about the order of one process's streams.)
+
+Headline-like width (LSTM 512, 320 caption rows, L = 30, V = 4,000): SCST
+steps captured and replayed as HIP graphs around the streamed bucket
+all-reduce (parallel/dist.py).  Device stamps (utils/stamps.py) are on: the
+comm stream stamps ``comm0`` right after it waited for the vocab-head
+slice's event and ``comm1`` after the embedding slice's; the replayed graph
+stamps ``bwd_end`` when the whole backward is done.  Saves the stamps of a
+few replayed steps and whether every step's backward recorded its slice
+events."""
 import os
 import sys
 
@@ -17,7 +25,6 @@ import torch
 from cst_captioning_amd.cli import build_model, load_splits
 from cst_captioning_amd.config import parse_opts
 from cst_captioning_amd.data import CaptionLoader
-from cst_captioning_amd.parallel import init_distributed
 from cst_captioning_amd.train.trainer import Trainer
 from cst_captioning_amd.utils import stamps
 
@@ -30,7 +37,14 @@ ARGS = ['--synthetic', 'msrvtt', '--synthetic_videos', '64', '--synthetic_vocab'
 
 
 def main(out):
-    ctx = init_distributed()
+    import torch.distributed as dist
+    from cst_captioning_amd.parallel import DistContext
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group('gloo', rank=0, world_size=1,
+                            init_method='tcp://127.0.0.1:%s' % sys.argv[2])
+    ctx = DistContext(rank=0, world_size=2, local_rank=0, device=dev, backend='gloo')
     opt = parse_opts(ARGS)
     tr_split, _, _ = load_splits(opt)
     loader = CaptionLoader(tr_split, opt.batch_size, opt.train_seq_per_img, 'train', ctx.device,
@@ -50,10 +64,9 @@ def main(out):
         if i >= 3:
             runs.append(stamps.read())
     stamps.disable()
-    if ctx.is_main:
-        torch.save({'stamps': runs, 'events_ok': oks, 'graphed': tr._graph is not None,
-                    'comm_priority': tr.bucket.comm.priority}, out)
-    ctx.destroy()
+    torch.save({'stamps': runs, 'events_ok': oks, 'graphed': tr._graph is not None,
+                'comm_priority': tr.bucket.comm.priority}, out)
+    dist.destroy_process_group()
 
 
 if __name__ == '__main__':

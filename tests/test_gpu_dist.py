@@ -118,18 +118,26 @@ def test_engine_dp_scst_step_matches_per_shard_mean(tmp_path):
 
 def test_dp_slice_allreduce_starts_inside_the_backward(tmp_path):
     """The shipped DP path overlaps communication with the backward: in the
-    trainer's replayed SCST step (two ranks, shared GPU), the comm stream
-    passes the vocab-head slice's event -- and would start that slice's
-    all-reduce -- while the replayed backward is still running: the
-    ``comm0`` stamp (enqueued eagerly on the comm stream after the event
-    wait) lands before the graph's own ``bwd_end`` stamp.  Before round 5 the
-    comm stream first waited for the whole replay, which this catches."""
-    r = _run(2, str(tmp_path / 'ov.pt'), 1, mode='overlap', worker='gpu_overlap_worker.py')
+    trainer's replayed SCST step (data-parallel code path, the collectives
+    of a 1-rank gloo group), the comm stream passes the vocab-head slice's
+    event -- where that slice's all-reduce starts -- while the replayed
+    backward is still running: the ``comm0`` stamp (enqueued eagerly on the
+    comm stream after the event wait) lands before the graph's own
+    ``bwd_end`` stamp.  Before round 5 the comm stream first waited for the
+    whole replay, which this catches."""
+    out = str(tmp_path / 'ov.pt')
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get('PYTHONPATH', ''),
+               CSTCAP_TEST_IMPL='hip', PYTHONFAULTHANDLER='1')
+    r = subprocess.run([sys.executable, os.path.join(HERE, 'gpu_overlap_worker.py'), out,
+                        str(_free_port())], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    r = torch.load(out, weights_only=False)
     assert r['graphed'], 'the steps must be replayed graphs'
     assert all(r['events_ok'][1:]), r['events_ok']  # captured record nodes of both slices
     assert r['comm_priority'] < 0  # high priority: a hardware queue of its own
     for st in r['stamps']:
-        assert 'comm0' in st and 'bwd_end' in st, st
+        assert 'comm0' in st and 'bwd_end' in st, sorted(st.items(), key=lambda kv: kv[1])
         # the vocab head is final under the reverse loop, long before the tail
-        assert st['comm0'] < st['bwd_end'] - 50.0, st
-        assert st['comm0'] > st.get('bwd.begin', 0.0), st
+        assert st['comm0'] < st['bwd_end'] - 50.0, sorted(st.items(), key=lambda kv: kv[1])
+        assert st['comm0'] > st.get('bwd.begin', 0.0), sorted(st.items(), key=lambda kv: kv[1])
