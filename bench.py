@@ -51,10 +51,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # BASELINE.md publishes no number for the metric (BASELINE.json "published":
-# {}), so vs_baseline is null; the self-measured reference-semantics and
-# same-precision PyTorch runs are reported as separate ratios
+# {}), so vs_baseline is null; the self-measured reference-semantics run is
+# reported as a separate ratio
 BASELINE_FILE = os.path.join(REPO, 'profiles', 'reference_semantics_baseline.json')
-SAME_PRECISION_FILE = os.path.join(REPO, 'profiles', 'r2', 'bench_r2_torch_bf16_autocast.json')
+BCMR_FILE = os.path.join(REPO, 'profiles', 'bench_bcmr_msrvtt_seed123.npz')
 
 
 def parse():
@@ -93,6 +93,13 @@ def parse():
                    help='scst, headline config: also time the beam-5 evaluation decode of one '
                         'batch (BASELINE config 5) on the trained weights and report it as the '
                         '"beam5" field')
+    p.add_argument('--cst', type=int, default=1,
+                   help='scst, headline config: also time the CST recipe (README "CST_MS_SCB": '
+                        'consensus baseline from the GT captions, --scb_baseline) in the same '
+                        'invocation and report it as the "cst" field')
+    p.add_argument('--scb_baseline', type=int, default=1, choices=[1, 2],
+                   help='CST baseline: 1 = GT consensus scores (CST_MS_SCB), 2 = the samples\' own '
+                        'scores (CST_MS_SCB(*))')
     p.add_argument('--json_out', default='')
     p.add_argument('--profile_phases', type=int, default=0,
                    help='print the mean per-phase GPU time (HIP events) of the timed steps')
@@ -132,10 +139,12 @@ def relaunch_if_needed(a):
     sys.exit(subprocess.call(cmd))
 
 
-def run_config(a, ctx, num_chunks, sync, sync_debug=0):
+def run_config(a, ctx, num_chunks, sync, sync_debug=0, mode=None):
     """Build the dataset, model, engine and trainer for ``num_chunks`` frames
     per video, run ``a.warmup`` untimed and ``a.steps`` timed steps (barrier +
-    synchronize on both sides, MAX over ranks) and free the GPU buffers."""
+    synchronize on both sides, MAX over ranks) and free the GPU buffers.
+    ``mode`` overrides ``a.mode`` (the extra CST run of an SCST bench)."""
+    mode = mode or a.mode
     import gc
     import torch
     from cst_captioning_amd.config import default_opts
@@ -147,6 +156,23 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
     t_gen = time.time()
     ds = make_synthetic('msrvtt', num_videos=a.videos, vocab_size=a.vocab, seed=a.seed,
                         num_chunks=num_chunks)
+    bcmr_src = None
+    if mode == 'cst' and a.scb_baseline == 1:
+        # GT consensus scores of CST_MS_SCB: prepro/evalscores.py's coco CIDEr
+        # of each GT caption against the video's other captions, cached for
+        # the bench dataset (scripts/make_bench_bcmr.py; the reference reads
+        # them from a file as well, dataloader.py:62-71)
+        import numpy as np
+        z = np.load(BCMR_FILE, allow_pickle=False) if os.path.exists(BCMR_FILE) else None
+        if (z is not None and int(z['seed']) == a.seed and int(z['videos']) == a.videos
+                and int(z['vocab']) == a.vocab):
+            ds.bcmrscores = np.asarray(z['CIDEr'], dtype=np.float64)
+            bcmr_src = 'prepro/evalscores.py (cached: %s)' % os.path.relpath(BCMR_FILE, REPO)
+        else:
+            from cst_captioning_amd.prepro.evalscores import compute_consensus_scores
+            ds.bcmrscores = compute_consensus_scores(ds.gt_refs, 20, True, tokenize=False,
+                                                     metrics=('CIDEr',))['CIDEr']
+            bcmr_src = 'prepro/evalscores.py'
     t_gen = time.time() - t_gen
     S = 20
     opt = default_opts(
@@ -155,8 +181,9 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
         drop_prob_lm=0.5, rnn_type=a.rnn_type, num_layers=a.num_layers, learning_rate=1e-4,
         grad_clip=0.25, model_type=a.model_type, num_chunks=num_chunks, eval_metric='CIDEr',
         max_epochs=10 ** 9, print_log_interval=0,
-        use_rl=1 if a.mode != 'xe' else 0, use_rl_after=0, use_cst=1 if a.mode == 'cst' else 0,
-        use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=2, scb_captions=S,
+        use_rl=1 if mode != 'xe' else 0, use_rl_after=0, use_cst=1 if mode == 'cst' else 0,
+        use_mixer=1, mixer_from=1, use_eos=1, expand_feat=1, scb_baseline=a.scb_baseline,
+        scb_captions=S,
         impl=a.impl, precision=a.precision, reward_device=a.reward,
         dedupe_greedy=a.dedupe_greedy, seed=a.seed, loglevel='WARNING', save_last=0,
         profile_phases=a.profile_phases, cuda_graph=a.cuda_graph, grad_wire=a.grad_wire)
@@ -168,12 +195,12 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
     loader = CaptionLoader(ds, a.batch_size, S, 'train', dev, ctx.rank, ctx.world_size, a.seed)
     model, engine = build_model(opt, dev, a.impl)
     trainer = Trainer(opt, model, loader, None, ctx, engine)
-    trainer.rl_training = a.mode != 'xe'
+    trainer.rl_training = mode != 'xe'
     n_params = sum(p.numel() for p in model.parameters())
 
     def step():
         data = loader.get_batch()
-        if a.mode == 'beam':  # BASELINE config 5: beam-5 evaluation decode
+        if mode == 'beam':  # BASELINE config 5: beam-5 evaluation decode
             model.eval()
             with torch.no_grad():
                 seq, _ = model.sample(data['feats'], {'beam_size': a.beam_size})
@@ -234,7 +261,7 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
             print('  %9.1f  %s' % (v, k), file=sys.stderr)
         sys.stderr.flush()
     beam = None
-    if (a.beam5 and a.mode == 'scst' and num_chunks == 1 and engine is not None
+    if (a.beam5 and mode == 'scst' and num_chunks == 1 and engine is not None
             and dev.type == 'cuda'):
         # BASELINE config 5: beam-5 evaluation decode of one batch (64 videos
         # per rank) with the weights the timed steps trained
@@ -265,13 +292,27 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0):
            'exp_fix': int(engine.exp_fix_rows.item()) if engine is not None else None,
            'graph': int(trainer._graph is not None), 'n_params': n_params, 't_gen': t_gen,
            'bf16': engine is not None or trainer.autocast_bf16, 'stamps': stamp_mean,
-           'beam5': beam}
+           'beam5': beam, 'bcmr': bcmr_src, 'blaslt': _blaslt_choices(engine)}
     del trainer, model, engine, loader, ds, step, out
     gc.collect()
     if dev.type == 'cuda':
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
     return res
+
+
+def _blaslt_choices(engine):
+    """The hipBLASLt algorithm the X = E W plan chose per shape (candidate
+    index in the heuristic's list, its measured us): recorded so a run's
+    numerics can be reproduced with CSTCAP_BLASLT_ALGO=<index>."""
+    if engine is None:
+        return None
+    from cst_captioning_amd import _ext
+    try:
+        return [{'m': int(c[0]), 'n': int(c[1]), 'k': int(c[2]), 'candidate': int(c[3]),
+                 'us': round(c[4], 1)} for c in _ext.ops().gemm_tuned_choices()]
+    except Exception:
+        return None
 
 
 def main():
@@ -300,6 +341,15 @@ def main():
                 'skipped_steps': r['skipped']}
         if r['stamps']:
             att8['stamps_us'] = r['stamps']
+    cst = None
+    if a.cst and a.mode == 'scst' and a.num_chunks == 1:
+        # the CST recipe of the same job (the reference's namesake), same steps
+        # / warmup, after the previous runs' buffers are freed
+        r = run_config(a, ctx, 1, sync, mode='cst')
+        cst = {'value': round(r['caps'], 2), 'ms_per_step': round(r['ms'], 3),
+               'recipe': 'CST_MS_SCB' if a.scb_baseline == 1 else 'CST_MS_SCB(*)',
+               'scb_baseline': a.scb_baseline, 'scb_captions': 20, 'bcmr': r['bcmr'],
+               'final_loss': r['loss'], 'skipped_steps': r['skipped']}
     dt, ms, caps, vids = main_run['dt'], main_run['ms'], main_run['caps'], main_run['vids']
     loss, n_params, t_gen = main_run['loss'], main_run['n_params'], main_run['t_gen']
     S = 20
@@ -308,7 +358,7 @@ def main():
             return None
         with open(path) as f:
             return json.load(f).get('value')
-    ref_sem, same_prec = _value(BASELINE_FILE), _value(SAME_PRECISION_FILE)
+    ref_sem = _value(BASELINE_FILE)
     if a.mode == 'beam':
         metric, value, unit = 'beam-%d evaluation decode videos/sec (whole job)' % a.beam_size, \
             vids, 'videos/s'
@@ -324,13 +374,11 @@ def main():
         'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': round(ms, 3),
         'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': None,  # no published number
-        # self-measured, same job on one MI355X: reference semantics (PyTorch
-        # ops, fp32, CPU CIDEr-D; profiles/reference_semantics_baseline.json)
-        # and the same-precision PyTorch path (bf16 autocast, GPU CIDEr-D)
+        # self-measured, same job on one MI355X, NOT a published baseline:
+        # reference semantics (PyTorch ops, fp32, CPU CIDEr-D in Python;
+        # profiles/reference_semantics_baseline.json)
         'vs_reference_semantics_1gpu': (round(caps / ctx.world_size / ref_sem, 2)
                                         if (ref_sem and a.mode == 'scst') else None),
-        'vs_pytorch_bf16_1gpu': (round(caps / ctx.world_size / same_prec, 2)
-                                 if (same_prec and a.mode == 'scst') else None),
         # effective compute dtype: the fused engine is bf16; the PyTorch path is
         # bf16 under autocast with --precision bf16 on a GPU, else fp32
         'dtype': 'bf16' if main_run['bf16'] else 'fp32',
@@ -359,6 +407,11 @@ def main():
         # BASELINE.json's metric names the LSTM-attn decoder: its temporal-
         # attention config (C = 8 frames, MFMA attention) on the same job
         rec['att8'] = att8
+    if cst is not None:
+        # the CST recipe (README CST_MS_SCB), fused consensus-baseline loss
+        rec['cst'] = cst
+    if main_run.get('blaslt'):
+        rec['blaslt_x_choice'] = main_run['blaslt']
     if main_run.get('beam5'):
         # BASELINE config 5: beam-5 evaluation decode (graph-replayed), whole job
         rec['beam5'] = main_run['beam5']

@@ -420,6 +420,16 @@ constexpr int BIG_BIAS_OFF = BigTile::LDS_BYTES;      // 256 fp32 biases, behind
 constexpr int BIG_LDS = BIG_BIAS_OFF + BIG_V * 4;     // 129 KB
 static_assert(BIG_GS_BYTES + 128 * BIG_STAGE_LD * 2 <= BigTile::LDS_BYTES, "epilogue LDS");
 
+// Phase stamps of the big launch (microbenchmark diagnostics only): when set,
+// thread 0 of workgroup b writes the wall clock (100 MHz) at its start, after
+// the main loop, after the statistics / staging, and at its end to
+// g_big_dbg[4 b + phase].  Null in every real run.
+__device__ int64_t* g_big_dbg = nullptr;
+__device__ __forceinline__ void big_phase(int bid, int ph) {
+  if (g_big_dbg != nullptr && threadIdx.x == 0) g_big_dbg[4 * bid + ph] = (int64_t)wall_clock64();
+}
+void set_big_debug(int64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_big_dbg), &p, sizeof(p)); }
+
 __host__ __device__ constexpr int big_lstm_tiles(int R, int H) {
   return ((4 * H) / BIG_R) * ((R + BIG_R - 1) / BIG_R);
 }
@@ -455,6 +465,7 @@ __device__ __forceinline__ void vocab_big_block(int bid, char* lds, VOCAB_TR_PAR
     big_sources(W, V, H, v0, hd, R, ldh, r0, nk, a, bs);
     big_mainloop(nk, a, bs, lds, acc);
   }
+  big_phase(blockIdx.x, 1);
   if (flags & VF_BENCH_MAINLOOP) {  // microbenchmark: main loop only
     if (acc[0][0][0] == 1234.5f) part[0].pad = acc[T::TM - 1][T::TN - 1][15];
     return;
@@ -591,6 +602,7 @@ __device__ __forceinline__ void vocab_big_block(int bid, char* lds, VOCAB_TR_PAR
       }
     }
     gs[g * BIG_R + row_l] = st;
+    if (j == 0) big_phase(blockIdx.x, 2);
     if (save16) {
       __syncthreads();  // this half's rows staged
       // 128 rows x 256 entries: 32 x 16 B per row, 512-byte row segments;
@@ -663,6 +675,23 @@ __device__ __forceinline__ void lstm_big_block(int bid, char* lds, const uint16_
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w / T::WAVES_N,
             wc = w % T::WAVES_N;
+  // video gates: every load issued unconditionally (clamped rows) before any
+  // store, so they are in flight together (a load under a per-element row
+  // test is a dependent round trip each)
+  if (vgate != nullptr) {
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j) {
+      const int n = n0 + wc * T::WN + 32 * j + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int r = min(r0 + wr * T::WM + 32 * i + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3),
+                            R - 1);
+          acc[i][j][k] += vgate[(int64_t)(r / vdiv) * G4 + n];
+        }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < T::TN; ++j) {
     const int n = n0 + wc * T::WN + 32 * j + (lane & 31);
@@ -671,10 +700,7 @@ __device__ __forceinline__ void lstm_big_block(int bid, char* lds, const uint16_
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int r = r0 + wr * T::WM + 32 * i + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3);
-        if (r < R) {
-          const float vg = vgate != nullptr ? vgate[(int64_t)(r / vdiv) * G4 + n] : 0.f;
-          pre[(int64_t)r * G4 + n] = acc[i][j][k] + vg;
-        }
+        if (r < R) pre[(int64_t)r * G4 + n] = acc[i][j][k];
       }
   }
 }
@@ -684,11 +710,13 @@ __global__ __launch_bounds__(512, 1) void vocab_lstm_big_kernel(
     const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int bid = blockIdx.x;
+  big_phase(bid, 0);
   if (bid < n_lstm_pad) {
     if (bid < big_lstm_tiles(R, H)) lstm_big_block(bid, lds, h_t, R, H, whh, vgate, vdiv, pre);
-    return;
+  } else {
+    vocab_big_block(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
   }
-  vocab_big_block(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
+  big_phase(bid, 3);
 }
 
 template <int BN, int STAGES, int OCC, bool TOPK = false>

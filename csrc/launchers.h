@@ -6,6 +6,9 @@
 
 namespace cst {
 
+// vocab.hip: phase stamps of the big-tile decode launch (diagnostics; nullptr = off)
+void set_big_debug(int64_t* p);
+
 // cider_d.hip
 void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
                     const int64_t* ht_keys, const float* ht_vals, uint32_t ht_cap,

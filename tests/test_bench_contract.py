@@ -56,6 +56,12 @@ def test_bench_json_line(world, launcher):
     att = rec['att8']
     assert att['temporal_attention_frames'] == 8 and att['value'] > 0
     assert abs(att['value'] - 4 * 20 * world / (att['ms_per_step'] / 1e3)) < 0.02 * att['value']
+    # the CST recipe (CST_MS_SCB: GT consensus baseline), same invocation
+    cst = rec['cst']
+    assert cst['recipe'] == 'CST_MS_SCB' and cst['scb_baseline'] == 1 and cst['value'] > 0
+    assert cst['bcmr'].startswith('prepro/evalscores.py')
+    assert abs(cst['value'] - 4 * 20 * world / (cst['ms_per_step'] / 1e3)) < 0.02 * cst['value']
+    assert 'vs_pytorch_bf16_1gpu' not in rec
 
 
 def test_bench_world_size_mismatch_fails():
