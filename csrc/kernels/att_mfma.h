@@ -168,15 +168,15 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    // release: this workgroup's slot stores happen-before the ticket; the
-    // last arriver's acquire (below) makes every slot visible to it
-    const int ticket = __hip_atomic_fetch_add(g.cnt + b, 1, __ATOMIC_RELEASE,
+    // sc1 slot stores drained by vmcnt(0) above, sc1 slot loads below: the
+    // no-fence hand-off form (see loss.hip scst_loss_fwd_kernel)
+    const int ticket = __hip_atomic_fetch_add(g.cnt + b, 1, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
     *s_flag = ticket == NS - 1;
   }
   __syncthreads();
   if (!*s_flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only)
   // 3. last workgroup of the video: scores, softmax, vgate.  The gate-table
   // tiles do not depend on alpha: all of this wave's are requested first, so
   // their latency overlaps the slot loads and the softmax.

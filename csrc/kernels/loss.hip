@@ -101,14 +101,20 @@ __global__ __launch_bounds__(256) void scst_loss_fwd_kernel(
     __hip_atomic_store(part + 4 * blockIdx.x + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(part + 4 * blockIdx.x + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // release: the partial stores above happen-before the ticket; the last
-    // arriver acquires (below) before it reads the other workgroups' partials
-    const int ticket = __hip_atomic_fetch_add(ws, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // Hand-off of the partials (gfx950): they are stored write-through (sc1,
+    // agent-scope relaxed atomic stores) and drained by s_waitcnt vmcnt(0)
+    // before the ticket, and the last arriver reads them with sc1 loads only
+    // (agent-scope relaxed atomic loads, which bypass the non-coherent L1).
+    // That is the valid no-fence form of an inter-workgroup hand-off on this
+    // chip (CDNA HIP guide, Guideline 16 / split-K seam): an agent-scope
+    // release here would add an L2 write-back (buffer_wbl2) on the critical
+    // path, an agent-scope acquire an L1 invalidate, neither needed.
+    const int ticket = __hip_atomic_fetch_add(ws, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = ticket == (int)gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order: loads after the ticket)
   // last workgroup: the partials in workgroup order, 4 per thread pass
   float a[4] = {0.f, 0.f, 0.f, 0.f};
   if (threadIdx.x < 64) {

@@ -314,8 +314,8 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const float wv = ew[i][k];
+        for (int k = 0; k < 16; ++k) {  // (the weights of the sum above, recomputed)
+          const float wv = __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], wsc, -wl));
           cum += wv;
           const bool hit = cand < 0 && cum >= tm && wv > 0.f;
           cand = hit ? vb + 32 * i + 8 * (k >> 2) + (k & 3) : cand;
@@ -494,46 +494,56 @@ __device__ __forceinline__ void vocab_big_block(int bid, char* lds, VOCAB_TR_PAR
         acc[i][j][4 * q + 2] += bb.z;
         acc[i][j][4 * q + 3] += bb.w;
       }
-    float m = -INFINITY;
+    // Every reduction over the lane's 64 entries runs as TM = 4 independent
+    // chains of 16 (one per 32-entry vocabulary block i), combined at the end:
+    // 4-way instruction-level parallelism instead of one 64-long dependent chain.
+    float mx[T::TM];
 #pragma unroll
-    for (int i = 0; i < T::TM; ++i)
+    for (int i = 0; i < T::TM; ++i) {
+      mx[i] = acc[i][j][0];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) m = fmaxf(m, acc[i][j][k]);
+      for (int k = 1; k < 16; ++k) mx[i] = fmaxf(mx[i], acc[i][j][k]);
+    }
+    const float m = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
     const float msafe = m == -INFINITY ? 0.f : m;
     const float ml = msafe * L2E;
-    float ew[T::TM][16];
-    float s = 0.f;
+    // exp weights: summed per block and, with the exp store, packed to LDS as
+    // they are formed (not kept: the sampler recomputes its block's weights,
+    // which keeps the epilogue inside 256 VGPRs without spills)
+    const bool exp_store = save16 && (flags & VF_EXP);
+    const float f = exp_store ? __builtin_amdgcn_exp2f((msafe - ec[j]) * L2E) : 0.f;
+    uint16_t* et = stage + srow * BIG_STAGE_LD;
+    float seg[T::TM];  // per-block sums; the row's sum adds them in block order
 #pragma unroll
-    for (int i = 0; i < T::TM; ++i)
+    for (int i = 0; i < T::TM; ++i) {
+      seg[i] = 0.f;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        ew[i][k] = __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], L2E, -ml));
-        s += ew[i][k];
+      for (int q = 0; q < 4; ++q) {
+        float e4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          e4[e] = __builtin_amdgcn_exp2f(fmaf(acc[i][j][4 * q + e], L2E, -ml));
+          seg[i] += e4[e];
+        }
+        if (exp_store) {  // E = exp(x - eoff) = exp(x - m) exp(m - eoff) (vocab_tr_block)
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(e4[0] * f) | ((uint32_t)f2bf(e4[1] * f) << 16);
+          pk.y = (uint32_t)f2bf(e4[2] * f) | ((uint32_t)f2bf(e4[3] * f) << 16);
+          *reinterpret_cast<uint2*>(et + vl0 + 32 * i + 8 * q) = pk;
+        }
       }
-    if (save16) {
-      uint16_t* et = stage + srow * BIG_STAGE_LD;
-      if (flags & VF_EXP) {  // E = exp(x - eoff) = exp(x - m) exp(m - eoff) (vocab_tr_block)
-        const float f = __builtin_amdgcn_exp2f((msafe - ec[j]) * L2E);
+    }
+    const float s = ((seg[0] + seg[1]) + seg[2]) + seg[3];
+    if (save16 && !exp_store) {  // fp16 logits (step 0; entries past V hold -inf)
 #pragma unroll
-        for (int i = 0; i < T::TM; ++i)
+      for (int i = 0; i < T::TM; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(ew[i][4 * q] * f) | ((uint32_t)f2bf(ew[i][4 * q + 1] * f) << 16);
-            pk.y = (uint32_t)f2bf(ew[i][4 * q + 2] * f) | ((uint32_t)f2bf(ew[i][4 * q + 3] * f) << 16);
-            *reinterpret_cast<uint2*>(et + vl0 + 32 * i + 8 * q) = pk;
-          }
-      } else {  // fp16 logits (step 0; entries past V hold -inf)
-#pragma unroll
-        for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            uint2 pk;
-            pk.x = (uint32_t)f2h(acc[i][j][4 * q]) | ((uint32_t)f2h(acc[i][j][4 * q + 1]) << 16);
-            pk.y = (uint32_t)f2h(acc[i][j][4 * q + 2]) | ((uint32_t)f2h(acc[i][j][4 * q + 3]) << 16);
-            *reinterpret_cast<uint2*>(et + vl0 + 32 * i + 8 * q) = pk;
-          }
-      }
+        for (int q = 0; q < 4; ++q) {
+          uint2 pk;
+          pk.x = (uint32_t)f2h(acc[i][j][4 * q]) | ((uint32_t)f2h(acc[i][j][4 * q + 1]) << 16);
+          pk.y = (uint32_t)f2h(acc[i][j][4 * q + 2]) | ((uint32_t)f2h(acc[i][j][4 * q + 3]) << 16);
+          *reinterpret_cast<uint2*>(et + vl0 + 32 * i + 8 * q) = pk;
+        }
     }
     GroupStat st;
     st.m = m;
@@ -541,58 +551,90 @@ __device__ __forceinline__ void vocab_big_block(int bid, char* lds, VOCAB_TR_PAR
     st.pad = 0.f;
     st.xidx = 0x7fffffff;
     if (flags & VF_ARGMAX) {
+      int xi[T::TM];
 #pragma unroll
-      for (int i = 0; i < T::TM; ++i)
+      for (int i = 0; i < T::TM; ++i) {
+        xi[i] = 0x7fffffff;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 15; k >= 0; --k) {  // the first maximal entry of the block
           const int v = v0 + vl0 + 32 * i + 8 * (k >> 2) + (k & 3);
-          st.xidx = min(st.xidx, acc[i][j][k] == m ? v : 0x7fffffff);
+          xi[i] = acc[i][j][k] == m ? v : xi[i];
         }
+      }
+      st.xidx = min(min(xi[0], xi[1]), min(xi[2], xi[3]));
     }
     st.xt = -INFINITY;
     if (tgt != nullptr) {
       const int d = tg[j] - (v0 + vl0);
       const bool mine = d >= 0 && d < 32 * T::TM && (d & 4) == 0;
-      const int kk = mine ? (d >> 5) * 16 + ((d >> 3) & 3) * 4 + (d & 3) : -1;
+      const int kk = mine ? ((d >> 3) & 3) * 4 + (d & 3) : -1;  // entry within block d >> 5
+      float xt[T::TM];
 #pragma unroll
-      for (int i = 0; i < T::TM; ++i)
+      for (int i = 0; i < T::TM; ++i) {
+        xt[i] = -INFINITY;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) st.xt = (i * 16 + k == kk) ? acc[i][j][k] : st.xt;
+        for (int k = 0; k < 16; ++k) xt[i] = k == kk ? acc[i][j][k] : xt[i];
+      }
+      const int bi = d >> 5;
+      st.xt = bi == 0 ? xt[0] : bi == 1 ? xt[1] : bi == 2 ? xt[2] : xt[3];
+      st.xt = mine ? st.xt : -INFINITY;
     }
     st.zkey = -INFINITY;
     st.zlogit = 0.f;
     st.zidx = 0x7fffffff;
     if (flags & VF_SAMPLE) {
       const float wl = msafe * inv_temp * L2E, wsc = inv_temp * L2E;
-      float sw = s;
       if (!temp1) {
-        sw = 0.f;
 #pragma unroll
-        for (int i = 0; i < T::TM; ++i)
+        for (int i = 0; i < T::TM; ++i) {
+          seg[i] = 0.f;
 #pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            ew[i][k] = __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], wsc, -wl));
-            sw += ew[i][k];
-          }
+          for (int k = 0; k < 16; ++k) seg[i] += __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], wsc, -wl));
+        }
       }
+      // block prefixes in the summation order of sw (P[TM] = sw)
+      float P[T::TM + 1];
+      P[0] = 0.f;
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i) P[i + 1] = i == 0 ? seg[0] : P[i] + seg[i];
+      const float sw = P[T::TM];
       const uint32_t rr = (uint32_t)min(r, R - 1);
       const uint32_t seed = rng_seed(rng, RNG_SLOT_SAMPLE);
       const uint32_t key = mix32(seed ^ mix32(rr * 0x9E3779B1u + (uint32_t)step * 0x85EBCA77u) ^
                                  (uint32_t)(vt * 4 + g) * 0xC2B2AE3Du);
       const float u = ((float)(key >> 8) + 0.5f) * (1.0f / 16777216.0f);
       const float tm = u * sw;
-      float cum = 0.f, cl = 0.f;
-      int cand = -1;
+      // inverse CDF: the block a whose prefix range holds tm (the first with
+      // P[a + 1] >= tm), then the scan inside it; the 4 block scans run side by
+      // side and the chosen one is selected.  A block's scan that meets no
+      // entry at its threshold (rounding at the block's end) takes its last
+      // positive weight.
+      int cb[T::TM];
+      float cv[T::TM];
 #pragma unroll
-      for (int i = 0; i < T::TM; ++i)
+      for (int i = 0; i < T::TM; ++i) {
+        const float ti = tm - P[i];
+        float c = 0.f;
+        int ci = -1, lp = -1;
+        float cli = 0.f, lpl = 0.f;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const float wv = ew[i][k];
-          cum += wv;
-          const bool hit = cand < 0 && cum >= tm && wv > 0.f;
-          cand = hit ? v0 + vl0 + 32 * i + 8 * (k >> 2) + (k & 3) : cand;
-          cl = hit ? acc[i][j][k] : cl;
+        for (int k = 0; k < 16; ++k) {  // (the weights of the sum above, recomputed)
+          const float wv = __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], wsc, -wl));
+          const int v = v0 + vl0 + 32 * i + 8 * (k >> 2) + (k & 3);
+          c += wv;
+          const bool pos = wv > 0.f;
+          const bool hit = ci < 0 && c >= ti && pos;
+          ci = hit ? v : ci;
+          cli = hit ? acc[i][j][k] : cli;
+          lp = pos ? v : lp;
+          lpl = pos ? acc[i][j][k] : lpl;
         }
+        cb[i] = ci >= 0 ? ci : lp;
+        cv[i] = ci >= 0 ? cli : lpl;
+      }
+      const int a = P[1] >= tm ? 0 : P[2] >= tm ? 1 : P[3] >= tm ? 2 : 3;
+      const int cand = a == 0 ? cb[0] : a == 1 ? cb[1] : a == 2 ? cb[2] : cb[3];
+      const float cl = a == 0 ? cv[0] : a == 1 ? cv[1] : a == 2 ? cv[2] : cv[3];
       if (sw > 0.f && cand >= 0) {
         const uint32_t key2 = mix32(key ^ 0x68E31DA4u);
         const float u2 = ((float)(key2 >> 8) + 0.5f) * (1.0f / 16777216.0f);
@@ -675,33 +717,46 @@ __device__ __forceinline__ void lstm_big_block(int bid, char* lds, const uint16_
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w / T::WAVES_N,
             wc = w % T::WAVES_N;
-  // video gates: every load issued unconditionally (clamped rows) before any
-  // store, so they are in flight together (a load under a per-element row
-  // test is a dependent round trip each)
-  if (vgate != nullptr) {
+  // the C tile leaves through LDS 64 rows at a time (row stride 260 floats):
+  // rows q * 64 .. q * 64 + 63 are accumulator blocks i = 2 (q % 2), +1 of
+  // the waves with wr = q / 2; then 16-byte row segments (+ the row's video
+  // gates) to pre
+  constexpr int CLD = BIG_R + 4;
+  float* Cs = reinterpret_cast<float*>(lds);
 #pragma unroll
-    for (int j = 0; j < T::TN; ++j) {
-      const int n = n0 + wc * T::WN + 32 * j + (lane & 31);
+  for (int q = 0; q < 4; ++q) {
+    if (wr == q / 2) {
 #pragma unroll
-      for (int i = 0; i < T::TM; ++i)
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * (q % 2) + ii;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int r = min(r0 + wr * T::WM + 32 * i + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3),
-                            R - 1);
-          acc[i][j][k] += vgate[(int64_t)(r / vdiv) * G4 + n];
+        for (int j = 0; j < T::TN; ++j) {
+          const int col = wc * T::WN + 32 * j + (lane & 31);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const int rl = 32 * ii + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3);
+            Cs[rl * CLD + col] = acc[i][j][k];
+          }
         }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < T::TN; ++j) {
-    const int n = n0 + wc * T::WN + 32 * j + (lane & 31);
-#pragma unroll
-    for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int r = r0 + wr * T::WM + 32 * i + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3);
-        if (r < R) pre[(int64_t)r * G4 + n] = acc[i][j][k];
       }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int idx = (int)threadIdx.x + p * T::THREADS;  // 64 rows x 64 float4
+      const int rl = idx >> 6, c4 = idx & 63;
+      const int r = r0 + q * 64 + rl;
+      if (r < R) {
+        float4 x = *reinterpret_cast<const float4*>(Cs + rl * CLD + 4 * c4);
+        if (vgate != nullptr) {
+          const float4 vg =
+              *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * G4 + n0 + 4 * c4);
+          x.x += vg.x, x.y += vg.y, x.z += vg.z, x.w += vg.w;
+        }
+        *reinterpret_cast<float4*>(pre + (int64_t)r * G4 + n0 + 4 * c4) = x;
+      }
+    }
+    __syncthreads();
   }
 }
 
