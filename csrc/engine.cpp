@@ -1438,6 +1438,45 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
     vg_rows = at::empty({R, H4}, f32);
     qb = at::empty({R, A}, f32);
   }
+  // Fused form (one layer, no attention, K <= 8): per decode step TWO launches
+  // -- the vocab launch (tile top-K candidates + partials) carrying the NEXT
+  // step's recurrent GEMM pre = h W_hh^T + video gates for every current row,
+  // then beam_fused_step_kernel (LSE, candidate top-K, selection / fork /
+  // harvest, and the cell of the new beams from their parents' pre and c) --
+  // instead of five (vocab, combine, top-K merge, beam step, LSTM step).
+  if (tile_topk && !has_att && NL == 1) {
+    at::Tensor pre = at::empty({R, H4}, f32);
+    const float* VG = vgate.data_ptr<float>();
+    // step 0: every row's cell from the initial state and BOS
+    launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, ptab.data_ptr<float>(),
+                         reinterpret_cast<const uint16_t*>(h[0].data_ptr()), c[0].data_ptr<float>(),
+                         VG, (int)K, (int)R, (int)H, WHH,
+                         reinterpret_cast<uint16_t*>(h[1].data_ptr()), c[1].data_ptr<float>(),
+                         nullptr, (int)H, 0.f, nullptr, 0, nullptr, st, nullptr, (int)cell);
+    for (int64_t t = 1; t < T - 1; ++t) {
+      // vocab projection of h_t (rows = beams of step t) + pre_{t+1} of every row
+      const at::Tensor& ht = h[t & 1];
+      const bool next = t < T - 2;
+      (void)launch_vocab_lstm_fwd(reinterpret_cast<const uint16_t*>(ht.data_ptr()), (int)H, (int)R,
+                                  (int)H, W, blog.data_ptr<float>(), (int)V,
+                                  reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl,
+                                  part.data_ptr(), nullptr, 0, VF_TOPK_H | ((int)K << 8), 1.f,
+                                  nullptr, (int)t, reinterpret_cast<const uint16_t*>(ht.data_ptr()),
+                                  WHH, VG, (int)K, next ? pre.data_ptr<float>() : nullptr, st, 0,
+                                  nullptr, nullptr, nullptr);
+      BeamFusedArgs ba{reinterpret_cast<const VocabPartial*>(part.data_ptr()),
+                       reinterpret_cast<const float2*>(logits.data_ptr()), n_vt, (int)R, (int)K,
+                       (int)B, (int)T, beam_sum.data_ptr<float>(), seq_hist.data_ptr<int64_t>(),
+                       lp_hist.data_ptr<float>(), best_ppl.data_ptr<float>(),
+                       best_seq.data_ptr<int64_t>(), best_lp.data_ptr<float>(),
+                       tok.data_ptr<int64_t>(), next ? pre.data_ptr<float>() : nullptr,
+                       ptab.data_ptr<float>(), c[t & 1].data_ptr<float>(),
+                       c[(t + 1) & 1].data_ptr<float>(),
+                       reinterpret_cast<uint16_t*>(h[(t + 1) & 1].data_ptr()), (int)H, (int)cell};
+      launch_beam_fused_step(ba, (int)t, st);
+    }
+    return {best_seq, best_lp};
+  }
   for (int64_t t = 0; t < T - 1; ++t) {
     if (t >= 1) {
       if (tile_topk)

@@ -21,6 +21,8 @@
 //   * the LSTM state is not copied: the next step's LSTM kernel reads h/c of
 //     row `parent[r]` (row_map).
 #include "../common.h"
+#include "../launchers.h"
+#include "vocab_common.h"
 
 namespace cst {
 
@@ -283,6 +285,182 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
       best_seq[(int64_t)b * T + pos] = sh_new[(int64_t)(b * K + win) * T + pos];
       best_lp[(int64_t)b * T + pos] = lh_new[(int64_t)(b * K + win) * T + pos];
     }
+}
+
+// Fused beam step (one 256-thread workgroup per video, beam size K <= 8),
+// replacing combine + candidate top-K + beam step + LSTM step (4 launches):
+//   A. each of the video's K rows (one wavefront per row): the LSE from the
+//      vocab launch's tile partials and the row's K best log-probs from its
+//      n_vt x K tile candidates (VF_TOPK), into LDS;
+//   B. the reference's selection / fork / harvest (beam_step_kernel's rules);
+//   C. the next step's LSTM cell for the K new beams: gates = pre[parent] +
+//      P[token] (pre = h_t W_hh^T + video gates of ALL current rows, computed
+//      by the recurrent tiles of the vocab launch, so a new beam reads its
+//      parent's row), c from the parent's c -> h (bf16), c.
+// Per decode step: this launch + the vocab launch (which also carries the
+// next step's recurrent GEMM).
+__global__ __launch_bounds__(256) void beam_fused_step_kernel(BeamFusedArgs a, int t) {
+  __shared__ float s_tv[BEAM_MAXK * BEAM_MAXK];
+  __shared__ int s_ti[BEAM_MAXK * BEAM_MAXK];
+  __shared__ float s_p[BEAM_MAXK * BEAM_MAXK];
+  __shared__ int s_sel[BEAM_MAXK];
+  __shared__ float s_sum_old[BEAM_MAXK];
+  __shared__ int s_win;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int K = a.K, R = a.R, T = a.T, n_vt = a.n_vt;
+  // -- A. per-row LSE and top-K ---------------------------------------------------
+  for (int q = w; q < K; q += 4) {
+    const int r = b * K + q;
+    float m = -INFINITY, sm = 0.f;
+    for (int vt = lane; vt < n_vt; vt += 64) {
+      const VocabPartial p = a.part[(int64_t)vt * R + r];
+      const float M = fmaxf(m, p.m);
+      sm = (m == -INFINITY ? 0.f : sm * __expf(m - M)) + (p.m == -INFINITY ? 0.f : p.s * __expf(p.m - M));
+      m = M;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(sm, o, 64);
+      const float M = fmaxf(m, m2);
+      sm = (m == -INFINITY ? 0.f : sm * __expf(m - M)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - M));
+      m = M;
+    }
+    const float L = m + __logf(sm);
+    constexpr int MK = 8;
+    float bv[MK];
+    int bi[MK];
+#pragma unroll
+    for (int k = 0; k < MK; ++k) bv[k] = -INFINITY, bi[k] = 0x7fffffff;
+    const int n = n_vt * K;
+    float thr = -INFINITY;
+    for (int c0 = lane; c0 < n; c0 += 64 * 4) {
+      float2 xs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + 64 * u;
+        xs[u] = c < n ? a.cand[((int64_t)(c / K) * R + r) * K + c % K]
+                      : make_float2(-INFINITY, __int_as_float(0x7fffffff));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float cv = xs[u].x;
+        int ci = __float_as_int(xs[u].y);
+        if (!(cv > thr || (cv == thr && ci < 0x7fffffff))) continue;
+#pragma unroll
+        for (int p = 0; p < MK; ++p) {
+          if (p < K && (cv > bv[p] || (cv == bv[p] && ci < bi[p]))) {
+            const float tv = bv[p];
+            const int tix = bi[p];
+            bv[p] = cv, bi[p] = ci;
+            cv = tv, ci = tix;
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < MK; ++p) thr = p == K - 1 ? bv[p] : thr;
+      }
+    }
+    for (int k = 0; k < K; ++k) {
+      float best = bv[0];
+      int besti = bi[0];
+      wave_argmax(best, besti);
+      if (bi[0] == besti) {
+#pragma unroll
+        for (int p = 0; p + 1 < MK; ++p) bv[p] = bv[p + 1], bi[p] = bi[p + 1];
+        bv[MK - 1] = -INFINITY, bi[MK - 1] = 0x7fffffff;
+      }
+      if (lane == 0) s_tv[q * K + k] = best - L, s_ti[q * K + k] = besti;
+    }
+  }
+  if (tid < K) s_sum_old[tid] = a.beam_sum[b * K + tid];
+  __syncthreads();
+  // -- B. selection (beam_step_kernel's rules), every thread at the barriers ------
+  const int rows = t == 1 ? 1 : K;
+  const int ncand = rows * K;
+  if (tid < ncand) {
+    const int c = tid / rows, q = tid % rows;
+    s_p[tid] = s_sum_old[q] + s_tv[q * K + c];
+  }
+  __syncthreads();
+  for (int v = 0; v < K; ++v) {
+    if (w == 0) {
+      float best = -INFINITY;
+      int bj = 0x7fffffff;
+      for (int j = lane; j < ncand; j += 64) {
+        bool taken = false;
+        for (int u = 0; u < v; ++u) taken |= (s_sel[u] == j);
+        const float p = s_p[j];
+        if (!taken && (p > best || (p == best && j < bj))) best = p, bj = j;
+      }
+      wave_argmax(best, bj);
+      if (lane == 0) s_sel[v] = bj;
+    }
+    __syncthreads();
+  }
+  const int64_t* sh_old = a.seq_hist + (int64_t)((t + 1) & 1) * R * T;
+  const float* lh_old = a.lp_hist + (int64_t)((t + 1) & 1) * R * T;
+  int64_t* sh_new = a.seq_hist + (int64_t)(t & 1) * R * T;
+  float* lh_new = a.lp_hist + (int64_t)(t & 1) * R * T;
+  for (int e = tid; e < K * T; e += 256) {
+    const int v = e / T, pos = e % T;
+    const int j = s_sel[v], c = j / rows, q = j % rows;
+    const int64_t src = (int64_t)(b * K + q) * T + pos, dst = (int64_t)(b * K + v) * T + pos;
+    if (pos < t - 1) {
+      sh_new[dst] = sh_old[src];
+      lh_new[dst] = lh_old[src];
+    } else if (pos == t - 1) {
+      sh_new[dst] = s_ti[q * K + c];
+      lh_new[dst] = s_tv[q * K + c];
+    } else {
+      sh_new[dst] = 0;
+      lh_new[dst] = 0.f;
+    }
+  }
+  if (tid < K) {
+    const int v = tid, j = s_sel[v], c = j / rows, q = j % rows;
+    a.beam_sum[b * K + v] = s_p[j];
+    a.tok_out[b * K + v] = s_ti[q * K + c];
+  }
+  if (tid == 0) {  // harvest, in beam order (earliest wins ties)
+    int win = -1;
+    float bp = a.best_ppl[b];
+    for (int v = 0; v < K; ++v) {
+      const int j = s_sel[v], c = j / rows, q = j % rows;
+      if (s_ti[q * K + c] == 0 || t == T - 2) {
+        const float ppl = t > 1 ? __expf(-s_p[j] / (float)(t - 1)) : 10000.f;
+        if (ppl < bp) bp = ppl, win = v;
+      }
+    }
+    if (win >= 0) a.best_ppl[b] = bp;
+    s_win = win;
+  }
+  __syncthreads();  // (the history stores above precede the harvest copy)
+  const int win = s_win;
+  if (win >= 0)
+    for (int pos = tid; pos < T; pos += 256) {
+      a.best_seq[(int64_t)b * T + pos] = sh_new[(int64_t)(b * K + win) * T + pos];
+      a.best_lp[(int64_t)b * T + pos] = lh_new[(int64_t)(b * K + win) * T + pos];
+    }
+  if (a.pre == nullptr) return;
+  // -- C. the next step's cell for the K new beams ---------------------------------
+  const int H = a.H;
+  for (int e = tid; e < K * H; e += 256) {
+    const int v = e / H, u = e % H;
+    const int j = s_sel[v], c = j / rows, q = j % rows;
+    const int pr = b * K + q, tk = s_ti[q * K + c];
+    const float4 pv = *reinterpret_cast<const float4*>(a.pre + (int64_t)pr * 4 * H + 4 * u);
+    const float4 xv = *reinterpret_cast<const float4*>(a.ptab + (int64_t)tk * 4 * H + 4 * u);
+    const CellFwd cf = cell_fwd(a.cell, pv.x + xv.x, pv.y + xv.y, pv.z + xv.z, pv.w + xv.w,
+                                a.c_in[(int64_t)pr * H + u]);
+    const int64_t o = (int64_t)(b * K + v) * H + u;
+    a.c_out[o] = cf.c;
+    a.h_out[o] = f2bf(cf.h);
+  }
+}
+
+void launch_beam_fused_step(const BeamFusedArgs& a, int t, hipStream_t stream) {
+  if (a.K < 1 || a.K > 8) throw std::runtime_error("beam_fused_step: K must be in [1, 8]");
+  hipLaunchKernelGGL(beam_fused_step_kernel, dim3(a.B), dim3(256), 0, stream, a, t);
+  post_launch("beam_fused_step_kernel", stream);
 }
 
 void launch_beam_topk(const float* logits, int64_t ldl, int V, int R, int K, const float* lse,

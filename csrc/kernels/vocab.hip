@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
 // the MFMA temporal attention of step t+1, one per video (att_mfma.h): they
 // depend only on h_t too, and are dispatched first, so they finish under the
 // vocabulary tiles.
-template <int BN, int STAGES, int OCC, class LT, int AV>
+template <int BN, int STAGES, int OCC, class LT, int AV, bool TOPK = false>
 __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
     VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
     const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad, int NQ,
@@ -1149,7 +1149,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
       lstm_gemm_block<LT>(bid, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
     return;
   }
-  vocab_tr_block<BN, STAGES>(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
+  vocab_tr_block<BN, STAGES, TOPK>(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
 }
 
 // Exp-store conversion of one decode step's saved fp16 logits, in place:
@@ -1308,7 +1308,7 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   post_launch("vocab_combine_kernel", stream);
 }
 
-template <int BN, int STAGES, int OCC, class LT, int AV>
+template <int BN, int STAGES, int OCC, class LT, int AV, bool TOPK = false>
 static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
@@ -1333,11 +1333,11 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   const int grid = n_att + n_l + n_vt * n_rt;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV>,
+    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, TOPK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV>), dim3(grid), dim3(256),
+  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, TOPK>), dim3(grid), dim3(256),
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
                      tgt, tgt_stride, flags, inv_temp, rng, step, eoff, h_t, whh, vgate, vdiv, pre,
                      n_l, NQ, q_out, a, n_att);
@@ -1357,6 +1357,15 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
   // 2 stages to fit): one block's epilogue overlaps the others' main loops.
   // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
   // CU (3 interleaved rounds; profiles/r2/ab_vocab_tiles.txt)
+  if ((flags & VF_TOPK) && att == nullptr) {  // beam search: per-tile top-K candidates
+    if (vf_topk_k(flags) < 1 || vf_topk_k(flags) > VF_TOPK_MAXK)
+      throw std::runtime_error("vocab_lstm_fwd: VF_TOPK needs 1 <= K <= 8");
+    launch_vocab_lstm_t<64, 2, 3, LGTile2, 0, true>(hd, ldh, R, H, W, bias, V, logits16, ldl, part,
+                                                    tgt, tgt_stride, flags, inv_temp, rng, step,
+                                                    h_t, whh, vgate, vdiv, pre, NQ, q_out, stream,
+                                                    eoff, nullptr);
+    return vocab_num_tiles(V);
+  }
   if (vocab_big_ok(R, H, flags, NQ, att != nullptr))
     return launch_vocab_lstm_big(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
                                  flags, inv_temp, rng, step, h_t, whh, vgate, vdiv, pre, stream,

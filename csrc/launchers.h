@@ -9,6 +9,27 @@ namespace cst {
 // vocab.hip: phase stamps of the big-tile decode launch (diagnostics; nullptr = off)
 void set_big_debug(int64_t* p);
 
+// beam.hip: fused beam step (LSE + candidate top-K + selection + next cell)
+struct BeamFusedArgs {
+  const struct VocabPartial* part;  // (n_vt, R) tile partials of the vocab launch
+  const float2* cand;               // (n_vt, R, K) tile candidates (VF_TOPK)
+  int n_vt, R, K, B, T;
+  float* beam_sum;
+  int64_t* seq_hist;  // (2, R, T)
+  float* lp_hist;
+  float* best_ppl;
+  int64_t* best_seq;
+  float* best_lp;
+  int64_t* tok_out;
+  const float* pre;   // (R, 4H) h_t W_hh^T + video gates; nullptr = no cell (last step)
+  const float* ptab;  // (V, 4H)
+  const float* c_in;  // (R, H)
+  float* c_out;
+  uint16_t* h_out;    // (R, H) bf16
+  int H, cell;
+};
+void launch_beam_fused_step(const BeamFusedArgs& a, int t, hipStream_t stream);
+
 // cider_d.hip
 void launch_cider_d(const int64_t* hyps, int T, const int64_t* hyp_video, int N,
                     const int64_t* ht_keys, const float* ht_vals, uint32_t ht_cap,
