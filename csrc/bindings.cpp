@@ -72,7 +72,6 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
 std::vector<at::Tensor> vocab_select(at::Tensor hd, at::Tensor wlog, at::Tensor blog,
                                      at::Tensor rng, int64_t mode, double temperature,
                                      int64_t step);
-void big_debug_buffer(at::Tensor buf);
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
                        int64_t flags, bool save, int64_t iters, int64_t variant);
 at::Tensor cider_score(at::Tensor hyps, at::Tensor hyp_video, std::map<std::string, at::Tensor> t,
@@ -148,7 +147,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cider_score_cpu", &cst::cider_score_cpu);
   m.def("flat_adam_step", &cst::flat_adam_step);
   m.def("refresh_shadows", &cst::refresh_shadows);
-  m.def("big_debug_buffer", &cst::big_debug_buffer);
   m.def("vocab_fwd_bench", &cst::vocab_fwd_bench);
   m.def("vgrad_colsum_bench", &cst::vgrad_colsum_bench);
   m.def("token_sort_bench", &cst::token_sort_bench);

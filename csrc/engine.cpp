@@ -1554,19 +1554,6 @@ static double time_launches(F&& launch, int64_t iters, hipStream_t st) {
   return 1000.0 * ms / (double)iters;
 }
 
-// per-workgroup phase stamps of the big-tile decode launch (4 int64 per
-// workgroup: start, main loop done, first half's statistics done, end);
-// an empty tensor switches them off
-void big_debug_buffer(at::Tensor buf) {
-  if (!buf.defined() || buf.numel() == 0) {
-    set_big_debug(nullptr);
-    return;
-  }
-  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kLong && buf.is_contiguous(),
-              "debug buffer: contiguous int64 GPU tensor");
-  set_big_debug(buf.data_ptr<int64_t>());
-}
-
 double vocab_fwd_bench(at::Tensor hd, at::Tensor wlog, at::Tensor blog, at::Tensor tgt,
                        int64_t flags, bool save, int64_t iters, int64_t variant) {
   const int64_t R = hd.size(0), H = hd.size(1), V = wlog.size(0);

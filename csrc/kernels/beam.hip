@@ -442,18 +442,35 @@ __global__ __launch_bounds__(256) void beam_fused_step_kernel(BeamFusedArgs a, i
     }
   if (a.pre == nullptr) return;
   // -- C. the next step's cell for the K new beams ---------------------------------
-  const int H = a.H;
-  for (int e = tid; e < K * H; e += 256) {
-    const int v = e / H, u = e % H;
-    const int j = s_sel[v], c = j / rows, q = j % rows;
-    const int pr = b * K + q, tk = s_ti[q * K + c];
-    const float4 pv = *reinterpret_cast<const float4*>(a.pre + (int64_t)pr * 4 * H + 4 * u);
-    const float4 xv = *reinterpret_cast<const float4*>(a.ptab + (int64_t)tk * 4 * H + 4 * u);
-    const CellFwd cf = cell_fwd(a.cell, pv.x + xv.x, pv.y + xv.y, pv.z + xv.z, pv.w + xv.w,
-                                a.c_in[(int64_t)pr * H + u]);
-    const int64_t o = (int64_t)(b * K + v) * H + u;
-    a.c_out[o] = cf.c;
-    a.h_out[o] = f2bf(cf.h);
+  // batches of CB elements per thread: every load of a batch is issued before
+  // the first store (the stores could alias the inputs as far as the compiler
+  // knows, which would serialise the loads: one round trip per element)
+  const int H = a.H, n = K * H;
+  constexpr int CB = 8;
+  for (int e0 = tid; e0 < n; e0 += 256 * CB) {
+    float4 pv[CB], xv[CB];
+    float cv[CB];
+    int64_t ob[CB];
+#pragma unroll
+    for (int k = 0; k < CB; ++k) {
+      const int e = min(e0 + 256 * k, n - 1);  // (clamped: no branch around the loads)
+      const int v = e / H, u = e % H;
+      const int j = s_sel[v], c = j / rows, q = j % rows;
+      const int pr = b * K + q, tk = s_ti[q * K + c];
+      pv[k] = *reinterpret_cast<const float4*>(a.pre + (int64_t)pr * 4 * H + 4 * u);
+      xv[k] = *reinterpret_cast<const float4*>(a.ptab + (int64_t)tk * 4 * H + 4 * u);
+      cv[k] = a.c_in[(int64_t)pr * H + u];
+      ob[k] = (int64_t)(b * K + v) * H + u;
+    }
+#pragma unroll
+    for (int k = 0; k < CB; ++k) {
+      if (e0 + 256 * k < n) {
+        const CellFwd cf = cell_fwd(a.cell, pv[k].x + xv[k].x, pv[k].y + xv[k].y,
+                                    pv[k].z + xv[k].z, pv[k].w + xv[k].w, cv[k]);
+        a.c_out[ob[k]] = cf.c;
+        a.h_out[ob[k]] = f2bf(cf.h);
+      }
+    }
   }
 }
 

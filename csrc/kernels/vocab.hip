@@ -33,7 +33,6 @@
 //   * step 0 of the exp store (see VF_EXP): fp16 logits -> bf16
 //     exp(x - lse) in place; the backward (vocab_grad.hip) never forms dS.
 #include "gemm_tile.h"
-#include "gemm_big.h"
 #include "lstm_gemm.h"
 #include "att_mfma.h"
 #include "vocab_common.h"
@@ -399,379 +398,6 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
             *reinterpret_cast<const uint4*>(et + row * EXP_STAGE_LD + 8 * ch);
     }
   }
-}
-
-// -------------------------------------------------------------------------------
-// Big-tile decode launch (gemm_big.h): 256 vocab x 256 caption-row tiles, one
-// 512-thread workgroup per CU, the whole decode step (vocabulary tiles + the
-// next step's recurrent tiles) in ONE round of workgroups.  Same transposed
-// register epilogue as vocab_tr_block: wave (wr, wc) holds vocab entries
-// wr * 128 + 32 i + 8 q + 4 half + e (i < 4, q < 4, e < 4) of caption rows
-// wc * 64 + 32 j + (lane & 31) (j < 2), so every per-row statistic is a
-// register loop over the lane's 64 entries; the 4 lane groups of a row
-// (2 halves x 2 vocabulary waves) merge through LDS.  The exp store / fp16
-// logits are staged per row half (128 rows x 256 entries) and written as
-// 512-byte row segments.  Training / sampling / greedy flags only (beam
-// search's VF_TOPK / VF_SAVE_F32 stay on the 128 x 64 tiles).
-constexpr int BIG_V = 256, BIG_R = 256;
-constexpr int BIG_STAGE_LD = BIG_V + 8;               // bf16 entries per staged row
-constexpr int BIG_GS_BYTES = 4 * BIG_R * 32;          // GroupStat [4][256]
-constexpr int BIG_BIAS_OFF = BigTile::LDS_BYTES;      // 256 fp32 biases, behind the stages
-constexpr int BIG_LDS = BIG_BIAS_OFF + BIG_V * 4;     // 129 KB
-static_assert(BIG_GS_BYTES + 128 * BIG_STAGE_LD * 2 <= BigTile::LDS_BYTES, "epilogue LDS");
-
-// Phase stamps of the big launch (microbenchmark diagnostics only): when set,
-// thread 0 of workgroup b writes the wall clock (100 MHz) at its start, after
-// the main loop, after the statistics / staging, and at its end to
-// g_big_dbg[4 b + phase].  Null in every real run.
-__device__ int64_t* g_big_dbg = nullptr;
-__device__ __forceinline__ void big_phase(int bid, int ph) {
-  if (g_big_dbg != nullptr && threadIdx.x == 0) g_big_dbg[4 * bid + ph] = (int64_t)wall_clock64();
-}
-void set_big_debug(int64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_big_dbg), &p, sizeof(p)); }
-
-__host__ __device__ constexpr int big_lstm_tiles(int R, int H) {
-  return ((4 * H) / BIG_R) * ((R + BIG_R - 1) / BIG_R);
-}
-
-__device__ __forceinline__ void vocab_big_block(int bid, char* lds, VOCAB_TR_PARAMS) {
-  using T = BigTile;
-  const int n_vt = (V + BIG_V - 1) / BIG_V, n_rt = (R + BIG_R - 1) / BIG_R;
-  const int b = xcd_remap(bid, n_vt * n_rt);
-  const int vt = b / n_rt, rt = b % n_rt;
-  const int v0 = vt * BIG_V, r0 = rt * BIG_R;
-  const int nk = H / 64;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w / T::WAVES_N,
-            wc = w % T::WAVES_N;
-  const int half = lane >> 5;
-  const int vl0 = wr * T::WM + 4 * half;  // the lane's first tile-local vocab entry
-  float* sbias = reinterpret_cast<float*>(lds + BIG_BIAS_OFF);
-  // the tile's bias (columns past V: -inf, they vanish from every statistic),
-  // loaded now, stored to LDS after the main loop (its latency hides there)
-  const float bload =
-      threadIdx.x < BIG_V && v0 + (int)threadIdx.x < V ? bias[v0 + threadIdx.x] : -INFINITY;
-  int tg[T::TN];
-  float ec[T::TN];
-#pragma unroll
-  for (int j = 0; j < T::TN; ++j) {
-    const int r = min(r0 + wc * T::WN + 32 * j + (lane & 31), R - 1);
-    tg[j] = tgt != nullptr ? (int)tgt[(int64_t)r * tgt_stride] : -1;
-    ec[j] = eoff != nullptr ? eoff[r] : 0.f;
-  }
-  f32x16 acc[T::TM][T::TN];
-  {
-    DmaSrc<T::NA> a;
-    DmaSrc<T::NB> bs;
-    big_sources(W, V, H, v0, hd, R, ldh, r0, nk, a, bs);
-    big_mainloop(nk, a, bs, lds, acc);
-  }
-  big_phase(blockIdx.x, 1);
-  if (flags & VF_BENCH_MAINLOOP) {  // microbenchmark: main loop only
-    if (acc[0][0][0] == 1234.5f) part[0].pad = acc[T::TM - 1][T::TN - 1][15];
-    return;
-  }
-  if (threadIdx.x < BIG_V) sbias[threadIdx.x] = bload;
-  __syncthreads();
-  GroupStat* gs = reinterpret_cast<GroupStat*>(lds);  // [4 groups][256 rows]
-  uint16_t* stage = reinterpret_cast<uint16_t*>(lds + BIG_GS_BYTES);  // [128 rows][BIG_STAGE_LD]
-  const bool save16 = logits16 != nullptr;
-  const int g = wr * 2 + half;
-  const bool temp1 = inv_temp == 1.f;
-  constexpr float L2E = 1.4426950408889634f;
-#pragma unroll
-  for (int j = 0; j < T::TN; ++j) {
-    const int row_l = wc * T::WN + 32 * j + (lane & 31);  // tile-local row
-    const int srow = wc * 32 + (lane & 31);                // staged row of this half
-    const int r = r0 + row_l;
-    // x = logits (in place in the accumulators of j)
-#pragma unroll
-    for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 bb = *reinterpret_cast<const float4*>(sbias + vl0 + 32 * i + 8 * q);
-        acc[i][j][4 * q] += bb.x;
-        acc[i][j][4 * q + 1] += bb.y;
-        acc[i][j][4 * q + 2] += bb.z;
-        acc[i][j][4 * q + 3] += bb.w;
-      }
-    // Every reduction over the lane's 64 entries runs as TM = 4 independent
-    // chains of 16 (one per 32-entry vocabulary block i), combined at the end:
-    // 4-way instruction-level parallelism instead of one 64-long dependent chain.
-    float mx[T::TM];
-#pragma unroll
-    for (int i = 0; i < T::TM; ++i) {
-      mx[i] = acc[i][j][0];
-#pragma unroll
-      for (int k = 1; k < 16; ++k) mx[i] = fmaxf(mx[i], acc[i][j][k]);
-    }
-    const float m = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
-    const float msafe = m == -INFINITY ? 0.f : m;
-    const float ml = msafe * L2E;
-    // exp weights: summed per block and, with the exp store, packed to LDS as
-    // they are formed (not kept: the sampler recomputes its block's weights,
-    // which keeps the epilogue inside 256 VGPRs without spills)
-    const bool exp_store = save16 && (flags & VF_EXP);
-    const float f = exp_store ? __builtin_amdgcn_exp2f((msafe - ec[j]) * L2E) : 0.f;
-    uint16_t* et = stage + srow * BIG_STAGE_LD;
-    float seg[T::TM];  // per-block sums; the row's sum adds them in block order
-#pragma unroll
-    for (int i = 0; i < T::TM; ++i) {
-      seg[i] = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float e4[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          e4[e] = __builtin_amdgcn_exp2f(fmaf(acc[i][j][4 * q + e], L2E, -ml));
-          seg[i] += e4[e];
-        }
-        if (exp_store) {  // E = exp(x - eoff) = exp(x - m) exp(m - eoff) (vocab_tr_block)
-          uint2 pk;
-          pk.x = (uint32_t)f2bf(e4[0] * f) | ((uint32_t)f2bf(e4[1] * f) << 16);
-          pk.y = (uint32_t)f2bf(e4[2] * f) | ((uint32_t)f2bf(e4[3] * f) << 16);
-          *reinterpret_cast<uint2*>(et + vl0 + 32 * i + 8 * q) = pk;
-        }
-      }
-    }
-    const float s = ((seg[0] + seg[1]) + seg[2]) + seg[3];
-    if (save16 && !exp_store) {  // fp16 logits (step 0; entries past V hold -inf)
-#pragma unroll
-      for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint2 pk;
-          pk.x = (uint32_t)f2h(acc[i][j][4 * q]) | ((uint32_t)f2h(acc[i][j][4 * q + 1]) << 16);
-          pk.y = (uint32_t)f2h(acc[i][j][4 * q + 2]) | ((uint32_t)f2h(acc[i][j][4 * q + 3]) << 16);
-          *reinterpret_cast<uint2*>(et + vl0 + 32 * i + 8 * q) = pk;
-        }
-    }
-    GroupStat st;
-    st.m = m;
-    st.s = s;
-    st.pad = 0.f;
-    st.xidx = 0x7fffffff;
-    if (flags & VF_ARGMAX) {
-      int xi[T::TM];
-#pragma unroll
-      for (int i = 0; i < T::TM; ++i) {
-        xi[i] = 0x7fffffff;
-#pragma unroll
-        for (int k = 15; k >= 0; --k) {  // the first maximal entry of the block
-          const int v = v0 + vl0 + 32 * i + 8 * (k >> 2) + (k & 3);
-          xi[i] = acc[i][j][k] == m ? v : xi[i];
-        }
-      }
-      st.xidx = min(min(xi[0], xi[1]), min(xi[2], xi[3]));
-    }
-    st.xt = -INFINITY;
-    if (tgt != nullptr) {
-      const int d = tg[j] - (v0 + vl0);
-      const bool mine = d >= 0 && d < 32 * T::TM && (d & 4) == 0;
-      const int kk = mine ? ((d >> 3) & 3) * 4 + (d & 3) : -1;  // entry within block d >> 5
-      float xt[T::TM];
-#pragma unroll
-      for (int i = 0; i < T::TM; ++i) {
-        xt[i] = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) xt[i] = k == kk ? acc[i][j][k] : xt[i];
-      }
-      const int bi = d >> 5;
-      st.xt = bi == 0 ? xt[0] : bi == 1 ? xt[1] : bi == 2 ? xt[2] : xt[3];
-      st.xt = mine ? st.xt : -INFINITY;
-    }
-    st.zkey = -INFINITY;
-    st.zlogit = 0.f;
-    st.zidx = 0x7fffffff;
-    if (flags & VF_SAMPLE) {
-      const float wl = msafe * inv_temp * L2E, wsc = inv_temp * L2E;
-      if (!temp1) {
-#pragma unroll
-        for (int i = 0; i < T::TM; ++i) {
-          seg[i] = 0.f;
-#pragma unroll
-          for (int k = 0; k < 16; ++k) seg[i] += __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], wsc, -wl));
-        }
-      }
-      // block prefixes in the summation order of sw (P[TM] = sw)
-      float P[T::TM + 1];
-      P[0] = 0.f;
-#pragma unroll
-      for (int i = 0; i < T::TM; ++i) P[i + 1] = i == 0 ? seg[0] : P[i] + seg[i];
-      const float sw = P[T::TM];
-      const uint32_t rr = (uint32_t)min(r, R - 1);
-      const uint32_t seed = rng_seed(rng, RNG_SLOT_SAMPLE);
-      const uint32_t key = mix32(seed ^ mix32(rr * 0x9E3779B1u + (uint32_t)step * 0x85EBCA77u) ^
-                                 (uint32_t)(vt * 4 + g) * 0xC2B2AE3Du);
-      const float u = ((float)(key >> 8) + 0.5f) * (1.0f / 16777216.0f);
-      const float tm = u * sw;
-      // inverse CDF: the block a whose prefix range holds tm (the first with
-      // P[a + 1] >= tm), then the scan inside it; the 4 block scans run side by
-      // side and the chosen one is selected.  A block's scan that meets no
-      // entry at its threshold (rounding at the block's end) takes its last
-      // positive weight.
-      int cb[T::TM];
-      float cv[T::TM];
-#pragma unroll
-      for (int i = 0; i < T::TM; ++i) {
-        const float ti = tm - P[i];
-        float c = 0.f;
-        int ci = -1, lp = -1;
-        float cli = 0.f, lpl = 0.f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {  // (the weights of the sum above, recomputed)
-          const float wv = __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], wsc, -wl));
-          const int v = v0 + vl0 + 32 * i + 8 * (k >> 2) + (k & 3);
-          c += wv;
-          const bool pos = wv > 0.f;
-          const bool hit = ci < 0 && c >= ti && pos;
-          ci = hit ? v : ci;
-          cli = hit ? acc[i][j][k] : cli;
-          lp = pos ? v : lp;
-          lpl = pos ? acc[i][j][k] : lpl;
-        }
-        cb[i] = ci >= 0 ? ci : lp;
-        cv[i] = ci >= 0 ? cli : lpl;
-      }
-      const int a = P[1] >= tm ? 0 : P[2] >= tm ? 1 : P[3] >= tm ? 2 : 3;
-      const int cand = a == 0 ? cb[0] : a == 1 ? cb[1] : a == 2 ? cb[2] : cb[3];
-      const float cl = a == 0 ? cv[0] : a == 1 ? cv[1] : a == 2 ? cv[2] : cv[3];
-      if (sw > 0.f && cand >= 0) {
-        const uint32_t key2 = mix32(key ^ 0x68E31DA4u);
-        const float u2 = ((float)(key2 >> 8) + 0.5f) * (1.0f / 16777216.0f);
-        st.zkey = msafe * inv_temp + __logf(sw) - __logf(-__logf(u2));
-        st.zidx = cand;
-        st.zlogit = cl;
-      }
-    }
-    gs[g * BIG_R + row_l] = st;
-    if (j == 0) big_phase(blockIdx.x, 2);
-    if (save16) {
-      __syncthreads();  // this half's rows staged
-      // 128 rows x 256 entries: 32 x 16 B per row, 512-byte row segments;
-      // columns past V hold 0 (exp store) / -inf (fp16), written up to ldl
-#pragma unroll 2
-      for (int idx = threadIdx.x; idx < 128 * (BIG_V / 8); idx += T::THREADS) {
-        const int sr = idx / (BIG_V / 8), ch = idx % (BIG_V / 8);
-        const int rr2 = r0 + (sr >> 5) * T::WN + 32 * j + (sr & 31), v = v0 + 8 * ch;
-        if (rr2 < R && v + 8 <= ldl)
-          *reinterpret_cast<uint4*>(logits16 + (int64_t)rr2 * ldl + v) =
-              *reinterpret_cast<const uint4*>(stage + sr * BIG_STAGE_LD + 8 * ch);
-      }
-      __syncthreads();  // (the stage is rewritten by the next half)
-    }
-  }
-  if (!save16) __syncthreads();
-  // merge the 4 lane groups of each row -> one VocabPartial per (tile, row)
-  if (threadIdx.x < BIG_R) {
-    const int row_l = threadIdx.x, r = r0 + row_l;
-    if (r < R) {
-      GroupStat a = gs[row_l];
-#pragma unroll
-      for (int q = 1; q < 4; ++q) {
-        const GroupStat c = gs[q * BIG_R + row_l];
-        const float M = fmaxf(a.m, c.m);
-        a.s = (a.m == -INFINITY ? 0.f : a.s * __expf(a.m - M)) +
-              (c.m == -INFINITY ? 0.f : c.s * __expf(c.m - M));
-        if (c.m > a.m || (c.m == a.m && c.xidx < a.xidx)) a.xidx = c.xidx;
-        a.m = M;
-        if (c.zkey > a.zkey || (c.zkey == a.zkey && c.zidx < a.zidx)) {
-          a.zkey = c.zkey;
-          a.zidx = c.zidx;
-          a.zlogit = c.zlogit;
-        }
-        a.xt = fmaxf(a.xt, c.xt);
-      }
-      VocabPartial p;
-      p.m = a.m;
-      p.s = a.s;
-      p.zval = a.zkey;
-      p.zlogit = a.zlogit;
-      p.zidx = a.zidx;
-      p.xidx = a.xidx;
-      p.xtgt = a.xt;
-      p.pad = 0.f;
-      part[(int64_t)vt * R + r] = p;
-    }
-  }
-}
-
-// Recurrent tiles of the big launch: pre[r][n] = sum_k h[r][k] W_hh[n][k] +
-// vgate[r / vdiv][n], 256 rows x 256 gate columns per tile, stored straight
-// from the accumulators (a wave instruction writes 2 rows x 128 B).
-__device__ __forceinline__ void lstm_big_block(int bid, char* lds, const uint16_t* __restrict__ h,
-                                               int R, int H, const uint16_t* __restrict__ whh,
-                                               const float* __restrict__ vgate, int vdiv,
-                                               float* __restrict__ pre) {
-  using T = BigTile;
-  const int G4 = 4 * H;
-  const int n_nt = G4 / BIG_R, n_rt = (R + BIG_R - 1) / BIG_R;
-  const int b = xcd_remap(bid, n_nt * n_rt);
-  const int nt = b / n_rt, rt = b % n_rt;
-  const int r0 = rt * BIG_R, n0 = nt * BIG_R;
-  f32x16 acc[T::TM][T::TN];
-  {
-    DmaSrc<T::NA> a;
-    DmaSrc<T::NB> bs;
-    big_sources(h, R, H, r0, whh, G4, H, n0, H / 64, a, bs);
-    big_mainloop(H / 64, a, bs, lds, acc);
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w / T::WAVES_N,
-            wc = w % T::WAVES_N;
-  // the C tile leaves through LDS 64 rows at a time (row stride 260 floats):
-  // rows q * 64 .. q * 64 + 63 are accumulator blocks i = 2 (q % 2), +1 of
-  // the waves with wr = q / 2; then 16-byte row segments (+ the row's video
-  // gates) to pre
-  constexpr int CLD = BIG_R + 4;
-  float* Cs = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (wr == q / 2) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        const int i = 2 * (q % 2) + ii;
-#pragma unroll
-        for (int j = 0; j < T::TN; ++j) {
-          const int col = wc * T::WN + 32 * j + (lane & 31);
-#pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            const int rl = 32 * ii + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3);
-            Cs[rl * CLD + col] = acc[i][j][k];
-          }
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int idx = (int)threadIdx.x + p * T::THREADS;  // 64 rows x 64 float4
-      const int rl = idx >> 6, c4 = idx & 63;
-      const int r = r0 + q * 64 + rl;
-      if (r < R) {
-        float4 x = *reinterpret_cast<const float4*>(Cs + rl * CLD + 4 * c4);
-        if (vgate != nullptr) {
-          const float4 vg =
-              *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * G4 + n0 + 4 * c4);
-          x.x += vg.x, x.y += vg.y, x.z += vg.z, x.w += vg.w;
-        }
-        *reinterpret_cast<float4*>(pre + (int64_t)r * G4 + n0 + 4 * c4) = x;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void vocab_lstm_big_kernel(
-    VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
-    const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int bid = blockIdx.x;
-  big_phase(bid, 0);
-  if (bid < n_lstm_pad) {
-    if (bid < big_lstm_tiles(R, H)) lstm_big_block(bid, lds, h_t, R, H, whh, vgate, vdiv, pre);
-  } else {
-    vocab_big_block(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
-  }
-  big_phase(bid, 3);
 }
 
 template <int BN, int STAGES, int OCC, bool TOPK = false>
@@ -1220,45 +846,6 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
                                 flags, inv_temp, rng, step, stream, eoff);
 }
 
-// The big-tile launch applies to training / sampling / greedy decode steps of
-// at least BIG_MIN_ROWS rows without temporal attention (the 64-row greedy
-// baseline and beam search keep the 128 x 64 tiles).  CSTCAP_DECODE_TILES=small
-// forces the 128 x 64 tiles (A/B runs).
-constexpr int BIG_MIN_ROWS = 512;
-static bool big_tiles_enabled() {
-  static const int on = [] {
-    const char* e = getenv("CSTCAP_DECODE_TILES");
-    return (e != nullptr && e[0] == 's') ? 0 : 1;
-  }();
-  return on != 0;
-}
-bool vocab_big_ok(int R, int H, int flags, int NQ, bool att) {
-  return big_tiles_enabled() && !att && NQ == 0 && R >= BIG_MIN_ROWS && H % 64 == 0 &&
-         (4 * H) % BIG_R == 0 && !(flags & (VF_TOPK | VF_SAVE_F32));
-}
-
-static int launch_vocab_lstm_big(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
-                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
-                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
-                                 float inv_temp, const uint32_t* rng, int step,
-                                 const uint16_t* h_t, const uint16_t* whh, const float* vgate,
-                                 int vdiv, float* pre, hipStream_t stream, const float* eoff) {
-  const int n_vt = (V + BIG_V - 1) / BIG_V, n_rt = (R + BIG_R - 1) / BIG_R;
-  const int n_l = pre != nullptr ? (big_lstm_tiles(R, H) + 7) / 8 * 8 : 0;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_lstm_big_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, BIG_LDS);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(vocab_lstm_big_kernel, dim3(n_l + n_vt * n_rt), dim3(BigTile::THREADS),
-                     BIG_LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl,
-                     (VocabPartial*)part, tgt, tgt_stride, flags, inv_temp, rng, step, eoff, h_t,
-                     whh, vgate, vdiv, pre, n_l);
-  post_launch("vocab_lstm_big_kernel", stream);
-  return n_vt;
-}
-
 // microbenchmark only (scripts/microbench_kernels.py): other tile / pipeline
 // shapes of the vocab kernel, <BN, STAGES, OCC>
 void launch_vocab_fwd_variant(int variant, const uint16_t* hd, int ldh, int R, int H,
@@ -1269,12 +856,6 @@ void launch_vocab_fwd_variant(int variant, const uint16_t* hd, int ldh, int R, i
 #define VV(BN, ST, OC)                                                                          \
   launch_vocab_fwd_tr<BN, ST, OC>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, \
                                   flags, inv_temp, rng, step, stream)
-  if (variant == 9) {  // the big-tile launch (vocabulary tiles only)
-    (void)launch_vocab_lstm_big(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
-                                flags, inv_temp, rng, step, nullptr, nullptr, nullptr, 1, nullptr,
-                                stream, nullptr);
-    return;
-  }
   switch (variant) {
     case 1: VV(128, 3, 1); break;
     case 2: VV(128, 4, 1); break;
@@ -1366,10 +947,6 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
                                                     eoff, nullptr);
     return vocab_num_tiles(V);
   }
-  if (vocab_big_ok(R, H, flags, NQ, att != nullptr))
-    return launch_vocab_lstm_big(hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride,
-                                 flags, inv_temp, rng, step, h_t, whh, vgate, vdiv, pre, stream,
-                                 eoff);
 #define VL(AVX)                                                                            \
   launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, \
                                               tgt, tgt_stride, flags, inv_temp, rng, step,  \

@@ -6,9 +6,6 @@
 
 namespace cst {
 
-// vocab.hip: phase stamps of the big-tile decode launch (diagnostics; nullptr = off)
-void set_big_debug(int64_t* p);
-
 // beam.hip: fused beam step (LSE + candidate top-K + selection + next cell)
 struct BeamFusedArgs {
   const struct VocabPartial* part;  // (n_vt, R) tile partials of the vocab launch
