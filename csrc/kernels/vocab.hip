@@ -313,8 +313,8 @@ __device__ __forceinline__ void vocab_tr_block(int bid, char* lds, VOCAB_TR_PARA
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {  // (the weights of the sum above, recomputed)
-          const float wv = __builtin_amdgcn_exp2f(fmaf(acc[i][j][k], wsc, -wl));
+        for (int k = 0; k < 16; ++k) {
+          const float wv = ew[i][k];
           cum += wv;
           const bool hit = cand < 0 && cum >= tm && wv > 0.f;
           cand = hit ? vb + 32 * i + 8 * (k >> 2) + (k & 3) : cand;
