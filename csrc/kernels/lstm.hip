@@ -181,15 +181,28 @@ __device__ __forceinline__ void lstm_bwd_load_epi(int r0, int R, int H, int rg, 
                                                   const DhOneHot& oh, uint2* pg, float* pc,
                                                   float* pcp, float* pdc, float* pdl) {
   constexpr int RG = 4 * GROUPS, RPT = BM / RG;
+  // Branch-free: every load of the batch is issued back to back (a load under
+  // a per-element null test becomes a branch with its own vmcnt(0) wait, one
+  // dependent round trip per element); absent operands read a stand-in
+  // pointer and are replaced afterwards (wave-uniform selects)
+  const float* cpv = c_prev != nullptr ? c_prev : c_t;
+  const float* dsv = dh_scale != nullptr ? dh_scale : dh_logit;
+  float psc[RPT];
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int r = min(r0 + rg + RG * i, R - 1);
     const int64_t o = (int64_t)r * H + hu;
     pg[i] = *reinterpret_cast<const uint2*>(gates + (int64_t)r * 4 * H + 4 * hu);
     pc[i] = c_t[o];
-    pcp[i] = c_prev ? c_prev[o] : 0.f;
+    pcp[i] = cpv[o];
     pdc[i] = dc_carry[o];
-    pdl[i] = dh_logit[o] * (dh_scale ? dh_scale[r] : 1.f);
+    pdl[i] = dh_logit[o];
+    psc[i] = dsv[r];
+  }
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    pcp[i] = c_prev != nullptr ? pcp[i] : 0.f;
+    pdl[i] *= dh_scale != nullptr ? psc[i] : 1.f;
   }
   // forward-computed X = E W: the one-hot terms a W[ys] + b W[yx] of the row
   // (uniform branches; the token rows are gathered with the other operands)
@@ -450,24 +463,19 @@ __global__ __launch_bounds__(256, 3) void lstm_step_bwd_sk_kernel(
   // needed (loss.hip scst_loss_fwd_kernel), only the compiler's order
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (tid == 0) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // epilogue operands first (their latency overlaps the slab loads)
   const int u = tid & 63, rg = tid >> 6, hu = u0 + u;
-  constexpr int RPT = 16;  // rows rg + 4 i
-  uint2 pg[RPT];
-  float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
-  lstm_bwd_load_epi<64, 1>(r0, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit, dh_scale, oh,
-                           pg, pc, pcp, pdc, pdl);
-  // the SPLIT partials in split order (sc1 loads)
-  float sum[16];
-  const float* base = slab + (int64_t)tile * SPLIT * 4096 + w * 1024 + lane;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) sum[r] = 0.f;
-#pragma unroll
-  for (int q = 0; q < SPLIT; ++q)
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      sum[r] += __hip_atomic_load(base + q * 4096 + r * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the SPLIT partials in split order (sc1 loads) -> the dh tile in LDS
   {
+    float sum[16];
+    const float* base = slab + (int64_t)tile * SPLIT * 4096 + w * 1024 + lane;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sum[r] = 0.f;
+#pragma unroll
+    for (int q = 0; q < SPLIT; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sum[r] += __hip_atomic_load(base + q * 4096 + r * 64, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
     f32x16 tot[1][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) tot[0][0][r] = sum[r];
@@ -477,22 +485,32 @@ __global__ __launch_bounds__(256, 3) void lstm_step_bwd_sk_kernel(
   const float* C = reinterpret_cast<const float*>(lds);
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
+  // the cell backward of the tile's 64 rows x 64 units, rows rg + 4 i, in two
+  // halves of 8 rows (operands of a half loaded in one batch: lstm_bwd_load_epi)
 #pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int row = rg + 4 * i, r = r0 + row;
-    if (r < R) {
-      const int64_t o = (int64_t)r * H + hu;
-      float dh = C[row * TL::CSTRIDE + u];
-      const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
-      if (keep) dh += pdl[i] * inv_keep;
-      const uint2 gp = pg[i];
-      const CellBwd cb = cell_bwd(cell, dh, pdc[i], bf2f(gp.x & 0xffff), bf2f(gp.x >> 16),
-                                  bf2f(gp.y & 0xffff), bf2f(gp.y >> 16), pc[i], pcp[i]);
-      dc_carry[o] = cb.carry;
-      uint2 pk;
-      pk.x = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
-      pk.y = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
-      *reinterpret_cast<uint2*>(dG + (int64_t)r * KD + 4 * hu) = pk;
+  for (int hh = 0; hh < 2; ++hh) {
+    constexpr int RPT = 8;
+    uint2 pg[RPT];
+    float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
+    lstm_bwd_load_epi<32, 1>(r0 + 32 * hh, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit,
+                             dh_scale, oh, pg, pc, pcp, pdc, pdl);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int row = 32 * hh + rg + 4 * i, r = r0 + row;
+      if (r < R) {
+        const int64_t o = (int64_t)r * H + hu;
+        float dh = C[row * TL::CSTRIDE + u];
+        const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
+        if (keep) dh += pdl[i] * inv_keep;
+        const uint2 gp = pg[i];
+        const CellBwd cb = cell_bwd(cell, dh, pdc[i], bf2f(gp.x & 0xffff), bf2f(gp.x >> 16),
+                                    bf2f(gp.y & 0xffff), bf2f(gp.y >> 16), pc[i], pcp[i]);
+        dc_carry[o] = cb.carry;
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
+        pk.y = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
+        *reinterpret_cast<uint2*>(dG + (int64_t)r * KD + 4 * hu) = pk;
+      }
     }
   }
 }
