@@ -874,21 +874,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                     has_xe ? oh_b.data_ptr<float>() + t * R : nullptr,
                     has_xe ? oh_yx.data_ptr<int>() + t * R : nullptr};
   };
-  // layer 0 without attention: the split-K step kernel (lstm.hip
-  // lstm_step_bwd_sk_kernel), fp32 partial slabs + per-tile tickets (zeroed
-  // here, in the captured graph a memset node; re-armed by each last arriver).
-  // CSTCAP_BWD_SPLIT=0 keeps the in-block form (A/B runs).
-  static const bool bwd_sk_env = [] {
-    const char* e = getenv("CSTCAP_BWD_SPLIT");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  const bool bwd_sk = bwd_sk_env && !has_att;
-  at::Tensor sk_slab, sk_cnt;
-  if (bwd_sk) {
-    const int64_t nt = lstm_bwd_sk_tiles((int)R, (int)H);
-    sk_slab = at::empty({nt * lstm_bwd_sk_split() * 4096}, f32);
-    sk_cnt = at::zeros({nt}, i32);
-  }
   size_t next_chunk = 0;
   for (int64_t t = n_steps - 1; t >= 0; --t) {
     if (next_chunk < dhd_chunks.size() && t == dhd_chunks[next_chunk][1] - 1)
@@ -923,23 +908,14 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       dh0_in = dX_up.data_ptr<float>();
       dh0_sc = nullptr;
     }
-    const uint16_t* dg_next0 =
-        t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr;
-    const float* c_prev0 =
-        t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr);
-    if (!(bwd_sk && launch_lstm_step_bwd_sk(
-              dg_next0, reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dh0_in,
-              dc.data_ptr<float>(), reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
-              c_all[t].data_ptr<float>(), c_prev0, (int)R, (int)H, (float)drop_p, RNG, key(0, t),
-              reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc,
-              NL == 1 ? &oh_t : nullptr, sk_slab.data_ptr<float>(), sk_cnt.data_ptr<int>())))
-      launch_lstm_step_bwd(dg_next0, reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dh0_in,
-                           dc.data_ptr<float>(),
-                           reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()),
-                           c_all[t].data_ptr<float>(), c_prev0, (int)R, (int)H, (float)drop_p, RNG,
-                           key(0, t), reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD,
-                           st, (int)cell, dh0_sc, att_mfma ? &abe : nullptr,
-                           NL == 1 ? &oh_t : nullptr);
+    launch_lstm_step_bwd(
+        t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
+        reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dh0_in, dc.data_ptr<float>(),
+        reinterpret_cast<const uint16_t*>(gates_all[t].data_ptr()), c_all[t].data_ptr<float>(),
+        t > 0 ? c_all[t - 1].data_ptr<float>() : (has_s0 ? state0[1].data_ptr<float>() : nullptr),
+        (int)R, (int)H, (float)drop_p, RNG, key(0, t),
+        reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc,
+        att_mfma ? &abe : nullptr, NL == 1 ? &oh_t : nullptr);
     if (att_mfma)
       launch_att_bwd_mfma(dal_part.data_ptr<float>(), (int)(H / 64), (int)R,
                           a_alpha[t].data_ptr<float>(), t > 0 ? a_q[t].data_ptr<float>() : nullptr,

@@ -393,158 +393,6 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
   }
 }
 
-// Split-K form of the backward step (no attention epilogue): the K range of
-// each 64 x 64 tile is split over SPLIT workgroups of 256 threads (3 LDS
-// stages, 48 KB: 3 workgroups per CU, 640 workgroups at the headline shape,
-// one round), so the dependent K loop of a workgroup is 32 / SPLIT K-tiles
-// instead of 16.  Each workgroup leaves its fp32 partial tile in a slab
-// (write-through sc1 stores, drained by every storing wave's vmcnt(0)), one
-// lane takes a relaxed agent-scope ticket, and the LAST arriver of the tile
-// sums the SPLIT slabs (sc1 loads) in split order -- deterministic,
-// whatever the arrival order -- then loads the epilogue operands and runs the
-// cell backward as lstm_step_bwd_kernel does.  The ticket word is zeroed by
-// the caller before the loop and re-armed by the last arriver.
-// (The in-block form: 160 workgroups of 512 threads on the 256 CUs, each
-// a 16-deep K loop, ~29 us per step in rocprofv3: the reverse loop's bound.)
-template <int SPLIT>
-__global__ __launch_bounds__(256, 3) void lstm_step_bwd_sk_kernel(
-    const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
-    const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
-    const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
-    const float* __restrict__ c_prev, int R, int H, float drop_p,
-    const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int cell,
-    const float* __restrict__ dh_scale, DhOneHot oh, float* __restrict__ slab,
-    int* __restrict__ cnt) {
-  using TL = Tile<64, 64, LSTM_BWD_STAGES>;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  // (the last-arriver flag lives in the one dynamic LDS array, behind the
-  // stages: a second __shared__ object can make hipcc drain vmcnt before the
-  // main loop's LDS reads)
-  int* s_last = reinterpret_cast<int*>(lds + TL::LDS_BYTES);
-  const int n_ut = H / 64, n_rt = (R + 63) / 64, n_tiles = n_ut * n_rt;
-  const int b = xcd_remap_l(blockIdx.x, n_tiles * SPLIT);  // a tile's splits: consecutive
-  const int tile = b / SPLIT, sp = b % SPLIT;
-  const int ut = tile / n_rt, rt = tile % n_rt;
-  const int r0 = rt * 64, u0 = ut * 64;
-  const int nk_all = dg_next != nullptr ? KD / 64 : 0;
-  const int nks = nk_all / SPLIT, k0 = sp * nks;  // (launcher: nk_all % SPLIT == 0)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  f32x16 acc[1][1];
-  if (nks > 0) {
-    DmaSrc<2> a, bsrc;
-    a.r0 = a.r1 = make_rsrc(dg_next, (int64_t)R * KD * 2);
-    bsrc.r0 = bsrc.r1 = make_rsrc(whhT, (int64_t)H * KD * 2);
-    a.ksplit = bsrc.ksplit = nks;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = dma_row(w, i, lane);
-      a.voff0[i] = a.voff1[i] = min(r0 + row, R - 1) * KD * 2 + k0 * 128 + dma_chunk(row, lane) * 16;
-      bsrc.voff0[i] = bsrc.voff1[i] = (u0 + row) * KD * 2 + k0 * 128 + dma_chunk(row, lane) * 16;
-    }
-    gemm_nt_mainloop<TL>(nks, a, bsrc, lds, acc);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
-  }
-  // this split's partial -> its slab (accumulator lane order), sc1 stores
-  float* mine = slab + ((int64_t)tile * SPLIT + sp) * 4096 + w * 1024 + lane;
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-    __hip_atomic_store(mine + r * 64, acc[0][0][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-  __syncthreads();
-  if (tid == 0) {
-    const int t = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_last = t == SPLIT - 1;
-  }
-  __syncthreads();
-  if (!*s_last) return;
-  // every load of the handed-off slabs below is an sc1 load: no agent acquire
-  // needed (loss.hip scst_loss_fwd_kernel), only the compiler's order
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (tid == 0) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int u = tid & 63, rg = tid >> 6, hu = u0 + u;
-  // the SPLIT partials in split order (sc1 loads) -> the dh tile in LDS
-  {
-    float sum[16];
-    const float* base = slab + (int64_t)tile * SPLIT * 4096 + w * 1024 + lane;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sum[r] = 0.f;
-#pragma unroll
-    for (int q = 0; q < SPLIT; ++q)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        sum[r] += __hip_atomic_load(base + q * 4096 + r * 64, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-    f32x16 tot[1][1];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tot[0][0][r] = sum[r];
-    store_acc_to_lds<TL>(tot, reinterpret_cast<float*>(lds), [](int) { return 0.f; });
-  }
-  __syncthreads();
-  const float* C = reinterpret_cast<const float*>(lds);
-  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-  const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
-  // the cell backward of the tile's 64 rows x 64 units, rows rg + 4 i, in two
-  // halves of 8 rows (operands of a half loaded in one batch: lstm_bwd_load_epi)
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    constexpr int RPT = 8;
-    uint2 pg[RPT];
-    float pc[RPT], pcp[RPT], pdc[RPT], pdl[RPT];
-    lstm_bwd_load_epi<32, 1>(r0 + 32 * hh, R, H, rg, hu, gates, c_t, c_prev, dc_carry, dh_logit,
-                             dh_scale, oh, pg, pc, pcp, pdc, pdl);
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int row = 32 * hh + rg + 4 * i, r = r0 + row;
-      if (r < R) {
-        const int64_t o = (int64_t)r * H + hu;
-        float dh = C[row * TL::CSTRIDE + u];
-        const bool keep = drop_p <= 0.f || dropout_keep(seed, step, r, hu, drop_p);
-        if (keep) dh += pdl[i] * inv_keep;
-        const uint2 gp = pg[i];
-        const CellBwd cb = cell_bwd(cell, dh, pdc[i], bf2f(gp.x & 0xffff), bf2f(gp.x >> 16),
-                                    bf2f(gp.y & 0xffff), bf2f(gp.y >> 16), pc[i], pcp[i]);
-        dc_carry[o] = cb.carry;
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
-        pk.y = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
-        *reinterpret_cast<uint2*>(dG + (int64_t)r * KD + 4 * hu) = pk;
-      }
-    }
-  }
-}
-
-int lstm_bwd_sk_split() { return 4; }
-int lstm_bwd_sk_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
-
-// split-K backward step (no attention): slab = lstm_bwd_sk_tiles * SPLIT *
-// 4096 floats, cnt = lstm_bwd_sk_tiles ints, zero before the first step
-bool launch_lstm_step_bwd_sk(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
-                             float* dc_carry, const uint16_t* gates, const float* c_t,
-                             const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
-                             int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                             const float* dh_scale, const DhOneHot* ohp, float* slab, int* cnt) {
-  constexpr int SPLIT = 4;
-  using TL = Tile<64, 64, LSTM_BWD_STAGES>;
-  if (H % 64 != 0 || (KD / 64) % SPLIT != 0 || KD % 64 != 0) return false;
-  const DhOneHot oh = ohp != nullptr ? *ohp : DhOneHot{};
-  constexpr int LDS = TL::LDS_BYTES + 16;  // (C tile 64 x 72 floats fits in the stages)
-  static_assert(64 * TL::CSTRIDE * 4 <= TL::LDS_BYTES, "C tile in the stages");
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_sk_kernel<SPLIT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr_set = true;
-  }
-  const int n = lstm_bwd_sk_tiles(R, H) * SPLIT;
-  hipLaunchKernelGGL(lstm_step_bwd_sk_kernel<SPLIT>, dim3(n), dim3(256), LDS, stream, dg_next,
-                     whhT, dh_logit, dc_carry, gates, c_t, c_prev, R, H, drop_p, rng, step, dG, KD,
-                     cell, dh_scale, oh, slab, cnt);
-  post_launch("lstm_step_bwd_sk_kernel", stream);
-  return true;
-}
-
 int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
 template <int GROUPS, bool ATT = false, int CP = 8, int STAGES = LSTM_BWD_STAGES>

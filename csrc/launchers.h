@@ -235,14 +235,6 @@ struct AttBwdEpi {
   float* dal_part;       // (H / 64, R, CP) fp32
 };
 bool att_bwd_epi_ok(int vdiv, int C, int H);
-// split-K backward step, no attention (lstm.hip); false = shape not supported
-int lstm_bwd_sk_split();
-int lstm_bwd_sk_tiles(int R, int H);
-bool launch_lstm_step_bwd_sk(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
-                             float* dc_carry, const uint16_t* gates, const float* c_t,
-                             const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
-                             int step, uint16_t* dG, int KD, hipStream_t stream, int cell,
-                             const float* dh_scale, const DhOneHot* ohp, float* slab, int* cnt);
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,
                           const float* c_prev, int R, int H, float drop_p, const uint32_t* rng,
