@@ -97,6 +97,13 @@ __device__ __forceinline__ float tanhf_(float x) {
   const float t = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
   return copysignf(t, x);
 }
+// attention scorer tanh: tanh(x) = 1 - 2 / (exp(2x) + 1): one exp, one
+// reciprocal, three plain ops (saturates to +-1 through exp -> inf / 0); the
+// forward (att_mfma.h) and backward scorers use the same form
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
 
 // murmur3 32-bit finaliser: avalanche hash used as a counter-based RNG for
 // the per-element sampling draws (hash(row-key ^ v * odd constant)).

@@ -430,8 +430,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   // Step 0 (q = 0) and other shapes use the attention kernels of attention.hip.
   const int CPAD = C <= 8 ? 8 : 16;
   const bool att_mfma = has_att && att_mfma_ok((int)vgate_div, (int)C, (int)A, (int)H, per_frame);
-  at::Tensor gv16, vg16, att_ep, att_cnt;
+  at::Tensor gv16, vg16, att_ep, att_cnt, u_all;
   if (att_mfma) {
+    // training: the scorer values tanh(P + q) of steps >= 1 (fp16), read by
+    // the fused attention backward (lstm.hip att_bwd_fused_wg)
+    if (save) u_all = at::empty({n_steps, R, C, A}, f32.dtype(at::kHalf));
     gv16 = at::zeros({Bv, H4, CPAD}, bf);  // frame-minor, frames zero-padded
     gv16.narrow(2, 0, C).copy_(a_gv.transpose(1, 2));
     vg16 = at::empty({R, H4}, bf);
@@ -475,7 +478,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                        reinterpret_cast<uint16_t*>(vg16.data_ptr()),
                        save ? alpha_all[t + 1].data_ptr<float>() : nullptr,
                        save ? q_next.data_ptr<float>() : nullptr, att_ep.data_ptr<float>(),
-                       att_cnt.data_ptr<int>()};
+                       att_cnt.data_ptr<int>(),
+                       save ? reinterpret_cast<uint16_t*>(u_all[t + 1].data_ptr()) : nullptr};
     const bool q_tiles = has_att && !att_mfma;  // W_q tiles in the recurrent GEMM
     const int n_vt = launch_vocab_lstm_fwd(
         vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
@@ -515,7 +519,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   }
   stamp(STAMP_FWD_END, st);
   // saved: {logits16, hd of the top layer (vocab input), layer 0's gates, c, h}
-  // (+ {alpha_all, q_all}) (+ {h, c, gates of layer l, hd of layer l-1} per l >= 1)
+  // (+ {alpha_all, q_all, u_all}) (+ {h, c, gates of layer l, hd of layer l-1} per l >= 1)
   std::vector<at::Tensor> out = {seq, g_sel, want_xe ? g_xe : at::Tensor(), lse};
   if (save) {
     out.push_back(logits16);
@@ -526,6 +530,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     if (has_att) {
       out.push_back(alpha_all);
       out.push_back(q_all);
+      out.push_back(u_all.defined() ? u_all : at::empty({0}, f32.dtype(at::kHalf)));
     }
     for (int64_t l = 1; l < NL; ++l) {
       out.push_back(Hs[l]);
@@ -587,11 +592,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   TORCH_CHECK(toks.numel() == n_steps * R, "toks must hold one token per (step, row)");
   const uint32_t* RNG = rng_ptr(rng);
   const bool has_att = !att.empty();
-  at::Tensor a_gv, a_pre, a_wq, a_wa, a_alpha, a_q;
+  at::Tensor a_gv, a_pre, a_wq, a_wa, a_alpha, a_q, a_u;
   int64_t Bv = 0, C = 0, A = 0, vdiv = 1;
   if (has_att) {
-    TORCH_CHECK(att.size() == 6, "att = {Gv, P, W_q, w_a, alpha_all, q_all}");
+    TORCH_CHECK(att.size() == 6 || att.size() == 7,
+                "att = {Gv, P, W_q, w_a, alpha_all, q_all[, u_all]}");
     a_gv = att[0], a_pre = att[1], a_wq = att[2], a_wa = att[3], a_alpha = att[4], a_q = att[5];
+    if (att.size() == 7 && att[6].numel() > 0) a_u = att[6];
     Bv = a_gv.size(0), C = a_gv.size(1), A = a_pre.size(2);
     vdiv = R / Bv;
     TORCH_CHECK(Bv * vdiv == R && a_alpha.size(0) == n_steps && a_alpha.size(2) == C &&
@@ -835,13 +842,23 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const bool att_mfma = has_att &&
                         att_mfma_ok((int)vdiv, (int)C, (int)A, (int)H, per_frame) &&
                         att_bwd_epi_ok((int)vdiv, (int)C, (int)H) && (KD / 64) % 2 == 0;
-  at::Tensor gvb16, dal_part;
+  at::Tensor gvb16, dal_part, att_flags;
   AttBwdEpi abe{};
+  // the attention backward of step t + 1 runs as extra workgroups of step t's
+  // launch (lstm.hip att_bwd_fused_wg) instead of a launch of its own between
+  // the two reverse steps; the dalpha partials alternate between two buffers
+  // (att8: 4.717 / 4.728 vs 4.884 / 4.939 ms per step unfused, interleaved on
+  // one box, profiles/r5/README_r5.md)
+  const bool att_fuse = att_mfma && n_steps > 1 && a_u.defined() &&
+                        a_u.scalar_type() == at::kHalf && a_u.size(0) == n_steps &&
+                        a_u.size(1) == R && a_u.size(2) == C && a_u.size(3) == A &&
+                        att_bwd_fuse_ok((int)vdiv, (int)C, (int)A, (int)H, (int)Bv, (int)R);
   if (att_mfma) {
     // gate tables with the 4 packed gates of a unit innermost: (Bv, H, CP, 4)
     gvb16 = at::zeros({Bv, H, CPAD, 4}, wx.options());
     gvb16.narrow(2, 0, C).copy_(a_gv.view({Bv, C, H, 4}).permute({0, 2, 1, 3}));
-    dal_part = at::empty({H / 64, R, CPAD}, f32);
+    dal_part = at::empty({2, H / 64, R, CPAD}, f32);
+    if (att_fuse) att_flags = at::zeros({n_steps, Bv}, i32);
     abe = AttBwdEpi{reinterpret_cast<const uint16_t*>(gvb16.data_ptr()), (int)vdiv, (int)C, CPAD,
                     dal_part.data_ptr<float>()};
     dpre_part = at::zeros({Bv, C, A}, f32);
@@ -908,6 +925,23 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       dh0_in = dX_up.data_ptr<float>();
       dh0_sc = nullptr;
     }
+    if (att_mfma) {
+      abe.dal_part = dal_part[t & 1].data_ptr<float>();
+      abe.flags = nullptr;
+      if (att_fuse && t + 1 < n_steps) {  // + step t + 1's attention backward
+        abe.flags = att_flags[t + 1].data_ptr<int>();
+        abe.dal_next = dal_part[(t + 1) & 1].data_ptr<float>();
+        abe.alpha = a_alpha[t + 1].data_ptr<float>();
+        abe.u = reinterpret_cast<const uint16_t*>(a_u[t + 1].data_ptr());
+        abe.wa = a_wa.data_ptr<float>();
+        abe.Bv = (int)Bv;
+        abe.A = (int)A;
+        abe.G4 = (int)H4;
+        abe.dP_acc = dpre_part.data_ptr<float>();
+        abe.dwa_part = dwa_part.data_ptr<float>();
+        abe.dba_part = dba_part.data_ptr<float>();
+      }
+    }
     launch_lstm_step_bwd(
         t + 1 < n_steps ? reinterpret_cast<const uint16_t*>(dG_all[t + 1].data_ptr()) : nullptr,
         reinterpret_cast<const uint16_t*>(whhT.data_ptr()), dh0_in, dc.data_ptr<float>(),
@@ -916,8 +950,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         (int)R, (int)H, (float)drop_p, RNG, key(0, t),
         reinterpret_cast<uint16_t*>(dG_all[t].data_ptr()), (int)KD, st, (int)cell, dh0_sc,
         att_mfma ? &abe : nullptr, NL == 1 ? &oh_t : nullptr);
-    if (att_mfma)
-      launch_att_bwd_mfma(dal_part.data_ptr<float>(), (int)(H / 64), (int)R,
+    if (att_fuse) {
+      // (step t's attention backward: in step t - 1's launch, or after the loop)
+    } else if (att_mfma)
+      launch_att_bwd_mfma(dal_part[t & 1].data_ptr<float>(), (int)(H / 64), (int)R,
                           a_alpha[t].data_ptr<float>(), t > 0 ? a_q[t].data_ptr<float>() : nullptr,
                           a_pre.data_ptr<float>(), a_wa.data_ptr<float>(), (int)Bv, (int)vdiv,
                           (int)C, CPAD, (int)A, (int)H4,
@@ -933,6 +969,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                      dba_part.data_ptr<float>(), st, per_frame);
     if (t == n_steps - 1) stamp(STAMP_BWD_LOOP0, st);
   }
+  if (att_fuse)
+    launch_att_bwd_mfma(dal_part[0].data_ptr<float>(), (int)(H / 64), (int)R,
+                        a_alpha[0].data_ptr<float>(), nullptr, a_pre.data_ptr<float>(),
+                        a_wa.data_ptr<float>(), (int)Bv, (int)vdiv, (int)C, CPAD, (int)A, (int)H4,
+                        reinterpret_cast<uint16_t*>(dG_all[0].data_ptr()), (int)KD, 0,
+                        dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
+                        dba_part.data_ptr<float>(), st);
   stamp(STAMP_BWD_LOOP, st);
   at::Tensor dvg;
   if (!has_att) {

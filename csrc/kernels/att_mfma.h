@@ -56,13 +56,6 @@ __device__ __forceinline__ bf16x8 ld_bf16x8(const uint16_t* p) {
   return *reinterpret_cast<const bf16x8*>(p);
 }
 
-// tanh(x) = 1 - 2 / (exp(2x) + 1): one exp, one reciprocal, three plain ops
-// (saturates to +-1 through exp -> inf / 0)
-__device__ __forceinline__ float tanh_fast(float x) {
-  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
-  return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
-}
-
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 // CP: frames padded to 8 / 16.  blk = b * NS + s.
@@ -144,10 +137,17 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     float ec[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      ec[j] = wv.x * tanh_fast(p.x + acc[j][0]);
-      ec[j] = fmaf(wv.y, tanh_fast(p.y + acc[j][1]), ec[j]);
-      ec[j] = fmaf(wv.z, tanh_fast(p.z + acc[j][2]), ec[j]);
-      ec[j] = fmaf(wv.w, tanh_fast(p.w + acc[j][3]), ec[j]);
+      const float t0 = tanh_fast(p.x + acc[j][0]), t1 = tanh_fast(p.y + acc[j][1]);
+      const float t2 = tanh_fast(p.z + acc[j][2]), t3 = tanh_fast(p.w + acc[j][3]);
+      ec[j] = wv.x * t0;
+      ec[j] = fmaf(wv.y, t1, ec[j]);
+      ec[j] = fmaf(wv.z, t2, ec[j]);
+      ec[j] = fmaf(wv.w, t3, ec[j]);
+      const int row = 16 * j + ru;
+      if (g.u_out != nullptr && row < vdiv)  // the backward's scorer values (fp16)
+        *reinterpret_cast<uint2*>(g.u_out + ((int64_t)(row0 + row) * C + c) * A + a0 + u0) =
+            make_uint2((uint32_t)f2h(t0) | ((uint32_t)f2h(t1) << 16),
+                       (uint32_t)f2h(t2) | ((uint32_t)f2h(t3) << 16));
       ec[j] += __shfl_xor(ec[j], 16, 64);
       ec[j] += __shfl_xor(ec[j], 32, 64);
     }

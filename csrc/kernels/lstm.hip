@@ -243,7 +243,302 @@ bool att_bwd_epi_ok(int vdiv, int C, int H) {
          2 * 64 * 72 * 4 + nv * 64 * 4 * CP * 2 <= 2 * LSTM_BWD_STAGES * 16384;
 }
 
-template <int BM, int STAGES, int GROUPS, bool ATT, int CP>
+// Fused attention backward (AttBwdEpi::flags): one 512-thread workgroup per
+// video, thread = (4 query units, row group of 4): A <= 512, rows <= 32.  The
+// K-tiles of the launch's GEMM are reordered per group: group g streams its
+// half of the dG_{t+1} tiles, then its half of the A / 64 tail tiles, so both
+// groups reach the tail (dq_{t+1}, produced by the attention workgroups of the
+// SAME launch) last.
+constexpr int ATTF_MAXR = 32, ATTF_RG = 4;
+bool att_bwd_fuse_ok(int vdiv, int C, int A, int H, int Bv, int R) {
+  const int CP = C <= 8 ? 8 : 16;
+  return att_bwd_epi_ok(vdiv, C, H) && vdiv <= ATTF_MAXR && vdiv * CP <= 512 && A % 128 == 0 &&
+         A <= 512 && H % 128 == 0 && H / 64 <= 16 && Bv * vdiv == R;
+}
+
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// The attention workgroup (video b) of step t + 1 (see AttBwdEpi).  The scorer
+// values u = tanh(P + q) come from the forward (fp16, AttMfmaArgs::u_out), so
+// the backward has no transcendental:
+//   dalpha[r][c] = the sum of the H/64 step-(t+1) partials; softmax backward
+//   de = alpha (dalpha - sum_k alpha_k dalpha_k); thread (units 4 cq..4 cq+3,
+//   rows rq, rq + 4, ...): dq[r][a] = w_a[a] sum_c de[r][c] (1 - u^2) (4 bf16
+//   written through -- sc1 -- into dg_next's tail).  Hand-off to the GEMM
+//   workgroups of the launch: every wave drains its stores (vmcnt(0)), a
+//   workgroup barrier, then ONE agent-scope add on the video's flag; the
+//   readers poll it and load the tail with sc1 loads (the no-fence form of
+//   loss.hip / att_mfma.h).  Only then (off the critical path) dP[b][c][a] =
+//   sum_r de (1 - u^2) w_a and dw_a = sum_{r, c} de u over the 4 row groups
+//   (LDS), db_a by thread 0.  The u loads of the first 16 rows go out first:
+//   they depend on nothing, so they overlap the dalpha loads and the softmax.
+template <int CP>
+__device__ __forceinline__ void att_bwd_fused_wg(const AttBwdEpi& f, int b, int R, int n_ut,
+                                                 uint16_t* __restrict__ dgn, int ldg, char* lds) {
+  float* s_da = reinterpret_cast<float*>(lds);
+  float* s_de = s_da + ATTF_MAXR * CP;
+  float* s_red = s_de + ATTF_MAXR * CP;  // (ATTF_RG - 1) x 128 x (8 frames x 4 + 4)
+  const int tid = threadIdx.x, vdiv = f.vdiv, C = f.C, A = f.A;
+  const int row0 = b * vdiv, nrc = vdiv * CP;
+  const int cq = tid & 127, rq = tid >> 7;  // (rq is wave-uniform)
+  const bool acol = 4 * cq < A;
+  const int a = min(4 * cq, A - 4);
+  constexpr int RB = 4;  // rows per batch and thread
+  auto u_batch = [&](int i0, uint2 (&u)[RB][CP]) {
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int k = min(rq + ATTF_RG * (i0 + i), vdiv - 1);
+#pragma unroll
+      for (int c = 0; c < CP; ++c)
+        u[i][c] = *reinterpret_cast<const uint2*>(f.u + ((int64_t)(row0 + k) * C + min(c, C - 1)) * A + a);
+    }
+  };
+  uint2 ub[RB][CP];
+  u_batch(0, ub);
+  float dsum = 0.f;
+  {
+    const int rc = min(tid, nrc - 1);
+    const float* pp = f.dal_next + (int64_t)row0 * CP + rc;
+    float x[16];
+#pragma unroll
+    for (int ut = 0; ut < 16; ++ut) x[ut] = pp[(int64_t)min(ut, n_ut - 1) * R * CP];
+#pragma unroll
+    for (int ut = 0; ut < 16; ++ut) dsum += ut < n_ut ? x[ut] : 0.f;
+  }
+  const float4 wa4 = *reinterpret_cast<const float4*>(f.wa + a);
+  const f32x2_t wa01 = {wa4.x, wa4.y}, wa23 = {wa4.z, wa4.w};
+  float alr[CP];
+  {
+    const int rr = min(tid, vdiv - 1);
+#pragma unroll
+    for (int c = 0; c < CP; ++c) alr[c] = f.alpha[(int64_t)(row0 + rr) * C + min(c, C - 1)];
+#pragma unroll
+    for (int c = 0; c < CP; ++c) alr[c] = c < C ? alr[c] : 0.f;
+  }
+  if (tid < nrc) s_da[tid] = dsum;
+  __syncthreads();
+  if (tid < vdiv) {
+    float sa = 0.f;
+#pragma unroll
+    for (int c = 0; c < CP; ++c) sa += alr[c] * s_da[tid * CP + c];
+#pragma unroll
+    for (int c = 0; c < CP; ++c) s_de[tid * CP + c] = alr[c] * (s_da[tid * CP + c] - sa);
+  }
+  __syncthreads();
+  // dq rows of this thread; dP / dw_a contributions kept in registers
+  f32x2_t dp[CP][2], dw[2];
+#pragma unroll
+  for (int c = 0; c < CP; ++c) dp[c][0] = dp[c][1] = f32x2_t{0.f, 0.f};
+  dw[0] = dw[1] = f32x2_t{0.f, 0.f};
+  auto rows = [&](int i0, const uint2 (&u)[RB][CP]) {
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int k = rq + ATTF_RG * (i0 + i);
+      if (k < vdiv) {  // (wave-uniform)
+        f32x2_t dq01 = {0.f, 0.f}, dq23 = {0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < CP; ++c) {
+          if (c < C) {
+            const float de = s_de[k * CP + c];
+            const f32x2_t u01 = {h2f(u[i][c].x & 0xffff), h2f(u[i][c].x >> 16)};
+            const f32x2_t u23 = {h2f(u[i][c].y & 0xffff), h2f(u[i][c].y >> 16)};
+            const f32x2_t de2 = {de, de};
+            const f32x2_t g01 = de2 * (1.f - u01 * u01), g23 = de2 * (1.f - u23 * u23);
+            dq01 += g01;
+            dq23 += g23;
+            dp[c][0] += g01;
+            dp[c][1] += g23;
+            dw[0] += de2 * u01;
+            dw[1] += de2 * u23;
+          }
+        }
+        dq01 *= wa01;
+        dq23 *= wa23;
+        if (acol) {
+          const uint64_t pk = (uint64_t)((uint32_t)f2bf(dq01.x) | ((uint32_t)f2bf(dq01.y) << 16)) |
+                              ((uint64_t)((uint32_t)f2bf(dq23.x) | ((uint32_t)f2bf(dq23.y) << 16))
+                               << 32);
+          __hip_atomic_store(reinterpret_cast<uint64_t*>(dgn + (int64_t)(row0 + k) * ldg + f.G4 + a),
+                             pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  };
+  rows(0, ub);
+  if (vdiv > ATTF_RG * RB) {  // rows 16..31
+    u_batch(RB, ub);
+    rows(RB, ub);
+  }
+  wait_vmcnt<0>();  // this wave's dq stores are done
+  __syncthreads();
+  if (tid == 0)
+    __hip_atomic_fetch_add(f.flags + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // off the critical path: db_a, then dP / dw_a over the 4 row groups, 8
+  // frames per LDS round
+  if (tid == 0) {
+    float sb = 0.f;
+    for (int r = 0; r < vdiv; ++r)
+      for (int c = 0; c < C; ++c) sb += s_de[r * CP + c];
+    f.dba_part[b] += sb;
+  }
+  constexpr int RS = 8 * 4 + 4;  // LDS floats per (group, unit quad)
+#pragma unroll
+  for (int c0 = 0; c0 < CP; c0 += 8) {
+    if (rq > 0) {
+      float* sr = s_red + ((rq - 1) * 128 + cq) * RS;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        sr[4 * c] = dp[c0 + c][0].x;
+        sr[4 * c + 1] = dp[c0 + c][0].y;
+        sr[4 * c + 2] = dp[c0 + c][1].x;
+        sr[4 * c + 3] = dp[c0 + c][1].y;
+      }
+      if (c0 == 0) {
+        sr[32] = dw[0].x;
+        sr[33] = dw[0].y;
+        sr[34] = dw[1].x;
+        sr[35] = dw[1].y;
+      }
+    }
+    __syncthreads();
+    if (rq == 0 && acol) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (c0 + c < C) {
+          float4 v = make_float4(dp[c0 + c][0].x, dp[c0 + c][0].y, dp[c0 + c][1].x, dp[c0 + c][1].y);
+#pragma unroll
+          for (int g = 0; g < ATTF_RG - 1; ++g) {
+            const float* sr = s_red + (g * 128 + cq) * RS + 4 * c;
+            v.x += sr[0];
+            v.y += sr[1];
+            v.z += sr[2];
+            v.w += sr[3];
+          }
+          float4* dst = reinterpret_cast<float4*>(f.dP_acc + ((int64_t)b * C + c0 + c) * A + a);
+          const float4 o = *dst;
+          *dst = make_float4(o.x + wa4.x * v.x, o.y + wa4.y * v.y, o.z + wa4.z * v.z,
+                             o.w + wa4.w * v.w);
+        }
+      }
+      if (c0 == 0) {
+        float4 v = make_float4(dw[0].x, dw[0].y, dw[1].x, dw[1].y);
+#pragma unroll
+        for (int g = 0; g < ATTF_RG - 1; ++g) {
+          const float* sr = s_red + (g * 128 + cq) * RS + 32;
+          v.x += sr[0];
+          v.y += sr[1];
+          v.z += sr[2];
+          v.w += sr[3];
+        }
+        float4* dst = reinterpret_cast<float4*>(f.dwa_part + (int64_t)b * A + a);
+        const float4 o = *dst;
+        *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+      }
+    }
+    if (c0 + 8 < CP) __syncthreads();
+  }
+}
+
+// glds16 with a cache policy (aux 16 = sc1: the load bypasses the non-coherent
+// caches -- data written through by another workgroup of the launch)
+template <int AUX>
+__device__ __forceinline__ void glds16_aux(rsrc_t r, int voff, int soff, char* lds_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_base, 16, voff, soff, 0, AUX);
+}
+
+// Wait (one poll per wave) until the attention workgroups of videos
+// [v0, v0 + nv) released their dq rows.  They precede this workgroup in
+// dispatch order (lower blockIdx), so they are resident or done; the bound
+// only guarantees that every wave exits.
+__device__ __forceinline__ void att_fuse_wait(const int* flags, int v0, int nv) {
+  const int lane = threadIdx.x & 63;
+  for (int it = 0; it < (1 << 22); ++it) {
+    const int f = __hip_atomic_load(flags + v0 + min(lane, nv - 1), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+    if (__all(f > 0)) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// The step kernel's main loop with the fused attention's ordering: K-tiles
+// [0, ksplit) of the group from the primary offsets (dG_{t+1} columns, plain
+// loads), [ksplit, nk) from the tail offsets (dq_{t+1} columns) -- issued
+// only after att_fuse_wait, with sc1 (write-through data of this launch's
+// attention workgroups).  Otherwise as gemm_nt_mainloop_g.
+template <class TL, bool GATE>
+__device__ __forceinline__ void gemm_bwd_mainloop_tail(int tid, int nk, const DmaSrc<TL::BM / 32>& a,
+                                                       const DmaSrc<TL::BN / 32>& b, char* lds,
+                                                       f32x16 (&acc)[TL::TM][TL::TN],
+                                                       const int* flags, int v0, int nv) {
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+#pragma unroll
+  for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TL::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  bool waited = !GATE;
+  auto issue = [&](int buf, int kt) {
+    char* A = lds + buf * TL::STAGE_BYTES;
+    char* B = A + TL::A_BYTES;
+    if (kt < a.ksplit) {
+#pragma unroll
+      for (int i = 0; i < TL::BM / 32; ++i)
+        glds16(a.r0, a.voff0[i], kt * 128, A + 1024 * (w + 4 * i));
+#pragma unroll
+      for (int i = 0; i < TL::BN / 32; ++i)
+        glds16(b.r0, b.voff0[i], kt * 128, B + 1024 * (w + 4 * i));
+    } else {
+      if (!waited) {
+        att_fuse_wait(flags, v0, nv);
+        waited = true;
+      }
+      const int ks = (kt - a.ksplit) * 128;
+#pragma unroll
+      for (int i = 0; i < TL::BM / 32; ++i)
+        glds16_aux<GATE ? 16 : 0>(a.r1, a.voff1[i], ks, A + 1024 * (w + 4 * i));  // 16: sc1
+#pragma unroll
+      for (int i = 0; i < TL::BN / 32; ++i)
+        glds16(b.r1, b.voff1[i], ks, B + 1024 * (w + 4 * i));
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < TL::STAGES - 1; ++p)
+    if (p < nk) issue(p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (TL::STAGES > 2 && kt + 1 < nk) {
+      wait_vmcnt<TL::NI * (TL::STAGES - 2)>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + TL::STAGES - 1 < nk) issue((kt + TL::STAGES - 1) % TL::STAGES, kt + TL::STAGES - 1);
+    const char* A = lds + (kt % TL::STAGES) * TL::STAGE_BYTES;
+    const char* B = A + TL::A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + (lane >> 5);
+      bf16x8 af[TL::TM], bfr[TL::TN];
+#pragma unroll
+      for (int i = 0; i < TL::TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wr * TL::WM + i * 32 + (lane & 31), c));
+#pragma unroll
+      for (int j = 0; j < TL::TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(wc * TL::WN + j * 32 + (lane & 31), c));
+#pragma unroll
+      for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+}
+
+template <int BM, int STAGES, int GROUPS, bool ATT, int CP, bool FUSE = false>
 __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ dg_next, const uint16_t* __restrict__ whhT,
     const float* __restrict__ dh_logit, float* __restrict__ dc_carry,
@@ -254,7 +549,12 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
-  const int b = xcd_remap_l(blockIdx.x, n_tiles);
+  static_assert(!FUSE || ATT, "the fused attention backward extends the attention epilogue");
+  if (FUSE && (int)blockIdx.x < att.Bv) {  // step t + 1's attention backward (AttBwdEpi)
+    att_bwd_fused_wg<CP>(att, blockIdx.x, R, n_ut, const_cast<uint16_t*>(dg_next), KD, lds);
+    return;
+  }
+  const int b = xcd_remap_l((int)blockIdx.x - (FUSE ? att.Bv : 0), n_tiles);
   const int ut = b / n_rt, rt = b % n_rt;
   const int r0 = rt * BM, u0 = ut * 64;
   const int nk_all = dg_next != nullptr ? KD / 64 : 0;  // KD = 4H (+ A with attention)
@@ -272,7 +572,9 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
   static_assert(!ATT || (GROUPS == 2 && BM == 64), "attention epilogue: 2 groups of 64 rows");
   constexpr int SLICE = 64 * 4 * CP;  // bf16 per video slice
   int v0 = 0, nvs = 0;
-  uint4 gpf[ATT ? ATT_EPI_PF : 1];
+  // (a native vector type: an array of HIP's uint4 struct stayed a stack
+  // object -- scratch stores / loads around the main loop)
+  u32x4_t gpf[ATT ? ATT_EPI_PF : 1];
   if (ATT) {
     v0 = r0 / att.vdiv;
     nvs = min(r0 + BM, R) - 1 >= r0 ? (min(r0 + BM, R) - 1) / att.vdiv - v0 + 1 : 0;
@@ -280,13 +582,40 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     for (int k = 0; k < ATT_EPI_PF; ++k) {  // (unconditional loads, clamped)
       const int ch = tid + k * 256 * GROUPS, vj = min(ch / (SLICE / 8), nvs - 1),
                 o = ch % (SLICE / 8);
-      gpf[k] = reinterpret_cast<const uint4*>(
+      gpf[k] = reinterpret_cast<const u32x4_t*>(
           att.gvb16 + ((int64_t)(v0 + vj) * H + u0) * CP * 4)[o];
     }
   }
 
   f32x16 acc[TL::TM][TL::TN];
-  if (nkg > 0) {
+  if (FUSE && nkg > 0) {
+    // group g: dG_{t+1} tiles [g nkd / 2, (g + 1) nkd / 2), then dq_{t+1} tail
+    // tiles [nkd + g nka / 2, nkd + (g + 1) nka / 2)
+    const int lane = gtid & 63, w = gtid >> 6;
+    const int nkd = (KD - att.A) / 64, nka = att.A / 64;
+    DmaSrc<BM / 32> a;
+    DmaSrc<64 / 32> bsrc;
+    a.r0 = a.r1 = make_rsrc(dg_next, (int64_t)R * KD * 2);
+    a.ksplit = bsrc.ksplit = nkd / 2;
+#pragma unroll
+    for (int i = 0; i < BM / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      const int base = min(r0 + row, R - 1) * KD * 2 + dma_chunk(row, lane) * 16;
+      a.voff0[i] = base + grp * (nkd / 2) * 128;
+      a.voff1[i] = base + (nkd + grp * (nka / 2)) * 128;
+    }
+    bsrc.r0 = bsrc.r1 = make_rsrc(whhT, (int64_t)H * KD * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = dma_row(w, i, lane);
+      const int base = (u0 + row) * KD * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff0[i] = base + grp * (nkd / 2) * 128;
+      bsrc.voff1[i] = base + (nkd + grp * (nka / 2)) * 128;
+    }
+    gemm_bwd_mainloop_tail<TL, true>(gtid, nkd / 2 + nka / 2, a, bsrc,
+                                     lds + grp * TL::STAGES * TL::STAGE_BYTES, acc, att.flags, v0,
+                                     nvs);
+  } else if (nkg > 0) {
     const int lane = gtid & 63, w = gtid >> 6;
     DmaSrc<BM / 32> a;
     DmaSrc<64 / 32> bsrc;
@@ -328,7 +657,7 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
       const int ch = tid + k * 256 * GROUPS;
       if (ch < nvs * (SLICE / 8)) {
         const int uu = (ch % (SLICE / 8)) / NCH, c2 = ch % NCH;
-        reinterpret_cast<uint4*>(s_gv)[ch - c2 + (c2 ^ ((uu / SWD) & (NCH - 1)))] = gpf[k];
+        reinterpret_cast<u32x4_t*>(s_gv)[ch - c2 + (c2 ^ ((uu / SWD) & (NCH - 1)))] = gpf[k];
       }
     }
   }
@@ -395,7 +724,8 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
 
 int lstm_bwd_tiles(int R, int H) { return (H / 64) * ((R + 63) / 64); }
 
-template <int GROUPS, bool ATT = false, int CP = 8, int STAGES = LSTM_BWD_STAGES>
+template <int GROUPS, bool ATT = false, int CP = 8, bool FUSE = false,
+          int STAGES = LSTM_BWD_STAGES>
 static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT,
                                    const float* dh_logit, float* dc_carry, const uint16_t* gates,
                                    const float* c_t, const float* c_prev, int R, int H,
@@ -409,12 +739,13 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
                           : GROUPS * BM * TL::CSTRIDE * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP>,
+    (void)hipFuncSetAttribute((const void*)lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP, FUSE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  const int n = (H / 64) * ((R + BM - 1) / BM);
-  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP>), dim3(n),
+  // (fused: the attention workgroups first, blockIdx < Bv -- see att_fuse_wait)
+  const int n = (H / 64) * ((R + BM - 1) / BM) + (FUSE ? att.Bv : 0);
+  hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP, FUSE>), dim3(n),
                      dim3(256 * GROUPS), LDS, stream, dg_next, whhT, dh_logit, dc_carry, gates,
                      c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale, att, oh);
   post_launch("lstm_step_bwd_kernel", stream);
@@ -433,6 +764,21 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
     if ((KD / 64) % 2 != 0 || !att_bwd_epi_ok(att->vdiv, att->C, H) ||
         att->CP != (att->C <= 8 ? 8 : 16))
       throw std::runtime_error("lstm_step_bwd: unsupported attention epilogue shape");
+    if (att->flags != nullptr) {
+      if (dg_next == nullptr || !att_bwd_fuse_ok(att->vdiv, att->C, att->A, H, att->Bv, R) ||
+          KD != 4 * H + att->A || att->G4 != 4 * H || att->dal_next == nullptr ||
+          att->dal_next == att->dal_part)
+        throw std::runtime_error("lstm_step_bwd: unsupported fused attention backward");
+      if (att->CP == 8)
+        launch_lstm_step_bwd_g<2, true, 8, true>(dg_next, whhT, dh_logit, dc_carry, gates, c_t,
+                                                 c_prev, R, H, drop_p, rng, step, dG, KD, stream,
+                                                 cell, dh_scale, *att, oh);
+      else
+        launch_lstm_step_bwd_g<2, true, 16, true>(dg_next, whhT, dh_logit, dc_carry, gates, c_t,
+                                                  c_prev, R, H, drop_p, rng, step, dG, KD, stream,
+                                                  cell, dh_scale, *att, oh);
+      return;
+    }
     if (att->CP == 8)
       launch_lstm_step_bwd_g<2, true, 8>(dg_next, whhT, dh_logit, dc_carry, gates, c_t, c_prev,
                                          R, H, drop_p, rng, step, dG, KD, stream, cell, dh_scale,

@@ -125,6 +125,8 @@ struct AttMfmaArgs {
   float* q_out;          // nullable (R, A) fp32
   float* e_part;         // (Bv, A / 64, 32, CP) partial-score slots
   int* cnt;              // (Bv) tickets, zero at the first launch (re-armed by the kernel)
+  uint16_t* u_out;       // nullable (R, C, A) fp16 scorer values tanh(P + q) (training:
+                         // the fused attention backward reads them instead of recomputing)
 };
 // the MFMA attention path applies: rows per video 2..32, C <= 16, A % 64 == 0,
 // A <= 1024, H % 32 == 0, 64 <= H <= 512, the shared scorer (not per frame)
@@ -232,8 +234,26 @@ struct DhOneHot {
 struct AttBwdEpi {
   const uint16_t* gvb16;  // (Bv, H, CP, 4) bf16 gate tables, the 4 gates of a unit innermost
   int vdiv, C, CP;
-  float* dal_part;       // (H / 64, R, CP) fp32
+  float* dal_part;       // (H / 64, R, CP) fp32, this step's partials
+  // Attention backward of step t + 1 fused into step t's launch (flags != null):
+  // Bv extra workgroups, dispatched first (blockIdx < Bv), turn step t + 1's
+  // dalpha partials (dal_next) into dq_{t+1} (bf16, written through into the
+  // tail columns [G4, G4 + A) of dg_next, the launch's own A operand) and
+  // accumulate dP / dw_a / db_a; each then bumps flags[video].  The GEMM
+  // workgroups stream the dG_{t+1} columns first and wait for their videos'
+  // flags only before the tail K-tiles (lstm.hip).
+  int* flags;             // (Bv) int32, zero before the launch (per step)
+  const float* dal_next;  // (H / 64, R, CP): step t + 1's partials (other buffer)
+  const float* alpha;     // (R, C) of step t + 1
+  const uint16_t* u;      // (R, C, A) fp16 tanh(P + q) of step t + 1 (AttMfmaArgs::u_out)
+  const float* wa;        // (A)
+  int Bv, A, G4;
+  float* dP_acc;    // (Bv, C, A)
+  float* dwa_part;  // (Bv, A)
+  float* dba_part;  // (Bv)
 };
+// fused attention backward (AttBwdEpi::flags) supported for this shape
+bool att_bwd_fuse_ok(int vdiv, int C, int A, int H, int Bv, int R);
 bool att_bwd_epi_ok(int vdiv, int C, int H);
 void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const float* dh_logit,
                           float* dc_carry, const uint16_t* gates, const float* c_t,

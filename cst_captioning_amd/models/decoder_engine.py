@@ -188,9 +188,9 @@ class _DecoderFn(torch.autograd.Function):
             ctx.saved = (lse, *outs[4:9], seq, labels, bos, xw)
             if ctx.store_exp and eng.x_after_rollout and xw.numel() == 0:
                 eng._x_pending = ctx  # launch_x computes X = E W for this forward
-            if has_att:  # Gv, P, W_q, w_a, alpha_all, q_all
-                ctx.att_saved = (att[0], att[1], att[2], att[3], outs[9], outs[10])
-            ctx.up_saved = outs[11 if has_att else 9:]  # (h, c, gates, hd_in) per upper layer
+            if has_att:  # Gv, P, W_q, w_a, alpha_all, q_all, u_all (fp16 scorer values)
+                ctx.att_saved = (att[0], att[1], att[2], att[3], outs[9], outs[10], outs[11])
+            ctx.up_saved = outs[12 if has_att else 9:]  # (h, c, gates, hd_in) per upper layer
         else:
             ctx.saved = None
         ctx.att_shapes = (att_wa.shape, att_ba.shape) if has_att else None

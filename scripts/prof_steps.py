@@ -7,7 +7,11 @@ end (``cst::adam_update_kernel``): the window is (end of the (N+1)-th last
 delimiter, end of the last delimiter].  Run the bench with ``--att8 0
 --beam5 0`` so nothing follows the timed steps.
 
-usage: prof_steps.py TRACE.csv N [ROWS] [DELIM]
+usage: prof_steps.py TRACE.csv N [ROWS] [DELIM] [SEQ]
+
+SEQ: '|'-separated kernel-name substrings; the last step's launches of those
+kernels are listed in order (start offset from the step start, duration, gap
+to the previous listed launch's end).
 """
 import collections
 import csv
@@ -40,6 +44,18 @@ def main():
     for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1]))[:rows_out]:
         print('%-62s %8s %6.1f %9.1f %10.1f' % (k[0], k[1], len(v) / n, sum(v) / len(v),
                                                  sum(v) / n))
+    if len(sys.argv) > 5:
+        pats = sys.argv[5].split('|')
+        step = [r for r in win if ends[-2] < r['s'] <= hi]
+        t0, prev = step[0]['s'], None
+        print('last step, launches matching %s:' % sys.argv[5])
+        print('%10s %9s %9s  %s' % ('start us', 'dur us', 'gap us', 'kernel'))
+        for r in step:
+            if any(p in r['Kernel_Name'] for p in pats):
+                gap = (r['s'] - prev) / 1e3 if prev is not None else 0.0
+                print('%10.1f %9.1f %9.1f  %s' % ((r['s'] - t0) / 1e3, (r['e'] - r['s']) / 1e3, gap,
+                                                  r['Kernel_Name'][:70]))
+                prev = r['e']
 
 
 if __name__ == '__main__':
