@@ -672,12 +672,20 @@ class DecoderEngine:
         parameters (W_q, w_a, b_a) as autograd inputs of the Function."""
         if self.manet:
             return self._manet_inputs(model, feats)
-        frames = self._encode(model, feats)  # (B, C, F*H), FeatPool dropout in train mode
         ta = model.temporal_att
+        from ..ops.featpool import att_inputs, fused_ok
+        if fused_ok(model.feat_pool, feats) and feats[0].dim() == 3:
+            # one node: FeatPool + one bf16 GEMM for Gv and P (ops/featpool.py;
+            # att8 4.597 / 4.584 vs 4.776 / 4.780 ms per step with the two fp32
+            # Linears below and their autograd backward, profiles/r5/README_r5.md)
+            gv, pre = att_inputs(self, model, feats)
+            return (gv, pre, ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), gv.size(0)
+        frames = self._encode(model, feats)  # (B, C, F*H), FeatPool dropout in train mode
         w_iv = model.core.rnn.weight_ih_l0[:, self.E:]
-        # (fp32 GEMMs: under bf16 autocast the projected frames' bias gradient
-        # drifted to 8.8 % of the fp32 reference at H = 64,
-        # tests/test_gpu_attention.py)
+        # (fp32 GEMMs here: under bf16 autocast -- bf16 gradients too -- the
+        # projected frames' bias gradient drifted to 8.8 % of the fp32
+        # reference at H = 64, tests/test_gpu_attention.py; the fused node
+        # keeps the gradients fp32 and rounds only the GEMM operands)
         gv = self.pack_rows(F.linear(frames, w_iv), self.src_ie, 2)
         pre = ta.precompute(frames)
         return (gv, pre, ta.f_h.weight, ta.align.weight.view(-1), ta.align.bias), frames.size(0)

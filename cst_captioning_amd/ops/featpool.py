@@ -95,6 +95,88 @@ class _FeatPoolVgateFn(torch.autograd.Function):
         return (None,) * (4 + nf) + tuple(g[:nf]) + tuple(g[nf:]) + (d_wih,)
 
 
+class _AttInputsFn(torch.autograd.Function):
+    """Temporal attention's per-batch operands in one node: FeatPool over the
+    C frames, then ONE bf16 GEMM (fp32 accumulate) against the stacked weight
+    ``[W_ih[:, E:]; W_f]`` for the per-frame gate table ``Gv = pack(frames .
+    W_iv^T)`` and the projected frames ``P = frames . W_f^T + b_f``
+    (reference: ``/root/reference/model.py:119-142``; the module computes them
+    as two fp32 Linears).  Backward: ``dframes = [dGv | dP] . [W_iv; W_f]``
+    and ``[dW_iv; dW_f] = [dGv | dP]^T . frames`` as one bf16 GEMM each; W_ih's
+    video columns and the FeatPool parameters are written straight into their
+    gradient-bucket slots when the trainer registered them (as
+    :class:`_FeatPoolVgateFn`), else returned."""
+
+    @staticmethod
+    def forward(ctx, eng, p, rng, nf, C, *args):
+        xs, ws, bs = args[:nf], args[nf:2 * nf], args[2 * nf:3 * nf]
+        w_ih, wf, bf = args[3 * nf:3 * nf + 3]
+        wsd = [w.detach() for w in ws]
+        fc = _ext.ops().featpool_forward(list(xs), wsd, [b.detach() for b in bs], p, rng)
+        E, G4, A = eng.E, w_ih.size(0), wf.size(0)
+        wcat = torch.empty(G4 + A, fc.size(1), dtype=torch.bfloat16, device=fc.device)
+        wcat[:G4].copy_(w_ih.detach()[:, E:])
+        wcat[G4:].copy_(wf.detach())
+        fc16 = fc.to(torch.bfloat16)
+        y = torch.mm(fc16, wcat.t(), out_dtype=torch.float32)  # (N * C, 4H + A)
+        B = xs[0].size(0) // C
+        gv = eng.pack_rows(y[:, :G4], eng.src_ie, 1).view(B, C, -1)
+        pre = (y[:, G4:] + bf.detach()).view(B, C, A)
+        ctx.eng, ctx.p, ctx.nf, ctx.wih_shape, ctx.G4 = eng, p, nf, w_ih.shape, G4
+        ctx.save_for_backward(fc, fc16, wcat, *xs, *wsd)
+        return gv, pre
+
+    @staticmethod
+    def backward(ctx, dgv, dpre):
+        eng, nf, G4 = ctx.eng, ctx.nf, ctx.G4
+        fc, fc16, wcat, *rest = ctx.saved_tensors
+        xs, ws = list(rest[:nf]), list(rest[nf:])
+        E, N = eng.E, fc.size(0)
+        A = wcat.size(0) - G4
+        dy = torch.empty(N, G4 + A, dtype=torch.bfloat16, device=fc.device)
+        if dgv is not None:
+            dy[:, :G4].copy_(dgv.reshape(N, -1).index_select(1, eng.dst_ie))  # PyTorch gate order
+        else:
+            dy[:, :G4].zero_()
+        if dpre is not None:
+            dpre = dpre.reshape(N, A)
+            dy[:, G4:].copy_(dpre)
+            dbf = dpre.sum(0)
+        else:
+            dy[:, G4:].zero_()
+            dbf = None
+        dfc = torch.mm(dy, wcat, out_dtype=torch.float32)
+        direct = eng.take_video_slots()
+        dyt = dy.t()
+        dwf = torch.mm(dyt[G4:], fc16, out_dtype=torch.float32)
+        if direct is not None:  # the decoder backward wrote W_ih's token columns
+            torch.mm(dyt[:G4], fc16, out_dtype=torch.float32, out=direct['wih'][:, E:])
+            outs = [direct['fp_w%d' % f] for f in range(nf)] + \
+                   [direct['fp_b%d' % f] for f in range(nf)]
+            _ext.ops().featpool_backward(dfc, fc, xs, ws, ctx.p, outs)
+            return (None,) * (5 + 3 * nf) + (None, dwf, dbf)
+        d_wih = fc.new_zeros(ctx.wih_shape)
+        d_wih[:, E:] = torch.mm(dyt[:G4], fc16, out_dtype=torch.float32)
+        g = _ext.ops().featpool_backward(dfc, fc, xs, ws, ctx.p, [])
+        return (None,) * (5 + nf) + tuple(g[:nf]) + tuple(g[nf:]) + (d_wih, dwf, dbf)
+
+
+def att_inputs(eng, model, feats):
+    """Temporal attention operands (Gv (B, C, 4H) packed, P (B, C, A)) of the
+    fused engine through :class:`_AttInputsFn` (train-mode FeatPool dropout as
+    the module's)."""
+    pool = model.feat_pool
+    lins = [m[0] for m in pool.feat_list]
+    p = float(pool.feat_list[0][2].p) if pool.training else 0.0
+    dev = feats[0].device
+    rng = _seeds(p, dev)
+    xs = [_rows(f) for f in feats]
+    ta = model.temporal_att
+    return _AttInputsFn.apply(eng, p, rng, len(xs), feats[0].size(1), *xs, *[l.weight for l in lins],
+                              *[l.bias for l in lins], model.core.rnn.weight_ih_l0,
+                              ta.f_feat.weight, ta.f_feat.bias)
+
+
 # Tests may pin the dropout seeds: a callable dev -> int32[2] device tensor
 # (graph-vs-eager equivalence, tests/test_gpu_graph.py).  None = a fresh
 # on-device draw per pass (graph-safe).
