@@ -287,36 +287,84 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
     }
 }
 
-// Fused beam step (one 256-thread workgroup per video, beam size K <= 8),
+// Fused beam step (one 512-thread workgroup per video, beam size K <= 8),
 // replacing combine + candidate top-K + beam step + LSTM step (4 launches):
-//   A. each of the video's K rows (one wavefront per row): the LSE from the
-//      vocab launch's tile partials and the row's K best log-probs from its
+//   0. prefetch of everything that does not depend on this step's selection:
+//      the cell operands of the video's K current rows for this thread's
+//      hidden units (pre = h_t W_hh^T + video gates, computed by the
+//      recurrent tiles of the vocab launch; c_t) and the K history rows (LDS);
+//   A. wavefront q < K, row q of the video: its candidate and partial loads
+//      are issued together (one round trip), then the LSE from the vocab
+//      launch's tile partials and the row's K best log-probs from its
 //      n_vt x K tile candidates (VF_TOPK), into LDS;
-//   B. the reference's selection / fork / harvest (beam_step_kernel's rules);
+//   B. the reference's selection / fork / harvest (beam_step_kernel's rules),
+//      the new history rows written from LDS;
 //   C. the next step's LSTM cell for the K new beams: gates = pre[parent] +
-//      P[token] (pre = h_t W_hh^T + video gates of ALL current rows, computed
-//      by the recurrent tiles of the vocab launch, so a new beam reads its
-//      parent's row), c from the parent's c -> h (bf16), c.
+//      P[token] (the only gather left after the selection), c from the
+//      parent's c -> h (bf16), c; the parent's operands are picked from the
+//      prefetched registers by unrolled selects (no dynamic register index).
 // Per decode step: this launch + the vocab launch (which also carries the
-// next step's recurrent GEMM).
-__global__ __launch_bounds__(256) void beam_fused_step_kernel(BeamFusedArgs a, int t) {
-  __shared__ float s_tv[BEAM_MAXK * BEAM_MAXK];
-  __shared__ int s_ti[BEAM_MAXK * BEAM_MAXK];
-  __shared__ float s_p[BEAM_MAXK * BEAM_MAXK];
-  __shared__ int s_sel[BEAM_MAXK];
-  __shared__ float s_sum_old[BEAM_MAXK];
+// next step's recurrent GEMM).  (The 256-thread form with per-phase loads --
+// two rows per wavefront, two candidate batches, cell operands loaded after
+// the selection -- was ~10 dependent memory round trips per step: 30.4 us,
+// profiles/r5/steps_head_beam.txt.)
+constexpr int BF_THREADS = 512, BF_MAXK = 8, BF_MAXC = 12, BF_MAXP = 2, BF_MAXT = 64;
+template <int UPT>
+__global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedArgs a, int t) {
+  __shared__ float s_tv[BF_MAXK * BF_MAXK];
+  __shared__ int s_ti[BF_MAXK * BF_MAXK];
+  __shared__ float s_p[BF_MAXK * BF_MAXK];
+  __shared__ int s_sel[BF_MAXK];
+  __shared__ float s_sum_old[BF_MAXK];
   __shared__ int s_win;
+  __shared__ int64_t s_sh[BF_MAXK * BF_MAXT];
+  __shared__ float s_lh[BF_MAXK * BF_MAXT];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int K = a.K, R = a.R, T = a.T, n_vt = a.n_vt;
-  // -- A. per-row LSE and top-K ---------------------------------------------------
-  for (int q = w; q < K; q += 4) {
-    const int r = b * K + q;
+  const int K = a.K, R = a.R, T = a.T, n_vt = a.n_vt, H = a.H;
+  const int rows = t == 1 ? 1 : K;
+  // -- 0. prefetch ------------------------------------------------------------------
+  const bool cell = a.pre != nullptr;
+  float4 ppre[BF_MAXK][UPT];
+  float pc[BF_MAXK][UPT];
+  if (cell) {
+#pragma unroll
+    for (int q = 0; q < BF_MAXK; ++q)
+#pragma unroll
+      for (int j = 0; j < UPT; ++j) {
+        const int u = min(tid + BF_THREADS * j, H - 1);
+        const int64_t r = (int64_t)b * K + min(q, K - 1);
+        ppre[q][j] = *reinterpret_cast<const float4*>(a.pre + r * 4 * H + 4 * u);
+        pc[q][j] = a.c_in[r * H + u];
+      }
+  }
+  const int64_t* sh_old = a.seq_hist + (int64_t)((t + 1) & 1) * R * T;
+  const float* lh_old = a.lp_hist + (int64_t)((t + 1) & 1) * R * T;
+  for (int e = tid; e < K * T; e += BF_THREADS) {
+    s_sh[e] = sh_old[(int64_t)b * K * T + e];
+    s_lh[e] = lh_old[(int64_t)b * K * T + e];
+  }
+  // -- A. per-row LSE and top-K, one wavefront per row -------------------------------
+  if (w < K) {
+    const int r = b * K + w, n = n_vt * K;
+    float2 xs[BF_MAXC];
+#pragma unroll
+    for (int i = 0; i < BF_MAXC; ++i) {  // (clamped, masked below)
+      const int c = min(lane + 64 * i, n - 1);
+      xs[i] = a.cand[((int64_t)(c / K) * R + r) * K + c % K];
+    }
+    float2 pp[BF_MAXP];
+#pragma unroll
+    for (int i = 0; i < BF_MAXP; ++i)
+      pp[i] = *reinterpret_cast<const float2*>(a.part + (int64_t)min(lane + 64 * i, n_vt - 1) * R + r);
     float m = -INFINITY, sm = 0.f;
-    for (int vt = lane; vt < n_vt; vt += 64) {
-      const VocabPartial p = a.part[(int64_t)vt * R + r];
-      const float M = fmaxf(m, p.m);
-      sm = (m == -INFINITY ? 0.f : sm * __expf(m - M)) + (p.m == -INFINITY ? 0.f : p.s * __expf(p.m - M));
-      m = M;
+#pragma unroll
+    for (int i = 0; i < BF_MAXP; ++i) {
+      if (lane + 64 * i < n_vt) {
+        const float pm = pp[i].x, ps = pp[i].y;
+        const float M = fmaxf(m, pm);
+        sm = (m == -INFINITY ? 0.f : sm * __expf(m - M)) + (pm == -INFINITY ? 0.f : ps * __expf(pm - M));
+        m = M;
+      }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -326,38 +374,28 @@ __global__ __launch_bounds__(256) void beam_fused_step_kernel(BeamFusedArgs a, i
       m = M;
     }
     const float L = m + __logf(sm);
-    constexpr int MK = 8;
-    float bv[MK];
-    int bi[MK];
+    float bv[BF_MAXK];
+    int bi[BF_MAXK];
 #pragma unroll
-    for (int k = 0; k < MK; ++k) bv[k] = -INFINITY, bi[k] = 0x7fffffff;
-    const int n = n_vt * K;
+    for (int k = 0; k < BF_MAXK; ++k) bv[k] = -INFINITY, bi[k] = 0x7fffffff;
     float thr = -INFINITY;
-    for (int c0 = lane; c0 < n; c0 += 64 * 4) {
-      float2 xs[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = c0 + 64 * u;
-        xs[u] = c < n ? a.cand[((int64_t)(c / K) * R + r) * K + c % K]
-                      : make_float2(-INFINITY, __int_as_float(0x7fffffff));
-      }
+    for (int i = 0; i < BF_MAXC; ++i) {
+      const bool ok = lane + 64 * i < n;
+      float cv = ok ? xs[i].x : -INFINITY;
+      int ci = ok ? __float_as_int(xs[i].y) : 0x7fffffff;
+      if (!(cv > thr || (cv == thr && ci < 0x7fffffff))) continue;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float cv = xs[u].x;
-        int ci = __float_as_int(xs[u].y);
-        if (!(cv > thr || (cv == thr && ci < 0x7fffffff))) continue;
-#pragma unroll
-        for (int p = 0; p < MK; ++p) {
-          if (p < K && (cv > bv[p] || (cv == bv[p] && ci < bi[p]))) {
-            const float tv = bv[p];
-            const int tix = bi[p];
-            bv[p] = cv, bi[p] = ci;
-            cv = tv, ci = tix;
-          }
+      for (int p = 0; p < BF_MAXK; ++p) {
+        if (p < K && (cv > bv[p] || (cv == bv[p] && ci < bi[p]))) {
+          const float tv = bv[p];
+          const int tix = bi[p];
+          bv[p] = cv, bi[p] = ci;
+          cv = tv, ci = tix;
         }
-#pragma unroll
-        for (int p = 0; p < MK; ++p) thr = p == K - 1 ? bv[p] : thr;
       }
+#pragma unroll
+      for (int p = 0; p < BF_MAXK; ++p) thr = p == K - 1 ? bv[p] : thr;
     }
     for (int k = 0; k < K; ++k) {
       float best = bv[0];
@@ -365,16 +403,15 @@ __global__ __launch_bounds__(256) void beam_fused_step_kernel(BeamFusedArgs a, i
       wave_argmax(best, besti);
       if (bi[0] == besti) {
 #pragma unroll
-        for (int p = 0; p + 1 < MK; ++p) bv[p] = bv[p + 1], bi[p] = bi[p + 1];
-        bv[MK - 1] = -INFINITY, bi[MK - 1] = 0x7fffffff;
+        for (int p = 0; p + 1 < BF_MAXK; ++p) bv[p] = bv[p + 1], bi[p] = bi[p + 1];
+        bv[BF_MAXK - 1] = -INFINITY, bi[BF_MAXK - 1] = 0x7fffffff;
       }
-      if (lane == 0) s_tv[q * K + k] = best - L, s_ti[q * K + k] = besti;
+      if (lane == 0) s_tv[w * K + k] = best - L, s_ti[w * K + k] = besti;
     }
   }
   if (tid < K) s_sum_old[tid] = a.beam_sum[b * K + tid];
   __syncthreads();
   // -- B. selection (beam_step_kernel's rules), every thread at the barriers ------
-  const int rows = t == 1 ? 1 : K;
   const int ncand = rows * K;
   if (tid < ncand) {
     const int c = tid / rows, q = tid % rows;
@@ -396,24 +433,14 @@ __global__ __launch_bounds__(256) void beam_fused_step_kernel(BeamFusedArgs a, i
     }
     __syncthreads();
   }
-  const int64_t* sh_old = a.seq_hist + (int64_t)((t + 1) & 1) * R * T;
-  const float* lh_old = a.lp_hist + (int64_t)((t + 1) & 1) * R * T;
   int64_t* sh_new = a.seq_hist + (int64_t)(t & 1) * R * T;
   float* lh_new = a.lp_hist + (int64_t)(t & 1) * R * T;
-  for (int e = tid; e < K * T; e += 256) {
+  for (int e = tid; e < K * T; e += BF_THREADS) {
     const int v = e / T, pos = e % T;
     const int j = s_sel[v], c = j / rows, q = j % rows;
-    const int64_t src = (int64_t)(b * K + q) * T + pos, dst = (int64_t)(b * K + v) * T + pos;
-    if (pos < t - 1) {
-      sh_new[dst] = sh_old[src];
-      lh_new[dst] = lh_old[src];
-    } else if (pos == t - 1) {
-      sh_new[dst] = s_ti[q * K + c];
-      lh_new[dst] = s_tv[q * K + c];
-    } else {
-      sh_new[dst] = 0;
-      lh_new[dst] = 0.f;
-    }
+    const int64_t dst = (int64_t)(b * K + v) * T + pos;
+    sh_new[dst] = pos < t - 1 ? s_sh[q * T + pos] : (pos == t - 1 ? (int64_t)s_ti[q * K + c] : 0);
+    lh_new[dst] = pos < t - 1 ? s_lh[q * T + pos] : (pos == t - 1 ? s_tv[q * K + c] : 0.f);
   }
   if (tid < K) {
     const int v = tid, j = s_sel[v], c = j / rows, q = j % rows;
@@ -433,50 +460,63 @@ __global__ __launch_bounds__(256) void beam_fused_step_kernel(BeamFusedArgs a, i
     if (win >= 0) a.best_ppl[b] = bp;
     s_win = win;
   }
-  __syncthreads();  // (the history stores above precede the harvest copy)
+  __syncthreads();
   const int win = s_win;
-  if (win >= 0)
-    for (int pos = tid; pos < T; pos += 256) {
-      a.best_seq[(int64_t)b * T + pos] = sh_new[(int64_t)(b * K + win) * T + pos];
-      a.best_lp[(int64_t)b * T + pos] = lh_new[(int64_t)(b * K + win) * T + pos];
+  if (win >= 0) {  // the winner's new row, formed from LDS like the history rows
+    const int j = s_sel[win], c = j / rows, q = j % rows;
+    for (int pos = tid; pos < T; pos += BF_THREADS) {
+      a.best_seq[(int64_t)b * T + pos] =
+          pos < t - 1 ? s_sh[q * T + pos] : (pos == t - 1 ? (int64_t)s_ti[q * K + c] : 0);
+      a.best_lp[(int64_t)b * T + pos] =
+          pos < t - 1 ? s_lh[q * T + pos] : (pos == t - 1 ? s_tv[q * K + c] : 0.f);
     }
-  if (a.pre == nullptr) return;
+  }
+  if (!cell) return;
   // -- C. the next step's cell for the K new beams ---------------------------------
-  // batches of CB elements per thread: every load of a batch is issued before
-  // the first store (the stores could alias the inputs as far as the compiler
-  // knows, which would serialise the loads: one round trip per element)
-  const int H = a.H, n = K * H;
-  constexpr int CB = 8;
-  for (int e0 = tid; e0 < n; e0 += 256 * CB) {
-    float4 pv[CB], xv[CB];
-    float cv[CB];
-    int64_t ob[CB];
+  float4 xv[BF_MAXK][UPT];
+  int par[BF_MAXK];
 #pragma unroll
-    for (int k = 0; k < CB; ++k) {
-      const int e = min(e0 + 256 * k, n - 1);  // (clamped: no branch around the loads)
-      const int v = e / H, u = e % H;
-      const int j = s_sel[v], c = j / rows, q = j % rows;
-      const int pr = b * K + q, tk = s_ti[q * K + c];
-      pv[k] = *reinterpret_cast<const float4*>(a.pre + (int64_t)pr * 4 * H + 4 * u);
-      xv[k] = *reinterpret_cast<const float4*>(a.ptab + (int64_t)tk * 4 * H + 4 * u);
-      cv[k] = a.c_in[(int64_t)pr * H + u];
-      ob[k] = (int64_t)(b * K + v) * H + u;
+  for (int v = 0; v < BF_MAXK; ++v) {  // the token-table rows: all gathers out at once
+    const int vv = min(v, K - 1), j = s_sel[vv], c = j / rows, q = j % rows;
+    par[v] = q;
+    const int64_t tk = s_ti[q * K + c];
+#pragma unroll
+    for (int jj = 0; jj < UPT; ++jj) {
+      const int u = min(tid + BF_THREADS * jj, H - 1);
+      xv[v][jj] = *reinterpret_cast<const float4*>(a.ptab + tk * 4 * H + 4 * u);
     }
+  }
 #pragma unroll
-    for (int k = 0; k < CB; ++k) {
-      if (e0 + 256 * k < n) {
-        const CellFwd cf = cell_fwd(a.cell, pv[k].x + xv[k].x, pv[k].y + xv[k].y,
-                                    pv[k].z + xv[k].z, pv[k].w + xv[k].w, cv[k]);
-        a.c_out[ob[k]] = cf.c;
-        a.h_out[ob[k]] = f2bf(cf.h);
+  for (int v = 0; v < BF_MAXK; ++v) {
+    if (v < K) {
+#pragma unroll
+      for (int jj = 0; jj < UPT; ++jj) {
+        const int u = tid + BF_THREADS * jj;
+        if (u < H) {
+          float4 pv = ppre[0][jj];
+          float cv = pc[0][jj];
+#pragma unroll
+          for (int q = 1; q < BF_MAXK; ++q)
+            if (par[v] == q) pv = ppre[q][jj], cv = pc[q][jj];
+          const CellFwd cf = cell_fwd(a.cell, pv.x + xv[v][jj].x, pv.y + xv[v][jj].y,
+                                      pv.z + xv[v][jj].z, pv.w + xv[v][jj].w, cv);
+          const int64_t o = (int64_t)(b * K + v) * H + u;
+          a.c_out[o] = cf.c;
+          a.h_out[o] = f2bf(cf.h);
+        }
       }
     }
   }
 }
 
 void launch_beam_fused_step(const BeamFusedArgs& a, int t, hipStream_t stream) {
-  if (a.K < 1 || a.K > 8) throw std::runtime_error("beam_fused_step: K must be in [1, 8]");
-  hipLaunchKernelGGL(beam_fused_step_kernel, dim3(a.B), dim3(256), 0, stream, a, t);
+  if (a.K < 1 || a.K > BF_MAXK || a.T > BF_MAXT || a.n_vt > 64 * BF_MAXP ||
+      a.n_vt * a.K > 64 * BF_MAXC || (a.pre != nullptr && a.H > 2 * BF_THREADS))
+    throw std::runtime_error("beam_fused_step: K <= 8, T <= 64, n_vt <= 128, n_vt K <= 768, H <= 1024");
+  if (a.pre == nullptr || a.H <= BF_THREADS)
+    hipLaunchKernelGGL(beam_fused_step_kernel<1>, dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
+  else
+    hipLaunchKernelGGL(beam_fused_step_kernel<2>, dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
   post_launch("beam_fused_step_kernel", stream);
 }
 
