@@ -110,6 +110,56 @@ __device__ __forceinline__ void shadow_store(const ShadowSegs& ss, int64_t e, fl
   }
 }
 
+// The 4 consecutive parameters [e0, e0 + 4) of one float4 of the update: per
+// segment one range test; a float4 inside one segment (the common case) takes
+// one int32 row division and 4 contiguous bf16 stores (the per-element path
+// cost a 64-bit division and a segment scan per parameter: VALU-bound
+// update pass); float4s straddling a segment or row boundary fall back.
+__device__ __forceinline__ void shadow_store4(const ShadowSegs& ss, int64_t e0, const float4& v) {
+  const float vals[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < SHADOW_MAX_SEGS; ++k) {
+    if (k >= ss.n) break;
+    const ShadowSeg& g = ss.s[k];
+    const int64_t j0 = e0 - g.off;
+    if (j0 < -3 || j0 >= g.n) continue;  // no overlap
+    if (j0 < 0 || j0 + 3 >= g.n) {       // partial overlap: per parameter
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (j0 + q >= 0 && j0 + q < g.n) shadow_store(ss, e0 + q, vals[q]);
+      continue;
+    }
+    if (g.kind == SHADOW_PLAIN) {
+      uint16_t* d = g.dst + j0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = f2bf(vals[q]);
+      continue;
+    }
+    const int jj = (int)j0, row = jj / g.cols, col = jj - row * g.cols;
+    if (col + 3 >= g.cols) {  // crosses a source row
+#pragma unroll
+      for (int q = 0; q < 4; ++q) shadow_store(ss, e0 + q, vals[q]);
+      continue;
+    }
+    const int64_t pr = packed_gate_row(row, g.H, g.slots);
+    if (g.kind == SHADOW_GATES_IH) {
+      uint16_t* d = g.dst + pr * (g.E + g.H) + col;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (col + q < g.E) d[q] = f2bf(vals[q]);
+    } else {  // SHADOW_GATES_HH
+      uint16_t* d = g.dst + pr * (g.E + g.H) + g.E + col;
+      uint16_t* d2 = g.dst2 + pr * g.ld2 + col;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint16_t bq = f2bf(vals[q]);
+        d[q] = bq;
+        d2[q] = bq;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* __restrict__ p,
                                                              ShadowSegs ss, int seg) {
   const ShadowSeg& g = ss.s[seg];
@@ -172,12 +222,7 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_update_kernel(
     p4[i] = pp;
     m4[i] = mm;
     v4[i] = vv;
-    if (ss.n > 0) {
-      shadow_store(ss, 4 * i, pp.x);
-      shadow_store(ss, 4 * i + 1, pp.y);
-      shadow_store(ss, 4 * i + 2, pp.z);
-      shadow_store(ss, 4 * i + 3, pp.w);
-    }
+    if (ss.n > 0) shadow_store4(ss, 4 * i, pp);
   }
   if (blockIdx.x == 0) {
     for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += ADAM_THREADS) {
