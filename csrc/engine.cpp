@@ -977,6 +977,25 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                         dpre_part.data_ptr<float>(), dwa_part.data_ptr<float>(),
                         dba_part.data_ptr<float>(), st);
   stamp(STAMP_BWD_LOOP, st);
+  // attention: the per-frame gate-table gradient dGv needs only the finished
+  // dG rows; it runs on the second side stream under the post-loop chain
+  // below (joined before the results are returned).  (Its tensors live at
+  // function scope: allocated on the main stream, which waits for them.)
+  at::Tensor dgv_part, dGv_side;
+  if (has_att && C <= 8) {
+    dgv_part = at::empty({att_dgv_chunks((int)n_steps), Bv, C, H4}, f32);
+    dGv_side = at::empty({Bv, C, H4}, f32);
+    (void)hipEventRecord(aux.ev[1], st);
+    (void)hipStreamWaitEvent(side2.stream(), aux.ev[1], 0);
+    launch_att_dgv(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)KD,
+                   a_alpha.data_ptr<float>(), (int)n_steps, (int)R, (int)Bv, (int)vdiv, (int)C,
+                   (int)H4, dgv_part.data_ptr<float>(), side2.stream());
+    {
+      c10::hip::HIPStreamGuard guard(side2);
+      at::sum_out(dGv_side, dgv_part, 0);
+    }
+    (void)hipEventRecord(aux.ev[5], side2.stream());
+  }
   at::Tensor dvg;
   if (!has_att) {
     TORCH_CHECK(vgate_div >= 1 && R % vgate_div == 0, "vgate_div must divide the rows");
@@ -1073,12 +1092,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r] (kernels/attention.hip:
     // one pass over the bf16 dG rows, partials per step chunk)
     at::Tensor dGv;
-    if (C <= 8) {
-      at::Tensor part = at::empty({att_dgv_chunks((int)n_steps), Bv, C, H4}, f32);
-      launch_att_dgv(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), (int)KD,
-                     a_alpha.data_ptr<float>(), (int)n_steps, (int)R, (int)Bv, (int)vdiv, (int)C,
-                     (int)H4, part.data_ptr<float>(), st);
-      dGv = part.sum(0);
+    if (C <= 8) {  // (computed on the side stream after the loop)
+      (void)hipStreamWaitEvent(st, aux.ev[5], 0);
+      dGv = dGv_side;
     } else {  // one batched GEMM per (step, video), K = rows per video
       at::Tensor al = a_alpha.to(at::kBFloat16).view({n_steps * Bv, vdiv, C}).transpose(1, 2);
       at::Tensor dgv = dG_all.view({n_steps * Bv, vdiv, KD}).narrow(2, 0, H4);
