@@ -1000,6 +1000,15 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   if (!has_att) {
     TORCH_CHECK(vgate_div >= 1 && R % vgate_div == 0, "vgate_div must divide the rows");
     dvg = at::empty({R / vgate_div, H4}, f32);
+    // (Bv, 4H): sum over time and over the rows of each video in one pass
+    // (kernels/embed_grad.hip), streaming the finished dG rows on the second
+    // side stream under the post-loop GEMM chain (joined before returning)
+    (void)hipEventRecord(aux.ev[1], st);
+    (void)hipStreamWaitEvent(side2.stream(), aux.ev[1], 0);
+    launch_video_gate_grad(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), KD,
+                           (int)n_steps, (int)R, (int)vgate_div, (int)H4, dvg.data_ptr<float>(),
+                           side2.stream());
+    (void)hipEventRecord(aux.ev[5], side2.stream());
   }
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
   at::Tensor dG2 = dGx.narrow(1, 0, H4);
@@ -1083,11 +1092,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);
   std::vector<at::Tensor> res;
   if (!has_att) {
-    // (Bv, 4H): sum over time and over the rows of each video in one pass
-    // (kernels/embed_grad.hip; was a (R, 4H) sum over time, 78 us, plus a
-    // per-video sum in Python)
-    launch_video_gate_grad(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), KD,
-                           (int)n_steps, (int)R, (int)vgate_div, (int)H4, dvg.data_ptr<float>(), st);
+    (void)hipStreamWaitEvent(st, aux.ev[5], 0);  // dvg (second side stream, above)
   } else {
     // dGv[b, c] = sum_{t, rows of b} alpha[t, r, c] dG_t[r] (kernels/attention.hip:
     // one pass over the bf16 dG rows, partials per step chunk)
