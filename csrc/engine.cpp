@@ -1484,26 +1484,53 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
   // then beam_fused_step_kernel (LSE, candidate top-K, selection / fork /
   // harvest, and the cell of the new beams from their parents' pre and c) --
   // instead of five (vocab, combine, top-K merge, beam step, LSTM step).
-  if (tile_topk && !has_att && NL == 1) {
+  // With temporal attention (MFMA shape) the vocab launch also carries the
+  // attention workgroups: every current row's next video gates (bf16) from
+  // its own h_t, which the fused step adds for the parent like pre.
+  const bool att_fused = has_att && !per_frame && att_mfma_ok((int)K, (int)C, (int)A, (int)H, 0);
+  if (tile_topk && NL == 1 && (!has_att || att_fused)) {
     at::Tensor pre = at::empty({R, H4}, f32);
-    const float* VG = vgate.data_ptr<float>();
+    const float* VG = has_att ? nullptr : vgate.data_ptr<float>();
+    at::Tensor gv16, vg16, att_ep, att_cnt;
+    const int CPAD = C <= 8 ? 8 : 16;
+    if (has_att) {
+      gv16 = at::zeros({B, H4, CPAD}, wx.options());  // frame-minor, frames zero-padded
+      gv16.narrow(2, 0, C).copy_(att[0].transpose(1, 2));
+      vg16 = at::empty({R, H4}, wx.options());
+      att_ep = at::empty({B, A / 64, 32, CPAD}, f32);
+      att_cnt = at::zeros({B}, at::TensorOptions().dtype(at::kInt).device(wx.device()));
+      // step 0 (q = 0): the VALU scorer's fp32 video gates of every row
+      launch_att_fwd(att[0].data_ptr<float>(), att[1].data_ptr<float>(), nullptr, nullptr,
+                     att[3].data_ptr<float>(), att[4].data_ptr<float>(), (int)B, (int)K, (int)C,
+                     (int)A, (int)H4, vg_rows.data_ptr<float>(), nullptr, st, 0, per_frame);
+    }
     // step 0: every row's cell from the initial state and BOS
     launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, ptab.data_ptr<float>(),
                          reinterpret_cast<const uint16_t*>(h[0].data_ptr()), c[0].data_ptr<float>(),
-                         VG, (int)K, (int)R, (int)H, WHH,
+                         has_att ? vg_rows.data_ptr<float>() : VG, has_att ? 1 : (int)K, (int)R,
+                         (int)H, WHH,
                          reinterpret_cast<uint16_t*>(h[1].data_ptr()), c[1].data_ptr<float>(),
                          nullptr, (int)H, 0.f, nullptr, 0, nullptr, st, nullptr, (int)cell);
     for (int64_t t = 1; t < T - 1; ++t) {
       // vocab projection of h_t (rows = beams of step t) + pre_{t+1} of every row
       const at::Tensor& ht = h[t & 1];
       const bool next = t < T - 2;
+      AttMfmaArgs am{};
+      if (has_att && next)
+        am = AttMfmaArgs{reinterpret_cast<const uint16_t*>(ht.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(att[2].data_ptr()),
+                         att[1].data_ptr<float>(), att[3].data_ptr<float>(),
+                         att[4].data_ptr<float>(), reinterpret_cast<const uint16_t*>(gv16.data_ptr()),
+                         (int)H, (int)A, (int)C, CPAD, (int)H4, (int)K, (int)B,
+                         reinterpret_cast<uint16_t*>(vg16.data_ptr()), nullptr, nullptr,
+                         att_ep.data_ptr<float>(), att_cnt.data_ptr<int>()};
       (void)launch_vocab_lstm_fwd(reinterpret_cast<const uint16_t*>(ht.data_ptr()), (int)H, (int)R,
                                   (int)H, W, blog.data_ptr<float>(), (int)V,
                                   reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl,
                                   part.data_ptr(), nullptr, 0, VF_TOPK_H | ((int)K << 8), 1.f,
                                   nullptr, (int)t, reinterpret_cast<const uint16_t*>(ht.data_ptr()),
                                   WHH, VG, (int)K, next ? pre.data_ptr<float>() : nullptr, st, 0,
-                                  nullptr, nullptr, nullptr);
+                                  nullptr, nullptr, has_att && next ? &am : nullptr);
       BeamFusedArgs ba{reinterpret_cast<const VocabPartial*>(part.data_ptr()),
                        reinterpret_cast<const float2*>(logits.data_ptr()), n_vt, (int)R, (int)K,
                        (int)B, (int)T, beam_sum.data_ptr<float>(), seq_hist.data_ptr<int64_t>(),
@@ -1512,7 +1539,9 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                        tok.data_ptr<int64_t>(), next ? pre.data_ptr<float>() : nullptr,
                        ptab.data_ptr<float>(), c[t & 1].data_ptr<float>(),
                        c[(t + 1) & 1].data_ptr<float>(),
-                       reinterpret_cast<uint16_t*>(h[(t + 1) & 1].data_ptr()), (int)H, (int)cell};
+                       reinterpret_cast<uint16_t*>(h[(t + 1) & 1].data_ptr()), (int)H, (int)cell,
+                       has_att && next ? reinterpret_cast<const uint16_t*>(vg16.data_ptr())
+                                       : nullptr};
       launch_beam_fused_step(ba, (int)t, st);
     }
     return {best_seq, best_lp};

@@ -326,6 +326,7 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
   const bool cell = a.pre != nullptr;
   float4 ppre[BF_MAXK][UPT];
   float pc[BF_MAXK][UPT];
+  const bool att = a.vg16 != nullptr;
   if (cell) {
 #pragma unroll
     for (int q = 0; q < BF_MAXK; ++q)
@@ -336,6 +337,26 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
         ppre[q][j] = *reinterpret_cast<const float4*>(a.pre + r * 4 * H + 4 * u);
         pc[q][j] = a.c_in[r * H + u];
       }
+    if (att) {  // (uniform) the rows' video gates (temporal attention), added to pre
+      uint2 pv[BF_MAXK][UPT];
+#pragma unroll
+      for (int q = 0; q < BF_MAXK; ++q)
+#pragma unroll
+        for (int j = 0; j < UPT; ++j) {
+          const int u = min(tid + BF_THREADS * j, H - 1);
+          const int64_t r = (int64_t)b * K + min(q, K - 1);
+          pv[q][j] = *reinterpret_cast<const uint2*>(a.vg16 + r * 4 * H + 4 * u);
+        }
+#pragma unroll
+      for (int q = 0; q < BF_MAXK; ++q)
+#pragma unroll
+        for (int j = 0; j < UPT; ++j) {
+          ppre[q][j].x += bf2f(pv[q][j].x & 0xffff);
+          ppre[q][j].y += bf2f(pv[q][j].x >> 16);
+          ppre[q][j].z += bf2f(pv[q][j].y & 0xffff);
+          ppre[q][j].w += bf2f(pv[q][j].y >> 16);
+        }
+    }
   }
   const int64_t* sh_old = a.seq_hist + (int64_t)((t + 1) & 1) * R * T;
   const float* lh_old = a.lp_hist + (int64_t)((t + 1) & 1) * R * T;

@@ -938,13 +938,32 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
   // 2 stages to fit): one block's epilogue overlaps the others' main loops.
   // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
   // CU (3 interleaved rounds; profiles/r2/ab_vocab_tiles.txt)
-  if ((flags & VF_TOPK) && att == nullptr) {  // beam search: per-tile top-K candidates
+  if (flags & VF_TOPK) {  // beam search: per-tile top-K candidates
     if (vf_topk_k(flags) < 1 || vf_topk_k(flags) > VF_TOPK_MAXK)
       throw std::runtime_error("vocab_lstm_fwd: VF_TOPK needs 1 <= K <= 8");
-    launch_vocab_lstm_t<64, 2, 3, LGTile2, 0, true>(hd, ldh, R, H, W, bias, V, logits16, ldl, part,
-                                                    tgt, tgt_stride, flags, inv_temp, rng, step,
-                                                    h_t, whh, vgate, vdiv, pre, NQ, q_out, stream,
-                                                    eoff, nullptr);
+    if (att == nullptr) {
+      launch_vocab_lstm_t<64, 2, 3, LGTile2, 0, true>(hd, ldh, R, H, W, bias, V, logits16, ldl,
+                                                      part, tgt, tgt_stride, flags, inv_temp, rng,
+                                                      step, h_t, whh, vgate, vdiv, pre, NQ, q_out,
+                                                      stream, eoff, nullptr);
+      return vocab_num_tiles(V);
+    }
+    // beam search with temporal attention: the attention workgroups compute
+    // every current row's next video gates (vg16) from its own h_t; the fused
+    // beam step then picks the parent's row, like pre
+    check_att_mfma(*att);
+#define VT(AVX)                                                                                 \
+  case AVX:                                                                                      \
+    launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX, true>(hd, ldh, R, H, W, bias, V, logits16, ldl,   \
+                                                      part, tgt, tgt_stride, flags, inv_temp, rng, \
+                                                      step, h_t, whh, vgate, vdiv, pre, NQ, q_out, \
+                                                      stream, eoff, att);                          \
+    break;
+    switch (att_variant(att->C)) {
+      ATT_VARIANTS(VT)
+      default: throw std::runtime_error("vocab_lstm_fwd: no attention variant");
+    }
+#undef VT
     return vocab_num_tiles(V);
   }
 #define VL(AVX)                                                                            \

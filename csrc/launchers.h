@@ -24,6 +24,7 @@ struct BeamFusedArgs {
   float* c_out;
   uint16_t* h_out;    // (R, H) bf16
   int H, cell;
+  const uint16_t* vg16;  // nullable (R, 4H) bf16 video gates of every current row (attention)
 };
 void launch_beam_fused_step(const BeamFusedArgs& a, int t, hipStream_t stream);
 

@@ -832,39 +832,46 @@ class DecoderEngine:
         self.ensure_ptab()
         blog = model.logit.bias.detach().float().contiguous()
         vg = vg.detach().float().contiguous()
-        if (not att and not state0 and self.layers == 1 and vg.is_cuda
+        if (not state0 and self.layers == 1 and vg.is_cuda
                 and os.environ.get('CSTCAP_BEAM_GRAPH', '1') != '0'
                 and not torch.cuda.is_current_stream_capturing()):
-            return self._beam_graphed(vg, blog, K, model.seq_length)
+            return self._beam_graphed(vg, blog, K, model.seq_length, att)
         seq, lp = _ext.ops().beam_search(self.wx, self.ptab, self.whh, self.wlog, blog, vg, K,
                                          model.seq_length, BOS, att, self.cell, state0,
                                          self.upper_operands())
         return seq, lp
 
-    def _beam_graphed(self, vg, blog, K, T):
-        """The whole beam decode (T-1 steps x 5 launches) replayed as one
-        captured HIP graph per (videos, K, T): the weights are the engine's
-        persistent shadows (updated in place); the video gates and the fp32
-        logit bias are copied into the graph's own static buffers before each
-        replay (``blog`` may be a fresh temporary per call, so the graph never
-        reads the caller's memory), the outputs cloned out."""
-        key = (tuple(vg.shape), tuple(blog.shape), int(K), int(T))
+    def _beam_graphed(self, vg, blog, K, T, att=()):
+        """The whole beam decode (T-1 steps) replayed as one captured HIP
+        graph per (shapes, K, T): the weights are the engine's persistent
+        shadows (updated in place); the video gates, the fp32 logit bias and
+        the per-batch attention operands (Gv, P, w_a, b_a; W_q is a shadow)
+        are copied into the graph's own static buffers before each replay (the
+        caller's tensors may be fresh temporaries, so the graph never reads
+        the caller's memory), the outputs cloned out."""
+        att = list(att)
+        dyn = [i for i, t in enumerate(att) if t is not self.wq]  # per-call operands
+        key = (tuple(vg.shape), tuple(blog.shape), int(K), int(T),
+               tuple(tuple(t.shape) for t in att))
         cache = self.__dict__.setdefault('_beam_graphs', {})
         ent = cache.get(key)
         if ent is None:
             if len(cache) >= 4:
                 cache.clear()
             static_vg, static_b = vg.clone(), blog.clone()
+            static_att = [t.clone() if i in dyn else t for i, t in enumerate(att)]
             args = lambda: (self.wx, self.ptab, self.whh, self.wlog, static_b, static_vg, K, T,
-                            BOS, [], self.cell, [], [])
+                            BOS, static_att, self.cell, [], [])
             _ext.ops().beam_search(*args())  # (kernel attributes, allocator, outside capture)
             torch.cuda.synchronize(vg.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 out = _ext.ops().beam_search(*args())
-            ent = cache[key] = (g, static_vg, static_b, out)
-        g, static_vg, static_b, out = ent
+            ent = cache[key] = (g, static_vg, static_b, static_att, out)
+        g, static_vg, static_b, static_att, out = ent
         static_vg.copy_(vg)
         static_b.copy_(blog)
+        for i in dyn:
+            static_att[i].copy_(att[i])
         g.replay()
         return out[0].clone(), out[1].clone()
