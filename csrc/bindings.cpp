@@ -87,6 +87,7 @@ void stamp_buffer(at::Tensor buf);
 void stamp_now(int64_t slot);
 int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
+at::Tensor att_mfma_phases(at::Tensor gv, at::Tensor P, at::Tensor wa, at::Tensor ba, int64_t R);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -175,4 +176,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stamp_now", &cst::stamp_now);
   m.def("wall_clock_khz", &cst::wall_clock_khz);
   m.def("vocab_x", &cst::vocab_x);
+  m.def("att_mfma_phases", &cst::att_mfma_phases);
 }

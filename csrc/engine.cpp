@@ -1664,6 +1664,40 @@ double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t ite
       iters, st);
 }
 
+// Phase stamps of one launch of the MFMA attention workgroups (microbenchmark,
+// scripts/microbench_att.py): (Bv * A / 64, 8) int64 wall-clock ticks, phases
+// 0 start, 1 operands in LDS, 2 query MFMA, 3 scores, 4 ticket, and for the
+// video's last workgroup 5 slot sums, 6 end (-1 where not reached).
+at::Tensor att_mfma_phases(at::Tensor gv, at::Tensor P, at::Tensor wa, at::Tensor ba, int64_t R) {
+  check_cuda(gv, "gv");
+  const int64_t Bv = gv.size(0), C = gv.size(1), H4 = gv.size(2), A = P.size(2), H = H4 / 4;
+  const int vdiv = (int)(R / Bv), CP = C <= 8 ? 8 : 16;
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(gv.device());
+  auto bf = gv.options().dtype(at::kBFloat16);
+  at::Tensor h = (at::rand({R, H}, f32) * 2 - 1).to(at::kBFloat16);
+  at::Tensor wq = (at::randn({A, H}, f32) * 0.05).to(at::kBFloat16);
+  at::Tensor gv16 = at::zeros({Bv, H4, CP}, bf), vg = at::empty({R, H4}, bf);
+  gv16.narrow(2, 0, C).copy_(gv.transpose(1, 2));
+  at::Tensor alpha = at::empty({R, C}, f32), qo = at::empty({R, A}, f32);
+  at::Tensor ep = at::empty({Bv, A / 64, 32, CP}, f32);
+  at::Tensor cnt = at::zeros({Bv}, f32.dtype(at::kInt));
+  at::Tensor dbg = at::full({Bv * (A / 64), 8}, -1, f32.dtype(at::kLong));
+  AttMfmaArgs am{reinterpret_cast<const uint16_t*>(h.data_ptr()),
+                 reinterpret_cast<const uint16_t*>(wq.data_ptr()), P.data_ptr<float>(),
+                 wa.data_ptr<float>(), ba.data_ptr<float>(),
+                 reinterpret_cast<const uint16_t*>(gv16.data_ptr()), (int)H, (int)A, (int)C, CP,
+                 (int)H4, vdiv, (int)Bv, reinterpret_cast<uint16_t*>(vg.data_ptr()),
+                 alpha.data_ptr<float>(), qo.data_ptr<float>(), ep.data_ptr<float>(),
+                 cnt.data_ptr<int>(), nullptr, nullptr};
+  hipStream_t st = cur_stream();
+  launch_att_mfma_fwd(am, st);  // warm-up
+  (void)hipStreamSynchronize(st);
+  am.dbg = dbg.data_ptr<int64_t>();
+  launch_att_mfma_fwd(am, st);
+  (void)hipStreamSynchronize(st);
+  return dbg;
+}
+
 // temporal attention kernels alone (one decode / reverse step): Gv (Bv, C, 4H)
 // fp32, P (Bv, C, A), q (R, A), w_a (A), b_a (1); which = 0: forward
 // (accumulating into pre), 1: backward (dG rows (R, 4H + A) bf16, dq written)

@@ -58,6 +58,11 @@ __device__ __forceinline__ bf16x8 ld_bf16x8(const uint16_t* p) {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+// phase stamp of a workgroup (microbenchmark only: AttMfmaArgs::dbg)
+__device__ __forceinline__ void att_phase(const AttMfmaArgs& g, int blk, int k) {
+  if (g.dbg != nullptr && threadIdx.x == 0) g.dbg[blk * 8 + k] = (int64_t)wall_clock64();
+}
+
 // CP: frames padded to 8 / 16.  blk = b * NS + s.
 template <int CP>
 __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g, char* lds) {
@@ -72,6 +77,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int row0 = b * vdiv, a0 = s * ATT_SLICE;
+  att_phase(g, blk, 0);
   // h rows of the video -> LDS by LDS-DMA (rows >= vdiv repeat the last row)
   const int cpr = H / 8;  // 16-byte chunks per row
   const int swm = (cpr < 16 ? cpr : 16) - 1;
@@ -103,6 +109,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     reinterpret_cast<float4*>(s_wa)[tid] = reinterpret_cast<const float4*>(g.wa + a0)[tid];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // h rows, P, w_a in LDS
+  att_phase(g, blk, 1);
   // 1. q^T tiles (16 units x 16 rows) x 2 row tiles
   f32x4v acc[2];
 #pragma unroll
@@ -121,6 +128,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
   }
   // lane: units u0 .. u0 + 3 (registers 0..3) of rows 16 j + ru
   const int u0 = 16 * w + 4 * ku;
+  att_phase(g, blk, 2);
   if (g.q_out != nullptr) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -157,6 +165,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     }
   }
   __syncthreads();
+  att_phase(g, blk, 3);
   // the slice's partial (rows x frames) -> its slot, write-through (sc1)
   float* slot = g.e_part + ((int64_t)b * NS + s) * 32 * CP;
   for (int i = tid; i < 32 * CP; i += 256) {
@@ -175,6 +184,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     *s_flag = ticket == NS - 1;
   }
   __syncthreads();
+  att_phase(g, blk, 4);
   if (!*s_flag) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only)
   // 3. last workgroup of the video: scores, softmax, vgate.  The gate-table
@@ -210,6 +220,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     }
   }
   __syncthreads();
+  att_phase(g, blk, 5);
   if (tid < 32) {
     float x[CP], mx = -INFINITY;
     const float ba = g.ba[0];
@@ -256,6 +267,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
       }
     }
   }
+  att_phase(g, blk, 6);
 }
 
 // attention variant of a kernel template: 0 = none, else the padded frame

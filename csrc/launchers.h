@@ -128,6 +128,7 @@ struct AttMfmaArgs {
   int* cnt;              // (Bv) tickets, zero at the first launch (re-armed by the kernel)
   uint16_t* u_out;       // nullable (R, C, A) fp16 scorer values tanh(P + q) (training:
                          // the fused attention backward reads them instead of recomputing)
+  int64_t* dbg;          // nullable (workgroups, 8) wall-clock phase stamps (microbenchmark)
 };
 // the MFMA attention path applies: rows per video 2..32, C <= 16, A % 64 == 0,
 // A <= 1024, H % 32 == 0, 64 <= H <= 512, the shared scorer (not per frame)
