@@ -202,6 +202,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     ga[i] = ld_bf16x8(gvb + (int64_t)(n0 + r) * CP + (CP == 16 ? 8 * hh : 0));
   }
   if (tid == 0) g.cnt[b] = 0;  // re-arm for the next step (stream-ordered)
+  const float ba = g.ba[0];      // (requested with the slot loads)
   // the NS slots summed per (row, frame): one pair per thread, all slot loads
   // of a thread out together (sc1, the hand-off's loads)
   {
@@ -223,7 +224,6 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
   att_phase(g, blk, 5);
   if (tid < 32) {
     float x[CP], mx = -INFINITY;
-    const float ba = g.ba[0];
 #pragma unroll
     for (int c = 0; c < CP; ++c) x[c] = s_e[tid * CP + c] + ba;
 #pragma unroll
@@ -245,25 +245,28 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     }
   }
   __syncthreads();
-  // vgate^T tiles: 4H / 32 gate-column tiles over the 4 waves
+  // vgate tiles (32 rows x 32 gate columns): 4H / 32 tiles over the 4 waves.
+  // A = alpha (rows), B = the gate table (columns): a lane then holds one
+  // gate column of 16 rows, so each store instruction writes two rows' 64-byte
+  // runs (32 lanes = 32 consecutive columns).  (With the gate table as A a
+  // lane held 16 columns of ONE row: every store instruction scattered 64
+  // 8-byte pieces over 32 rows, ~7 us of the last workgroup's tail at the
+  // headline shape, scripts/microbench_att.py phase stamps.)
   const bf16x8 bal = ld_bf16x8(s_alb + r * 16 + 8 * hh);
   const bf16x8 zero8 = {};
-  const bool rv = r < vdiv;
 #pragma unroll
   for (int i = 0; i < MAXT; ++i) {
     const int n0 = (w * ntw + i) * 32;
     f32x16 o;
 #pragma unroll
     for (int k = 0; k < 16; ++k) o[k] = 0.f;
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ghalf ? ga[i] : zero8, bal, o, 0, 0, 0);
-    if (rv && i < ntw) {
-      uint16_t* dst = g.vg_out + (int64_t)(row0 + r) * G4 + n0 + 4 * hh;
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bal, ghalf ? ga[i] : zero8, o, 0, 0, 0);
+    if (i < ntw) {
+      uint16_t* dst = g.vg_out + (int64_t)row0 * G4 + n0 + r;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(o[4 * j]) | ((uint32_t)f2bf(o[4 * j + 1]) << 16);
-        pk.y = (uint32_t)f2bf(o[4 * j + 2]) | ((uint32_t)f2bf(o[4 * j + 3]) << 16);
-        *reinterpret_cast<uint2*>(dst + 8 * j) = pk;
+      for (int k = 0; k < 16; ++k) {
+        const int row = (k & 3) + 8 * (k >> 2) + 4 * hh;
+        if (row < vdiv) dst[(int64_t)row * G4] = f2bf(o[k]);
       }
     }
   }

@@ -309,7 +309,7 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
 // the selection -- was ~10 dependent memory round trips per step: 30.4 us,
 // profiles/r5/steps_head_beam.txt.)
 constexpr int BF_THREADS = 512, BF_MAXK = 8, BF_MAXC = 12, BF_MAXP = 2, BF_MAXT = 64;
-template <int UPT>
+template <int UPT, int KP>
 __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedArgs a, int t) {
   __shared__ float s_tv[BF_MAXK * BF_MAXK];
   __shared__ int s_ti[BF_MAXK * BF_MAXK];
@@ -324,12 +324,12 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
   const int rows = t == 1 ? 1 : K;
   // -- 0. prefetch ------------------------------------------------------------------
   const bool cell = a.pre != nullptr;
-  float4 ppre[BF_MAXK][UPT];
-  float pc[BF_MAXK][UPT];
+  float4 ppre[KP][UPT];
+  float pc[KP][UPT];
   const bool att = a.vg16 != nullptr;
   if (cell) {
 #pragma unroll
-    for (int q = 0; q < BF_MAXK; ++q)
+    for (int q = 0; q < KP; ++q)
 #pragma unroll
       for (int j = 0; j < UPT; ++j) {
         const int u = min(tid + BF_THREADS * j, H - 1);
@@ -338,9 +338,9 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
         pc[q][j] = a.c_in[r * H + u];
       }
     if (att) {  // (uniform) the rows' video gates (temporal attention), added to pre
-      uint2 pv[BF_MAXK][UPT];
+      uint2 pv[KP][UPT];
 #pragma unroll
-      for (int q = 0; q < BF_MAXK; ++q)
+      for (int q = 0; q < KP; ++q)
 #pragma unroll
         for (int j = 0; j < UPT; ++j) {
           const int u = min(tid + BF_THREADS * j, H - 1);
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
           pv[q][j] = *reinterpret_cast<const uint2*>(a.vg16 + r * 4 * H + 4 * u);
         }
 #pragma unroll
-      for (int q = 0; q < BF_MAXK; ++q)
+      for (int q = 0; q < KP; ++q)
 #pragma unroll
         for (int j = 0; j < UPT; ++j) {
           ppre[q][j].x += bf2f(pv[q][j].x & 0xffff);
@@ -358,6 +358,10 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
         }
     }
   }
+  // the beams' running sums and the video's best perplexity (read after the
+  // selection; loaded now)
+  const float sum_old = a.beam_sum[b * K + min(tid, K - 1)];
+  const float ppl_old = a.best_ppl[b];
   const int64_t* sh_old = a.seq_hist + (int64_t)((t + 1) & 1) * R * T;
   const float* lh_old = a.lp_hist + (int64_t)((t + 1) & 1) * R * T;
   for (int e = tid; e < K * T; e += BF_THREADS) {
@@ -430,8 +434,30 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
       if (lane == 0) s_tv[w * K + k] = best - L, s_ti[w * K + k] = besti;
     }
   }
-  if (tid < K) s_sum_old[tid] = a.beam_sum[b * K + tid];
+  if (tid < K) s_sum_old[tid] = sum_old;
   __syncthreads();
+  // the token-table rows of every candidate (K rows x K tokens, known now)
+  // for this thread's units, requested before the selection: after it only
+  // register selects remain
+  // (register budget: only for K <= 5 beams at H <= 512; else gathered after
+  // the selection)
+  // (measured slower: 25 candidate rows per thread -- 5x the gathered bytes
+  // -- cost more than the round trip they save: 1.428 vs 1.172 ms per beam-5
+  // decode of 64 videos)
+  constexpr bool PFC = false;
+  float4 xc[PFC ? KP * KP : 1][UPT];
+  if (PFC && cell) {
+#pragma unroll
+    for (int e = 0; e < KP * KP; ++e) {
+      const int q = min(e / KP, K - 1), c = min(e % KP, K - 1);
+      const int64_t tk = s_ti[q * K + c];
+#pragma unroll
+      for (int jj = 0; jj < UPT; ++jj) {
+        const int u = min(tid + BF_THREADS * jj, H - 1);
+        xc[e][jj] = *reinterpret_cast<const float4*>(a.ptab + tk * 4 * H + 4 * u);
+      }
+    }
+  }
   // -- B. selection (beam_step_kernel's rules), every thread at the barriers ------
   const int ncand = rows * K;
   if (tid < ncand) {
@@ -470,7 +496,7 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
   }
   if (tid == 0) {  // harvest, in beam order (earliest wins ties)
     int win = -1;
-    float bp = a.best_ppl[b];
+    float bp = ppl_old;
     for (int v = 0; v < K; ++v) {
       const int j = s_sel[v], c = j / rows, q = j % rows;
       if (s_ti[q * K + c] == 0 || t == T - 2) {
@@ -494,21 +520,33 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
   }
   if (!cell) return;
   // -- C. the next step's cell for the K new beams ---------------------------------
-  float4 xv[BF_MAXK][UPT];
-  int par[BF_MAXK];
+  float4 xv[KP][UPT];
+  int par[KP];
 #pragma unroll
-  for (int v = 0; v < BF_MAXK; ++v) {  // the token-table rows: all gathers out at once
+  for (int v = 0; v < KP; ++v) {  // the selected candidates' token-table rows
     const int vv = min(v, K - 1), j = s_sel[vv], c = j / rows, q = j % rows;
     par[v] = q;
-    const int64_t tk = s_ti[q * K + c];
+    if constexpr (PFC) {  // prefetched: register selects
+      const int e = q * KP + c;
 #pragma unroll
-    for (int jj = 0; jj < UPT; ++jj) {
-      const int u = min(tid + BF_THREADS * jj, H - 1);
-      xv[v][jj] = *reinterpret_cast<const float4*>(a.ptab + tk * 4 * H + 4 * u);
+      for (int jj = 0; jj < UPT; ++jj) {
+        float4 x = xc[0][jj];
+#pragma unroll
+        for (int f = 1; f < KP * KP; ++f)
+          if (e == f) x = xc[f][jj];
+        xv[v][jj] = x;
+      }
+    } else {  // all gathers out at once
+      const int64_t tk = s_ti[q * K + c];
+#pragma unroll
+      for (int jj = 0; jj < UPT; ++jj) {
+        const int u = min(tid + BF_THREADS * jj, H - 1);
+        xv[v][jj] = *reinterpret_cast<const float4*>(a.ptab + tk * 4 * H + 4 * u);
+      }
     }
   }
 #pragma unroll
-  for (int v = 0; v < BF_MAXK; ++v) {
+  for (int v = 0; v < KP; ++v) {
     if (v < K) {
 #pragma unroll
       for (int jj = 0; jj < UPT; ++jj) {
@@ -517,7 +555,7 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
           float4 pv = ppre[0][jj];
           float cv = pc[0][jj];
 #pragma unroll
-          for (int q = 1; q < BF_MAXK; ++q)
+          for (int q = 1; q < KP; ++q)
             if (par[v] == q) pv = ppre[q][jj], cv = pc[q][jj];
           const CellFwd cf = cell_fwd(a.cell, pv.x + xv[v][jj].x, pv.y + xv[v][jj].y,
                                       pv.z + xv[v][jj].z, pv.w + xv[v][jj].w, cv);
@@ -534,10 +572,16 @@ void launch_beam_fused_step(const BeamFusedArgs& a, int t, hipStream_t stream) {
   if (a.K < 1 || a.K > BF_MAXK || a.T > BF_MAXT || a.n_vt > 64 * BF_MAXP ||
       a.n_vt * a.K > 64 * BF_MAXC || (a.pre != nullptr && a.H > 2 * BF_THREADS))
     throw std::runtime_error("beam_fused_step: K <= 8, T <= 64, n_vt <= 128, n_vt K <= 768, H <= 1024");
-  if (a.pre == nullptr || a.H <= BF_THREADS)
-    hipLaunchKernelGGL(beam_fused_step_kernel<1>, dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
+  // register budget: K <= 4 / 8 beams, H <= 512 / 1024 units per workgroup
+  const bool one = a.pre == nullptr || a.H <= BF_THREADS;
+  if (a.K <= 4 && one)
+    hipLaunchKernelGGL((beam_fused_step_kernel<1, 4>), dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
+  else if (a.K <= 5 && one)
+    hipLaunchKernelGGL((beam_fused_step_kernel<1, 5>), dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
+  else if (one)
+    hipLaunchKernelGGL((beam_fused_step_kernel<1, 8>), dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
   else
-    hipLaunchKernelGGL(beam_fused_step_kernel<2>, dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
+    hipLaunchKernelGGL((beam_fused_step_kernel<2, 8>), dim3(a.B), dim3(BF_THREADS), 0, stream, a, t);
   post_launch("beam_fused_step_kernel", stream);
 }
 
