@@ -1667,7 +1667,7 @@ double vgrad_colsum_bench(at::Tensor E, at::Tensor alpha, int64_t V, int64_t ite
 // Phase stamps of one launch of the MFMA attention workgroups (microbenchmark,
 // scripts/microbench_att.py): (Bv * A / 64, 8) int64 wall-clock ticks, phases
 // 0 start, 1 operands in LDS, 2 query MFMA, 3 scores, 4 ticket, and for the
-// video's last workgroup 5 slot sums, 6 end (-1 where not reached).
+// video's last workgroup 5 slot sums, 7 softmax, 6 end (-1 where not reached).
 at::Tensor att_mfma_phases(at::Tensor gv, at::Tensor P, at::Tensor wa, at::Tensor ba, int64_t R) {
   check_cuda(gv, "gv");
   const int64_t Bv = gv.size(0), C = gv.size(1), H4 = gv.size(2), A = P.size(2), H = H4 / 4;

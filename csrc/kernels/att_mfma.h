@@ -245,6 +245,7 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
     }
   }
   __syncthreads();
+  att_phase(g, blk, 7);
   // vgate tiles (32 rows x 32 gate columns): 4H / 32 tiles over the 4 waves.
   // A = alpha (rows), B = the gate table (columns): a lane then holds one
   // gate column of 16 rows, so each store instruction writes two rows' 64-byte
@@ -254,20 +255,26 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
   // headline shape, scripts/microbench_att.py phase stamps.)
   const bf16x8 bal = ld_bf16x8(s_alb + r * 16 + 8 * hh);
   const bf16x8 zero8 = {};
+  // the 16 output rows of this lane: one pointer each, formed once (the
+  // tile's column offset is then an immediate of the store)
+  uint16_t* prow[16];
+  bool vrow[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int row = (k & 3) + 8 * (k >> 2) + 4 * hh;
+    vrow[k] = row < vdiv;
+    prow[k] = g.vg_out + (int64_t)(row0 + min(row, vdiv - 1)) * G4 + w * ntw * 32 + r;
+  }
 #pragma unroll
   for (int i = 0; i < MAXT; ++i) {
-    const int n0 = (w * ntw + i) * 32;
     f32x16 o;
 #pragma unroll
     for (int k = 0; k < 16; ++k) o[k] = 0.f;
     o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bal, ghalf ? ga[i] : zero8, o, 0, 0, 0);
     if (i < ntw) {
-      uint16_t* dst = g.vg_out + (int64_t)row0 * G4 + n0 + r;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int row = (k & 3) + 8 * (k >> 2) + 4 * hh;
-        if (row < vdiv) dst[(int64_t)row * G4] = f2bf(o[k]);
-      }
+      for (int k = 0; k < 16; ++k)
+        if (vrow[k]) prow[k][32 * i] = f2bf(o[k]);
     }
   }
   att_phase(g, blk, 6);

@@ -30,7 +30,7 @@ print(json.dumps(res))
 ph = C.att_mfma_phases(gv, P, wa, ba, R).cpu().double() * 10.0 / 1000.0  # us
 t0 = ph[:, 0].min()
 out = {}
-names = ['start', 'operands', 'qgemm', 'scores', 'ticket', 'slots', 'end']
+names = ['start', 'operands', 'qgemm', 'scores', 'ticket', 'slots', 'end', 'softmax']
 for k, n in enumerate(names):
     col = ph[:, k]
     ok = ph[:, k] >= 0
