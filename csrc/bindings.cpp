@@ -36,7 +36,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          std::vector<at::Tensor> state0,
                                          std::vector<at::Tensor> up, at::Tensor blog,
                                          at::Tensor fix_total, int64_t vgate_div,
-                                         at::Tensor xw);
+                                         at::Tensor xw, std::vector<at::Tensor> vg_bwd,
+                                         int64_t vg_nf, double vg_p);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,

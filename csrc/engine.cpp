@@ -111,7 +111,7 @@ constexpr int MAX_DHD_CHUNKS = 32;  // per-chunk events of the vocab-head dHd GE
 struct DeviceAux {
   std::vector<hipEvent_t> ev;
   c10::hip::HIPStream side[2];
-  hipEvent_t grad_ev[2];  // data parallelism: gradient groups final (set_grad_events)
+  hipEvent_t grad_ev[3];  // data parallelism: gradient groups final (set_grad_events)
 };
 static DeviceAux& device_aux(int dev_index) {
   static std::map<int, DeviceAux*> aux;
@@ -142,9 +142,9 @@ void set_grad_events(bool on) { g_grad_events_on = on; }
 // record nodes): the trainer checks that a step (or the capture of one)
 // recorded both events before its comm stream relies on them -- a wait on an
 // event this step never recorded would order nothing
-static int64_t g_grad_ev_count[2] = {0, 0};
+static int64_t g_grad_ev_count[3] = {0, 0, 0};
 int64_t grad_event_count(int64_t k) {
-  TORCH_CHECK(k >= 0 && k < 2, "grad_event_count: group 0 or 1");
+  TORCH_CHECK(k >= 0 && k < 3, "grad_event_count: group 0, 1 or 2");
   return g_grad_ev_count[k];
 }
 static void record_grad_event(hipEvent_t ev, hipStream_t s, int k) {
@@ -171,14 +171,14 @@ static void record_grad_event(hipEvent_t ev, hipStream_t s, int k) {
   e = hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
   TORCH_CHECK(e == hipSuccess, "grad event: capture dependencies: ", hipGetErrorString(e));
 }
-void grad_event_record(int64_t k, int64_t stream) {  // (tests)
-  TORCH_CHECK(k >= 0 && k < 2, "grad_event_record: group 0 or 1");
+void grad_event_record(int64_t k, int64_t stream) {
+  TORCH_CHECK(k >= 0 && k < 3, "grad_event_record: group 0, 1 or 2");
   int dev = 0;
   (void)hipGetDevice(&dev);
   record_grad_event(device_aux(dev).grad_ev[k], reinterpret_cast<hipStream_t>(stream), (int)k);
 }
 void grad_event_wait(int64_t k, int64_t stream) {
-  TORCH_CHECK(k >= 0 && k < 2, "grad_event_wait: group 0 or 1");
+  TORCH_CHECK(k >= 0 && k < 3, "grad_event_wait: group 0, 1 or 2");
   int dev = 0;
   (void)hipGetDevice(&dev);
   (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), device_aux(dev).grad_ev[k], 0);
@@ -565,6 +565,20 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
 //            the loop on one GPU, concurrently with the loop under data
 //            parallelism so the vocab head's all-reduce (comm_stream waits
 //            on it) hides under the loop.
+std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
+                                          std::vector<at::Tensor> xs,
+                                          std::vector<at::Tensor> ws, double drop_p,
+                                          std::vector<at::Tensor> outs);
+
+// vg_bwd (concat model, data parallelism with direct gradient slots): the
+// video-gate / FeatPool backward and the packed -> PyTorch row order of the
+// LSTM weight gradients done HERE instead of after the call, so W_ih's and
+// the FeatPool parameters' gradients are final shortly after the reverse loop
+// (a third early all-reduce slice, grad event 2):
+//   {dst_ie, dst_hh (int64 row maps), W_ih slot (4H x (E + Fv)), W_hh slot
+//    (4H x H), W_ih (fp32 parameter), fc (FeatPool output, B x Fv),
+//    FeatPool weight slots x vg_nf, bias slots x vg_nf, inputs x vg_nf,
+//    weights x vg_nf}; vg_p the FeatPool dropout.
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -577,7 +591,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          std::vector<at::Tensor> state0,
                                          std::vector<at::Tensor> up, at::Tensor blog,
                                          at::Tensor fix_total, int64_t vgate_div,
-                                         at::Tensor xw) {
+                                         at::Tensor xw, std::vector<at::Tensor> vg_bwd,
+                                         int64_t vg_nf, double vg_p) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -997,6 +1012,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     (void)hipEventRecord(aux.ev[5], side2.stream());
   }
   at::Tensor dvg;
+  const bool vg_direct = !has_att && !vg_bwd.empty();
+  if (vg_direct)
+    TORCH_CHECK(vg_nf >= 1 && (int64_t)vg_bwd.size() == 6 + 4 * vg_nf && NL == 1 && !has_s0,
+                "vg_bwd = {dst_ie, dst_hh, W_ih slot, W_hh slot, W_ih, fc, FeatPool slots, "
+                "inputs, weights}");
+  std::vector<at::Tensor> vg_keep;  // (side-stream temporaries, released after the join)
   if (!has_att) {
     TORCH_CHECK(vgate_div >= 1 && R % vgate_div == 0, "vgate_div must divide the rows");
     dvg = at::empty({R / vgate_div, H4}, f32);
@@ -1008,6 +1029,22 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     launch_video_gate_grad(reinterpret_cast<const uint16_t*>(dG_all.data_ptr()), KD,
                            (int)n_steps, (int)R, (int)vgate_div, (int)H4, dvg.data_ptr<float>(),
                            side2.stream());
+    if (vg_direct) {
+      // video-gate and FeatPool backward on the same stream (ops/featpool.py
+      // _FeatPoolVgateFn does this after the call otherwise): dfc = dvg W_iv,
+      // dW_iv = dvg^T fc into W_ih's slot, FeatPool gradients into theirs
+      c10::hip::HIPStreamGuard guard(side2);
+      at::Tensor dvg_u = dvg.index_select(1, vg_bwd[0]);  // PyTorch gate order
+      const int64_t Fv = vg_bwd[4].size(1) - E;
+      at::Tensor dfc = at::mm(dvg_u, vg_bwd[4].narrow(1, E, Fv));
+      at::Tensor wiv_slot = vg_bwd[2].narrow(1, E, Fv);
+      at::mm_out(wiv_slot, dvg_u.t(), vg_bwd[5]);
+      std::vector<at::Tensor> outs(vg_bwd.begin() + 6, vg_bwd.begin() + 6 + 2 * vg_nf);
+      std::vector<at::Tensor> xs(vg_bwd.begin() + 6 + 2 * vg_nf, vg_bwd.begin() + 6 + 3 * vg_nf);
+      std::vector<at::Tensor> wsv(vg_bwd.begin() + 6 + 3 * vg_nf, vg_bwd.begin() + 6 + 4 * vg_nf);
+      (void)featpool_backward(dfc, vg_bwd[5], xs, wsv, vg_p, outs);
+      vg_keep = {dvg_u, dfc};
+    }
     (void)hipEventRecord(aux.ev[5], side2.stream());
   }
   at::Tensor dGx = dG_all.view({NR, KD});  // [dG | dq] rows
@@ -1086,7 +1123,15 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       dWie.copy_(at::mm(S_tok.t(), emb, at::kFloat));
   }
   stamp(STAMP_BWD_TOKGEMM, st);
+  if (vg_direct) {
+    // W_ih's token columns (packed -> PyTorch rows) and, from the second side
+    // stream, its video columns and the FeatPool gradients: slice 2 is final
+    vg_bwd[2].narrow(1, 0, E).copy_(dWx.narrow(1, 0, E).index_select(0, vg_bwd[0]));
+    (void)hipStreamWaitEvent(st, aux.ev[5], 0);
+    if (grad_ev) record_grad_event(aux.grad_ev[2], st, 2);
+  }
   whh_grad();
+  if (vg_direct) vg_bwd[3].copy_(dWx.narrow(1, E, H).index_select(0, vg_bwd[1]));
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
     dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);

@@ -182,6 +182,9 @@ class _DecoderFn(torch.autograd.Function):
         ctx.shapes = (w_ih.shape, emb_w.shape)
         ctx.has_att = has_att
         ctx.state0 = state0 if save else []
+        # the video-gate node of this pass (ops/featpool.py _FeatPoolVgateFn)
+        vg_pending = eng.__dict__.pop('_vg_pending', None)
+        ctx.vg_ctx = vg_pending if (save and not has_att and not state0) else None
         ctx.att_saved = None
         ctx.xw_late = None
         if save:
@@ -266,13 +269,25 @@ class _DecoderFn(torch.autograd.Function):
         # and add onto these disjoint token columns in either order.
         emb_direct = direct is not None and 'emb' in direct
         out_emb = direct['emb'] if emb_direct else empty
+        # concat model with direct slots: the video-gate / FeatPool backward
+        # and the W_ih / W_hh row unpacking run inside the engine, right after
+        # the reverse loop (third streamed DP slice)
+        vg_bwd, vg_nf, vg_p = [], 0, 0.0
+        vg_ctx, ctx.vg_ctx = getattr(ctx, 'vg_ctx', None), None
+        if (vg_ctx is not None and emb_direct and 'fp_w0' in direct and eng.layers == 1
+                and not ctx.state0):
+            fc, xs, wsd, vg_p, vg_nf = vg_ctx
+            vg_bwd = ([eng.dst_ie, eng.dst_hh, direct['wih'], direct['whh'],
+                       eng.model.core.rnn.weight_ih_l0.detach(), fc]
+                      + [direct['fp_w%d' % f] for f in range(vg_nf)]
+                      + [direct['fp_b%d' % f] for f in range(vg_nf)] + list(xs) + list(wsd))
         res = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
             ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell,
             ctx.state0, eng.upper_operands(ctx.up_saved), ctx.logit_b, eng.exp_fix_rows,
-            vdiv, xw if ctx.store_exp else empty)
+            vdiv, xw if ctx.store_exp else empty, vg_bwd, vg_nf, float(vg_p))
         ctx.logit_b = None
         ctx.up_saved = None
         d_up = []
@@ -294,10 +309,14 @@ class _DecoderFn(torch.autograd.Function):
             d_emb = None
         E = eng.E
         # packed gate rows -> the PyTorch weights' rows (unused slots dropped)
-        d_ie = dWx[:, :E].index_select(0, eng.dst_ie)
-        d_hh = dWx[:, E:].index_select(0, eng.dst_hh)
+        if not vg_bwd:
+            d_ie = dWx[:, :E].index_select(0, eng.dst_ie)
+            d_hh = dWx[:, E:].index_select(0, eng.dst_hh)
         w_ih_shape, emb_shape = ctx.shapes
-        if emb_direct:
+        if vg_bwd:  # (written by the engine)
+            d_wih = d_whh = None
+            eng._vg_done = True
+        elif emb_direct:
             direct['wih'][:, :E].copy_(d_ie)
             direct['whh'].copy_(d_hh)
             d_wih = d_whh = None

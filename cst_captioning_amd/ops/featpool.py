@@ -71,11 +71,20 @@ class _FeatPoolVgateFn(torch.autograd.Function):
         vg = eng.pack_rows(torch.mm(fc, w_iv.t()), eng.src_ie, 1)
         ctx.eng, ctx.p, ctx.nf, ctx.wih_shape = eng, p, nf, w_ih.shape
         ctx.save_for_backward(fc, *xs, *wsd)
+        # the decoder forward that consumes vg takes these, so its backward
+        # can run this node's backward inside the engine (vg_bwd)
+        eng._vg_pending = (fc, list(xs), wsd, p, nf)
         return vg
 
     @staticmethod
     def backward(ctx, dvg):
         eng, nf = ctx.eng, ctx.nf
+        if getattr(eng, '_vg_done', False):
+            # the decoder backward already ran this node's backward (vg_bwd)
+            # and wrote W_ih's video columns and the FeatPool gradient slots
+            eng._vg_done = False
+            eng.take_video_slots()
+            return (None,) * (4 + 4 * nf)
         fc, *rest = ctx.saved_tensors
         xs, ws = list(rest[:nf]), list(rest[nf:])
         E = eng.E

@@ -272,9 +272,13 @@ class FlatGradBucket:
 
     def set_groups(self, groups, ctx):
         """Leading slices reduced as soon as the backward marks them final:
-        ``groups`` = [params of slice 0, params of slice 1] (at most two; they
-        must be the buffer's leading parameters, in order).  The fused
-        backward records the matching events (engine ``set_grad_events``)."""
+        ``groups`` = [params of slice 0, params of slice 1(, slice 2)] (at
+        most three; they must be the buffer's leading parameters, in order).
+        The fused backward records the matching events (engine
+        ``set_grad_events``): vocab head, embedding, and for the concat model
+        W_ih + FeatPool (the video-gate backward done inside the engine)."""
+        assert 1 <= len(groups) <= 3, 'one to three streamed slices'
+
         self.groups = []
         off = 0
         want = [p for g in groups for p in g]
@@ -299,7 +303,7 @@ class FlatGradBucket:
     @staticmethod
     def _event_counts():
         from .. import _ext
-        return tuple(_ext.ops().grad_event_count(k) for k in range(2))
+        return tuple(_ext.ops().grad_event_count(k) for k in range(3))
 
     def mark_start(self):
         """Record the step-start event on the current stream before a step's

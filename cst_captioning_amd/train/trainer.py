@@ -90,7 +90,17 @@ class Trainer:
         # bucket order = the order the fused backward finalises gradients:
         # vocab head (under the reverse loop), embedding (post-loop tail), rest
         early = [model.logit.weight, model.logit.bias]
-        self.bucket = FlatGradBucket(model.parameters(), first=early + [model.embed.weight],
+        # concat model on the engine: W_ih and the FeatPool parameters are
+        # final shortly after the reverse loop (the engine runs the video-gate
+        # backward there: decoder_engine ``vg_bwd``), a third streamed slice
+        third = []
+        if (engine is not None and not engine.attention and not engine.standard
+                and engine.layers == 1 and hasattr(model, 'feat_pool')):
+            third = [model.core.rnn.weight_ih_l0] + \
+                [m[0].weight for m in model.feat_pool.feat_list] + \
+                [m[0].bias for m in model.feat_pool.feat_list]
+        self.bucket = FlatGradBucket(model.parameters(),
+                                     first=early + [model.embed.weight] + third,
                                      world_size=self.ctx.world_size,
                                      wire=getattr(opt, 'grad_wire', 'fp32'),
                                      update=getattr(opt, 'dp_update', 'allreduce'))
@@ -102,7 +112,8 @@ class Trainer:
                 and not getattr(opt, 'no_early_allreduce', 0) and self.bucket.wire == 'fp32'
                 and not self.bucket.sharded):
             from .. import _ext
-            self.bucket.set_groups([early, [model.embed.weight]], self.ctx)
+            self.bucket.set_groups([early, [model.embed.weight]] + ([third] if third else []),
+                                   self.ctx)
             _ext.ops().set_grad_events(True)
         if engine is not None:
             # the fused backward writes the vocab-head, embedding and LSTM

@@ -20,7 +20,7 @@ import torch
 # StampSlot: forward 0..2, backward 0..10)
 TRAINER = ['step', 'rollout_enq', 'greedy_begin', 'greedy_end', 'sample_scores', 'loss',
            'bwd_end', 'adam_begin', 'adam_end', 'ptab_end', 'x_end', 'gathered', 'prev_end',
-           'comm0', 'comm1']
+           'comm0', 'comm1', 'comm2']
 # executor slots 0..2 (csrc), 3: the decode's prologue (video gates) done (Python)
 FWD = ['begin', 'step0', 'end', 'vgate']
 BWD = ['begin', 'onehot', 'dhd0', 'dhd', 'loop0', 'loop', 'dw', 'side', 'toksum', 'tokgemm',

@@ -13,7 +13,8 @@ Headline-like width (LSTM 512, 320 caption rows, L = 30, V = 4,000): SCST
 steps captured and replayed as HIP graphs around the streamed bucket
 all-reduce (parallel/dist.py).  Device stamps (utils/stamps.py) are on: the
 comm stream stamps ``comm0`` right after it waited for the vocab-head
-slice's event and ``comm1`` after the embedding slice's; the replayed graph
+slice's event, ``comm1`` after the embedding slice's and ``comm2`` after the
+W_ih + FeatPool slice's; the replayed graph
 stamps ``bwd_end`` when the whole backward is done.  Saves the stamps of a
 few replayed steps and whether every step's backward recorded its slice
 events."""
@@ -65,7 +66,8 @@ def main(out):
             runs.append(stamps.read())
     stamps.disable()
     torch.save({'stamps': runs, 'events_ok': oks, 'graphed': tr._graph is not None,
-                'comm_priority': tr.bucket.comm.priority}, out)
+                'comm_priority': tr.bucket.comm.priority, 'n_groups': len(tr.bucket.groups)},
+               out)
     dist.destroy_process_group()
 
 

@@ -141,3 +141,12 @@ def test_dp_slice_allreduce_starts_inside_the_backward(tmp_path):
         # the vocab head is final under the reverse loop, long before the tail
         assert st['comm0'] < st['bwd_end'] - 50.0, sorted(st.items(), key=lambda kv: kv[1])
         assert st['comm0'] > st.get('bwd.begin', 0.0), sorted(st.items(), key=lambda kv: kv[1])
+        # the third slice (W_ih + FeatPool: the video-gate backward runs in
+        # the engine on a side stream right after the loop) starts after the
+        # loop and before the remainder is reduced (behind adam_begin).  At
+        # this small width it lands within ~10 us of bwd_end either side; at
+        # the headline width ~290 us before it (scripts/dp_overlap_stamps.py,
+        # profiles/r5/dp_model_n8.md)
+        assert 'comm2' in st and st['bwd.loop'] < st['comm2'] < st['adam_begin'], \
+            sorted(st.items(), key=lambda kv: kv[1])
+        assert r['n_groups'] == 3

@@ -586,7 +586,7 @@ def test_exp_store_lse_jump_rows_recomputed():
     res = ops.decoder_backward(wx, wlog, emb, lse.contiguous(), Es, hd.contiguous(), gates, c_all,
                                h_all, seq, torch.empty(0, dtype=torch.long, device=DEV), toks,
                                dg_sel, empty, 0.0, torch.empty(0, dtype=torch.int32, device=DEV),
-                               empty, empty, 0, [], empty, empty, 0, [], [], blog, fix_total, 1, empty)
+                               empty, empty, 0, [], empty, empty, 0, [], [], blog, fix_total, 1, empty, [], 0, 0.0)
     torch.cuda.synchronize()
     assert int(fix_total) == n_jump
     dWlog, dblog = res[1], res[2]
@@ -606,7 +606,7 @@ def test_exp_store_lse_jump_rows_recomputed():
                                 c_all, h_all, seq, torch.empty(0, dtype=torch.long, device=DEV),
                                 toks, dg_sel, empty, 0.0,
                                 torch.empty(0, dtype=torch.int32, device=DEV), empty, empty, 0,
-                                [], empty, empty, 0, [], [], empty, empty, 1, empty)
+                                [], empty, empty, 0, [], [], empty, empty, 1, empty, [], 0, 0.0)
     bad = res0[1]
     assert (not torch.isfinite(bad).all()) or (bad - ref_w).norm() / ref_w.norm() > 0.1
     # X = E W from the rollout (engine.cpp "X in the rollout"): the listed rows'
@@ -618,7 +618,7 @@ def test_exp_store_lse_jump_rows_recomputed():
                                 c_all, h_all, seq, torch.empty(0, dtype=torch.long, device=DEV),
                                 toks, dg_sel, empty, 0.0,
                                 torch.empty(0, dtype=torch.int32, device=DEV), empty, empty, 0,
-                                [], empty, empty, 0, [], [], blog, fix2, 1, xw)
+                                [], empty, empty, 0, [], [], blog, fix2, 1, xw, [], 0, 0.0)
     torch.cuda.synchronize()
     assert int(fix2) == n_jump
     for k in (0, 1, 2, 3, 4):  # dWx (the loop's dG), dWlog, dblog, d_emb, d_vgate
