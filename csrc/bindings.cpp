@@ -89,6 +89,7 @@ void stamp_now(int64_t slot);
 int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
 at::Tensor att_mfma_phases(at::Tensor gv, at::Tensor P, at::Tensor wa, at::Tensor ba, int64_t R);
+at::Tensor wgrad_tn(at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -178,4 +179,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wall_clock_khz", &cst::wall_clock_khz);
   m.def("vocab_x", &cst::vocab_x);
   m.def("att_mfma_phases", &cst::att_mfma_phases);
+  m.def("wgrad_tn", &cst::wgrad_tn);
 }

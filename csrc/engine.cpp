@@ -579,6 +579,40 @@ std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
 //    (4H x H), W_ih (fp32 parameter), fc (FeatPool output, B x Fv),
 //    FeatPool weight slots x vg_nf, bias slots x vg_nf, inputs x vg_nf,
 //    weights x vg_nf}; vg_p the FeatPool dropout.
+// C = A^T B over the first K rows of the bf16 row-major operands A (K x >= M)
+// and B (K x >= N) through the hand-written split-K kernel (kernels/wgrad.hip):
+// rows [0, M0) of C into C0 (row stride ldc0), rows [M0, M) into C1.  Returns
+// false (nothing launched) when the shapes do not fit the kernel.
+static bool wgrad_tn_into(const at::Tensor& A, int64_t lda, const at::Tensor& B, int64_t ldb,
+                          int64_t M, int64_t N, int64_t K, float* C0, int64_t ldc0, int64_t M0,
+                          float* C1, int64_t ldc1, hipStream_t st) {
+  if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16 ||
+      !wgrad_tn_ok(M, N, K, lda, ldb, A.data_ptr(), B.data_ptr()))
+    return false;
+  const int S = wgrad_tn_splits(M, N, K);
+  at::Tensor ws;
+  if (S > 1) ws = at::empty({S, M, N}, A.options().dtype(at::kFloat));
+  WgradArgs g{reinterpret_cast<const uint16_t*>(A.data_ptr()), lda,
+              reinterpret_cast<const uint16_t*>(B.data_ptr()), ldb, (int)M, (int)N, (int)K, S, 0,
+              S > 1 ? ws.data_ptr<float>() : nullptr, C0, ldc0, (int)M0, C1, ldc1};
+  launch_wgrad_tn(g, st);
+  return true;
+}
+
+// test entry: C (M x N) fp32 = A[:K]^T B[:K]
+at::Tensor wgrad_tn(at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
+                  A.size(0) >= K && B.size(0) >= K && A.size(1) >= M && B.size(1) >= N,
+              "wgrad_tn: operand shapes");
+  at::Tensor C = at::empty({M, N}, A.options().dtype(at::kFloat));
+  TORCH_CHECK(wgrad_tn_into(A, A.stride(0), B, B.stride(0), M, N, K, C.data_ptr<float>(), N, M,
+                            nullptr, 0, cur_stream()),
+              "wgrad_tn: shapes not supported (M, N multiples of 128, 16-byte rows)");
+  return C;
+}
+
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
                                          at::Tensor lse, at::Tensor logits16,
                                          at::Tensor hdrop_all, at::Tensor gates_all,
@@ -1066,7 +1100,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // recurrent columns dW_hh = sum_t dG_t^T h_{t-1} (+ dG_0^T h0 with an
   // initial state); with attention the extra rows of [dG | dq]^T h_prev are dW_q
   auto whh_grad = [&]() {
-    if (n_steps > 1) {
+    if (n_steps > 1 && h_all.is_contiguous() &&
+        wgrad_tn_into(dGx.narrow(0, R, (n_steps - 1) * R), KD, h_all, H, KD, H,
+                      (n_steps - 1) * R, dWx.data_ptr<float>() + E, E + H, H4,
+                      has_att ? dWq.data_ptr<float>() : nullptr, H, st)) {
+      // (hand-written split-K MFMA kernel, kernels/wgrad.hip: rows [0, 4H) of
+      // [dG | dq]^T h_prev into dW_hh's columns of dWx, the dq rows into dW_q)
+    } else if (n_steps > 1) {
       at::Tensor wh;
       wh = grouped_wgrad(dGx.narrow(0, R, (n_steps - 1) * R),
                          h_all.narrow(0, 0, n_steps - 1).reshape({(n_steps - 1) * R, H}),
@@ -1114,7 +1154,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     for (int64_t g = 8; g >= 2; --g)
       if (V % g == 0 && V / g >= 512) { nk = g; break; }
     at::Tensor dWie = dWx.narrow(1, 0, E);
-    if (nk > 1 && emb.is_contiguous())
+    if (emb.dim() == 2 && emb.stride(1) == 1 && S_tok.is_contiguous() &&
+        wgrad_tn_into(S_tok, H4, emb, emb.stride(0), H4, E, V, dWie.data_ptr<float>(), E + H, H4,
+                      nullptr, 0, st)) {
+      // (hand-written split-K MFMA kernel, kernels/wgrad.hip)
+    } else if (nk > 1 && emb.is_contiguous())
       at::sum_out(dWie,
                   at::bmm(S_tok.view({nk, V / nk, H4}).transpose(1, 2), emb.view({nk, V / nk, E}),
                           at::kFloat),

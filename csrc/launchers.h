@@ -350,6 +350,28 @@ void launch_token_long_zero(const int* ws, int V, int C, float* S32, hipStream_t
 void launch_token_group_sum(const uint16_t* x, int C, int64_t ld, const int* stok,
                             const int* srow, int N, const int* ws, int V, uint16_t* S, float* S32,
                             hipStream_t stream);
+// Weight-gradient GEMM C = A^T B of K-major bf16 operands (kernels/wgrad.hip):
+// A (K x >= M, row stride lda), B (K x >= N, ldb); rows [0, M0) of C go to C0
+// (row stride ldc0), rows [M0, M) to C1 (ldc1).  S > 1: split-K through the
+// fp32 workspace ws (S x M x N) and a fixed-order reduce.  kts is set by the
+// launcher (K-tiles per split).
+struct WgradArgs {
+  const uint16_t* A;
+  int64_t lda;
+  const uint16_t* B;
+  int64_t ldb;
+  int M, N, K, S, kts;
+  float* ws;
+  float* C0;
+  int64_t ldc0;
+  int M0;
+  float* C1;
+  int64_t ldc1;
+};
+bool wgrad_tn_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A,
+                 const void* B);
+int wgrad_tn_splits(int64_t M, int64_t N, int64_t K);
+void launch_wgrad_tn(WgradArgs g, hipStream_t stream);
 // d_vgate (Bv = R / vdiv, G4) fp32 = sum over the n_steps steps and the vdiv
 // rows of each video of the bf16 rows dG (row stride ld, first G4 columns)
 void launch_video_gate_grad(const uint16_t* dG, int64_t ld, int n_steps, int R, int vdiv, int G4,
