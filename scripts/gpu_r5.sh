@@ -14,6 +14,11 @@ if [ -z "$SKIP_TESTS" ]; then
   e=$?; tail -n 3 gpurun_out/pytest_$TAG.log
   [ $e -eq 0 ] || exit $e
 fi
+if [ -z "$SKIP_SMOKE" ]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+    > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
+  tail -n 1 gpurun_out/smoke_$TAG.log
+fi
 if [ -z "$SKIP_BENCH" ]; then
   timeout -k 10 400 python bench.py $BENCH_ARGS > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
   tail -n 1 gpurun_out/bench_$TAG.json | cut -c1-400
