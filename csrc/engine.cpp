@@ -445,9 +445,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   // step 0: fused cell step from (h_{-1}, c_{-1}) = (h0, c0)
   stamp(STAMP_FWD_BEGIN, st);
   if (has_att) run_att(0);
+  // (zero initial state: null h / c, the kernel skips the recurrent GEMM)
   launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
-                       ptab.data_ptr<float>(), reinterpret_cast<uint16_t*>(h0.data_ptr()),
-                       c0.data_ptr<float>(), VG, VDIV, (int)R, (int)H, WHH, h_buf(0, 0),
+                       ptab.data_ptr<float>(),
+                       state0.empty() ? nullptr : reinterpret_cast<uint16_t*>(h0.data_ptr()),
+                       state0.empty() ? nullptr : c0.data_ptr<float>(), VG, VDIV, (int)R, (int)H, WHH, h_buf(0, 0),
                        c_buf(0, 0), hd_buf(0, 0), (int)H, (float)drop_p, RNG, key(0, 0),
                        gates_buf(0, 0), st, nullptr, (int)cell);
   for (int64_t l = 1; l < NL; ++l) upper_step(l, 0);
@@ -813,7 +815,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       // exp-store range guard: rows whose LSE jumped by > 60 since the previous
       // step are listed and recomputed exactly (vocab_grad.hip vgrad_fix)
       const bool guard = blog.defined() && blog.numel() == V;
-      at::Tensor fix = guard ? at::zeros({1 + NR}, i32) : at::Tensor();
+      // (only the row counter fix[0] needs zeroing: the list entries are
+      // written by vgrad_onehot before vgrad_fix reads them)
+      at::Tensor fix = guard ? at::empty({1 + NR}, i32) : at::Tensor();
+      if (guard) (void)hipMemsetAsync(fix.data_ptr(), 0, sizeof(int), side.stream());
       VGradRows va{(int)R, (int)n_steps, (int)T_sel, (int)H, (int)V, lse.data_ptr<float>(),
                    has_sel ? seq.data_ptr<int64_t>() : nullptr,
                    has_sel ? dg_sel.data_ptr<float>() : nullptr,
@@ -1099,11 +1104,11 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   };
   // recurrent columns dW_hh = sum_t dG_t^T h_{t-1} (+ dG_0^T h0 with an
   // initial state); with attention the extra rows of [dG | dq]^T h_prev are dW_q
-  auto whh_grad = [&]() {
+  auto whh_grad = [&](hipStream_t ws) {  // (current stream: ws)
     if (n_steps > 1 && h_all.is_contiguous() &&
         wgrad_tn_into(dGx.narrow(0, R, (n_steps - 1) * R), KD, h_all, H, KD, H,
                       (n_steps - 1) * R, dWx.data_ptr<float>() + E, E + H, H4,
-                      has_att ? dWq.data_ptr<float>() : nullptr, H, st)) {
+                      has_att ? dWq.data_ptr<float>() : nullptr, H, ws)) {
       // (hand-written split-K MFMA kernel, kernels/wgrad.hip: rows [0, 4H) of
       // [dG | dq]^T h_prev into dW_hh's columns of dWx, the dq rows into dW_q)
     } else if (n_steps > 1) {
@@ -1128,10 +1133,21 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // stream before returning.)
   // (starting them only after the main stream's per-token sums measured
   // slower: 3.76-3.81 vs 3.71-3.72 ms, profiles/r3/ab_toksum_first.txt)
-  // The recurrent-weight GEMMs run after the input-token chain on the main
-  // stream (on the idle side stream after the loop, or their late steps'
-  // share on it during the loop, measured slower: they contend with the
-  // input-token chain / the loop, profiles/r4/README_r4.md).
+
+  // The recurrent-weight gradient (hand-written split-K GEMM, kernels/wgrad.hip)
+  // on the first side stream, idle after dW_logit + the bias sums, concurrent
+  // with the input-token chain below: interleaved on one box 3.351-3.386 vs
+  // 3.362-3.402 ms per step after that chain on the main stream
+  // (profiles/r5/tail/ab_ws_*.json; with the round-4 vendor GEMMs the same
+  // move measured slower)
+  {
+    (void)hipEventRecord(aux.ev[4], st);  // the loop's dG rows
+    (void)hipStreamWaitEvent(side.stream(), aux.ev[4], 0);
+    c10::hip::HIPStreamGuard guard(side);
+    whh_grad(side.stream());
+    if (vg_direct) vg_bwd[3].copy_(dWx.narrow(1, E, H).index_select(0, vg_bwd[1]));
+    (void)hipEventRecord(ev_done, side.stream());  // (joined below)
+  }
 
   // 5. input-token gradients through the per-token sums S[v] = sum of the dG
   //    rows whose input token is v (bf16, V x 4H): embedding gradient S W_ie,
@@ -1174,8 +1190,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     (void)hipStreamWaitEvent(st, aux.ev[5], 0);
     if (grad_ev) record_grad_event(aux.grad_ev[2], st, 2);
   }
-  whh_grad();
-  if (vg_direct) vg_bwd[3].copy_(dWx.narrow(1, E, H).index_select(0, vg_bwd[1]));
   at::Tensor dh0;
   if (has_s0)  // step 0's recurrent input h0: dh0 = dG_0 W_hh
     dh0 = at::mm(dG2.narrow(0, 0, R), wx.narrow(1, E, H), at::kFloat);

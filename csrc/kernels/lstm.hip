@@ -72,13 +72,16 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
     pre_px[i] = ptab ? *reinterpret_cast<const float4*>(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u)
                      : make_float4(0.f, 0.f, 0.f, 0.f);
     pre_vg[i] = *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
-    pre_c[i] = c_prev[(int64_t)(row_map ? row_map[r] : r) * H + hu];
+    pre_c[i] = c_prev ? c_prev[(int64_t)(row_map ? row_map[r] : r) * H + hu] : 0.f;
     CST_DCHECK(s_tok[row] >= 0);
     CST_DCHECK(row_map == nullptr || (row_map[r] >= 0 && row_map[r] < R));
   }
 
+  // h_prev == nullptr: zero initial state (step 0 without an initial state),
+  // no recurrent GEMM -- the step is the table gather and the cell
+  const bool zero_h = h_prev == nullptr;
   f32x16 acc[LTile::TM][LTile::TN];
-  {
+  if (!zero_h) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     DmaSrc<BM / 32> a;
     DmaSrc<LB_N / 32> bsrc;
@@ -103,8 +106,10 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
   }
 
   float* C = reinterpret_cast<float*>(lds);
-  store_acc_to_lds<LTile>(acc, C, [](int) { return 0.f; });
-  __syncthreads();
+  if (!zero_h) {
+    store_acc_to_lds<LTile>(acc, C, [](int) { return 0.f; });
+    __syncthreads();
+  }
 
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
@@ -112,7 +117,8 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
   for (int i = 0; i < RPT; ++i) {
     const int row = rg + 16 * i, r = r0 + row;
     if (r < R) {
-      const float4 pre = *reinterpret_cast<const float4*>(C + row * LTile::CSTRIDE + 4 * u);
+      const float4 pre = zero_h ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                : *reinterpret_cast<const float4*>(C + row * LTile::CSTRIDE + 4 * u);
       const float4 vg = pre_vg[i], px = pre_px[i];
       const CellFwd cf = cell_fwd(cell, pre.x + vg.x + px.x, pre.y + vg.y + px.y,
                                   pre.z + vg.z + px.z, pre.w + vg.w + px.w, pre_c[i]);

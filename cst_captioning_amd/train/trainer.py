@@ -336,16 +336,19 @@ class Trainer:
                 loss, extra = self.rl_loss(data, scb)
             else:
                 loss, extra = self.xe_loss(data)
-        stamps.base('bwd')
-        loss.backward()
-        stamps.base(None)
-        stamps.mark('bwd_end')
-        self.timer.mark('backward')
+        # (the flag is enqueued before the backward: its few small launches run
+        # while the backward's first operand, X = E W, is still computing,
+        # instead of between the backward and the Adam pass)
         skip = None
         if getattr(opt, 'nan_guard', 1):
             skip = ~torch.isfinite(loss.detach())
             if self.ctx.enabled and not self.bucket.sharded:  # every rank must skip
                 self.bucket.set_flag(skip)  # together: the flag rides the all-reduce
+        stamps.base('bwd')
+        loss.backward()
+        stamps.base(None)
+        stamps.mark('bwd_end')
+        self.timer.mark('backward')
         extra.update(loss=loss.detach(), mixer_from=mixer_from, scb_captions=scb)
         return extra, skip
 
