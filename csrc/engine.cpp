@@ -806,42 +806,58 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     if (grad_ev) record_grad_event(aux.grad_ev[0], side.stream(), 0);
     if (early_comm) (void)hipStreamWaitEvent(reinterpret_cast<hipStream_t>(comm_stream), ev_done, 0);
   };
+  // alpha, one-hot terms folded into E (dS = diag(alpha) E'); exp-store range
+  // guard: rows whose LSE jumped by > 60 since the previous step are listed
+  // and recomputed exactly (vocab_grad.hip vgrad_fix)
+  auto onehot_pass = [&](hipStream_t s) {
+    const bool guard = blog.defined() && blog.numel() == V;
+    // (only the row counter fix[0] needs zeroing: the list entries are
+    // written by vgrad_onehot before vgrad_fix reads them)
+    at::Tensor fix = guard ? at::empty({1 + NR}, i32) : at::Tensor();
+    if (guard) (void)hipMemsetAsync(fix.data_ptr(), 0, sizeof(int), s);
+    VGradRows va{(int)R, (int)n_steps, (int)T_sel, (int)H, (int)V, lse.data_ptr<float>(),
+                 has_sel ? seq.data_ptr<int64_t>() : nullptr,
+                 has_sel ? dg_sel.data_ptr<float>() : nullptr,
+                 has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
+                 has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
+                 has_xe ? dg_xe.size(1) : 0, guard ? fix.data_ptr<int>() : nullptr,
+                 ptr_or_null<float>(oh_a), ptr_or_null<int>(oh_ys), ptr_or_null<float>(oh_b),
+                 ptr_or_null<int>(oh_yx), have_x ? dHd.data_ptr<float>() : nullptr};
+    launch_vgrad_onehot(va, reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl,
+                        alpha.data_ptr<float>(), s);
+    if (guard) {
+      TORCH_CHECK(blog.is_cuda() && blog.scalar_type() == at::kFloat && blog.is_contiguous(),
+                  "blog must be a contiguous fp32 GPU tensor");
+      TORCH_CHECK(!fix_total.defined() || fix_total.numel() == 0 ||
+                      (fix_total.is_cuda() && fix_total.scalar_type() == at::kInt),
+                  "fix_total must be an int32 GPU tensor");
+      launch_vgrad_fix(va, reinterpret_cast<const uint16_t*>(hd2.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
+                       reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl, alpha.data_ptr<float>(),
+                       ptr_or_null<int>(fix_total), s);
+    }
+    stamp(STAMP_BWD_ONEHOT, s);
+  };
   stamp(STAMP_BWD_BEGIN, st);
+  // Forward X: the loop's first operands are the row weights of this pass and
+  // X itself, so the pass runs on the main stream -- no hop to the side stream
+  // and back before the loop; the side stream's dW work waits for it.
+  // (3.416-3.427 vs 3.429-3.431 ms per step with the pass on the side stream,
+  // interleaved on one box, profiles/r5/tail/ab_ohm_*.json)
+  const bool oh_main = have_x && !ds_ready;
+  if (oh_main) {
+    onehot_pass(st);
+    stamp(STAMP_BWD_DHD0, st);
+    dhd_chunks.clear();  // (X is final: the loop waits for no chunk)
+  }
   (void)hipEventRecord(ev_ready, st);
+  // (the side stream's dW work held back until the first 1 / 2 reverse steps
+  // are enqueued, so they do not share the CUs with the GEMM's first wave,
+  // measured slower: 3.462-3.489 ms per step, profiles/r5/tail/ab_ohm_d*.json)
   (void)hipStreamWaitEvent(side.stream(), ev_ready, 0);
   {
     c10::hip::HIPStreamGuard guard(side);
-    if (!ds_ready) {  // alpha, one-hot terms folded into E (dS = diag(alpha) E')
-      // exp-store range guard: rows whose LSE jumped by > 60 since the previous
-      // step are listed and recomputed exactly (vocab_grad.hip vgrad_fix)
-      const bool guard = blog.defined() && blog.numel() == V;
-      // (only the row counter fix[0] needs zeroing: the list entries are
-      // written by vgrad_onehot before vgrad_fix reads them)
-      at::Tensor fix = guard ? at::empty({1 + NR}, i32) : at::Tensor();
-      if (guard) (void)hipMemsetAsync(fix.data_ptr(), 0, sizeof(int), side.stream());
-      VGradRows va{(int)R, (int)n_steps, (int)T_sel, (int)H, (int)V, lse.data_ptr<float>(),
-                   has_sel ? seq.data_ptr<int64_t>() : nullptr,
-                   has_sel ? dg_sel.data_ptr<float>() : nullptr,
-                   has_xe ? labels.data_ptr<int64_t>() + 1 : nullptr,
-                   has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
-                   has_xe ? dg_xe.size(1) : 0, guard ? fix.data_ptr<int>() : nullptr,
-                   ptr_or_null<float>(oh_a), ptr_or_null<int>(oh_ys), ptr_or_null<float>(oh_b),
-                   ptr_or_null<int>(oh_yx), have_x ? dHd.data_ptr<float>() : nullptr};
-      launch_vgrad_onehot(va, reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl,
-                          alpha.data_ptr<float>(), side.stream());
-      if (guard) {
-        TORCH_CHECK(blog.is_cuda() && blog.scalar_type() == at::kFloat && blog.is_contiguous(),
-                    "blog must be a contiguous fp32 GPU tensor");
-        TORCH_CHECK(!fix_total.defined() || fix_total.numel() == 0 ||
-                        (fix_total.is_cuda() && fix_total.scalar_type() == at::kInt),
-                    "fix_total must be an int32 GPU tensor");
-        launch_vgrad_fix(va, reinterpret_cast<const uint16_t*>(hd2.data_ptr()),
-                         reinterpret_cast<const uint16_t*>(wlog.data_ptr()), blog.data_ptr<float>(),
-                         reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl, alpha.data_ptr<float>(),
-                         ptr_or_null<int>(fix_total), side.stream());
-      }
-      stamp(STAMP_BWD_ONEHOT, side.stream());
-    }
+    if (!ds_ready && !oh_main) onehot_pass(side.stream());
     // X = E' W, chunk by chunk; the reverse loop reads alpha X (row scales at
     // load), and the scaled Hd rows of the dW GEMM are formed under it
     for (size_t ci = 0; ci < dhd_chunks.size(); ++ci) {
