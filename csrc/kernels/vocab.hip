@@ -455,14 +455,16 @@ void launch_att_mfma_fwd(const AttMfmaArgs& a, hipStream_t stream) {
 // token-selection modes of one decode step
 enum SelMode : int { SEL_GT = 0, SEL_SAMPLE = 1, SEL_GREEDY = 2, SEL_SS = 3 };
 
-// 32 lanes per row (a half wavefront), 8 rows per 256-thread block: each lane
-// merges ~3 tiles, then a 5-step shuffle tree finishes the row.
-// 64-thread blocks (2 rows): 640 blocks at R = 1280 spread the combine and
-// the cell epilogue's 33 MB of traffic over every CU.
-constexpr int CMB_LANES = 32, CMB_THREADS = 64, CMB_ROWS = CMB_THREADS / CMB_LANES;
+// One wavefront per row (64-thread blocks, 1,280 at R = 1280): each lane
+// merges 2 tiles (6-step shuffle tree) and owns 8 of the cell epilogue's
+// hidden units, so the chain partials -> merge -> token -> table row -> cell
+// runs with half the per-lane work of the earlier half-wave rows (3.331-3.345
+// vs 3.367-3.380 ms per training step, interleaved on one box,
+// profiles/r5/combine/ab_c64_*.json).  LANES stays a template parameter.
+constexpr int CMB_LANES = 64, CMB_THREADS = 64, CMB_ROWS = CMB_THREADS / CMB_LANES;
 // end-of-sequence flags: per decode step CMB_CNT_SLOTS slots, one 128-byte
 // line apart (see vocab_combine_kernel)
-constexpr int CMB_CNT_SLOTS = CMB_LANES, CMB_CNT_STRIDE = 32;
+constexpr int CMB_CNT_SLOTS = 64, CMB_CNT_STRIDE = 32;
 int combine_count_ints_per_step() { return CMB_CNT_SLOTS * CMB_CNT_STRIDE; }
 
 // Cell epilogue of the NEXT decode step, applied as soon as its input token
@@ -566,6 +568,7 @@ __device__ __forceinline__ int finish_row(const RowStat& a, int r, const RowSel&
   return (int)tok;
 }
 
+template <int LANES>
 __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     const VocabPartial* __restrict__ part, int n_vt, int R, float* __restrict__ lse_out,
     int64_t* __restrict__ tok_out, int64_t tok_stride, float* __restrict__ g_sel,
@@ -575,8 +578,8 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     uint8_t* __restrict__ unfinished, CellArgs cell) {
   __shared__ int s_nonzero;
   int tok_final = 0;
-  const int sub = threadIdx.x & (CMB_LANES - 1);
-  const int r = blockIdx.x * CMB_ROWS + (threadIdx.x / CMB_LANES);
+  const int sub = threadIdx.x & (LANES - 1);
+  const int r = blockIdx.x * (CMB_THREADS / LANES) + (threadIdx.x / LANES);
   const bool valid = r < R;
   if (threadIdx.x == 0) s_nonzero = 0;
   // The row's tile partials are loaded unconditionally (clamped index,
@@ -588,19 +591,19 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   // the partials, they delayed the merge; requested after the merge, their
   // latency added to the chain).  Only the token's table row waits for the
   // merge.
-  constexpr int CMB_MAXP = 4;  // n_vt <= 128: V <= 16384 at 128-wide tiles
-  const bool fastp = n_vt <= CMB_MAXP * CMB_LANES;
+  constexpr int CMB_MAXP = 128 / LANES;  // n_vt <= 128: V <= 16384 at 128-wide tiles
+  const bool fastp = n_vt <= CMB_MAXP * LANES;
   VocabPartial pp[CMB_MAXP];
   if (valid && fastp) {
 #pragma unroll
     for (int k = 0; k < CMB_MAXP; ++k)
-      pp[k] = part[(int64_t)min(sub + k * CMB_LANES, n_vt - 1) * R + r];
+      pp[k] = part[(int64_t)min(sub + k * LANES, n_vt - 1) * R + r];
   }
   const bool do_cell = cell.pre != nullptr && tok_out != nullptr;
   // one batch of CELL_U units per lane covers H <= 512 (every lane of the row
   // owns units sub, sub + 32, ...); larger H loads per batch after the merge
-  constexpr int CELL_U = 16;
-  const bool pre_early = do_cell && valid && cell.H <= CMB_LANES * CELL_U;
+  constexpr int CELL_U = 512 / LANES;
+  const bool pre_early = do_cell && valid && cell.H <= LANES * CELL_U;
   float4 pe[CELL_U];
   float ce[CELL_U];
   uint2 ve[CELL_U];
@@ -609,7 +612,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     const float* prow = cell.pre + (int64_t)r * 4 * H;
 #pragma unroll
     for (int k = 0; k < CELL_U; ++k) {
-      const int u = min(sub + k * CMB_LANES, H - 1);  // (clamped: no branch)
+      const int u = min(sub + k * LANES, H - 1);  // (clamped: no branch)
       pe[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
       ce[k] = cell.c_prev[(int64_t)r * H + u];
       if (cell.vg16 != nullptr)
@@ -624,34 +627,37 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     gt_pre = gt ? gt[(int64_t)r * gt_stride] : 0;
     unf_pre = unfinished == nullptr || unfinished[r] != 0;
   }
-  // "some row emitted a non-EOS token at the previous step": one flag slot
-  // per lane of the half-wave (CMB_CNT_SLOTS cache-line-strided slots, written
-  // by the blocks of that step), OR-reduced across the 32 lanes
+  // "some row emitted a non-EOS token at the previous step": CMB_CNT_SLOTS
+  // cache-line-strided flag slots (written by the blocks of that step), read
+  // by the row's lanes and OR-reduced across them
   int nz_prev = 1;
   if (counts != nullptr && count_step > 1 && tok_out != nullptr) {
-    nz_prev = counts[((count_step - 1) * CMB_CNT_SLOTS + sub) * CMB_CNT_STRIDE];
+    nz_prev = 0;
 #pragma unroll
-    for (int o = 1; o < CMB_LANES; o <<= 1) nz_prev |= __shfl_xor(nz_prev, o, 64);
+    for (int k = sub; k < CMB_CNT_SLOTS; k += LANES)
+      nz_prev |= counts[((count_step - 1) * CMB_CNT_SLOTS + k) * CMB_CNT_STRIDE];
+#pragma unroll
+    for (int o = 1; o < LANES; o <<= 1) nz_prev |= __shfl_xor(nz_prev, o, 64);
   }
   const bool dead_pre = nz_prev == 0;
   RowStat a = {-INFINITY, 0.f, -INFINITY, 0.f, -INFINITY, -INFINITY, 0x7fffffff, 0x7fffffff};
   if (valid && fastp) {
 #pragma unroll
     for (int k = 0; k < CMB_MAXP; ++k) {
-      if (sub + k * CMB_LANES < n_vt) {
+      if (sub + k * LANES < n_vt) {
         const VocabPartial& p = pp[k];
         merge_stat(a, p.m, p.s, p.zval, p.zlogit, p.zidx, p.m, p.xidx, p.xtgt);
       }
     }
   } else if (valid) {
 #pragma unroll 4
-    for (int t = sub; t < n_vt; t += CMB_LANES) {
+    for (int t = sub; t < n_vt; t += LANES) {
       const VocabPartial p = part[(int64_t)t * R + r];
       merge_stat(a, p.m, p.s, p.zval, p.zlogit, p.zidx, p.m, p.xidx, p.xtgt);
     }
   }
 #pragma unroll
-  for (int o = 1; o < CMB_LANES; o <<= 1) {
+  for (int o = 1; o < LANES; o <<= 1) {
     merge_stat(a, __shfl_xor(a.m, o, 64), __shfl_xor(a.s, o, 64), __shfl_xor(a.zv, o, 64),
                __shfl_xor(a.zl, o, 64), __shfl_xor(a.zi, o, 64), __shfl_xor(a.xm, o, 64),
                __shfl_xor(a.xi, o, 64), __shfl_xor(a.xt, o, 64));
@@ -665,7 +671,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   }
   if (do_cell) {
     // the row's 32 lanes: lane k owns hidden units k, k + 32, ... (coalesced)
-    const int tk = __shfl(tok_final, (int)(threadIdx.x & 63) & ~(CMB_LANES - 1), 64);
+    const int tk = __shfl(tok_final, (int)(threadIdx.x & 63) & ~(LANES - 1), 64);
     if (valid) {
       const int H = cell.H;
       const float* prow = cell.pre + (int64_t)r * 4 * H;
@@ -675,7 +681,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
       // batches of CELL_U units (all of H = 512 in one): every load of a
       // batch is issued before the first store (the stores could alias the
       // inputs as far as the compiler knows, which would serialise the loads)
-      for (int u0 = sub; u0 < H; u0 += CMB_LANES * CELL_U) {
+      for (int u0 = sub; u0 < H; u0 += LANES * CELL_U) {
         float4 p[CELL_U], x[CELL_U];
         float cp[CELL_U];
         uint2 vq[CELL_U];
@@ -685,12 +691,12 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
             p[k] = pe[k];
             cp[k] = ce[k];
             vq[k] = ve[k];
-            x[k] = *reinterpret_cast<const float4*>(trow + 4 * min(u0 + k * CMB_LANES, H - 1));
+            x[k] = *reinterpret_cast<const float4*>(trow + 4 * min(u0 + k * LANES, H - 1));
           }
         } else {
 #pragma unroll
           for (int k = 0; k < CELL_U; ++k) {
-            const int u = u0 + k * CMB_LANES;
+            const int u = u0 + k * LANES;
             if (u < H) {
               p[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
               x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
@@ -711,7 +717,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
         }
 #pragma unroll
         for (int k = 0; k < CELL_U; ++k) {
-          const int u = u0 + k * CMB_LANES;
+          const int u = u0 + k * LANES;
           if (u < H) {
             const CellFwd cf = cell_fwd(cell.cell, p[k].x + x[k].x, p[k].y + x[k].y,
                                         p[k].z + x[k].z, p[k].w + x[k].w, cp[k]);
@@ -881,11 +887,10 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
     cell = CellArgs{cl->pre, cl->vg16, cl->ptab, cl->c_prev, cl->c_out, cl->h_out,
                     cl->hdrop_out, cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step, cl->cell};
   }
-  hipLaunchKernelGGL(vocab_combine_kernel, dim3((R + CMB_ROWS - 1) / CMB_ROWS), dim3(CMB_THREADS), 0,
-                     stream,
-                     (const VocabPartial*)part, n_vt, R, lse_out, tok_out, tok_stride, g_sel,
-                     gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode, ss_prob, rng, step,
-                     counts, count_step, unfinished, cell);
+  hipLaunchKernelGGL(vocab_combine_kernel<CMB_LANES>, dim3((R + CMB_ROWS - 1) / CMB_ROWS),
+                     dim3(CMB_THREADS), 0, stream, (const VocabPartial*)part, n_vt, R, lse_out,
+                     tok_out, tok_stride, g_sel, gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode,
+                     ss_prob, rng, step, counts, count_step, unfinished, cell);
   post_launch("vocab_combine_kernel", stream);
 }
 
