@@ -112,6 +112,7 @@ struct DeviceAux {
   std::vector<hipEvent_t> ev;
   c10::hip::HIPStream side[2];
   hipEvent_t grad_ev[3];  // data parallelism: gradient groups final (set_grad_events)
+  hipEvent_t fwd_ev[2];   // decoder_forward: step 0's exp-store conversion fork / join
 };
 static DeviceAux& device_aux(int dev_index) {
   static std::map<int, DeviceAux*> aux;
@@ -122,6 +123,7 @@ static DeviceAux& device_aux(int dev_index) {
     a->ev.resize(6 + MAX_DHD_CHUNKS);
     for (auto& e : a->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     for (auto& e : a->grad_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    for (auto& e : a->fwd_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     it = aux.emplace(dev_index, a).first;
   }
   return *it->second;
@@ -457,6 +459,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   // the recurrent GEMM of step t+1 (pre = h_t W_hh^T + vgate, layer 0), then
   // the combine picks token t+1 and applies step t+1's cell epilogue (pre +
   // P[token]); the upper layers of step t+1 follow.
+  bool conv_join = false;
   for (int64_t t = 0; t < n_steps; ++t) {
     const bool next = t + 1 < n_steps;
     uint16_t* hd = hd_buf(NL - 1, t);
@@ -512,13 +515,23 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                            use_counts ? counts.data_ptr<int>() : nullptr, (int)(t + 1),
                            use_unfinished ? unfinished.data_ptr<uint8_t>() : nullptr, st,
                            next ? &cl : nullptr);
-    if (save && store_exp && t == 0)
+    if (save && store_exp && t == 0) {
+      // only the backward reads step 0's exp store: the conversion runs on a
+      // side stream, off the decode chain, joined after the loop
+      DeviceAux& aux = device_aux((int)dev.index());
+      const hipStream_t cs = aux.side[1].stream();
+      (void)hipEventRecord(aux.fwd_ev[0], st);
+      (void)hipStreamWaitEvent(cs, aux.fwd_ev[0], 0);
       launch_vocab_exp_convert(reinterpret_cast<uint16_t*>(logits16[0].data_ptr()), ldl, (int)V,
-                               (int)R, lse[0].data_ptr<float>(), st);
+                               (int)R, lse[0].data_ptr<float>(), cs);
+      (void)hipEventRecord(aux.fwd_ev[1], cs);
+      conv_join = true;
+    }
     if (next)
       for (int64_t l = 1; l < NL; ++l) upper_step(l, t + 1);
     if (t == 0) stamp(STAMP_FWD_STEP0, st);
   }
+  if (conv_join) (void)hipStreamWaitEvent(st, device_aux((int)dev.index()).fwd_ev[1], 0);
   stamp(STAMP_FWD_END, st);
   // saved: {logits16, hd of the top layer (vocab input), layer 0's gates, c, h}
   // (+ {alpha_all, q_all, u_all}) (+ {h, c, gates of layer l, hd of layer l-1} per l >= 1)

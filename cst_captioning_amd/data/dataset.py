@@ -96,7 +96,20 @@ class VideoCaptionDataset:
         """Features/labels uploaded once and cached per device."""
         key = str(device)
         if key not in self._device_cache:
-            d = {'feats': [torch.from_numpy(f).to(device) for f in self.feats]}
+            fs = [torch.from_numpy(f) for f in self.feats]
+            if (len(fs) > 1 and all(f.shape[:-1] == fs[0].shape[:-1] and f.dtype == fs[0].dtype
+                                    and f.shape[-1] % 4 == 0 for f in fs)):
+                # one (N, [C,] sum d) array, the modalities as column views: a batch
+                # is ONE row gather (FeatPool reads column slices with 16-byte
+                # aligned rows) instead of one gather launch per modality
+                cat = torch.cat(fs, -1).to(device)
+                offs = [0]
+                for f in fs:
+                    offs.append(offs[-1] + f.shape[-1])
+                d = {'feats': [cat[..., offs[i]:offs[i + 1]] for i in range(len(fs))],
+                     'feats_cat': (cat, offs)}
+            else:
+                d = {'feats': [f.to(device) for f in fs]}
             if self.has_label:
                 d['labels'] = torch.from_numpy(self.labels).to(device)
             if self.bcmrscores is not None:
@@ -311,7 +324,12 @@ class CaptionLoader:
         keys = set(keys) if keys is not None else {'feats', 'labels', 'masks', 'bcmrscores'}
         out = {}
         if 'feats' in keys:
-            out['feats'] = [f.index_select(0, vid_t) for f in dev['feats']]
+            if 'feats_cat' in dev:
+                cat, offs = dev['feats_cat']
+                g = cat.index_select(0, vid_t)
+                out['feats'] = [g[..., offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+            else:
+                out['feats'] = [f.index_select(0, vid_t) for f in dev['feats']]
         if rows_t is not None:
             if keys & {'labels', 'masks'}:
                 labels = dev['labels'].index_select(0, rows_t)
