@@ -1153,16 +1153,6 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     }
     if (has_s0) dWx.narrow(1, E, H).add_(at::mm(dG2.narrow(0, 0, R).t(), state0[0], at::kFloat));
   };
-  // One GPU: after the loop the main stream's chain (per-token sums, the
-  // input-token GEMMs) outlasts the side stream's dW_logit GEMM + bias column
-  // sums, so the recurrent-weight GEMMs join the side stream (with the
-  // split-K S^T emb below: 3.775-3.799 vs 3.832-3.846 ms per step,
-  // interleaved on one box, profiles/r2/ab_whh_side_splitk.txt).  (Outputs
-  // written there were allocated on the main stream, which joins the side
-  // stream before returning.)
-  // (starting them only after the main stream's per-token sums measured
-  // slower: 3.76-3.81 vs 3.71-3.72 ms, profiles/r3/ab_toksum_first.txt)
-
   // The recurrent-weight gradient (hand-written split-K GEMM, kernels/wgrad.hip)
   // on the first side stream, idle after dW_logit + the bias sums, concurrent
   // with the input-token chain below: interleaved on one box 3.351-3.386 vs
@@ -1189,6 +1179,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   stamp(STAMP_BWD_TOKSUM, st);
   at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st, 1);
+  // (dW_ie on the second side stream, concurrent with the embedding GEMM:
+  // 3.355-3.361 vs 3.342-3.356 ms per step, profiles/r5/tail/ab_wie_*.json)
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
   // (4H / 64) x (E / 64) tiles on the chip with a 10.5k-long K (164 us, ~134
   // TFLOP/s at V = 10,509); a split-K batch over the largest divisor of V up to
