@@ -465,21 +465,21 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
     s_p[tid] = s_sum_old[q] + s_tv[q * K + c];
   }
   __syncthreads();
-  for (int v = 0; v < K; ++v) {
-    if (w == 0) {
-      float best = -INFINITY;
-      int bj = 0x7fffffff;
-      for (int j = lane; j < ncand; j += 64) {
-        bool taken = false;
-        for (int u = 0; u < v; ++u) taken |= (s_sel[u] == j);
-        const float p = s_p[j];
-        if (!taken && (p > best || (p == best && j < bj))) best = p, bj = j;
-      }
-      wave_argmax(best, bj);
-      if (lane == 0) s_sel[v] = bj;
+  // the K best candidates in one pass: candidate j's rank is the number of
+  // candidates ahead of it (higher sum, or equal sum and lower index -- the
+  // order of the reference's repeated pick-the-best rounds), and the first K
+  // ranks are the selection in order (ncand <= 64: one wavefront, one barrier
+  // instead of K rounds of an argmax and a barrier)
+  if (tid < ncand) {
+    const float p = s_p[tid];
+    int rank = 0;
+    for (int i = 0; i < ncand; ++i) {
+      const float pi = s_p[i];
+      rank += (pi > p || (pi == p && i < tid)) ? 1 : 0;
     }
-    __syncthreads();
+    if (rank < K) s_sel[rank] = tid;
   }
+  __syncthreads();
   int64_t* sh_new = a.seq_hist + (int64_t)(t & 1) * R * T;
   float* lh_new = a.lp_hist + (int64_t)(t & 1) * R * T;
   for (int e = tid; e < K * T; e += BF_THREADS) {
