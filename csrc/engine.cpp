@@ -913,6 +913,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // 4. reverse LSTM loop on the main stream
   at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
   at::Tensor dc = at::zeros({R, H}, f32);
+  // (these loop operands filled on the second side stream concurrently with
+  // the one-hot pass measured slower: att8 4.487-4.516 vs 4.379-4.417 ms,
+  // headline 3.424-3.514 vs 3.337-3.339, profiles/r5/tail/ab_prep*.json)
   // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel; with
   // attention [W_hh^T | W_q^T] (H, 4H + A), so the step GEMM over
   // [dG_{t+1} | dq_{t+1}] also adds dq_{t+1} W_q (q_{t+1} = W_q h_t) into dh_t
