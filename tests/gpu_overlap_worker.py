@@ -43,9 +43,13 @@ def main(out):
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group('gloo', rank=0, world_size=1,
-                            init_method='tcp://127.0.0.1:%s' % sys.argv[2])
-    ctx = DistContext(rank=0, world_size=2, local_rank=0, device=dev, backend='gloo')
+    backend = sys.argv[3] if len(sys.argv) > 3 else 'gloo'
+    kw = {'device_id': dev} if backend == 'nccl' else {}
+    # ('nccl' = RCCL: a 1-rank communicator runs the real RCCL collectives of
+    # the shipped path on the comm stream)
+    dist.init_process_group(backend, rank=0, world_size=1,
+                            init_method='tcp://127.0.0.1:%s' % sys.argv[2], **kw)
+    ctx = DistContext(rank=0, world_size=2, local_rank=0, device=dev, backend=backend)
     opt = parse_opts(ARGS)
     tr_split, _, _ = load_splits(opt)
     loader = CaptionLoader(tr_split, opt.batch_size, opt.train_seq_per_img, 'train', ctx.device,
@@ -65,7 +69,9 @@ def main(out):
         if i >= 3:
             runs.append(stamps.read())
     stamps.disable()
+    finite = bool(torch.isfinite(tr.bucket.data).all())
     torch.save({'stamps': runs, 'events_ok': oks, 'graphed': tr._graph is not None,
+                'finite': finite, 'backend': dist.get_backend(),
                 'comm_priority': tr.bucket.comm.priority, 'n_groups': len(tr.bucket.groups)},
                out)
     dist.destroy_process_group()

@@ -150,3 +150,24 @@ def test_dp_slice_allreduce_starts_inside_the_backward(tmp_path):
         assert 'comm2' in st and st['bwd.loop'] < st['comm2'] < st['adam_begin'], \
             sorted(st.items(), key=lambda kv: kv[1])
         assert r['n_groups'] == 3
+
+
+def test_dp_step_over_rccl_one_rank(tmp_path):
+    """The same replayed DP step with the collectives on RCCL (backend
+    ``nccl``, a 1-rank communicator -- a one-GPU box cannot hold two RCCL
+    ranks): the streamed slice all-reduces are real RCCL launches on the
+    high-priority comm stream, issued around the replayed graphs; the steps
+    complete, the weights stay finite and the slice order holds as under
+    gloo."""
+    out = str(tmp_path / 'ov_rccl.pt')
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get('PYTHONPATH', ''),
+               CSTCAP_TEST_IMPL='hip', PYTHONFAULTHANDLER='1')
+    r = subprocess.run([sys.executable, os.path.join(HERE, 'gpu_overlap_worker.py'), out,
+                        str(_free_port()), 'nccl'], env=env, cwd=ROOT, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    r = torch.load(out, weights_only=False)
+    assert r['backend'] == 'nccl' and r['graphed'] and r['finite']
+    assert all(r['events_ok'][1:]), r['events_ok']
+    for st in r['stamps']:
+        assert st['comm0'] < st['bwd_end'], sorted(st.items(), key=lambda kv: kv[1])
