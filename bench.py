@@ -97,6 +97,12 @@ def parse():
                    help='scst, headline config: also time the CST recipe (README "CST_MS_SCB": '
                         'consensus baseline from the GT captions, --scb_baseline) in the same '
                         'invocation and report it as the "cst" field')
+    p.add_argument('--xe', type=int, default=1,
+                   help='scst, headline config: also time the XE recipe (BASELINE config 2, the '
+                        'reference\'s cross-entropy warm-up stage: teacher forcing, same '
+                        'model / batch) in the same invocation and report it as the "xe" field')
+    p.add_argument('--comm_priority', default='high', choices=['high', 'normal'],
+                   help='data parallelism: priority of the gradient all-reduce stream')
     p.add_argument('--scb_baseline', type=int, default=1, choices=[1, 2],
                    help='CST baseline: 1 = GT consensus scores (CST_MS_SCB), 2 = the samples\' own '
                         'scores (CST_MS_SCB(*))')
@@ -186,7 +192,8 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0, mode=None):
         scb_captions=S,
         impl=a.impl, precision=a.precision, reward_device=a.reward,
         dedupe_greedy=a.dedupe_greedy, seed=a.seed, loglevel='WARNING', save_last=0,
-        profile_phases=a.profile_phases, cuda_graph=a.cuda_graph, grad_wire=a.grad_wire)
+        profile_phases=a.profile_phases, cuda_graph=a.cuda_graph, grad_wire=a.grad_wire,
+        comm_priority=a.comm_priority)
     opt.vocab = {i: w for i, w in enumerate(ds.vocab)}
     opt.vocab_size = ds.vocab_size
     opt.seq_length = ds.seq_length
@@ -285,7 +292,14 @@ def run_config(a, ctx, num_chunks, sync, sync_debug=0, mode=None):
                 'ms_per_batch': round(tb / nb * 1e3, 3), 'videos_per_batch_per_gpu': a.batch_size,
                 'beam_size': 5, 'decodes': nb}
         model.train()
+    dev_err = None
+    if engine is not None and dev.type == 'cuda':
+        # failed cross-workgroup hand-offs counted on the device over every
+        # step of this run (csrc/engine.cpp device_errors); 0 = none
+        from cst_captioning_amd import _ext
+        dev_err = int(_ext.ops().device_errors(dev.index or 0))
     res = {'dt': dt, 'ms': dt / a.steps * 1e3, 'loss': float(out['loss']),
+           'device_errors': dev_err,
            'caps': a.batch_size * S * ctx.world_size * a.steps / dt,
            'vids': a.batch_size * ctx.world_size * a.steps / dt, 'phases': phases,
            'skipped': int(trainer.optimizer.skipped().item()),
@@ -350,6 +364,14 @@ def main():
                'recipe': 'CST_MS_SCB' if a.scb_baseline == 1 else 'CST_MS_SCB(*)',
                'scb_baseline': a.scb_baseline, 'scb_captions': 20, 'bcmr': r['bcmr'],
                'final_loss': r['loss'], 'skipped_steps': r['skipped']}
+    xe = None
+    if a.xe and a.mode == 'scst' and a.num_chunks == 1:
+        # BASELINE config 2: the XE (teacher-forced cross-entropy) stage of the
+        # same job on the same fused path (graph replay, X after the forward)
+        r = run_config(a, ctx, 1, sync, mode='xe')
+        xe = {'value': round(r['caps'], 2), 'ms_per_step': round(r['ms'], 3),
+              'recipe': 'XE (teacher forcing)', 'final_loss': r['loss'],
+              'skipped_steps': r['skipped'], 'cuda_graph': r['graph']}
     dt, ms, caps, vids = main_run['dt'], main_run['ms'], main_run['caps'], main_run['vids']
     loss, n_params, t_gen = main_run['loss'], main_run['n_params'], main_run['t_gen']
     S = 20
@@ -402,6 +424,10 @@ def main():
         # exp-store rows the backward recomputed (LSE jump > 60 between steps)
         'exp_fix_rows': main_run['exp_fix'],
         'world_size_seen': ctx.world_size, 'backend': ctx.backend or 'none',
+        'comm_priority': a.comm_priority,
+        # failed cross-workgroup hand-offs counted on the device (bounded flag
+        # polls that gave up) over the headline run; must be 0
+        'device_errors': main_run['device_errors'],
     }
     if att8 is not None:
         # BASELINE.json's metric names the LSTM-attn decoder: its temporal-
@@ -410,6 +436,8 @@ def main():
     if cst is not None:
         # the CST recipe (README CST_MS_SCB), fused consensus-baseline loss
         rec['cst'] = cst
+    if xe is not None:
+        rec['xe'] = xe
     if main_run.get('blaslt'):
         rec['blaslt_x_choice'] = main_run['blaslt']
     if main_run.get('beam5'):

@@ -19,6 +19,11 @@ void set_grad_events(bool on);
 void grad_event_wait(int64_t k, int64_t stream);
 void grad_event_record(int64_t k, int64_t stream);
 int64_t grad_event_count(int64_t k);
+void set_poll_bound(int64_t n);
+void set_bwd_loop(bool on);
+double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases);
+int64_t device_errors(int64_t dev_index);
+void reset_device_errors(int64_t dev_index);
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand);
 std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at::Tensor b,
@@ -86,6 +91,7 @@ void refresh_shadows(at::Tensor p, at::Tensor shadow_meta, std::vector<at::Tenso
 void set_stamp_base(int64_t base);
 void stamp_buffer(at::Tensor buf);
 void stamp_now(int64_t slot);
+void busy_copy(at::Tensor buf, int64_t blocks, double us, int64_t stream);
 int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
 at::Tensor att_mfma_phases(at::Tensor gv, at::Tensor P, at::Tensor wa, at::Tensor ba, int64_t R);
@@ -166,6 +172,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_event_wait", &cst::grad_event_wait);
   m.def("grad_event_record", &cst::grad_event_record);
   m.def("grad_event_count", &cst::grad_event_count);
+  m.def("set_poll_bound", &cst::set_poll_bound,
+        "polls of a bounded cross-workgroup wait before it gives up (tests: 0)");
+  m.def("set_bwd_loop", &cst::set_bwd_loop,
+        "reverse LSTM loop as one persistent launch (true, default) or one launch per step");
+  m.def("lstm_bwd_loop_bench", &cst::lstm_bwd_loop_bench,
+        "persistent reverse loop alone on random operands: us per launch (+ phase stamps)");
+  m.def("device_errors", &cst::device_errors,
+        "failed cross-workgroup hand-offs counted on the device (synchronous read)");
+  m.def("reset_device_errors", &cst::reset_device_errors);
   m.def("att_mfma_fwd", &cst::att_mfma_fwd);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);
@@ -176,6 +191,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_stamp_base", &cst::set_stamp_base);
   m.def("stamp_buffer", &cst::stamp_buffer);
   m.def("stamp_now", &cst::stamp_now);
+  m.def("busy_copy", &cst::busy_copy,
+        "stand-in for a collective's kernel: copying workgroups for a given time");
   m.def("wall_clock_khz", &cst::wall_clock_khz);
   m.def("vocab_x", &cst::vocab_x);
   m.def("att_mfma_phases", &cst::att_mfma_phases);

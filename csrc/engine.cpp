@@ -93,6 +93,14 @@ static void check_cuda(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
+// stand-in for a collective's kernel on `stream` (0: the current stream):
+// `blocks` copying workgroups for `us` microseconds over `buf` (fp32 scratch)
+void busy_copy(at::Tensor buf, int64_t blocks, double us, int64_t stream) {
+  check_cuda(buf, "buf");
+  TORCH_CHECK(buf.scalar_type() == at::kFloat && buf.is_contiguous(), "busy_copy: fp32 scratch");
+  launch_busy_copy(buf.data_ptr<float>(), buf.numel(), (int)blocks, us,
+                   stream != 0 ? reinterpret_cast<hipStream_t>(stream) : cur_stream());
+}
 
 // rng: int32[2] device tensor {dropout seed, sampling seed} (or undefined /
 // empty: seeds 0).  Kernels read it from device memory, so a captured HIP
@@ -127,6 +135,63 @@ static DeviceAux& device_aux(int dev_index) {
     it = aux.emplace(dev_index, a).first;
   }
   return *it->second;
+}
+
+// Device error word (one int32 per device, zero until a kernel reports a
+// failed cross-workgroup hand-off): a bounded flag poll that runs out of polls
+// (lstm.hip att_fuse_wait) adds 1 instead of silently reading operands that
+// may not be written yet.  The trainer reads it at log time and raises; the
+// bench reports it.  set_poll_bound(0) forces every such wait to give up
+// (tests of the counter).
+static int g_poll_bound = 1 << 20;
+static int* device_err_word(int dev_index) {
+  static std::map<int, int*> words;
+  auto it = words.find(dev_index);
+  if (it == words.end()) {
+    int* p = nullptr;
+    c10::hip::HIPGuard guard(dev_index);
+    TORCH_CHECK(hipMalloc(&p, sizeof(int)) == hipSuccess, "device error word: hipMalloc");
+    TORCH_CHECK(hipMemset(p, 0, sizeof(int)) == hipSuccess, "device error word: hipMemset");
+    it = words.emplace(dev_index, p).first;
+  }
+  return it->second;
+}
+// persistent reverse loop on (default; CSTCAP_BWD_LOOP=0 or set_bwd_loop(false):
+// one launch per step)
+static bool g_bwd_loop = [] {
+  const char* e = getenv("CSTCAP_BWD_LOOP");
+  return e == nullptr || atoi(e) != 0;
+}();
+void set_bwd_loop(bool on) { g_bwd_loop = on; }
+void set_poll_bound(int64_t n) { g_poll_bound = (int)std::max<int64_t>(0, n); }
+// team counters of the persistent reverse loop (lstm_loop.hip), per device;
+// the launcher zeroes the used prefix before every launch
+static int* loop_counters(int dev_index, int ints) {
+  static std::map<int, std::pair<int*, int>> bufs;
+  auto it = bufs.find(dev_index);
+  if (it == bufs.end() || it->second.second < ints) {
+    TORCH_CHECK(it == bufs.end(), "persistent reverse loop: counter block too small");
+    int* p = nullptr;
+    c10::hip::HIPGuard guard(dev_index);
+    const int n = std::max(ints, 4096);
+    TORCH_CHECK(hipMalloc(&p, sizeof(int) * n) == hipSuccess, "loop counters: hipMalloc");
+    TORCH_CHECK(hipMemset(p, 0, sizeof(int) * n) == hipSuccess, "loop counters: hipMemset");
+    it = bufs.emplace(dev_index, std::make_pair(p, n)).first;
+  }
+  return it->second.first;
+}
+int64_t device_errors(int64_t dev_index) {
+  int* p = device_err_word((int)dev_index);
+  int v = 0;
+  c10::hip::HIPGuard guard((int)dev_index);
+  TORCH_CHECK(hipMemcpy(&v, p, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess,
+              "device error word: read");
+  return v;
+}
+void reset_device_errors(int64_t dev_index) {
+  int* p = device_err_word((int)dev_index);
+  c10::hip::HIPGuard guard((int)dev_index);
+  TORCH_CHECK(hipMemset(p, 0, sizeof(int)) == hipSuccess, "device error word: reset");
 }
 
 // Data parallelism, communication overlapped with the backward: with
@@ -614,6 +679,60 @@ static bool wgrad_tn_into(const at::Tensor& A, int64_t lda, const at::Tensor& B,
   return true;
 }
 
+// microbenchmark of the persistent reverse loop alone (random operands of the
+// given shape): mean us per launch over `iters` launches; `phases` (int64,
+// grid x T x 4, nullable-empty) receives the last launch's per-step stamps
+// (step start, team wait done, operands + GEMM done, step published)
+double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases) {
+  TORCH_CHECK(lstm_bwd_loop_ok((int)R, (int)H, (int)T), "lstm_bwd_loop_bench: unsupported shape");
+  auto dev = at::Device(at::kCUDA, at::hip::getCurrentHIPStream().device_index());
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+  auto b16 = at::TensorOptions().dtype(at::kBFloat16).device(dev);
+  at::Tensor dG = at::empty({T, R, 4 * H}, b16);
+  at::Tensor whhT = (at::randn({H, 4 * H}, f32) * 0.05).to(at::kBFloat16);
+  at::Tensor dh = at::randn({T, R, H}, f32) * 0.01;
+  at::Tensor gates = at::rand({T, R, 4 * H}, f32).to(at::kBFloat16);
+  at::Tensor c_all = at::randn({T, R, H}, f32);
+  at::Tensor dc = at::empty({R, H}, f32);
+  at::Tensor rng = at::zeros({2}, at::TensorOptions().dtype(at::kInt).device(dev));
+  BwdLoopArgs la{};
+  la.dG = reinterpret_cast<uint16_t*>(dG.data_ptr());
+  la.whhT = reinterpret_cast<const uint16_t*>(whhT.data_ptr());
+  la.dh = dh.data_ptr<float>();
+  la.gates = reinterpret_cast<const uint16_t*>(gates.data_ptr());
+  la.c_all = c_all.data_ptr<float>();
+  la.dc_out = dc.data_ptr<float>();
+  la.R = (int)R;
+  la.H = (int)H;
+  la.T = (int)T;
+  la.drop_p = 0.5f;
+  la.rng = reinterpret_cast<const uint32_t*>(rng.data_ptr());
+  la.cnt = loop_counters(dev.index(), lstm_bwd_loop_counter_ints((int)R, (int)H));
+  la.err = device_err_word(dev.index());
+  la.poll_bound = g_poll_bound;
+  hipStream_t st = cur_stream();
+  for (int i = 0; i < 3; ++i) launch_lstm_bwd_loop(la, st);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, st);
+  for (int64_t i = 0; i < iters; ++i) launch_lstm_bwd_loop(la, st);
+  (void)hipEventRecord(e1, st);
+  if (phases.defined() && phases.numel() > 0) {
+    TORCH_CHECK(phases.scalar_type() == at::kLong && phases.is_cuda() && phases.is_contiguous(),
+                "phases: int64 GPU tensor");
+    la.phases = phases.data_ptr<int64_t>();
+    launch_lstm_bwd_loop(la, st);
+  }
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamSynchronize(st);
+  return ms * 1e3 / std::max<int64_t>(iters, 1);
+}
+
 // test entry: C (M x N) fp32 = A[:K]^T B[:K]
 at::Tensor wgrad_tn(at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K) {
   check_cuda(A, "A");
@@ -722,6 +841,13 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     TORCH_CHECK((int)dhd_chunks.size() <= MAX_DHD_CHUNKS, "too many decode steps for the dHd chunks");
   }
 
+  // The whole reverse recurrence as ONE persistent launch (lstm_loop.hip):
+  // one-layer decoders without attention / initial state whose shape fits
+  // (headline: 256 workgroups, one per CU, all resident: the side stream's
+  // vocab-head weight gradients start after it).  CSTCAP_BWD_LOOP=0 keeps the
+  // launch per step.
+  const bool persistent = g_bwd_loop && NL == 1 && !has_att && !has_s0 &&
+                          lstm_bwd_loop_ok((int)R, (int)H, (int)n_steps);
   // 1-2. vocab head on the side stream.  Exp store (training): alpha and the
   // one-hot terms folded into E, X = E' W (dHd = alpha X, scaled by the
   // loop), the alpha-scaled Hd rows for dW; kernels/vocab_grad.hip.  Dense
@@ -851,6 +977,18 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     }
     stamp(STAMP_BWD_ONEHOT, s);
   };
+  // the vocab head's weight gradients (current stream: side)
+  auto side_dw = [&]() {
+    if (!ds_ready)
+      launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
+                        reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
+                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
+    stamp(STAMP_BWD_DHD, side.stream());
+    dw_gemm();
+    stamp(STAMP_BWD_DW, side.stream());
+    db_sums(side.stream());
+    dw_done();
+  };
   stamp(STAMP_BWD_BEGIN, st);
   // Forward X: the loop's first operands are the row weights of this pass and
   // X itself, so the pass runs on the main stream -- no hop to the side stream
@@ -880,15 +1018,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       (void)hipEventRecord(aux.ev[6 + ci], side.stream());
       if (ci == 0) stamp(STAMP_BWD_DHD0, side.stream());
     }
-    if (!ds_ready)
-      launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
-                        reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
-                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
-    stamp(STAMP_BWD_DHD, side.stream());
-    dw_gemm();
-    stamp(STAMP_BWD_DW, side.stream());
-    db_sums(side.stream());
-    dw_done();
+    if (!persistent) side_dw();
   }
   // token-only operands of the embedding / input-weight gradients: rows
   // grouped by input token (counting sort), per-token sum scratch
@@ -977,8 +1107,50 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                     has_xe ? oh_b.data_ptr<float>() + t * R : nullptr,
                     has_xe ? oh_yx.data_ptr<int>() + t * R : nullptr};
   };
+  if (persistent) {
+    // every dHd chunk first (forward X: none), then the loop
+    for (size_t ci = 0; ci < dhd_chunks.size(); ++ci)
+      (void)hipStreamWaitEvent(st, aux.ev[6 + ci], 0);
+    BwdLoopArgs la{};
+    la.dG = reinterpret_cast<uint16_t*>(dG_all.data_ptr());
+    la.whhT = reinterpret_cast<const uint16_t*>(whhT.data_ptr());
+    la.dh = dHd.data_ptr<float>();
+    la.scale = ds_ready ? nullptr : alpha.data_ptr<float>();
+    if (have_x) {
+      la.oh_W = reinterpret_cast<const uint16_t*>(wlog.data_ptr());
+      la.oh_a = oh_a.data_ptr<float>();
+      la.oh_ys = oh_ys.data_ptr<int>();
+      if (has_xe) {
+        la.oh_b = oh_b.data_ptr<float>();
+        la.oh_yx = oh_yx.data_ptr<int>();
+      }
+    }
+    la.gates = reinterpret_cast<const uint16_t*>(gates_all.data_ptr());
+    la.c_all = c_all.data_ptr<float>();
+    la.dc_out = dc.data_ptr<float>();
+    la.R = (int)R;
+    la.H = (int)H;
+    la.T = (int)n_steps;
+    la.cell = (int)cell;
+    la.drop_p = (float)drop_p;
+    la.rng = RNG;
+    la.cnt = loop_counters((int)dev.index(), lstm_bwd_loop_counter_ints((int)R, (int)H));
+    la.err = device_err_word((int)dev.index());
+    la.poll_bound = g_poll_bound;
+    TORCH_CHECK(gates_all.is_contiguous() && c_all.is_contiguous() && dG_all.is_contiguous() &&
+                    dHd.is_contiguous() && gates_all.size(0) >= n_steps && c_all.size(0) >= n_steps,
+                "persistent reverse loop: operand layout");
+    launch_lstm_bwd_loop(la, st);
+    stamp(STAMP_BWD_LOOP0, st);
+    // the vocab head's weight gradients after the loop (every CU is the
+    // loop's until it ends), concurrently with the post-loop chain below
+    (void)hipEventRecord(aux.ev[4], st);
+    (void)hipStreamWaitEvent(side.stream(), aux.ev[4], 0);
+    c10::hip::HIPStreamGuard guard(side);
+    side_dw();
+  }
   size_t next_chunk = 0;
-  for (int64_t t = n_steps - 1; t >= 0; --t) {
+  for (int64_t t = persistent ? -1 : n_steps - 1; t >= 0; --t) {
     if (next_chunk < dhd_chunks.size() && t == dhd_chunks[next_chunk][1] - 1)
       (void)hipStreamWaitEvent(st, aux.ev[6 + next_chunk++], 0);  // dHd rows of this chunk
     const DhOneHot oh_t = dh_onehot_t(t);
@@ -1026,6 +1198,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
         abe.dP_acc = dpre_part.data_ptr<float>();
         abe.dwa_part = dwa_part.data_ptr<float>();
         abe.dba_part = dba_part.data_ptr<float>();
+        abe.poll_bound = g_poll_bound;
+        abe.poll_err = device_err_word((int)dev.index());
       }
     }
     launch_lstm_step_bwd(

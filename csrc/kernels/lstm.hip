@@ -457,14 +457,24 @@ __device__ __forceinline__ void glds16_aux(rsrc_t r, int voff, int soff, char* l
 // [v0, v0 + nv) released their dq rows.  They precede this workgroup in
 // dispatch order (lower blockIdx), so they are resident or done; the bound
 // only guarantees that every wave exits.
-__device__ __forceinline__ void att_fuse_wait(const int* flags, int v0, int nv) {
+// A wait that runs out of polls counts itself in the device error word
+// (poll_err, read by the host after the step: engine.device_errors); the
+// gradient of that step is then not trusted (the trainer raises).
+__device__ __forceinline__ void att_fuse_wait(const int* flags, int v0, int nv, int bound,
+                                              int* err) {
   const int lane = threadIdx.x & 63;
-  for (int it = 0; it < (1 << 22); ++it) {
+  bool ok = false;
+  for (int it = 0; it < bound; ++it) {
     const int f = __hip_atomic_load(flags + v0 + min(lane, nv - 1), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
-    if (__all(f > 0)) break;
+    if (__all(f > 0)) {
+      ok = true;
+      break;
+    }
     __builtin_amdgcn_s_sleep(2);
   }
+  if (!ok && lane == 0 && err != nullptr)
+    __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The step kernel's main loop with the fused attention's ordering: K-tiles
@@ -476,7 +486,8 @@ template <class TL, bool GATE>
 __device__ __forceinline__ void gemm_bwd_mainloop_tail(int tid, int nk, const DmaSrc<TL::BM / 32>& a,
                                                        const DmaSrc<TL::BN / 32>& b, char* lds,
                                                        f32x16 (&acc)[TL::TM][TL::TN],
-                                                       const int* flags, int v0, int nv) {
+                                                       const int* flags, int v0, int nv,
+                                                       int bound, int* err) {
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
@@ -499,7 +510,7 @@ __device__ __forceinline__ void gemm_bwd_mainloop_tail(int tid, int nk, const Dm
         glds16(b.r0, b.voff0[i], kt * 128, B + 1024 * (w + 4 * i));
     } else {
       if (!waited) {
-        att_fuse_wait(flags, v0, nv);
+        att_fuse_wait(flags, v0, nv, bound, err);
         waited = true;
       }
       const int ks = (kt - a.ksplit) * 128;
@@ -551,17 +562,18 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     const uint16_t* __restrict__ gates, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, int R, int H, float drop_p,
     const uint32_t* __restrict__ rng, int step, uint16_t* __restrict__ dG, int KD, int cell,
-    const float* __restrict__ dh_scale, AttBwdEpi att, DhOneHot oh) {
+    const float* __restrict__ dh_scale, AttBwdEpi att, DhOneHot oh, int map_rows) {
   using TL = Tile<BM, 64, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n_ut = H / 64, n_rt = (R + BM - 1) / BM, n_tiles = n_ut * n_rt;
   static_assert(!FUSE || ATT, "the fused attention backward extends the attention epilogue");
   if (FUSE && (int)blockIdx.x < att.Bv) {  // step t + 1's attention backward (AttBwdEpi)
-    att_bwd_fused_wg<CP>(att, blockIdx.x, R, n_ut, const_cast<uint16_t*>(dg_next), KD, lds);
+    const int vb = map_rows ? xcd_remap_l(blockIdx.x, att.Bv) : (int)blockIdx.x;
+    att_bwd_fused_wg<CP>(att, vb, R, n_ut, const_cast<uint16_t*>(dg_next), KD, lds);
     return;
   }
   const int b = xcd_remap_l((int)blockIdx.x - (FUSE ? att.Bv : 0), n_tiles);
-  const int ut = b / n_rt, rt = b % n_rt;
+  const int ut = map_rows ? b % n_ut : b / n_rt, rt = map_rows ? b / n_ut : b % n_rt;
   const int r0 = rt * BM, u0 = ut * 64;
   const int nk_all = dg_next != nullptr ? KD / 64 : 0;  // KD = 4H (+ A with attention)
   const int grp = threadIdx.x >> 8, gtid = threadIdx.x & 255;
@@ -620,7 +632,7 @@ __global__ __launch_bounds__(256 * GROUPS) void lstm_step_bwd_kernel(
     }
     gemm_bwd_mainloop_tail<TL, true>(gtid, nkd / 2 + nka / 2, a, bsrc,
                                      lds + grp * TL::STAGES * TL::STAGE_BYTES, acc, att.flags, v0,
-                                     nvs);
+                                     nvs, att.poll_bound, att.poll_err);
   } else if (nkg > 0) {
     const int lane = gtid & 63, w = gtid >> 6;
     DmaSrc<BM / 32> a;
@@ -751,9 +763,11 @@ static void launch_lstm_step_bwd_g(const uint16_t* dg_next, const uint16_t* whhT
   }
   // (fused: the attention workgroups first, blockIdx < Bv -- see att_fuse_wait)
   const int n = (H / 64) * ((R + BM - 1) / BM) + (FUSE ? att.Bv : 0);
+  static const int map_rows = getenv("CSTCAP_BWD_MAP") ? atoi(getenv("CSTCAP_BWD_MAP")) : 1;
   hipLaunchKernelGGL((lstm_step_bwd_kernel<BM, STAGES, GROUPS, ATT, CP, FUSE>), dim3(n),
                      dim3(256 * GROUPS), LDS, stream, dg_next, whhT, dh_logit, dc_carry, gates,
-                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale, att, oh);
+                     c_t, c_prev, R, H, drop_p, rng, step, dG, KD, cell, dh_scale, att, oh,
+                     map_rows);
   post_launch("lstm_step_bwd_kernel", stream);
 }
 

@@ -253,6 +253,10 @@ struct AttBwdEpi {
   float* dP_acc;    // (Bv, C, A)
   float* dwa_part;  // (Bv, A)
   float* dba_part;  // (Bv)
+  // bounded flag poll of the GEMM workgroups: polls before giving up, and the
+  // device error word a wait that gave up increments (nullable)
+  int poll_bound;
+  int* poll_err;
 };
 // fused attention backward (AttBwdEpi::flags) supported for this shape
 bool att_bwd_fuse_ok(int vdiv, int C, int A, int H, int Bv, int R);
@@ -264,6 +268,34 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
                           const float* dh_scale = nullptr,  // dh_logit row scales (nullable)
                           const AttBwdEpi* att = nullptr,
                           const struct DhOneHot* oh = nullptr);
+
+// lstm_loop.hip: the whole reverse recurrence of a one-layer decoder without
+// attention / initial state in ONE persistent launch (see the file header)
+struct BwdLoopArgs {
+  uint16_t* dG;            // (T, R, 4H) bf16 out: gate gradients of every step
+  const uint16_t* whhT;    // (H, 4H) bf16 W_hh^T (packed gate columns)
+  const float* dh;         // (T, R, H) fp32 vocab-head h gradient (X or dHd)
+  const float* scale;      // (T, R) row scales of dh (nullable)
+  const uint16_t* oh_W;    // one-hot terms (DhOneHot, all steps; oh_a null: none)
+  const float* oh_a;
+  const int* oh_ys;
+  const float* oh_b;
+  const int* oh_yx;
+  const uint16_t* gates;   // (T, R, 4H) bf16 saved gate activations
+  const float* c_all;      // (T, R, H) fp32 cell states
+  float* dc_out;           // (R, H) final state-gradient carry (nullable)
+  int R, H, T, cell;
+  float drop_p;
+  const uint32_t* rng;
+  int* cnt;                // team counters (lstm_bwd_loop_counter_ints), zeroed per launch
+  int* err;                // device error word (nullable)
+  int poll_bound;
+  int nub, nrb, rows_per_group, rows_per_block;  // (set by the launcher)
+  int64_t* phases;         // microbenchmark: (grid, T, 4) wall-clock stamps (nullable)
+};
+bool lstm_bwd_loop_ok(int R, int H, int T);
+int lstm_bwd_loop_counter_ints(int R, int H);
+void launch_lstm_bwd_loop(BwdLoopArgs a, hipStream_t stream);
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal
 // attention with per_frame = 1: scorer weights w_a (C, A), biases b_a (C))
@@ -386,6 +418,7 @@ void launch_token_sort(const int64_t* toks, int N, int V, int* ws, int* stok, in
 void set_stamp_buffer(int64_t* buf, int slots);
 bool stamps_enabled();
 void launch_stamp(int slot, hipStream_t stream);
+void launch_busy_copy(float* buf, int64_t n_floats, int blocks, double us, hipStream_t stream);
 // slots written by the C++ executor, relative to the base the caller set
 // (engine.cpp set_stamp_base): forward and backward phases
 enum StampSlot : int {

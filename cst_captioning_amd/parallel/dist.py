@@ -270,14 +270,16 @@ class FlatGradBucket:
         ``grad_scale``), so no separate pass over the buffer divides it."""
         return 1.0 / ctx.world_size if (ctx.enabled and self.wire == 'fp32') else 1.0
 
-    def set_groups(self, groups, ctx):
+    def set_groups(self, groups, ctx, priority='high'):
         """Leading slices reduced as soon as the backward marks them final:
         ``groups`` = [params of slice 0, params of slice 1(, slice 2)] (at
         most three; they must be the buffer's leading parameters, in order).
         The fused backward records the matching events (engine
         ``set_grad_events``): vocab head, embedding, and for the concat model
-        W_ih + FeatPool (the video-gate backward done inside the engine)."""
+        W_ih + FeatPool (the video-gate backward done inside the engine).
+        ``priority``: 'high' or 'normal' priority for the comm stream."""
         assert 1 <= len(groups) <= 3, 'one to three streamed slices'
+        assert priority in ('high', 'normal'), 'comm priority: high or normal'
 
         self.groups = []
         off = 0
@@ -294,10 +296,22 @@ class FlatGradBucket:
             # normal-priority queues with the replayed graph -- an in-order
             # queue shared with the graph would hold the collective behind
             # the whole replay whatever the event says.
-            self.comm = torch.cuda.Stream(device=self.grad.device, priority=-1)
+            # (--comm_priority normal: priority 0, for the measured trade-off
+            # against the high-priority queue's CU share during the reverse
+            # loop, profiles/r6/README_r6.md)
+            self.comm = torch.cuda.Stream(device=self.grad.device,
+                                          priority=-1 if priority == 'high' else 0)
             self._ev_start = torch.cuda.Event()
         self._counts = None
         self.events_ok = False
+
+    standin = None  # (workgroups, us): see all_reduce
+
+    def _standin_buf(self):
+        buf = getattr(self, '_standin_scratch', None)
+        if buf is None:
+            buf = self._standin_scratch = torch.empty(64 << 20, device=self.grad.device)
+        return buf
 
     # -- streamed slices: ordering bookkeeping -------------------------------------
     @staticmethod
@@ -388,6 +402,11 @@ class FlatGradBucket:
                 if events_ok:
                     _ext.ops().grad_event_wait(k, self.comm.cuda_stream)
                 stamps.mark('comm%d' % k)
+                if k == 0 and self.standin is not None:
+                    # measurement hook (tests / scripts): a collective-shaped
+                    # stand-in kernel where the vocab-head slice's ring runs
+                    blocks, us = self.standin
+                    _ext.ops().busy_copy(self._standin_buf(), blocks, us, self.comm.cuda_stream)
                 w = dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM,
                                     async_op=not sync_on_stream)
                 if w is not None:

@@ -113,7 +113,7 @@ class Trainer:
                 and not self.bucket.sharded):
             from .. import _ext
             self.bucket.set_groups([early, [model.embed.weight]] + ([third] if third else []),
-                                   self.ctx)
+                                   self.ctx, priority=getattr(opt, 'comm_priority', 'high'))
             _ext.ops().set_grad_events(True)
         if engine is not None:
             # the fused backward writes the vocab-head, embedding and LSTM
@@ -142,6 +142,9 @@ class Trainer:
         # SCST with the fused engine: X = E W launched right after the rollout
         # (engine.launch_x); False keeps the backward's own E' W GEMM (tests)
         self.use_x_after_rollout = True
+        # XE steps: X = E W after the teacher-forced forward too (else the
+        # backward computes it in reverse-order chunks under the loop)
+        self.xe_x_after_forward = os.environ.get('CSTCAP_XE_XAFTER', '1') == '1'
         # PyTorch decoder path at --precision bf16: torch autocast (bf16 GEMMs /
         # LSTM, fp32 softmax), the same-precision baseline of the fused engine
         self.autocast_bf16 = (engine is None and self.device.type == 'cuda'
@@ -289,6 +292,10 @@ class Trainer:
     def xe_loss(self, data):
         if self.engine is not None:
             lp = self.engine.teacher_forced(self.model, data['feats'], data['labels'])
+            # the vocab head's X = E W right after the teacher-forced forward,
+            # on the engine's stream (as after an RL rollout): the backward's
+            # reverse loop then starts on X instead of on its first chunk
+            self.engine.launch_x()
             self.timer.mark('rollout')
             return self.xe_criterion(lp, data['labels'][:, 1:], data['masks'][:, 1:]), {}
         pred = self.model(data['feats'], data['labels'])[0]
@@ -323,10 +330,11 @@ class Trainer:
         if self.engine is not None and self.device.type == 'cuda':
             self.engine.prefetch_ptab()  # under the prologue, on a side stream
         if self.engine is not None:
-            # RL steps: the vocab head's X = E W right after the rollout, on the
-            # engine's stream (rl_loss -> engine.launch_x); nothing consumes it
-            # in an XE step
-            self.engine.x_after_rollout = bool(self.rl_training and self.use_x_after_rollout)
+            # the vocab head's X = E W right after the rollout (RL: rl_loss ->
+            # engine.launch_x) or the teacher-forced forward (XE: xe_loss), on
+            # the engine's stream
+            self.engine.x_after_rollout = bool(self.use_x_after_rollout and
+                                               (self.rl_training or self.xe_x_after_forward))
         m.train()
         self.optimizer.zero_grad()
         m.set_seq_per_img(self.train_loader.get_seq_per_img())
@@ -652,6 +660,19 @@ class Trainer:
         self.ctx.all_reduce_(t, average=True)
         return t.tolist()
 
+    def check_device_errors(self):
+        """Failed cross-workgroup hand-offs counted on the device (a bounded
+        flag poll that ran out of polls, csrc/kernels/lstm.hip att_fuse_wait):
+        the gradients of those steps are not trusted, so training stops."""
+        if self.device.type != 'cuda':
+            return 0
+        from .. import _ext
+        n = int(_ext.ops().device_errors(self.device.index or 0))
+        if n:
+            raise RuntimeError('%d cross-workgroup hand-off(s) timed out on the device; '
+                               'the affected gradients are not trusted' % n)
+        return n
+
     def _log(self, out, elapsed):
         opt, infos = self.opt, self.infos
         vals = self.reduce_log_scalars(out)
@@ -674,6 +695,7 @@ class Trainer:
         items.append(('Skipped', int(self.optimizer.skipped().item())))
         if self.engine is not None:  # exp-store rows recomputed (LSE jump > 60)
             items.append(('ExpFix', int(self.engine.exp_fix_rows.item())))
+            self.check_device_errors()
         # throughput since the previous log line (the scalar reduction above
         # synchronised the device, so the wall clock covers finished work)
         now = time.perf_counter()
