@@ -21,7 +21,8 @@ void grad_event_record(int64_t k, int64_t stream);
 int64_t grad_event_count(int64_t k);
 void set_poll_bound(int64_t n);
 void set_bwd_loop(bool on);
-double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases);
+double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases,
+                           int64_t dbg);
 int64_t device_errors(int64_t dev_index);
 void reset_device_errors(int64_t dev_index);
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
@@ -96,6 +97,8 @@ int64_t wall_clock_khz();
 void vocab_x(at::Tensor logits16, at::Tensor wlog, at::Tensor out);
 at::Tensor att_mfma_phases(at::Tensor gv, at::Tensor P, at::Tensor wa, at::Tensor ba, int64_t R);
 at::Tensor wgrad_tn(at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K);
+std::vector<at::Tensor> wgrad_tn_colsum(at::Tensor A, at::Tensor B, at::Tensor al, int64_t M,
+                                        int64_t N, int64_t K);
 
 template <class T>
 static at::Tensor to_tensor(const std::vector<T>& v, at::ScalarType st) {
@@ -176,7 +179,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "polls of a bounded cross-workgroup wait before it gives up (tests: 0)");
   m.def("set_bwd_loop", &cst::set_bwd_loop,
         "reverse LSTM loop as one persistent launch (true, default) or one launch per step");
-  m.def("lstm_bwd_loop_bench", &cst::lstm_bwd_loop_bench,
+  m.def("lstm_bwd_loop_bench", &cst::lstm_bwd_loop_bench, py::arg("R"), py::arg("H"), py::arg("T"),
+        py::arg("iters"), py::arg("phases"), py::arg("dbg") = 0,
         "persistent reverse loop alone on random operands: us per launch (+ phase stamps)");
   m.def("device_errors", &cst::device_errors,
         "failed cross-workgroup hand-offs counted on the device (synchronous read)");
@@ -197,4 +201,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vocab_x", &cst::vocab_x);
   m.def("att_mfma_phases", &cst::att_mfma_phases);
   m.def("wgrad_tn", &cst::wgrad_tn);
+  m.def("wgrad_tn_colsum", &cst::wgrad_tn_colsum);
 }

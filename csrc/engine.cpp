@@ -663,18 +663,23 @@ std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
 // and B (K x >= N) through the hand-written split-K kernel (kernels/wgrad.hip):
 // rows [0, M0) of C into C0 (row stride ldc0), rows [M0, M) into C1.  Returns
 // false (nothing launched) when the shapes do not fit the kernel.
+// al / db (optional, N = 512): also db[m] = sum_k al[k] A[k][m] (fused column
+// sums of the A tiles in LDS)
 static bool wgrad_tn_into(const at::Tensor& A, int64_t lda, const at::Tensor& B, int64_t ldb,
                           int64_t M, int64_t N, int64_t K, float* C0, int64_t ldc0, int64_t M0,
-                          float* C1, int64_t ldc1, hipStream_t st) {
+                          float* C1, int64_t ldc1, hipStream_t st, const float* al = nullptr,
+                          float* db = nullptr) {
   if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16 ||
-      !wgrad_tn_ok(M, N, K, lda, ldb, A.data_ptr(), B.data_ptr()))
+      !wgrad_tn_ok(M, N, K, lda, ldb, A.data_ptr(), B.data_ptr()) || (db != nullptr && N != 512))
     return false;
   const int S = wgrad_tn_splits(M, N, K);
-  at::Tensor ws;
+  at::Tensor ws, ws_db;
   if (S > 1) ws = at::empty({S, M, N}, A.options().dtype(at::kFloat));
+  if (S > 1 && db != nullptr) ws_db = at::empty({S, M}, A.options().dtype(at::kFloat));
   WgradArgs g{reinterpret_cast<const uint16_t*>(A.data_ptr()), lda,
               reinterpret_cast<const uint16_t*>(B.data_ptr()), ldb, (int)M, (int)N, (int)K, S, 0,
-              S > 1 ? ws.data_ptr<float>() : nullptr, C0, ldc0, (int)M0, C1, ldc1};
+              S > 1 ? ws.data_ptr<float>() : nullptr, C0, ldc0, (int)M0, C1, ldc1,
+              db != nullptr ? al : nullptr, db, ws_db.defined() ? ws_db.data_ptr<float>() : nullptr};
   launch_wgrad_tn(g, st);
   return true;
 }
@@ -683,7 +688,8 @@ static bool wgrad_tn_into(const at::Tensor& A, int64_t lda, const at::Tensor& B,
 // given shape): mean us per launch over `iters` launches; `phases` (int64,
 // grid x T x 4, nullable-empty) receives the last launch's per-step stamps
 // (step start, team wait done, operands + GEMM done, step published)
-double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases) {
+double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases,
+                           int64_t dbg) {
   TORCH_CHECK(lstm_bwd_loop_ok((int)R, (int)H, (int)T), "lstm_bwd_loop_bench: unsupported shape");
   auto dev = at::Device(at::kCUDA, at::hip::getCurrentHIPStream().device_index());
   auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
@@ -710,6 +716,7 @@ double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::T
   la.cnt = loop_counters(dev.index(), lstm_bwd_loop_counter_ints((int)R, (int)H));
   la.err = device_err_word(dev.index());
   la.poll_bound = g_poll_bound;
+  la.dbg = (int)dbg;
   hipStream_t st = cur_stream();
   for (int i = 0; i < 3; ++i) launch_lstm_bwd_loop(la, st);
   hipEvent_t e0, e1;
@@ -743,8 +750,26 @@ at::Tensor wgrad_tn(at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K)
   at::Tensor C = at::empty({M, N}, A.options().dtype(at::kFloat));
   TORCH_CHECK(wgrad_tn_into(A, A.stride(0), B, B.stride(0), M, N, K, C.data_ptr<float>(), N, M,
                             nullptr, 0, cur_stream()),
-              "wgrad_tn: shapes not supported (M, N multiples of 128, 16-byte rows)");
+              "wgrad_tn: shapes not supported (N a multiple of 128, 16-byte rows)");
   return C;
+}
+
+// test entry of the fused form: {C (M x N), db (M)} with db[m] = sum_k al[k] A[k][m]
+std::vector<at::Tensor> wgrad_tn_colsum(at::Tensor A, at::Tensor B, at::Tensor al, int64_t M,
+                                        int64_t N, int64_t K) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  check_cuda(al, "al");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
+                  A.size(0) >= K && B.size(0) >= K && A.size(1) >= M && B.size(1) >= N &&
+                  al.scalar_type() == at::kFloat && al.is_contiguous() && al.numel() >= K,
+              "wgrad_tn_colsum: operand shapes");
+  at::Tensor C = at::empty({M, N}, A.options().dtype(at::kFloat));
+  at::Tensor db = at::empty({M}, A.options().dtype(at::kFloat));
+  TORCH_CHECK(wgrad_tn_into(A, A.stride(0), B, B.stride(0), M, N, K, C.data_ptr<float>(), N, M,
+                            nullptr, 0, cur_stream(), al.data_ptr<float>(), db.data_ptr<float>()),
+              "wgrad_tn_colsum: shapes not supported (N = 512, 16-byte rows)");
+  return {C, db};
 }
 
 std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Tensor emb,
@@ -889,10 +914,25 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // (the bias gradient as two extra bf16 columns (alpha hi / lo) of the dW
   // GEMM instead of the column sums measured slower: the N = 528 GEMM took
   // ~100 us longer, profiles/r3/ab_dbdw.txt)
+  // dW GEMM over augmented rows [alpha Hd | alpha_hi | alpha_lo | 0 x 14]
+  // (bf16, H + 16 columns): the same pass over E' also yields the bias
+  // gradient (columns H, H + 1 of the product), instead of a separate
+  // column-sum pass over the 753 MB exp store.  CSTCAP_DW_AUG=0: the separate
+  // column sums (vgrad_colsum).
+  static const bool dw_aug_env = [] {
+    const char* e = getenv("CSTCAP_DW_AUG");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  static const bool dw_wgrad_env = [] {
+    const char* e = getenv("CSTCAP_DW_WGRAD");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  const bool dw_aug = !ds_ready && dw_aug_env && !dw_wgrad_env;
+  const int64_t ldhs = dw_aug ? H + 16 : H;
   if (!ds_ready) {
     alpha = at::empty({NR}, f32);
-    hs = at::empty({NR, H}, wx.options());
-    cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
+    hs = at::empty({NR, ldhs}, wx.options());
+    if (!dw_aug) cs_part = at::empty({vgrad_colsum_blocks(NR), V}, f32);
   }
   auto launch_colsum = [&](hipStream_t s) {
     launch_vgrad_colsum(reinterpret_cast<const uint16_t*>(buf.data_ptr()), ldl, (int)V, NR,
@@ -922,8 +962,31 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // step count; 4 groups: 3.745-3.774 vs 3.792-3.831 ms per step for one
   // GEMM, 7 groups 3.862-3.873, profiles/r3/ab_sched.txt)
   const int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
+  // CSTCAP_DW_WGRAD=1: dW_logit AND the bias column sums in one hand-written
+  // split-K MFMA kernel instead (kernels/wgrad.hip: M = V with a ragged last
+  // tile, the sums from the E' tiles already in LDS): one pass over the exp
+  // store too, but 737 us at the headline shape against 392 + 209 us for the
+  // vendor batch + the column sums (profiles/r6/README_r6.md)
+  bool dw_fused = false;
   auto dw_gemm = [&]() {  // (current stream: side)
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
+    if (dw_aug) {
+      // split-K batch over the augmented rows; the partial products summed
+      // into the dW slot and the bias gradient (hi + lo columns)
+      const int64_t kr = NR / dw_split;
+      at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
+      at::Tensor p = at::bmm(a, hs.view({dw_split, kr, ldhs}), at::kFloat);  // (split, V, H + 16)
+      at::sum_out(dWlog, p.narrow(2, 0, H), 0);
+      at::sum_out(dblog, p.narrow(2, H, 2), at::IntArrayRef({0, 2}));
+      dw_fused = true;
+      return;
+    }
+    if (!ds_ready && dw_wgrad_env &&
+        wgrad_tn_into(buf.view({NR, ldl}), ldl, hs, H, V, H, NR, dWlog.data_ptr<float>(), H, V,
+                      nullptr, 0, side.stream(), alpha.data_ptr<float>(), dblog.data_ptr<float>())) {
+      dw_fused = true;
+      return;
+    }
     // (hipBLASLt's measured choice as one GEMM: 3.683-3.731 vs 3.628-3.682 ms
     // per step, the round-4 hand-written GEMM 3.746-3.795: the split-K batch)
     if (dw_split == 1) {
@@ -937,7 +1000,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   auto db_sums = [&](hipStream_t s) {  // (current stream: s)
     if (ds_ready)
       dblog.copy_(ds_bias);
-    else
+    else if (!dw_fused)
       launch_colsum(s);
   };
   auto dw_done = [&]() {
@@ -982,7 +1045,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     if (!ds_ready)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
                         reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
-                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream());
+                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream(), (int)ldhs);
     stamp(STAMP_BWD_DHD, side.stream());
     dw_gemm();
     stamp(STAMP_BWD_DW, side.stream());
@@ -1354,7 +1417,18 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
-  at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
+  // d_emb = S W_ie (M = V, N = E, K = 4H): the measured hipBLASLt choice
+  // (host/blaslt_tuned.cpp) -- PyTorch's heuristic pick ran it at 0.17 PF/s
+  // (130 us, profiles/r5/final5/steps_final5.txt).  CSTCAP_DEMB_TUNED=0: at::mm.
+  static const bool demb_tuned = [] {
+    const char* e = getenv("CSTCAP_DEMB_TUNED");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (demb_tuned && d_emb.is_contiguous() && d_emb.scalar_type() == at::kFloat &&
+      S_tok.is_contiguous() && wx.stride(1) == 1)
+    gemm_bf16_tuned(d_emb, S_tok, false, wx.narrow(1, 0, E), false, 24);
+  else
+    at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st, 1);
   // (dW_ie on the second side stream, concurrent with the embedding GEMM:
   // 3.355-3.361 vs 3.342-3.356 ms per step, profiles/r5/tail/ab_wie_*.json)

@@ -48,19 +48,17 @@ constexpr int LP_UT = 4;       // 16-unit tiles per workgroup (64 units)
 constexpr int LP_RT = 3;       // 16-row tiles per workgroup (<= 48 rows)
 constexpr int LP_MAXR = 16 * LP_RT;
 constexpr int LP_NF = LP_UT * LP_RT;  // accumulator fragments per wave
-// LDS: K-partials [wave][fragment][lane] float4, then the staged epilogue
-// operands, rows padded by one 16-byte chunk (conflict-free ds_read_b128 of
-// 16 consecutive rows at the same column)
+constexpr int LP_PF = 3;              // K-steps of B fragments in flight
+// LDS: the K-partials [wave][fragment][lane] float4, then per fragment the
+// staged epilogue operands of the wave that owns it (private to that wave:
+// it stages them itself, so no barrier orders their reuse): gates (2 KB:
+// 16 rows x 16 units x 4 gates bf16), two rotating c buffers (c_t and
+// c_{t-1}: step t's c_{t-1} is step t - 1's c_t) and the h gradient rows
+// dl (1 KB each: 16 rows x 16 units fp32).  Layout = the reader's lanes
+// (lane = 16 ku + ru reads 16-byte chunk 16 ku + ru of each 1 KB piece).
 constexpr int LP_PART_BYTES = LP_WAVES * LP_NF * 64 * 16;
-constexpr int LP_GSTRIDE = 33, LP_CSTRIDE = 17;  // 16-byte chunks per staged row
-// (each staged operand reserves whole 1 KB DMA instructions)
-constexpr int LP_G_BYTES = (LP_MAXR * LP_GSTRIDE + 63) / 64 * 1024;
-constexpr int LP_C_BYTES = (LP_MAXR * LP_CSTRIDE + 63) / 64 * 1024;
-constexpr int LP_G_OFF = LP_PART_BYTES;
-constexpr int LP_CT_OFF = LP_G_OFF + LP_G_BYTES;
-constexpr int LP_CP_OFF = LP_CT_OFF + LP_C_BYTES;
-constexpr int LP_DL_OFF = LP_CP_OFF + LP_C_BYTES;
-constexpr int LP_LDS = LP_DL_OFF + LP_C_BYTES;
+constexpr int LP_FRAG_BYTES = 5 * 1024;  // gates 2 KB, c x 2, dl
+constexpr int LP_LDS = LP_PART_BYTES + LP_NF * LP_FRAG_BYTES;
 static_assert(LP_LDS <= 160 * 1024, "persistent reverse loop: LDS budget");
 constexpr int LP_CNT_STRIDE = 32;  // ints between team counters (128 B)
 
@@ -71,24 +69,20 @@ __device__ __forceinline__ bf16x8 ld_sc1_b128(rsrc_t r, int voff) {
   const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 16);  // 16: sc1
   return __builtin_bit_cast(bf16x8, v);
 }
-
-// one staged operand: rows [0, nrows) x `chunks` 16-byte chunks of the
-// global rows (row stride `gstride` bytes, column offset `goff`), to LDS rows
-// of `stride` chunks; instruction k of the operand fills LDS chunks
-// [64 k, 64 k + 64)
-__device__ __forceinline__ void stage_rows(rsrc_t r, int64_t row0_bytes, int gstride, int goff,
-                                           int nrows, int chunks, int stride, char* lds, int k,
-                                           int lane) {
-  const int p = 64 * k + lane;
-  int row = p / stride, c = p - row * stride;
-  // padding chunks and rows past the block reload a valid chunk (harmless)
-  c = c < chunks ? c : chunks - 1;
-  row = row < nrows ? row : nrows - 1;
-  const int voff = (int)(row0_bytes + (int64_t)row * gstride) + goff + 16 * c;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds + 1024 * k), 16, voff, 0, 0, 0);
+// (microbenchmark variants only, BwdLoopArgs::dbg: plain loads / no loads)
+__device__ __forceinline__ bf16x8 ld_dbg_b128(rsrc_t r, int voff, int dbg) {
+  if (dbg & 2) return __builtin_bit_cast(bf16x8, u32x4v{(uint32_t)voff, 0u, 0u, 0u});
+  const u32x4v v = (dbg & 1) ? __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0)
+                             : __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 16);
+  return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int KS>
+// one LDS-DMA instruction: lane l moves the 16 bytes at voff(l) to dst + 16 l
+__device__ __forceinline__ void dma16(rsrc_t r, int voff, char* dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 16, voff, 0, 0, 0);
+}
+
+template <int KS, bool DBG = false>
 __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int H = a.H, R = a.R, T = a.T, KD = 4 * H;
@@ -119,7 +113,7 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArg
   // the unit tile, row ru of the row tile.
   const int e_ut = w & 3;
   const int nslot = w < 4 ? 2 : 1;
-  int e_rt[2], e_row[2];
+  int e_rt[2], e_row[2], e_src[2];
   bool e_ok[2];
   e_rt[0] = w < 4 ? 0 : 1;
   e_rt[1] = 2;
@@ -127,9 +121,9 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArg
   for (int s = 0; s < 2; ++s) {
     e_row[s] = 16 * e_rt[s] + ru;  // local row
     e_ok[s] = s < nslot && e_row[s] < nrows;
+    e_src[s] = r_lo + min(e_row[s], nrows - 1);  // (staging source row, clamped)
   }
-  const int q = 4 * e_ut + ku;  // unit quad within the 64 units
-  const int uq = u0 + 4 * q;    // first global unit of the quad
+  const int uq = u0 + 16 * e_ut + 4 * ku;  // first global unit of the lane's quad
   f32x4v dcr[2];
   dcr[0] = dcr[1] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
@@ -137,58 +131,42 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArg
   const rsrc_t r_gates = make_rsrc(a.gates, (int64_t)T * R * KD * 2);
   const rsrc_t r_c = make_rsrc(a.c_all, (int64_t)T * R * H * 4);
   const rsrc_t r_dl = make_rsrc(a.dh, (int64_t)T * R * H * 4);
-  const int n_g = (nrows * LP_GSTRIDE + 63) / 64, n_c = (nrows * LP_CSTRIDE + 63) / 64;
   const float inv_keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
   const uint32_t seed = rng_seed(a.rng, RNG_SLOT_DROPOUT);
   int* cnt = a.cnt + team * LP_CNT_STRIDE;
   f32x4v* part = reinterpret_cast<f32x4v*>(lds);
+  char* fr[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) fr[s] = lds + LP_PART_BYTES + (e_ut * LP_RT + e_rt[s]) * LP_FRAG_BYTES;
+  // staging of the wave's own fragments (wave-uniform): gates / dl of step
+  // ts, c of step tc into rotating buffer tc & 1
+  auto stage = [&](int ts, int tc, bool with_gd) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s >= nslot) continue;
+      const int64_t row = (int64_t)e_src[s];
+      if (with_gd) {
+        const int gb = (int)(((ts * (int64_t)R + row) * KD + 4 * uq) * 2);
+        dma16(r_gates, gb, fr[s]);
+        dma16(r_gates, gb + 16, fr[s] + 1024);
+        dma16(r_dl, (int)(((ts * (int64_t)R + row) * H + uq) * 4), fr[s] + 4096);
+      }
+      if (tc >= 0) dma16(r_c, (int)(((tc * (int64_t)R + row) * H + uq) * 4), fr[s] + 2048 + 1024 * (tc & 1));
+    }
+  };
   // (microbenchmark: per-step phase stamps of every workgroup, lane 0 of wave 0)
   int64_t* ph = a.phases != nullptr ? a.phases + (int64_t)blockIdx.x * T * 4 : nullptr;
 #define LP_STAMP(t, k) \
   if (ph != nullptr && tid == 0) ph[(int64_t)(T - 1 - (t)) * 4 + (k)] = (int64_t)wall_clock64();
 
+  // prologue: step T-1's operands and c_{T-2}
+  stage(T - 1, T - 1, true);
+  if (T >= 2) stage(0, T - 2, false);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
   for (int t = T - 1; t >= 0; --t) {
     LP_STAMP(t, 0)
-    // 1. stage step t's epilogue operands (waves 1..7; wave 0 polls)
-    if (w > 0) {
-      const int n_ins = n_g + n_c * (t > 0 ? 3 : 2);
-      for (int k = w - 1; k < n_ins; k += LP_WAVES - 1) {
-        if (k < n_g) {
-          stage_rows(r_gates, ((int64_t)t * R + r_lo) * KD * 2, KD * 2, u0 * 8, nrows, 32,
-                     LP_GSTRIDE, lds + LP_G_OFF, k, lane);
-        } else {
-          const int kk = k - n_g, which = kk / n_c, kc = kk - which * n_c;
-          // which: 0 = dh_logit, 1 = c_t, 2 = c_{t-1}
-          const int ts = which == 2 ? t - 1 : t;
-          stage_rows(which == 0 ? r_dl : r_c, ((int64_t)ts * R + r_lo) * H * 4, H * 4, u0 * 4,
-                     nrows, 16, LP_CSTRIDE,
-                     lds + (which == 0 ? LP_DL_OFF : which == 1 ? LP_CT_OFF : LP_CP_OFF), kc,
-                     lane);
-        }
-      }
-    }
-    // the per-row scalars of the thread's rows (plain loads: not written here)
-    float e_sc[2], e_a[2], e_b[2];
-    uint2 e_w[2], e_wx[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r = r_lo + min(e_row[s], nrows - 1);
-      const int64_t tr = (int64_t)t * R + r;
-      e_sc[s] = a.scale != nullptr ? a.scale[tr] : 1.f;
-      e_a[s] = 0.f;
-      e_b[s] = 0.f;
-      e_w[s] = e_wx[s] = make_uint2(0u, 0u);
-      if (a.oh_a != nullptr) {
-        e_a[s] = a.oh_a[tr];
-        e_w[s] = *reinterpret_cast<const uint2*>(a.oh_W + (int64_t)max(a.oh_ys[tr], 0) * H + uq);
-      }
-      if (a.oh_b != nullptr) {
-        e_b[s] = a.oh_b[tr];
-        e_wx[s] = *reinterpret_cast<const uint2*>(a.oh_W + (int64_t)max(a.oh_yx[tr], 0) * H + uq);
-      }
-    }
-
-    // 2. dh_rec = dG_{t+1} W_hh over this wave's K range, summed over waves
+    // 1. dh_rec = dG_{t+1} W_hh over this wave's K range, summed over waves
     f32x4v acc[LP_UT][LP_RT];
 #pragma unroll
     for (int ut = 0; ut < LP_UT; ++ut)
@@ -217,56 +195,58 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArg
       for (int rt = 0; rt < LP_RT; ++rt)
         boff[rt] = (int)((((int64_t)(t + 1) * R + r_lo + min(16 * rt + ru, nrows - 1)) * KD + k0 +
                           8 * ku) * 2);
-      // two K-steps of B fragments in flight ahead of the MFMAs
-      bf16x8 bq[2][LP_RT];
+      // LP_PF K-steps of B fragments in flight ahead of the MFMAs
+      bf16x8 bq[LP_PF][LP_RT];
 #pragma unroll
-      for (int rt = 0; rt < LP_RT; ++rt) bq[0][rt] = ld_sc1_b128(r_dg, boff[rt]);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        if (ks + 1 < KS) {
+      for (int p = 0; p < LP_PF - 1; ++p)
+        if (p < KS)
 #pragma unroll
           for (int rt = 0; rt < LP_RT; ++rt)
-            bq[(ks + 1) & 1][rt] = ld_sc1_b128(r_dg, boff[rt] + 64 * (ks + 1));
+            bq[p][rt] = DBG ? ld_dbg_b128(r_dg, boff[rt] + 64 * p, a.dbg) : ld_sc1_b128(r_dg, boff[rt] + 64 * p);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + LP_PF - 1 < KS) {
+#pragma unroll
+          for (int rt = 0; rt < LP_RT; ++rt)
+            bq[(ks + LP_PF - 1) % LP_PF][rt] =
+                DBG ? ld_dbg_b128(r_dg, boff[rt] + 64 * (ks + LP_PF - 1), a.dbg)
+                    : ld_sc1_b128(r_dg, boff[rt] + 64 * (ks + LP_PF - 1));
         }
 #pragma unroll
         for (int ut = 0; ut < LP_UT; ++ut)
 #pragma unroll
           for (int rt = 0; rt < LP_RT; ++rt)
-            acc[ut][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ut][ks], bq[ks & 1][rt],
+            acc[ut][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ut][ks], bq[ks % LP_PF][rt],
                                                                   acc[ut][rt], 0, 0, 0);
       }
 #pragma unroll
       for (int ut = 0; ut < LP_UT; ++ut)
 #pragma unroll
         for (int rt = 0; rt < LP_RT; ++rt) part[(w * LP_NF + ut * LP_RT + rt) * 64 + lane] = acc[ut][rt];
+      __syncthreads();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged operands landed (every wave)
-    __syncthreads();
     LP_STAMP(t, 2)
 
-    // 3. cell backward of the thread's (row, 4 units) slots
+    // 2. cell backward of the lane's (row, 4 units) slots; the operands were
+    // staged (and drained) during step t + 1
+    uint32_t ow[2][8];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      if (!e_ok[s]) continue;
-      const int i = e_row[s], r = r_lo + i;
+      if (s >= nslot) continue;
       f32x4v dh4 = f32x4v{0.f, 0.f, 0.f, 0.f};
       if (gemm) {
         const int f = e_ut * LP_RT + e_rt[s];
 #pragma unroll
         for (int ww = 0; ww < LP_WAVES; ++ww) dh4 += part[(ww * LP_NF + f) * 64 + lane];
       }
-      const uint4 gq0 = reinterpret_cast<const uint4*>(lds + LP_G_OFF)[i * LP_GSTRIDE + 2 * q];
-      const uint4 gq1 = reinterpret_cast<const uint4*>(lds + LP_G_OFF)[i * LP_GSTRIDE + 2 * q + 1];
-      const f32x4v ct = reinterpret_cast<const f32x4v*>(lds + LP_CT_OFF)[i * LP_CSTRIDE + q];
-      const f32x4v cp = t > 0 ? reinterpret_cast<const f32x4v*>(lds + LP_CP_OFF)[i * LP_CSTRIDE + q]
+      const uint4 gq0 = reinterpret_cast<const uint4*>(fr[s])[lane];
+      const uint4 gq1 = reinterpret_cast<const uint4*>(fr[s] + 1024)[lane];
+      const f32x4v ct = reinterpret_cast<const f32x4v*>(fr[s] + 2048 + 1024 * (t & 1))[lane];
+      const f32x4v cp = t > 0 ? reinterpret_cast<const f32x4v*>(fr[s] + 2048 + 1024 * ((t - 1) & 1))[lane]
                               : f32x4v{0.f, 0.f, 0.f, 0.f};
-      f32x4v dl = reinterpret_cast<const f32x4v*>(lds + LP_DL_OFF)[i * LP_CSTRIDE + q] * e_sc[s];
-      dl[0] = fmaf(e_a[s], bf2f(e_w[s].x & 0xffff), fmaf(e_b[s], bf2f(e_wx[s].x & 0xffff), dl[0]));
-      dl[1] = fmaf(e_a[s], bf2f(e_w[s].x >> 16), fmaf(e_b[s], bf2f(e_wx[s].x >> 16), dl[1]));
-      dl[2] = fmaf(e_a[s], bf2f(e_w[s].y & 0xffff), fmaf(e_b[s], bf2f(e_wx[s].y & 0xffff), dl[2]));
-      dl[3] = fmaf(e_a[s], bf2f(e_w[s].y >> 16), fmaf(e_b[s], bf2f(e_wx[s].y >> 16), dl[3]));
+      const f32x4v dl = reinterpret_cast<const f32x4v*>(fr[s] + 4096)[lane];
       const uint32_t gw[8] = {gq0.x, gq0.y, gq0.z, gq0.w, gq1.x, gq1.y, gq1.z, gq1.w};
-      uint32_t ow[8];
+      const int r = r_lo + e_row[s];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int u = uq + k;
@@ -276,16 +256,32 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArg
         const CellBwd cb = cell_bwd(a.cell, dh, dcr[s][k], bf2f(g01 & 0xffff), bf2f(g01 >> 16),
                                     bf2f(g23 & 0xffff), bf2f(g23 >> 16), ct[k], cp[k]);
         dcr[s][k] = cb.carry;
-        ow[2 * k] = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
-        ow[2 * k + 1] = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
+        ow[s][2 * k] = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
+        ow[s][2 * k + 1] = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
       }
-      const int voff = (int)((((int64_t)t * R + r) * KD + 4 * uq) * 2);
-      // write-through (sc1): team members read these rows in step t - 1
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{ow[0], ow[1], ow[2], ow[3]}, r_dg, voff, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{ow[4], ow[5], ow[6], ow[7]}, r_dg, voff + 16, 0,
-                                             16);
     }
-    // 4. publish step t: every storing wave drains, then ONE lane signals
+    // 3. step t - 1's operands into this wave's own fragments (its reads of
+    // them are done: their values are in registers), then the dG_t rows
+    if (t > 0) stage(t - 1, t - 2, true);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (!e_ok[s]) continue;
+      const int voff = (int)((((int64_t)t * R + r_lo + e_row[s]) * KD + 4 * uq) * 2);
+      // write-through (sc1): team members read these rows in step t - 1
+      if (DBG && (a.dbg & 4)) {  // (microbenchmark: plain stores)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4v{ow[s][0], ow[s][1], ow[s][2], ow[s][3]},
+                                               r_dg, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4v{ow[s][4], ow[s][5], ow[s][6], ow[s][7]},
+                                               r_dg, voff + 16, 0, 0);
+        continue;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{ow[s][0], ow[s][1], ow[s][2], ow[s][3]}, r_dg,
+                                             voff, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{ow[s][4], ow[s][5], ow[s][6], ow[s][7]}, r_dg,
+                                             voff + 16, 0, 16);
+    }
+    // 4. publish step t: every storing wave drains (its staging too), then
+    // ONE lane signals
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     LP_STAMP(t, 3)
@@ -297,6 +293,38 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArg
     for (int s = 0; s < 2; ++s)
       if (e_ok[s])
         *reinterpret_cast<f32x4v*>(a.dc_out + (int64_t)(r_lo + e_row[s]) * H + uq) = dcr[s];
+  }
+}
+
+// dl = scale * dh + a W[ys] + b W[yx] in place, one wavefront per row (the
+// loop reads the folded rows; lstm_bwd_loop_fold)
+__global__ __launch_bounds__(256) void lstm_bwd_fold_kernel(BwdLoopArgs a, int64_t NR) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= NR) return;
+  const int lane = threadIdx.x & 63, H = a.H;
+  const float sc = a.scale != nullptr ? a.scale[row] : 1.f;
+  const float wa = a.oh_a != nullptr ? a.oh_a[row] : 0.f;
+  const float wb = a.oh_b != nullptr ? a.oh_b[row] : 0.f;
+  const int ys = a.oh_a != nullptr ? max(a.oh_ys[row], 0) : 0;
+  const int yx = a.oh_b != nullptr ? max(a.oh_yx[row], 0) : 0;
+  float* d = const_cast<float*>(a.dh) + row * H;
+  for (int u = 4 * lane; u < H; u += 256) {
+    f32x4v x = *reinterpret_cast<const f32x4v*>(d + u) * sc;
+    if (a.oh_a != nullptr) {
+      const uint2 q = *reinterpret_cast<const uint2*>(a.oh_W + (int64_t)ys * H + u);
+      x[0] = fmaf(wa, bf2f(q.x & 0xffff), x[0]);
+      x[1] = fmaf(wa, bf2f(q.x >> 16), x[1]);
+      x[2] = fmaf(wa, bf2f(q.y & 0xffff), x[2]);
+      x[3] = fmaf(wa, bf2f(q.y >> 16), x[3]);
+    }
+    if (a.oh_b != nullptr) {
+      const uint2 q = *reinterpret_cast<const uint2*>(a.oh_W + (int64_t)yx * H + u);
+      x[0] = fmaf(wb, bf2f(q.x & 0xffff), x[0]);
+      x[1] = fmaf(wb, bf2f(q.x >> 16), x[1]);
+      x[2] = fmaf(wb, bf2f(q.y & 0xffff), x[2]);
+      x[3] = fmaf(wb, bf2f(q.y >> 16), x[3]);
+    }
+    *reinterpret_cast<f32x4v*>(d + u) = x;
   }
 }
 
@@ -347,23 +375,35 @@ void launch_lstm_bwd_loop(BwdLoopArgs a, hipStream_t stream) {
   a.nrb = g.nrb;
   a.rows_per_group = g.rows_per_group;
   a.rows_per_block = g.rows_per_block;
+  if (a.scale != nullptr || a.oh_a != nullptr) {
+    // the row scales and one-hot rows folded into dh (in place) first
+    const int64_t NR = (int64_t)a.T * a.R;
+    hipLaunchKernelGGL(lstm_bwd_fold_kernel, dim3((unsigned)((NR + 3) / 4)), dim3(256), 0, stream,
+                       a, NR);
+    post_launch("lstm_bwd_fold_kernel", stream);
+  }
   // team counters: zeroed by a memset node ahead of every launch
   (void)hipMemsetAsync(a.cnt, 0, sizeof(int) * 8 * g.nrb * LP_CNT_STRIDE, stream);
-#define LP_LAUNCH(KSV)                                                                          \
+#define LP_LAUNCH(KSV, DB)                                                                      \
   {                                                                                             \
     static bool attr = false;                                                                   \
     if (!attr) {                                                                                \
-      (void)hipFuncSetAttribute((const void*)lstm_bwd_loop_kernel<KSV>,                         \
+      (void)hipFuncSetAttribute((const void*)lstm_bwd_loop_kernel<KSV, DB>,                     \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LP_LDS);            \
       attr = true;                                                                              \
     }                                                                                           \
-    hipLaunchKernelGGL(lstm_bwd_loop_kernel<KSV>, dim3(g.grid), dim3(LP_THREADS), LP_LDS, stream, \
-                       a);                                                                      \
+    hipLaunchKernelGGL((lstm_bwd_loop_kernel<KSV, DB>), dim3(g.grid), dim3(LP_THREADS), LP_LDS,    \
+                       stream, a);                                                              \
   }
-  switch (a.H) {
-    case 128: LP_LAUNCH(2) break;
-    case 256: LP_LAUNCH(4) break;
-    default: LP_LAUNCH(8) break;
+  if (a.dbg != 0) {
+    if (a.H != 512) throw std::runtime_error("lstm_bwd_loop: debug variants at H = 512 only");
+    LP_LAUNCH(8, true)
+  } else {
+    switch (a.H) {
+      case 128: LP_LAUNCH(2, false) break;
+      case 256: LP_LAUNCH(4, false) break;
+      default: LP_LAUNCH(8, false) break;
+    }
   }
 #undef LP_LAUNCH
   post_launch("lstm_bwd_loop_kernel", stream);

@@ -38,6 +38,9 @@ namespace {
 
 constexpr int WG_BM = 128, WG_BN = 128, WG_BK = 64;
 constexpr int WG_A_BYTES = WG_BK * WG_BM * 2, WG_STAGE = WG_A_BYTES + WG_BK * WG_BN * 2;
+// fused column sums (CS): per stage the K tile's 64 weights (one 1 KB DMA
+// instruction, the first 256 bytes used) behind the operand stages
+constexpr int WG_AL_BYTES = 1024;
 // LDS-DMA wave-instructions per operand per stage per wave: 64 rows x 256 B =
 // 16 KiB = 16 instructions of 1 KiB (4 rows each), over 4 waves
 constexpr int WG_NI = WG_BK * 256 / 1024 / 4;
@@ -61,10 +64,14 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int off0, int off1) 
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int STAGES>
+// CS: the block also sums al[k] A[k][m] over its K range for the 32 columns
+// [m0 + 32 tn, m0 + 32 tn + 32) of its A tile (N = 512: the 4 column tiles of
+// an m tile split its 128 columns), from the A stage already in LDS: thread
+// (column c = tid & 31, K group kg = tid >> 5) adds 8 rows per K tile.
+template <int STAGES, bool CS>
 __global__ __launch_bounds__(256, 2) void wgrad_tn_kernel(WgradArgs g) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tiles_n = g.N / WG_BN, tiles = (g.M / WG_BM) * tiles_n;
+  const int tiles_n = g.N / WG_BN, tiles = ((g.M + WG_BM - 1) / WG_BM) * tiles_n;
   const int b = xcd_remap_w((int)blockIdx.x, tiles * g.S);
   const int s = b / tiles, t = b - s * tiles;
   const int tm = t / tiles_n, tn = t - tm * tiles_n;
@@ -92,6 +99,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn_kernel(WgradArgs g) {
     vb[i] = row * (int)g.ldb * 2 + n0 * 2 + ch * 16;
   }
   const int sa = WG_BK * (int)g.lda * 2, sb = WG_BK * (int)g.ldb * 2;  // bytes per K-tile
+  const rsrc_t ral = CS ? make_rsrc(g.al + kb, (int64_t)(g.K - kb) * 4) : ra;
+  char* s_al = lds + STAGES * WG_STAGE;
   auto issue = [&](int buf, int kt) {
     char* A = lds + buf * WG_STAGE;
     char* B = A + WG_A_BYTES;
@@ -99,7 +108,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn_kernel(WgradArgs g) {
     for (int i = 0; i < WG_NI; ++i) glds16(ra, va[i], kt * sa, A + 1024 * (w + 4 * i));
 #pragma unroll
     for (int i = 0; i < WG_NI; ++i) glds16(rb, vb[i], kt * sb, B + 1024 * (w + 4 * i));
+    if (CS && w == 0)  // the tile's 64 weights (lanes >= 16 duplicate, unused)
+      glds16(ral, 16 * (lane & 15), kt * WG_BK * 4, s_al + buf * WG_AL_BYTES);
   };
+  const int cs_c = threadIdx.x & 31, cs_kg = threadIdx.x >> 5;
+  const int cs_m = 32 * tn + cs_c;  // column within the A tile
+  float cs_acc = 0.f;
 
   // transposed-read offsets (within a 16-row K sub-step): group gq = l / 16
   // reads rows 8 (gq >> 1) + 4 jj + q, columns c0 + 16 (gq & 1) + 4 p .. + 3
@@ -137,6 +151,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn_kernel(WgradArgs g) {
     if (kt + STAGES - 1 < nk) issue((kt + STAGES - 1) % STAGES, kt + STAGES - 1);
     const char* A = lds + (kt % STAGES) * WG_STAGE;
     const char* B = A + WG_A_BYTES;
+    if (CS) {
+      const float* al = reinterpret_cast<const float*>(s_al + (kt % STAGES) * WG_AL_BYTES);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = 8 * cs_kg + i;
+        const uint16_t x = *reinterpret_cast<const uint16_t*>(
+            A + 256 * row + 16 * ((cs_m >> 3) ^ tr_swz(row)) + 2 * (cs_m & 7));
+        cs_acc = fmaf(al[row], bf2f(x), cs_acc);
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < WG_BK / 16; ++ks) {
       bf16x8 af[2], bfr[2];
@@ -152,6 +176,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn_kernel(WgradArgs g) {
     }
   }
 
+  if (CS) {  // the 8 K groups' sums of each column, through LDS
+    __syncthreads();  // (every wave is past its last LDS read of the stages)
+    float* s_red = reinterpret_cast<float*>(lds);
+    s_red[cs_kg * 32 + cs_c] = cs_acc;
+    __syncthreads();
+    const int m = m0 + cs_m;
+    if (threadIdx.x < 32 && m < g.M) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += s_red[k * 32 + cs_c];
+      if (g.S > 1)
+        g.ws_db[(int64_t)s * g.M + m] = v;
+      else
+        g.db[m] = v;
+    }
+  }
   // lane: column n0 + 64 wc + 32 j + (l & 31), rows m0 + 64 wr + 32 i + (r & 3) + 8 (r >> 2) + 4 (l >> 5)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -161,6 +201,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn_kernel(WgradArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + 64 * wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= g.M) continue;  // (ragged last m tile)
         float* dst;
         if (g.S > 1)
           dst = g.ws + ((int64_t)s * g.M + m) * g.N + n;
@@ -175,6 +216,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn_kernel(WgradArgs g) {
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs g) {
   const int n4 = g.N / 4;
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g.db != nullptr && idx < g.M) {  // fused column sums: the S partials in split order
+    float v = g.ws_db[idx];
+    for (int s = 1; s < g.S; ++s) v += g.ws_db[(int64_t)s * g.M + idx];
+    g.db[idx] = v;
+  }
   if (idx >= (int64_t)g.M * n4) return;
   const int m = (int)(idx / n4), c = (int)(idx - (int64_t)m * n4) * 4;
   const int64_t slab = (int64_t)g.M * g.N;
@@ -190,15 +236,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs g) {
 
 }  // namespace
 
+// M need not be a multiple of 128: the last m tile reads up to 128 columns
+// of every A row (past M they run into the row stride / the next row, or
+// past the last row's end, where the buffer resource returns zeros) and
+// stores only the columns < M
 bool wgrad_tn_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A,
                  const void* B) {
-  return M > 0 && N > 0 && K > 0 && M % WG_BM == 0 && N % WG_BN == 0 && lda % 8 == 0 &&
-         ldb % 8 == 0 && lda >= M && ldb >= N && (reinterpret_cast<uintptr_t>(A) & 15) == 0 &&
-         (reinterpret_cast<uintptr_t>(B) & 15) == 0 && K * std::max(lda, ldb) * 2 < (1LL << 31);
+  return M > 0 && N > 0 && K > 0 && N % WG_BN == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         lda >= M && ldb >= N && (reinterpret_cast<uintptr_t>(A) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(B) & 15) == 0 &&
+         K * std::max(lda, ldb) * 2 + 256 < (1LL << 31);
 }
 
 int wgrad_tn_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = (M / WG_BM) * (N / WG_BN);
+  const int64_t tiles = ((M + WG_BM - 1) / WG_BM) * (N / WG_BN);
   const int64_t nkt = (K + WG_BK - 1) / WG_BK;
   int64_t S = std::max<int64_t>(1, (512 + tiles - 1) / tiles);  // >= 2 blocks per CU
   S = std::min<int64_t>(S, std::max<int64_t>(1, nkt / 4));      // >= 4 K-tiles per split
@@ -212,12 +263,28 @@ void launch_wgrad_tn(WgradArgs g, hipStream_t stream) {
   g.kts = (int)((nkt + g.S - 1) / g.S);
   g.S = (int)((nkt + g.kts - 1) / g.kts);
   if (g.S > 1 && g.ws == nullptr) throw std::runtime_error("wgrad_tn: split-K needs a workspace");
-  const int blocks = (g.M / WG_BM) * (g.N / WG_BN) * g.S;
+  const bool cs = g.db != nullptr;
+  if (cs && (g.N != 512 || g.al == nullptr || (g.S > 1 && g.ws_db == nullptr)))
+    throw std::runtime_error("wgrad_tn: fused column sums need N = 512, weights and a workspace");
+  const int blocks = ((g.M + WG_BM - 1) / WG_BM) * (g.N / WG_BN) * g.S;
   constexpr int STAGES = 2;
-  hipLaunchKernelGGL(wgrad_tn_kernel<STAGES>, dim3(blocks), dim3(256), STAGES * WG_STAGE, stream, g);
+  if (cs) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)wgrad_tn_kernel<STAGES, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                STAGES * (WG_STAGE + WG_AL_BYTES));
+      attr = true;
+    }
+    hipLaunchKernelGGL((wgrad_tn_kernel<STAGES, true>), dim3(blocks), dim3(256),
+                       STAGES * (WG_STAGE + WG_AL_BYTES), stream, g);
+  } else {
+    hipLaunchKernelGGL((wgrad_tn_kernel<STAGES, false>), dim3(blocks), dim3(256), STAGES * WG_STAGE,
+                       stream, g);
+  }
   post_launch("wgrad_tn_kernel", stream);
   if (g.S > 1) {
-    const int64_t n = (int64_t)g.M * (g.N / 4);
+    const int64_t n = std::max<int64_t>((int64_t)g.M * (g.N / 4), cs ? g.M : 0);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, g);
     post_launch("wgrad_reduce_kernel", stream);
   }

@@ -200,7 +200,7 @@ void launch_vgrad_fix(const VGradRows& g, const uint16_t* hd, const uint16_t* W,
 // dhd = alpha . dhd in place (X = E' W -> dHd; dhd nullable: the consumer
 // scales the rows itself), hs = bf16(alpha . hd)
 void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd, float* dhd,
-                       uint16_t* hs, hipStream_t stream);
+                       uint16_t* hs, hipStream_t stream, int ldhs = 0);
 // dblog = sum_r alpha_r E_rv (two launches: per-row-block partials, reduce);
 // part: vgrad_colsum_blocks(NR) * V floats
 int vgrad_colsum_blocks(int64_t NR);
@@ -274,7 +274,8 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
 struct BwdLoopArgs {
   uint16_t* dG;            // (T, R, 4H) bf16 out: gate gradients of every step
   const uint16_t* whhT;    // (H, 4H) bf16 W_hh^T (packed gate columns)
-  const float* dh;         // (T, R, H) fp32 vocab-head h gradient (X or dHd)
+  const float* dh;         // (T, R, H) fp32 vocab-head h gradient (X or dHd); the row
+                           // scales and one-hot terms are folded into it IN PLACE
   const float* scale;      // (T, R) row scales of dh (nullable)
   const uint16_t* oh_W;    // one-hot terms (DhOneHot, all steps; oh_a null: none)
   const float* oh_a;
@@ -292,6 +293,8 @@ struct BwdLoopArgs {
   int poll_bound;
   int nub, nrb, rows_per_group, rows_per_block;  // (set by the launcher)
   int64_t* phases;         // microbenchmark: (grid, T, 4) wall-clock stamps (nullable)
+  int dbg;                 // microbenchmark variants: 1 plain B loads, 2 no B loads,
+                           // 4 plain dG stores (results not valid)
 };
 bool lstm_bwd_loop_ok(int R, int H, int T);
 int lstm_bwd_loop_counter_ints(int R, int H);
@@ -399,6 +402,11 @@ struct WgradArgs {
   int M0;
   float* C1;
   int64_t ldc1;
+  // fused weighted column sums (N == 512 only): db[m] = sum_k al[k] A[k][m]
+  // (al: K floats; ws_db: S x M floats when S > 1); null: none
+  const float* al;
+  float* db;
+  float* ws_db;
 };
 bool wgrad_tn_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A,
                  const void* B);

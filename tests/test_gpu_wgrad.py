@@ -55,3 +55,36 @@ def test_wgrad_headline_whh_shape():
 def test_wgrad_headline_token_shape():
     # S^T emb: K = V = 10,509 per-token rows
     _check(2048, 512, 10509, seed=2)
+
+
+def _check_colsum(M, K, lda, seed=0, nan_pad=True):
+    """dW_logit form: M = V columns of the exp store (row stride lda >= M, the
+    last 128-column tile ragged), N = H = 512, plus the fused weighted column
+    sums db = A^T al (the bias gradient)."""
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    N = 512
+    A = torch.rand(K, lda, generator=g).to(torch.bfloat16).to(DEV)
+    if nan_pad and lda > M:  # the row padding past V must not reach any output
+        A[:, M:] = float('nan')
+    B = (torch.randn(K, N, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    al = (torch.randn(K, generator=g) * 1e-2).to(DEV)
+    C, db = _ops().wgrad_tn_colsum(A, B, al, M, N, K)
+    torch.cuda.synchronize()
+    ref = A[:, :M].float().t() @ B.float()
+    ref_db = A[:, :M].float().t() @ al
+    assert torch.isfinite(C).all() and torch.isfinite(db).all()
+    assert ((C - ref).norm() / ref.norm()).item() < 1e-5
+    assert ((db - ref_db).norm() / ref_db.norm()).item() < 1e-5
+    C2, db2 = _ops().wgrad_tn_colsum(A, B, al, M, N, K)
+    assert torch.equal(C, C2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize('M,K,lda', [(300, 1000, 320), (128, 64, 128), (1299, 5 * 130, 1344)])
+def test_wgrad_ragged_m_with_column_sums(M, K, lda):
+    _check_colsum(M, K, lda)
+
+
+def test_wgrad_headline_dw_logit_with_bias_sums():
+    # dW_logit = E'^T (alpha Hd) and db = E'^T alpha: M = V = 10,509 (ldl =
+    # 10,560), K = 28 x 1280 rollout rows
+    _check_colsum(10509, 28 * 1280, 10560, seed=3, nan_pad=False)
