@@ -20,7 +20,7 @@ void grad_event_wait(int64_t k, int64_t stream);
 void grad_event_record(int64_t k, int64_t stream);
 int64_t grad_event_count(int64_t k);
 void set_poll_bound(int64_t n);
-void set_bwd_loop(bool on);
+void set_bwd_loop(int64_t mode);
 double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases,
                            int64_t dbg);
 int64_t device_errors(int64_t dev_index);
@@ -178,7 +178,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_poll_bound", &cst::set_poll_bound,
         "polls of a bounded cross-workgroup wait before it gives up (tests: 0)");
   m.def("set_bwd_loop", &cst::set_bwd_loop,
-        "reverse LSTM loop as one persistent launch (true, default) or one launch per step");
+        "reverse LSTM loop: 1 one persistent launch, row-read form (default); 2 persistent, "
+        "K-split team GEMM; 0 one launch per step");
   m.def("lstm_bwd_loop_bench", &cst::lstm_bwd_loop_bench, py::arg("R"), py::arg("H"), py::arg("T"),
         py::arg("iters"), py::arg("phases"), py::arg("dbg") = 0,
         "persistent reverse loop alone on random operands: us per launch (+ phase stamps)");

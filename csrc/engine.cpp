@@ -158,11 +158,32 @@ static int* device_err_word(int dev_index) {
 }
 // persistent reverse loop on (default; CSTCAP_BWD_LOOP=0 or set_bwd_loop(false):
 // one launch per step)
-static bool g_bwd_loop = [] {
+// (CSTCAP_BWD_LOOP=1: the persistent form whose workgroups read their rows'
+// whole dG_{t+1} -- the default; 2: the K-split form that exchanges fp32
+// partials instead, measured slower: 361.8 vs 331.6 us per loop alone,
+// 3.359-3.371 vs 3.338-3.345 ms per step, profiles/r6/README_r6.md)
+static int g_bwd_loop = [] {
   const char* e = getenv("CSTCAP_BWD_LOOP");
-  return e == nullptr || atoi(e) != 0;
+  return e == nullptr ? 1 : atoi(e);
 }();
-void set_bwd_loop(bool on) { g_bwd_loop = on; }
+void set_bwd_loop(int64_t mode) { g_bwd_loop = (int)mode; }
+// exchange slabs of the K-split persistent loop, per device (grown on demand
+// outside graph capture)
+static float* loop_xb(int dev_index, int64_t floats) {
+  static std::map<int, std::pair<float*, int64_t>> bufs;
+  auto it = bufs.find(dev_index);
+  if (it != bufs.end() && it->second.second >= floats) return it->second.first;
+  c10::hip::HIPGuard guard(dev_index);
+  if (it != bufs.end()) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(it->second.first);
+    bufs.erase(it);
+  }
+  float* p = nullptr;
+  TORCH_CHECK(hipMalloc(&p, sizeof(float) * floats) == hipSuccess, "loop exchange slabs: hipMalloc");
+  bufs.emplace(dev_index, std::make_pair(p, floats));
+  return p;
+}
 void set_poll_bound(int64_t n) { g_poll_bound = (int)std::max<int64_t>(0, n); }
 // team counters of the persistent reverse loop (lstm_loop.hip), per device;
 // the launcher zeroes the used prefix before every launch
@@ -717,6 +738,9 @@ double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::T
   la.err = device_err_word(dev.index());
   la.poll_bound = g_poll_bound;
   la.dbg = (int)dbg;
+  la.form = dbg >= 8 ? 0 : 1;  // (dbg 8: the K-split form; 0-7: the row-read form's variants)
+  if (dbg >= 8) la.dbg = 0;
+  if (la.form == 0) la.xb = loop_xb(dev.index(), lstm_bwd_loop_xb_floats((int)R, (int)H));
   hipStream_t st = cur_stream();
   for (int i = 0; i < 3; ++i) launch_lstm_bwd_loop(la, st);
   hipEvent_t e0, e1;
@@ -871,7 +895,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // (headline: 256 workgroups, one per CU, all resident: the side stream's
   // vocab-head weight gradients start after it).  CSTCAP_BWD_LOOP=0 keeps the
   // launch per step.
-  const bool persistent = g_bwd_loop && NL == 1 && !has_att && !has_s0 &&
+  const bool persistent = g_bwd_loop != 0 && NL == 1 && !has_att && !has_s0 &&
                           lstm_bwd_loop_ok((int)R, (int)H, (int)n_steps);
   // 1-2. vocab head on the side stream.  Exp store (training): alpha and the
   // one-hot terms folded into E, X = E' W (dHd = alpha X, scaled by the
@@ -1200,6 +1224,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     la.cnt = loop_counters((int)dev.index(), lstm_bwd_loop_counter_ints((int)R, (int)H));
     la.err = device_err_word((int)dev.index());
     la.poll_bound = g_poll_bound;
+    la.form = g_bwd_loop == 2 ? 0 : 1;
+    if (la.form == 0) la.xb = loop_xb((int)dev.index(), lstm_bwd_loop_xb_floats((int)R, (int)H));
     TORCH_CHECK(gates_all.is_contiguous() && c_all.is_contiguous() && dG_all.is_contiguous() &&
                     dHd.is_contiguous() && gates_all.size(0) >= n_steps && c_all.size(0) >= n_steps,
                 "persistent reverse loop: operand layout");

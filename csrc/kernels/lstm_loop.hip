@@ -296,6 +296,260 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_loop_kernel(BwdLoopArg
   }
 }
 
+// ---------------------------------------------------------------------------
+// K-split form (CSTCAP_BWD_LOOP=2; measured slower than the row-read form
+// above, 361.8 vs 331.6 us per loop: the partials' write-through round trip
+// through MALL costs what the redundant row reads did): the team's nub
+// workgroups split K = 4H instead
+// of the hidden units.  Workgroup j of a team owns hidden units [64 j, 64 j +
+// 64) for the cell backward, so it PRODUCES the dG columns [256 j, 256 j +
+// 256) (4 packed gates x 64 units) -- exactly its K slice of the next step's
+// GEMM.  Per step:
+//   1. dh partials P_j[rows][all H units] over its own K slice, with the
+//      B operand (its dG_{t+1} columns, bf16) already in LDS from its own
+//      epilogue -- no global read of dG at all; wave w computes the 64 units
+//      of unit block w (A operand: the W_hh^T slice [64 w .. +64) x [256 j ..
+//      +256), 128 VGPRs, resident for the whole loop);
+//   2. wave w hands P_j[rows][unit block w] (fp32, 12 KB) to workgroup w of
+//      the team: write-through (sc1) stores into a parity-double-buffered
+//      exchange slab, every wave drains, one lane adds to the team counter
+//      (its own partial stays in LDS);
+//   3. after the team counter shows every member's partials of this step,
+//      the epilogue lanes sum the nub - 1 partials (sc1 loads) and their own,
+//      run the cell backward, write dG_t to global memory (plain stores: only
+//      later kernels read it) and their K slice of it into the LDS B operand.
+// Per step a workgroup moves 7 x 12 KB out and in (headline) instead of
+// reading the row block's whole dG rows (160 KB, the same rows by all 8 team
+// members).  The exchange slab of parity p is rewritten two steps later, when
+// every member has published the step in between -- i.e. finished reading it.
+constexpr int LK_BSTRIDE = 528;   // bytes per LDS B row: 256 bf16 + 16 (conflict-free)
+constexpr int LK_B_BYTES = LP_MAXR * LK_BSTRIDE;
+constexpr int LK_OWN_BYTES = LP_NF * 64 * 16;  // own partial [frag][lane] float4
+constexpr int LK_B_OFF = 0, LK_OWN_OFF = LK_B_BYTES, LK_FR_OFF = LK_OWN_OFF + LK_OWN_BYTES;
+constexpr int LK_LDS = LK_FR_OFF + LP_NF * LP_FRAG_BYTES;
+static_assert(LK_LDS <= 160 * 1024, "K-split reverse loop: LDS budget");
+constexpr int LK_SLAB = LP_NF * 64 * 4;  // floats per (dst, src) partial: 12 frags x 64 lanes x 4
+
+__global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_ksplit_kernel(BwdLoopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int H = a.H, R = a.R, T = a.T, KD = 4 * H, nub = a.nub;
+  const int g = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int ub = j % nub, rb = j / nub;
+  const int team = g * a.nrb + rb;
+  const int u0 = 64 * ub;
+  const int rg0 = g * a.rows_per_group, rg1 = min(rg0 + a.rows_per_group, R);
+  const int r_lo = rg0 + rb * a.rows_per_block;
+  const int r_hi = min(r_lo + a.rows_per_block, rg1);
+  const int nrows = r_hi - r_lo;  // >= 1 (launcher)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ru = lane & 15, ku = lane >> 4;
+  const bool gemm_wave = w < nub;  // wave w: the partial of unit block w
+
+  // W_hh^T[64 w + 16 ut + ru][256 ub + 32 ks + 8 ku ..]: A fragments, resident
+  bf16x8 wf[LP_UT][8];
+#pragma unroll
+  for (int ut = 0; ut < LP_UT; ++ut)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      wf[ut][ks] = *reinterpret_cast<const bf16x8*>(
+          a.whhT + (int64_t)(64 * min(w, nub - 1) + 16 * ut + ru) * KD + 256 * ub + 32 * ks + 8 * ku);
+
+  // epilogue ownership as in lstm_bwd_loop_kernel
+  const int e_ut = w & 3;
+  const int nslot = w < 4 ? 2 : 1;
+  int e_rt[2], e_row[2], e_src[2];
+  bool e_ok[2];
+  e_rt[0] = w < 4 ? 0 : 1;
+  e_rt[1] = 2;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    e_row[s] = 16 * e_rt[s] + ru;
+    e_ok[s] = s < nslot && e_row[s] < nrows;
+    e_src[s] = r_lo + min(e_row[s], nrows - 1);
+  }
+  const int uq = u0 + 16 * e_ut + 4 * ku;
+  f32x4v dcr[2];
+  dcr[0] = dcr[1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const rsrc_t r_gates = make_rsrc(a.gates, (int64_t)T * R * KD * 2);
+  const rsrc_t r_c = make_rsrc(a.c_all, (int64_t)T * R * H * 4);
+  const rsrc_t r_dl = make_rsrc(a.dh, (int64_t)T * R * H * 4);
+  const float inv_keep = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
+  const uint32_t seed = rng_seed(a.rng, RNG_SLOT_DROPOUT);
+  int* cnt = a.cnt + team * LP_CNT_STRIDE;
+  char* b_lds = lds + LK_B_OFF;
+  f32x4v* own = reinterpret_cast<f32x4v*>(lds + LK_OWN_OFF);
+  char* fr[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) fr[s] = lds + LK_FR_OFF + (e_ut * LP_RT + e_rt[s]) * LP_FRAG_BYTES;
+  // exchange slabs: xb[parity][team][dst][src][frag][lane] float4
+  const int64_t team_floats = (int64_t)nub * nub * LK_SLAB;
+  const int nteams = 8 * a.nrb;
+  auto slab = [&](int par, int dst, int src) -> float* {
+    return a.xb + ((int64_t)par * nteams + team) * team_floats + ((int64_t)dst * nub + src) * LK_SLAB;
+  };
+  const rsrc_t r_xb = make_rsrc(a.xb, (int64_t)2 * nteams * team_floats * 4);
+  auto stage = [&](int ts, int tc, bool with_gd) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s >= nslot) continue;
+      const int64_t row = (int64_t)e_src[s];
+      if (with_gd) {
+        const int gb = (int)(((ts * (int64_t)R + row) * KD + 4 * uq) * 2);
+        dma16(r_gates, gb, fr[s]);
+        dma16(r_gates, gb + 16, fr[s] + 1024);
+        dma16(r_dl, (int)(((ts * (int64_t)R + row) * H + uq) * 4), fr[s] + 4096);
+      }
+      if (tc >= 0) dma16(r_c, (int)(((tc * (int64_t)R + row) * H + uq) * 4), fr[s] + 2048 + 1024 * (tc & 1));
+    }
+  };
+  int64_t* ph = a.phases != nullptr ? a.phases + (int64_t)blockIdx.x * T * 4 : nullptr;
+#define LK_STAMP(t, k) \
+  if (ph != nullptr && tid == 0) ph[(int64_t)(T - 1 - (t)) * 4 + (k)] = (int64_t)wall_clock64();
+
+  stage(T - 1, T - 1, true);
+  if (T >= 2) stage(0, T - 2, false);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = T - 1; t >= 0; --t) {
+    LK_STAMP(t, 0)
+    const bool gemm = t + 1 < T;
+    const int par = t & 1;
+    if (gemm) {
+      // 1. partial of unit block w over this workgroup's K slice
+      if (gemm_wave) {
+        f32x4v acc[LP_UT][LP_RT];
+#pragma unroll
+        for (int ut = 0; ut < LP_UT; ++ut)
+#pragma unroll
+          for (int rt = 0; rt < LP_RT; ++rt) acc[ut][rt] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          bf16x8 bq[LP_RT];
+#pragma unroll
+          for (int rt = 0; rt < LP_RT; ++rt)
+            bq[rt] = *reinterpret_cast<const bf16x8*>(b_lds + (16 * rt + ru) * LK_BSTRIDE +
+                                                      2 * (32 * ks + 8 * ku));
+#pragma unroll
+          for (int ut = 0; ut < LP_UT; ++ut)
+#pragma unroll
+            for (int rt = 0; rt < LP_RT; ++rt)
+              acc[ut][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ut][ks], bq[rt], acc[ut][rt],
+                                                                    0, 0, 0);
+        }
+        LK_STAMP(t, 1)
+        // 2. hand-off: own unit block into LDS, the others write-through
+        if (w == ub) {
+#pragma unroll
+          for (int ut = 0; ut < LP_UT; ++ut)
+#pragma unroll
+            for (int rt = 0; rt < LP_RT; ++rt) own[(ut * LP_RT + rt) * 64 + lane] = acc[ut][rt];
+        } else {
+          const int base = (int)((slab(par, w, ub) - a.xb) * 4);
+#pragma unroll
+          for (int ut = 0; ut < LP_UT; ++ut)
+#pragma unroll
+            for (int rt = 0; rt < LP_RT; ++rt)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc[ut][rt]), r_xb,
+                                                     base + ((ut * LP_RT + rt) * 64 + lane) * 16, 0,
+                                                     16);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+      __syncthreads();
+      if (tid == 0) {
+        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int target = nub * (T - 1 - t);
+        bool ok = false;
+        for (int it = 0; it < a.poll_bound; ++it) {
+          if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+            ok = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok && a.err != nullptr)
+          __hip_atomic_fetch_add(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only)
+    }
+    LK_STAMP(t, 2)
+
+    // 3. the sum of the team's partials + cell backward of the lane's slots
+    uint32_t ow[2][8];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s >= nslot) continue;
+      const int f = e_ut * LP_RT + e_rt[s];
+      f32x4v dh4 = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (gemm) {
+        f32x4v pv[7];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {  // (sources past nub - 1: loaded clamped, not added)
+          const int src = min(q < ub ? q : q + 1, nub - 1);
+          const int off = (int)((slab(par, ub, src) - a.xb) * 4) + (f * 64 + lane) * 16;
+          pv[q] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r_xb, off, 0, 16));
+        }
+        dh4 = own[f * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+          if (q < nub - 1) dh4 += pv[q];
+      }
+      const uint4 gq0 = reinterpret_cast<const uint4*>(fr[s])[lane];
+      const uint4 gq1 = reinterpret_cast<const uint4*>(fr[s] + 1024)[lane];
+      const f32x4v ct = reinterpret_cast<const f32x4v*>(fr[s] + 2048 + 1024 * (t & 1))[lane];
+      const f32x4v cp = t > 0 ? reinterpret_cast<const f32x4v*>(fr[s] + 2048 + 1024 * ((t - 1) & 1))[lane]
+                              : f32x4v{0.f, 0.f, 0.f, 0.f};
+      const f32x4v dl = reinterpret_cast<const f32x4v*>(fr[s] + 4096)[lane];
+      const uint32_t gw[8] = {gq0.x, gq0.y, gq0.z, gq0.w, gq1.x, gq1.y, gq1.z, gq1.w};
+      const int r = r_lo + e_row[s];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int u = uq + k;
+        const bool keep = a.drop_p <= 0.f || dropout_keep(seed, t, r, u, a.drop_p);
+        const float dh = dh4[k] + (keep ? dl[k] * inv_keep : 0.f);
+        const uint32_t g01 = gw[2 * k], g23 = gw[2 * k + 1];
+        const CellBwd cb = cell_bwd(a.cell, dh, dcr[s][k], bf2f(g01 & 0xffff), bf2f(g01 >> 16),
+                                    bf2f(g23 & 0xffff), bf2f(g23 >> 16), ct[k], cp[k]);
+        dcr[s][k] = cb.carry;
+        ow[s][2 * k] = (uint32_t)f2bf(cb.d0) | ((uint32_t)f2bf(cb.d1) << 16);
+        ow[s][2 * k + 1] = (uint32_t)f2bf(cb.d2) | ((uint32_t)f2bf(cb.d3) << 16);
+      }
+    }
+    // 4. step t - 1's staged operands (this wave's own fragments), dG_t out:
+    // global (later kernels) and this workgroup's K slice into the B operand
+    if (t > 0) stage(t - 1, t - 2, true);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s >= nslot) continue;
+      // B row 16 rt + ru, K bytes [2 x 4 x (uq - u0), + 32): padding rows get
+      // their values too (harmless: their partials are never read)
+      char* bp = b_lds + e_row[s] * LK_BSTRIDE + 8 * (uq - u0);
+      *reinterpret_cast<u32x4v*>(bp) = u32x4v{ow[s][0], ow[s][1], ow[s][2], ow[s][3]};
+      *reinterpret_cast<u32x4v*>(bp + 16) = u32x4v{ow[s][4], ow[s][5], ow[s][6], ow[s][7]};
+      if (e_ok[s]) {
+        uint16_t* dst = a.dG + (((int64_t)t * R + r_lo + e_row[s]) * KD + 4 * uq);
+        *reinterpret_cast<u32x4v*>(dst) = u32x4v{ow[s][0], ow[s][1], ow[s][2], ow[s][3]};
+        *reinterpret_cast<u32x4v*>(dst + 8) = u32x4v{ow[s][4], ow[s][5], ow[s][6], ow[s][7]};
+      }
+    }
+    // the B operand complete (LDS writes); the staging DMA and the dG stores
+    // are drained by the next step's hand-off wait, before its epilogue
+    __syncthreads();
+    LK_STAMP(t, 3)
+  }
+#undef LK_STAMP
+  if (a.dc_out != nullptr) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (e_ok[s])
+        *reinterpret_cast<f32x4v*>(a.dc_out + (int64_t)(r_lo + e_row[s]) * H + uq) = dcr[s];
+  }
+}
+
 // dl = scale * dh + a W[ys] + b W[yx] in place, one wavefront per row (the
 // loop reads the folded rows; lstm_bwd_loop_fold)
 __global__ __launch_bounds__(256) void lstm_bwd_fold_kernel(BwdLoopArgs a, int64_t NR) {
@@ -368,6 +622,11 @@ int lstm_bwd_loop_counter_ints(int R, int H) {
   return 8 * g.nrb * LP_CNT_STRIDE;
 }
 
+int64_t lstm_bwd_loop_xb_floats(int R, int H) {
+  const LoopGeom g = loop_geom(R, H);
+  return (int64_t)2 * 8 * g.nrb * g.nub * g.nub * LK_SLAB;
+}
+
 void launch_lstm_bwd_loop(BwdLoopArgs a, hipStream_t stream) {
   if (!lstm_bwd_loop_ok(a.R, a.H, a.T)) throw std::runtime_error("lstm_bwd_loop: unsupported shape");
   const LoopGeom g = loop_geom(a.R, a.H);
@@ -395,7 +654,16 @@ void launch_lstm_bwd_loop(BwdLoopArgs a, hipStream_t stream) {
     hipLaunchKernelGGL((lstm_bwd_loop_kernel<KSV, DB>), dim3(g.grid), dim3(LP_THREADS), LP_LDS,    \
                        stream, a);                                                              \
   }
-  if (a.dbg != 0) {
+  if (a.form == 0) {  // K-split (default)
+    if (a.xb == nullptr) throw std::runtime_error("lstm_bwd_loop: K-split form needs the exchange slabs");
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)lstm_bwd_ksplit_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LK_LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL(lstm_bwd_ksplit_kernel, dim3(g.grid), dim3(LP_THREADS), LK_LDS, stream, a);
+  } else if (a.dbg != 0) {
     if (a.H != 512) throw std::runtime_error("lstm_bwd_loop: debug variants at H = 512 only");
     LP_LAUNCH(8, true)
   } else {

@@ -293,11 +293,15 @@ struct BwdLoopArgs {
   int poll_bound;
   int nub, nrb, rows_per_group, rows_per_block;  // (set by the launcher)
   int64_t* phases;         // microbenchmark: (grid, T, 4) wall-clock stamps (nullable)
-  int dbg;                 // microbenchmark variants: 1 plain B loads, 2 no B loads,
-                           // 4 plain dG stores (results not valid)
+  int dbg;                 // microbenchmark variants of form 1: 1 plain B loads, 2 no B
+                           // loads, 4 plain dG stores (results not valid)
+  int form;                // 1: each workgroup reads its rows' whole dG_{t+1} (default);
+                           // 0: K-split team GEMM, partials exchanged (lstm_loop.hip)
+  float* xb;               // form 0: exchange slabs (lstm_bwd_loop_xb_floats)
 };
 bool lstm_bwd_loop_ok(int R, int H, int T);
 int lstm_bwd_loop_counter_ints(int R, int H);
+int64_t lstm_bwd_loop_xb_floats(int R, int H);
 void launch_lstm_bwd_loop(BwdLoopArgs a, hipStream_t stream);
 
 // attention.hip (temporal attention over num_chunks frames; MANet modal

@@ -1,5 +1,6 @@
-"""The reverse LSTM loop as ONE persistent launch (csrc/kernels/lstm_loop.hip)
-against the launch-per-step form (csrc/kernels/lstm.hip lstm_step_bwd_kernel)
+"""The reverse LSTM loop as ONE persistent launch (csrc/kernels/lstm_loop.hip:
+the K-split team GEMM with exchanged partials, and the row-read form) against
+the launch-per-step form (csrc/kernels/lstm.hip lstm_step_bwd_kernel)
 on identical inputs: the same forward (fixed RNG words), the REINFORCE /
 cross-entropy backward run once per form.  Both compute the same products
 with fp32 accumulation in a different summation order, so the gradients agree
@@ -45,13 +46,14 @@ def _grads(model, eng, data, mode, reward):
             if p.grad is not None}
 
 
+@pytest.mark.parametrize('form', [1, 2], ids=['rowread', 'ksplit'])
 @pytest.mark.parametrize('videos,S,H,V,mode', [
     (64, 20, 512, 10509, 'rl'),    # headline: 256 workgroups, 40-row blocks
     (64, 20, 512, 10509, 'xe'),
     (16, 20, 256, 3000, 'rl'),     # 8 x 40 rows, 4 unit blocks
     (10, 13, 128, 1299, 'rl'),     # ragged groups: 130 rows -> 17-row groups
 ], ids=['headline_rl', 'headline_xe', 'h256', 'h128_ragged'])
-def test_persistent_loop_matches_per_step_launches(videos, S, H, V, mode):
+def test_persistent_loop_matches_per_step_launches(videos, S, H, V, mode, form):
     from cst_captioning_amd import _ext
     ops = _ext.ops()
     model, eng, loader = _model(videos, S, H, V)
@@ -64,12 +66,12 @@ def test_persistent_loop_matches_per_step_launches(videos, S, H, V, mode):
     reward = torch.randn(videos * S, device=DEV)
     ops.reset_device_errors(0)
     try:
-        ops.set_bwd_loop(False)
+        ops.set_bwd_loop(0)
         ref = _grads(model, eng, data, mode, reward)
-        ops.set_bwd_loop(True)
+        ops.set_bwd_loop(form)
         got = _grads(model, eng, data, mode, reward)
     finally:
-        ops.set_bwd_loop(True)
+        ops.set_bwd_loop(1)
     assert ops.device_errors(0) == 0
     assert set(got) == set(ref)
     errs = {n: ((got[n] - ref[n]).norm() / (ref[n].norm() + 1e-20)).item() for n in ref}
