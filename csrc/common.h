@@ -87,6 +87,16 @@ __device__ __forceinline__ float h2f(uint16_t h) {
 __device__ __forceinline__ uint16_t f2h(float f) {
   return __builtin_bit_cast(uint16_t, (_Float16)f);
 }
+// 4 consecutive fp16 values (8 bytes) as a float4 (the fp16 gate tables:
+// the projected-embedding table P and the recurrent pre-activations)
+__device__ __forceinline__ float4 ld_h4(const uint16_t* p) {
+  const uint2 q = *reinterpret_cast<const uint2*>(p);
+  return make_float4(h2f(q.x & 0xffff), h2f(q.x >> 16), h2f(q.y & 0xffff), h2f(q.y >> 16));
+}
+__device__ __forceinline__ uint2 pack_h4(float a, float b, float c, float d) {
+  return make_uint2((uint32_t)f2h(a) | ((uint32_t)f2h(b) << 16),
+                    (uint32_t)f2h(c) | ((uint32_t)f2h(d) << 16));
+}
 
 // fast gate nonlinearities: one exp + one reciprocal each (rel. err ~1e-6)
 __device__ __forceinline__ float sigmoidf_(float x) {

@@ -316,8 +316,9 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   if (!has_att) TORCH_CHECK(vgate.scalar_type() == at::kFloat, "vgate must be fp32");
   check_cuda(ptab, "ptab");
   check_cuda(whh, "whh");
-  TORCH_CHECK(ptab.scalar_type() == at::kFloat && ptab.size(0) == emb.size(0) &&
-                  ptab.size(1) == wx.size(0), "ptab must be fp32 (V, 4H)");
+  TORCH_CHECK(ptab.scalar_type() == at::kHalf && ptab.size(0) == emb.size(0) &&
+                  ptab.size(1) == wx.size(0), "ptab must be fp16 (V, 4H)");
+  const uint16_t* PTAB = reinterpret_cast<const uint16_t*>(ptab.data_ptr());
   TORCH_CHECK(whh.scalar_type() == at::kBFloat16 && whh.size(0) >= wx.size(0) &&
                   whh.size(1) * 4 == wx.size(0), "whh must be bf16 (4H[+A], H)");
   const int64_t H4 = wx.size(0), H = H4 / 4, E = emb.size(1), V = wlog.size(0);
@@ -469,7 +470,18 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     h0 = zeros_view(dev, R * H, at::kBFloat16).view({R, H});
     c0 = zeros_view(dev, R * H, at::kFloat).view({R, H});
   }
-  at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32) : at::Tensor();
+  // pre-activations of the next step (the decode launch's recurrent tiles ->
+  // the combine's cell epilogue) in fp16: half the bytes of the combine's
+  // largest operand; fp32 where the VALU attention adds its video term into
+  // them in place (attention without the MFMA path)
+  static const bool pre16_env = [] {
+    const char* e = getenv("CSTCAP_PRE16");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const bool pre16 =
+      pre16_env && !(has_att && !att_mfma_ok((int)vgate_div, (int)C, (int)A, (int)H, per_frame));
+  at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32.dtype(pre16 ? at::kHalf : at::kFloat))
+                               : at::Tensor();
   at::Tensor xin = NL > 1 ? at::empty({R, H4}, f32) : at::Tensor();
 
   // layer l >= 1 at step t (its zero initial state is h0 / c0's zeros)
@@ -535,7 +547,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   if (has_att) run_att(0);
   // (zero initial state: null h / c, the kernel skips the recurrent GEMM)
   launch_lstm_step_fwd(have_labels ? LAB : bos.data_ptr<int64_t>(), have_labels ? L : 1,
-                       ptab.data_ptr<float>(),
+                       PTAB,
                        state0.empty() ? nullptr : reinterpret_cast<uint16_t*>(h0.data_ptr()),
                        state0.empty() ? nullptr : c0.data_ptr<float>(), VG, VDIV, (int)R, (int)H, WHH, h_buf(0, 0),
                        c_buf(0, 0), hd_buf(0, 0), (int)H, (float)drop_p, RNG, key(0, 0),
@@ -576,9 +588,10 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
         vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
         save ? reinterpret_cast<uint16_t*>(logits16[t].data_ptr()) : nullptr, ldl, part.data_ptr(),
         tgt, L, vflags, inv_temp, RNG, (int)t, h_buf(0, t), WHH, has_att ? nullptr : VG, VDIV,
-        next ? pre.data_ptr<float>() : nullptr, st, q_tiles ? (int)A : 0,
+        next ? reinterpret_cast<float*>(pre.data_ptr()) : nullptr, st, q_tiles ? (int)A : 0,
         q_tiles && next ? q_next.data_ptr<float>() : nullptr,
-        exp_t ? lse[t - 1].data_ptr<float>() : nullptr, att_mfma && next ? &am : nullptr);
+        exp_t ? lse[t - 1].data_ptr<float>() : nullptr, att_mfma && next ? &am : nullptr,
+        pre16 ? 1 : 0);
     if (q_tiles && next)
       launch_att_fwd(a_gv.data_ptr<float>(), a_pre.data_ptr<float>(), q_next.data_ptr<float>(),
                      nullptr, a_wa.data_ptr<float>(), a_ba.data_ptr<float>(), (int)Bv,
@@ -588,10 +601,11 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     CellLaunch cl{};
     if (next) {
       TORCH_CHECK(choose, "internal: a next step needs a chosen token");
-      cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_buf(0, t), c_buf(0, t + 1),
+      cl = CellLaunch{pre.data_ptr(), PTAB, c_buf(0, t), c_buf(0, t + 1),
                       h_buf(0, t + 1), hd_buf(0, t + 1), (int)H, gates_buf(0, t + 1), (int)H,
                       (float)drop_p, key(0, t + 1), (int)cell,
-                      att_mfma ? reinterpret_cast<const uint16_t*>(vg16.data_ptr()) : nullptr};
+                      att_mfma ? reinterpret_cast<const uint16_t*>(vg16.data_ptr()) : nullptr,
+                      pre16 ? 1 : 0};
     }
     launch_vocab_combine(part.data_ptr(), n_vt, (int)R, lse[t].data_ptr<float>(),
                            choose ? seq.data_ptr<int64_t>() + t : nullptr, T - 1,
@@ -996,7 +1010,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     const at::Tensor& rhs = ds_ready ? hd2 : hs;
     if (dw_aug) {
       // split-K batch over the augmented rows; the partial products summed
-      // into the dW slot and the bias gradient (hi + lo columns)
+      // into the dW slot and the bias gradient (hi + lo columns).  (One GEMM
+      // over all rows with the measured hipBLASLt choice: 3.439-3.451 vs
+      // 3.330-3.343 ms per step, profiles/r6/README_r6.md)
       const int64_t kr = NR / dw_split;
       at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
       at::Tensor p = at::bmm(a, hs.view({dw_split, kr, ldhs}), at::kFloat);  // (split, V, H + 16)
@@ -1906,7 +1922,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                      (int)A, (int)H4, vg_rows.data_ptr<float>(), nullptr, st, 0, per_frame);
     }
     // step 0: every row's cell from the initial state and BOS
-    launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, ptab.data_ptr<float>(),
+    launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, reinterpret_cast<const uint16_t*>(ptab.data_ptr()),
                          reinterpret_cast<const uint16_t*>(h[0].data_ptr()), c[0].data_ptr<float>(),
                          has_att ? vg_rows.data_ptr<float>() : VG, has_att ? 1 : (int)K, (int)R,
                          (int)H, WHH,
@@ -1938,7 +1954,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                        lp_hist.data_ptr<float>(), best_ppl.data_ptr<float>(),
                        best_seq.data_ptr<int64_t>(), best_lp.data_ptr<float>(),
                        tok.data_ptr<int64_t>(), next ? pre.data_ptr<float>() : nullptr,
-                       ptab.data_ptr<float>(), c[t & 1].data_ptr<float>(),
+                       reinterpret_cast<const uint16_t*>(ptab.data_ptr()), c[t & 1].data_ptr<float>(),
                        c[(t + 1) & 1].data_ptr<float>(),
                        reinterpret_cast<uint16_t*>(h[(t + 1) & 1].data_ptr()), (int)H, (int)cell,
                        has_att && next ? reinterpret_cast<const uint16_t*>(vg16.data_ptr())
@@ -1974,7 +1990,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                      att[3].data_ptr<float>(), att[4].data_ptr<float>(), (int)B, (int)K, (int)C,
                      (int)A, (int)H4, vg_rows.data_ptr<float>(), nullptr, st, 0, per_frame);
     }
-    launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, ptab.data_ptr<float>(),
+    launch_lstm_step_fwd(tok.data_ptr<int64_t>(), 1, reinterpret_cast<const uint16_t*>(ptab.data_ptr()),
                          reinterpret_cast<const uint16_t*>(hp.data_ptr()), cp.data_ptr<float>(),
                          has_att ? vg_rows.data_ptr<float>() : vgate.data_ptr<float>(),
                          has_att ? 1 : (int)K, (int)R, (int)H, WHH,
@@ -2284,9 +2300,9 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
     TORCH_CHECK(lstm, "the cell needs the recurrent part");
     check_cuda(ptab, "ptab");
     check_cuda(c_prev, "c_prev");
-    TORCH_CHECK(ptab.scalar_type() == at::kFloat && ptab.size(0) == V && ptab.size(1) == 4 * H &&
+    TORCH_CHECK(ptab.scalar_type() == at::kHalf && ptab.size(0) == V && ptab.size(1) == 4 * H &&
                     c_prev.scalar_type() == at::kFloat && c_prev.numel() == R * H,
-                "ptab (V, 4H) / c_prev (R, H) fp32");
+                "ptab (V, 4H) fp16 / c_prev (R, H) fp32");
   }
   const bool has_unf = unfinished.defined() && unfinished.numel() > 0;
   if (has_unf)
@@ -2332,11 +2348,12 @@ std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor
       st, 0, nullptr, save == 2 ? eoff.data_ptr<float>() : nullptr, nullptr);
   CellLaunch cl{};
   if (do_cell)
-    cl = CellLaunch{pre.data_ptr<float>(), ptab.data_ptr<float>(), c_prev.data_ptr<float>(),
-                    c_out.data_ptr<float>(), reinterpret_cast<uint16_t*>(h_out.data_ptr()),
+    cl = CellLaunch{pre.data_ptr<float>(), reinterpret_cast<const uint16_t*>(ptab.data_ptr()),
+                    c_prev.data_ptr<float>(), c_out.data_ptr<float>(),
+                    reinterpret_cast<uint16_t*>(h_out.data_ptr()),
                     reinterpret_cast<uint16_t*>(hdrop.data_ptr()), (int)H,
                     reinterpret_cast<uint16_t*>(gates.data_ptr()), (int)H, (float)drop_p,
-                    (int)step + 1, (int)cell, nullptr};
+                    (int)step + 1, (int)cell, nullptr, 0};
   launch_vocab_combine(part.data_ptr(), n, (int)R, lse.data_ptr<float>(), tok.data_ptr<int64_t>(),
                        1, gsel.data_ptr<float>(), 1, has_tgt ? gxe.data_ptr<float>() : nullptr, 1,
                        TG, 1, (int)mode, (float)ss_prob, rng_ptr(rng), (int)step, CNT, 2, UNF, st,

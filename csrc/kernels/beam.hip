@@ -454,7 +454,7 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
 #pragma unroll
       for (int jj = 0; jj < UPT; ++jj) {
         const int u = min(tid + BF_THREADS * jj, H - 1);
-        xc[e][jj] = *reinterpret_cast<const float4*>(a.ptab + tk * 4 * H + 4 * u);
+        xc[e][jj] = ld_h4(a.ptab + tk * 4 * H + 4 * u);
       }
     }
   }
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(BF_THREADS) void beam_fused_step_kernel(BeamFusedAr
 #pragma unroll
       for (int jj = 0; jj < UPT; ++jj) {
         const int u = min(tid + BF_THREADS * jj, H - 1);
-        xv[v][jj] = *reinterpret_cast<const float4*>(a.ptab + tk * 4 * H + 4 * u);
+        xv[v][jj] = ld_h4(a.ptab + tk * 4 * H + 4 * u);
       }
     }
   }

@@ -38,7 +38,7 @@ __device__ __forceinline__ int xcd_remap_l(int bid, int nwg) {
 
 template <int BM, int STAGES>
 __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
-    const int64_t* __restrict__ tok, int64_t tok_stride, const float* __restrict__ ptab,
+    const int64_t* __restrict__ tok, int64_t tok_stride, const uint16_t* __restrict__ ptab,
     const uint16_t* __restrict__ h_prev, const float* __restrict__ c_prev,
     const float* __restrict__ vgate, int vgate_div, int R, int H,
     const uint16_t* __restrict__ whh, uint16_t* __restrict__ h_out, float* __restrict__ c_out,
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256, 2) void lstm_step_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int row = rg + 16 * i, r = min(r0 + row, R - 1);
-    pre_px[i] = ptab ? *reinterpret_cast<const float4*>(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u)
+    pre_px[i] = ptab ? ld_h4(ptab + (int64_t)s_tok[row] * (4 * H) + n0 + 4 * u)
                      : make_float4(0.f, 0.f, 0.f, 0.f);
     pre_vg[i] = *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vgate_div) * (4 * H) + n0 + 4 * u);
     pre_c[i] = c_prev ? c_prev[(int64_t)(row_map ? row_map[r] : r) * H + hu] : 0.f;
@@ -819,7 +819,7 @@ void launch_lstm_step_bwd(const uint16_t* dg_next, const uint16_t* whhT, const f
 }
 
 // 128-row tiles x 64 packed gate columns, 3 LDS stages (72 KB, 2 blocks per CU)
-void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
+void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* ptab,
                           const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,

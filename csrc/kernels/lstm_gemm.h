@@ -3,7 +3,9 @@
 //
 //   pre_{t+1}[r][n] = sum_k h_t[r][k] W_hh[n][k] + vgate[r / vdiv][n]
 //
-// (packed gate order, fp32 out).  With temporal attention the weight operand
+// (packed gate order, fp32 accumulation; fp32 out, or fp16 with PH: the
+// combine reads half the bytes -- pre-activations are O(1), fp16 keeps 11
+// significant bits where the saved gates and h are bf16).  With temporal attention the weight operand
 // carries NQ = A extra rows (W_q): those tiles write the attention query of
 // step t+1, q_{t+1} = h_t W_q^T, to q_out instead, and vgate is nullptr (the
 // attention kernel adds the per-row video term into pre afterwards).
@@ -30,7 +32,7 @@ __host__ __device__ constexpr int lstm_gemm_blocks(int R, int H, int NQ = 0) {
   return ((4 * H + NQ) / LG_BN) * ((R + LG_BM - 1) / LG_BM);
 }
 
-template <class LT = LGTile>
+template <class LT = LGTile, bool PH = false>
 __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restrict__ h, int R,
                                                 int H, const uint16_t* __restrict__ whh,
                                                 const float* __restrict__ vgate, int vdiv,
@@ -80,8 +82,15 @@ __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restr
       } else if (vgate != nullptr) {
         const float4 vg =
             *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * (4 * H) + n0 + 4 * u);
-        *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) =
-            make_float4(x.x + vg.x, x.y + vg.y, x.z + vg.z, x.w + vg.w);
+        if (PH)
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(pre) + (int64_t)r * (4 * H) + n0 +
+                                    4 * u) = pack_h4(x.x + vg.x, x.y + vg.y, x.z + vg.z, x.w + vg.w);
+        else
+          *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) =
+              make_float4(x.x + vg.x, x.y + vg.y, x.z + vg.z, x.w + vg.w);
+      } else if (PH) {
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(pre) + (int64_t)r * (4 * H) + n0 +
+                                  4 * u) = pack_h4(x.x, x.y, x.z, x.w);
       } else {
         *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) = x;
       }

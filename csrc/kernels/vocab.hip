@@ -470,9 +470,10 @@ int combine_count_ints_per_step() { return CMB_CNT_SLOTS * CMB_CNT_STRIDE; }
 // Cell epilogue of the NEXT decode step, applied as soon as its input token
 // is chosen (see lstm_gemm.h): gates = pre + P[tok] -> i, f, g, o -> c, h.
 struct CellArgs {
-  const float* pre;    // (R, 4H) h_t W_hh^T + vgate, packed gates; nullptr = no cell
+  const void* pre;     // (R, 4H) h_t W_hh^T + vgate, packed gates, fp32 (fp16 with
+                       // pre_half); nullptr = no cell
   const uint16_t* vg16;  // nullable (R, 4H) bf16 per-row video gates (MFMA attention)
-  const float* ptab;   // (V, 4H) projected embedding table
+  const uint16_t* ptab;  // (V, 4H) fp16 projected embedding table
   const float* c_prev;
   float* c_out;
   uint16_t* h_out;
@@ -483,7 +484,15 @@ struct CellArgs {
   float drop_p;
   int step;  // decode step of the cell (dropout mask index)
   int cell;  // CellType
+  int pre_half;
 };
+// the 4 packed pre-activations of hidden unit u of a row (PH: fp16 pre)
+template <bool PH>
+__device__ __forceinline__ float4 load_pre(const CellArgs& c, int64_t row_off, int u) {
+  return PH ? ld_h4(reinterpret_cast<const uint16_t*>(c.pre) + row_off + 4 * u)
+            : *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(c.pre) + row_off +
+                                               4 * u);
+}
 
 struct RowStat {
   float m, s, zv, zl, xm, xt;
@@ -568,7 +577,7 @@ __device__ __forceinline__ int finish_row(const RowStat& a, int r, const RowSel&
   return (int)tok;
 }
 
-template <int LANES>
+template <int LANES, bool PH>
 __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     const VocabPartial* __restrict__ part, int n_vt, int R, float* __restrict__ lse_out,
     int64_t* __restrict__ tok_out, int64_t tok_stride, float* __restrict__ g_sel,
@@ -609,11 +618,11 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   uint2 ve[CELL_U];
   if (pre_early) {
     const int H = cell.H;
-    const float* prow = cell.pre + (int64_t)r * 4 * H;
+    const int64_t prow = (int64_t)r * 4 * H;
 #pragma unroll
     for (int k = 0; k < CELL_U; ++k) {
       const int u = min(sub + k * LANES, H - 1);  // (clamped: no branch)
-      pe[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
+      pe[k] = load_pre<PH>(cell, prow, u);
       ce[k] = cell.c_prev[(int64_t)r * H + u];
       if (cell.vg16 != nullptr)
         ve[k] = *reinterpret_cast<const uint2*>(cell.vg16 + (int64_t)r * 4 * H + 4 * u);
@@ -674,8 +683,8 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     const int tk = __shfl(tok_final, (int)(threadIdx.x & 63) & ~(LANES - 1), 64);
     if (valid) {
       const int H = cell.H;
-      const float* prow = cell.pre + (int64_t)r * 4 * H;
-      const float* trow = cell.ptab + (int64_t)tk * 4 * H;
+      const int64_t prow = (int64_t)r * 4 * H;
+      const uint16_t* trow = cell.ptab + (int64_t)tk * 4 * H;
       const float inv_keep = cell.drop_p > 0.f ? 1.f / (1.f - cell.drop_p) : 1.f;
       const uint32_t dseed = rng_seed(rng, RNG_SLOT_DROPOUT);
       // batches of CELL_U units (all of H = 512 in one): every load of a
@@ -691,15 +700,15 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
             p[k] = pe[k];
             cp[k] = ce[k];
             vq[k] = ve[k];
-            x[k] = *reinterpret_cast<const float4*>(trow + 4 * min(u0 + k * LANES, H - 1));
+            x[k] = ld_h4(trow + 4 * min(u0 + k * LANES, H - 1));
           }
         } else {
 #pragma unroll
           for (int k = 0; k < CELL_U; ++k) {
             const int u = u0 + k * LANES;
             if (u < H) {
-              p[k] = *reinterpret_cast<const float4*>(prow + 4 * u);
-              x[k] = *reinterpret_cast<const float4*>(trow + 4 * u);
+              p[k] = load_pre<PH>(cell, prow, u);
+              x[k] = ld_h4(trow + 4 * u);
               cp[k] = cell.c_prev[(int64_t)r * H + u];
               if (cell.vg16 != nullptr)
                 vq[k] = *reinterpret_cast<const uint2*>(cell.vg16 + (int64_t)r * 4 * H + 4 * u);
@@ -760,7 +769,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
 // the MFMA temporal attention of step t+1, one per video (att_mfma.h): they
 // depend only on h_t too, and are dispatched first, so they finish under the
 // vocabulary tiles.
-template <int BN, int STAGES, int OCC, class LT, int AV, bool TOPK = false>
+template <int BN, int STAGES, int OCC, class LT, int AV, bool TOPK = false, bool PH = false>
 __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
     VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
     const float* __restrict__ vgate, int vdiv, float* __restrict__ pre, int n_lstm_pad, int NQ,
@@ -778,7 +787,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
   }
   if (bid < n_lstm_pad) {
     if (bid < lstm_gemm_blocks(R, H, NQ))
-      lstm_gemm_block<LT>(bid, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
+      lstm_gemm_block<LT, PH>(bid, h_t, R, H, whh, vgate, vdiv, pre, lds, NQ, q_out);
     return;
   }
   vocab_tr_block<BN, STAGES, TOPK>(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
@@ -885,16 +894,21 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   CellArgs cell{};
   if (cl != nullptr) {
     cell = CellArgs{cl->pre, cl->vg16, cl->ptab, cl->c_prev, cl->c_out, cl->h_out,
-                    cl->hdrop_out, cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step, cl->cell};
+                    cl->hdrop_out, cl->ldh, cl->gates_out, cl->H, cl->drop_p, cl->step, cl->cell,
+                    cl->pre_half};
   }
-  hipLaunchKernelGGL(vocab_combine_kernel<CMB_LANES>, dim3((R + CMB_ROWS - 1) / CMB_ROWS),
+  // (fp16 pre as a template parameter: a runtime select between the two
+  // load forms cost 1.6 us per combine, 14.3 vs 12.7 us in rocprofv3)
+  auto kern = cell.pre_half ? vocab_combine_kernel<CMB_LANES, true>
+                            : vocab_combine_kernel<CMB_LANES, false>;
+  hipLaunchKernelGGL(kern, dim3((R + CMB_ROWS - 1) / CMB_ROWS),
                      dim3(CMB_THREADS), 0, stream, (const VocabPartial*)part, n_vt, R, lse_out,
                      tok_out, tok_stride, g_sel, gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode,
                      ss_prob, rng, step, counts, count_step, unfinished, cell);
   post_launch("vocab_combine_kernel", stream);
 }
 
-template <int BN, int STAGES, int OCC, class LT, int AV, bool TOPK = false>
+template <int BN, int STAGES, int OCC, class LT, int AV, bool TOPK = false, bool PH = false>
 static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const uint16_t* W,
                                 const float* bias, int V, uint16_t* logits16, int64_t ldl,
                                 void* part, const int64_t* tgt, int64_t tgt_stride, int flags,
@@ -919,11 +933,11 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   const int grid = n_att + n_l + n_vt * n_rt;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, TOPK>,
+    (void)hipFuncSetAttribute((const void*)vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, TOPK, PH>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, TOPK>), dim3(grid), dim3(256),
+  hipLaunchKernelGGL((vocab_lstm_fwd_kernel<BN, STAGES, OCC, LT, AV, TOPK, PH>), dim3(grid), dim3(256),
                      LDS, stream, hd, ldh, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part,
                      tgt, tgt_stride, flags, inv_temp, rng, step, eoff, h_t, whh, vgate, vdiv, pre,
                      n_l, NQ, q_out, a, n_att);
@@ -938,11 +952,12 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
                           const int64_t* tgt, int64_t tgt_stride, int flags, float inv_temp,
                           const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                           const float* vgate, int vdiv, float* pre, hipStream_t stream, int NQ,
-                          float* q_out, const float* eoff, const AttMfmaArgs* att) {
+                          float* q_out, const float* eoff, const AttMfmaArgs* att, int pre_half) {
   // 64-row tiles, 3 blocks per CU (48 KB of LDS each; the recurrent tiles use
   // 2 stages to fit): one block's epilogue overlaps the others' main loops.
   // Measured 4.47 vs 4.54 ms per step against 128-row tiles at 2 blocks per
   // CU (3 interleaved rounds; profiles/r2/ab_vocab_tiles.txt)
+  if ((flags & VF_TOPK) && pre_half) throw std::runtime_error("vocab_lstm_fwd: fp16 pre with VF_TOPK");
   if (flags & VF_TOPK) {  // beam search: per-tile top-K candidates
     if (vf_topk_k(flags) < 1 || vf_topk_k(flags) > VF_TOPK_MAXK)
       throw std::runtime_error("vocab_lstm_fwd: VF_TOPK needs 1 <= K <= 8");
@@ -971,11 +986,16 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
 #undef VT
     return vocab_num_tiles(V);
   }
-#define VL(AVX)                                                                            \
-  launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, \
-                                              tgt, tgt_stride, flags, inv_temp, rng, step,  \
-                                              h_t, whh, vgate, vdiv, pre, NQ, q_out, stream, \
-                                              eoff, att)
+#define VL(AVX)                                                                                \
+  if (pre_half)                                                                                \
+    launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX, false, true>(                                  \
+        hd, ldh, R, H, W, bias, V, logits16, ldl, part, tgt, tgt_stride, flags, inv_temp, rng, \
+        step, h_t, whh, vgate, vdiv, pre, NQ, q_out, stream, eoff, att);                       \
+  else                                                                                         \
+    launch_vocab_lstm_t<64, 2, 3, LGTile2, AVX>(hd, ldh, R, H, W, bias, V, logits16, ldl, part, \
+                                                tgt, tgt_stride, flags, inv_temp, rng, step,  \
+                                                h_t, whh, vgate, vdiv, pre, NQ, q_out, stream, \
+                                                eoff, att)
   if (att == nullptr) {
     VL(0);
     return vocab_num_tiles(V);

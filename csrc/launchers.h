@@ -19,7 +19,7 @@ struct BeamFusedArgs {
   float* best_lp;
   int64_t* tok_out;
   const float* pre;   // (R, 4H) h_t W_hh^T + video gates; nullptr = no cell (last step)
-  const float* ptab;  // (V, 4H)
+  const uint16_t* ptab;  // (V, 4H) fp16
   const float* c_in;  // (R, H)
   float* c_out;
   uint16_t* h_out;    // (R, H) bf16
@@ -84,8 +84,8 @@ void launch_vocab_fwd(const uint16_t* hd, int ldh, int R, int H, const uint16_t*
                       const float* eoff = nullptr);  // flags: 1 = sample, 2 = argmax, 8 = fp32 logits, 16 = exp store
 // Cell epilogue of the next step, fused into the combine (see lstm_gemm.h).
 struct CellLaunch {
-  const float* pre;
-  const float* ptab;
+  const void* pre;        // (R, 4H) fp32, or fp16 with pre_half
+  const uint16_t* ptab;   // (V, 4H) fp16 projected embedding table
   const float* c_prev;
   float* c_out;
   uint16_t* h_out;
@@ -97,6 +97,7 @@ struct CellLaunch {
   int step;
   int cell;  // CellType (common.h)
   const uint16_t* vg16;  // nullable (R, 4H) bf16 per-row video gates (attention)
+  int pre_half;
 };
 // temporal-attention forward operands (kernels/att_fwd.h)
 struct AttFwdArgs {
@@ -155,7 +156,7 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
                            const uint32_t* rng, int step, const uint16_t* h_t, const uint16_t* whh,
                            const float* vgate, int vdiv, float* pre, hipStream_t stream,
                            int NQ = 0, float* q_out = nullptr, const float* eoff = nullptr,
-                           const AttMfmaArgs* att = nullptr);
+                           const AttMfmaArgs* att = nullptr, int pre_half = 0);
 // exp store of step 0: fp16 logits rows -> bf16 exp(x - lse_r), in place
 void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,
                               hipStream_t stream);
@@ -208,7 +209,7 @@ void launch_vgrad_colsum(const uint16_t* E, int64_t ldl, int V, int64_t NR, cons
                          float* part, float* dblog, hipStream_t stream);
 
 // lstm.hip
-void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const float* ptab,
+void launch_lstm_step_fwd(const int64_t* tok, int64_t tok_stride, const uint16_t* ptab,
                           const uint16_t* h_prev, const float* c_prev, const float* vgate,
                           int vgate_div, int R, int H, const uint16_t* whh, uint16_t* h_out,
                           float* c_out, uint16_t* hdrop_out, int ldh, float drop_p,

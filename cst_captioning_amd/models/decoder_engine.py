@@ -405,7 +405,10 @@ class DecoderEngine:
         self.wq = self.whh_q[4 * H:] if self.attention else None
         self.emb = torch.empty(V, E, **bf)
         self.wlog = torch.empty(V, H, **bf)
-        self.ptab = torch.empty(V, 4 * H, dtype=torch.float32, device=dev)
+        # (fp16: the decode's cell epilogue gathers one row per caption row and
+        # step; half the bytes of fp32, 11 significant bits for these O(1)
+        # gate pre-activation terms)
+        self.ptab = torch.empty(V, 4 * H, dtype=torch.float16, device=dev)
         # upper layers of a stacked decoder: packed [W_ih_l | W_hh_l] and a
         # contiguous copy of W_hh_l (the step kernel's B operand)
         self.layers = getattr(model, 'num_layers', 1)
@@ -500,7 +503,7 @@ class DecoderEngine:
     def update_ptab(self):
         # input-token gate table P = emb . W_ie^T (V x 4H, packed gate order):
         # one GEMM per optimizer step instead of K=E of work in every decode step
-        torch.mm(self.emb, self.wx[:, :self.E].t(), out_dtype=torch.float32, out=self.ptab)
+        self.ptab.copy_(torch.mm(self.emb, self.wx[:, :self.E].t(), out_dtype=torch.float32))
         self._ptab_version = self.weights_version
 
     def prefetch_ptab(self):

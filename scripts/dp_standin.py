@@ -68,7 +68,7 @@ def run(dev, ctx, ds, priority, blocks, us, steps):
     # device stamps (a new capture carries the stamp nodes)
     for name, standin in (('stamps_no_standin', None), ('stamps_standin', (blocks, us))):
         tr.bucket.standin = standin
-        tr._graph = None
+        tr._graph_key = None  # (recaptured with the stamp nodes)
         stamps.enable(dev)
         for _ in range(3):
             tr.train_step(loader.get_batch(), 0)

@@ -146,7 +146,7 @@ def test_sampling_matches_softmax():
 
 def _cell_inputs(R, V, H, seed):
     g = torch.Generator(device=DEV).manual_seed(seed)
-    ptab = torch.randn(V, 4 * H, device=DEV, generator=g) * 0.5
+    ptab = (torch.randn(V, 4 * H, device=DEV, generator=g) * 0.5).half()  # (the engine's fp16 table)
     c_prev = torch.randn(R, H, device=DEV, generator=g)
     return ptab, c_prev
 
@@ -182,7 +182,7 @@ def test_combine_cell_matches_fp32(R, vdiv, mode, eos, unf, save):
         assert bool((o[11].view(3, -1)[2] != 0).any()) == bool((tok != 0).any())
     # the cell against fp32 PyTorch: gates = h W_hh^T + vgate + P[token]
     pre = h.float() @ whh.float().t() + vg.repeat_interleave(vdiv, 0)[:R]
-    gates = (pre + ptab[tok]).view(R, H, 4)
+    gates = (pre + ptab[tok].float()).view(R, H, 4)
     i_, f_, g_, o_ = (gates[..., k] for k in range(4))
     c_ref = torch.sigmoid(f_) * c_prev + torch.sigmoid(i_) * torch.tanh(g_)
     h_ref = torch.sigmoid(o_) * torch.tanh(c_ref)
