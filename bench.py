@@ -101,8 +101,9 @@ def parse():
                    help='scst, headline config: also time the XE recipe (BASELINE config 2, the '
                         'reference\'s cross-entropy warm-up stage: teacher forcing, same '
                         'model / batch) in the same invocation and report it as the "xe" field')
-    p.add_argument('--comm_priority', default='high', choices=['high', 'normal'],
-                   help='data parallelism: priority of the gradient all-reduce stream')
+    p.add_argument('--comm_priority', default='normal', choices=['high', 'normal'],
+                   help='data parallelism: priority of the gradient all-reduce stream (high '
+                        'measured 1.7x slower per step, profiles/r6/dp_standin_rccl.json)')
     p.add_argument('--scb_baseline', type=int, default=1, choices=[1, 2],
                    help='CST baseline: 1 = GT consensus scores (CST_MS_SCB), 2 = the samples\' own '
                         'scores (CST_MS_SCB(*))')

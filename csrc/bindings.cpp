@@ -21,6 +21,7 @@ void grad_event_record(int64_t k, int64_t stream);
 int64_t grad_event_count(int64_t k);
 void set_poll_bound(int64_t n);
 void set_bwd_loop(int64_t mode);
+void set_att_fuse(bool on);
 double lstm_bwd_loop_bench(int64_t R, int64_t H, int64_t T, int64_t iters, at::Tensor phases,
                            int64_t dbg);
 int64_t device_errors(int64_t dev_index);
@@ -183,6 +184,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_bwd_loop_bench", &cst::lstm_bwd_loop_bench, py::arg("R"), py::arg("H"), py::arg("T"),
         py::arg("iters"), py::arg("phases"), py::arg("dbg") = 0,
         "persistent reverse loop alone on random operands: us per launch (+ phase stamps)");
+  m.def("set_att_fuse", &cst::set_att_fuse,
+        "attention backward fused into the reverse step (true, default) or a launch per step");
   m.def("device_errors", &cst::device_errors,
         "failed cross-workgroup hand-offs counted on the device (synchronous read)");
   m.def("reset_device_errors", &cst::reset_device_errors);

@@ -115,6 +115,21 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
 
+// Scorer value u = tanh(.) of the temporal attention as ONE fp16 word for the
+// backward: v = 1 - |u| with u's sign.  The backward needs u and 1 - u^2 =
+// v (2 - v); stored as u itself, 1 - u^2 cancels near saturation (|u| -> 1:
+// fp16 spacing 2^-11 below 1, up to 100 % relative error of the tanh
+// derivative), while v keeps fp16's relative precision exactly there; for
+// small |u| the absolute error of u stays below 2^-12.
+__device__ __forceinline__ uint16_t u_enc(float u) { return f2h(copysignf(1.f - fabsf(u), u)); }
+struct UDec {
+  float u, d;  // u and 1 - u^2
+};
+__device__ __forceinline__ UDec u_dec(uint16_t h) {
+  const float x = h2f(h), v = fabsf(x);
+  return UDec{copysignf(1.f - v, x), v * (2.f - v)};
+}
+
 // murmur3 32-bit finaliser: avalanche hash used as a counter-based RNG for
 // the per-element sampling draws (hash(row-key ^ v * odd constant)).
 __device__ __forceinline__ uint32_t mix32(uint32_t h) {

@@ -167,6 +167,11 @@ static int g_bwd_loop = [] {
   return e == nullptr ? 1 : atoi(e);
 }();
 void set_bwd_loop(int64_t mode) { g_bwd_loop = (int)mode; }
+// fused attention backward (lstm.hip att_bwd_fused_wg, the fp16 scorer values
+// of the forward) on; off: the separate att_bwd_mfma launch per step, which
+// recomputes tanh(P + q) in fp32 (tests of the fp16 encoding)
+static bool g_att_fuse = true;
+void set_att_fuse(bool on) { g_att_fuse = on; }
 // exchange slabs of the K-split persistent loop, per device (grown on demand
 // outside graph capture)
 static float* loop_xb(int dev_index, int64_t floats) {
@@ -1168,7 +1173,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // the two reverse steps; the dalpha partials alternate between two buffers
   // (att8: 4.717 / 4.728 vs 4.884 / 4.939 ms per step unfused, interleaved on
   // one box, profiles/r5/README_r5.md)
-  const bool att_fuse = att_mfma && n_steps > 1 && a_u.defined() &&
+  const bool att_fuse = g_att_fuse && att_mfma && n_steps > 1 && a_u.defined() &&
                         a_u.scalar_type() == at::kHalf && a_u.size(0) == n_steps &&
                         a_u.size(1) == R && a_u.size(2) == C && a_u.size(3) == A &&
                         att_bwd_fuse_ok((int)vdiv, (int)C, (int)A, (int)H, (int)Bv, (int)R);

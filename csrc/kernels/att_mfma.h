@@ -152,10 +152,10 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
       ec[j] = fmaf(wv.z, t2, ec[j]);
       ec[j] = fmaf(wv.w, t3, ec[j]);
       const int row = 16 * j + ru;
-      if (g.u_out != nullptr && row < vdiv)  // the backward's scorer values (fp16)
+      if (g.u_out != nullptr && row < vdiv)  // the backward's scorer values (fp16, u_enc)
         *reinterpret_cast<uint2*>(g.u_out + ((int64_t)(row0 + row) * C + c) * A + a0 + u0) =
-            make_uint2((uint32_t)f2h(t0) | ((uint32_t)f2h(t1) << 16),
-                       (uint32_t)f2h(t2) | ((uint32_t)f2h(t3) << 16));
+            make_uint2((uint32_t)u_enc(t0) | ((uint32_t)u_enc(t1) << 16),
+                       (uint32_t)u_enc(t2) | ((uint32_t)u_enc(t3) << 16));
       ec[j] += __shfl_xor(ec[j], 16, 64);
       ec[j] += __shfl_xor(ec[j], 32, 64);
     }

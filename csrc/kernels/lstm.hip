@@ -266,8 +266,9 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 // The attention workgroup (video b) of step t + 1 (see AttBwdEpi).  The scorer
-// values u = tanh(P + q) come from the forward (fp16, AttMfmaArgs::u_out), so
-// the backward has no transcendental:
+// values u = tanh(P + q) come from the forward (one fp16 word each, common.h
+// u_enc: accurate 1 - u^2 near saturation), so the backward has no
+// transcendental:
 //   dalpha[r][c] = the sum of the H/64 step-(t+1) partials; softmax backward
 //   de = alpha (dalpha - sum_k alpha_k dalpha_k); thread (units 4 cq..4 cq+3,
 //   rows rq, rq + 4, ...): dq[r][a] = w_a[a] sum_c de[r][c] (1 - u^2) (4 bf16
@@ -347,10 +348,11 @@ __device__ __forceinline__ void att_bwd_fused_wg(const AttBwdEpi& f, int b, int 
         for (int c = 0; c < CP; ++c) {
           if (c < C) {
             const float de = s_de[k * CP + c];
-            const f32x2_t u01 = {h2f(u[i][c].x & 0xffff), h2f(u[i][c].x >> 16)};
-            const f32x2_t u23 = {h2f(u[i][c].y & 0xffff), h2f(u[i][c].y >> 16)};
+            const UDec e0 = u_dec(u[i][c].x & 0xffff), e1 = u_dec(u[i][c].x >> 16);
+            const UDec e2 = u_dec(u[i][c].y & 0xffff), e3 = u_dec(u[i][c].y >> 16);
+            const f32x2_t u01 = {e0.u, e1.u}, u23 = {e2.u, e3.u};
             const f32x2_t de2 = {de, de};
-            const f32x2_t g01 = de2 * (1.f - u01 * u01), g23 = de2 * (1.f - u23 * u23);
+            const f32x2_t g01 = de2 * f32x2_t{e0.d, e1.d}, g23 = de2 * f32x2_t{e2.d, e3.d};
             dq01 += g01;
             dq23 += g23;
             dp[c][0] += g01;

@@ -125,10 +125,11 @@ def build_parser():
     add('--grad_wire', type=str, default='fp32', choices=['fp32', 'bf16'],
         help='data-parallel gradient reduction: fp32 all-reduce, or bf16 on the wire with '
              'fp32 accumulation (all-to-all + all-gather, half the bytes)')
-    add('--comm_priority', type=str, default='high', choices=['high', 'normal'],
+    add('--comm_priority', type=str, default='normal', choices=['high', 'normal'],
         help='data parallelism: priority of the stream that all-reduces the gradient slices '
-             'under the backward (high: a hardware queue of its own; normal: shares the '
-             'normal-priority queues with the replayed step)')
+             'under the backward.  normal (default); high: a hardware queue of its own, '
+             'measured to slow the whole replayed step from 3.38 to 5.75 ms '
+             '(scripts/dp_standin.py, profiles/r6/dp_standin_rccl.json)')
     add('--dp_update', type=str, default='allreduce', choices=['allreduce', 'sharded'],
         help='data-parallel update: all-reduce the fp32 gradient and run Adam on the whole '
              'buffer on every rank (default), or reduce-scatter -> Adam on this rank\'s '

@@ -182,9 +182,12 @@ class _DecoderFn(torch.autograd.Function):
         ctx.shapes = (w_ih.shape, emb_w.shape)
         ctx.has_att = has_att
         ctx.state0 = state0 if save else []
-        # the video-gate node of this pass (ops/featpool.py _FeatPoolVgateFn)
+        # the video-gate node that produced THIS call's vgate (ops/featpool.py
+        # VgHandoff: matched by the tensor's identity; any other pending
+        # hand-off is dropped here)
         vg_pending = eng.__dict__.pop('_vg_pending', None)
-        ctx.vg_ctx = vg_pending if (save and not has_att and not state0) else None
+        ctx.vg_ctx = (vg_pending if (save and not has_att and not state0 and vg_pending is not None
+                                     and vg_pending.matches(vgate)) else None)
         ctx.att_saved = None
         ctx.xw_late = None
         if save:
@@ -276,7 +279,7 @@ class _DecoderFn(torch.autograd.Function):
         vg_ctx, ctx.vg_ctx = getattr(ctx, 'vg_ctx', None), None
         if (vg_ctx is not None and emb_direct and 'fp_w0' in direct and eng.layers == 1
                 and not ctx.state0):
-            fc, xs, wsd, vg_p, vg_nf = vg_ctx
+            fc, xs, wsd, vg_p, vg_nf = vg_ctx.payload
             vg_bwd = ([eng.dst_ie, eng.dst_hh, direct['wih'], direct['whh'],
                        eng.model.core.rnn.weight_ih_l0.detach(), fc]
                       + [direct['fp_w%d' % f] for f in range(vg_nf)]
@@ -320,7 +323,7 @@ class _DecoderFn(torch.autograd.Function):
         w_ih_shape, emb_shape = ctx.shapes
         if vg_bwd:  # (written by the engine)
             d_wih = d_whh = None
-            eng._vg_done = True
+            vg_ctx.done = True  # the video-gate node's own backward is a no-op
         elif emb_direct:
             direct['wih'][:, :E].copy_(d_ie)
             direct['whh'].copy_(d_hh)

@@ -54,6 +54,26 @@ class _FeatPoolFn(torch.autograd.Function):
         return (None, None, None) + (None,) * nf + tuple(g[:nf]) + tuple(g[nf:])
 
 
+class VgHandoff:
+    """Hand-off between one :class:`_FeatPoolVgateFn` node and the decoder
+    node that consumes ITS output: the payload the decoder backward needs to
+    run this node's backward inside the engine, the identity of the vg tensor
+    it belongs to (data pointer and shape: a decoder call with another vg
+    ignores it), and ``done``, set by that decoder backward so this node's
+    own backward becomes a no-op.  Kept on the node's ctx, not on the engine:
+    a stale hand-off from a no-grad / eval call cannot leak into the next
+    training step."""
+    __slots__ = ('payload', 'key', 'done')
+
+    def __init__(self, payload, vg):
+        self.payload = payload
+        self.key = (vg.data_ptr(), tuple(vg.shape))
+        self.done = False
+
+    def matches(self, vg):
+        return vg is not None and self.key == (vg.data_ptr(), tuple(vg.shape))
+
+
 class _FeatPoolVgateFn(torch.autograd.Function):
     """FeatPool + the video gate term of the fused engine in one node:
     ``vg = pack(FeatPool(x) . W_ih[:, E:]^T)`` (packed gate slots, see
@@ -63,7 +83,7 @@ class _FeatPoolVgateFn(torch.autograd.Function):
     zero-fill / accumulate passes), else returned."""
 
     @staticmethod
-    def forward(ctx, eng, p, rng, nf, *args):
+    def forward(ctx, eng, p, rng, nf, record, *args):
         xs, ws, bs, w_ih = args[:nf], args[nf:2 * nf], args[2 * nf:3 * nf], args[3 * nf]
         wsd = [w.detach() for w in ws]
         fc = _ext.ops().featpool_forward(list(xs), wsd, [b.detach() for b in bs], p, rng)
@@ -72,19 +92,21 @@ class _FeatPoolVgateFn(torch.autograd.Function):
         ctx.eng, ctx.p, ctx.nf, ctx.wih_shape = eng, p, nf, w_ih.shape
         ctx.save_for_backward(fc, *xs, *wsd)
         # the decoder forward that consumes vg takes these, so its backward
-        # can run this node's backward inside the engine (vg_bwd)
-        eng._vg_pending = (fc, list(xs), wsd, p, nf)
+        # can run this node's backward inside the engine (vg_bwd); only when
+        # this node is recorded for a backward (no hand-off from eval / beam)
+        ctx.handoff = VgHandoff((fc, list(xs), wsd, p, nf), vg) if record else None
+        eng._vg_pending = ctx.handoff
         return vg
 
     @staticmethod
     def backward(ctx, dvg):
         eng, nf = ctx.eng, ctx.nf
-        if getattr(eng, '_vg_done', False):
+        h, ctx.handoff = ctx.handoff, None
+        if h is not None and h.done:
             # the decoder backward already ran this node's backward (vg_bwd)
             # and wrote W_ih's video columns and the FeatPool gradient slots
-            eng._vg_done = False
             eng.take_video_slots()
-            return (None,) * (4 + 4 * nf)
+            return (None,) * (5 + 4 * nf)
         fc, *rest = ctx.saved_tensors
         xs, ws = list(rest[:nf]), list(rest[nf:])
         E = eng.E
@@ -97,11 +119,11 @@ class _FeatPoolVgateFn(torch.autograd.Function):
             outs = [direct['fp_w%d' % f] for f in range(nf)] + \
                    [direct['fp_b%d' % f] for f in range(nf)]
             _ext.ops().featpool_backward(dfc, fc, xs, ws, ctx.p, outs)
-            return (None,) * (4 + 4 * nf)
+            return (None,) * (5 + 4 * nf)
         d_wih = fc.new_zeros(ctx.wih_shape)
         d_wih[:, E:] = dvg_u.t() @ fc
         g = _ext.ops().featpool_backward(dfc, fc, xs, ws, ctx.p, [])
-        return (None,) * (4 + nf) + tuple(g[:nf]) + tuple(g[nf:]) + (d_wih,)
+        return (None,) * (5 + nf) + tuple(g[:nf]) + tuple(g[nf:]) + (d_wih,)
 
 
 class _AttInputsFn(torch.autograd.Function):
@@ -209,8 +231,9 @@ def featpool_vgate(eng, model, feats):
     dev = feats[0].device
     rng = _seeds(p, dev)
     xs = [_rows(f) for f in feats]
-    return _FeatPoolVgateFn.apply(eng, p, rng, len(xs), *xs, *[l.weight for l in lins],
-                                  *[l.bias for l in lins], model.core.rnn.weight_ih_l0)
+    params = [l.weight for l in lins] + [l.bias for l in lins] + [model.core.rnn.weight_ih_l0]
+    record = torch.is_grad_enabled() and any(t.requires_grad for t in params + xs)
+    return _FeatPoolVgateFn.apply(eng, p, rng, len(xs), record, *xs, *params)
 
 
 def featpool(pool, feats):

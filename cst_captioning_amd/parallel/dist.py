@@ -270,7 +270,7 @@ class FlatGradBucket:
         ``grad_scale``), so no separate pass over the buffer divides it."""
         return 1.0 / ctx.world_size if (ctx.enabled and self.wire == 'fp32') else 1.0
 
-    def set_groups(self, groups, ctx, priority='high'):
+    def set_groups(self, groups, ctx, priority='normal'):
         """Leading slices reduced as soon as the backward marks them final:
         ``groups`` = [params of slice 0, params of slice 1(, slice 2)] (at
         most three; they must be the buffer's leading parameters, in order).
@@ -290,15 +290,15 @@ class FlatGradBucket:
             self.groups.append((off, off + n))
             off += n
         if self.grad.is_cuda and self.comm is None:
-            # A HIGH-priority stream: the HIP runtime keeps one pool of
-            # hardware queues per priority (GPU_MAX_HW_QUEUES each), so this
-            # stream gets a queue of its own instead of sharing one of the 4
-            # normal-priority queues with the replayed graph -- an in-order
-            # queue shared with the graph would hold the collective behind
-            # the whole replay whatever the event says.
-            # (--comm_priority normal: priority 0, for the measured trade-off
-            # against the high-priority queue's CU share during the reverse
-            # loop, profiles/r6/README_r6.md)
+            # Normal priority by default.  A HIGH-priority stream gets a
+            # hardware queue of its own (the HIP runtime keeps one pool of
+            # queues per priority), but measured with the trainer's replayed
+            # step and 1-rank RCCL collectives on it, the high-priority queue
+            # slowed the WHOLE step from 3.38 to 5.75 ms (the rollout most),
+            # and a 32-workgroup stand-in for a ring kernel cost +160 us at
+            # normal vs +290 us at high priority (scripts/dp_standin.py,
+            # profiles/r6/dp_standin_rccl.json); the slices still start
+            # inside the backward at normal priority.
             self.comm = torch.cuda.Stream(device=self.grad.device,
                                           priority=-1 if priority == 'high' else 0)
             self._ev_start = torch.cuda.Event()

@@ -1,7 +1,7 @@
 """Comm-stream priority under a collective-shaped load (verdict r5 item 5).
 
 The trainer's data-parallel step at the HEADLINE shape (64 videos x 20
-captions, V = 10,509, L = 30; DistContext world size 2 over a 1-rank gloo
+captions, V = 10,509, L = 30; DistContext world size 2 over a 1-rank
 group, so the streamed bucket, the slice events and the replayed graphs are
 built exactly as under RCCL while each collective is a no-op).  Where the
 vocab-head slice's all-reduce starts -- on the comm stream, right after the
@@ -99,8 +99,13 @@ def main():
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group('gloo', rank=0, world_size=1, init_method='tcp://127.0.0.1:%s' % port)
-    ctx = DistContext(rank=0, world_size=2, local_rank=0, device=dev, backend='gloo')
+    # a 1-rank RCCL communicator (backend nccl): the collectives of the
+    # shipped path are real RCCL launches on the comm stream, each a no-op
+    # copy (a 1-rank gloo group would route every CUDA all-reduce through the
+    # host, ~5 ms per step, profiles/r6/dp_standin_gloo_distorted.json)
+    dist.init_process_group('nccl', rank=0, world_size=1, init_method='tcp://127.0.0.1:%s' % port,
+                            device_id=dev)
+    ctx = DistContext(rank=0, world_size=2, local_rank=0, device=dev, backend='nccl')
     ds = make_synthetic('msrvtt', num_videos=6513, vocab_size=10509, seed=123)
     res = {'standin_blocks': blocks, 'standin_us': us, 'steps': steps}
     for pr in ('high', 'normal'):

@@ -58,8 +58,13 @@ def main(out):
     opt.seq_length, opt.feat_dims = loader.get_seq_length(), loader.get_feat_dims()
     model, engine = build_model(opt, ctx.device)
     assert engine is not None
+    opt.comm_priority = os.environ.get('CSTCAP_TEST_COMM_PRIO', 'normal')
     tr = Trainer(opt, model, loader, None, ctx, engine)
     tr.rl_training = True
+    standin = os.environ.get('CSTCAP_TEST_STANDIN')  # 'blocks,us': a ring-kernel stand-in
+    if standin:
+        b, us = standin.split(',')
+        tr.bucket.standin = (int(b), float(us))
     stamps.enable(ctx.device)  # before the capture: the graph carries the stamp nodes
     runs = []
     oks = []

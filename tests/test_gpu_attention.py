@@ -135,3 +135,79 @@ def test_attention_greedy_and_beam_match_torch(H, S):
         assert (b == b_ref).all(1).float().mean().item() >= 0.8, (K, b, b_ref)
 
 
+
+
+def test_fused_attention_backward_fp16_scorer_values_near_saturation():
+    """The fused attention backward reads the forward's scorer values u =
+    tanh(P + q) as one fp16 word each (common.h u_enc: 1 - |u| with u's
+    sign), the per-step launch recomputes tanh in fp32.  With the scorer
+    inputs scaled so most u are saturated (|u| > 0.99), the attention
+    parameters' gradients of the two paths agree to 1e-2 relative (the
+    plain fp16 u lost up to all of 1 - u^2 there)."""
+    from cst_captioning_amd import _ext
+    from cst_captioning_amd.models import CrossEntropyCriterion
+    ops = _ext.ops()
+    ds, opt, model, loader = _tiny(C=8, H=128, S=10)
+    with torch.no_grad():
+        model.temporal_att.f_feat.weight.mul_(8.0)  # saturate tanh(P + q)
+    eng = _engine(model, opt)
+    model.train()
+    data = loader.get_batch()
+    grads = {}
+    try:
+        for fuse in (False, True):
+            ops.set_att_fuse(fuse)
+            model.zero_grad(set_to_none=True)
+            torch.manual_seed(0)
+            g_xe = eng.teacher_forced(model, data['feats'], data['labels'])
+            CrossEntropyCriterion()(g_xe, data['labels'][:, 1:], data['masks'][:, 1:]).backward()
+            grads[fuse] = {n: p.grad.clone() for n, p in model.named_parameters()
+                           if p.grad is not None}
+    finally:
+        ops.set_att_fuse(True)
+    for k in ('temporal_att.f_h.weight', 'temporal_att.f_feat.weight', 'temporal_att.f_feat.bias',
+              'temporal_att.align.weight', 'core.rnn.weight_hh_l0'):
+        a, b = grads[True][k], grads[False][k]
+        err = ((a - b).norm() / (b.norm() + 1e-20)).item()
+        assert err < 1e-2, (k, err)
+
+
+@pytest.mark.parametrize('H', [128, 512])
+def test_attention_inputs_node_matches_fp32_module_path(H):
+    """ops/featpool.py _AttInputsFn (FeatPool + ONE bf16-operand GEMM for the
+    per-frame gate table Gv and the projected frames P, fp32 accumulation and
+    fp32 gradients) against the model's fp32 module path (FeatPool module,
+    the W_ih video-column Linear and temporal_att.f_feat): outputs and the
+    gradients of W_ih's video columns, f_feat and the FeatPool parameters
+    under random upstream gradients.  Stated tolerance: 1e-2 relative (only
+    the GEMM operands and the upstream gradient are bf16-rounded)."""
+    from cst_captioning_amd.ops.featpool import att_inputs
+    ds, opt, model, loader = _tiny(C=8, H=H, S=5, feat_dims=(96, 64))
+    eng = _engine(model, opt)
+    model.eval()  # (no FeatPool dropout: both paths see the same frames)
+    data = loader.get_batch()
+    feats = data['feats']
+    gv, pre = att_inputs(eng, model, feats)
+    ref = copy.deepcopy(model)
+    frames = ref.feat_pool(feats)  # (B, C, F*H), fp32 module
+    w_iv = ref.core.rnn.weight_ih_l0[:, eng.E:]
+    gv_ref = eng.pack_rows(torch.nn.functional.linear(frames, w_iv), eng.src_ie, 2)
+    pre_ref = ref.temporal_att.f_feat(frames)
+    for a, b in ((gv, gv_ref), (pre, pre_ref)):
+        assert ((a - b).norm() / b.norm()).item() < 1e-2
+    g = torch.Generator(device=DEV).manual_seed(7)
+    dgv = torch.randn(gv.shape, device=DEV, generator=g)
+    dpre = torch.randn(pre.shape, device=DEV, generator=g)
+    torch.autograd.backward([gv, pre], [dgv, dpre])
+    torch.autograd.backward([gv_ref, pre_ref], [dgv, dpre])
+    names = ['core.rnn.weight_ih_l0', 'temporal_att.f_feat.weight', 'temporal_att.f_feat.bias']
+    names += [n for n, _ in model.named_parameters() if n.startswith('feat_pool')]
+    got = dict(model.named_parameters())
+    want = dict(ref.named_parameters())
+    for n in names:
+        a, b = got[n].grad, want[n].grad
+        assert a is not None and b is not None, n
+        if n == 'core.rnn.weight_ih_l0':  # the video columns (the token columns: no gradient here)
+            a, b = a[:, eng.E:], b[:, eng.E:]
+        err = ((a - b).norm() / (b.norm() + 1e-20)).item()
+        assert err < 1e-2, (n, err)
