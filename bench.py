@@ -353,7 +353,7 @@ def main():
         r = run_config(a, ctx, 8, sync)
         att8 = {'value': round(r['caps'], 2), 'ms_per_step': round(r['ms'], 3),
                 'temporal_attention_frames': 8, 'final_loss': r['loss'],
-                'skipped_steps': r['skipped']}
+                'skipped_steps': r['skipped'], 'device_errors': r['device_errors']}
         if r['stamps']:
             att8['stamps_us'] = r['stamps']
     cst = None
@@ -372,7 +372,8 @@ def main():
         r = run_config(a, ctx, 1, sync, mode='xe')
         xe = {'value': round(r['caps'], 2), 'ms_per_step': round(r['ms'], 3),
               'recipe': 'XE (teacher forcing)', 'final_loss': r['loss'],
-              'skipped_steps': r['skipped'], 'cuda_graph': r['graph']}
+              'skipped_steps': r['skipped'], 'cuda_graph': r['graph'],
+              'device_errors': r['device_errors']}
     dt, ms, caps, vids = main_run['dt'], main_run['ms'], main_run['caps'], main_run['vids']
     loss, n_params, t_gen = main_run['loss'], main_run['n_params'], main_run['t_gen']
     S = 20
