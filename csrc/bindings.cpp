@@ -60,6 +60,8 @@ std::vector<at::Tensor> cst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tens
                                          at::Tensor bref, int64_t S, int64_t k);
 std::vector<at::Tensor> scst_loss_forward(at::Tensor seq, at::Tensor lp, at::Tensor sample,
                                           at::Tensor greedy);
+std::vector<at::Tensor> xe_loss_forward(at::Tensor labels, at::Tensor lp, int64_t off);
+at::Tensor xe_loss_backward(at::Tensor cnt, at::Tensor out, at::Tensor dloss, int64_t T);
 at::Tensor scst_loss_backward(at::Tensor seq, at::Tensor reward, at::Tensor out,
                               at::Tensor dloss);
 at::Tensor featpool_forward(std::vector<at::Tensor> xs, std::vector<at::Tensor> ws,
@@ -195,6 +197,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scst_loss_forward", &cst::scst_loss_forward);
   m.def("cst_loss_forward", &cst::cst_loss_forward);
   m.def("scst_loss_backward", &cst::scst_loss_backward);
+  m.def("xe_loss_forward", &cst::xe_loss_forward);
+  m.def("xe_loss_backward", &cst::xe_loss_backward);
   m.def("featpool_backward", &cst::featpool_backward);
   m.def("set_stamp_base", &cst::set_stamp_base);
   m.def("stamp_buffer", &cst::stamp_buffer);

@@ -1001,10 +1001,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // dW = E'^T (alpha Hd): M = V, N = H, K = NR.  As one GEMM the 256 x 256
   // tiles put only (V / 256) x (H / 256) = 82 workgroups on the 256 CUs; a
   // split-K batch over groups of decode steps multiplies the tiles in flight,
-  // the partial products summed afterwards (the group count divides the
-  // step count; 4 groups: 3.745-3.774 vs 3.792-3.831 ms per step for one
-  // GEMM, 7 groups 3.862-3.873, profiles/r3/ab_sched.txt)
-  const int64_t dw_split = n_steps % 4 == 0 ? 4 : (n_steps % 2 == 0 ? 2 : 1);
+  // the partial products summed afterwards (4 groups: 3.745-3.774 vs
+  // 3.792-3.831 ms per step for one GEMM, 7 groups 3.862-3.873,
+  // profiles/r3/ab_sched.txt).  The groups split the rows, not the steps:
+  // tied to the step count, the 29 steps of an XE step ran one K = 37k GEMM
+  // (712 vs 461 us, profiles/r6/steps_xe3.txt)
+  const int64_t dw_split = NR % 4 == 0 ? 4 : (NR % 2 == 0 ? 2 : 1);
   // CSTCAP_DW_WGRAD=1: dW_logit AND the bias column sums in one hand-written
   // split-K MFMA kernel instead (kernels/wgrad.hip: M = V with a ragged last
   // tile, the sums from the E' tiles already in LDS): one pass over the exp
@@ -1391,14 +1393,24 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       c10::hip::HIPStreamGuard guard(side2);
       at::Tensor dvg_u = dvg.index_select(1, vg_bwd[0]);  // PyTorch gate order
       const int64_t Fv = vg_bwd[4].size(1) - E;
-      at::Tensor dfc = at::mm(dvg_u, vg_bwd[4].narrow(1, E, Fv));
+      // dfc = dvg W_iv and dW_iv = dvg^T fc (into the slot's column range):
+      // bf16 operands (W_iv's bf16 copy: one 4H x Fv conversion pass), fp32
+      // accumulation and output, the measured hipBLASLt choices.  As fp32
+      // at::mm, dfc ran as an MT32x16 fp32 kernel: 79 us alone and 380-575 us
+      // next to the dW_logit GEMM after the persistent loop
+      // (profiles/r6/steps_xe*.txt)
+      at::Tensor dvg16 = dvg_u.to(at::kBFloat16);
+      at::Tensor dfc = at::empty({dvg_u.size(0), Fv}, f32);
+      at::Tensor wiv16 = vg_bwd[4].narrow(1, E, Fv).to(at::kBFloat16);
+      at::Tensor fc16 = vg_bwd[5].to(at::kBFloat16);
+      gemm_bf16_tuned(dfc, dvg16, false, wiv16, false, 24);
       at::Tensor wiv_slot = vg_bwd[2].narrow(1, E, Fv);
-      at::mm_out(wiv_slot, dvg_u.t(), vg_bwd[5]);
+      gemm_bf16_tuned(wiv_slot, dvg16, true, fc16, false, 24);
       std::vector<at::Tensor> outs(vg_bwd.begin() + 6, vg_bwd.begin() + 6 + 2 * vg_nf);
       std::vector<at::Tensor> xs(vg_bwd.begin() + 6 + 2 * vg_nf, vg_bwd.begin() + 6 + 3 * vg_nf);
       std::vector<at::Tensor> wsv(vg_bwd.begin() + 6 + 3 * vg_nf, vg_bwd.begin() + 6 + 4 * vg_nf);
       (void)featpool_backward(dfc, vg_bwd[5], xs, wsv, vg_p, outs);
-      vg_keep = {dvg_u, dfc};
+      vg_keep = {dvg_u, dfc, dvg16, wiv16, fc16};
     }
     (void)hipEventRecord(aux.ev[5], side2.stream());
   }
@@ -1717,6 +1729,39 @@ at::Tensor scst_loss_backward(at::Tensor seq, at::Tensor reward, at::Tensor out,
   launch_scst_loss_bwd(seq.data_ptr<int64_t>(), reward.data_ptr<float>(), out.data_ptr<float>(),
                        dloss.data_ptr<float>(), (int)R, (int)T, dlp.data_ptr<float>(),
                        cur_stream());
+  return dlp;
+}
+
+// XE loss (csrc/kernels/loss.hip): labels (R, L) int64 -- the full label
+// rows the loader's masks come from --, lp (R, T) fp32 gathered GT log-probs
+// of columns off .. off + T - 1 -> {loss (0-dim), out = [loss, sum mask], cnt
+// (R) counted positions per row}
+std::vector<at::Tensor> xe_loss_forward(at::Tensor labels, at::Tensor lp, int64_t off) {
+  check_cuda(labels, "xe_loss labels");
+  check_cuda(lp, "xe_loss lp");
+  const int64_t R = labels.size(0), L = labels.size(1), T = lp.size(1);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && lp.scalar_type() == at::kFloat &&
+                  labels.dim() == 2 && lp.dim() == 2 && lp.size(0) == R && off >= 0 &&
+                  off + T <= L,
+              "xe_loss: labels (R, L) int64, lp (R, T) fp32 with off + T <= L");
+  auto f32 = lp.options();
+  at::Tensor out = at::empty({2}, f32), cnt = at::empty({R}, f32), loss = at::empty({}, f32);
+  at::Tensor ws = at::zeros({scst_loss_ws_ints((int)R)}, f32.dtype(at::kInt));
+  launch_xe_loss_fwd(labels.data_ptr<int64_t>(), (int)L, (int)off, lp.data_ptr<float>(), (int)R,
+                     (int)T, cnt.data_ptr<float>(), out.data_ptr<float>(), loss.data_ptr<float>(),
+                     ws.data_ptr<int>(), cur_stream());
+  return {loss, out, cnt};
+}
+
+at::Tensor xe_loss_backward(at::Tensor cnt, at::Tensor out, at::Tensor dloss, int64_t T) {
+  for (auto* t : {&cnt, &out, &dloss}) check_cuda(*t, "xe_loss operand");
+  TORCH_CHECK(dloss.scalar_type() == at::kFloat && dloss.numel() == 1 &&
+                  cnt.scalar_type() == at::kFloat && out.numel() == 2,
+              "xe_loss_backward: fp32 cnt (R), out (2), dloss scalar");
+  const int64_t R = cnt.size(0);
+  at::Tensor dlp = at::empty({R, T}, cnt.options());
+  launch_xe_loss_bwd(cnt.data_ptr<float>(), out.data_ptr<float>(), dloss.data_ptr<float>(), (int)R,
+                     (int)T, dlp.data_ptr<float>(), cur_stream());
   return dlp;
 }
 

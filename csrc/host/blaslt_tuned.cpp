@@ -154,16 +154,18 @@ Plan& get_plan(int dev, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ld
 
 }  // namespace
 
-// out (M x N fp32, row-major, contiguous) = op(a) op(b); a, b bf16 2-D views
-// with unit column stride (row stride = the leading dimension).  ta: a is
-// used transposed (a is K x M), tb likewise (b is N x K).
+// out (M x N fp32, row-major, unit column stride; its row stride is the
+// leading dimension, e.g. a column slice of a wider matrix) = op(a) op(b); a,
+// b bf16 2-D views with unit column stride (row stride = the leading
+// dimension).  ta: a is used transposed (a is K x M), tb likewise (b is N x K).
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm_bf16_tuned: GPU tensors");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
-                  out.scalar_type() == at::kFloat && out.is_contiguous() && a.dim() == 2 &&
-                  b.dim() == 2 && out.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
-              "gemm_bf16_tuned: bf16 a, b with unit column stride, contiguous fp32 out");
+                  out.scalar_type() == at::kFloat && out.dim() == 2 && out.stride(1) == 1 &&
+                  out.stride(0) >= out.size(1) && a.dim() == 2 && b.dim() == 2 &&
+                  a.stride(1) == 1 && b.stride(1) == 1,
+              "gemm_bf16_tuned: bf16 a, b and fp32 out with unit column stride");
   const int64_t M = out.size(0), N = out.size(1);
   const int64_t K = ta ? a.size(0) : a.size(1);
   TORCH_CHECK((ta ? a.size(1) : a.size(0)) == M && (tb ? b.size(1) : b.size(0)) == K &&
@@ -171,7 +173,7 @@ void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool t
               "gemm_bf16_tuned: shapes");
   hipStream_t st = at::hip::getCurrentHIPStream().stream();
   // C^T (N x M) = op(b)^T op(a)^T, column-major: A' = b's memory, B' = a's
-  const int64_t lda = b.stride(0), ldb = a.stride(0), ldc = N;
+  const int64_t lda = b.stride(0), ldb = a.stride(0), ldc = out.stride(0);
   Plan& p = get_plan((int)out.device().index(), N, M, K, lda, ldb, ldc, tb, ta, b.data_ptr(),
                      a.data_ptr(), out.data_ptr(), st, (int)n_cand);
   const float one = 1.f, zero = 0.f;
@@ -185,7 +187,8 @@ void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool t
 std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at::Tensor b,
                                        bool tb) {
   const int64_t M = out.size(0), N = out.size(1), K = ta ? a.size(0) : a.size(1);
-  Key key{(int)out.device().index(), N, M, K, b.stride(0), a.stride(0), N, (int)tb, (int)ta};
+  Key key{(int)out.device().index(), N, M, K, b.stride(0), a.stride(0), out.stride(0), (int)tb,
+          (int)ta};
   std::vector<double> v;
   auto it = state().plans.find(key);
   if (it == state().plans.end()) return v;

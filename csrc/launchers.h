@@ -381,6 +381,13 @@ void launch_scst_loss_fwd(const int64_t* seq, const float* lp, int R, int T, con
                           int* ws, CstBase cb, hipStream_t stream);
 void launch_scst_loss_bwd(const int64_t* seq, const float* reward, const float* out,
                           const float* dloss, int R, int T, float* dlp, hipStream_t stream);
+// XE criterion with the loader's caption masks computed from the label rows
+// (R x L int64): cnt (R) = counted log-probs per row, out = {loss, sum mask};
+// ws as for the SCST loss
+void launch_xe_loss_fwd(const int64_t* labels, int L, int off, const float* lp, int R, int T,
+                        float* cnt, float* out, float* loss, int* ws, hipStream_t stream);
+void launch_xe_loss_bwd(const float* cnt, const float* out, const float* dloss, int R, int T,
+                        float* dlp, hipStream_t stream);
 
 // embed_grad.hip
 // per-token sums S[v] (bf16, V x C) of the bf16 rows x[srow[i]] (row stride ld)

@@ -36,6 +36,30 @@ class _SCSTLossFn(torch.autograd.Function):
         return None, dlp, None, None, None
 
 
+class _XELossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, labels, lp, off):
+        loss, out, cnt = _ext.ops().xe_loss_forward(labels, lp.detach().float().contiguous(), off)
+        ctx.save_for_backward(cnt, out)
+        ctx.T = lp.size(1)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        cnt, out = ctx.saved_tensors
+        dlp = _ext.ops().xe_loss_backward(cnt, out, dloss.float().reshape(1).contiguous(), ctx.T)
+        return None, dlp, None
+
+
+def xe_loss(labels, logprobs, off=1):
+    """CrossEntropyCriterion(logprobs, labels[:, off:], masks[:, off:]) with
+    the loader's masks (caption plus EOS: positions < nonzeros + 1,
+    ``data/dataset.py`` gather) computed from the full label rows in the same
+    launch: ``logprobs`` (R, T) are the gathered GT log-probs of label columns
+    off .. off + T - 1."""
+    return _XELossFn.apply(labels.contiguous(), logprobs, int(off))
+
+
 def scst_loss(seq, logprobs, sample_scores, greedy_scores):
     """(loss, reward (R,), m, b): ``greedy_scores`` per row (R,) or per
     video (R / rows-per-video,)."""

@@ -145,6 +145,7 @@ class Trainer:
         # XE steps: X = E W after the teacher-forced forward too (else the
         # backward computes it in reverse-order chunks under the loop)
         self.xe_x_after_forward = os.environ.get('CSTCAP_XE_XAFTER', '1') == '1'
+        self._x_after_loss = False  # (xe_loss: X is launched after the loss)
         # PyTorch decoder path at --precision bf16: torch autocast (bf16 GEMMs /
         # LSTM, fp32 softmax), the same-precision baseline of the fused engine
         self.autocast_bf16 = (engine is None and self.device.type == 'cuda'
@@ -292,11 +293,21 @@ class Trainer:
     def xe_loss(self, data):
         if self.engine is not None:
             lp = self.engine.teacher_forced(self.model, data['feats'], data['labels'])
+            self.timer.mark('rollout')
+            if self.device.type == 'cuda':
+                # the masked cross-entropy with the loader's caption masks in
+                # one launch (ops/scst_loss.py xe_loss); the vocab head's X =
+                # E W follows the loss and its NaN-guard flag
+                # (_forward_backward): the X GEMM holds every CU, so small
+                # launches queued behind it waited for it (the masks' row
+                # count: 388 us "long" reduction, profiles/r6/steps_xe.txt)
+                from ..ops.scst_loss import xe_loss
+                self._x_after_loss = True
+                return xe_loss(data['labels'], lp, 1), {}
             # the vocab head's X = E W right after the teacher-forced forward,
             # on the engine's stream (as after an RL rollout): the backward's
             # reverse loop then starts on X instead of on its first chunk
             self.engine.launch_x()
-            self.timer.mark('rollout')
             return self.xe_criterion(lp, data['labels'][:, 1:], data['masks'][:, 1:]), {}
         pred = self.model(data['feats'], data['labels'])[0]
         self.timer.mark('rollout')
@@ -352,6 +363,9 @@ class Trainer:
             skip = ~torch.isfinite(loss.detach())
             if self.ctx.enabled and not self.bucket.sharded:  # every rank must skip
                 self.bucket.set_flag(skip)  # together: the flag rides the all-reduce
+        if self._x_after_loss:
+            self._x_after_loss = False
+            self.engine.launch_x()
         stamps.base('bwd')
         loss.backward()
         stamps.base(None)

@@ -500,6 +500,34 @@ def test_fused_scst_loss_matches_torch(per_video):
     torch.testing.assert_close(lp.grad, lp2.grad, rtol=1e-5, atol=1e-8)
 
 
+@pytest.mark.parametrize('tshort', [1, 2])
+def test_fused_xe_loss_matches_torch(tshort):
+    """csrc/kernels/loss.hip XE mode vs the loader's masks (data/dataset.py
+    gather: positions < nonzeros + 1) + CrossEntropyCriterion: loss and the
+    gradient w.r.t. the gathered log-probs; ragged captions, an empty one,
+    a full-length one, and log-prob rows shorter than the label rows."""
+    from cst_captioning_amd.models import CrossEntropyCriterion
+    from cst_captioning_amd.ops.scst_loss import xe_loss
+    torch.manual_seed(0)
+    R, L = 1283, 32
+    lens = torch.randint(0, L - 1, (R,), device=DEV)
+    lens[0], lens[1] = 0, L - 2
+    pos = torch.arange(L, device=DEV)[None, :]
+    labels = torch.where((pos >= 1) & (pos <= lens[:, None]),
+                         torch.randint(1, 500, (R, L), device=DEV), torch.zeros_like(pos))
+    n = (labels != 0).sum(1, keepdim=True) + 1
+    masks = (pos < n).float()
+    T = L - tshort
+    lp = (-torch.rand(R, T, device=DEV) * 5).requires_grad_(True)
+    loss = xe_loss(labels, lp, 1)
+    lp2 = lp.detach().clone().requires_grad_(True)
+    ref = CrossEntropyCriterion()(lp2, labels[:, 1:], masks[:, 1:])
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-6)
+    (3.0 * loss).backward()
+    (3.0 * ref).backward()
+    torch.testing.assert_close(lp.grad, lp2.grad, rtol=1e-5, atol=1e-8)
+
+
 def test_exp_store_backward_matches_dense_path():
     """The training backward (exp store, one-hot terms folded into E, no dS
     pass: csrc/kernels/vocab_grad.hip) against the dense-dS backward of the
