@@ -325,7 +325,8 @@ def _blaslt_choices(engine):
     from cst_captioning_amd import _ext
     try:
         return [{'m': int(c[0]), 'n': int(c[1]), 'k': int(c[2]), 'candidate': int(c[3]),
-                 'us': round(c[4], 1)} for c in _ext.ops().gemm_tuned_choices()]
+                 'us': round(c[4], 1), 'batch': int(c[5])}
+                for c in _ext.ops().gemm_tuned_choices()]
     except Exception:
         return None
 

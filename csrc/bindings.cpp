@@ -28,6 +28,8 @@ int64_t device_errors(int64_t dev_index);
 void reset_device_errors(int64_t dev_index);
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand);
+void gemm_bf16_tuned_batched(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
+                             int64_t n_cand);
 std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at::Tensor b,
                                        bool tb);
 std::vector<std::vector<double>> gemm_tuned_choices();
@@ -44,7 +46,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          std::vector<at::Tensor> up, at::Tensor blog,
                                          at::Tensor fix_total, int64_t vgate_div,
                                          at::Tensor xw, std::vector<at::Tensor> vg_bwd,
-                                         int64_t vg_nf, double vg_p);
+                                         int64_t vg_nf, double vg_p, int64_t x_wait);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,
@@ -156,7 +158,14 @@ static at::Tensor cider_score_cpu(at::Tensor hyps, at::Tensor hyp_video,
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "cst_captioning_amd native extension: gfx950 HIP kernels + C++ decoder executor";
   m.def("decoder_forward", &cst::decoder_forward);
-  m.def("decoder_backward", &cst::decoder_backward);
+  m.def("decoder_backward", &cst::decoder_backward, py::arg("wx"), py::arg("wlog"), py::arg("emb"),
+        py::arg("lse"), py::arg("logits16"), py::arg("hdrop_all"), py::arg("gates_all"),
+        py::arg("c_all"), py::arg("h_all"), py::arg("seq"), py::arg("labels"), py::arg("toks"),
+        py::arg("dg_sel"), py::arg("dg_xe"), py::arg("drop_p"), py::arg("rng"),
+        py::arg("out_wlog"), py::arg("out_blog"), py::arg("comm_stream"), py::arg("att"),
+        py::arg("out_emb"), py::arg("ds_bias"), py::arg("cell"), py::arg("state0"), py::arg("up"),
+        py::arg("blog"), py::arg("fix_total"), py::arg("vgate_div"), py::arg("xw"),
+        py::arg("vg_bwd"), py::arg("vg_nf"), py::arg("vg_p"), py::arg("x_wait") = 0);
   m.def("cider_build_tables", &cst::cider_build_tables);
   m.def("cider_score", &cst::cider_score);
   m.def("cider_score_cpu", &cst::cider_score_cpu);
@@ -172,6 +181,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_step_test", &cst::decode_step_test);
   m.def("gemm_bf16_tuned", &cst::gemm_bf16_tuned, py::arg("out"), py::arg("a"), py::arg("ta"),
         py::arg("b"), py::arg("tb"), py::arg("n_cand") = 24);
+  m.def("gemm_bf16_tuned_batched", &cst::gemm_bf16_tuned_batched, py::arg("out"), py::arg("a"),
+        py::arg("ta"), py::arg("b"), py::arg("tb"), py::arg("n_cand") = 24);
   m.def("gemm_tuned_timings", &cst::gemm_tuned_timings);
   m.def("gemm_tuned_choices", &cst::gemm_tuned_choices);
   m.def("set_grad_events", &cst::set_grad_events);

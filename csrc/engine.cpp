@@ -55,6 +55,8 @@ void stamp_now(int64_t slot) { launch_stamp((int)slot, cur_stream()); }
 
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand);
+void gemm_bf16_tuned_batched(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
+                             int64_t n_cand);
 
 // X = E W of a training forward's exp store (n, R, ldl) bf16 -> out (n, R, H)
 // fp32, on the current stream (engine.launch_x; the same GEMM as the
@@ -128,7 +130,7 @@ static DeviceAux& device_aux(int dev_index) {
   if (it == aux.end()) {
     auto* a = new DeviceAux{{}, {c10::hip::getStreamFromPool(false, dev_index),
                                  c10::hip::getStreamFromPool(false, dev_index)}};
-    a->ev.resize(6 + MAX_DHD_CHUNKS);
+    a->ev.resize(7 + MAX_DHD_CHUNKS);  // (the last: decoder_backward's pre-X point)
     for (auto& e : a->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     for (auto& e : a->grad_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     for (auto& e : a->fwd_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -828,7 +830,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          std::vector<at::Tensor> up, at::Tensor blog,
                                          at::Tensor fix_total, int64_t vgate_div,
                                          at::Tensor xw, std::vector<at::Tensor> vg_bwd,
-                                         int64_t vg_nf, double vg_p) {
+                                         int64_t vg_nf, double vg_p, int64_t x_wait) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -962,6 +964,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // gradient (columns H, H + 1 of the product), instead of a separate
   // column-sum pass over the 753 MB exp store.  CSTCAP_DW_AUG=0: the separate
   // column sums (vgrad_colsum).
+  static const bool dw_tuned_env = [] {
+    const char* e = getenv("CSTCAP_DW_TUNED");
+    return e != nullptr && e[0] == '1';
+  }();
   static const bool dw_aug_env = [] {
     const char* e = getenv("CSTCAP_DW_AUG");
     return e == nullptr || atoi(e) != 0;
@@ -1021,8 +1027,17 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       // over all rows with the measured hipBLASLt choice: 3.439-3.451 vs
       // 3.330-3.343 ms per step, profiles/r6/README_r6.md)
       const int64_t kr = NR / dw_split;
-      at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
-      at::Tensor p = at::bmm(a, hs.view({dw_split, kr, ldhs}), at::kFloat);  // (split, V, H + 16)
+      at::Tensor p;  // (split, V, H + 16)
+      if (dw_tuned_env) {
+        // the batch with the measured hipBLASLt choice (gemm_bf16_tuned_batched)
+        p = at::empty({dw_split, V, ldhs}, f32);
+        gemm_bf16_tuned_batched(
+            p, buf.view({NR, ldl}).as_strided({dw_split, kr, V}, {kr * ldl, ldl, 1}), true,
+            hs.view({dw_split, kr, ldhs}), false, 24);
+      } else {
+        at::Tensor a = buf.view({NR, ldl}).as_strided({dw_split, V, kr}, {kr * ldl, 1, ldl});
+        p = at::bmm(a, hs.view({dw_split, kr, ldhs}), at::kFloat);
+      }
       at::sum_out(dWlog, p.narrow(2, 0, H), 0);
       at::sum_out(dblog, p.narrow(2, H, 2), at::IntArrayRef({0, 2}));
       dw_fused = true;
@@ -1058,12 +1073,12 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // alpha, one-hot terms folded into E (dS = diag(alpha) E'); exp-store range
   // guard: rows whose LSE jumped by > 60 since the previous step are listed
   // and recomputed exactly (vocab_grad.hip vgrad_fix)
+  // (only the row counter fix[0] needs zeroing: the list entries are written
+  // by vgrad_onehot before vgrad_fix reads them)
+  at::Tensor fix = !ds_ready && blog.defined() && blog.numel() == V ? at::empty({1 + NR}, i32)
+                                                                     : at::Tensor();
   auto onehot_pass = [&](hipStream_t s) {
-    const bool guard = blog.defined() && blog.numel() == V;
-    // (only the row counter fix[0] needs zeroing: the list entries are
-    // written by vgrad_onehot before vgrad_fix reads them)
-    at::Tensor fix = guard ? at::empty({1 + NR}, i32) : at::Tensor();
-    if (guard) (void)hipMemsetAsync(fix.data_ptr(), 0, sizeof(int), s);
+    const bool guard = fix.defined();
     VGradRows va{(int)R, (int)n_steps, (int)T_sel, (int)H, (int)V, lse.data_ptr<float>(),
                  has_sel ? seq.data_ptr<int64_t>() : nullptr,
                  has_sel ? dg_sel.data_ptr<float>() : nullptr,
@@ -1099,6 +1114,41 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     db_sums(side.stream());
     dw_done();
   };
+  // X-independent preparation of the loop first, then the wait for X
+  // (x_wait: the event engine.launch_x recorded after X = E W): the counter
+  // resets, the dc zeros, the W_hh^T copy and the token sort run under the X
+  // GEMM instead of between it and the loop (they sat on the critical path
+  // after X, profiles/r6/steps_scst*.txt)
+  if (fix.defined()) (void)hipMemsetAsync(fix.data_ptr(), 0, sizeof(int), st);
+  at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
+  at::Tensor dc = at::zeros({R, H}, f32);
+  // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel; with
+  // attention [W_hh^T | W_q^T] (H, 4H + A), so the step GEMM over
+  // [dG_{t+1} | dq_{t+1}] also adds dq_{t+1} W_q (q_{t+1} = W_q h_t) into dh_t
+  at::Tensor whhT = has_att ? at::cat({wx.narrow(1, E, H).t(), a_wq.t()}, 1).contiguous()
+                            : wx.narrow(1, E, H).t().contiguous();
+  // token-only operands of the embedding / input-weight gradients: rows
+  // grouped by input token (counting sort), per-token sum scratch
+  const bool emb_direct = out_emb.defined() && out_emb.numel() > 0;
+  if (emb_direct)
+    TORCH_CHECK(out_emb.is_contiguous() && out_emb.scalar_type() == at::kFloat &&
+                    out_emb.size(0) == V && out_emb.size(1) == E,
+                "out_emb must be a contiguous fp32 (V, E) tensor");
+  at::Tensor d_emb = emb_direct ? out_emb : at::empty({V, E}, f32);
+  at::Tensor sort_ws = at::empty({2 * V + 1}, i32);
+  at::Tensor stok = at::empty({NR}, i32), srow = at::empty({NR}, i32);
+  at::Tensor S_tok = at::empty({V, H4}, wx.options());  // per-token gate-gradient sums
+  at::Tensor S32 = at::empty({V, H4}, f32);  // rows of long groups only (token_long_zero)
+  // on the second side stream, off the critical path (needed after the loop)
+  hipEvent_t ev_pre = aux.ev[6 + MAX_DHD_CHUNKS];
+  (void)hipEventRecord(ev_pre, st);
+  (void)hipStreamWaitEvent(side2.stream(), ev_pre, 0);
+  launch_token_sort(toks.data_ptr<int64_t>(), (int)NR, (int)V, sort_ws.data_ptr<int>(),
+                    stok.data_ptr<int>(), srow.data_ptr<int>(), side2.stream());
+  launch_token_long_zero(sort_ws.data_ptr<int>(), (int)V, (int)H4, S32.data_ptr<float>(),
+                         side2.stream());
+  (void)hipEventRecord(ev_tok, side2.stream());
+  if (x_wait != 0) (void)hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(x_wait), 0);
   stamp(STAMP_BWD_BEGIN, st);
   // Forward X: the loop's first operands are the row weights of this pass and
   // X itself, so the pass runs on the main stream -- no hop to the side stream
@@ -1130,37 +1180,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     }
     if (!persistent) side_dw();
   }
-  // token-only operands of the embedding / input-weight gradients: rows
-  // grouped by input token (counting sort), per-token sum scratch
-  const bool emb_direct = out_emb.defined() && out_emb.numel() > 0;
-  if (emb_direct)
-    TORCH_CHECK(out_emb.is_contiguous() && out_emb.scalar_type() == at::kFloat &&
-                    out_emb.size(0) == V && out_emb.size(1) == E,
-                "out_emb must be a contiguous fp32 (V, E) tensor");
-  at::Tensor d_emb = emb_direct ? out_emb : at::empty({V, E}, f32);
-  at::Tensor sort_ws = at::empty({2 * V + 1}, i32);
-  at::Tensor stok = at::empty({NR}, i32), srow = at::empty({NR}, i32);
-  at::Tensor S_tok = at::empty({V, H4}, wx.options());  // per-token gate-gradient sums
-  at::Tensor S32 = at::empty({V, H4}, f32);  // rows of long groups only (token_long_zero)
-  // on the second side stream, off the critical path (needed after the loop)
-  (void)hipStreamWaitEvent(side2.stream(), ev_ready, 0);
-  launch_token_sort(toks.data_ptr<int64_t>(), (int)NR, (int)V, sort_ws.data_ptr<int>(),
-                    stok.data_ptr<int>(), srow.data_ptr<int>(), side2.stream());
-  launch_token_long_zero(sort_ws.data_ptr<int>(), (int)V, (int)H4, S32.data_ptr<float>(),
-                         side2.stream());
-  (void)hipEventRecord(ev_tok, side2.stream());
-
   // 4. reverse LSTM loop on the main stream
-  at::Tensor dG_all = at::empty({n_steps, R, KD}, wx.options());
-  at::Tensor dc = at::zeros({R, H}, f32);
-  // (these loop operands filled on the second side stream concurrently with
+  // (the loop operands filled on the second side stream concurrently with
   // the one-hot pass measured slower: att8 4.487-4.516 vs 4.379-4.417 ms,
   // headline 3.424-3.514 vs 3.337-3.339, profiles/r5/tail/ab_prep*.json)
-  // W_hh^T (H, 4H): K-contiguous B operand of the fused step kernel; with
-  // attention [W_hh^T | W_q^T] (H, 4H + A), so the step GEMM over
-  // [dG_{t+1} | dq_{t+1}] also adds dq_{t+1} W_q (q_{t+1} = W_q h_t) into dh_t
-  at::Tensor whhT = has_att ? at::cat({wx.narrow(1, E, H).t(), a_wq.t()}, 1).contiguous()
-                            : wx.narrow(1, E, H).t().contiguous();
   at::Tensor dpre_part, dwa_part, dba_part;
   // MFMA attention path backward: dalpha partials from the step kernel's
   // epilogue (lstm.hip) + att_bwd_mfma (attention.hip); else att_bwd

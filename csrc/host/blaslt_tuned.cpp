@@ -42,8 +42,14 @@ struct Plan {
   std::vector<std::pair<int, float>> timings;  // (candidate, us)
 };
 
-// key: device, m, n, k, lda, ldb, ldc, transA, transB (column-major terms)
-using Key = std::tuple<int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int>;
+// key: device, m, n, k, lda, ldb, ldc, transA, transB (column-major terms),
+// batch count, batch strides of A, B, C (1, 0, 0, 0: one GEMM)
+using Key = std::tuple<int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int64_t,
+                       int64_t, int64_t, int64_t>;
+
+struct Batch {
+  int64_t count = 1, sa = 0, sb = 0, sc = 0;
+};
 
 struct State {
   hipblasLtHandle_t handle = nullptr;
@@ -67,10 +73,10 @@ bool capturing(hipStream_t st) {
 // column-major: D (m x n, ldc) = op(A) (m x k) op(B) (k x n); bf16 A/B, fp32 C/D
 Plan& get_plan(int dev, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
                bool ta, bool tb, const void* A, const void* B, void* C, hipStream_t st,
-               int n_cand) {
+               int n_cand, Batch bt = Batch{}) {
   State& S = state();
   if (S.handle == nullptr) BLT_CHECK(hipblasLtCreate(&S.handle));
-  Key key{dev, m, n, k, lda, ldb, ldc, (int)ta, (int)tb};
+  Key key{dev, m, n, k, lda, ldb, ldc, (int)ta, (int)tb, bt.count, bt.sa, bt.sb, bt.sc};
   auto it = S.plans.find(key);
   if (it != S.plans.end() && it->second.have_algo) return it->second;
   Plan& p = S.plans[key];
@@ -82,6 +88,17 @@ Plan& get_plan(int dev, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ld
     BLT_CHECK(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, ta ? k : m, ta ? m : k, lda));
     BLT_CHECK(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, tb ? n : k, tb ? k : n, ldb));
     BLT_CHECK(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, m, n, ldc));
+    if (bt.count > 1) {
+      const int32_t cnt = (int32_t)bt.count;
+      const int64_t st3[3] = {bt.sa, bt.sb, bt.sc};
+      hipblasLtMatrixLayout_t ls[3] = {p.la, p.lb, p.lc};
+      for (int i = 0; i < 3; ++i) {
+        BLT_CHECK(hipblasLtMatrixLayoutSetAttribute(ls[i], HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &cnt,
+                                                    sizeof(cnt)));
+        BLT_CHECK(hipblasLtMatrixLayoutSetAttribute(
+            ls[i], HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &st3[i], sizeof(st3[i])));
+      }
+    }
   }
   hipblasLtMatmulPreference_t pref;
   BLT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
@@ -183,12 +200,42 @@ void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool t
                             ws.data_ptr(), p.ws, st));
 }
 
+// Strided batch of the same: out (B, M, N) fp32, a (B, M, K) or with ta
+// (B, K, M), b (B, K, N) or with tb (B, N, K); every operand's last dimension
+// has unit stride, the middle one is the leading dimension, the first the
+// batch stride.
+void gemm_bf16_tuned_batched(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
+                             int64_t n_cand) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm_bf16_tuned_batched: GPU tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+                  out.scalar_type() == at::kFloat && out.dim() == 3 && a.dim() == 3 &&
+                  b.dim() == 3 && out.stride(2) == 1 && a.stride(2) == 1 && b.stride(2) == 1 &&
+                  out.stride(1) >= out.size(2) && a.size(0) == out.size(0) &&
+                  b.size(0) == out.size(0),
+              "gemm_bf16_tuned_batched: (B, ., .) bf16 a, b and fp32 out, unit last stride");
+  const int64_t M = out.size(1), N = out.size(2);
+  const int64_t K = ta ? a.size(1) : a.size(2);
+  TORCH_CHECK((ta ? a.size(2) : a.size(1)) == M && (tb ? b.size(2) : b.size(1)) == K &&
+                  (tb ? b.size(1) : b.size(2)) == N,
+              "gemm_bf16_tuned_batched: shapes");
+  hipStream_t st = at::hip::getCurrentHIPStream().stream();
+  const int64_t lda = b.stride(1), ldb = a.stride(1), ldc = out.stride(1);
+  Batch bt{out.size(0), b.stride(0), a.stride(0), out.stride(0)};
+  Plan& p = get_plan((int)out.device().index(), N, M, K, lda, ldb, ldc, tb, ta, b.data_ptr(),
+                     a.data_ptr(), out.data_ptr(), st, (int)n_cand, bt);
+  const float one = 1.f, zero = 0.f;
+  auto& ws = state().workspace[(int)out.device().index()];
+  BLT_CHECK(hipblasLtMatmul(state().handle, p.desc, &one, b.data_ptr(), p.la, a.data_ptr(), p.lb,
+                            &zero, out.data_ptr(), p.lc, out.data_ptr(), p.lc, &p.algo,
+                            ws.data_ptr(), p.ws, st));
+}
+
 // the timings of the candidates measured for the last plan of a shape (us)
 std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at::Tensor b,
                                        bool tb) {
   const int64_t M = out.size(0), N = out.size(1), K = ta ? a.size(0) : a.size(1);
   Key key{(int)out.device().index(), N, M, K, b.stride(0), a.stride(0), out.stride(0), (int)tb,
-          (int)ta};
+          (int)ta, 1, 0, 0, 0};
   std::vector<double> v;
   auto it = state().plans.find(key);
   if (it == state().plans.end()) return v;
@@ -196,7 +243,8 @@ std::vector<double> gemm_tuned_timings(at::Tensor out, at::Tensor a, bool ta, at
   return v;
 }
 
-// every tuned plan: {m, n, k (column-major terms), chosen candidate, its us}
+// every tuned plan: {m, n, k (column-major terms), chosen candidate, its us,
+// batch count}
 std::vector<std::vector<double>> gemm_tuned_choices() {
   std::vector<std::vector<double>> v;
   for (auto& kv : state().plans) {
@@ -206,7 +254,8 @@ std::vector<std::vector<double>> gemm_tuned_choices() {
     for (auto& t : p.timings)
       if (t.first == p.chosen) us = t.second;
     v.push_back({(double)std::get<1>(kv.first), (double)std::get<2>(kv.first),
-                 (double)std::get<3>(kv.first), (double)p.chosen, us});
+                 (double)std::get<3>(kv.first), (double)p.chosen, us,
+                 (double)std::get<9>(kv.first)});
   }
   return v;
 }

@@ -553,6 +553,8 @@ __global__ __launch_bounds__(LP_THREADS, 1) void lstm_bwd_ksplit_kernel(BwdLoopA
 // dl = scale * dh + a W[ys] + b W[yx] in place, one wavefront per row (the
 // loop reads the folded rows; lstm_bwd_loop_fold)
 __global__ __launch_bounds__(256) void lstm_bwd_fold_kernel(BwdLoopArgs a, int64_t NR) {
+  if (blockIdx.x == 0)  // the loop's team counters (the loop launch follows on this stream)
+    for (int i = threadIdx.x; i < 8 * a.nrb * LP_CNT_STRIDE; i += 256) a.cnt[i] = 0;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= NR) return;
   const int lane = threadIdx.x & 63, H = a.H;
@@ -635,14 +637,17 @@ void launch_lstm_bwd_loop(BwdLoopArgs a, hipStream_t stream) {
   a.rows_per_group = g.rows_per_group;
   a.rows_per_block = g.rows_per_block;
   if (a.scale != nullptr || a.oh_a != nullptr) {
-    // the row scales and one-hot rows folded into dh (in place) first
+    // the row scales and one-hot rows folded into dh (in place) first; the
+    // fold also zeroes the team counters (one memset node less between X and
+    // the loop)
     const int64_t NR = (int64_t)a.T * a.R;
     hipLaunchKernelGGL(lstm_bwd_fold_kernel, dim3((unsigned)((NR + 3) / 4)), dim3(256), 0, stream,
                        a, NR);
     post_launch("lstm_bwd_fold_kernel", stream);
+  } else {
+    // team counters: zeroed by a memset node ahead of every launch
+    (void)hipMemsetAsync(a.cnt, 0, sizeof(int) * 8 * g.nrb * LP_CNT_STRIDE, stream);
   }
-  // team counters: zeroed by a memset node ahead of every launch
-  (void)hipMemsetAsync(a.cnt, 0, sizeof(int) * 8 * g.nrb * LP_CNT_STRIDE, stream);
 #define LP_LAUNCH(KSV, DB)                                                                      \
   {                                                                                             \
     static bool attr = false;                                                                   \
@@ -654,7 +659,7 @@ void launch_lstm_bwd_loop(BwdLoopArgs a, hipStream_t stream) {
     hipLaunchKernelGGL((lstm_bwd_loop_kernel<KSV, DB>), dim3(g.grid), dim3(LP_THREADS), LP_LDS,    \
                        stream, a);                                                              \
   }
-  if (a.form == 0) {  // K-split (default)
+  if (a.form == 0) {  // K-split (CSTCAP_BWD_LOOP=2)
     if (a.xb == nullptr) throw std::runtime_error("lstm_bwd_loop: K-split form needs the exchange slabs");
     static bool attr = false;
     if (!attr) {

@@ -961,6 +961,21 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
   if (flags & VF_TOPK) {  // beam search: per-tile top-K candidates
     if (vf_topk_k(flags) < 1 || vf_topk_k(flags) > VF_TOPK_MAXK)
       throw std::runtime_error("vocab_lstm_fwd: VF_TOPK needs 1 <= K <= 8");
+    static const int beam_bn = [] {
+      const char* e = getenv("CSTCAP_BEAM_BN");
+      return e != nullptr && atoi(e) == 128 ? 128 : 64;
+    }();
+    if (att == nullptr && beam_bn == 128) {
+      // 128-row tiles: the vocabulary matrix streamed ceil(R / 128) instead
+      // of ceil(R / 64) times per step -- measured slower at the headline
+      // beam shape (R = 320: 1.31 vs 1.09 ms per 64-video batch, 249
+      // workgroups at 2 per CU against 415 at 3, profiles/r6/README_r6.md)
+      launch_vocab_lstm_t<128, 2, 2, LGTile2, 0, true>(hd, ldh, R, H, W, bias, V, logits16, ldl,
+                                                       part, tgt, tgt_stride, flags, inv_temp, rng,
+                                                       step, h_t, whh, vgate, vdiv, pre, NQ, q_out,
+                                                       stream, eoff, nullptr);
+      return vocab_num_tiles(V);
+    }
     if (att == nullptr) {
       launch_vocab_lstm_t<64, 2, 3, LGTile2, 0, true>(hd, ldh, R, H, W, bias, V, logits16, ldl,
                                                       part, tgt, tgt_stride, flags, inv_temp, rng,

@@ -284,18 +284,19 @@ class _DecoderFn(torch.autograd.Function):
                        eng.model.core.rnn.weight_ih_l0.detach(), fc]
                       + [direct['fp_w%d' % f] for f in range(vg_nf)]
                       + [direct['fp_b%d' % f] for f in range(vg_nf)] + list(xs) + list(wsd))
-        if x_ev is not None:
-            # the operand preparation above (token rows, contiguous gradients)
-            # needs no X; it runs while the X stream still computes (3.362-3.402
-            # vs 3.400-3.418 ms per step waiting first, profiles/r5/tail/)
-            torch.cuda.current_stream(xw.device).wait_event(x_ev)
+        # the operand preparation above (token rows, contiguous gradients)
+        # needs no X; it runs while the X stream still computes (3.362-3.402
+        # vs 3.400-3.418 ms per step waiting first, profiles/r5/tail/), and so
+        # does the backward's own X-independent prologue: the native call
+        # waits for X itself (x_wait: the raw event handle)
         res = _ext.ops().decoder_backward(
             eng.wx, eng.wlog, eng.emb, lse, logits16, hdrop, gates, c_all, h_all, seq,
             labels if labels is not None else torch.empty(0, dtype=torch.long, device=lse.device),
             toks, g_sel if g_sel is not None else empty, g_xe if g_xe is not None else empty,
             ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell,
             ctx.state0, eng.upper_operands(ctx.up_saved), ctx.logit_b, eng.exp_fix_rows,
-            vdiv, xw if ctx.store_exp else empty, vg_bwd, vg_nf, float(vg_p))
+            vdiv, xw if ctx.store_exp else empty, vg_bwd, vg_nf, float(vg_p),
+            0 if x_ev is None else int(x_ev.cuda_event))
         ctx.logit_b = None
         ctx.up_saved = None
         d_up = []

@@ -294,7 +294,10 @@ class Trainer:
         if self.engine is not None:
             lp = self.engine.teacher_forced(self.model, data['feats'], data['labels'])
             self.timer.mark('rollout')
-            if self.device.type == 'cuda':
+            # (a batch whose masks were not set by hand: the loader's caption
+            # masks, derived from the labels)
+            derived = isinstance(data, LazyGather) and not dict.__contains__(data, 'masks')
+            if self.device.type == 'cuda' and derived:
                 # the masked cross-entropy with the loader's caption masks in
                 # one launch (ops/scst_loss.py xe_loss); the vocab head's X =
                 # E W follows the loss and its NaN-guard flag

@@ -654,3 +654,34 @@ def test_exp_store_lse_jump_rows_recomputed():
         assert torch.isfinite(a).all(), k
         err = (a - b).norm() / (b.norm() + 1e-12)
         assert err < 2e-2, (k, float(err))
+
+
+@pytest.mark.parametrize('batched', [False, True])
+def test_tuned_blaslt_gemm_matches_torch(batched):
+    """csrc/host/blaslt_tuned.cpp: the measured-choice hipBLASLt GEMM (bf16
+    operands, fp32 output) against the fp32 product of the same bf16 values:
+    a transposed A operand with a leading dimension wider than the row, a
+    strided output (column slice of a wider matrix), and the strided batch
+    (the dW_logit split-K groups of decoder_backward)."""
+    from cst_captioning_amd import _ext
+    ops = _ext.ops()
+    torch.manual_seed(0)
+    if not batched:
+        K, M, N = 64, 300, 200
+        a = torch.randn(K, M + 8, device=DEV).to(torch.bfloat16)[:, :M]  # (K, M), ld M + 8
+        b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+        wide = torch.full((M, N + 40), 7.0, device=DEV)
+        out = wide[:, 20:20 + N]
+        ops.gemm_bf16_tuned(out, a, True, b, False)
+        ref = a.float().t() @ b.float()
+        torch.testing.assert_close(out, ref, rtol=2e-5, atol=2e-4)
+        assert (wide[:, :20] == 7.0).all() and (wide[:, 20 + N:] == 7.0).all()
+    else:
+        B, K, M, N, ld = 4, 256, 520, 48, 536
+        rows = torch.randn(B * K, ld, device=DEV).to(torch.bfloat16)
+        a = rows.as_strided((B, K, M), (K * ld, ld, 1))
+        b = torch.randn(B, K, N, device=DEV).to(torch.bfloat16)
+        out = torch.empty(B, M, N, device=DEV)
+        ops.gemm_bf16_tuned_batched(out, a, True, b, False)
+        ref = torch.bmm(a.float().transpose(1, 2), b.float())
+        torch.testing.assert_close(out, ref, rtol=2e-5, atol=2e-4)
