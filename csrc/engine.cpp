@@ -1103,8 +1103,9 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     stamp(STAMP_BWD_ONEHOT, s);
   };
   // the vocab head's weight gradients (current stream: side)
+  bool rows_early = false;  // the scaled Hd rows already formed (persistent loop)
   auto side_dw = [&]() {
-    if (!ds_ready)
+    if (!ds_ready && !rows_early)
       launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
                         reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
                         reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream(), (int)ldhs);
@@ -1178,7 +1179,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       (void)hipEventRecord(aux.ev[6 + ci], side.stream());
       if (ci == 0) stamp(STAMP_BWD_DHD0, side.stream());
     }
-    if (!persistent) side_dw();
+    if (!persistent) {
+      side_dw();
+    } else if (!ds_ready) {
+      // the dW GEMM's scaled Hd rows need only alpha: formed now, next to the
+      // fold on the main stream, instead of between the loop and the GEMM
+      launch_vgrad_rows(alpha.data_ptr<float>(), NR, (int)H,
+                        reinterpret_cast<const uint16_t*>(hd2.data_ptr()), nullptr,
+                        reinterpret_cast<uint16_t*>(hs.data_ptr()), side.stream(), (int)ldhs);
+      rows_early = true;
+    }
   }
   // 4. reverse LSTM loop on the main stream
   // (the loop operands filled on the second side stream concurrently with

@@ -507,7 +507,15 @@ class DecoderEngine:
     def update_ptab(self):
         # input-token gate table P = emb . W_ie^T (V x 4H, packed gate order):
         # one GEMM per optimizer step instead of K=E of work in every decode step
-        self.ptab.copy_(torch.mm(self.emb, self.wx[:, :self.E].t(), out_dtype=torch.float32))
+        if self.emb.is_cuda:
+            # the measured hipBLASLt choice (host/blaslt_tuned.cpp): PyTorch's
+            # pick ran this 22 GFLOP product at 0.27 PF/s (81 us,
+            # profiles/r6/steps_xe_after_fixes.txt)
+            p32 = torch.empty(self.ptab.shape, dtype=torch.float32, device=self.emb.device)
+            _ext.ops().gemm_bf16_tuned(p32, self.emb, False, self.wx[:, :self.E], True)
+            self.ptab.copy_(p32)
+        else:
+            self.ptab.copy_(torch.mm(self.emb, self.wx[:, :self.E].t(), out_dtype=torch.float32))
         self._ptab_version = self.weights_version
 
     def prefetch_ptab(self):
