@@ -13,7 +13,7 @@ run() {
   local p=$1; shift
   rm -rf gpurun_out/$TAG/$p
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/$TAG/$p -o $p -- \
-    python bench.py --steps 2 --warmup 3 --cuda_graph $GRAPH --att8 0 --beam5 0 --cst 0 ${BENCH_ARGS} \
+    python bench.py --steps 2 --warmup 3 --cuda_graph $GRAPH --att8 0 --beam5 0 --cst 0 --xe 0 ${BENCH_ARGS} \
     > gpurun_out/$TAG/$p.log 2>&1
 }
 run p1 FETCH_SIZE || exit $?
