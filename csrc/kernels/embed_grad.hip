@@ -87,12 +87,17 @@ __global__ __launch_bounds__(256) void token_group_sum_kernel(
         }
       }
     } else {  // this chunk's part of a long group
+      // (zero partials skip their atomics: the longest group of a teacher-
+      // forced XE step is the padding token 0 after the captions end, ~25k
+      // rows whose gate gradients are all zero -- 390 chunks x 2,048 atomics
+      // on the same row serialised at the memory side)
 #pragma unroll
       for (int j = 0; j < MAXJ; ++j) {
         const int c = tid + 256 * j;
         if (c < nch)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) atomicAdd(S32 + (int64_t)v * C + 8 * c + k, acc[j][k]);
+          for (int k = 0; k < 8; ++k)
+            if (acc[j][k] != 0.f) atomicAdd(S32 + (int64_t)v * C + 8 * c + k, acc[j][k]);
       }
     }
 #pragma unroll

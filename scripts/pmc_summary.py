@@ -37,7 +37,8 @@ for p in ('p1', 'p2', 'p3', 'p4'):
     for r in rows:
         d = int(r['Dispatch_Id'])
         if lo < d <= hi:
-            short = r['Kernel_Name'].split('(')[0].replace('void ', '')[:48]
+            short = (r['Kernel_Name'].replace('(anonymous namespace)::', '')
+                     .split('(')[0].replace('void ', '')[:48])
             agg[short][r['Counter_Name']] += float(r['Counter_Value'])
 tot_r = tot_w = tot_m = 0.0
 out = []
