@@ -968,15 +968,19 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     const char* e = getenv("CSTCAP_DW_TUNED");
     return e != nullptr && e[0] == '1';
   }();
-  static const bool dw_aug_env = [] {
+  // CSTCAP_DW_AUG unset: the augmented rows with the persistent loop only
+  // (dW after the loop); with the per-step loop the dW GEMM runs UNDER the
+  // loop, where its 16 extra columns contend with the latency-bound step
+  // kernels and the column sums' 210 long workgroups leave them CU slots
+  static const int dw_aug_env = [] {
     const char* e = getenv("CSTCAP_DW_AUG");
-    return e == nullptr || atoi(e) != 0;
+    return e == nullptr || e[0] == 0 ? -1 : atoi(e);
   }();
   static const bool dw_wgrad_env = [] {
     const char* e = getenv("CSTCAP_DW_WGRAD");
     return e != nullptr && atoi(e) != 0;
   }();
-  const bool dw_aug = !ds_ready && dw_aug_env && !dw_wgrad_env;
+  const bool dw_aug = !ds_ready && !dw_wgrad_env && (dw_aug_env < 0 ? persistent : dw_aug_env != 0);
   const int64_t ldhs = dw_aug ? H + 16 : H;
   if (!ds_ready) {
     alpha = at::empty({NR}, f32);
