@@ -918,6 +918,16 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // launch per step.
   const bool persistent = g_bwd_loop != 0 && NL == 1 && !has_att && !has_s0 &&
                           lstm_bwd_loop_ok((int)R, (int)H, (int)n_steps);
+  // dW_logit after the persistent loop starts once the main stream's token
+  // sums are enqueued (1; 0: right after the loop, 2: after the d_emb GEMM):
+  // its long-running GEMM workgroups no longer hold every CU while the
+  // latency-bound post-loop chain waits for slots.  Interleaved on one box:
+  // 3.210-3.218 (1) / 3.232-3.237 (2) vs 3.292-3.295 ms (0) per headline
+  // step, XE 3.32-3.34 vs 3.39-3.40 (profiles/r6/README_r6.md)
+  static const int dw_late = [] {
+    const char* e = getenv("CSTCAP_DW_LATE");
+    return e != nullptr ? atoi(e) : 1;
+  }();
   // 1-2. vocab head on the side stream.  Exp store (training): alpha and the
   // one-hot terms folded into E, X = E' W (dHd = alpha X, scaled by the
   // loop), the alpha-scaled Hd rows for dW; kernels/vocab_grad.hip.  Dense
@@ -1293,11 +1303,22 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     stamp(STAMP_BWD_LOOP0, st);
     // the vocab head's weight gradients after the loop (every CU is the
     // loop's until it ends), concurrently with the post-loop chain below
+    // (CSTCAP_DW_LATE=1 / 2: started after the token sums / the d_emb GEMM
+    // of that chain instead)
+    if (dw_late == 0) {
+      (void)hipEventRecord(aux.ev[4], st);
+      (void)hipStreamWaitEvent(side.stream(), aux.ev[4], 0);
+      c10::hip::HIPStreamGuard guard(side);
+      side_dw();
+    }
+  }
+  auto late_dw = [&](int at) {
+    if (!persistent || dw_late != at) return;
     (void)hipEventRecord(aux.ev[4], st);
     (void)hipStreamWaitEvent(side.stream(), aux.ev[4], 0);
     c10::hip::HIPStreamGuard guard(side);
     side_dw();
-  }
+  };
   size_t next_chunk = 0;
   for (int64_t t = persistent ? -1 : n_steps - 1; t >= 0; --t) {
     if (next_chunk < dhd_chunks.size() && t == dhd_chunks[next_chunk][1] - 1)
@@ -1513,6 +1534,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                          sort_ws.data_ptr<int>(), (int)V,
                          reinterpret_cast<uint16_t*>(S_tok.data_ptr()), S32.data_ptr<float>(), st);
   stamp(STAMP_BWD_TOKSUM, st);
+  late_dw(1);
   // d_emb = S W_ie (M = V, N = E, K = 4H): the measured hipBLASLt choice
   // (host/blaslt_tuned.cpp) -- PyTorch's heuristic pick ran it at 0.17 PF/s
   // (130 us, profiles/r5/final5/steps_final5.txt).  CSTCAP_DEMB_TUNED=0: at::mm.
@@ -1526,6 +1548,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   else
     at::mm_out(d_emb, S_tok, wx.narrow(1, 0, E), at::kFloat);
   if (grad_ev && emb_direct) record_grad_event(aux.grad_ev[1], st, 1);
+  late_dw(2);
   // (dW_ie on the second side stream, concurrent with the embedding GEMM:
   // 3.355-3.361 vs 3.342-3.356 ms per step, profiles/r5/tail/ab_wie_*.json)
   // input columns dW_ie = S^T emb: M = 4H, N = E, K = V.  One GEMM puts only
