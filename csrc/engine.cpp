@@ -1010,6 +1010,10 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // profiles/r2/ab_vh_sched.txt).  Data parallelism runs them concurrently
   // with the loop, so the vocab head's all-reduce hides under it.
   const bool early_comm = early && comm_stream != 0;
+  // (data parallelism: dW_logit right after the persistent loop, so the vocab
+  // head's all-reduce starts ~270 us before the backward ends and hides under
+  // the post-loop chain -- test_gpu_dist.py; late, it would start at the end)
+  const int dw_late_at = early_comm || (g_grad_events_on && early) ? 0 : dw_late;
   // DP overlap (set_grad_events): vocab head / embedding gradients final events
   const bool grad_ev = g_grad_events_on && early;
   // dW_logit and the bias column sums run on the side stream under the
@@ -1305,7 +1309,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     // loop's until it ends), concurrently with the post-loop chain below
     // (CSTCAP_DW_LATE=1 / 2: started after the token sums / the d_emb GEMM
     // of that chain instead)
-    if (dw_late == 0) {
+    if (dw_late_at == 0) {
       (void)hipEventRecord(aux.ev[4], st);
       (void)hipStreamWaitEvent(side.stream(), aux.ev[4], 0);
       c10::hip::HIPStreamGuard guard(side);
@@ -1313,7 +1317,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     }
   }
   auto late_dw = [&](int at) {
-    if (!persistent || dw_late != at) return;
+    if (!persistent || dw_late_at != at) return;
     (void)hipEventRecord(aux.ev[4], st);
     (void)hipStreamWaitEvent(side.stream(), aux.ev[4], 0);
     c10::hip::HIPStreamGuard guard(side);
