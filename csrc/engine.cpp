@@ -1434,7 +1434,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   const bool vg_direct = !has_att && !vg_bwd.empty();
   if (vg_direct)
     TORCH_CHECK(vg_nf >= 1 && (int64_t)vg_bwd.size() == 6 + 4 * vg_nf && NL == 1 && !has_s0,
-                "vg_bwd = {dst_ie, dst_hh, W_ih slot, W_hh slot, W_ih, fc, FeatPool slots, "
+                "vg_bwd = {dst_ie, dst_hh, W_ih slot, W_hh slot, packed W_iv shadow, fc, FeatPool slots, "
                 "inputs, weights}");
   std::vector<at::Tensor> vg_keep;  // (side-stream temporaries, released after the join)
   if (!has_att) {
@@ -1453,26 +1453,30 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       // _FeatPoolVgateFn does this after the call otherwise): dfc = dvg W_iv,
       // dW_iv = dvg^T fc into W_ih's slot, FeatPool gradients into theirs
       c10::hip::HIPStreamGuard guard(side2);
-      at::Tensor dvg_u = dvg.index_select(1, vg_bwd[0]);  // PyTorch gate order
-      const int64_t Fv = vg_bwd[4].size(1) - E;
-      // dfc = dvg W_iv and dW_iv = dvg^T fc (into the slot's column range):
-      // bf16 operands (W_iv's bf16 copy: one 4H x Fv conversion pass), fp32
-      // accumulation and output, the measured hipBLASLt choices.  As fp32
-      // at::mm, dfc ran as an MT32x16 fp32 kernel: 79 us alone and 380-575 us
-      // next to the dW_logit GEMM after the persistent loop
-      // (profiles/r6/steps_xe*.txt)
-      at::Tensor dvg16 = dvg_u.to(at::kBFloat16);
-      at::Tensor dfc = at::empty({dvg_u.size(0), Fv}, f32);
-      at::Tensor wiv16 = vg_bwd[4].narrow(1, E, Fv).to(at::kBFloat16);
+      // dfc = dvg W_iv (packed gate order on both sides: vg_bwd[4] is the
+      // engine's packed bf16 W_iv shadow, zero rows in unused slots) and
+      // dW_iv = dvg^T fc (PyTorch gate order, into the slot's column range):
+      // bf16 operands, fp32 accumulation and output, the measured hipBLASLt
+      // choices.  As fp32 at::mm, dfc ran as an MT32x16 fp32 kernel: 79 us
+      // alone and 380-575 us next to the dW_logit GEMM after the persistent
+      // loop (profiles/r6/steps_xe*.txt)
+      TORCH_CHECK(vg_bwd[4].scalar_type() == at::kBFloat16 && vg_bwd[4].size(0) == H4,
+                  "vg_bwd[4]: the packed bf16 (4H, Fv) W_iv shadow");
+      const int64_t Fv = vg_bwd[4].size(1);
+      at::Tensor dvg_p16 = dvg.to(at::kBFloat16);
+      at::Tensor dvg16 = dvg_p16.index_select(1, vg_bwd[0]);  // PyTorch gate order
+      at::Tensor dvg_u = dvg16;
+      at::Tensor dfc = at::empty({dvg.size(0), Fv}, f32);
+      at::Tensor wiv16 = vg_bwd[4];
       at::Tensor fc16 = vg_bwd[5].to(at::kBFloat16);
-      gemm_bf16_tuned(dfc, dvg16, false, wiv16, false, 24);
+      gemm_bf16_tuned(dfc, dvg_p16, false, wiv16, false, 24);
       at::Tensor wiv_slot = vg_bwd[2].narrow(1, E, Fv);
       gemm_bf16_tuned(wiv_slot, dvg16, true, fc16, false, 24);
       std::vector<at::Tensor> outs(vg_bwd.begin() + 6, vg_bwd.begin() + 6 + 2 * vg_nf);
       std::vector<at::Tensor> xs(vg_bwd.begin() + 6 + 2 * vg_nf, vg_bwd.begin() + 6 + 3 * vg_nf);
       std::vector<at::Tensor> wsv(vg_bwd.begin() + 6 + 3 * vg_nf, vg_bwd.begin() + 6 + 4 * vg_nf);
       (void)featpool_backward(dfc, vg_bwd[5], xs, wsv, vg_p, outs);
-      vg_keep = {dvg_u, dfc, dvg16, wiv16, fc16};
+      vg_keep = {dvg_u, dfc, dvg16, dvg_p16, fc16};
     }
     (void)hipEventRecord(aux.ev[5], side2.stream());
   }
@@ -1886,6 +1890,9 @@ static ShadowSegs make_shadow_segs(const at::Tensor& meta, const std::vector<at:
       if (g.kind == SHADOW_GATES_HH)
         TORCH_CHECK(g.dst2 != nullptr && g.cols == g.H && d2.numel() >= 4 * (int64_t)g.H * g.ld2,
                     "W_hh shadow needs its packed copy");
+      if (g.kind == SHADOW_GATES_IH && g.dst2 != nullptr)
+        TORCH_CHECK(g.cols > g.E && g.ld2 >= g.cols - g.E && d2.numel() >= 4 * (int64_t)g.H * g.ld2,
+                    "W_ih video-column shadow shape");
     }
   }
   return ss;

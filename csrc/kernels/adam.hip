@@ -102,6 +102,7 @@ __device__ __forceinline__ void shadow_store(const ShadowSegs& ss, int64_t e, fl
       const int64_t pr = packed_gate_row(row, g.H, g.slots);
       if (g.kind == SHADOW_GATES_IH) {
         if (col < g.E) g.dst[pr * (g.E + g.H) + col] = b;
+        else if (g.dst2 != nullptr) g.dst2[pr * g.ld2 + (col - g.E)] = b;  // video columns
       } else {  // SHADOW_GATES_HH
         g.dst[pr * (g.E + g.H) + g.E + col] = b;
         g.dst2[pr * g.ld2 + col] = b;
@@ -143,10 +144,18 @@ __device__ __forceinline__ void shadow_store4(const ShadowSegs& ss, int64_t e0, 
     }
     const int64_t pr = packed_gate_row(row, g.H, g.slots);
     if (g.kind == SHADOW_GATES_IH) {
-      uint16_t* d = g.dst + pr * (g.E + g.H) + col;
+      if (col + 3 < g.E) {
+        uint16_t* d = g.dst + pr * (g.E + g.H) + col;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (col + q < g.E) d[q] = f2bf(vals[q]);
+        for (int q = 0; q < 4; ++q) d[q] = f2bf(vals[q]);
+      } else if (g.dst2 != nullptr && col >= g.E) {  // packed video columns
+        uint16_t* d = g.dst2 + pr * g.ld2 + (col - g.E);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = f2bf(vals[q]);
+      } else {  // straddles the token / video boundary, or no video shadow
+#pragma unroll
+        for (int q = 0; q < 4; ++q) shadow_store(ss, e0 + q, vals[q]);
+      }
     } else {  // SHADOW_GATES_HH
       uint16_t* d = g.dst + pr * (g.E + g.H) + g.E + col;
       uint16_t* d2 = g.dst2 + pr * g.ld2 + col;

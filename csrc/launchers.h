@@ -48,7 +48,8 @@ struct ShadowSeg {
   int cols;         // row length of the source matrix (GATES kinds)
   int H, E;         // cell sizes: packed wx is (4H, E + H)
   uint16_t* dst;    // PLAIN: dst[j]; GATES kinds: packed wx
-  uint16_t* dst2;   // GATES_HH: packed W_hh copy (row stride ld2)
+  uint16_t* dst2;   // GATES_HH: packed W_hh copy; GATES_IH: packed video columns
+                    // [E, cols) of W_ih (nullable); row stride ld2
   int ld2;
   int slots;        // GATES kinds: packed slot of source gate g = bits [2g, 2g + 2)
 };

@@ -278,10 +278,9 @@ class _DecoderFn(torch.autograd.Function):
         vg_bwd, vg_nf, vg_p = [], 0, 0.0
         vg_ctx, ctx.vg_ctx = getattr(ctx, 'vg_ctx', None), None
         if (vg_ctx is not None and emb_direct and 'fp_w0' in direct and eng.layers == 1
-                and not ctx.state0):
+                and not ctx.state0 and eng.wiv is not None):
             fc, xs, wsd, vg_p, vg_nf = vg_ctx.payload
-            vg_bwd = ([eng.dst_ie, eng.dst_hh, direct['wih'], direct['whh'],
-                       eng.model.core.rnn.weight_ih_l0.detach(), fc]
+            vg_bwd = ([eng.dst_ie, eng.dst_hh, direct['wih'], direct['whh'], eng.wiv, fc]
                       + [direct['fp_w%d' % f] for f in range(vg_nf)]
                       + [direct['fp_b%d' % f] for f in range(vg_nf)] + list(xs) + list(wsd))
         # the operand preparation above (token rows, contiguous gradients)
@@ -409,6 +408,12 @@ class DecoderEngine:
         self.wq = self.whh_q[4 * H:] if self.attention else None
         self.emb = torch.empty(V, E, **bf)
         self.wlog = torch.empty(V, H, **bf)
+        # W_ih's video columns in packed gate rows (zero rows in unused gate
+        # slots): the operand of the per-video gate term vg = fc W_iv^T and of
+        # its backward dfc = dvg W_iv, written by the fused Adam pass like the
+        # other shadows (no per-step conversion)
+        fv = model.core.rnn.weight_ih_l0.size(1) - E
+        self.wiv = torch.zeros(4 * H, fv, **bf) if fv > 0 and not self.standard else None
         # (fp16: the decode's cell epilogue gathers one row per caption row and
         # step; half the bytes of fp32, 11 significant bits for these O(1)
         # gate pre-activation terms)
@@ -453,8 +458,9 @@ class DecoderEngine:
         empty = torch.empty(0, dtype=torch.bfloat16, device=self.wx.device)
         segs = [(m.logit.weight, 0, 0, self.wlog, empty, 0, 0, E),
                 (m.embed.weight, 0, 0, self.emb, empty, 0, 0, E),
-                (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx, empty, 0, self.slots_ie,
-                 E),
+                (rnn.weight_ih_l0, 1, rnn.weight_ih_l0.size(1), self.wx,
+                 empty if self.wiv is None else self.wiv,
+                 0 if self.wiv is None else self.wiv.size(1), self.slots_ie, E),
                 (rnn.weight_hh_l0, 2, H, self.wx, self.whh_q, H, self.slots_hh, E)]
         if self.attention:  # (MANet: the first F rows of the padded W_q)
             segs.append((self._query_weight(), 0, 0, self.wq, empty, 0, 0, E))
@@ -481,6 +487,8 @@ class DecoderEngine:
         self.wx[:, :E].copy_(self.pack_rows(w_ih[:, :E], self.src_ie))
         self.wx[:, E:].copy_(self.pack_rows(w_hh, self.src_hh))
         self.whh.copy_(self.wx[:, E:])
+        if self.wiv is not None:
+            self.wiv.copy_(self.pack_rows(w_ih[:, E:], self.src_ie))
         self.emb.copy_(m.embed.weight)
         self.wlog.copy_(m.logit.weight)
         if self.attention:

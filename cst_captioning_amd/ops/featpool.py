@@ -88,18 +88,19 @@ class _FeatPoolVgateFn(torch.autograd.Function):
         wsd = [w.detach() for w in ws]
         fc = _ext.ops().featpool_forward(list(xs), wsd, [b.detach() for b in bs], p, rng)
         w_iv = w_ih.detach()[:, eng.E:]
-        if fc.is_cuda:
-            # bf16 operands, fp32 accumulate and output, the measured hipBLASLt
-            # choice (host/blaslt_tuned.cpp): the fp32 product ran as an MT16x64
-            # fp32 kernel, 39 us on the forward's critical path
+        wiv = getattr(eng, 'wiv', None)
+        if fc.is_cuda and wiv is not None:
+            # bf16 operands (W_iv: the engine's packed shadow, rows already in
+            # packed gate order, so the product IS the packed gate term), fp32
+            # accumulate and output, the measured hipBLASLt choice
+            # (host/blaslt_tuned.cpp): the fp32 product ran as an MT16x64 fp32
+            # kernel, 39 us on the forward's critical path
             # (profiles/r6/steps_xe_after_fixes.txt); the decoder's other input
             # terms are bf16 products too
-            y = torch.empty(fc.size(0), w_iv.size(0), device=fc.device)
-            _ext.ops().gemm_bf16_tuned(y, fc.to(torch.bfloat16), False, w_iv.to(torch.bfloat16),
-                                       True)
+            vg = torch.empty(fc.size(0), wiv.size(0), device=fc.device)
+            _ext.ops().gemm_bf16_tuned(vg, fc.to(torch.bfloat16), False, wiv, True)
         else:
-            y = torch.mm(fc, w_iv.t())
-        vg = eng.pack_rows(y, eng.src_ie, 1)
+            vg = eng.pack_rows(torch.mm(fc, w_iv.t()), eng.src_ie, 1)
         ctx.eng, ctx.p, ctx.nf, ctx.wih_shape = eng, p, nf, w_ih.shape
         ctx.save_for_backward(fc, *xs, *wsd)
         # the decoder forward that consumes vg takes these, so its backward
