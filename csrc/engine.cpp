@@ -969,8 +969,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
   // (the bias gradient as two extra bf16 columns (alpha hi / lo) of the dW
   // GEMM instead of the column sums measured slower: the N = 528 GEMM took
   // ~100 us longer, profiles/r3/ab_dbdw.txt)
-  // dW GEMM over augmented rows [alpha Hd | alpha_hi | alpha_lo | 0 x 14]
-  // (bf16, H + 16 columns): the same pass over E' also yields the bias
+  // dW GEMM over augmented rows [alpha Hd | alpha_hi | alpha_lo | 0 ...]
+  // (bf16, H + dw_pad columns): the same pass over E' also yields the bias
   // gradient (columns H, H + 1 of the product), instead of a separate
   // column-sum pass over the 753 MB exp store.  CSTCAP_DW_AUG=0: the separate
   // column sums (vgrad_colsum).
@@ -991,7 +991,15 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
     return e != nullptr && atoi(e) != 0;
   }();
   const bool dw_aug = !ds_ready && !dw_wgrad_env && (dw_aug_env < 0 ? persistent : dw_aug_env != 0);
-  const int64_t ldhs = dw_aug ? H + 16 : H;
+  // (the augmented rows padded to H + 64 columns: hipBLASLt's pick for the
+  // split-K batch runs 443 us at N = 576 against 479 at N = 528 and 537 at
+  // N = 512, isolated timings, profiles/r6/README_r6.md; CSTCAP_DW_PAD)
+  static const int64_t dw_pad = [] {
+    const char* e = getenv("CSTCAP_DW_PAD");
+    const int64_t v = e != nullptr ? atoll(e) : 64;
+    return v >= 16 && v <= 512 && v % 8 == 0 ? v : 64;
+  }();
+  const int64_t ldhs = dw_aug ? H + dw_pad : H;
   if (!ds_ready) {
     alpha = at::empty({NR}, f32);
     hs = at::empty({NR, ldhs}, wx.options());
@@ -1045,7 +1053,7 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
       // over all rows with the measured hipBLASLt choice: 3.439-3.451 vs
       // 3.330-3.343 ms per step, profiles/r6/README_r6.md)
       const int64_t kr = NR / dw_split;
-      at::Tensor p;  // (split, V, H + 16)
+      at::Tensor p;  // (split, V, ldhs)
       if (dw_tuned_env) {
         // the batch with the measured hipBLASLt choice (gemm_bf16_tuned_batched)
         p = at::empty({dw_split, V, ldhs}, f32);

@@ -181,7 +181,7 @@ constexpr int VG_THREADS = 256, VG_ROWS = VG_THREADS / WAVE;
 // Hd) (and dHd = alpha X in place when dhd is given; the engine instead lets
 // the reverse loop scale the rows it reads, so this pass leaves the critical
 // path).
-// ldhs > H (augmented rows, ldhs = H + 16): columns H, H + 1 of the row also
+// ldhs > H (augmented rows, ldhs = H + 8k): columns H, H + 1 of the row also
 // get alpha as two bf16 words (hi, lo = alpha - hi) and the rest zeros, so the
 // dW GEMM over these rows also yields the bias gradient E'^T alpha
 __global__ __launch_bounds__(VG_THREADS) void vgrad_rows_kernel(
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(VG_THREADS) void vgrad_rows_kernel(
   if (row >= NR) return;
   const int lane = threadIdx.x & 63;
   const float al = alpha[row];
-  if (ldhs > H && lane < 2) {
+  if (8 * lane < ldhs - H) {
     const uint16_t hi = f2bf(al), lo = f2bf(al - bf2f(hi));
     *reinterpret_cast<uint4*>(hs + row * ldhs + H + 8 * lane) =
         make_uint4(lane == 0 ? ((uint32_t)hi | ((uint32_t)lo << 16)) : 0u, 0u, 0u, 0u);
@@ -220,7 +220,8 @@ void launch_vgrad_rows(const float* alpha, int64_t NR, int H, const uint16_t* hd
                        uint16_t* hs, hipStream_t stream, int ldhs) {
   if (ldhs <= 0) ldhs = H;
   if (H % 8 != 0) throw std::runtime_error("vgrad_rows: H must be a multiple of 8");
-  if (ldhs != H && ldhs != H + 16) throw std::runtime_error("vgrad_rows: ldhs must be H or H + 16");
+  if (ldhs < H || (ldhs - H) % 8 != 0 || ldhs - H > 8 * WAVE)
+    throw std::runtime_error("vgrad_rows: ldhs must be H + 8k (k <= 64)");
   hipLaunchKernelGGL(vgrad_rows_kernel, dim3((unsigned)((NR + VG_ROWS - 1) / VG_ROWS)),
                      dim3(VG_THREADS), 0, stream, alpha, NR, H, hd, dhd, hs, ldhs);
   post_launch("vgrad_rows_kernel", stream);
