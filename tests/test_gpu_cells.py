@@ -217,9 +217,14 @@ def test_cell_graph_training_keeps_packed_shadows(variant):
     assert not torch.equal(w0, model.core.rnn.weight_hh_l0.detach())
     got = [t.clone() for t in (eng.wx, eng.whh_q, eng.emb, eng.wlog, eng.current_ptab())]
     got_up = [t.clone() for t in eng.wup + eng.whh_up]
+    wiv = None if eng.wiv is None else eng.wiv.clone()
+    assert (wiv is None) == (mt == 'standard')
     eng.refresh_weights()
     for g, r in zip(got, (eng.wx, eng.whh_q, eng.emb, eng.wlog)):
         assert torch.equal(g, r)
+    if wiv is not None:  # the video columns' packed shadow, zero rows in unused slots
+        assert torch.equal(wiv, eng.wiv)
+        assert not eng.wiv[(eng.src_ie == eng.gates * eng.H)].any()
     assert len(got_up) == 2 * (nl - 1)
     for g, r in zip(got_up, eng.wup + eng.whh_up):
         assert torch.equal(g, r)

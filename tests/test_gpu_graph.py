@@ -157,9 +157,12 @@ def test_adam_pass_writes_the_bf16_shadows():
         tr.train_step(loader.get_batch(), 0)
     eng = tr.engine
     got = [t.clone() for t in (eng.wx, eng.whh_q, eng.emb, eng.wlog, eng.current_ptab())]
+    assert eng.wiv is not None  # concat model: W_ih's video columns, packed
+    wiv = eng.wiv.clone()
     eng.refresh_weights()
     for g, r in zip(got, (eng.wx, eng.whh_q, eng.emb, eng.wlog)):
         assert torch.equal(g, r)
+    assert torch.equal(wiv, eng.wiv)
     torch.testing.assert_close(got[4], eng.ptab, rtol=1e-5, atol=1e-5)
 
 
