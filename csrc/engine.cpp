@@ -485,8 +485,21 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     const char* e = getenv("CSTCAP_PRE16");
     return e == nullptr || atoi(e) != 0;
   }();
-  const bool pre16 =
-      pre16_env && !(has_att && !att_mfma_ok((int)vgate_div, (int)C, (int)A, (int)H, per_frame));
+  // CSTCAP_GREEDY_ATT_MFMA=1: a forward that saves nothing (the SCST greedy
+  // baseline, one row per video) takes the MFMA attention too.  Opt-in: its
+  // A / 64 workgroups per video (512 per greedy step at the att8 shape, each
+  // computing 32-row tiles for one row) slow the concurrent sampled rollout
+  // more than the VALU scorer + query GEMM they replace (att8 4.730 / 4.771
+  // vs 4.607 / 4.602 ms, interleaved on one box, profiles/r6/s2/).
+  static const bool fwd1_env = [] {
+    const char* e = getenv("CSTCAP_GREEDY_ATT_MFMA");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  const bool att_mfma =
+      has_att && (save || !fwd1_env
+                      ? att_mfma_ok((int)vgate_div, (int)C, (int)A, (int)H, per_frame)
+                      : att_mfma_fwd_ok((int)vgate_div, (int)C, (int)A, (int)H, per_frame));
+  const bool pre16 = pre16_env && !(has_att && !att_mfma);
   at::Tensor pre = n_steps > 1 ? at::empty({R, H4}, f32.dtype(pre16 ? at::kHalf : at::kFloat))
                                : at::Tensor();
   at::Tensor xin = NL > 1 ? at::empty({R, H4}, f32) : at::Tensor();
@@ -536,7 +549,6 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
   // adds; no attention launch between the decode launch and the combine.
   // Step 0 (q = 0) and other shapes use the attention kernels of attention.hip.
   const int CPAD = C <= 8 ? 8 : 16;
-  const bool att_mfma = has_att && att_mfma_ok((int)vgate_div, (int)C, (int)A, (int)H, per_frame);
   at::Tensor gv16, vg16, att_ep, att_cnt, u_all;
   if (att_mfma) {
     // training: the scorer values tanh(P + q) of steps >= 1 (fp16), read by
@@ -2346,7 +2358,7 @@ std::vector<at::Tensor> att_mfma_fwd(at::Tensor h, at::Tensor wq, at::Tensor P, 
                   gv.size(0) == Bv && gv.size(1) == C && gv.size(2) == 4 * H && R % Bv == 0,
               "att_mfma: operand shapes");
   const int vdiv = (int)(R / Bv), CP = C <= 8 ? 8 : 16;
-  TORCH_CHECK(att_mfma_ok(vdiv, (int)C, (int)A, (int)H, 0), "att_mfma: unsupported shape");
+  TORCH_CHECK(att_mfma_fwd_ok(vdiv, (int)C, (int)A, (int)H, 0), "att_mfma: unsupported shape");
   at::Tensor gv16 = at::zeros({Bv, 4 * H, CP}, h.options());
   gv16.narrow(2, 0, C).copy_(gv.transpose(1, 2));
   at::Tensor vg = at::empty({R, 4 * H}, h.options());

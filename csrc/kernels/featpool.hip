@@ -7,10 +7,10 @@
 // on MI355X.  Here:
 //   * forward: ONE launch of 64 x 64 output tiles for every modality at once,
 //     split over K (256-wide chunks) so ~240 workgroups fill the chip; fp32
-//     operands on the fp32 matrix cores (MFMA 32x32x2 f32: the module keeps
-//     the reference's fp32 precision -- bf16 operands would move ReLU
-//     decisions near zero and with them whole gradient terms); partial
-//     tiles go to a workspace and
+//     operands (the module keeps the reference's fp32 precision -- plain bf16
+//     operands would move ReLU decisions near zero and with them whole
+//     gradient terms), split into bf16 hi + lo on the bf16 matrix cores (see
+//     fp_mfma_step); partial tiles go to a workspace and
 //     a second launch sums them, adds the bias, applies ReLU and the dropout
 //     mask (counter hash of (seed, row, column), like the decoder's dropout)
 //     and writes the concatenated (rows, F*H) output;
@@ -31,16 +31,35 @@ constexpr int FP_LDA = FP_KS + 1;  // fp32 row stride in LDS (conflict-free colu
 constexpr int FEATPOOL_DROP_KEY = 0x46504C;  // dropout_keep "step" key of FeatPool
 
 // One 64x64 tile += A(64 x KS) B(64 x KS)^T from fp32 LDS tiles (row stride
-// FP_LDA): wave w owns the 32x32 quarter (w >> 1, w & 1); each MFMA takes
-// k = 2: lane l supplies row / column l % 32 at k = l / 32.
+// FP_LDA): wave w owns the 32x32 quarter (w >> 1, w & 1).  The fp32 operands
+// are split in registers into hi = bf16(x) and lo = bf16(x - hi) (x = hi + lo
+// to 2^-16 relative) and each 16-deep step is three bf16 MFMAs (hi hi + hi lo
+// + lo hi, fp32 accumulate; the dropped lo lo term is below 2^-16): products
+// within ~2^-16 of fp32 for 6 x 32 instead of 16 x 64 matrix-core cycles per
+// 32-deep K step (v_mfma_f32_32x32x16_bf16 vs v_mfma_f32_32x32x2_f32, whose
+// fp32 rate is 1/16 of bf16; the att8 frame FeatPool over 512 rows took 49 us
+// forward and 55 us backward on the fp32 matrix cores).
+// 32x32x16 bf16: lane l supplies row / column l % 32 at k = 8 (l / 32) + 0..7
+// (the same LDS words the fp32 form read, conflict-free with stride FP_LDA).
 __device__ __forceinline__ void fp_mfma_step(const float* As, const float* Bs, f32x16& acc) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w >> 1, wc = w & 1;
-  const float* ar = As + (wr * 32 + (lane & 31)) * FP_LDA + (lane >> 5);
-  const float* br = Bs + (wc * 32 + (lane & 31)) * FP_LDA + (lane >> 5);
+  const float* ar = As + (wr * 32 + (lane & 31)) * FP_LDA + 8 * (lane >> 5);
+  const float* br = Bs + (wc * 32 + (lane & 31)) * FP_LDA + 8 * (lane >> 5);
 #pragma unroll
-  for (int s = 0; s < FP_KS / 2; ++s)
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * s], br[2 * s], acc, 0, 0, 0);
+  for (int s = 0; s < FP_KS / 16; ++s) {
+    bf16x8 ah, al, bh, bl;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float a = ar[16 * s + e], b = br[16 * s + e];
+      const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+      ah[e] = ha, al[e] = (__bf16)(a - (float)ha);
+      bh[e] = hb, bl[e] = (__bf16)(b - (float)hb);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  }
 }
 
 // (row, col) of accumulator element r of lane `lane` in the 64x64 tile
@@ -121,9 +140,20 @@ __global__ __launch_bounds__(256) void featpool_fwd_epilogue_kernel(FeatPoolArgs
   const int nkc = (g.d + FP_KCH - 1) / FP_KCH, nut = a.H / FP_T;
   const int rt = r / FP_T, ut = u / FP_T;
   const int base = g.blk0 + (rt * nut + ut) * nkc;
-  float z = g.b[u];
-  for (int kc = 0; kc < nkc; ++kc)
-    z += ws[(int64_t)(base + kc) * FP_T * FP_T + (r % FP_T) * FP_T + (u % FP_T)];
+  // the K chunks' partials: 8 loads in flight per thread (4 independent sums)
+  // instead of one dependent load per chunk (up to 16 chunks per modality)
+  const float* src = ws + (int64_t)base * FP_T * FP_T + (r % FP_T) * FP_T + (u % FP_T);
+  float zs[4] = {g.b[u], 0.f, 0.f, 0.f};
+  int kc = 0;
+  for (; kc + 8 <= nkc; kc += 8) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = src[(int64_t)(kc + e) * FP_T * FP_T];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) zs[e & 3] += v[e];
+  }
+  for (; kc < nkc; ++kc) zs[kc & 3] += src[(int64_t)kc * FP_T * FP_T];
+  const float z = (zs[0] + zs[1]) + (zs[2] + zs[3]);
   float y = fmaxf(z, 0.f);
   if (drop_p > 0.f) {
     const bool keep = dropout_keep(rng_seed(rng, RNG_SLOT_DROPOUT), FEATPOOL_DROP_KEY, r, col, drop_p);

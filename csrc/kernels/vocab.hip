@@ -416,14 +416,19 @@ __global__ __launch_bounds__(256) void att_mfma_fwd_kernel(AttMfmaArgs att) {
 // host dispatch over the attention variants (frames padded to 8 / 16)
 #define ATT_VARIANTS(X) X(8) X(16)
 
-bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame) {
-  return !per_frame && vdiv >= 2 && vdiv <= 32 && C >= 1 && C <= 16 && A % ATT_SLICE == 0 &&
+bool att_mfma_fwd_ok(int vdiv, int C, int A, int H, int per_frame) {
+  return !per_frame && vdiv >= 1 && vdiv <= 32 && C >= 1 && C <= 16 && A % ATT_SLICE == 0 &&
          A <= 16 * ATT_SLICE && H % 32 == 0 && H >= 64 && H <= 512 &&
          att_mfma_lds_bytes(C, C <= 8 ? 8 : 16, H) <= 48 * 1024;
 }
+// training (the saved forward feeds the fused attention backward, which needs
+// two or more rows per video): 2..32 rows per video
+bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame) {
+  return vdiv >= 2 && att_mfma_fwd_ok(vdiv, C, A, H, per_frame);
+}
 
 static void check_att_mfma(const AttMfmaArgs& a) {
-  if (!att_mfma_ok(a.vdiv, a.C, a.A, a.H, 0) || a.G4 != 4 * a.H || a.CP != (a.C <= 8 ? 8 : 16) ||
+  if (!att_mfma_fwd_ok(a.vdiv, a.C, a.A, a.H, 0) || a.G4 != 4 * a.H || a.CP != (a.C <= 8 ? 8 : 16) ||
       a.e_part == nullptr || a.cnt == nullptr)
     throw std::runtime_error("att_mfma: unsupported attention shape");
 }

@@ -135,6 +135,9 @@ struct AttMfmaArgs {
 // the MFMA attention path applies: rows per video 2..32, C <= 16, A % 64 == 0,
 // A <= 1024, H % 32 == 0, 64 <= H <= 512, the shared scorer (not per frame)
 bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame);
+// the same for a forward that saves nothing for a backward (the SCST greedy
+// baseline, evaluation): one row per video allowed
+bool att_mfma_fwd_ok(int vdiv, int C, int A, int H, int per_frame);
 // standalone launch of the same workgroups (tests / microbenchmarks)
 void launch_att_mfma_fwd(const AttMfmaArgs& a, hipStream_t stream);
 // size of the end-of-sequence flag area per decode step (ints) of `counts`

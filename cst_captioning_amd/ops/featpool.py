@@ -4,7 +4,8 @@ backward, for the fused decoder engine (the PyTorch path keeps
 :class:`~cst_captioning_amd.models.modules.FeatPool`).
 
 Reference: ``/root/reference/model.py:46-69``.  Same function, parameters
-and fp32 precision (fp32 matrix cores); dropout masks come from a counter
+and fp32 operands (split into bf16 hi + lo on the bf16 matrix cores, three
+MFMAs per step: products within ~2^-16 of fp32); dropout masks come from a counter
 hash of (seed, row, column) drawn on the device (graph-safe),
 distribution-identical to ``nn.Dropout``.
 """

@@ -25,7 +25,9 @@ DEV = 'cuda'
 
 
 @pytest.mark.parametrize('Bv,vdiv,C,A,H', [(64, 20, 8, 512, 512), (7, 32, 16, 256, 128),
-                                           (9, 2, 3, 128, 256), (5, 13, 12, 384, 64)])
+                                           (9, 2, 3, 128, 256), (5, 13, 12, 384, 64),
+                                           # one row per video: the SCST greedy baseline
+                                           (64, 1, 8, 512, 512), (9, 1, 3, 128, 256)])
 def test_att_mfma_kernel_matches_fp32(Bv, vdiv, C, A, H):
     from cst_captioning_amd import _ext
     ops = _ext.ops()

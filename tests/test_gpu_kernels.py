@@ -435,9 +435,10 @@ def test_fused_featpool_matches_torch(rows):
     out = featpool(pool, feats)
     ref = ref_pool(feats)
     assert out.shape == ref.shape == (rows, 4 * 512)
-    # fp32 matrix cores: equal up to the summation order
+    # fp32 operands split into bf16 hi + lo on the bf16 matrix cores (three
+    # MFMAs per step): products within ~2^-16 of fp32
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
-    assert ((out - ref).norm() / ref.norm()).item() < 1e-5
+    assert ((out - ref).norm() / ref.norm()).item() < 5e-5
     assert ((out > 0) != (ref > 0)).float().mean().item() < 1e-4
     g = torch.randn_like(out)
     (out * g).sum().backward()
@@ -449,7 +450,7 @@ def test_fused_featpool_matches_torch(rows):
         dzf = dz[:, 512 * f:512 * (f + 1)]
         ref_dw = dzf.t() @ x
         err = ((m[0].weight.grad - ref_dw).norm() / ref_dw.norm()).item()
-        assert err < 1e-5, (f, err)
+        assert err < 5e-5, (f, err)
         torch.testing.assert_close(m[0].bias.grad, dzf.sum(0), rtol=1e-4, atol=1e-4)
     # dropout: about half the units kept, survivors scaled by 2, and the
     # backward routes gradient exactly through the survivors
@@ -468,7 +469,7 @@ def test_fused_featpool_matches_torch(rows):
     dz = kept[:, :512].float() * 2.0
     torch.testing.assert_close(w0.bias.grad, dz.sum(0), rtol=1e-4, atol=1e-4)
     ref_dw = dz.t() @ x0
-    assert ((w0.weight.grad - ref_dw).norm() / ref_dw.norm()).item() < 1e-5
+    assert ((w0.weight.grad - ref_dw).norm() / ref_dw.norm()).item() < 5e-5
 
 
 @pytest.mark.parametrize('per_video', [True, False])
