@@ -14,7 +14,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att,
                                         int64_t cell, std::vector<at::Tensor> state0,
-                                        std::vector<at::Tensor> up, bool store_exp);
+                                        std::vector<at::Tensor> up, bool store_exp,
+                                        bool xe_rows);
 void set_grad_events(bool on);
 void grad_event_wait(int64_t k, int64_t stream);
 void grad_event_record(int64_t k, int64_t stream);
@@ -46,7 +47,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          std::vector<at::Tensor> up, at::Tensor blog,
                                          at::Tensor fix_total, int64_t vgate_div,
                                          at::Tensor xw, std::vector<at::Tensor> vg_bwd,
-                                         int64_t vg_nf, double vg_p, int64_t x_wait);
+                                         int64_t vg_nf, double vg_p, int64_t x_wait,
+                                         bool exp_zero_off);
 std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor whh,
                                     at::Tensor wlog, at::Tensor blog, at::Tensor vgate,
                                     int64_t K, int64_t T, int64_t bos_index,
@@ -165,7 +167,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_wlog"), py::arg("out_blog"), py::arg("comm_stream"), py::arg("att"),
         py::arg("out_emb"), py::arg("ds_bias"), py::arg("cell"), py::arg("state0"), py::arg("up"),
         py::arg("blog"), py::arg("fix_total"), py::arg("vgate_div"), py::arg("xw"),
-        py::arg("vg_bwd"), py::arg("vg_nf"), py::arg("vg_p"), py::arg("x_wait") = 0);
+        py::arg("vg_bwd"), py::arg("vg_nf"), py::arg("vg_p"), py::arg("x_wait") = 0,
+        py::arg("exp_zero_off") = false);
   m.def("cider_build_tables", &cst::cider_build_tables);
   m.def("cider_score", &cst::cider_score);
   m.def("cider_score_cpu", &cst::cider_score_cpu);

@@ -118,6 +118,7 @@ static const uint32_t* rng_ptr(const at::Tensor& rng) {
 // Events and side streams are created once per device and reused: nothing
 // is created or destroyed while a HIP graph is being captured.
 constexpr int MAX_DHD_CHUNKS = 32;  // per-chunk events of the vocab-head dHd GEMM
+constexpr int XE_MAX_STEPS = 64;  // XE all rows: decode steps per forward
 struct DeviceAux {
   std::vector<hipEvent_t> ev;
   c10::hip::HIPStream side[2];
@@ -306,7 +307,8 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                                         bool save, bool want_xe, bool use_counts,
                                         bool use_unfinished, std::vector<at::Tensor> att,
                                         int64_t cell, std::vector<at::Tensor> state0,
-                                        std::vector<at::Tensor> up, bool store_exp) {
+                                        std::vector<at::Tensor> up, bool store_exp,
+                                        bool xe_rows) {
   check_cuda(wx, "wx");
   TORCH_CHECK(cell >= 0 && cell <= 2, "cell: 0 lstm, 1 gru, 2 rnn (tanh)");  // CellType (common.h)
   check_cuda(emb, "emb");
@@ -559,6 +561,61 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
     vg16 = at::empty({R, H4}, bf);
     att_ep = at::empty({Bv, A / 64, 32, CPAD}, f32);
     att_cnt = at::zeros({Bv}, at::TensorOptions().dtype(at::kInt).device(dev));
+  }
+
+  // XE all rows (xe_rows: a teacher-forced training forward).  Every input
+  // token is a label, known before the vocabulary projection of the previous
+  // step, so the cell needs no combine: ONE launch per step runs the
+  // vocabulary tiles of step t (E = exp(x), offset 0 -- the backward's
+  // VGradRows::zero_off -- and the per-tile partials) together with the WHOLE
+  // LSTM step t+1 (lstm_gemm.h lstm_cell_block: recurrent GEMM + table row +
+  // cell); ONE combine over all rows after the chain gives every step's LSE
+  // and target log-prob: the per-step combine (~12 us with its cell epilogue)
+  // leaves the chain.  (Per-step combines on a side stream contended with the
+  // chain: XE 3.279 / 3.308 vs 3.213 / 3.258 ms per step, profiles/r6/s2/.)  seq = labels[:, 1:T], exactly as the
+  // per-step combine picks them (a step after which every row emitted EOS only
+  // forces tokens the labels already hold as 0).
+  if (xe_rows) {
+    TORCH_CHECK(save && store_exp && want_xe && have_labels && NL == 1 && !has_att &&
+                    state0.empty() && n_steps == T && n_steps <= XE_MAX_STEPS,
+                "xe_rows: a saved, exp-store teacher-forced forward of a one-layer decoder "
+                "without attention / initial state, <= 64 steps");
+    for (int64_t t = 0; t + 1 < T; ++t)
+      TORCH_CHECK(modes[t] == SEL_GT_H, "xe_rows: teacher forcing at every step");
+    const int n_vt = vocab_num_tiles((int)V);
+    const int64_t pstep = (int64_t)n_vt * R * vocab_partial_bytes();  // partial bytes per step
+    at::Tensor part_all = at::empty({n_steps * pstep / 4}, f32);
+    at::Tensor tgt_all = labels.narrow(1, 1, n_steps).t().contiguous();  // (n_steps, R)
+    at::Tensor gx = at::empty({n_steps, R}, f32);
+    stamp(STAMP_FWD_BEGIN, st);
+    launch_lstm_step_fwd(LAB, L, PTAB, nullptr, nullptr, VG, VDIV, (int)R, (int)H, WHH,
+                         h_buf(0, 0), c_buf(0, 0), hd_buf(0, 0), (int)H, (float)drop_p, RNG,
+                         key(0, 0), gates_buf(0, 0), st, nullptr, (int)cell);
+    stamp(STAMP_FWD_STEP0, st);
+    for (int64_t t = 0; t < n_steps; ++t) {
+      const bool next = t + 1 < n_steps;
+      XeCell xc{};
+      if (next)
+        xc = XeCell{LAB + (t + 1), L, PTAB, c_buf(0, t), h_buf(0, t + 1), c_buf(0, t + 1),
+                    hd_buf(0, t + 1), gates_buf(0, t + 1), (float)drop_p, key(0, t + 1),
+                    (int)cell};
+      char* pt = reinterpret_cast<char*>(part_all.data_ptr()) + t * pstep;
+      launch_vocab_lstm_xe(hd_buf(0, t), (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
+                           reinterpret_cast<uint16_t*>(logits16[t].data_ptr()), ldl, pt,
+                           tgt_all.data_ptr<int64_t>() + t * R, RNG, h_buf(0, t), WHH, VG, VDIV,
+                           next ? &xc : nullptr, st);
+    }
+    // every step's LSE and target log-probs: one combine over all rows (the
+    // per-step partial blocks), after the chain
+    launch_vocab_combine(part_all.data_ptr(), n_vt, (int)(n_steps * R), lse.data_ptr<float>(),
+                         nullptr, 0, nullptr, 0, gx.data_ptr<float>(), 1, nullptr, 0, SEL_GT_H,
+                         0.f, RNG, 0, nullptr, 0, nullptr, st, nullptr, (int)R);
+    at::Tensor gxt = gx.t();  // (R, T)
+    g_xe.copy_(gxt);
+    g_sel.copy_(gxt.narrow(1, 0, T - 1));
+    seq.copy_(labels.narrow(1, 1, T - 1));
+    stamp(STAMP_FWD_END, st);
+    return {seq, g_sel, g_xe, lse, logits16, HDs[0], Gs[0], Cs[0], Hs[0]};
   }
 
   // step 0: fused cell step from (h_{-1}, c_{-1}) = (h0, c0)
@@ -842,7 +899,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                                          std::vector<at::Tensor> up, at::Tensor blog,
                                          at::Tensor fix_total, int64_t vgate_div,
                                          at::Tensor xw, std::vector<at::Tensor> vg_bwd,
-                                         int64_t vg_nf, double vg_p, int64_t x_wait) {
+                                         int64_t vg_nf, double vg_p, int64_t x_wait,
+                                         bool exp_zero_off) {
   const int64_t n_steps = logits16.size(0), R = logits16.size(1), ldl = logits16.size(2);
   const int64_t H4 = wx.size(0), H = H4 / 4, E = wx.size(1) - H, V = wlog.size(0);
   const int64_t T_sel = seq.size(1);
@@ -1124,7 +1182,8 @@ std::vector<at::Tensor> decoder_backward(at::Tensor wx, at::Tensor wlog, at::Ten
                  has_xe ? labels.size(1) : 0, has_xe ? dg_xe.data_ptr<float>() : nullptr,
                  has_xe ? dg_xe.size(1) : 0, guard ? fix.data_ptr<int>() : nullptr,
                  ptr_or_null<float>(oh_a), ptr_or_null<int>(oh_ys), ptr_or_null<float>(oh_b),
-                 ptr_or_null<int>(oh_yx), have_x ? dHd.data_ptr<float>() : nullptr};
+                 ptr_or_null<int>(oh_yx), have_x ? dHd.data_ptr<float>() : nullptr,
+                 exp_zero_off ? 1 : 0};
     launch_vgrad_onehot(va, reinterpret_cast<uint16_t*>(buf.data_ptr()), ldl,
                         alpha.data_ptr<float>(), s);
     if (guard) {

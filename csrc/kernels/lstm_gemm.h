@@ -15,6 +15,7 @@
 // kernel once the token is known (vocab_combine_kernel's cell epilogue).
 #pragma once
 #include "gemm_tile.h"
+#include "../launchers.h"
 
 namespace cst {
 
@@ -94,6 +95,87 @@ __device__ __forceinline__ void lstm_gemm_block(int bid, const uint16_t* __restr
       } else {
         *reinterpret_cast<float4*>(pre + (int64_t)r * (4 * H) + n0 + 4 * u) = x;
       }
+    }
+  }
+}
+
+// The whole LSTM step of one tile (recurrent GEMM + the cell), for the XE
+// all-rows forward (engine.cpp): with teacher forcing the input token of step
+// t+1 is its label, known before the vocabulary projection of step t, so the
+// cell needs no combine and the step rides in the decode launch of the
+// previous step's vocabulary tiles.  gates = h_t W_hh^T + vgate + P[tok] ->
+// cell -> c, h, dropout(h), saved gates: the epilogue of lstm.hip
+// lstm_step_fwd_kernel on the lstm_gemm_block tiles (its operands gathered
+// before the main loop, so their latency hides under the GEMM).
+// (XeCell: launchers.h)
+template <class LT>
+__device__ __forceinline__ void lstm_cell_block(int bid, const uint16_t* __restrict__ h, int R,
+                                                int H, const uint16_t* __restrict__ whh,
+                                                const float* __restrict__ vgate, int vdiv,
+                                                const XeCell& xc, const uint32_t* __restrict__ rng,
+                                                char* lds) {
+  const int n_nt = (4 * H) / LG_BN, n_rt = (R + LG_BM - 1) / LG_BM;
+  const int b = xcd_remap_g(bid, n_nt * n_rt);
+  const int nt = b / n_rt, rt = b % n_rt;
+  const int r0 = rt * LG_BM, n0 = nt * LG_BN;
+  const int nk = H / 64;
+  const int u = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int hu = nt * 16 + u;  // hidden unit of the lane's 4 packed gates
+  constexpr int RPT = LG_BM / 16;
+  float4 px[RPT], vg[RPT];
+  float cp[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = min(r0 + rg + 16 * i, R - 1);
+    const int tk = (int)xc.tok[(int64_t)r * xc.tok_stride];
+    px[i] = ld_h4(xc.ptab + (int64_t)tk * (4 * H) + n0 + 4 * u);
+    vg[i] = *reinterpret_cast<const float4*>(vgate + (int64_t)(r / vdiv) * (4 * H) + n0 + 4 * u);
+    cp[i] = xc.c_prev[(int64_t)r * H + hu];
+  }
+  f32x16 acc[LT::TM][LT::TN];
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    DmaSrc<LG_BM / 32> a;
+    DmaSrc<LG_BN / 32> bsrc;
+    a.r0 = a.r1 = make_rsrc(h, (int64_t)R * H * 2);
+    a.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < LG_BM / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      a.voff0[i] = min(r0 + row, R - 1) * H * 2 + dma_chunk(row, lane) * 16;
+      a.voff1[i] = a.voff0[i];
+    }
+    bsrc.r0 = bsrc.r1 = make_rsrc(whh, (int64_t)4 * H * H * 2);
+    bsrc.ksplit = nk;
+#pragma unroll
+    for (int i = 0; i < LG_BN / 32; ++i) {
+      const int row = dma_row(w, i, lane);
+      bsrc.voff0[i] = (n0 + row) * H * 2 + dma_chunk(row, lane) * 16;
+      bsrc.voff1[i] = bsrc.voff0[i];
+    }
+    gemm_nt_mainloop<LT>(nk, a, bsrc, lds, acc);
+  }
+  float* C = reinterpret_cast<float*>(lds);
+  store_acc_to_lds<LT>(acc, C, [](int) { return 0.f; });
+  __syncthreads();
+  const float inv_keep = xc.drop_p > 0.f ? 1.f / (1.f - xc.drop_p) : 1.f;
+  const uint32_t seed = rng_seed(rng, RNG_SLOT_DROPOUT);
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int row = rg + 16 * i, r = r0 + row;
+    if (r < R) {
+      const float4 x = *reinterpret_cast<const float4*>(C + row * LT::CSTRIDE + 4 * u);
+      const CellFwd cf = cell_fwd(xc.cell, x.x + vg[i].x + px[i].x, x.y + vg[i].y + px[i].y,
+                                  x.z + vg[i].z + px[i].z, x.w + vg[i].w + px[i].w, cp[i]);
+      const int64_t o = (int64_t)r * H + hu;
+      xc.c_out[o] = cf.c;
+      xc.h_out[o] = f2bf(cf.h);
+      const bool keep = xc.drop_p <= 0.f || dropout_keep(seed, xc.key, r, hu, xc.drop_p);
+      xc.hd_out[o] = f2bf(keep ? cf.h * inv_keep : 0.f);
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(cf.s0) | ((uint32_t)f2bf(cf.s1) << 16);
+      pk.y = (uint32_t)f2bf(cf.s2) | ((uint32_t)f2bf(cf.s3) << 16);
+      *reinterpret_cast<uint2*>(xc.gates_out + (int64_t)r * 4 * H + n0 + 4 * u) = pk;
     }
   }
 }

@@ -589,7 +589,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
     int64_t gsel_stride, float* __restrict__ g_xe, int64_t gxe_stride,
     const int64_t* __restrict__ gt, int64_t gt_stride, int mode, float ss_prob,
     const uint32_t* __restrict__ rng, int step, int* __restrict__ counts, int count_step,
-    uint8_t* __restrict__ unfinished, CellArgs cell) {
+    uint8_t* __restrict__ unfinished, CellArgs cell, int Rs) {
   __shared__ int s_nonzero;
   int tok_final = 0;
   const int sub = threadIdx.x & (LANES - 1);
@@ -608,10 +608,13 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   constexpr int CMB_MAXP = 128 / LANES;  // n_vt <= 128: V <= 16384 at 128-wide tiles
   const bool fastp = n_vt <= CMB_MAXP * LANES;
   VocabPartial pp[CMB_MAXP];
+  // the row's partials: tile t at prow[t * Rs] (Rs = R: one block of rows)
+  const int rq = valid ? r : 0;
+  const VocabPartial* prow = part + (int64_t)(rq / Rs) * n_vt * Rs + (rq % Rs);
   if (valid && fastp) {
 #pragma unroll
     for (int k = 0; k < CMB_MAXP; ++k)
-      pp[k] = part[(int64_t)min(sub + k * LANES, n_vt - 1) * R + r];
+      pp[k] = prow[(int64_t)min(sub + k * LANES, n_vt - 1) * Rs];
   }
   const bool do_cell = cell.pre != nullptr && tok_out != nullptr;
   // one batch of CELL_U units per lane covers H <= 512 (every lane of the row
@@ -666,7 +669,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   } else if (valid) {
 #pragma unroll 4
     for (int t = sub; t < n_vt; t += LANES) {
-      const VocabPartial p = part[(int64_t)t * R + r];
+      const VocabPartial p = prow[(int64_t)t * Rs];
       merge_stat(a, p.m, p.s, p.zval, p.zlogit, p.zidx, p.m, p.xidx, p.xtgt);
     }
   }
@@ -798,6 +801,23 @@ __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
   vocab_tr_block<BN, STAGES, TOPK>(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
 }
 
+// XE all rows (engine.cpp): the first n_lstm_pad workgroups run the WHOLE
+// LSTM step of the next rows (lstm_gemm.h lstm_cell_block: the input token is
+// the label, so the cell needs no combine), the rest the vocabulary tiles of
+// the current rows.  Either part may be empty.
+template <int BN, int STAGES, int OCC>
+__global__ __launch_bounds__(256, OCC) void vocab_lstm_xe_kernel(
+    VOCAB_TR_PARAMS, const uint16_t* __restrict__ h_t, const uint16_t* __restrict__ whh,
+    const float* __restrict__ vgate, int vdiv, XeCell xc, int n_lstm_pad) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int bid = blockIdx.x;
+  if (bid < n_lstm_pad) {
+    if (bid < lstm_gemm_blocks(R, H)) lstm_cell_block<LGTile2>(bid, h_t, R, H, whh, vgate, vdiv, xc, rng, lds);
+    return;
+  }
+  vocab_tr_block<BN, STAGES>(bid - n_lstm_pad, lds, VOCAB_TR_ARGS);
+}
+
 // Exp-store conversion of one decode step's saved fp16 logits, in place:
 // E = bf16(exp(x - lse_r)).  Used for step 0 only, whose rows have no
 // previous-step LSE to offset by in the decode kernel (steps >= 1 write E
@@ -895,7 +915,9 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
                           float ss_prob, const uint32_t* rng, int step, int* counts,
                           int count_step, uint8_t* unfinished, hipStream_t stream,
-                          const CellLaunch* cl) {
+                          const CellLaunch* cl, int rows_per_step) {
+  const int Rs = rows_per_step > 0 ? rows_per_step : R;
+  if (R % Rs != 0) throw std::runtime_error("vocab_combine: R must be a multiple of rows_per_step");
   CellArgs cell{};
   if (cl != nullptr) {
     cell = CellArgs{cl->pre, cl->vg16, cl->ptab, cl->c_prev, cl->c_out, cl->h_out,
@@ -909,7 +931,7 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   hipLaunchKernelGGL(kern, dim3((R + CMB_ROWS - 1) / CMB_ROWS),
                      dim3(CMB_THREADS), 0, stream, (const VocabPartial*)part, n_vt, R, lse_out,
                      tok_out, tok_stride, g_sel, gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode,
-                     ss_prob, rng, step, counts, count_step, unfinished, cell);
+                     ss_prob, rng, step, counts, count_step, unfinished, cell, Rs);
   post_launch("vocab_combine_kernel", stream);
 }
 
@@ -1032,6 +1054,35 @@ int launch_vocab_lstm_fwd(const uint16_t* hd, int ldh, int R, int H, const uint1
   }
 #undef VL
   return vocab_num_tiles(V);
+}
+
+void launch_vocab_lstm_xe(const uint16_t* hd, int R, int H, const uint16_t* W, const float* bias,
+                          int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
+                          const uint32_t* rng, const uint16_t* h_t, const uint16_t* whh,
+                          const float* vgate, int vdiv, const XeCell* xc, hipStream_t stream) {
+  constexpr int BN = 64, STAGES = 2, OCC = 3;
+  using TL = Tile<VT_V, BN, STAGES>;
+  constexpr int LV = TL::STAGES * TL::STAGE_BYTES > epilogue_lds_bytes(BN)
+                         ? TL::STAGES * TL::STAGE_BYTES
+                         : epilogue_lds_bytes(BN);
+  constexpr int LDS = LV > LGTile2::LDS_BYTES ? LV : LGTile2::LDS_BYTES;
+  if (H % 64 != 0 || (xc != nullptr && (h_t == nullptr || vgate == nullptr)))
+    throw std::runtime_error("vocab_lstm_xe: unsupported operands");
+  const int n_vt = (V + VT_V - 1) / VT_V, n_rt = (R + BN - 1) / BN;
+  const int n_l = xc != nullptr ? (lstm_gemm_blocks(R, H) + 7) / 8 * 8 : 0;
+  const int grid = n_l + (hd != nullptr ? n_vt * n_rt : 0);
+  if (grid == 0) return;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)vocab_lstm_xe_kernel<BN, STAGES, OCC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  const XeCell x = xc != nullptr ? *xc : XeCell{};
+  hipLaunchKernelGGL((vocab_lstm_xe_kernel<BN, STAGES, OCC>), dim3(grid), dim3(256), LDS, stream,
+                     hd, H, R, H, W, bias, V, logits16, ldl, (VocabPartial*)part, tgt, 1,
+                     /*flags: VF_EXP*/ 16, 1.f, rng, 0, nullptr, h_t, whh, vgate, vdiv, x, n_l);
+  post_launch("vocab_lstm_xe_kernel", stream);
 }
 
 void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const float* lse,

@@ -21,6 +21,9 @@
 // 2^-10 (|a| + |b|) s: its softmax part is then off by at most 2^-10 (|a| +
 // |b|) in total.
 //
+// (The XE all-rows forward, engine.cpp, writes E = exp(x) with c = 0 for every
+// row: VGradRows::zero_off, s_r = exp(-lse_r), guarded for |lse_r| > 60.)
+//
 // Range of the exp store: E = exp(x - c) with c = the previous step's LSE
 // stays inside bf16 (fp32's exponent range) while the row's LSE moves by
 // less than ~80 between steps (overflow above, loss of the row's mass to
@@ -48,7 +51,10 @@ __device__ __forceinline__ RowW row_weights(const VGradRows& g, int64_t row, boo
   w.ys = sel ? (int)g.y_sel[(int64_t)r * g.T_sel + t] : -1;
   w.b = g.dg_xe != nullptr ? g.dg_xe[(int64_t)r * g.dgxe_rs + t] : 0.f;
   w.yx = g.dg_xe != nullptr ? (int)g.y_xe[(int64_t)r * g.yxe_rs + t] : -1;
-  w.s = (t > 0 && !unit_s) ? __expf(g.lse[(int64_t)(t - 1) * g.R + r] - g.lse[row]) : 1.f;
+  w.s = unit_s       ? 1.f
+        : g.zero_off ? __expf(-g.lse[row])
+        : t > 0      ? __expf(g.lse[(int64_t)(t - 1) * g.R + r] - g.lse[row])
+                     : 1.f;
   w.al = -(w.a + w.b) * w.s;
   // weights that (nearly) cancel on two different tokens: keep alpha away from
   // 0 so the one-hot terms stay representable (ys == yx cancels exactly)
@@ -91,8 +97,8 @@ __global__ __launch_bounds__(256) void vgrad_onehot_kernel(VGradRows g, uint16_t
       g.oh_yx[row] = w.yx;
     }
   }
-  if (g.fix != nullptr && t > 0) {
-    const float d = g.lse[row] - g.lse[row - g.R];
+  if (g.fix != nullptr && (t > 0 || g.zero_off)) {
+    const float d = g.zero_off ? g.lse[row] : g.lse[row] - g.lse[row - g.R];
     if (fabsf(d) > EXP_SAFE_LSE_JUMP) {  // E may be out of range: recomputed by vgrad_fix
       const int k = atomicAdd(g.fix, 1);
       g.fix[1 + k] = (int)row;

@@ -146,7 +146,11 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
                           int64_t tok_stride, float* g_sel, int64_t gsel_stride, float* g_xe,
                           int64_t gxe_stride, const int64_t* gt, int64_t gt_stride, int mode,
                           float ss_prob, const uint32_t* rng, int step, int* counts, int count_step,
-                          uint8_t* unfinished, hipStream_t stream, const CellLaunch* cell = nullptr);
+                          uint8_t* unfinished, hipStream_t stream, const CellLaunch* cell = nullptr,
+                          int rows_per_step = 0);
+// (rows_per_step > 0: the partials are per-step blocks [R / rows_per_step]
+// [n_vt][rows_per_step] -- the XE all-rows forward combines every step's rows
+// in one launch; 0: one block [n_vt][R])
 // vocab projection of step t + recurrent GEMM of step t+1 in one launch
 // (tiled transposed-epilogue kernel; pre == nullptr: vocab only).  NQ > 0:
 // whh has 4H + NQ rows, the last NQ (W_q) produce the attention query q_out
@@ -168,6 +172,31 @@ void launch_vocab_exp_convert(uint16_t* buf, int64_t ldl, int V, int R, const fl
 // vocab_grad.hip: vocab-head backward from the exp store (see that file).
 // Row weights of the NR = n_steps * R rollout rows: sampled / chosen tokens
 // (weight dg_sel) and XE targets (weight dg_xe)
+// XE all rows (engine.cpp): the cell operands of a whole-step LSTM tile
+// (lstm_gemm.h lstm_cell_block) inside the previous step's decode launch
+struct XeCell {
+  const int64_t* tok;  // input tokens of the step (row stride tok_stride)
+  int64_t tok_stride;
+  const uint16_t* ptab;  // fp16 (V, 4H) projected-embedding gate table
+  const float* c_prev;   // (R, H)
+  uint16_t* h_out;       // (R, H) bf16
+  float* c_out;          // (R, H)
+  uint16_t* hd_out;      // (R, H) bf16 dropout(h)
+  uint16_t* gates_out;   // (R, 4H) bf16 packed cell gates (saved for the backward)
+  float drop_p;
+  int key;   // dropout key of the step
+  int cell;  // CellType
+};
+
+// one decode launch of the XE all-rows forward: the whole LSTM step of h_t's
+// successor (xc non-null: h_t W_hh^T + vgate + P[tok] -> cell) and the
+// vocabulary tiles of the rows hd (non-null): E = exp(x) (offset 0, bf16) into
+// logits16 and the per-tile partials (target logit tgt), no token choice
+void launch_vocab_lstm_xe(const uint16_t* hd, int R, int H, const uint16_t* W, const float* bias,
+                          int V, uint16_t* logits16, int64_t ldl, void* part, const int64_t* tgt,
+                          const uint32_t* rng, const uint16_t* h_t, const uint16_t* whh,
+                          const float* vgate, int vdiv, const XeCell* xc, hipStream_t stream);
+
 struct VGradRows {
   int R, n_steps, T_sel, H, V;
   const float* lse;       // (n_steps, R)
@@ -190,6 +219,10 @@ struct VGradRows {
   float* oh_b;
   int* oh_yx;
   float* X;  // (NR, H) fp32, nullable
+  // the forward wrote E = exp(x) (offset 0: the XE all-rows forward) instead
+  // of exp(x - the previous step's LSE): s = exp(-lse), and the range guard
+  // lists rows with |lse| > EXP_SAFE_LSE_JUMP (step 0 included)
+  int zero_off;
 };
 constexpr float EXP_SAFE_LSE_JUMP = 60.f;
 // alpha (NR) and the one-hot terms folded into E (NR rows, stride ldl), in place

@@ -80,6 +80,9 @@ from .. import _ext
 from ..utils.text import BOS
 
 SEL_GT, SEL_SAMPLE, SEL_GREEDY, SEL_SS = 0, 1, 2, 3
+# teacher-forced training forwards on the XE decode launches (csrc/engine.cpp
+# "XE all rows"); CSTCAP_XE_ROWS=0: the general per-step launches + combine
+XE_ROWS = os.environ.get('CSTCAP_XE_ROWS', '1') != '0'
 
 # cell id of csrc/common.h CellType, gate groups of the PyTorch weights, and
 # the packed slot of each gate group on the input / recurrent side
@@ -154,6 +157,13 @@ class _DecoderFn(torch.autograd.Function):
         state0 = []
         if h0 is not None:  # bf16 h (the recurrent GEMM operand), fp32 c
             state0 = [h0.detach().bfloat16().contiguous(), c0.detach().float().contiguous()]
+        store_exp = bool(save and not want_full)
+        # XE all rows (csrc/engine.cpp): teacher forcing of a training forward
+        # runs one launch per step (vocabulary tiles of step t + the whole LSTM
+        # step t+1) with the combines on a side stream
+        xe_rows = bool(store_exp and want_xe and labels is not None and not has_att
+                       and not state0 and eng.layers == 1 and XE_ROWS and T <= 64
+                       and all(m == SEL_GT for m in modes[:T - 1]))
         outs = _ext.ops().decoder_forward(
             eng.wx, eng.emb, eng.ptab, eng.whh_q if has_att else eng.whh, eng.wlog,
             logit_b.detach().float().contiguous(),
@@ -161,7 +171,8 @@ class _DecoderFn(torch.autograd.Function):
             labels if labels is not None else torch.empty(0, dtype=torch.long),
             bos if bos is not None else torch.empty(0, dtype=torch.long), R, T, modes, ss_prob,
             drop_p, temperature, rng, save, want_xe, use_counts, use_unfinished, att, eng.cell,
-            state0, eng.upper_operands(), bool(save and not want_full))
+            state0, eng.upper_operands(), store_exp, xe_rows)
+        ctx.xe_rows = xe_rows
         xw = torch.empty(0, device=dev)  # X = E W: engine.launch_x after the rollout
         seq, g_sel, g_xe, lse = outs[:4]
         ctx.save_dims = (R, T, vdiv, want_xe)
@@ -295,7 +306,7 @@ class _DecoderFn(torch.autograd.Function):
             ctx.drop_p, ctx.rng, out_w, out_b, comm, att, out_emb, ds_bias, eng.cell,
             ctx.state0, eng.upper_operands(ctx.up_saved), ctx.logit_b, eng.exp_fix_rows,
             vdiv, xw if ctx.store_exp else empty, vg_bwd, vg_nf, float(vg_p),
-            0 if x_ev is None else int(x_ev.cuda_event))
+            0 if x_ev is None else int(x_ev.cuda_event), ctx.xe_rows)
         ctx.logit_b = None
         ctx.up_saved = None
         d_up = []

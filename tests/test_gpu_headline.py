@@ -274,3 +274,47 @@ def test_headline_beam5_graph_replay_equals_eager():
     for (s1, l1), (s0, l0) in zip(outs['1'], outs['0']):
         assert torch.equal(s1, s0)
         assert torch.equal(l1, l0)
+
+
+@pytest.mark.parametrize('bias_shift', [0.0, 70.0])
+def test_headline_teacher_forced_xe_launches_match_per_step(bias_shift):
+    """XE all rows (csrc/engine.cpp: one launch per step = the vocabulary tiles
+    of step t + the whole LSTM step t+1, E = exp(x) with offset 0, the combines
+    on a side stream) against the general per-step launches + combine (E =
+    exp(x - previous LSE)): the same target log-probs and parameter
+    gradients.  bias_shift = 70 puts every row's LSE above the exp store's
+    guard (|lse| > 60), so the zero-offset backward recomputes every row
+    exactly (vocab_grad.hip vgrad_fix, VGradRows::zero_off)."""
+    from cst_captioning_amd.models import CrossEntropyCriterion
+    from cst_captioning_amd.models import decoder_engine as de
+    model, eng, loader = _headline_model(seed=2)
+    with torch.no_grad():
+        model.logit.bias.add_(bias_shift)
+    eng.refresh_weights()
+    seed = 192837465
+    eng._rng = lambda dev: torch.tensor([seed, 31337], dtype=torch.int32, device=DEV)
+    model.train()
+    model.set_seq_per_img(20)
+    data = loader.get_batch()
+    labels, masks = data['labels'], data['masks']
+    out = {}
+    saved = de.XE_ROWS
+    try:
+        for rows in (True, False):
+            de.XE_ROWS = rows
+            model.zero_grad(set_to_none=True)
+            g_xe = eng.teacher_forced(model, data['feats'], labels)
+            CrossEntropyCriterion()(g_xe, labels[:, 1:], masks[:, 1:]).backward()
+            out[rows] = (g_xe.detach().clone(),
+                         {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                          if p.grad is not None})
+    finally:
+        de.XE_ROWS = saved
+    (g1, gr1), (g0, gr0) = out[True], out[False]
+    m = masks[:, 1:g1.size(1) + 1] > 0
+    assert torch.isfinite(g1).all()
+    assert (g1 - g0).abs()[m].max().item() < 2e-3
+    assert set(gr1) == set(gr0)
+    for n in gr0:
+        err = ((gr1[n] - gr0[n]).norm() / (gr0[n].norm() + 1e-12)).item()
+        assert err < 1e-2, (n, err)
