@@ -75,7 +75,8 @@ std::vector<at::Tensor> featpool_backward(at::Tensor dout, at::Tensor out,
                                           std::vector<at::Tensor> ws, double drop_p,
                                           std::vector<at::Tensor> outs);
 std::vector<at::Tensor> att_mfma_fwd(at::Tensor h, at::Tensor wq, at::Tensor P, at::Tensor wa,
-                                     at::Tensor ba, at::Tensor gv);
+                                     at::Tensor ba, at::Tensor gv,
+                                     int64_t whole);
 std::vector<at::Tensor> decode_step_test(at::Tensor hd, at::Tensor h, at::Tensor wlog,
                                          at::Tensor blog, at::Tensor whh, at::Tensor vgate,
                                          int64_t vdiv, at::Tensor tgt, at::Tensor eoff,
@@ -205,7 +206,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("device_errors", &cst::device_errors,
         "failed cross-workgroup hand-offs counted on the device (synchronous read)");
   m.def("reset_device_errors", &cst::reset_device_errors);
-  m.def("att_mfma_fwd", &cst::att_mfma_fwd);
+  m.def("att_mfma_fwd", &cst::att_mfma_fwd, py::arg("h"), py::arg("wq"), py::arg("P"),
+        py::arg("wa"), py::arg("ba"), py::arg("gv"), py::arg("whole") = -1);
   m.def("beam_search", &cst::beam_search);
   m.def("featpool_forward", &cst::featpool_forward);
   m.def("scst_loss_forward", &cst::scst_loss_forward);

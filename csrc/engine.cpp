@@ -659,6 +659,7 @@ std::vector<at::Tensor> decoder_forward(at::Tensor wx, at::Tensor emb, at::Tenso
                        save ? q_next.data_ptr<float>() : nullptr, att_ep.data_ptr<float>(),
                        att_cnt.data_ptr<int>(),
                        save ? reinterpret_cast<uint16_t*>(u_all[t + 1].data_ptr()) : nullptr};
+    if (att_mfma && next) am.whole = att_mfma_whole_default((int)C, (int)H);
     const bool q_tiles = has_att && !att_mfma;  // W_q tiles in the recurrent GEMM
     const int n_vt = launch_vocab_lstm_fwd(
         vin, (int)H, (int)R, (int)H, W, blog.data_ptr<float>(), (int)V,
@@ -2141,6 +2142,7 @@ std::vector<at::Tensor> beam_search(at::Tensor wx, at::Tensor ptab, at::Tensor w
                          (int)H, (int)A, (int)C, CPAD, (int)H4, (int)K, (int)B,
                          reinterpret_cast<uint16_t*>(vg16.data_ptr()), nullptr, nullptr,
                          att_ep.data_ptr<float>(), att_cnt.data_ptr<int>()};
+      if (has_att && next) am.whole = att_mfma_whole_default((int)C, (int)H);
       (void)launch_vocab_lstm_fwd(reinterpret_cast<const uint16_t*>(ht.data_ptr()), (int)H, (int)R,
                                   (int)H, W, blog.data_ptr<float>(), (int)V,
                                   reinterpret_cast<uint16_t*>(logits.data_ptr()), ldl,
@@ -2406,7 +2408,7 @@ double token_sort_bench(at::Tensor toks, int64_t V, int64_t iters) {
 // P (Bv, C, A), wa (A), ba (1) fp32, gv (Bv, C, 4H) fp32 ->
 // {vg (R, 4H) bf16, alpha (R, C), q (R, A)}
 std::vector<at::Tensor> att_mfma_fwd(at::Tensor h, at::Tensor wq, at::Tensor P, at::Tensor wa,
-                                     at::Tensor ba, at::Tensor gv) {
+                                     at::Tensor ba, at::Tensor gv, int64_t whole) {
   for (auto* t : {&h, &wq, &P, &wa, &ba, &gv}) check_cuda(*t, "att_mfma operand");
   TORCH_CHECK(h.scalar_type() == at::kBFloat16 && wq.scalar_type() == at::kBFloat16 &&
                   P.scalar_type() == at::kFloat && wa.scalar_type() == at::kFloat &&
@@ -2431,6 +2433,7 @@ std::vector<at::Tensor> att_mfma_fwd(at::Tensor h, at::Tensor wq, at::Tensor P, 
                 (int)(4 * H), vdiv, (int)Bv, reinterpret_cast<uint16_t*>(vg.data_ptr()),
                 alpha.data_ptr<float>(), q.data_ptr<float>(), ep.data_ptr<float>(),
                 cnt.data_ptr<int>()};
+  a.whole = whole < 0 ? att_mfma_whole_default((int)C, (int)H) : (whole != 0 ? 1 : 0);
   launch_att_mfma_fwd(a, cur_stream());
   return {vg, alpha, q};
 }

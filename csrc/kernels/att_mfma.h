@@ -280,10 +280,201 @@ __device__ __forceinline__ void att_mfma_fwd_block(int blk, const AttMfmaArgs& g
   att_phase(g, blk, 6);
 }
 
+// Whole-video form (AttMfmaArgs::whole): ONE workgroup per video loops over
+// the A / 64 query slices -- the video's h rows staged once, each slice's W_q
+// fragments requested while the previous slice's scores are formed -- and
+// accumulates the scores in LDS: no partial-score slots, no ticket, no
+// last-arriver hand-off, and Bv instead of Bv * A / 64 workgroups ahead of the
+// vocabulary tiles of the decode launch (at the att8 shape 64 instead of 512
+// workgroups holding CU slots while the vocabulary tiles wait).  Then the
+// softmax and vgate^T = Gv^T alpha^T exactly as the last arriver above.
+// Opt-in (CSTCAP_ATT_WHOLE=1): the slices in sequence outlast the vocabulary
+// tiles (att8 decode launch 63.8 vs 48.9 us, profiles/r6/s2/att_whole/).
+__host__ __device__ constexpr int att_mfma_video_lds_bytes(int C, int CP, int H) {
+  return att_mfma_lds_bytes(C, CP, H) + 32 * CP * 4;
+}
+
+template <int CP>
+__device__ __forceinline__ void att_mfma_fwd_video(int b, const AttMfmaArgs& g, char* lds) {
+  const int A = g.A, H = g.H, C = g.C, G4 = g.G4, vdiv = g.vdiv, NS = A / ATT_SLICE;
+  uint16_t* s_h = reinterpret_cast<uint16_t*>(lds);  // [32][H], chunks swizzled
+  float* s_P = reinterpret_cast<float*>(lds + 32 * H * 2);  // [C][64]
+  float* s_wa = s_P + C * ATT_SLICE;
+  float* s_e = s_wa + ATT_SLICE;
+  uint16_t* s_alb = reinterpret_cast<uint16_t*>(s_e + 4 * 32 * CP);
+  float* s_acc = reinterpret_cast<float*>(lds + att_mfma_lds_bytes(C, CP, H));  // [32][CP]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row0 = b * vdiv;
+  const int cpr = H / 8;
+  const int swm = (cpr < 16 ? cpr : 16) - 1;
+  {
+    const rsrc_t rh = make_rsrc(g.h + (int64_t)row0 * H, (int64_t)vdiv * H * 2);
+    const int nins = 32 * H * 2 / 1024;
+    for (int i = w; i < nins; i += 4) {
+      const int e = i * 64 + lane;
+      const int row = e / cpr, ch = e % cpr;
+      const int src = min(row, vdiv - 1) * cpr + (ch ^ (row & swm));
+      glds16(rh, src * 16, 0, reinterpret_cast<char*>(s_h) + 1024 * i);
+    }
+  }
+  for (int i = tid; i < 32 * CP; i += 256) s_acc[i] = 0.f;
+  const int ku = lane >> 4, ru = lane & 15;
+  constexpr int MAXK = 16;
+  const int nks = H / 32;
+  const int u0 = 16 * w + 4 * ku;
+  bf16x8 af[MAXK];
+  auto load_wq = [&](int s) {
+    const uint16_t* wrow = g.wq + (int64_t)(s * ATT_SLICE + 16 * w + ru) * H + 8 * ku;
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) af[k] = ld_bf16x8(wrow + 32 * min(k, nks - 1));
+  };
+  load_wq(0);
+  for (int s = 0; s < NS; ++s) {
+    const int a0 = s * ATT_SLICE;
+    for (int i = tid; i < C * (ATT_SLICE / 4); i += 256) {
+      const int c = i / (ATT_SLICE / 4), k = i % (ATT_SLICE / 4);
+      reinterpret_cast<float4*>(s_P)[i] =
+          reinterpret_cast<const float4*>(g.P + ((int64_t)b * C + c) * A + a0)[k];
+    }
+    if (tid < ATT_SLICE / 4)
+      reinterpret_cast<float4*>(s_wa)[tid] = reinterpret_cast<const float4*>(g.wa + a0)[tid];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // h rows (first slice), P, w_a in LDS; s_acc zeroed
+    f32x4v acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) {
+      if (k < nks) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = 16 * j + ru, ch = 4 * k + ku;
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(
+              reinterpret_cast<const char*>(s_h) + row * H * 2 + ((ch ^ (row & swm)) << 4));
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], bfr, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    // the next slice's W_q fragments, in flight under this slice's scores
+    if (s + 1 < NS) load_wq(s + 1);
+    if (g.q_out != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = 16 * j + ru;
+        if (row < vdiv)
+          *reinterpret_cast<float4*>(g.q_out + (int64_t)(row0 + row) * A + a0 + u0) =
+              make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+      }
+    }
+    const float4 wv = *reinterpret_cast<const float4*>(s_wa + u0);
+    for (int c = 0; c < C; ++c) {
+      const float4 p = *reinterpret_cast<const float4*>(s_P + c * ATT_SLICE + u0);
+      float ec[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float t0 = tanh_fast(p.x + acc[j][0]), t1 = tanh_fast(p.y + acc[j][1]);
+        const float t2 = tanh_fast(p.z + acc[j][2]), t3 = tanh_fast(p.w + acc[j][3]);
+        ec[j] = wv.x * t0;
+        ec[j] = fmaf(wv.y, t1, ec[j]);
+        ec[j] = fmaf(wv.z, t2, ec[j]);
+        ec[j] = fmaf(wv.w, t3, ec[j]);
+        const int row = 16 * j + ru;
+        if (g.u_out != nullptr && row < vdiv)
+          *reinterpret_cast<uint2*>(g.u_out + ((int64_t)(row0 + row) * C + c) * A + a0 + u0) =
+              make_uint2((uint32_t)u_enc(t0) | ((uint32_t)u_enc(t1) << 16),
+                         (uint32_t)u_enc(t2) | ((uint32_t)u_enc(t3) << 16));
+        ec[j] += __shfl_xor(ec[j], 16, 64);
+        ec[j] += __shfl_xor(ec[j], 32, 64);
+      }
+      if (ku == 0) {
+        s_e[(w * 32 + ru) * CP + c] = ec[0];
+        s_e[(w * 32 + 16 + ru) * CP + c] = ec[1];
+      }
+    }
+    __syncthreads();  // s_e complete; s_P / s_wa reads done
+    for (int i = tid; i < 32 * CP; i += 256) {
+      const int rr = i / CP, c = i % CP;
+      s_acc[i] += s_e[rr * CP + c] + s_e[(32 + rr) * CP + c] + s_e[(64 + rr) * CP + c] +
+                  s_e[(96 + rr) * CP + c];
+    }
+  }
+  // softmax over frames and vgate (as the last arriver of att_mfma_fwd_block)
+  const int hh = lane >> 5, r = lane & 31;
+  const int ntw = G4 / 128;
+  constexpr int MAXT = 16;
+  const uint16_t* gvb = g.gv16 + (int64_t)b * G4 * CP;
+  const bool ghalf = CP == 16 || hh == 0;
+  bf16x8 ga[MAXT];
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    const int n0 = (w * ntw + min(i, ntw - 1)) * 32;
+    ga[i] = ld_bf16x8(gvb + (int64_t)(n0 + r) * CP + (CP == 16 ? 8 * hh : 0));
+  }
+  const float ba = g.ba[0];
+  __syncthreads();  // s_acc complete
+  if (tid < 32) {
+    float x[CP], mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < CP; ++c) x[c] = s_acc[tid * CP + c] + ba;
+#pragma unroll
+    for (int c = 0; c < CP; ++c)
+      if (c < C) mx = fmaxf(mx, x[c]);
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < CP; ++c) {
+      x[c] = c < C ? __expf(x[c] - mx) : 0.f;
+      sum += x[c];
+    }
+    const float inv = 1.f / sum;
+    const bool ok = tid < vdiv;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float al = (c < CP && c < C && ok) ? x[c < CP ? c : 0] * inv : 0.f;
+      s_alb[tid * 16 + c] = f2bf(al);
+      if (c < C && ok && g.alpha_out != nullptr) g.alpha_out[(int64_t)(row0 + tid) * C + c] = al;
+    }
+  }
+  __syncthreads();
+  const bf16x8 bal = ld_bf16x8(s_alb + r * 16 + 8 * hh);
+  const bf16x8 zero8 = {};
+  uint16_t* prow[16];
+  bool vrow[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int row = (k & 3) + 8 * (k >> 2) + 4 * hh;
+    vrow[k] = row < vdiv;
+    prow[k] = g.vg_out + (int64_t)(row0 + min(row, vdiv - 1)) * G4 + w * ntw * 32 + r;
+  }
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    f32x16 o;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0.f;
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bal, ghalf ? ga[i] : zero8, o, 0, 0, 0);
+    if (i < ntw) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (vrow[k]) prow[k][32 * i] = f2bf(o[k]);
+    }
+  }
+}
+
 // attention variant of a kernel template: 0 = none, else the padded frame
 // count CP (8 or 16)
 constexpr int att_variant(int C) { return C <= 8 ? 8 : 16; }
 // workgroups of one step's attention
 __host__ __device__ constexpr int att_mfma_blocks(int Bv, int A) { return Bv * (A / ATT_SLICE); }
+__host__ __device__ inline int att_mfma_nblocks(const AttMfmaArgs& a) {
+  return a.whole ? a.Bv : att_mfma_blocks(a.Bv, a.A);
+}
+// one attention workgroup of either form
+template <int CP>
+__device__ __forceinline__ void att_mfma_fwd_any(int blk, const AttMfmaArgs& g, char* lds) {
+  if (g.whole)
+    att_mfma_fwd_video<CP>(blk, g, lds);
+  else
+    att_mfma_fwd_block<CP>(blk, g, lds);
+}
 
 }  // namespace cst

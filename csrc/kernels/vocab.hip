@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_fwd_tr_kernel(VOCAB_TR_PARAMS)
 template <int AV>
 __global__ __launch_bounds__(256) void att_mfma_fwd_kernel(AttMfmaArgs att) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  att_mfma_fwd_block<AV>(blockIdx.x, att, lds);
+  att_mfma_fwd_any<AV>(blockIdx.x, att, lds);
 }
 
 // host dispatch over the attention variants (frames padded to 8 / 16)
@@ -429,8 +429,21 @@ bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame) {
 
 static void check_att_mfma(const AttMfmaArgs& a) {
   if (!att_mfma_fwd_ok(a.vdiv, a.C, a.A, a.H, 0) || a.G4 != 4 * a.H || a.CP != (a.C <= 8 ? 8 : 16) ||
-      a.e_part == nullptr || a.cnt == nullptr)
+      (!a.whole && (a.e_part == nullptr || a.cnt == nullptr)) ||
+      (a.whole && att_mfma_video_lds_bytes(a.C, a.CP, a.H) > 48 * 1024))
     throw std::runtime_error("att_mfma: unsupported attention shape");
+}
+
+// CSTCAP_ATT_WHOLE=1: the whole-video form where its LDS fits.  Opt-in: one
+// workgroup running all A / 64 slices in sequence outlasts the vocabulary tiles
+// of the decode launch (att8 launch 63.8 vs 48.9 us; step 4.841 / 4.875 vs
+// 4.502 / 4.506 ms, interleaved, profiles/r6/s2/att_whole/)
+int att_mfma_whole_default(int C, int H) {
+  static const bool env = [] {
+    const char* e = getenv("CSTCAP_ATT_WHOLE");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return env && att_mfma_video_lds_bytes(C, C <= 8 ? 8 : 16, H) <= 48 * 1024 ? 1 : 0;
 }
 
 template <int AV>
@@ -442,7 +455,8 @@ static void launch_att_mfma_fwd_t(const AttMfmaArgs& a, hipStream_t stream) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 48 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(att_mfma_fwd_kernel<AV>, dim3(att_mfma_blocks(a.Bv, a.A)), dim3(256), lds,
+  hipLaunchKernelGGL(att_mfma_fwd_kernel<AV>, dim3(att_mfma_nblocks(a)), dim3(256),
+                     a.whole ? att_mfma_video_lds_bytes(a.C, a.CP, a.H) : lds,
                      stream, a);
   post_launch("att_mfma_fwd_kernel", stream);
 }
@@ -788,7 +802,7 @@ __global__ __launch_bounds__(256, OCC) void vocab_lstm_fwd_kernel(
     // (dispatched after the vocabulary tiles instead, into their drain:
     // att8 5.48-5.51 vs 5.19-5.22 ms per step, profiles/r3/ab_att_last.txt)
     if (bid < n_att) {
-      if (bid < att_mfma_blocks(att.Bv, att.A)) att_mfma_fwd_block<AV>(bid, att, lds);
+      if (bid < att_mfma_nblocks(att)) att_mfma_fwd_any<AV>(bid, att, lds);
       return;
     }
     bid -= n_att;
@@ -954,7 +968,7 @@ static void launch_vocab_lstm_t(const uint16_t* hd, int ldh, int R, int H, const
   int n_att = 0;
   if (AV != 0) {
     a = *att;
-    n_att = (att_mfma_blocks(a.Bv, a.A) + 7) / 8 * 8;
+    n_att = (att_mfma_nblocks(a) + 7) / 8 * 8;
   }
   const int n_l = pre != nullptr ? (lstm_gemm_blocks(R, H, NQ) + 7) / 8 * 8 : 0;
   const int grid = n_att + n_l + n_vt * n_rt;

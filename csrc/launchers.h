@@ -131,6 +131,8 @@ struct AttMfmaArgs {
   uint16_t* u_out;       // nullable (R, C, A) fp16 scorer values tanh(P + q) (training:
                          // the fused attention backward reads them instead of recomputing)
   int64_t* dbg;          // nullable (workgroups, 8) wall-clock phase stamps (microbenchmark)
+  int whole;             // 1: one workgroup per video loops over the A / 64 query slices
+                         // (att_mfma.h att_mfma_fwd_video: no slots / ticket)
 };
 // the MFMA attention path applies: rows per video 2..32, C <= 16, A % 64 == 0,
 // A <= 1024, H % 32 == 0, 64 <= H <= 512, the shared scorer (not per frame)
@@ -140,6 +142,8 @@ bool att_mfma_ok(int vdiv, int C, int A, int H, int per_frame);
 bool att_mfma_fwd_ok(int vdiv, int C, int A, int H, int per_frame);
 // standalone launch of the same workgroups (tests / microbenchmarks)
 void launch_att_mfma_fwd(const AttMfmaArgs& a, hipStream_t stream);
+// AttMfmaArgs::whole for a shape (1 with CSTCAP_ATT_WHOLE=1 where its LDS fits)
+int att_mfma_whole_default(int C, int H);
 // size of the end-of-sequence flag area per decode step (ints) of `counts`
 int combine_count_ints_per_step();
 void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int64_t* tok_out,

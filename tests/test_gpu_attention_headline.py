@@ -28,7 +28,8 @@ DEV = 'cuda'
                                            (9, 2, 3, 128, 256), (5, 13, 12, 384, 64),
                                            # one row per video: the SCST greedy baseline
                                            (64, 1, 8, 512, 512), (9, 1, 3, 128, 256)])
-def test_att_mfma_kernel_matches_fp32(Bv, vdiv, C, A, H):
+@pytest.mark.parametrize('whole', [1, 0])
+def test_att_mfma_kernel_matches_fp32(Bv, vdiv, C, A, H, whole):
     from cst_captioning_amd import _ext
     ops = _ext.ops()
     g = torch.Generator(device=DEV).manual_seed(Bv * 31 + C)
@@ -39,7 +40,9 @@ def test_att_mfma_kernel_matches_fp32(Bv, vdiv, C, A, H):
     wa = torch.randn(A, device=DEV, generator=g) * 0.3
     ba = torch.randn(1, device=DEV, generator=g)
     gv = torch.randn(Bv, C, 4 * H, device=DEV, generator=g)
-    vg, alpha, q = ops.att_mfma_fwd(h, wq, P, wa, ba, gv)
+    # whole = 1: one workgroup per video over every query slice; 0: A / 64
+    # workgroups per video with the last-arriver hand-off
+    vg, alpha, q = ops.att_mfma_fwd(h, wq, P, wa, ba, gv, whole)
     q_ref = h.float() @ wq.float().t()
     torch.testing.assert_close(q, q_ref, rtol=1e-4, atol=1e-4)
     pb = P.repeat_interleave(vdiv, 0)  # (R, C, A)
