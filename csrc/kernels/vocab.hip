@@ -474,13 +474,14 @@ void launch_att_mfma_fwd(const AttMfmaArgs& a, hipStream_t stream) {
 // token-selection modes of one decode step
 enum SelMode : int { SEL_GT = 0, SEL_SAMPLE = 1, SEL_GREEDY = 2, SEL_SS = 3 };
 
-// One wavefront per row (64-thread blocks, 1,280 at R = 1280): each lane
+// One wavefront per row (4 rows per 256-thread workgroup by default, see
+// launch_vocab_combine; 320 workgroups at R = 1280): each lane
 // merges 2 tiles (6-step shuffle tree) and owns 8 of the cell epilogue's
 // hidden units, so the chain partials -> merge -> token -> table row -> cell
 // runs with half the per-lane work of the earlier half-wave rows (3.331-3.345
 // vs 3.367-3.380 ms per training step, interleaved on one box,
 // profiles/r5/combine/ab_c64_*.json).  LANES stays a template parameter.
-constexpr int CMB_LANES = 64, CMB_THREADS = 64, CMB_ROWS = CMB_THREADS / CMB_LANES;
+constexpr int CMB_LANES = 64, CMB_THREADS = 64;
 // end-of-sequence flags: per decode step CMB_CNT_SLOTS slots, one 128-byte
 // line apart (see vocab_combine_kernel)
 constexpr int CMB_CNT_SLOTS = 64, CMB_CNT_STRIDE = 32;
@@ -596,8 +597,8 @@ __device__ __forceinline__ int finish_row(const RowStat& a, int r, const RowSel&
   return (int)tok;
 }
 
-template <int LANES, bool PH>
-__global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
+template <int LANES, bool PH, int NT = CMB_THREADS>
+__global__ __launch_bounds__(NT) void vocab_combine_kernel(
     const VocabPartial* __restrict__ part, int n_vt, int R, float* __restrict__ lse_out,
     int64_t* __restrict__ tok_out, int64_t tok_stride, float* __restrict__ g_sel,
     int64_t gsel_stride, float* __restrict__ g_xe, int64_t gxe_stride,
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(CMB_THREADS) void vocab_combine_kernel(
   __shared__ int s_nonzero;
   int tok_final = 0;
   const int sub = threadIdx.x & (LANES - 1);
-  const int r = blockIdx.x * (CMB_THREADS / LANES) + (threadIdx.x / LANES);
+  const int r = blockIdx.x * (NT / LANES) + (threadIdx.x / LANES);
   const bool valid = r < R;
   if (threadIdx.x == 0) s_nonzero = 0;
   // The row's tile partials are loaded unconditionally (clamped index,
@@ -940,10 +941,22 @@ void launch_vocab_combine(const void* part, int n_vt, int R, float* lse_out, int
   }
   // (fp16 pre as a template parameter: a runtime select between the two
   // load forms cost 1.6 us per combine, 14.3 vs 12.7 us in rocprofv3)
-  auto kern = cell.pre_half ? vocab_combine_kernel<CMB_LANES, true>
-                            : vocab_combine_kernel<CMB_LANES, false>;
-  hipLaunchKernelGGL(kern, dim3((R + CMB_ROWS - 1) / CMB_ROWS),
-                     dim3(CMB_THREADS), 0, stream, (const VocabPartial*)part, n_vt, R, lse_out,
+  // rows (wavefronts) per workgroup, CSTCAP_CMB_ROWS = 1 / 4 / 8: 4 by default
+  // (headline 3.072-3.081 vs 3.095-3.119 ms per step with one row per
+  // workgroup, three interleaved pairs, profiles/r6/s2/cmb_rows/)
+  static const int rows_wg = [] {
+    const char* e = getenv("CSTCAP_CMB_ROWS");
+    const int v = e != nullptr ? atoi(e) : 4;
+    return v == 1 || v == 8 ? v : 4;
+  }();
+  auto kern = rows_wg == 4   ? (cell.pre_half ? vocab_combine_kernel<CMB_LANES, true, 4 * CMB_LANES>
+                                              : vocab_combine_kernel<CMB_LANES, false, 4 * CMB_LANES>)
+              : rows_wg == 8 ? (cell.pre_half ? vocab_combine_kernel<CMB_LANES, true, 8 * CMB_LANES>
+                                              : vocab_combine_kernel<CMB_LANES, false, 8 * CMB_LANES>)
+                             : (cell.pre_half ? vocab_combine_kernel<CMB_LANES, true>
+                                              : vocab_combine_kernel<CMB_LANES, false>);
+  hipLaunchKernelGGL(kern, dim3((R + rows_wg - 1) / rows_wg),
+                     dim3(rows_wg * CMB_LANES), 0, stream, (const VocabPartial*)part, n_vt, R, lse_out,
                      tok_out, tok_stride, g_sel, gsel_stride, g_xe, gxe_stride, gt, gt_stride, mode,
                      ss_prob, rng, step, counts, count_step, unfinished, cell, Rs);
   post_launch("vocab_combine_kernel", stream);
