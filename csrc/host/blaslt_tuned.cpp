@@ -175,8 +175,19 @@ Plan& get_plan(int dev, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ld
 // leading dimension, e.g. a column slice of a wider matrix) = op(a) op(b); a,
 // b bf16 2-D views with unit column stride (row stride = the leading
 // dimension).  ta: a is used transposed (a is K x M), tb likewise (b is N x K).
+// CSTCAP_BLASLT_NCAND=<n>: time the heuristic's first n candidates instead
+// of the caller's count (every tuned shape)
+static int64_t ncand_override(int64_t n_cand) {
+  static const int64_t v = [] {
+    const char* e = getenv("CSTCAP_BLASLT_NCAND");
+    return e != nullptr ? (int64_t)atoi(e) : (int64_t)0;
+  }();
+  return v > 0 ? v : n_cand;
+}
+
 void gemm_bf16_tuned(at::Tensor out, at::Tensor a, bool ta, at::Tensor b, bool tb,
                      int64_t n_cand) {
+  n_cand = ncand_override(n_cand);
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm_bf16_tuned: GPU tensors");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
                   out.scalar_type() == at::kFloat && out.dim() == 2 && out.stride(1) == 1 &&
